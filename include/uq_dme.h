@@ -1,0 +1,89 @@
+/* uq_dme.h — C-ABI of the MI355X-native unbiased L1-ball type quantizer.
+ *
+ * The reference (Ritesh622/Unbiased-Quantization-Distributed-Mean-Estimation) is pure
+ * Python/PyTorch and has no FFI; every entry point below replaces one group of torch
+ * ops inside `Type_unbiased_quantize` (NMSE_Results/Codes/All_Schemes.py:609-641) or
+ * the DME client-mean around it (NMSE_Results/Codes/Normal_dist.py:137-138).  The
+ * Python binding that calls these through ctypes is the drop-in; INTEGRATION.md shows
+ * the binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *   - All buffers are DEVICE pointers, caller-allocated, row-major [n][d] f32 for
+ *     client vectors.  `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *   - The library never allocates, never synchronises, and is stream-ordered.
+ *   - Return 0 on success, a negative UQ_E* code on error; uq_last_error() gives a
+ *     thread-local message.  Launch errors are reported; kernel-side protocol
+ *     timeouts are reported by uq_check_status() after the stream is synchronised.
+ *   - No hidden RNG: the per-client uniform X of AS:634 is an input.
+ *   - m (lattice sum, AS:622-623) is passed explicitly; uq_rate_to_m() reproduces the
+ *     reference's rate table for callers that want it.
+ *   - torch_threads selects the f32 summation order of torch CPU `sum` (AS:624) for a
+ *     given intra-op thread count, so results are bit-identical to the CPU reference
+ *     run with that many threads.
+ */
+#ifndef UQ_DME_H
+#define UQ_DME_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UQ_OK 0
+#define UQ_E_INVALID (-1)   /* bad argument */
+#define UQ_E_HIP (-2)       /* HIP runtime error */
+#define UQ_E_WORKSPACE (-3) /* workspace too small */
+#define UQ_E_TIMEOUT (-4)   /* inter-workgroup protocol timed out (see uq_check_status) */
+
+/* Library ABI version (major*100 + minor). */
+int uq_version(void);
+
+/* Thread-local description of the last error returned on this thread. */
+const char* uq_last_error(void);
+
+/* AS:614-623: m = int(table[bits] * d).  Unknown `bits` -> UQ_E_INVALID (the
+ * reference raises KeyError). */
+int uq_rate_to_m(double bits_per_dimension, int64_t d, int64_t* m_out);
+
+/* Bytes of device workspace needed by the calls below for a batch of n vectors of
+ * length d summed in torch order for `torch_threads`.  The workspace also holds the
+ * status word read by uq_check_status(). */
+int uq_workspace_bytes(int64_t n, int64_t d, int32_t torch_threads, size_t* bytes_out);
+
+/* AS:624 — l1_out[j] = sum_i |x[j][i]| in torch CPU cascade order (f32 accumulate). */
+int uq_l1_torch_order_f32(const float* x, int64_t n, int64_t d, int32_t torch_threads,
+                          float* l1_out, void* ws, size_t ws_bytes, void* stream);
+
+/* AS:609-641 for a batch — out[j] = Type_unbiased_quantize(x[j], ·) with uniform X[j].
+ *   m       lattice sum (AS:623)
+ *   X       [n] device f32, the AS:634 draw per client
+ *   l1      [n] device f32 L1 norms, or NULL to compute them here (torch order)
+ *   l1_out  [n] device f32 or NULL: receives the L1 norms used */
+int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m,
+                         const float* X, const float* l1, float* l1_out,
+                         int32_t torch_threads, void* ws, size_t ws_bytes, void* stream);
+
+/* Normal_dist.py:137-138 — est[i] (+)= q[j][i] / n_div for j = 0..n-1 in client order
+ * (f32 IEEE division, f32 add).  accumulate=0 starts from zeros. */
+int uq_client_mean_f32(const float* q, int64_t n, int64_t d, float n_div, int32_t accumulate,
+                       float* est, void* stream);
+
+/* Quantize a batch and fold it into the client mean in one call:
+ *   q = Type_unbiased_quantize(x[j]) for all j (into `out`, or into workspace
+ *   scratch when out == NULL and the workspace is large enough), then
+ *   est (+)= q[j] / n_div in client order.  Bit-identical to the two calls above. */
+int uq_type_unbiased_mean_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m,
+                              const float* X, const float* l1, int32_t torch_threads,
+                              float n_div, int32_t accumulate, float* est,
+                              void* ws, size_t ws_bytes, void* stream);
+
+/* After the stream has been synchronised: UQ_OK, or UQ_E_TIMEOUT if any
+ * inter-workgroup wait in a previous call on this workspace gave up. Clears it. */
+int uq_check_status(void* ws, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UQ_DME_H */

@@ -1,0 +1,146 @@
+/* CPU ORACLE (C) — test infrastructure only, never the product path.
+ *
+ * Same restatement as oracle/uq_oracle.py, in plain C so the checker and the
+ * bench's cpu_baseline leg run at d = 2^20 in reasonable time.  Built by
+ * oracle/Makefile with -O2 -ffp-contract=off (no FMA contraction, IEEE f32
+ * division, denormals kept), loaded through ctypes by tests/ and bench.py only.
+ *
+ * Reference semantics followed (paths relative to the reference root):
+ *   NMSE_Results/Codes/All_Schemes.py:609-641  Type_unbiased_quantize
+ *     :624  L1 = |x|.sum()  -> torch CPU cascade order (ATen SumKernel)
+ *     :625-631 den, v, p, mp, floor, frac           (f32, IEEE)
+ *     :635  cumsum(frac) -> sequential fp64 accumulate, each prefix -> f32
+ *     :636-637 crossing test, :640 output
+ *   NMSE_Results/Codes/Normal_dist.py:137-138  est += q / n
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define TORCH_GRAIN 32768
+#define VEC_LANES 8
+#define ILP 4
+#define NUM_LEVELS 4
+
+static int ceil_log2_i64(int64_t x) {
+    if (x <= 1) return 0;
+    int r = 0;
+    uint64_t v = (uint64_t)(x - 1);
+    while (v) { r++; v >>= 1; }
+    return r;
+}
+
+/* ATen multi_row_sum over R rows of width W (row stride W), f32 accumulate. */
+static void cascade(const float* a, int64_t R, int W, float* out) {
+    int lp = ceil_log2_i64(R) / NUM_LEVELS;
+    if (lp < 4) lp = 4;
+    const int64_t step = (int64_t)1 << lp;
+    const int64_t mask = step - 1;
+    float acc[NUM_LEVELS][VEC_LANES * ILP];
+    memset(acc, 0, sizeof(acc));
+    int64_t i = 0;
+    for (; i + step <= R;) {
+        for (int64_t j = 0; j < step; ++j, ++i)
+            for (int k = 0; k < W; ++k) acc[0][k] += a[i * W + k];
+        for (int j = 1; j < NUM_LEVELS; ++j) {
+            for (int k = 0; k < W; ++k) { acc[j][k] += acc[j - 1][k]; acc[j - 1][k] = 0.0f; }
+            if ((i & (mask << (j * lp))) != 0) break;
+        }
+    }
+    for (; i < R; ++i)
+        for (int k = 0; k < W; ++k) acc[0][k] += a[i * W + k];
+    for (int j = 1; j < NUM_LEVELS; ++j)
+        for (int k = 0; k < W; ++k) acc[0][k] += acc[j][k];
+    for (int k = 0; k < W; ++k) out[k] = acc[0][k];
+}
+
+static float row_sum_scalar(const float* x, int64_t s) {
+    int64_t nilp = s / ILP;
+    float p[ILP] = {0, 0, 0, 0};
+    if (nilp) cascade(x, nilp, ILP, p);
+    for (int64_t k = nilp * ILP; k < s; ++k) p[0] += x[k];
+    for (int k = 1; k < ILP; ++k) p[0] += p[k];
+    return p[0];
+}
+
+static float chunk_sum(const float* x, int64_t s) {
+    if (s < VEC_LANES) return row_sum_scalar(x, s);
+    int64_t vs = s / VEC_LANES, nilp = vs / ILP;
+    float p[ILP * VEC_LANES];
+    memset(p, 0, sizeof(p));
+    if (nilp) cascade(x, nilp, ILP * VEC_LANES, p);
+    float p0[VEC_LANES];
+    for (int l = 0; l < VEC_LANES; ++l) p0[l] = p[l];
+    for (int64_t v = nilp * ILP; v < vs; ++v)
+        for (int l = 0; l < VEC_LANES; ++l) p0[l] += x[v * VEC_LANES + l];
+    for (int k = 1; k < ILP; ++k)
+        for (int l = 0; l < VEC_LANES; ++l) p0[l] += p[k * VEC_LANES + l];
+    float acc = 0.0f;
+    for (int64_t k = vs * VEC_LANES; k < s; ++k) acc += x[k];
+    for (int l = 0; l < VEC_LANES; ++l) acc += p0[l];
+    return acc;
+}
+
+/* |x| into scratch, then torch's chunking by intra-op thread count. */
+float uqo_l1_torch_order(const float* x, int64_t d, int torch_threads, float* scratch) {
+    if (d <= 0) return 0.0f;
+    for (int64_t i = 0; i < d; ++i) scratch[i] = fabsf(x[i]);
+    int T = torch_threads < 1 ? 1 : torch_threads;
+    if (d < TORCH_GRAIN || T == 1) return chunk_sum(scratch, d);
+    int64_t nt = (d + TORCH_GRAIN - 1) / TORCH_GRAIN;
+    if (nt > T) nt = T;
+    int64_t cs = (d + nt - 1) / nt;
+    float acc = 0.0f;
+    for (int64_t c = 0; c < nt; ++c) {
+        int64_t b = c * cs, e = b + cs < d ? b + cs : d;
+        if (e > b) acc += chunk_sum(scratch + b, e - b);
+    }
+    return acc;
+}
+
+static inline float torch_sign(float v) {
+    if (v > 0.0f) return 1.0f;
+    if (v < 0.0f) return -1.0f;
+    return 0.0f;  /* +-0 -> +0, NaN -> 0 */
+}
+
+/* One client vector.  l1 < 0 (or NaN-safe flag use_l1=0) -> compute. */
+float uqo_quantize(const float* x, float* out, int64_t d, int64_t m, float X,
+                   int torch_threads, int use_l1, float l1_in, float* scratch) {
+    float L = use_l1 ? l1_in : uqo_l1_torch_order(x, d, torch_threads, scratch);
+    const float den = L + 1e-12f;
+    const float fm = (float)m;
+    double acc = 0.0;
+    float c_prev = 0.0f;
+    for (int64_t i = 0; i < d; ++i) {
+        float v = x[i] / den;
+        float p = fabsf(v);
+        float mp = fm * p;
+        float fl = floorf(mp);
+        float fr = mp - fl;
+        acc += (double)fr;
+        float c = (float)acc;
+        float diff = floorf(c - X) - floorf(c_prev - X);
+        float r = (diff == 1.0f) ? 1.0f : 0.0f;
+        float t = (L * torch_sign(v)) * (fl + r);
+        out[i] = t / fm;
+        c_prev = c;
+    }
+    return L;
+}
+
+void uqo_quantize_batch(const float* x, float* out, int64_t n, int64_t d, int64_t m,
+                        const float* X, int torch_threads, float* l1_out, float* scratch) {
+    for (int64_t j = 0; j < n; ++j) {
+        float L = uqo_quantize(x + j * d, out + j * d, d, m, X[j], torch_threads, 0, 0.0f, scratch);
+        if (l1_out) l1_out[j] = L;
+    }
+}
+
+/* Normal_dist.py:137 — est += q / n, client order, f32. */
+void uqo_client_mean(const float* q, int64_t n, int64_t d, float n_div, float* est) {
+    for (int64_t i = 0; i < d; ++i) est[i] = 0.0f;
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i < d; ++i) est[i] += q[j * d + i] / n_div;
+}

@@ -1,0 +1,74 @@
+"""ctypes handle on the C oracle (oracle/uq_oracle.c).  Test infrastructure only:
+used by tests/ and bench.py's cpu_baseline leg as the checker, never shipped."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "libuq_oracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        i64, f, p = ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+        L.uqo_l1_torch_order.restype = f
+        L.uqo_l1_torch_order.argtypes = [p, i64, ctypes.c_int, p]
+        L.uqo_quantize.restype = f
+        L.uqo_quantize.argtypes = [p, p, i64, i64, f, ctypes.c_int, ctypes.c_int, f, p]
+        L.uqo_quantize_batch.restype = None
+        L.uqo_quantize_batch.argtypes = [p, p, i64, i64, i64, p, ctypes.c_int, p, p]
+        L.uqo_client_mean.restype = None
+        L.uqo_client_mean.argtypes = [p, i64, i64, f, p]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def l1_torch_order(x, torch_threads: int = 1) -> np.float32:
+    x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1)
+    scratch = np.empty(max(1, x.shape[0]), np.float32)
+    return np.float32(lib().uqo_l1_torch_order(_ptr(x), x.shape[0], torch_threads, _ptr(scratch)))
+
+
+def quantize_batch(x2d, m: int, X, torch_threads: int = 1):
+    x2d = np.ascontiguousarray(x2d, dtype=np.float32)
+    n, d = x2d.shape
+    X = np.ascontiguousarray(X, dtype=np.float32).reshape(n)
+    out = np.empty_like(x2d)
+    l1 = np.empty(n, np.float32)
+    scratch = np.empty(max(1, d), np.float32)
+    lib().uqo_quantize_batch(_ptr(x2d), _ptr(out), n, d, m, _ptr(X), torch_threads, _ptr(l1), _ptr(scratch))
+    return out, l1
+
+
+def quantize_with_l1(x, m: int, X: float, l1: float):
+    x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1)
+    out = np.empty_like(x)
+    scratch = np.empty(1, np.float32)
+    lib().uqo_quantize(_ptr(x), _ptr(out), x.shape[0], m, np.float32(X), 1, 1, np.float32(l1), _ptr(scratch))
+    return out
+
+
+def client_mean(q2d, n_div):
+    q2d = np.ascontiguousarray(q2d, dtype=np.float32)
+    n, d = q2d.shape
+    est = np.empty(d, np.float32)
+    lib().uqo_client_mean(_ptr(q2d), n, d, np.float32(n_div), _ptr(est))
+    return est

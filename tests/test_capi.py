@@ -1,0 +1,77 @@
+"""The C-ABI library loads and exports every symbol include/uq_dme.h declares, and its
+host-only entry points behave (no GPU needed: no kernel is launched here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import uqdme
+from uqdme import RATE_TABLE, rate_to_m
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "uq_dme.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(uq_[a-z0-9_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return uqdme.load_library()
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for n in ("uq_type_unbiased_f32", "uq_l1_torch_order_f32", "uq_client_mean_f32",
+              "uq_workspace_bytes", "uq_last_error", "uq_rate_to_m", "uq_check_status",
+              "uq_type_unbiased_mean_f32", "uq_version"):
+        assert n in names
+
+
+def test_library_exports_all_declared_symbols(lib):
+    from uqdme_amd import _lib as L
+    for n in declared_functions():
+        assert hasattr(lib, n), n
+        assert n in L.SIGNATURES, f"ctypes signature missing for {n}"
+
+
+def test_version_and_rate_table(lib):
+    assert lib.uq_version() >= 100
+    m = ctypes.c_int64()
+    for bits, l in RATE_TABLE.items():
+        for d in (1, 2, 1000, 1024, 172554, 1 << 20, 1 << 22):
+            assert lib.uq_rate_to_m(float(bits), d, ctypes.byref(m)) == 0
+            assert m.value == rate_to_m(bits, d) == int(l * d)
+    assert lib.uq_rate_to_m(3.3, 10, ctypes.byref(m)) == -1
+    assert b"KeyError" in lib.uq_last_error()
+
+
+def test_workspace_and_argument_errors(lib):
+    b = ctypes.c_size_t()
+    assert lib.uq_workspace_bytes(1024, 1 << 20, 1, ctypes.byref(b)) == 0
+    assert b.value >= 1024 * 256 * 8
+    assert lib.uq_workspace_bytes(4, 1000, 0, ctypes.byref(b)) == -1
+    assert lib.uq_workspace_bytes(-1, 1000, 1, ctypes.byref(b)) == -1
+    # empty batches are no-ops that never touch the device
+    assert lib.uq_type_unbiased_f32(None, None, 0, 100, 10, None, None, None, 1, None, 0, None) == 0
+    assert lib.uq_type_unbiased_f32(None, None, 4, 0, 0, None, None, None, 1, None, 0, None) == 0
+    # invalid arguments are rejected before any launch
+    assert lib.uq_type_unbiased_f32(None, None, 4, 100, 10, None, None, None, 1, None, 0, None) == -1
+    assert lib.uq_type_unbiased_f32(ctypes.c_void_p(16), ctypes.c_void_p(16), 4, 100, 10, ctypes.c_void_p(16),
+                                    None, None, 1, ctypes.c_void_p(16), 10, None) == -3
+    assert lib.uq_type_unbiased_f32(ctypes.c_void_p(16), ctypes.c_void_p(16), 4, 100, -5, ctypes.c_void_p(16),
+                                    None, None, 1, ctypes.c_void_p(16), 1 << 30, None) == -1
+    assert lib.uq_l1_torch_order_f32(ctypes.c_void_p(16), 4, 100, 65, None, ctypes.c_void_p(16), 1 << 30, None) == -1
+    assert lib.uq_client_mean_f32(None, 3, 10, 3.0, 0, None, None) == -1
+
+
+def test_drop_in_signature_and_name():
+    import inspect
+    f = uqdme.Type_unbiased_quantize
+    assert f.__name__ == "Type_unbiased_quantize"
+    sig = inspect.signature(f)
+    assert list(sig.parameters) == ["input_vector", "bits_per_dimension"]
+    assert sig.parameters["bits_per_dimension"].default == 1

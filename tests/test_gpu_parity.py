@@ -1,0 +1,225 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden fixtures
+and the CPU oracle on the same seeded inputs.  Bit-exact unless a test says otherwise;
+the north_star's floating-point tolerance (NMSE within 1e-6 relative) is written where
+it applies."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import uq_oracle as O
+from oracle import uq_oracle_c as C
+from tests import golden_data as G
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def uq(gpu_ready):
+    import uqdme
+    return uqdme
+
+
+def dev(a):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=f32)).cuda()
+
+
+def test_c1_harness_bit_exact(uq):
+    z = G.c1()
+    x = dev(z["x"])
+    q1, l1 = uq.quantize_dequantize(x, 1, X=z["X1"], torch_threads=1, return_l1=True)
+    q2 = uq.quantize_dequantize(x, 2, X=z["X2"], torch_threads=1)
+    assert G.bits_equal(q1.cpu().numpy(), z["q1"])
+    assert G.bits_equal(q2.cpu().numpy(), z["q2"])
+    e1 = uq.client_mean(q1, 16).cpu().numpy()
+    e2 = uq.client_mean(q2, 16).cpu().numpy()
+    assert G.bits_equal(e1, z["est1"])
+    assert G.bits_equal(e2, z["est2"])
+    n1 = O.script_nmse(e1, z["emp"], float(z["vec_norm_squared"]), 16)
+    n2 = O.script_nmse(e2, z["emp"], float(z["vec_norm_squared"]), 16)
+    assert abs(n1 - float(z["nmse1"])) <= 1e-6 * float(z["nmse1"])   # north_star tolerance
+    assert abs(n2 - float(z["nmse2"])) <= 1e-6 * float(z["nmse2"])
+    ref_l1 = [O.l1_torch_order(z["x"][j], 1) for j in range(16)]
+    assert G.bits_equal(l1.cpu().numpy(), np.array(ref_l1, f32))
+
+
+def test_fused_quantize_mean_matches_two_step(uq):
+    z = G.c1()
+    x = dev(z["x"])
+    est = uq.quantize_mean(x, 1, X=z["X1"], n_div=16, torch_threads=1)
+    assert G.bits_equal(est.cpu().numpy(), z["est1"])
+
+
+def test_edge_cases_bit_exact(uq):
+    n = 0
+    for name, R, X, x, q in G.edge_cases():
+        got = uq.quantize_dequantize(dev(x[None]), R, X=[X], torch_threads=1)[0].cpu().numpy()
+        assert G.bits_equal(got, q), (name, R, G.n_mismatch(got, q))
+        n += 1
+    assert n > 40
+
+
+def test_spec_vectors_mid_bit_exact(uq):
+    for sp, q, _, _ in G.spec_vectors(large=False):
+        x = G.spec_gen(sp)
+        got, l1 = uq.quantize_dequantize(dev(x[None]), sp["R"], X=[sp["X"]], torch_threads=sp["threads"],
+                                         return_l1=True)
+        assert l1.cpu().numpy()[0] == f32(sp["l1"]), sp
+        got = got[0].cpu().numpy()
+        assert G.bits_equal(got, q), (sp["dist"], sp["d"], sp["R"], G.n_mismatch(got, q))
+
+
+def test_spec_vectors_large_bit_exact(uq):
+    for sp, _, pos, qs in G.spec_vectors(large=True):
+        x = G.spec_gen(sp)
+        got, l1 = uq.quantize_dequantize(dev(x[None]), sp["R"], X=[sp["X"]], torch_threads=sp["threads"],
+                                         return_l1=True)
+        assert l1.cpu().numpy()[0] == f32(sp["l1"]), sp
+        got = got[0].cpu().numpy()
+        assert G.bits_equal(got[pos], qs), sp
+        assert G.sha(got) == sp["q_sha256"], (sp["dist"], sp["d"], sp["R"], sp["threads"])
+
+
+@pytest.mark.parametrize("T", [1, 2, 3, 8])
+def test_l1_torch_order_sweep(uq, T):
+    rng = np.random.default_rng(100 + T)
+    sizes = [1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 32, 33, 63, 64, 65, 511, 512, 513, 8191, 8192, 8193,
+             32767, 32768, 32769, 65535, 65536, 65537, 100003, 172554, 262144, 1 << 20]
+    for d in sizes:
+        x = (rng.standard_normal((3, d)) * rng.choice([1e-30, 1e-3, 1.0, 1e3, 1e30])).astype(f32)
+        got = uq.l1_torch_order(dev(x), T).cpu().numpy()
+        ref = np.array([C.l1_torch_order(x[j], T) for j in range(3)], f32)
+        assert G.bits_equal(got, ref), (d, T, got, ref)
+
+
+def test_random_batches_vs_oracle(uq):
+    rng = np.random.default_rng(7)
+    gens = [lambda s: rng.normal(0, 1, s), lambda s: rng.laplace(1, 2, s), lambda s: rng.lognormal(1, 2, s),
+            lambda s: rng.gamma(2, 2, s), lambda s: rng.choice(2, s, p=[.3, .7]).astype(float),
+            lambda s: rng.uniform(-1, 1, s)]
+    total = 0
+    for d in (1, 3, 4, 17, 100, 1001, 4095, 4096, 4097, 12289, 65536, 100003, 172554):
+        for gi, g in enumerate(gens):
+            n = 5
+            x = g((n, d)).astype(f32)
+            for R in (0.5, 1, 2, 6.5, 10):
+                X = rng.random(n).astype(f32)
+                m = O.rate_to_m(R, d)
+                got = uq.quantize_dequantize(dev(x), m=m, X=X, torch_threads=1).cpu().numpy()
+                ref, _ = C.quantize_batch(x, m, X, 1)
+                bad = G.n_mismatch(got, ref)
+                assert bad == 0, (d, gi, R, bad)
+                total += 1
+    assert total > 300
+
+
+def test_full_size_c2_subset_bit_exact_and_properties(uq):
+    """C2 shape (d=2^20): 32 clients bit-exact against the C oracle; then the whole
+    1024-client batch through size-independent properties: sum k == m per client and
+    |q| = L1*k/m reconstruction."""
+    d = 1 << 20
+    g = torch.Generator(device="cuda").manual_seed(0)
+    n = 1024
+    x = torch.randn(n, d, generator=g, device="cuda")
+    X = uq.draw_uniforms(n, torch.Generator().manual_seed(1))
+    m = O.rate_to_m(1, d)
+    q, l1 = uq.quantize_dequantize(x, m=m, X=X, torch_threads=1, return_l1=True)
+    torch.cuda.synchronize()
+    uq.check_status()
+    xs = x[:32].cpu().numpy()
+    ref, ref_l1 = C.quantize_batch(xs, m, X[:32].numpy(), 1)
+    assert G.bits_equal(l1[:32].cpu().numpy(), ref_l1)
+    assert G.n_mismatch(q[:32].cpu().numpy(), ref) == 0
+    # sum of lattice counts == m exactly, for every client (AS:640 with sum(fl + r) = m)
+    k = torch.round(q.abs().double() * m / l1.double()[:, None])
+    assert torch.all(k.sum(dim=1) == m)
+    # |q| * m / L1 is an integer count up to f32 rounding
+    assert torch.all((q.abs().double() * m / l1.double()[:, None] - k).abs() < 1e-3)
+    assert torch.all(k >= 0)
+
+
+def test_unbiasedness_statistical(uq):
+    """E[q] = x: average many independent quantizations of one vector."""
+    d, reps = 4096, 4000
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(d).astype(f32)
+    xb = dev(np.repeat(x[None], reps, axis=0))
+    X = uq.draw_uniforms(reps, torch.Generator().manual_seed(5))
+    q = uq.quantize_dequantize(xb, 1, X=X, torch_threads=1)
+    mean = q.double().mean(0).cpu().numpy()
+    L = float(np.abs(x).sum())
+    m = O.rate_to_m(1, d)
+    # per-coordinate std of q is <= L/m * 0.5; the error of the mean shrinks by sqrt(reps)
+    tol = 6 * 0.5 * L / m / np.sqrt(reps)
+    assert np.max(np.abs(mean - x)) < tol
+
+
+def test_drop_in_matches_reference_semantics(uq):
+    rng = np.random.default_rng(21)
+    uq.set_torch_threads(1)
+    try:
+        for d in (1, 5, 1000, 4099):
+            x = rng.standard_normal(d).astype(f32)
+            for R in (1, 2):
+                torch.manual_seed(77)
+                got = uq.Type_unbiased_quantize(x, R)
+                assert got.is_cuda and got.dtype == torch.float32 and got.shape == (d,)
+                torch.manual_seed(77)
+                X = torch.rand(1).item()
+                ref = O.type_unbiased_quantize(x, R, X)
+                assert G.bits_equal(got.cpu().numpy(), ref)
+                # one RNG draw consumed per call, like AS:634
+                torch.manual_seed(77)
+                uq.Type_unbiased_quantize(torch.from_numpy(x), R)
+                a = torch.rand(1)
+                torch.manual_seed(77)
+                torch.rand(1)
+                b = torch.rand(1)
+                assert a.item() == b.item()
+        xin = torch.from_numpy(rng.standard_normal(64).astype(f32)).cuda()
+        keep = xin.clone()
+        out = uq.Type_unbiased_quantize(xin, 1)
+        assert torch.equal(xin, keep) and out.data_ptr() != xin.data_ptr()
+        with pytest.raises(KeyError):
+            uq.Type_unbiased_quantize(xin, 3.3)
+        with pytest.raises(RuntimeError):
+            uq.Type_unbiased_quantize(torch.zeros(4, 4), 1)
+        assert uq.Type_unbiased_quantize(torch.zeros(0), 1).numel() == 0
+        # float64 and list inputs are rounded to f32 like torch.tensor(..., float32)
+        x64 = rng.standard_normal(300)
+        torch.manual_seed(3)
+        a = uq.Type_unbiased_quantize(x64, 1).cpu().numpy()
+        torch.manual_seed(3)
+        b = uq.Type_unbiased_quantize(list(x64.astype(f32)), 1).cpu().numpy()
+        assert G.bits_equal(a, b)
+    finally:
+        uq.set_torch_threads(None)
+
+
+def test_deterministic_repeat_and_unaligned(uq):
+    rng = np.random.default_rng(9)
+    d = 300001   # not a multiple of 4 -> unaligned rows -> scalar-load path
+    x = rng.laplace(1, 2, (6, d)).astype(f32)
+    X = rng.random(6).astype(f32)
+    a = uq.quantize_dequantize(dev(x), 2, X=X, torch_threads=1).cpu().numpy()
+    b = uq.quantize_dequantize(dev(x), 2, X=X, torch_threads=1).cpu().numpy()
+    assert G.bits_equal(a, b)
+    ref, _ = C.quantize_batch(x, O.rate_to_m(2, d), X, 1)
+    assert G.n_mismatch(a, ref) == 0
+    # offset view: base pointer not 16-B aligned
+    big = dev(np.concatenate([np.zeros(1, f32), x.reshape(-1)]))
+    xv = big[1:].view(6, d)
+    c = uq.quantize_dequantize(xv, 2, X=X, torch_threads=1).cpu().numpy()
+    assert G.bits_equal(a, c)
+
+
+def test_client_mean_order_and_accumulate(uq):
+    rng = np.random.default_rng(4)
+    for n, d in ((1, 10), (7, 1001), (33, 4096), (200, 65536)):
+        q = rng.standard_normal((n, d)).astype(f32)
+        got = uq.client_mean(dev(q), n).cpu().numpy()
+        assert G.bits_equal(got, C.client_mean(q, n)), (n, d)
+        est = uq.client_mean(dev(q[: n // 2 + 1]), n)
+        if n // 2 + 1 < n:
+            est = uq.client_mean(dev(q[n // 2 + 1:]), n, est=est, accumulate=True)
+        assert G.bits_equal(est.cpu().numpy(), C.client_mean(q, n)), (n, d, "split")

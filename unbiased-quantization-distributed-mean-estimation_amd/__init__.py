@@ -1,0 +1,19 @@
+"""MI355X-native unbiased L1-ball type quantizer for distributed mean estimation.
+
+Reference: Ritesh622/Unbiased-Quantization-Distributed-Mean-Estimation,
+`Type_unbiased_quantize` (NMSE_Results/Codes/All_Schemes.py:609-641) and the client
+mean around it (NMSE_Results/Codes/Normal_dist.py:133-138).  Import through the
+top-level alias `uqdme` (this directory name is not a Python identifier).
+"""
+from .rates import RATE_TABLE, rate_to_m
+from .quantizer import (
+    Type_unbiased_quantize, quantize_dequantize, client_mean, quantize_mean,
+    l1_torch_order, draw_uniforms, set_torch_threads, get_torch_threads, check_status,
+)
+from ._lib import UQError, load as load_library, library_path
+
+__all__ = [
+    "RATE_TABLE", "rate_to_m", "Type_unbiased_quantize", "quantize_dequantize", "client_mean",
+    "quantize_mean", "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
+    "check_status", "UQError", "load_library", "library_path",
+]

@@ -1,0 +1,70 @@
+"""ctypes binding of the C-ABI in include/uq_dme.h.
+
+Loading fails loudly: there is no CPU fallback anywhere in the product path.  The
+library is found in-tree (`_build/libuq_dme.so`); build it with build_ext.py or
+`__graft_entry__.build()`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from . import build_ext
+
+_lock = threading.Lock()
+_lib = None
+
+# (name, restype, argtypes) — must match include/uq_dme.h exactly.
+_i32, _i64, _f32, _f64, _p, _sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_float,
+                                   ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t)
+SIGNATURES = {
+    "uq_version": (ctypes.c_int, []),
+    "uq_last_error": (ctypes.c_char_p, []),
+    "uq_rate_to_m": (ctypes.c_int, [_f64, _i64, ctypes.POINTER(_i64)]),
+    "uq_workspace_bytes": (ctypes.c_int, [_i64, _i64, _i32, ctypes.POINTER(_sz)]),
+    "uq_l1_torch_order_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _sz, _p]),
+    "uq_type_unbiased_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _i32, _p, _sz, _p]),
+    "uq_client_mean_f32": (ctypes.c_int, [_p, _i64, _i64, _f32, _i32, _p, _p]),
+    "uq_type_unbiased_mean_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _p, _p, _i32, _f32, _i32, _p,
+                                                 _p, _sz, _p]),
+    "uq_check_status": (ctypes.c_int, [_p, _p]),
+}
+
+
+class UQError(RuntimeError):
+    """A C-ABI call returned a negative code."""
+
+
+def library_path() -> str:
+    return build_ext.SO
+
+
+def load(build_if_missing: bool = False):
+    """Load (once) and return the ctypes library.  Raises if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = library_path()
+        if not os.path.exists(path):
+            if build_if_missing:
+                build_ext.build()
+            else:
+                raise ImportError(
+                    f"HIP extension not built: {path} is missing. Run "
+                    "`python unbiased-quantization-distributed-mean-estimation_amd/build_ext.py` "
+                    "(no CPU fallback exists by design).")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().uq_last_error()
+        raise UQError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

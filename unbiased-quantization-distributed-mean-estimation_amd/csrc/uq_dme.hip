@@ -1,0 +1,651 @@
+// uq_dme.hip — MI355X (gfx950) kernels + C-ABI for the unbiased L1-ball type quantizer.
+//
+// Reference path (paths relative to the reference root):
+//   NMSE_Results/Codes/All_Schemes.py:609-641   Type_unbiased_quantize
+//   NMSE_Results/Codes/Normal_dist.py:137-138    est += Q(v, R) / n   (client mean)
+//
+// Kernels (one HIP stage per group of reference torch ops):
+//   K1a l1_partial_kernel   AS:624 |x|.sum(), torch CPU cascade: level-1 block sums
+//   K1b l1_finalize_kernel  AS:624 the rest of the cascade tree, one wave per client
+//   K2  quantize_kernel     AS:625-640 normalize -> floor/frac -> fp64 scan (cumsum)
+//                           -> crossing test -> dequantize, decoupled look-back
+//   K3  client_mean_kernel  ND:137-138 client-ordered f32 mean
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (no FMA contraction: the
+// reference computes m*p then floor then subtract as separate f32 ops), IEEE f32
+// division and denormals kept (the reference runs on torch CPU).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/uq_dme.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kGrain = 32768;     // at::internal::GRAIN_SIZE (torch CPU intra-op split)
+constexpr int kMaxChunks = 64;    // torch_threads supported by the L1 plan
+constexpr uint64_t kEmpty = ~0ull;                   // "aggregate not yet published"
+constexpr uint64_t kCanonNaN = 0x7FF8000000000000ull;  // NaN aggregates are canonicalised
+
+// ---- quantize tile geometry --------------------------------------------------------
+constexpr int kQBlock = 256;               // threads per workgroup (4 waves)
+constexpr int kQItems = 16;                // contiguous elements per thread
+constexpr int kQTile = kQBlock * kQItems;  // 4096 elements per tile
+constexpr int kQPad = 20;                  // LDS floats per thread row (16 + 4 pad)
+
+// ---- workspace layout --------------------------------------------------------------
+// [0,256)            control: u32 ticket, u32 status (sticky timeout flag)
+// [256, ...)         u64 agg[n][tiles]           (look-back aggregates)
+// then               f32 l1part[n][groups][32]  (level-1 block sums)
+// then               f32 l1[n]                  (computed norms)
+constexpr size_t kCtrlBytes = 256;
+
+struct L1Plan {
+    int32_t nchunks;
+    int32_t total_groups;            // level-1 groups per vector, all chunks
+    int64_t off[kMaxChunks];         // chunk offset (elements)
+    int64_t size[kMaxChunks];        // chunk length
+    int32_t lp[kMaxChunks];          // log2(step)
+    int32_t ng1[kMaxChunks];         // full level-1 groups in chunk
+    int32_t gbase[kMaxChunks];       // first group index of chunk
+};
+
+inline int ceil_log2_i64(int64_t x) {
+    if (x <= 1) return 0;
+    int r = 0;
+    uint64_t v = (uint64_t)(x - 1);
+    while (v) { ++r; v >>= 1; }
+    return r;
+}
+
+// Mirrors torch CPU: d < GRAIN or T == 1 -> one chunk; else nt = min(T, ceil(d/GRAIN))
+// chunks of ceil(d/nt), reduced independently and added in chunk order.
+bool make_plan(int64_t d, int32_t T, L1Plan* p) {
+    std::memset(p, 0, sizeof(*p));
+    if (T < 1) T = 1;
+    int64_t nt = 1, cs = d;
+    if (!(d < kGrain || T == 1)) {
+        nt = (d + kGrain - 1) / kGrain;
+        if (nt > T) nt = T;
+        cs = (d + nt - 1) / nt;
+    }
+    if (nt > kMaxChunks) return false;
+    int32_t g = 0, c = 0;
+    for (int64_t k = 0; k < nt; ++k) {
+        int64_t b = k * cs, e = b + cs < d ? b + cs : d;
+        if (e <= b) continue;
+        int64_t s = e - b;
+        p->off[c] = b;
+        p->size[c] = s;
+        int64_t rows = (s / 8) / 4;   // rows of 32 floats (8 lanes x 4 ILP)
+        int lp = ceil_log2_i64(rows) / 4;
+        if (lp < 4) lp = 4;
+        if (lp > 8) return false;
+        int64_t step = (int64_t)1 << lp;
+        int64_t nleaf = rows / step;
+        int64_t ng1 = nleaf / step;
+        if (ng1 > (int64_t)1 << 28) return false;
+        p->lp[c] = lp;
+        p->ng1[c] = (int32_t)ng1;
+        p->gbase[c] = g;
+        g += (int32_t)ng1;
+        ++c;
+    }
+    p->nchunks = c;
+    p->total_groups = g;
+    return true;
+}
+
+__device__ __forceinline__ float torch_sign(float v) {
+    // torch.sign: +1 / -1, and 0 for +-0 and NaN (AS:640 v.sign()).
+    return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f);
+}
+
+__device__ __forceinline__ uint64_t ld_relaxed_agent(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_relaxed_agent32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// =====================================================================================
+// K1a: level-1 block sums of |x| in torch cascade order.
+// One workgroup = one level-1 group = step leaves x step rows x 32 streams.
+// Thread (leaf b, quad q) sums rows [b*step, (b+1)*step) of streams 4q..4q+3
+// sequentially (ATen level 0); then 32 threads add the step leaves in order (level 1).
+// =====================================================================================
+template <bool VEC4>
+__global__ void __launch_bounds__(256)
+l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __restrict__ part) {
+    const int64_t vec = blockIdx.y;
+    int32_t G = blockIdx.x;
+    int c = 0;
+    while (c + 1 < plan.nchunks && G >= plan.gbase[c + 1]) ++c;
+    const int32_t g = G - plan.gbase[c];
+    const int lp = plan.lp[c];
+    const int step = 1 << lp;
+    const int tid = threadIdx.x;
+    const int nthreads = 8 * step;            // 8 quads x step leaves
+    __shared__ float leaf[256 * 4];           // [leaf][32] (step <= 32 -> <= 1024 floats)
+    const float* base = x + vec * d + plan.off[c] + (int64_t)g * step * step * 32;
+    if (tid < nthreads) {
+        const int q = tid & 7;
+        const int b = tid >> 3;
+        const float* p = base + ((int64_t)b * step) * 32 + 4 * q;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        for (int r = 0; r < step; ++r) {
+            float v0, v1, v2, v3;
+            if (VEC4) {
+                const float4 t = *reinterpret_cast<const float4*>(p + (int64_t)r * 32);
+                v0 = t.x; v1 = t.y; v2 = t.z; v3 = t.w;
+            } else {
+                const float* pr = p + (int64_t)r * 32;
+                v0 = pr[0]; v1 = pr[1]; v2 = pr[2]; v3 = pr[3];
+            }
+            a0 += fabsf(v0); a1 += fabsf(v1); a2 += fabsf(v2); a3 += fabsf(v3);
+        }
+        float* l = leaf + b * 32 + 4 * q;
+        l[0] = a0; l[1] = a1; l[2] = a2; l[3] = a3;
+    }
+    __syncthreads();
+    if (tid < 32) {
+        float acc = 0.f;
+        for (int b = 0; b < step; ++b) acc += leaf[b * 32 + tid];
+        part[(vec * plan.total_groups + G) * 32 + tid] = acc;
+    }
+}
+
+// Sequential sum of `nrows` rows of stream `a` starting at element `start` (|x|).
+__device__ float seq_rows(const float* __restrict__ xv, int64_t start, int64_t nrows, int a) {
+    float acc = 0.f;
+    for (int64_t r = 0; r < nrows; ++r) acc += fabsf(xv[start + r * 32 + a]);
+    return acc;
+}
+
+// =====================================================================================
+// K1b: finish the cascade for each client (one wave per client).
+// Lanes 0..31 own the 32 streams (8 lanes x 4 ILP): level-2/3 accumulation over the
+// level-1 block sums, the open level-1 group and the tail rows (ATen multi_row_sum),
+// then the ILP/lane/tail combination of ATen row_sum / vectorized_inner_sum, then the
+// chunk results in chunk order (torch parallel_reduce).
+// =====================================================================================
+__global__ void __launch_bounds__(64)
+l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
+                   const float* __restrict__ part, float* __restrict__ l1_out) {
+    const int64_t vec = blockIdx.x;
+    const int lane = threadIdx.x;
+    const float* xv = x + vec * d;
+    __shared__ float fin[32];
+    float total = 0.f;
+    for (int c = 0; c < plan.nchunks; ++c) {
+        const int64_t off = plan.off[c];
+        const int64_t s = plan.size[c];
+        float chunk_sum;
+        if (s < 8) {
+            // ATen scalar row_sum (ILP 4, rows < step -> all rows land in acc0).
+            float p[4] = {0.f, 0.f, 0.f, 0.f};
+            if (s >= 4)
+                for (int k = 0; k < 4; ++k) p[k] = 0.f + fabsf(xv[off + k]);
+            for (int64_t k = (s >= 4 ? 4 : 0); k < s; ++k) p[0] += fabsf(xv[off + k]);
+            chunk_sum = ((p[0] + p[1]) + p[2]) + p[3];
+        } else {
+            const int64_t vs = s / 8, rows = vs / 4;
+            const int lp = plan.lp[c];
+            const int64_t step = (int64_t)1 << lp;
+            const int64_t nleaf = rows / step;
+            const int64_t ng1 = plan.ng1[c];
+            const int64_t ng2 = ng1 / step;
+            if (lane < 32) {
+                const float* pp = part + (vec * plan.total_groups + plan.gbase[c]) * 32 + lane;
+                float acc3 = 0.f;
+                for (int64_t h = 0; h < ng2; ++h) {
+                    float b2 = 0.f;
+                    for (int64_t k = 0; k < step; ++k) b2 += pp[(h * step + k) * 32];
+                    acc3 += b2;
+                }
+                float acc2 = 0.f;
+                for (int64_t k = ng2 * step; k < ng1; ++k) acc2 += pp[k * 32];
+                float acc1 = 0.f;
+                for (int64_t b = ng1 * step; b < nleaf; ++b)
+                    acc1 += seq_rows(xv, off + b * step * 32, step, lane);
+                float acc0 = seq_rows(xv, off + nleaf * step * 32, rows - nleaf * step, lane);
+                fin[lane] = ((acc0 + acc1) + acc2) + acc3;
+            }
+            __syncthreads();
+            if (lane == 0) {
+                float p0[8];
+                for (int l = 0; l < 8; ++l) p0[l] = fin[l];
+                for (int64_t v = rows * 4; v < vs; ++v)
+                    for (int l = 0; l < 8; ++l) p0[l] += fabsf(xv[off + v * 8 + l]);
+                for (int k = 1; k < 4; ++k)
+                    for (int l = 0; l < 8; ++l) p0[l] += fin[k * 8 + l];
+                float acc = 0.f;
+                for (int64_t k = vs * 8; k < s; ++k) acc += fabsf(xv[off + k]);
+                for (int l = 0; l < 8; ++l) acc += p0[l];
+                fin[0] = acc;
+            }
+            __syncthreads();
+            chunk_sum = fin[0];
+            __syncthreads();
+        }
+        total += chunk_sum;
+    }
+    if (lane == 0) l1_out[vec] = total;
+}
+
+// =====================================================================================
+// K2: fused normalize / floor / fp64 scan / crossing / dequantize, one 4096-element
+// tile per workgroup.  Tiles are taken in ticket order (atomic counter), so a tile
+// only ever waits on tiles that have already started: no residency assumption.
+//
+// Scan (AS:635): torch CPU cumsum of f32 accumulates sequentially in fp64 and rounds
+// each prefix to f32.  Here each thread adds its 16 fractional parts sequentially in
+// fp64 from an fp64 base = (tile prefix) + (thread-exclusive prefix in the tile); the
+// tile prefix is the sum of ALL predecessor tile aggregates in a fixed order (every
+// predecessor publishes its aggregate as one 8-byte relaxed agent-scope store that is
+// its own ready flag), so the result is deterministic run to run.
+// =====================================================================================
+__device__ __forceinline__ double wave_incl_scan(double v, int lane) {
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const double t = __shfl_up(v, o, kWave);
+        if (lane >= o) v = t + v;
+    }
+    return v;
+}
+
+template <bool VEC4>
+__global__ void __launch_bounds__(kQBlock)
+quantize_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, int32_t tiles,
+                float fm, const float* __restrict__ Xs, const float* __restrict__ l1,
+                uint64_t* __restrict__ agg, uint32_t* __restrict__ ctrl) {
+    __shared__ __attribute__((aligned(16))) float s_data[kQBlock * kQPad];
+    __shared__ double s_wave[kQBlock / kWave];
+    __shared__ double s_prefix;
+    __shared__ uint32_t s_ticket;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wid = tid / kWave;
+    if (tid == 0) s_ticket = atomicAdd(ctrl, 1u);
+    __syncthreads();
+    const uint32_t ticket = s_ticket;
+    const int64_t vec = ticket / (uint32_t)tiles;
+    const int32_t tile = ticket % (uint32_t)tiles;
+    const int64_t t0 = (int64_t)tile * kQTile;
+    const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+    const float* xt = x + vec * d + t0;
+    float* ot = out + vec * d + t0;
+
+    // ---- stage the tile through LDS: coalesced global reads, padded rows ----------
+    if (VEC4 && len == kQTile) {
+#pragma unroll
+        for (int j = 0; j < kQTile / 4 / kQBlock; ++j) {
+            const int q = tid + j * kQBlock;   // float4 index in the tile
+            const float4 v = reinterpret_cast<const float4*>(xt)[q];
+            *reinterpret_cast<float4*>(&s_data[(q + (q >> 2)) * 4]) = v;
+        }
+    } else {
+        for (int i = tid; i < kQTile; i += kQBlock) {
+            const float v = i < len ? xt[i] : 0.0f;
+            s_data[i + (i >> 4) * 4] = v;
+        }
+    }
+    __syncthreads();
+
+    const float L = l1[vec];
+    const float den = L + 1e-12f;          // AS:625 (f32 add)
+    const float Xv = Xs[vec];
+    const float Ls_pos = L * 1.0f, Ls_neg = L * -1.0f, Ls_zero = L * 0.0f;
+
+    float xv[kQItems];
+    {
+        const float4* src = reinterpret_cast<const float4*>(&s_data[tid * kQPad]);
+#pragma unroll
+        for (int k = 0; k < kQItems / 4; ++k) {
+            const float4 t = src[k];
+            xv[4 * k] = t.x; xv[4 * k + 1] = t.y; xv[4 * k + 2] = t.z; xv[4 * k + 3] = t.w;
+        }
+    }
+    const int i0 = tid * kQItems;   // first element of this thread within the tile
+    float flv[kQItems], frv[kQItems], lsv[kQItems];
+    double tsum = 0.0;
+#pragma unroll
+    for (int k = 0; k < kQItems; ++k) {
+        const float v = xv[k] / den;       // AS:625 IEEE f32 division
+        const float p = fabsf(v);          // AS:626
+        const float mp = fm * p;           // AS:629
+        const float fl = floorf(mp);       // AS:630
+        float fr = mp - fl;                // AS:631
+        if (i0 + k >= len) fr = 0.0f;
+        const float sg = torch_sign(v);
+        flv[k] = fl;
+        frv[k] = fr;
+        lsv[k] = sg > 0.f ? Ls_pos : (sg < 0.f ? Ls_neg : Ls_zero);   // L1 * sign(v)
+        tsum += (double)fr;
+    }
+
+    // ---- block exclusive scan of the thread sums (fixed tree => deterministic) -----
+    const double incl = wave_incl_scan(tsum, lane);
+    double wexcl = __shfl_up(incl, 1, kWave);
+    if (lane == 0) wexcl = 0.0;
+    if (lane == kWave - 1) s_wave[wid] = incl;
+    __syncthreads();
+    double wbase = 0.0, tile_total = 0.0;
+#pragma unroll
+    for (int w = 0; w < kQBlock / kWave; ++w) {
+        if (w < wid) wbase += s_wave[w];
+        tile_total += s_wave[w];
+    }
+    const double texcl = wbase + wexcl;
+
+    // ---- publish this tile's aggregate, then sum all predecessors (look-back) ------
+    uint64_t* aggv = agg + vec * tiles;
+    if (tid == 0) {
+        uint64_t bits = __double_as_longlong(tile_total);
+        if (tile_total != tile_total) bits = kCanonNaN;
+        st_relaxed_agent(&aggv[tile], bits);
+    }
+    if (wid == 0) {
+        double acc = 0.0;
+        if (tile > 0) {
+            bool timed_out = false;
+            for (int32_t u = lane; u < tile; u += kWave) {
+                uint64_t b = ld_relaxed_agent(&aggv[u]);
+                uint32_t spins = 0;
+                while (b == kEmpty) {
+                    __builtin_amdgcn_s_sleep(2);
+                    b = ld_relaxed_agent(&aggv[u]);
+                    if (++spins > (1u << 20) || ld_relaxed_agent32(ctrl + 1) != 0u) {
+                        timed_out = true;
+                        break;
+                    }
+                }
+                if (timed_out) break;
+                acc += __longlong_as_double(b);
+            }
+            if (timed_out) __hip_atomic_store(ctrl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // fixed-shape tree over the lanes
+#pragma unroll
+            for (int o = kWave / 2; o > 0; o >>= 1) acc = acc + __shfl_xor(acc, o, kWave);
+        }
+        if (lane == 0) s_prefix = acc;
+    }
+    __syncthreads();
+
+    // ---- per element: prefix c_i, crossing test, dequantize (AS:635-640) ----------
+    double s = s_prefix + texcl;
+    float c_prev = (float)s;
+    float ov[kQItems];
+#pragma unroll
+    for (int k = 0; k < kQItems; ++k) {
+        s += (double)frv[k];
+        const float c = (float)s;
+        const float diff = floorf(c - Xv) - floorf(c_prev - Xv);   // AS:636
+        const float r = (diff == 1.0f) ? 1.0f : 0.0f;             // AS:637
+        ov[k] = (lsv[k] * (flv[k] + r)) / fm;                      // AS:640
+        c_prev = c;
+    }
+    __syncthreads();   // everyone has read s_data
+    {
+        float4* dst = reinterpret_cast<float4*>(&s_data[tid * kQPad]);
+#pragma unroll
+        for (int k = 0; k < kQItems / 4; ++k)
+            dst[k] = make_float4(ov[4 * k], ov[4 * k + 1], ov[4 * k + 2], ov[4 * k + 3]);
+    }
+    __syncthreads();
+    if (VEC4 && len == kQTile) {
+#pragma unroll
+        for (int j = 0; j < kQTile / 4 / kQBlock; ++j) {
+            const int q = tid + j * kQBlock;
+            reinterpret_cast<float4*>(ot)[q] = *reinterpret_cast<const float4*>(&s_data[(q + (q >> 2)) * 4]);
+        }
+    } else {
+        for (int i = tid; i < len; i += kQBlock) ot[i] = s_data[i + (i >> 4) * 4];
+    }
+}
+
+// =====================================================================================
+// K3: est[i] (+)= q[j][i] / n_div, j = 0..n-1 in order (ND:137-138).
+// Each thread owns 4 consecutive columns; loads for 8 clients are issued ahead.
+// =====================================================================================
+template <bool VEC4>
+__global__ void __launch_bounds__(256)
+client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, float n_div, int accumulate,
+                   float* __restrict__ est) {
+    const int64_t col = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (col >= d) return;
+    if (VEC4) {
+        float4 e = accumulate ? *reinterpret_cast<const float4*>(est + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+        int64_t j = 0;
+        for (; j + 8 <= n; j += 8) {
+            float4 t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const float4*>(q + (j + u) * d + col);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                e.x += t[u].x / n_div; e.y += t[u].y / n_div;
+                e.z += t[u].z / n_div; e.w += t[u].w / n_div;
+            }
+        }
+        for (; j < n; ++j) {
+            const float4 t = *reinterpret_cast<const float4*>(q + j * d + col);
+            e.x += t.x / n_div; e.y += t.y / n_div; e.z += t.z / n_div; e.w += t.w / n_div;
+        }
+        *reinterpret_cast<float4*>(est + col) = e;
+    } else {
+        const int cnt = (int)((d - col) < 4 ? (d - col) : 4);
+        for (int k = 0; k < cnt; ++k) {
+            float e = accumulate ? est[col + k] : 0.f;
+            for (int64_t j = 0; j < n; ++j) e += q[j * d + col + k] / n_div;
+            est[col + k] = e;
+        }
+    }
+}
+
+// ---- host-side helpers ---------------------------------------------------------------
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) return fail(UQ_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return UQ_OK;
+}
+
+struct WsLayout {
+    size_t agg_off, part_off, l1_off, total;
+    int32_t tiles;
+};
+
+WsLayout layout(int64_t n, int64_t d, const L1Plan& plan) {
+    WsLayout w{};
+    const int64_t tiles = (d + kQTile - 1) / kQTile;
+    w.tiles = (int32_t)tiles;
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    w.agg_off = kCtrlBytes;
+    w.part_off = up(w.agg_off + (size_t)n * tiles * sizeof(uint64_t));
+    w.l1_off = up(w.part_off + (size_t)n * plan.total_groups * 32 * sizeof(float));
+    w.total = up(w.l1_off + (size_t)n * sizeof(float));
+    return w;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int launch_l1(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* part, float* l1_out,
+              hipStream_t st) {
+    if (plan.total_groups > 0) {
+        bool vec4 = aligned16(x) && (d % 4 == 0);
+        for (int c = 0; c < plan.nchunks; ++c) vec4 = vec4 && (plan.off[c] % 4 == 0);
+        int maxstep = 16;
+        for (int c = 0; c < plan.nchunks; ++c) maxstep = std::max(maxstep, 1 << plan.lp[c]);
+        if (maxstep > 32) return fail(UQ_E_INVALID, "L1 cascade step > 32 unsupported (d too large)");
+        dim3 grid(plan.total_groups, (unsigned)n);
+        dim3 block(8 * maxstep);
+        if (vec4)
+            hipLaunchKernelGGL(l1_partial_kernel<true>, grid, block, 0, st, x, d, plan, part);
+        else
+            hipLaunchKernelGGL(l1_partial_kernel<false>, grid, block, 0, st, x, d, plan, part);
+        int rc = hip_check(hipGetLastError(), "l1_partial_kernel launch");
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(l1_finalize_kernel, dim3((unsigned)n), dim3(64), 0, st, x, d, plan, part, l1_out);
+    return hip_check(hipGetLastError(), "l1_finalize_kernel launch");
+}
+
+int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_t ws_bytes,
+                 L1Plan* plan, WsLayout* w) {
+    if (n < 0 || d < 0) return fail(UQ_E_INVALID, "n and d must be >= 0");
+    if (n > (int64_t)1 << 31 || d > (int64_t)1 << 40) return fail(UQ_E_INVALID, "n or d too large");
+    if (T < 1 || T > kMaxChunks) return fail(UQ_E_INVALID, "torch_threads must be in [1, 64]");
+    if (!make_plan(d, T, plan)) return fail(UQ_E_INVALID, "cannot build L1 plan for this d/torch_threads");
+    *w = layout(n, d, *plan);
+    if ((int64_t)w->tiles * n > 0xFFFFFFFFll) return fail(UQ_E_INVALID, "batch too large for one call");
+    if (n > 0 && d > 0) {
+        if (!x) return fail(UQ_E_INVALID, "null input pointer");
+        if (!ws) return fail(UQ_E_INVALID, "null workspace");
+        if (ws_bytes < w->total) return fail(UQ_E_WORKSPACE, "workspace too small");
+    }
+    return UQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int uq_version(void) { return 100; }
+
+const char* uq_last_error(void) { return g_err.c_str(); }
+
+int uq_rate_to_m(double bits, int64_t d, int64_t* m_out) {
+    // AS:614-620
+    static const double keys[20] = {0.5, 1, 1.5, 2, 2.5, 3, 3.5, 4, 4.5, 5,
+                                    5.5, 6, 6.5, 7, 7.5, 8, 8.5, 9, 9.5, 10};
+    static const double vals[20] = {0.08282, 0.21403, 0.39443, 0.63752, 0.96656, 1.41725, 2.04187,
+                                    2.91504, 4.14217, 5.87195, 8.31416, 11.76507, 16.64332, 23.54075,
+                                    33.29414, 47.0868, 66.59204, 94.17625, 133.18596, 188.35383};
+    if (!m_out) return fail(UQ_E_INVALID, "null m_out");
+    if (d < 0) return fail(UQ_E_INVALID, "d must be >= 0");
+    for (int i = 0; i < 20; ++i)
+        if (bits == keys[i]) {
+            *m_out = (int64_t)(vals[i] * (double)d);   // AS:623 int(l * d), truncation
+            return UQ_OK;
+        }
+    return fail(UQ_E_INVALID, "bits_per_dimension not in the rate table (reference raises KeyError)");
+}
+
+int uq_workspace_bytes(int64_t n, int64_t d, int32_t T, size_t* bytes_out) {
+    if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
+    L1Plan plan;
+    if (n < 0 || d < 0 || T < 1 || T > kMaxChunks) return fail(UQ_E_INVALID, "bad n/d/torch_threads");
+    if (!make_plan(d, T, &plan)) return fail(UQ_E_INVALID, "cannot build L1 plan");
+    *bytes_out = layout(n, d, plan).total;
+    return UQ_OK;
+}
+
+int uq_l1_torch_order_f32(const float* x, int64_t n, int64_t d, int32_t T, float* l1_out, void* ws,
+                          size_t ws_bytes, void* stream) {
+    L1Plan plan;
+    WsLayout w;
+    int rc = check_common(x, n, d, T, ws, ws_bytes, &plan, &w);
+    if (rc) return rc;
+    if (n == 0) return UQ_OK;
+    if (!l1_out) return fail(UQ_E_INVALID, "null l1_out");
+    hipStream_t st = (hipStream_t)stream;
+    if (d == 0) return hip_check(hipMemsetAsync(l1_out, 0, n * sizeof(float), st), "memset l1");
+    float* part = (float*)((char*)ws + w.part_off);
+    return launch_l1(x, n, d, plan, part, l1_out, st);
+}
+
+int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m, const float* X,
+                         const float* l1, float* l1_out, int32_t T, void* ws, size_t ws_bytes,
+                         void* stream) {
+    L1Plan plan;
+    WsLayout w;
+    int rc = check_common(x, n, d, T, ws, ws_bytes, &plan, &w);
+    if (rc) return rc;
+    if (m < 0) return fail(UQ_E_INVALID, "m must be >= 0");
+    if (n == 0 || d == 0) return UQ_OK;
+    if (!out || !X) return fail(UQ_E_INVALID, "null out or X");
+    hipStream_t st = (hipStream_t)stream;
+    char* wsb = (char*)ws;
+    float* l1buf = (float*)(wsb + w.l1_off);
+    const float* l1use = l1;
+    if (!l1use) {
+        rc = launch_l1(x, n, d, plan, (float*)(wsb + w.part_off), l1buf, st);
+        if (rc) return rc;
+        l1use = l1buf;
+    }
+    if (l1_out && l1_out != l1use) {
+        rc = hip_check(hipMemcpyAsync(l1_out, l1use, n * sizeof(float), hipMemcpyDeviceToDevice, st), "copy l1");
+        if (rc) return rc;
+    }
+    rc = hip_check(hipMemsetAsync(wsb, 0, sizeof(uint32_t), st), "memset ticket");
+    if (rc) return rc;
+    rc = hip_check(hipMemsetAsync(wsb + w.agg_off, 0xFF, (size_t)n * w.tiles * sizeof(uint64_t), st), "memset agg");
+    if (rc) return rc;
+    const float fm = (float)m;   // torch casts the Python int to f32 for `m * p` and `/ m`
+    const bool vec4 = aligned16(x) && aligned16(out) && (d % 4 == 0);
+    dim3 grid((unsigned)(w.tiles * n));
+    if (vec4)
+        hipLaunchKernelGGL(quantize_kernel<true>, grid, dim3(kQBlock), 0, st, x, out, d, w.tiles, fm, X, l1use,
+                           (uint64_t*)(wsb + w.agg_off), (uint32_t*)wsb);
+    else
+        hipLaunchKernelGGL(quantize_kernel<false>, grid, dim3(kQBlock), 0, st, x, out, d, w.tiles, fm, X, l1use,
+                           (uint64_t*)(wsb + w.agg_off), (uint32_t*)wsb);
+    return hip_check(hipGetLastError(), "quantize_kernel launch");
+}
+
+int uq_client_mean_f32(const float* q, int64_t n, int64_t d, float n_div, int32_t accumulate, float* est,
+                       void* stream) {
+    if (n < 0 || d < 0) return fail(UQ_E_INVALID, "n and d must be >= 0");
+    if (d == 0) return UQ_OK;
+    if (!est || (n > 0 && !q)) return fail(UQ_E_INVALID, "null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const bool vec4 = (n == 0 || aligned16(q)) && aligned16(est) && (d % 4 == 0);
+    const int64_t threads = (d + 3) / 4;
+    dim3 grid((unsigned)((threads + 255) / 256));
+    if (vec4)
+        hipLaunchKernelGGL(client_mean_kernel<true>, grid, dim3(256), 0, st, q, n, d, n_div, accumulate, est);
+    else
+        hipLaunchKernelGGL(client_mean_kernel<false>, grid, dim3(256), 0, st, q, n, d, n_div, accumulate, est);
+    return hip_check(hipGetLastError(), "client_mean_kernel launch");
+}
+
+int uq_type_unbiased_mean_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m, const float* X,
+                              const float* l1, int32_t T, float n_div, int32_t accumulate, float* est,
+                              void* ws, size_t ws_bytes, void* stream) {
+    if (!out) return fail(UQ_E_INVALID, "out must be non-NULL in this version");
+    int rc = uq_type_unbiased_f32(x, out, n, d, m, X, l1, nullptr, T, ws, ws_bytes, stream);
+    if (rc) return rc;
+    return uq_client_mean_f32(out, n, d, n_div, accumulate, est, stream);
+}
+
+int uq_check_status(void* ws, void* stream) {
+    if (!ws) return fail(UQ_E_INVALID, "null workspace");
+    hipStream_t st = (hipStream_t)stream;
+    uint32_t status = 0;
+    int rc = hip_check(hipMemcpyAsync(&status, (char*)ws + 4, 4, hipMemcpyDeviceToHost, st), "read status");
+    if (rc) return rc;
+    rc = hip_check(hipStreamSynchronize(st), "sync");
+    if (rc) return rc;
+    if (status) {
+        (void)hipMemsetAsync((char*)ws + 4, 0, 4, st);
+        (void)hipStreamSynchronize(st);
+        return fail(UQ_E_TIMEOUT, "inter-workgroup wait timed out");
+    }
+    return UQ_OK;
+}
+
+}  // extern "C"

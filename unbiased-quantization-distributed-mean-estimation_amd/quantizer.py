@@ -1,0 +1,225 @@
+"""Host-side mirror of the reference's quantizer interface, backed by HIP kernels.
+
+Drop-in:
+    Type_unbiased_quantize(input_vector, bits_per_dimension=1)
+        == NMSE_Results/Codes/All_Schemes.py:609-641, same name, argument meaning,
+        return type (new f32 tensor of shape (d,) on the GPU), RNG use (one draw from
+        torch's global CPU generator per call, AS:634) and errors (KeyError for an
+        unknown rate, AS:622; RuntimeError for non-1-D input, AS:635).
+
+Batched APIs (what the DME harness and the bench use):
+    quantize_dequantize(x[n, d], bits | m=, X[n])       -> q[n, d]
+    client_mean(q[n, d], n_div, est=None)                 -> est[d]   (ND:137-138)
+    quantize_mean(x[n, d], bits, X[n], n_div, est=None)   -> est[d]
+    l1_torch_order(x[n, d], torch_threads)                -> l1[n]    (AS:624)
+
+Every path calls the C-ABI in include/uq_dme.h; nothing here computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+import torch
+
+from . import _lib
+from .rates import RATE_TABLE, rate_to_m
+
+__all__ = [
+    "Type_unbiased_quantize", "quantize_dequantize", "client_mean", "quantize_mean",
+    "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
+]
+
+_ws_lock = threading.Lock()
+_ws_cache: dict = {}
+_torch_threads_override = None
+
+
+def set_torch_threads(t):
+    """Pin the torch-CPU summation order used for L1 (AS:624).  None -> follow
+    torch.get_num_threads() at call time, i.e. what the CPU reference would do in
+    this process."""
+    global _torch_threads_override
+    _torch_threads_override = None if t is None else int(t)
+
+
+def get_torch_threads() -> int:
+    if _torch_threads_override is not None:
+        return _torch_threads_override
+    env = os.environ.get("UQDME_TORCH_THREADS")
+    if env:
+        return int(env)
+    return int(torch.get_num_threads())
+
+
+def _device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("uqdme requires a ROCm GPU (no CPU fallback by design)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _stream_ptr(dev: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
+    """Per (device, stream) workspace, grown on demand (stream-ordered reuse)."""
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    with _ws_lock:
+        ws = _ws_cache.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
+            _ws_cache[key] = ws
+        return ws
+
+
+def _ws_bytes(n: int, d: int, T: int) -> int:
+    out = ctypes.c_size_t(0)
+    _lib.check(_lib.load().uq_workspace_bytes(n, d, T, ctypes.byref(out)), "uq_workspace_bytes")
+    return int(out.value)
+
+
+def draw_uniforms(n: int, generator: torch.Generator | None = None) -> torch.Tensor:
+    """n draws of AS:634's X from a CPU generator; torch.rand(n) equals n successive
+    torch.rand(1) calls, so this reproduces a per-client loop of the reference."""
+    return torch.rand(n, generator=generator, dtype=torch.float32)
+
+
+def _as_device_f32_2d(x, dev) -> torch.Tensor:
+    if not torch.is_tensor(x):
+        x = torch.as_tensor(np.asarray(x), dtype=torch.float32)
+    if x.dim() != 2:
+        raise ValueError("expected a 2-D [n, d] batch")
+    return x.to(device=dev, dtype=torch.float32).contiguous()
+
+
+def _resolve_m(bits, m, d):
+    if m is not None:
+        return int(m)
+    return rate_to_m(bits, d)
+
+
+def l1_torch_order(x, torch_threads: int | None = None) -> torch.Tensor:
+    """AS:624 `|x|.sum()` per row, bit-identical to torch CPU with `torch_threads` threads."""
+    dev = _device()
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    T = get_torch_threads() if torch_threads is None else int(torch_threads)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    nb = _ws_bytes(n, d, T)
+    ws = _workspace(dev, nb)
+    _lib.check(_lib.load().uq_l1_torch_order_f32(_ptr(x), n, d, T, _ptr(out), _ptr(ws), ws.numel(),
+                                                  _stream_ptr(dev)), "uq_l1_torch_order_f32")
+    return out
+
+
+def quantize_dequantize(x, bits_per_dimension=1, X=None, *, m: int | None = None,
+                        torch_threads: int | None = None, l1=None, out=None,
+                        return_l1: bool = False, generator: torch.Generator | None = None):
+    """Batched `Type_unbiased_quantize`: row j of `x` is quantized with uniform X[j].
+
+    X defaults to n fresh draws from the CPU generator (global one unless given)."""
+    dev = _device()
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    mm = _resolve_m(bits_per_dimension, m, d)
+    T = get_torch_threads() if torch_threads is None else int(torch_threads)
+    if X is None:
+        X = draw_uniforms(n, generator)
+    X = torch.as_tensor(X, dtype=torch.float32).reshape(-1).to(dev)
+    if X.numel() != n:
+        raise ValueError("X must have one draw per row")
+    if l1 is not None:
+        l1 = torch.as_tensor(l1, dtype=torch.float32).reshape(-1).to(dev).contiguous()
+        if l1.numel() != n:
+            raise ValueError("l1 must have one value per row")
+    if out is None:
+        out = torch.empty_like(x)
+    elif out.shape != x.shape or out.dtype != torch.float32 or out.device != x.device or not out.is_contiguous():
+        raise ValueError("out must be a contiguous f32 tensor like x")
+    l1_out = torch.empty(n, dtype=torch.float32, device=dev) if return_l1 else None
+    nb = _ws_bytes(n, d, T)
+    ws = _workspace(dev, nb)
+    _lib.check(_lib.load().uq_type_unbiased_f32(_ptr(x), _ptr(out), n, d, mm, _ptr(X), _ptr(l1), _ptr(l1_out),
+                                                T, _ptr(ws), ws.numel(), _stream_ptr(dev)),
+               "uq_type_unbiased_f32")
+    return (out, l1_out) if return_l1 else out
+
+
+def client_mean(q, n_div, est=None, accumulate: bool = False) -> torch.Tensor:
+    """ND:137-138: est (+)= q[j] / n_div over rows j in order (f32)."""
+    dev = _device()
+    q = _as_device_f32_2d(q, dev)
+    n, d = q.shape
+    if est is None:
+        est = torch.empty(d, dtype=torch.float32, device=dev)
+        accumulate = False
+    _lib.check(_lib.load().uq_client_mean_f32(_ptr(q), n, d, float(n_div), int(bool(accumulate)), _ptr(est),
+                                              _stream_ptr(dev)), "uq_client_mean_f32")
+    return est
+
+
+def quantize_mean(x, bits_per_dimension=1, X=None, n_div=None, *, m: int | None = None,
+                  torch_threads: int | None = None, est=None, accumulate: bool = False, out=None):
+    """Quantize every row and fold it into the client-ordered mean (ND:133-138)."""
+    dev = _device()
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    mm = _resolve_m(bits_per_dimension, m, d)
+    T = get_torch_threads() if torch_threads is None else int(torch_threads)
+    if X is None:
+        X = draw_uniforms(n)
+    X = torch.as_tensor(X, dtype=torch.float32).reshape(-1).to(dev)
+    if n_div is None:
+        n_div = n
+    if est is None:
+        est = torch.empty(d, dtype=torch.float32, device=dev)
+        accumulate = False
+    if out is None:
+        out = torch.empty_like(x)
+    nb = _ws_bytes(n, d, T)
+    ws = _workspace(dev, nb)
+    _lib.check(_lib.load().uq_type_unbiased_mean_f32(_ptr(x), _ptr(out), n, d, mm, _ptr(X), _ptr(None), T,
+                                                     float(n_div), int(bool(accumulate)), _ptr(est),
+                                                     _ptr(ws), ws.numel(), _stream_ptr(dev)),
+               "uq_type_unbiased_mean_f32")
+    return est
+
+
+def check_status() -> None:
+    """Synchronise the current stream and raise if an in-kernel wait timed out."""
+    dev = _device()
+    for (idx, sp), ws in list(_ws_cache.items()):
+        if idx == dev.index and sp == torch.cuda.current_stream(dev).cuda_stream:
+            _lib.check(_lib.load().uq_check_status(_ptr(ws), _stream_ptr(dev)), "uq_check_status")
+
+
+def Type_unbiased_quantize(input_vector, bits_per_dimension=1):
+    """Drop-in for NMSE_Results/Codes/All_Schemes.py:609 (same name: the Flower client
+    derives directory names from `__name__`, FLM:177).
+
+    AS:611  always copies `input_vector` to a new f32 tensor on the device
+    AS:622  unknown `bits_per_dimension` -> KeyError (checked before any work)
+    AS:634  consumes exactly one draw of torch's global CPU generator
+    Returns a new f32 tensor of shape (d,) on the GPU."""
+    dev = _device()
+    l_rate = RATE_TABLE[bits_per_dimension]          # KeyError like the reference
+    if torch.is_tensor(input_vector):
+        v = input_vector.detach().to(device=dev, dtype=torch.float32).clone()
+    else:
+        v = torch.tensor(np.asarray(input_vector), dtype=torch.float32, device=dev)
+    if v.dim() != 1:
+        raise RuntimeError("Type_unbiased_quantize expects a 1-D vector "
+                           "(the reference fails at torch.cat for other ranks)")
+    d = v.numel()
+    m = int(l_rate * d)
+    X = torch.rand(1)                                   # AS:634 (global CPU generator)
+    if d == 0:
+        return v
+    return quantize_dequantize(v.view(1, d), X=X, m=m).view(d)
