@@ -49,7 +49,8 @@ int uq_rate_to_m(double bits_per_dimension, int64_t d, int64_t* m_out);
 
 /* Bytes of device workspace needed by the calls below for a batch of n vectors of
  * length d summed in torch order for `torch_threads`.  The workspace also holds the
- * status word read by uq_check_status(). */
+ * status word read by uq_check_status().  A workspace must be zero-filled once before
+ * its first use (later calls re-initialise what they need themselves). */
 int uq_workspace_bytes(int64_t n, int64_t d, int32_t torch_threads, size_t* bytes_out);
 
 /* AS:624 — l1_out[j] = sum_i |x[j][i]| in torch CPU cascade order (f32 accumulate). */

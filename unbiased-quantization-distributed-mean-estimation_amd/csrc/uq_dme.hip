@@ -40,7 +40,9 @@ constexpr int kQTile = kQBlock * kQItems;  // 4096 elements per tile
 constexpr int kQPad = 20;                  // LDS floats per thread row (16 + 4 pad)
 
 // ---- workspace layout --------------------------------------------------------------
-// [0,256)            control: u32 ticket, u32 status (sticky timeout flag)
+// [0,256)            control: u32 ticket, u32 abort (both reset by every call),
+//                    u32 sticky error word (set on timeout; cleared by uq_check_status).
+//                    A new workspace must be zero-filled once before first use.
 // [256, ...)         u64 agg[n][tiles]           (look-back aggregates)
 // then               f32 l1part[n][groups][32]  (level-1 block sums)
 // then               f32 l1[n]                  (computed norms)
@@ -372,7 +374,10 @@ quantize_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d,
                 if (timed_out) break;
                 acc += __longlong_as_double(b);
             }
-            if (timed_out) __hip_atomic_store(ctrl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (timed_out) {
+                __hip_atomic_store(ctrl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             // fixed-shape tree over the lanes
 #pragma unroll
             for (int o = kWave / 2; o > 0; o >>= 1) acc = acc + __shfl_xor(acc, o, kWave);
@@ -591,7 +596,7 @@ int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64
         rc = hip_check(hipMemcpyAsync(l1_out, l1use, n * sizeof(float), hipMemcpyDeviceToDevice, st), "copy l1");
         if (rc) return rc;
     }
-    rc = hip_check(hipMemsetAsync(wsb, 0, sizeof(uint32_t), st), "memset ticket");
+    rc = hip_check(hipMemsetAsync(wsb, 0, 2 * sizeof(uint32_t), st), "memset ticket/abort");
     if (rc) return rc;
     rc = hip_check(hipMemsetAsync(wsb + w.agg_off, 0xFF, (size_t)n * w.tiles * sizeof(uint64_t), st), "memset agg");
     if (rc) return rc;
@@ -636,12 +641,12 @@ int uq_check_status(void* ws, void* stream) {
     if (!ws) return fail(UQ_E_INVALID, "null workspace");
     hipStream_t st = (hipStream_t)stream;
     uint32_t status = 0;
-    int rc = hip_check(hipMemcpyAsync(&status, (char*)ws + 4, 4, hipMemcpyDeviceToHost, st), "read status");
+    int rc = hip_check(hipMemcpyAsync(&status, (char*)ws + 8, 4, hipMemcpyDeviceToHost, st), "read status");
     if (rc) return rc;
     rc = hip_check(hipStreamSynchronize(st), "sync");
     if (rc) return rc;
     if (status) {
-        (void)hipMemsetAsync((char*)ws + 4, 0, 4, st);
+        (void)hipMemsetAsync((char*)ws + 8, 0, 4, st);
         (void)hipStreamSynchronize(st);
         return fail(UQ_E_TIMEOUT, "inter-workgroup wait timed out");
     }

@@ -74,7 +74,8 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
     with _ws_lock:
         ws = _ws_cache.get(key)
         if ws is None or ws.numel() < nbytes:
-            ws = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
+            # zero-filled once: the C-ABI requires a zeroed control block on first use
+            ws = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
             _ws_cache[key] = ws
         return ws
 
