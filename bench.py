@@ -1,0 +1,245 @@
+"""Throughput bench for the unbiased L1-ball type quantizer (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1], "C2"): per GPU, n=1024 client vectors of d=2^20
+i.i.d. N(0,1) f32, resident in HBM before timing; rate R=1 (m = 224426); L1 in the
+torch-CPU order of 1 thread.  One step = one pass of the hot path over the batch:
+    K1 torch-order L1 (AS:624)  ->  K2 fused quantize/dequantize (AS:625-640, writes q)
+    ->  K3 client-ordered mean (ND:137-138)  ->  [N>1] one RCCL reduce of est to rank 0.
+Clients shard across GPUs with no data-path collective except that final reduce
+(weak scaling: 1024 clients per GPU).  value = all clients processed / max-over-ranks
+time, in M-vectors/s.
+
+Rank 0 prints ONE JSON line.  `roofline` is computed for K2 from HIP events recorded
+around its launches inside the timed region (algorithmic bytes = 8*d per vector: read
+x + write q).  `cpu_baseline` times the C restatement of the reference path (oracle/,
+the checker) on this host for a bounded sample of the same clients, and the same
+sample doubles as a bit-parity and NMSE check of the GPU output.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "quantize+dequantize M-vectors/sec at d=2^20 (1/2/4/8 GPU) + NMSE vs reference"
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--clients", type=int, default=1024, help="clients per GPU")
+    ap.add_argument("--dim", type=int, default=1 << 20)
+    ap.add_argument("--bits", type=float, default=1)
+    ap.add_argument("--torch-threads", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/pmc_*.json)")
+    return ap.parse_args()
+
+
+def dist_init(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, rank, world, local
+    torch.cuda.set_device(0)
+    return None, 0, 1, 0
+
+
+def load_traffic(path, d, n):
+    """Per-launch HBM bytes of the quantize kernel from a committed PMC summary."""
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    for p in reversed(cands):
+        try:
+            j = json.load(open(p))
+        except Exception:
+            continue
+        if j.get("d") == d and j.get("clients") == n and "quantize_bytes_per_launch" in j:
+            return float(j["quantize_bytes_per_launch"]), os.path.relpath(p, ROOT)
+    return None, None
+
+
+def main():
+    args = parse()
+    dist, rank, world, local = dist_init(args)
+    import uqdme
+    from uqdme_amd import _lib
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n, d = args.clients, args.dim
+    m = uqdme.rate_to_m(args.bits, d)
+    T = args.torch_threads
+    n_total = n * world
+
+    # ---- synthetic inputs resident in HBM (generation is outside the timed region) ----
+    g = torch.Generator(device=dev).manual_seed(args.seed + 7919 * rank)
+    x = torch.randn(n, d, generator=g, device=dev, dtype=torch.float32)
+    X_cpu = torch.rand(n_total, generator=torch.Generator().manual_seed(args.seed))[rank * n:(rank + 1) * n]
+    X = X_cpu.to(dev)
+    q = torch.empty_like(x)
+    l1 = torch.empty(n, dtype=torch.float32, device=dev)
+    est = torch.empty(d, dtype=torch.float32, device=dev)
+    lib = _lib.load()
+    nb = ctypes_size(lib, n, d, T)
+    ws = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    P = lambda t: t.data_ptr()  # noqa: E731
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        _lib.check(lib.uq_l1_torch_order_f32(P(x), n, d, T, P(l1), P(ws), nb, sp), "l1")
+        if ev is not None:
+            ev[1].record(stream)
+        _lib.check(lib.uq_type_unbiased_f32(P(x), P(q), n, d, m, P(X), P(l1), None, T, P(ws), nb, sp), "quantize")
+        if ev is not None:
+            ev[2].record(stream)
+        _lib.check(lib.uq_client_mean_f32(P(q), n, d, float(n_total), 0, P(est), sp), "mean")
+        if ev is not None:
+            ev[3].record(stream)
+        if dist is not None:
+            dist.reduce(est, dst=0, op=dist.ReduceOp.SUM)
+        if ev is not None:
+            ev[4].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.check(lib.uq_check_status(P(ws), sp), "status after warmup")
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.check(lib.uq_check_status(P(ws), sp), "status after timed steps")
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    seg = np.array([[evs[k][i].elapsed_time(evs[k][i + 1]) for i in range(4)] for k in range(args.steps)])
+    seg_ms = seg.mean(axis=0)  # l1, quantize, mean, reduce
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = n_total * args.steps / elapsed / 1e6
+
+    q_ms = float(seg_ms[1])
+    alg_bytes = 8.0 * d * n                       # read x + write q, per quantize launch
+    achieved = alg_bytes / (q_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(args.traffic_json, d, n)
+
+    result = None
+    if rank == 0:
+        result = {
+            "metric": METRIC, "value": round(value, 6), "unit": "M-vectors/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: i.i.d. N(0,1) f32 per client (torch CUDA generator), X ~ U[0,1) from a CPU generator",
+            "config": {"workload": "C2 (BASELINE.json configs[1]): 1024 clients/GPU x d=2^20, Gaussian, R=1, "
+                                   "unbiased L1 type quantizer + client-ordered mean" + (" + RCCL reduce" if world > 1 else ""),
+                       "clients_per_gpu": n, "d": d, "bits_per_dimension": args.bits, "m": m,
+                       "torch_threads_l1_order": T, "parallelism": f"client-sharded x{world}"},
+            "kernel_ms": {"l1": round(float(seg_ms[0]), 4), "quantize": round(q_ms, 4),
+                          "client_mean": round(float(seg_ms[2]), 4), "reduce": round(float(seg_ms[3]), 4)},
+            "roofline": {"kernel": "quantize_kernel (K2)", "bound": "hbm", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "alg_bytes_per_launch": alg_bytes},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"], result["parity_sample"] = cpu_baseline(args, x, X_cpu, q, m, T)
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def ctypes_size(lib, n, d, T):
+    import ctypes
+    from uqdme_amd import _lib
+    b = ctypes.c_size_t()
+    _lib.check(lib.uq_workspace_bytes(n, d, T, ctypes.byref(b)), "workspace")
+    return int(b.value)
+
+
+def cpu_baseline(args, x, X_cpu, q, m, T):
+    """Time the C restatement of the reference path (oracle/, a checker) on host cores
+    for a bounded sample of the same clients; verify the GPU output on that sample."""
+    from oracle import uq_oracle_c as C
+    from oracle import uq_oracle as O
+    n, d = x.shape
+    budget = args.cpu_seconds
+    done = 0
+    t_cpu = 0.0
+    mism = 0
+    outs = []
+    idx = []
+    # spread the sample over the batch
+    order = list(range(0, n, max(1, n // 64))) + [j for j in range(n) if j % max(1, n // 64)]
+    for j in order:
+        xj = x[j].cpu().numpy()[None]
+        t0 = time.perf_counter()
+        ref, _ = C.quantize_batch(xj, m, X_cpu[j:j + 1].numpy(), T)
+        t_cpu += time.perf_counter() - t0
+        mism += int(np.count_nonzero(q[j].cpu().numpy().view(np.uint32) != ref[0].view(np.uint32)))
+        outs.append(ref[0])
+        idx.append(j)
+        done += 1
+        if t_cpu >= budget:
+            break
+    # NMSE on the sample (script formula ND:151-157), GPU vs CPU restatement
+    xs = x[idx].cpu().numpy()
+    emp = (xs.sum(axis=0, dtype=np.float32) / np.float32(len(idx))).astype(np.float32)
+    vns = float(np.sum(xs.astype(np.float64) ** 2))
+    est_gpu = C.client_mean(q[idx].cpu().numpy(), len(idx))
+    est_cpu = C.client_mean(np.stack(outs), len(idx))
+    nmse_gpu = O.script_nmse(est_gpu, emp, vns, len(idx))
+    nmse_cpu = O.script_nmse(est_cpu, emp, vns, len(idx))
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    base = {"value": round(done / t_cpu / 1e6, 9), "unit": "M-vectors/s", "cores": 1, "kind": "port",
+            "sample": f"{done} of the {n} benchmark clients (d=2^20, R=1), single-threaded C restatement "
+                      f"oracle/uq_oracle.c, {t_cpu:.1f} s on '{cpu_model}' ({os.cpu_count()} logical CPUs visible)",
+            "ms_per_vector": round(t_cpu * 1e3 / done, 3)}
+    par = {"clients_checked": done, "bit_mismatches": mism, "nmse_gpu": nmse_gpu, "nmse_cpu": nmse_cpu,
+           "nmse_rel_diff": abs(nmse_gpu - nmse_cpu) / max(nmse_cpu, 1e-300)}
+    return base, par
+
+
+if __name__ == "__main__":
+    main()
