@@ -1,0 +1,42 @@
+"""Timing-only ablation of the quantize kernel: builds variants with -D switches and
+times each on the C2 batch.  Results of ablated builds are wrong by construction."""
+import ctypes, os, subprocess, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = os.path.join(ROOT, "unbiased-quantization-distributed-mean-estimation_amd")
+SRC = os.path.join(PKG, "csrc", "uq_dme.hip")
+OUT = os.path.join(PKG, "_build", "abl")
+VARIANTS = {"base": [], "fastdiv": ["-DUQ_ABL_FAST_DIV"]}
+def build():
+    sys.path.insert(0, PKG)
+    import build_ext as be
+    os.makedirs(OUT, exist_ok=True)
+    for k, fl in VARIANTS.items():
+        subprocess.run([be.hipcc(), *be.HIPCC_FLAGS, *fl, "-o", os.path.join(OUT, f"{k}.so"), SRC], check=True)
+    for extra in sys.argv[2:]:          # name=path/to/alternative.hip
+        k, src = extra.split("=", 1)
+        subprocess.run([be.hipcc(), *be.HIPCC_FLAGS, "-I", os.path.join(PKG, "csrc"), "-o", os.path.join(OUT, f"{k}.so"), src], check=True)
+def run():
+    import torch
+    n, d = int(os.environ.get("N", 1024)), 1 << 20
+    x = torch.randn(n, d, device="cuda"); q = torch.empty_like(x)
+    X = torch.rand(n, device="cuda"); l1 = x.abs().sum(1)
+    names = sorted(f[:-3] for f in os.listdir(OUT) if f.endswith(".so"))
+    for k in names:
+        L = ctypes.CDLL(os.path.join(OUT, f"{k}.so"))
+        b = ctypes.c_size_t(); L.uq_workspace_bytes(ctypes.c_int64(n), ctypes.c_int64(d), 1, ctypes.byref(b))
+        ws = torch.zeros(b.value, dtype=torch.uint8, device="cuda")
+        f = L.uq_type_unbiased_f32
+        f.argtypes = [ctypes.c_void_p]*2 + [ctypes.c_int64]*3 + [ctypes.c_void_p]*3 + [ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        sp = torch.cuda.current_stream().cuda_stream
+        call = lambda: f(x.data_ptr(), q.data_ptr(), n, d, 224426, X.data_ptr(), l1.data_ptr(), None, 1, ws.data_ptr(), b.value, sp)
+        for _ in range(3): assert call() == 0
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10): call()
+        e1.record(); torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 10
+        print(f"{k:12s} {ms:8.3f} ms  {8*d*n/ms/1e6:8.1f} GB/s", flush=True)
+if __name__ == "__main__":
+    build() if sys.argv[1] == "build" else run()

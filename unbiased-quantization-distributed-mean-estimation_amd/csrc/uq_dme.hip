@@ -37,13 +37,17 @@ constexpr uint64_t kCanonNaN = 0x7FF8000000000000ull;  // NaN aggregates are can
 constexpr int kQBlock = 256;               // threads per workgroup (4 waves)
 constexpr int kQItems = 16;                // contiguous elements per thread
 constexpr int kQTile = kQBlock * kQItems;  // 4096 elements per tile
-constexpr int kQPad = 20;                  // LDS floats per thread row (16 + 4 pad)
+// LDS tile image: 256 rows of 16 floats (thread t owns row t).  Float4 column c of row r
+// lives at r*16 + 4*(c ^ ((r >> 2) & 3)): conflict-free for the per-row ds_read_b128 of
+// every lane group and for the coalesced staging writes, with no padding.
+constexpr int64_t kStreamMinClients = 256; // >= this many clients: one workgroup per vector
 
 // ---- workspace layout --------------------------------------------------------------
 // [0,256)            control: u32 ticket, u32 abort (both reset by every call),
 //                    u32 sticky error word (set on timeout; cleared by uq_check_status).
 //                    A new workspace must be zero-filled once before first use.
-// [256, ...)         u64 agg[n][tiles]           (look-back aggregates)
+// [256, ...)         u64 agg[n][tiles]           (look-back: tile aggregates A_t)
+// then               u64 incl[n][tiles]          (look-back: inclusive prefixes P_{t+1})
 // then               f32 l1part[n][groups][32]  (level-1 block sums)
 // then               f32 l1[n]                  (computed norms)
 constexpr size_t kCtrlBytes = 256;
@@ -102,11 +106,6 @@ bool make_plan(int64_t d, int32_t T, L1Plan* p) {
     p->nchunks = c;
     p->total_groups = g;
     return true;
-}
-
-__device__ __forceinline__ float torch_sign(float v) {
-    // torch.sign: +1 / -1, and 0 for +-0 and NaN (AS:640 v.sign()).
-    return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f);
 }
 
 __device__ __forceinline__ uint64_t ld_relaxed_agent(const uint64_t* p) {
@@ -245,16 +244,24 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
 }
 
 // =====================================================================================
-// K2: fused normalize / floor / fp64 scan / crossing / dequantize, one 4096-element
-// tile per workgroup.  Tiles are taken in ticket order (atomic counter), so a tile
-// only ever waits on tiles that have already started: no residency assumption.
+// K2: fused normalize / floor / fp64 scan / crossing / dequantize.
+//
+// Persistent workgroups walk 4096-element tiles in ticket order (one atomic counter):
+// a workgroup only ever waits on tiles with smaller tickets, which are either done or
+// owned by a running workgroup that will finish them first, so there is no residency
+// assumption and no deadlock.  While a tile is processed, the next ticket's tile is
+// already in flight into registers (prefetch), so HBM traffic overlaps the scan wait.
 //
 // Scan (AS:635): torch CPU cumsum of f32 accumulates sequentially in fp64 and rounds
-// each prefix to f32.  Here each thread adds its 16 fractional parts sequentially in
-// fp64 from an fp64 base = (tile prefix) + (thread-exclusive prefix in the tile); the
-// tile prefix is the sum of ALL predecessor tile aggregates in a fixed order (every
-// predecessor publishes its aggregate as one 8-byte relaxed agent-scope store that is
-// its own ready flag), so the result is deterministic run to run.
+// each prefix to f32.  Each thread adds its 16 fractional parts sequentially in fp64
+// from base = P_t + (thread-exclusive prefix in the tile).  The tile prefix P_t is
+// defined SERIALLY: P_0 = 0, P_{t+1} = fl64(P_t + A_t) with A_t the tile aggregate.
+// Tile t publishes A_t (agg[t]) as soon as it is known and P_{t+1} (incl[t]) once its
+// look-back is done.  Looking back, tile t takes the nearest published incl[j] and
+// re-applies A_{j+1}..A_{t-1} in forward order, which reproduces the serial recursion
+// bit-for-bit whichever j it found: the result does not depend on timing.
+// Every published value is one 8-byte relaxed agent-scope store that is its own ready
+// flag (sentinel = all ones; NaN aggregates are canonicalised), read with sc1 loads.
 // =====================================================================================
 __device__ __forceinline__ double wave_incl_scan(double v, int lane) {
 #pragma unroll
@@ -265,156 +272,326 @@ __device__ __forceinline__ double wave_incl_scan(double v, int lane) {
     return v;
 }
 
-template <bool VEC4>
-__global__ void __launch_bounds__(kQBlock)
-quantize_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, int32_t tiles,
-                float fm, const float* __restrict__ Xs, const float* __restrict__ l1,
-                uint64_t* __restrict__ agg, uint32_t* __restrict__ ctrl) {
-    __shared__ __attribute__((aligned(16))) float s_data[kQBlock * kQPad];
-    __shared__ double s_wave[kQBlock / kWave];
-    __shared__ double s_prefix;
-    __shared__ uint32_t s_ticket;
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wid = tid / kWave;
-    if (tid == 0) s_ticket = atomicAdd(ctrl, 1u);
-    __syncthreads();
-    const uint32_t ticket = s_ticket;
-    const int64_t vec = ticket / (uint32_t)tiles;
-    const int32_t tile = ticket % (uint32_t)tiles;
-    const int64_t t0 = (int64_t)tile * kQTile;
-    const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
-    const float* xt = x + vec * d + t0;
-    float* ot = out + vec * d + t0;
+__device__ __forceinline__ uint64_t canon_bits(double v) {
+    return v != v ? kCanonNaN : (uint64_t)__double_as_longlong(v);
+}
 
-    // ---- stage the tile through LDS: coalesced global reads, padded rows ----------
-    if (VEC4 && len == kQTile) {
-#pragma unroll
-        for (int j = 0; j < kQTile / 4 / kQBlock; ++j) {
-            const int q = tid + j * kQBlock;   // float4 index in the tile
-            const float4 v = reinterpret_cast<const float4*>(xt)[q];
-            *reinterpret_cast<float4*>(&s_data[(q + (q >> 2)) * 4]) = v;
-        }
-    } else {
-        for (int i = tid; i < kQTile; i += kQBlock) {
-            const float v = i < len ? xt[i] : 0.0f;
-            s_data[i + (i >> 4) * 4] = v;
-        }
+// Wave 0 of the workgroup: P_t for tile `tile` of the vector whose slots start at
+// agg/incl.  Returns false on timeout (the abort word is then set).
+__device__ bool look_back(const uint64_t* agg, const uint64_t* incl, int32_t tile, int lane,
+                          uint32_t* ctrl, double* out_prefix) {
+    if (tile == 0) {
+        *out_prefix = 0.0;
+        return true;
     }
-    __syncthreads();
-
-    const float L = l1[vec];
-    const float den = L + 1e-12f;          // AS:625 (f32 add)
-    const float Xv = Xs[vec];
-    const float Ls_pos = L * 1.0f, Ls_neg = L * -1.0f, Ls_zero = L * 0.0f;
-
-    float xv[kQItems];
-    {
-        const float4* src = reinterpret_cast<const float4*>(&s_data[tid * kQPad]);
-#pragma unroll
-        for (int k = 0; k < kQItems / 4; ++k) {
-            const float4 t = src[k];
-            xv[4 * k] = t.x; xv[4 * k + 1] = t.y; xv[4 * k + 2] = t.z; xv[4 * k + 3] = t.w;
-        }
-    }
-    const int i0 = tid * kQItems;   // first element of this thread within the tile
-    float flv[kQItems], frv[kQItems], lsv[kQItems];
-    double tsum = 0.0;
-#pragma unroll
-    for (int k = 0; k < kQItems; ++k) {
-        const float v = xv[k] / den;       // AS:625 IEEE f32 division
-        const float p = fabsf(v);          // AS:626
-        const float mp = fm * p;           // AS:629
-        const float fl = floorf(mp);       // AS:630
-        float fr = mp - fl;                // AS:631
-        if (i0 + k >= len) fr = 0.0f;
-        const float sg = torch_sign(v);
-        flv[k] = fl;
-        frv[k] = fr;
-        lsv[k] = sg > 0.f ? Ls_pos : (sg < 0.f ? Ls_neg : Ls_zero);   // L1 * sign(v)
-        tsum += (double)fr;
-    }
-
-    // ---- block exclusive scan of the thread sums (fixed tree => deterministic) -----
-    const double incl = wave_incl_scan(tsum, lane);
-    double wexcl = __shfl_up(incl, 1, kWave);
-    if (lane == 0) wexcl = 0.0;
-    if (lane == kWave - 1) s_wave[wid] = incl;
-    __syncthreads();
-    double wbase = 0.0, tile_total = 0.0;
-#pragma unroll
-    for (int w = 0; w < kQBlock / kWave; ++w) {
-        if (w < wid) wbase += s_wave[w];
-        tile_total += s_wave[w];
-    }
-    const double texcl = wbase + wexcl;
-
-    // ---- publish this tile's aggregate, then sum all predecessors (look-back) ------
-    uint64_t* aggv = agg + vec * tiles;
-    if (tid == 0) {
-        uint64_t bits = __double_as_longlong(tile_total);
-        if (tile_total != tile_total) bits = kCanonNaN;
-        st_relaxed_agent(&aggv[tile], bits);
-    }
-    if (wid == 0) {
-        double acc = 0.0;
-        if (tile > 0) {
-            bool timed_out = false;
-            for (int32_t u = lane; u < tile; u += kWave) {
-                uint64_t b = ld_relaxed_agent(&aggv[u]);
-                uint32_t spins = 0;
-                while (b == kEmpty) {
-                    __builtin_amdgcn_s_sleep(2);
-                    b = ld_relaxed_agent(&aggv[u]);
-                    if (++spins > (1u << 20) || ld_relaxed_agent32(ctrl + 1) != 0u) {
-                        timed_out = true;
-                        break;
-                    }
-                }
-                if (timed_out) break;
-                acc += __longlong_as_double(b);
+    uint32_t spins = 0;
+    for (;;) {
+        const int32_t j = tile - 1 - lane;          // lane 0 = nearest predecessor
+        const bool valid = j >= 0;
+        const uint64_t ib = valid ? ld_relaxed_agent(&incl[j]) : kEmpty;
+        const uint64_t ab = valid ? ld_relaxed_agent(&agg[j]) : kEmpty;
+        const uint64_t have_incl = __ballot(ib != kEmpty);
+        if (have_incl) {
+            const int L = __builtin_ctzll(have_incl);         // nearest published incl
+            const uint64_t need = (L == 0) ? 0ull : ((1ull << L) - 1ull);
+            const uint64_t have_agg = __ballot(ab != kEmpty);
+            if ((have_agg & need) == need) {
+                double P = __longlong_as_double(__shfl(ib, L, kWave));
+                for (int k = L - 1; k >= 0; --k)             // forward order: j0+1 .. t-1
+                    P = P + __longlong_as_double(__shfl(ab, k, kWave));
+                *out_prefix = P;
+                return true;
             }
-            if (timed_out) {
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 20) || ld_relaxed_agent32(ctrl + 1) != 0u) {
+            if (lane == 0) {
                 __hip_atomic_store(ctrl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            // fixed-shape tree over the lanes
-#pragma unroll
-            for (int o = kWave / 2; o > 0; o >>= 1) acc = acc + __shfl_xor(acc, o, kWave);
+            *out_prefix = 0.0;
+            return false;
         }
-        if (lane == 0) s_prefix = acc;
     }
-    __syncthreads();
+}
 
-    // ---- per element: prefix c_i, crossing test, dequantize (AS:635-640) ----------
-    double s = s_prefix + texcl;
-    float c_prev = (float)s;
-    float ov[kQItems];
+__device__ __forceinline__ int swz(int r, int c) { return r * 16 + 4 * (c ^ ((r >> 2) & 3)); }
+__device__ __forceinline__ int swz_elem(int i) { return swz(i >> 4, (i >> 2) & 3) + (i & 3); }
+
+struct TileRegs {
+    float4 v[kQItems / 4];   // VEC4: float4 q = tid + j*256; scalar: element tid + 256*(4j+c)
+};
+
+template <bool VEC4>
+__device__ __forceinline__ void load_tile(TileRegs& r, const float* __restrict__ x, int64_t d, int32_t tiles,
+                                          uint32_t ticket, int tid) {
+    const int64_t vec = ticket / (uint32_t)tiles;
+    const int64_t t0 = (int64_t)(ticket % (uint32_t)tiles) * kQTile;
+    const int64_t rem = d - t0;
+    const float* xt = x + vec * d + t0;
+    if (VEC4 && rem >= kQTile) {
 #pragma unroll
-    for (int k = 0; k < kQItems; ++k) {
-        s += (double)frv[k];
-        const float c = (float)s;
-        const float diff = floorf(c - Xv) - floorf(c_prev - Xv);   // AS:636
-        const float r = (diff == 1.0f) ? 1.0f : 0.0f;             // AS:637
-        ov[k] = (lsv[k] * (flv[k] + r)) / fm;                      // AS:640
-        c_prev = c;
-    }
-    __syncthreads();   // everyone has read s_data
-    {
-        float4* dst = reinterpret_cast<float4*>(&s_data[tid * kQPad]);
+        for (int j = 0; j < kQItems / 4; ++j) r.v[j] = reinterpret_cast<const float4*>(xt)[tid + j * kQBlock];
+    } else if (VEC4) {
 #pragma unroll
-        for (int k = 0; k < kQItems / 4; ++k)
-            dst[k] = make_float4(ov[4 * k], ov[4 * k + 1], ov[4 * k + 2], ov[4 * k + 3]);
+        for (int j = 0; j < kQItems / 4; ++j) {
+            const int64_t e = (int64_t)(tid + j * kQBlock) * 4;
+            r.v[j] = e < rem ? reinterpret_cast<const float4*>(xt)[tid + j * kQBlock] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kQItems / 4; ++j) {
+            float t[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int64_t e = tid + (int64_t)kQBlock * (4 * j + c);
+                t[c] = e < rem ? xt[e] : 0.0f;
+            }
+            r.v[j] = make_float4(t[0], t[1], t[2], t[3]);
+        }
     }
+}
+
+template <bool VEC4>
+__device__ __forceinline__ void stage_tile(const TileRegs& r, float* s_x, int tid) {
+    if (VEC4) {
+#pragma unroll
+        for (int j = 0; j < kQItems / 4; ++j) {
+            const int q = tid + j * kQBlock;        // float4 index = row*4 + column
+            *reinterpret_cast<float4*>(&s_x[swz(q >> 2, q & 3)]) = r.v[j];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kQItems / 4; ++j) {
+            const float t[4] = {r.v[j].x, r.v[j].y, r.v[j].z, r.v[j].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) s_x[swz_elem(tid + kQBlock * (4 * j + c))] = t[c];
+        }
+    }
+}
+
+// Per-tile compute shared by both K2 kernels.  The tile (kQTile elements, zero-padded)
+// is staged in LDS as 256 rows of 16 (+4 pad) floats; thread `tid` owns row `tid`.
+//   pass 1: x -> v = x/den, p = |v|, mp = fm*p, fl = floor(mp), fr = mp - fl
+//           (fl overwrites x in LDS, fr stays in registers, sign(v) as 2-bit codes),
+//           thread sums in fp64, then a fixed-tree block exclusive scan.
+//   pass 2: from base = P_t + exclusive prefix: c_i = f32(s += fr_i), crossing test,
+//           out = ((L1*sign(v)) * (fl + r)) / m  -> LDS (overwrites fl).
+// Output table (AS:640).  out = ((L1 * sign(v)) * (fl + r)) / f32(m) with k = fl + r a
+// small non-negative integer, so per client the workgroup tabulates
+//     tab[k] = RN( RN(L1 * k) / f32(m) )          k = 0 .. kTab-1   (IEEE division)
+// and every element with k < kTab reads its |out| from LDS; (-L1)*k = -RN(L1*k) and
+// (-a)/m = -(a/m) under round-to-nearest, so the sign is applied afterwards with
+// copysign.  k >= kTab (high rates, large coordinates) and NaN take the arithmetic path.
+constexpr int kTab = 256;
+
+__device__ __forceinline__ void build_table(float* s_tab, int tid, float L, float fm) {
+    for (int k = tid; k < kTab; k += kQBlock) s_tab[k] = (L * (float)k) / fm;
+}
+
+// sign(v) is folded into fl: fl_s = v < 0 ? -fl : fl (fl >= 0, so -0.0 marks a negative
+// coordinate whose floor is 0).  torch.sign(v) == 0 (v = +-0 or NaN) needs no code of
+// its own: v = +-0 gives fr = 0, hence r = 0 and out = (L1*0)*0/m = +0 = tab[0]; v = NaN
+// makes fl NaN and out NaN either way (AS:640).
+struct TileState {
+    double texcl;        // fp64 exclusive prefix of this thread's first element within the tile
+    double total;        // tile aggregate A_t (same value in every thread)
+};
+
+template <bool FULL>
+__device__ __forceinline__ void tile_pass1(float* s_x, float* s_fr, double* s_wave, int tid, int len, float den,
+                                           float fm, TileState& st) {
+    const int lane = tid & (kWave - 1);
+    const int wid = tid / kWave;
+    const int i0 = tid * kQItems;
+    double tsum = 0.0;
+#pragma unroll
+    for (int k4 = 0; k4 < kQItems / 4; ++k4) {
+        const int a = swz(tid, k4);
+        const float4 xv4 = *reinterpret_cast<const float4*>(&s_x[a]);
+        const float xs[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
+        float fls[4], frs[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float v = xs[c] / den;        // AS:625 IEEE f32 division
+            const float p = fabsf(v);           // AS:626
+            const float mp = fm * p;            // AS:629
+            const float fl = floorf(mp);        // AS:630
+            float fr = mp - fl;                 // AS:631
+            if (!FULL && i0 + 4 * k4 + c >= len) fr = 0.0f;
+            fls[c] = v < 0.0f ? -fl : fl;
+            frs[c] = fr;
+            tsum += (double)fr;
+        }
+        *reinterpret_cast<float4*>(&s_x[a]) = make_float4(fls[0], fls[1], fls[2], fls[3]);
+        *reinterpret_cast<float4*>(&s_fr[a]) = make_float4(frs[0], frs[1], frs[2], frs[3]);
+    }
+    const double incl_w = wave_incl_scan(tsum, lane);
+    double wexcl = __shfl_up(incl_w, 1, kWave);
+    if (lane == 0) wexcl = 0.0;
+    if (lane == kWave - 1) s_wave[wid] = incl_w;
     __syncthreads();
+    double wbase = 0.0, total = 0.0;
+#pragma unroll
+    for (int w = 0; w < kQBlock / kWave; ++w) {
+        if (w < wid) wbase += s_wave[w];
+        total += s_wave[w];
+    }
+    st.texcl = wbase + wexcl;
+    st.total = total;
+}
+
+__device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const float* s_tab, int tid, double P,
+                                           float L, float fm, float Xv, const TileState& st) {
+    double s = P + st.texcl;
+    float fprev = floorf((float)s - Xv);       // floor(c_{i-1} - X) of this thread's first element
+#pragma unroll
+    for (int k4 = 0; k4 < kQItems / 4; ++k4) {
+        const int a = swz(tid, k4);
+        const float4 fl4 = *reinterpret_cast<const float4*>(&s_x[a]);
+        const float4 fr4 = *reinterpret_cast<const float4*>(&s_fr[a]);
+        const float fls[4] = {fl4.x, fl4.y, fl4.z, fl4.w};
+        const float frs[4] = {fr4.x, fr4.y, fr4.z, fr4.w};
+        float o[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            s += (double)frs[c];                               // AS:635 fp64 running sum
+            const float fcur = floorf((float)s - Xv);          // AS:636 floor(c_i - X)
+            const float r = (fcur - fprev == 1.0f) ? 1.0f : 0.0f;   // AS:636-637
+            fprev = fcur;
+            const float kf = fabsf(fls[c]) + r;                // fl + r
+            float ov;
+            if (__builtin_expect(kf < (float)kTab, 1)) {
+                ov = copysignf(s_tab[(int)kf], fls[c]);        // AS:640 via the table
+            } else {
+                ov = (copysignf(L, fls[c]) * kf) / fm;         // AS:640 ((L1*sign)*(fl+r))/m
+            }
+            o[c] = ov;
+        }
+        *reinterpret_cast<float4*>(&s_x[a]) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+template <bool VEC4>
+__device__ __forceinline__ void store_tile(const float* s_data, float* __restrict__ ot, int len, int tid) {
     if (VEC4 && len == kQTile) {
 #pragma unroll
         for (int j = 0; j < kQTile / 4 / kQBlock; ++j) {
             const int q = tid + j * kQBlock;
-            reinterpret_cast<float4*>(ot)[q] = *reinterpret_cast<const float4*>(&s_data[(q + (q >> 2)) * 4]);
+            reinterpret_cast<float4*>(ot)[q] = *reinterpret_cast<const float4*>(&s_data[swz(q >> 2, q & 3)]);
         }
     } else {
-        for (int i = tid; i < len; i += kQBlock) ot[i] = s_data[i + (i >> 4) * 4];
+        for (int i = tid; i < len; i += kQBlock) ot[i] = s_data[swz_elem(i)];
+    }
+}
+
+// K2-stream: one workgroup streams one whole client vector, tiles in order, the next
+// tile prefetched into registers; P_{t+1} = fl64(P_t + A_t) carried in the workgroup.
+// No inter-workgroup communication at all.  Used when there are enough clients to
+// fill the GPU (batched DME, the bench workload).
+template <bool VEC4>
+__global__ void __launch_bounds__(kQBlock, 4)
+quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, int32_t tiles,
+                       float fm, const float* __restrict__ Xs, const float* __restrict__ l1) {
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];
+    __shared__ __attribute__((aligned(16))) float s_fr[kQTile];
+    __shared__ float s_tab[kTab];
+    __shared__ double s_wave[kQBlock / kWave];
+    const int tid = threadIdx.x;
+    const int64_t vec = blockIdx.x;
+    const float L = l1[vec];
+    const float den = L + 1e-12f;                  // AS:625 (f32 add)
+    const float Xv = Xs[vec];
+    TileRegs pre;
+    load_tile<VEC4>(pre, x, d, tiles, (uint32_t)(vec * tiles), tid);
+    build_table(s_tab, tid, L, fm);
+    double P = 0.0;
+    for (int32_t tile = 0; tile < tiles; ++tile) {
+        stage_tile<VEC4>(pre, s_x, tid);
+        __syncthreads();
+        if (tile + 1 < tiles) load_tile<VEC4>(pre, x, d, tiles, (uint32_t)(vec * tiles + tile + 1), tid);
+        const int64_t t0 = (int64_t)tile * kQTile;
+        const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+        TileState st;
+        if (len == kQTile)
+            tile_pass1<true>(s_x, s_fr, s_wave, tid, len, den, fm, st);
+        else
+            tile_pass1<false>(s_x, s_fr, s_wave, tid, len, den, fm, st);
+        tile_pass2(s_x, s_fr, s_tab, tid, P, L, fm, Xv, st);
+        P = P + st.total;                          // serial definition of the tile prefix
+        __syncthreads();
+        store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
+        __syncthreads();
+    }
+}
+
+// K2-lookback: persistent workgroups over ticketed tiles with the deterministic
+// decoupled look-back above.  Used when there are too few clients to fill the GPU
+// one-vector-per-workgroup (e.g. the per-client drop-in call).
+template <bool VEC4>
+__global__ void __launch_bounds__(kQBlock)
+quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, int32_t tiles,
+                         uint32_t total_tiles, float fm, const float* __restrict__ Xs, const float* __restrict__ l1,
+                         uint64_t* __restrict__ agg, uint64_t* __restrict__ incl, uint32_t* __restrict__ ctrl) {
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];
+    __shared__ __attribute__((aligned(16))) float s_fr[kQTile];
+    __shared__ double s_wave[kQBlock / kWave];
+    __shared__ float s_tab[kTab];
+    __shared__ double s_prefix;
+    __shared__ uint32_t s_ticket[2];
+    __shared__ int64_t s_tabvec;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wid = tid / kWave;
+
+    if (tid == 0) {
+        s_ticket[0] = atomicAdd(ctrl, 1u);
+        s_tabvec = -1;
+    }
+    __syncthreads();
+    uint32_t cur = s_ticket[0];
+    if (cur >= total_tiles) return;
+    TileRegs pre;
+    load_tile<VEC4>(pre, x, d, tiles, cur, tid);
+    int slot = 0;
+    for (;;) {
+        if (tid == 0) s_ticket[slot ^ 1] = atomicAdd(ctrl, 1u);
+        stage_tile<VEC4>(pre, s_x, tid);
+        __syncthreads();
+        const uint32_t nxt = s_ticket[slot ^ 1];
+        if (nxt < total_tiles) load_tile<VEC4>(pre, x, d, tiles, nxt, tid);
+        const int64_t vec = cur / (uint32_t)tiles;
+        const int32_t tile = cur % (uint32_t)tiles;
+        const int64_t t0 = (int64_t)tile * kQTile;
+        const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+        const float L = l1[vec];
+        const float den = L + 1e-12f;              // AS:625 (f32 add)
+        if (s_tabvec != vec) build_table(s_tab, tid, L, fm);   // uniform; tab read after pass 1's barrier
+        TileState st;
+        if (len == kQTile)
+            tile_pass1<true>(s_x, s_fr, s_wave, tid, len, den, fm, st);
+        else
+            tile_pass1<false>(s_x, s_fr, s_wave, tid, len, den, fm, st);
+        uint64_t* aggv = agg + vec * tiles;
+        uint64_t* inclv = incl + vec * tiles;
+        if (tid == 0) s_tabvec = vec;              // every thread has tested s_tabvec before pass 1's barrier
+        if (wid == 0) {
+            if (lane == 0 && tile > 0) st_relaxed_agent(&aggv[tile], canon_bits(st.total));
+            double P = 0.0;
+            look_back(aggv, inclv, tile, lane, ctrl, &P);
+            if (lane == 0) {
+                st_relaxed_agent(&inclv[tile], canon_bits(P + st.total));
+                s_prefix = P;
+            }
+        }
+        __syncthreads();
+        tile_pass2(s_x, s_fr, s_tab, tid, s_prefix, L, fm, Xs[vec], st);
+        __syncthreads();
+        store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
+        if (nxt >= total_tiles) break;
+        cur = nxt;
+        slot ^= 1;
+        __syncthreads();
     }
 }
 
@@ -470,7 +647,7 @@ int hip_check(hipError_t e, const char* what) {
 }
 
 struct WsLayout {
-    size_t agg_off, part_off, l1_off, total;
+    size_t agg_off, incl_off, part_off, l1_off, total;
     int32_t tiles;
 };
 
@@ -480,7 +657,8 @@ WsLayout layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.tiles = (int32_t)tiles;
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
     w.agg_off = kCtrlBytes;
-    w.part_off = up(w.agg_off + (size_t)n * tiles * sizeof(uint64_t));
+    w.incl_off = up(w.agg_off + (size_t)n * tiles * sizeof(uint64_t));
+    w.part_off = up(w.incl_off + (size_t)n * tiles * sizeof(uint64_t));
     w.l1_off = up(w.part_off + (size_t)n * plan.total_groups * 32 * sizeof(float));
     w.total = up(w.l1_off + (size_t)n * sizeof(float));
     return w;
@@ -507,6 +685,31 @@ int launch_l1(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* p
     }
     hipLaunchKernelGGL(l1_finalize_kernel, dim3((unsigned)n), dim3(64), 0, st, x, d, plan, part, l1_out);
     return hip_check(hipGetLastError(), "l1_finalize_kernel launch");
+}
+
+// Persistent grid for K2: (resident workgroups per CU) x CUs, from the occupancy API
+// (correctness never depends on it: tiles are ticketed).
+int persistent_grid(bool vec4, int* out) {
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc) return rc;
+    static thread_local int cache_dev = -1, cache_v[2] = {0, 0};
+    if (cache_dev != dev) {
+        int cus = 0;
+        rc = hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
+        if (rc) return rc;
+        for (int v = 0; v < 2; ++v) {
+            int per = 0;
+            rc = hip_check(v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, quantize_lookback_kernel<true>, kQBlock, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, quantize_lookback_kernel<false>, kQBlock, 0),
+                           "occupancy");
+            if (rc) return rc;
+            cache_v[v] = std::max(1, per) * std::max(1, cus);
+        }
+        cache_dev = dev;
+    }
+    *out = cache_v[vec4 ? 1 : 0];
+    return UQ_OK;
 }
 
 int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_t ws_bytes,
@@ -598,18 +801,35 @@ int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64
     }
     rc = hip_check(hipMemsetAsync(wsb, 0, 2 * sizeof(uint32_t), st), "memset ticket/abort");
     if (rc) return rc;
-    rc = hip_check(hipMemsetAsync(wsb + w.agg_off, 0xFF, (size_t)n * w.tiles * sizeof(uint64_t), st), "memset agg");
+    // agg and incl are contiguous: one fill of both look-back arrays
+    rc = hip_check(hipMemsetAsync(wsb + w.agg_off, 0xFF, w.part_off - w.agg_off, st), "memset look-back");
     if (rc) return rc;
     const float fm = (float)m;   // torch casts the Python int to f32 for `m * p` and `/ m`
     const bool vec4 = aligned16(x) && aligned16(out) && (d % 4 == 0);
-    dim3 grid((unsigned)(w.tiles * n));
+    const uint32_t total = (uint32_t)(w.tiles * n);
+    if (n >= kStreamMinClients) {
+        // enough clients to fill the GPU: one workgroup per client vector
+        if (vec4)
+            hipLaunchKernelGGL(quantize_stream_kernel<true>, dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, d,
+                               w.tiles, fm, X, l1use);
+        else
+            hipLaunchKernelGGL(quantize_stream_kernel<false>, dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, d,
+                               w.tiles, fm, X, l1use);
+        return hip_check(hipGetLastError(), "quantize_stream_kernel launch");
+    }
+    int grid_cap = 0;
+    rc = persistent_grid(vec4, &grid_cap);
+    if (rc) return rc;
+    dim3 grid((unsigned)std::min<int64_t>(total, grid_cap));
+    uint64_t* agg = (uint64_t*)(wsb + w.agg_off);
+    uint64_t* incl = (uint64_t*)(wsb + w.incl_off);
     if (vec4)
-        hipLaunchKernelGGL(quantize_kernel<true>, grid, dim3(kQBlock), 0, st, x, out, d, w.tiles, fm, X, l1use,
-                           (uint64_t*)(wsb + w.agg_off), (uint32_t*)wsb);
+        hipLaunchKernelGGL(quantize_lookback_kernel<true>, grid, dim3(kQBlock), 0, st, x, out, d, w.tiles, total, fm,
+                           X, l1use, agg, incl, (uint32_t*)wsb);
     else
-        hipLaunchKernelGGL(quantize_kernel<false>, grid, dim3(kQBlock), 0, st, x, out, d, w.tiles, fm, X, l1use,
-                           (uint64_t*)(wsb + w.agg_off), (uint32_t*)wsb);
-    return hip_check(hipGetLastError(), "quantize_kernel launch");
+        hipLaunchKernelGGL(quantize_lookback_kernel<false>, grid, dim3(kQBlock), 0, st, x, out, d, w.tiles, total,
+                           fm, X, l1use, agg, incl, (uint32_t*)wsb);
+    return hip_check(hipGetLastError(), "quantize_lookback_kernel launch");
 }
 
 int uq_client_mean_f32(const float* q, int64_t n, int64_t d, float n_div, int32_t accumulate, float* est,
