@@ -6,7 +6,7 @@ sys.path.insert(0, ROOT)
 PKG = os.path.join(ROOT, "unbiased-quantization-distributed-mean-estimation_amd")
 SRC = os.path.join(PKG, "csrc", "uq_dme.hip")
 OUT = os.path.join(PKG, "_build", "abl")
-VARIANTS = {"base": [], "fastdiv": ["-DUQ_ABL_FAST_DIV"]}
+VARIANTS = {"base": [], "copy": ["-DUQ_ABL_COPY"], "no_nt": ["-DUQ_NO_NT"]}
 def build():
     sys.path.insert(0, PKG)
     import build_ext as be

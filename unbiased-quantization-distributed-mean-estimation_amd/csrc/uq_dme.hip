@@ -322,6 +322,23 @@ struct TileRegs {
     float4 v[kQItems / 4];   // VEC4: float4 q = tid + j*256; scalar: element tid + 256*(4j+c)
 };
 
+// x is read once and q written once per call: non-temporal loads/stores (measured ~4%
+// faster on the C2 batch than default-policy accesses).  -DUQ_NO_NT restores them.
+#ifndef UQ_NO_NT
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_stream(const float4* p) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_stream(float4* p, float4 v) {
+    const f32x4 t = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
+}
+#else
+__device__ __forceinline__ float4 ld_stream(const float4* p) { return *p; }
+__device__ __forceinline__ void st_stream(float4* p, float4 v) { *p = v; }
+#endif
+
 template <bool VEC4>
 __device__ __forceinline__ void load_tile(TileRegs& r, const float* __restrict__ x, int64_t d, int32_t tiles,
                                           uint32_t ticket, int tid) {
@@ -331,7 +348,7 @@ __device__ __forceinline__ void load_tile(TileRegs& r, const float* __restrict__
     const float* xt = x + vec * d + t0;
     if (VEC4 && rem >= kQTile) {
 #pragma unroll
-        for (int j = 0; j < kQItems / 4; ++j) r.v[j] = reinterpret_cast<const float4*>(xt)[tid + j * kQBlock];
+        for (int j = 0; j < kQItems / 4; ++j) r.v[j] = ld_stream(reinterpret_cast<const float4*>(xt) + tid + j * kQBlock);
     } else if (VEC4) {
 #pragma unroll
         for (int j = 0; j < kQItems / 4; ++j) {
@@ -478,7 +495,7 @@ __device__ __forceinline__ void store_tile(const float* s_data, float* __restric
 #pragma unroll
         for (int j = 0; j < kQTile / 4 / kQBlock; ++j) {
             const int q = tid + j * kQBlock;
-            reinterpret_cast<float4*>(ot)[q] = *reinterpret_cast<const float4*>(&s_data[swz(q >> 2, q & 3)]);
+            st_stream(reinterpret_cast<float4*>(ot) + q, *reinterpret_cast<const float4*>(&s_data[swz(q >> 2, q & 3)]));
         }
     } else {
         for (int i = tid; i < len; i += kQBlock) ot[i] = s_data[swz_elem(i)];
@@ -513,12 +530,14 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         const int64_t t0 = (int64_t)tile * kQTile;
         const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
         TileState st;
+#ifndef UQ_ABL_COPY
         if (len == kQTile)
             tile_pass1<true>(s_x, s_fr, s_wave, tid, len, den, fm, st);
         else
             tile_pass1<false>(s_x, s_fr, s_wave, tid, len, den, fm, st);
         tile_pass2(s_x, s_fr, s_tab, tid, P, L, fm, Xv, st);
         P = P + st.total;                          // serial definition of the tile prefix
+#endif
         __syncthreads();
         store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
         __syncthreads();
