@@ -117,7 +117,7 @@ def main():
         _lib.check(lib.uq_type_unbiased_f32(P(x), P(q), n, d, m, P(X), P(l1), None, T, P(ws), nb, sp), "quantize")
         if ev is not None:
             ev[2].record(stream)
-        _lib.check(lib.uq_client_mean_f32(P(q), n, d, float(n_total), 0, P(est), sp), "mean")
+        _lib.check(lib.uq_client_mean_f32(P(q), n, d, d, float(n_total), 0, P(est), sp), "mean")
         if ev is not None:
             ev[3].record(stream)
         if dist is not None:

@@ -67,14 +67,16 @@ int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64
                          int32_t torch_threads, void* ws, size_t ws_bytes, void* stream);
 
 /* Normal_dist.py:137-138 — est[i] (+)= q[j][i] / n_div for j = 0..n-1 in client order
- * (f32 IEEE division, f32 add).  accumulate=0 starts from zeros. */
-int uq_client_mean_f32(const float* q, int64_t n, int64_t d, float n_div, int32_t accumulate,
-                       float* est, void* stream);
+ * (f32 IEEE division, f32 add).  Row j starts at q + j*ld (ld >= d, so a column block
+ * of a wider batch can be folded in).  accumulate=0 starts from zeros; accumulate=1
+ * continues from `est`, which makes the sum over a sequence of calls bit-identical
+ * to one call over all rows in the same order. */
+int uq_client_mean_f32(const float* q, int64_t n, int64_t d, int64_t ld, float n_div,
+                       int32_t accumulate, float* est, void* stream);
 
 /* Quantize a batch and fold it into the client mean in one call:
- *   q = Type_unbiased_quantize(x[j]) for all j (into `out`, or into workspace
- *   scratch when out == NULL and the workspace is large enough), then
- *   est (+)= q[j] / n_div in client order.  Bit-identical to the two calls above. */
+ *   q = Type_unbiased_quantize(x[j]) for all j (into `out`, which must be non-NULL),
+ *   then est (+)= q[j] / n_div in client order.  Bit-identical to the two calls above. */
 int uq_type_unbiased_mean_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m,
                               const float* X, const float* l1, int32_t torch_threads,
                               float n_div, int32_t accumulate, float* est,

@@ -65,7 +65,8 @@ def test_workspace_and_argument_errors(lib):
     assert lib.uq_type_unbiased_f32(ctypes.c_void_p(16), ctypes.c_void_p(16), 4, 100, -5, ctypes.c_void_p(16),
                                     None, None, 1, ctypes.c_void_p(16), 1 << 30, None) == -1
     assert lib.uq_l1_torch_order_f32(ctypes.c_void_p(16), 4, 100, 65, None, ctypes.c_void_p(16), 1 << 30, None) == -1
-    assert lib.uq_client_mean_f32(None, 3, 10, 3.0, 0, None, None) == -1
+    assert lib.uq_client_mean_f32(None, 3, 10, 10, 3.0, 0, None, None) == -1
+    assert lib.uq_client_mean_f32(ctypes.c_void_p(16), 3, 10, 9, 3.0, 0, ctypes.c_void_p(16), None) == -1
 
 
 def test_drop_in_signature_and_name():

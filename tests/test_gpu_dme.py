@@ -1,0 +1,67 @@
+"""GPU: the DME harness (dme.py, ND:77-221 restricted to the unbiased scheme) against the
+reference's own NMSE known answers, and the sharded-mean protocol with the HIP fold."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import uq_oracle as O
+from tests import golden_data as G
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def uq(gpu_ready):
+    import uqdme
+    return uqdme
+
+
+def test_nd_harness_known_answers(uq):
+    pts = G.nd_points()
+    for dist, rows in pts.items():
+        res = uq.nmse_simulation(dist, dim=2048, users=(1, 6, 11), num_instances=4)
+        k = 0
+        for ui, n in enumerate((1, 6, 11)):
+            for inst in range(4):
+                row = rows[k]
+                for r in (1, 2):
+                    got = float(res[r]["script"][ui, inst])
+                    ref = row[f"nmse{r}"]
+                    assert abs(got - ref) <= 1e-6 * ref, (dist, n, inst, r, got, ref)   # north_star tolerance
+                k += 1
+
+
+@pytest.mark.parametrize("dist", ["gamma", "bernoulli", "lognormal", "uniform"])
+def test_other_distributions_vs_oracle(uq, dist):
+    """Same harness, every scheme call checked bit-for-bit against the CPU oracle."""
+    from uqdme_amd.dme import draw_vectors
+    vecs, vns = draw_vectors(dist, 5, 2048, np.random.RandomState(3))
+    xs = np.stack([v.astype(np.float32) for v in vecs])
+    X = np.random.RandomState(4).random_sample(5).astype(np.float32)
+    for R in (1, 2):
+        q = uq.quantize_dequantize(torch.from_numpy(xs).cuda(), R, X=X, torch_threads=1).cpu().numpy()
+        ref = np.stack([O.type_unbiased_quantize(xs[j], R, X[j]) for j in range(5)])
+        assert G.bits_equal(q, ref), (dist, R, G.n_mismatch(q, ref))
+
+
+def test_sharded_mean_single_rank_nccl(uq):
+    """The RCCL path of distributed.py with one rank: ordered and reduce modes equal the
+    single-call client mean bit-for-bit."""
+    import os
+    import socket
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        q = torch.randn(33, 5000, device="cuda")
+        ref = uq.client_mean(q, 33.0)
+        for mode in ("reduce", "ordered"):
+            est = uq.sharded_client_mean(q, 33.0, mode=mode, block=1024)
+            torch.cuda.synchronize()
+            assert torch.equal(est, ref), mode
+    finally:
+        dist.destroy_process_group()

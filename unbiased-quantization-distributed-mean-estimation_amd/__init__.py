@@ -11,9 +11,12 @@ from .quantizer import (
     l1_torch_order, draw_uniforms, set_torch_threads, get_torch_threads, check_status,
 )
 from ._lib import UQError, load as load_library, library_path
+from .distributed import shard_range, sharded_client_mean, sharded_quantize_mean
+from .dme import DISTRIBUTIONS, nmse_simulation
 
 __all__ = [
     "RATE_TABLE", "rate_to_m", "Type_unbiased_quantize", "quantize_dequantize", "client_mean",
     "quantize_mean", "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
-    "check_status", "UQError", "load_library", "library_path",
+    "check_status", "UQError", "load_library", "library_path", "shard_range", "sharded_client_mean",
+    "sharded_quantize_mean", "DISTRIBUTIONS", "nmse_simulation",
 ]

@@ -25,7 +25,7 @@ SIGNATURES = {
     "uq_workspace_bytes": (ctypes.c_int, [_i64, _i64, _i32, ctypes.POINTER(_sz)]),
     "uq_l1_torch_order_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _sz, _p]),
     "uq_type_unbiased_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _i32, _p, _sz, _p]),
-    "uq_client_mean_f32": (ctypes.c_int, [_p, _i64, _i64, _f32, _i32, _p, _p]),
+    "uq_client_mean_f32": (ctypes.c_int, [_p, _i64, _i64, _i64, _f32, _i32, _p, _p]),
     "uq_type_unbiased_mean_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _p, _p, _i32, _f32, _i32, _p,
                                                  _p, _sz, _p]),
     "uq_check_status": (ctypes.c_int, [_p, _p]),

@@ -620,7 +620,7 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
 // =====================================================================================
 template <bool VEC4>
 __global__ void __launch_bounds__(256)
-client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, float n_div, int accumulate,
+client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, int64_t ld, float n_div, int accumulate,
                    float* __restrict__ est) {
     const int64_t col = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (col >= d) return;
@@ -630,7 +630,7 @@ client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, float n_di
         for (; j + 8 <= n; j += 8) {
             float4 t[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const float4*>(q + (j + u) * d + col);
+            for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const float4*>(q + (j + u) * ld + col);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 e.x += t[u].x / n_div; e.y += t[u].y / n_div;
@@ -638,7 +638,7 @@ client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, float n_di
             }
         }
         for (; j < n; ++j) {
-            const float4 t = *reinterpret_cast<const float4*>(q + j * d + col);
+            const float4 t = *reinterpret_cast<const float4*>(q + j * ld + col);
             e.x += t.x / n_div; e.y += t.y / n_div; e.z += t.z / n_div; e.w += t.w / n_div;
         }
         *reinterpret_cast<float4*>(est + col) = e;
@@ -646,7 +646,7 @@ client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, float n_di
         const int cnt = (int)((d - col) < 4 ? (d - col) : 4);
         for (int k = 0; k < cnt; ++k) {
             float e = accumulate ? est[col + k] : 0.f;
-            for (int64_t j = 0; j < n; ++j) e += q[j * d + col + k] / n_div;
+            for (int64_t j = 0; j < n; ++j) e += q[j * ld + col + k] / n_div;
             est[col + k] = e;
         }
     }
@@ -851,19 +851,20 @@ int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64
     return hip_check(hipGetLastError(), "quantize_lookback_kernel launch");
 }
 
-int uq_client_mean_f32(const float* q, int64_t n, int64_t d, float n_div, int32_t accumulate, float* est,
-                       void* stream) {
+int uq_client_mean_f32(const float* q, int64_t n, int64_t d, int64_t ld, float n_div, int32_t accumulate,
+                       float* est, void* stream) {
     if (n < 0 || d < 0) return fail(UQ_E_INVALID, "n and d must be >= 0");
+    if (ld < d) return fail(UQ_E_INVALID, "ld must be >= d");
     if (d == 0) return UQ_OK;
     if (!est || (n > 0 && !q)) return fail(UQ_E_INVALID, "null pointer");
     hipStream_t st = (hipStream_t)stream;
-    const bool vec4 = (n == 0 || aligned16(q)) && aligned16(est) && (d % 4 == 0);
+    const bool vec4 = (n == 0 || aligned16(q)) && aligned16(est) && (d % 4 == 0) && (ld % 4 == 0);
     const int64_t threads = (d + 3) / 4;
     dim3 grid((unsigned)((threads + 255) / 256));
     if (vec4)
-        hipLaunchKernelGGL(client_mean_kernel<true>, grid, dim3(256), 0, st, q, n, d, n_div, accumulate, est);
+        hipLaunchKernelGGL(client_mean_kernel<true>, grid, dim3(256), 0, st, q, n, d, ld, n_div, accumulate, est);
     else
-        hipLaunchKernelGGL(client_mean_kernel<false>, grid, dim3(256), 0, st, q, n, d, n_div, accumulate, est);
+        hipLaunchKernelGGL(client_mean_kernel<false>, grid, dim3(256), 0, st, q, n, d, ld, n_div, accumulate, est);
     return hip_check(hipGetLastError(), "client_mean_kernel launch");
 }
 
@@ -873,7 +874,7 @@ int uq_type_unbiased_mean_f32(const float* x, float* out, int64_t n, int64_t d, 
     if (!out) return fail(UQ_E_INVALID, "out must be non-NULL in this version");
     int rc = uq_type_unbiased_f32(x, out, n, d, m, X, l1, nullptr, T, ws, ws_bytes, stream);
     if (rc) return rc;
-    return uq_client_mean_f32(out, n, d, n_div, accumulate, est, stream);
+    return uq_client_mean_f32(out, n, d, d, n_div, accumulate, est, stream);
 }
 
 int uq_check_status(void* ws, void* stream) {

@@ -154,15 +154,27 @@ def quantize_dequantize(x, bits_per_dimension=1, X=None, *, m: int | None = None
 
 
 def client_mean(q, n_div, est=None, accumulate: bool = False) -> torch.Tensor:
-    """ND:137-138: est (+)= q[j] / n_div over rows j in order (f32)."""
+    """ND:137-138: est (+)= q[j] / n_div over rows j in order (f32).
+
+    `q` may be a column block of a wider row-major batch (unit column stride, any row
+    stride); with accumulate=True the sum continues from `est` bit-for-bit."""
     dev = _device()
-    q = _as_device_f32_2d(q, dev)
+    if not torch.is_tensor(q):
+        q = torch.as_tensor(np.asarray(q), dtype=torch.float32)
+    if q.dim() != 2:
+        raise ValueError("expected a 2-D [n, d] batch")
+    q = q.to(device=dev, dtype=torch.float32)
+    if q.shape[1] > 0 and (q.stride(1) != 1 or q.stride(0) < q.shape[1]):
+        q = q.contiguous()
     n, d = q.shape
+    ld = q.stride(0) if n > 0 else d
     if est is None:
         est = torch.empty(d, dtype=torch.float32, device=dev)
         accumulate = False
-    _lib.check(_lib.load().uq_client_mean_f32(_ptr(q), n, d, float(n_div), int(bool(accumulate)), _ptr(est),
-                                              _stream_ptr(dev)), "uq_client_mean_f32")
+    elif est.shape != (d,) or est.dtype != torch.float32 or est.device != q.device or not est.is_contiguous():
+        raise ValueError("est must be a contiguous f32 vector of length d on the same device")
+    _lib.check(_lib.load().uq_client_mean_f32(_ptr(q), n, d, max(ld, d), float(n_div), int(bool(accumulate)),
+                                              _ptr(est), _stream_ptr(dev)), "uq_client_mean_f32")
     return est
 
 
