@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/pmc_*.json)")
+    ap.add_argument("--mean-mode", choices=["reduce", "ordered"], default="reduce",
+                    help="N>1: one RCCL reduce of per-rank partial means, or the bit-exact ordered chain")
     return ap.parse_args()
 
 
@@ -117,11 +119,15 @@ def main():
         _lib.check(lib.uq_type_unbiased_f32(P(x), P(q), n, d, m, P(X), P(l1), None, T, P(ws), nb, sp), "quantize")
         if ev is not None:
             ev[2].record(stream)
-        _lib.check(lib.uq_client_mean_f32(P(q), n, d, d, float(n_total), 0, P(est), sp), "mean")
+        if dist is None or args.mean_mode == "reduce":
+            _lib.check(lib.uq_client_mean_f32(P(q), n, d, d, float(n_total), 0, P(est), sp), "mean")
         if ev is not None:
             ev[3].record(stream)
         if dist is not None:
-            dist.reduce(est, dst=0, op=dist.ReduceOp.SUM)
+            if args.mean_mode == "reduce":
+                dist.reduce(est, dst=0, op=dist.ReduceOp.SUM)      # the one RCCL collective
+            else:
+                uqdme.sharded_client_mean(q, float(n_total), mode="ordered", dst=0)
         if ev is not None:
             ev[4].record(stream)
 
@@ -167,7 +173,8 @@ def main():
             "config": {"workload": "C2 (BASELINE.json configs[1]): 1024 clients/GPU x d=2^20, Gaussian, R=1, "
                                    "unbiased L1 type quantizer + client-ordered mean" + (" + RCCL reduce" if world > 1 else ""),
                        "clients_per_gpu": n, "d": d, "bits_per_dimension": args.bits, "m": m,
-                       "torch_threads_l1_order": T, "parallelism": f"client-sharded x{world}"},
+                       "torch_threads_l1_order": T, "parallelism": f"client-sharded x{world}",
+                       "mean_mode": args.mean_mode if world > 1 else "single"},
             "kernel_ms": {"l1": round(float(seg_ms[0]), 4), "quantize": round(q_ms, 4),
                           "client_mean": round(float(seg_ms[2]), 4), "reduce": round(float(seg_ms[3]), 4)},
             "roofline": {"kernel": "quantize_kernel (K2)", "bound": "hbm", "achieved": round(achieved, 2),
