@@ -53,6 +53,13 @@ def parse():
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/pmc_*.json)")
     ap.add_argument("--mean-mode", choices=["reduce", "ordered"], default="reduce",
                     help="N>1: one RCCL reduce of per-rank partial means, or the bit-exact ordered chain")
+    ap.add_argument("--pipeline", choices=["q", "codes", "encode"], default="q",
+                    help="q: K2 writes the dequantized q, mean reads q (the reference's drop-in semantics); "
+                         "codes: K2 writes q AND type codes, mean decodes codes; "
+                         "encode: K2 writes codes only, the mean kernel dequantizes (DME wire pipeline)")
+    ap.add_argument("--side-pipelines", action="store_true", default=True,
+                    help="also time the other pipelines (reported under 'pipelines')")
+    ap.add_argument("--no-side-pipelines", dest="side_pipelines", action="store_false")
     return ap.parse_args()
 
 
@@ -110,31 +117,50 @@ def main():
     sp = stream.cuda_stream
     P = lambda t: t.data_ptr()  # noqa: E731
 
-    def step(ev=None):
+    codes = torch.empty((n, d), dtype=torch.int8, device=dev)
+    ovf = torch.zeros(n, dtype=torch.int32, device=dev)
+
+    def step(ev=None, pipeline=args.pipeline):
         if ev is not None:
             ev[0].record(stream)
         _lib.check(lib.uq_l1_torch_order_f32(P(x), n, d, T, P(l1), P(ws), nb, sp), "l1")
         if ev is not None:
             ev[1].record(stream)
-        _lib.check(lib.uq_type_unbiased_f32(P(x), P(q), n, d, m, P(X), P(l1), None, T, P(ws), nb, sp), "quantize")
+        if pipeline == "q":
+            _lib.check(lib.uq_type_unbiased_f32(P(x), P(q), n, d, m, P(X), P(l1), None, T, P(ws), nb, sp), "quantize")
+        else:
+            _lib.check(lib.uq_type_unbiased_codes_f32(P(x), P(q) if pipeline == "codes" else None, P(codes), P(ovf),
+                                                      n, d, m, P(X), P(l1), None, T, P(ws), nb, sp), "quantize")
         if ev is not None:
             ev[2].record(stream)
         if dist is None or args.mean_mode == "reduce":
-            _lib.check(lib.uq_client_mean_f32(P(q), n, d, d, float(n_total), 0, P(est), sp), "mean")
+            if pipeline == "q":
+                _lib.check(lib.uq_client_mean_f32(P(q), n, d, d, float(n_total), 0, P(est), sp), "mean")
+            else:
+                _lib.check(lib.uq_codes_mean_f32(P(codes), P(l1), n, d, m, float(n_total), 0, P(est), sp), "mean")
         if ev is not None:
             ev[3].record(stream)
         if dist is not None:
             if args.mean_mode == "reduce":
                 dist.reduce(est, dst=0, op=dist.ReduceOp.SUM)      # the one RCCL collective
             else:
+                if pipeline != "q":
+                    _lib.check(lib.uq_codes_decode_f32(P(codes), P(l1), n, d, m, P(q), sp), "decode")
                 uqdme.sharded_client_mean(q, float(n_total), mode="ordered", dst=0)
         if ev is not None:
             ev[4].record(stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    _lib.check(lib.uq_check_status(P(ws), sp), "status after warmup")
+    def time_pipeline(pipeline, steps):
+        for _ in range(2):
+            step(pipeline=pipeline)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            step(pipeline=pipeline)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / steps
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
     if dist is not None:
@@ -159,9 +185,21 @@ def main():
     value = n_total * args.steps / elapsed / 1e6
 
     q_ms = float(seg_ms[1])
-    alg_bytes = 8.0 * d * n                       # read x + write q, per quantize launch
+    # algorithmic bytes per K2 launch: read x (4d) + write q (4d) and/or codes (1d)
+    alg_bytes = float(d * n) * (4 + (4 if args.pipeline in ("q", "codes") else 0) + (1 if args.pipeline != "q" else 0))
     achieved = alg_bytes / (q_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(args.traffic_json, d, n)
+    if args.pipeline != "q":
+        traffic, traffic_src = None, None          # the committed PMC summary is for the q pipeline
+    side = {}
+    if args.side_pipelines and world == 1:
+        for pl in ("q", "codes", "encode"):
+            if pl != args.pipeline:
+                ms = time_pipeline(pl, max(3, args.steps // 2))
+                side[pl] = {"ms_per_step": round(ms, 4), "value": round(n_total / ms / 1e3, 6)}
+        _lib.check(lib.uq_check_status(P(ws), sp), "status after side pipelines")
+        if int(torch.count_nonzero(ovf)):
+            raise RuntimeError("type-code overflow in the bench workload")
 
     result = None
     if rank == 0:
@@ -174,10 +212,11 @@ def main():
                                    "unbiased L1 type quantizer + client-ordered mean" + (" + RCCL reduce" if world > 1 else ""),
                        "clients_per_gpu": n, "d": d, "bits_per_dimension": args.bits, "m": m,
                        "torch_threads_l1_order": T, "parallelism": f"client-sharded x{world}",
-                       "mean_mode": args.mean_mode if world > 1 else "single"},
+                       "mean_mode": args.mean_mode if world > 1 else "single", "pipeline": args.pipeline},
             "kernel_ms": {"l1": round(float(seg_ms[0]), 4), "quantize": round(q_ms, 4),
                           "client_mean": round(float(seg_ms[2]), 4), "reduce": round(float(seg_ms[3]), 4)},
-            "roofline": {"kernel": "quantize_kernel (K2)", "bound": "hbm", "achieved": round(achieved, 2),
+            "pipelines": side,
+            "roofline": {"kernel": "quantize_stream_kernel (K2)", "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes},

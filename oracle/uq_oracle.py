@@ -224,3 +224,21 @@ def script_nmse(est: np.ndarray, emp_mean: np.ndarray, vec_norm_squared: float,
 def quantize_dequantize_batch(x2d: np.ndarray, m: int, X: np.ndarray, torch_threads: int = 1):
     """Batched form: row j uses X[j]."""
     return np.stack([quantize_with_m(x2d[j], m, X[j], torch_threads) for j in range(x2d.shape[0])])
+
+
+def type_codes(x, m: int, X, torch_threads: int = 1, l1=None):
+    """Wire codes of the reference's output (see codes.py): k = fl + r per coordinate
+    (AS:630-637), code = k if sign(v) >= 0 else -k-1; overflow if any k > 127 or NaN."""
+    x = np.asarray(x, dtype=f32).reshape(-1)
+    L = l1_torch_order(x, torch_threads) if l1 is None else f32(l1)
+    v, fl, fr = fractional_parts(x, m, L)
+    c = prefix_c(fr)
+    Xf = f32(X)
+    with np.errstate(all="ignore"):
+        diff = np.floor((c[1:] - Xf).astype(f32)) - np.floor((c[:-1] - Xf).astype(f32))
+        r = (diff == 1).astype(f32)
+        k = (fl + r).astype(f32)
+    ok = k <= 127
+    kk = np.where(ok, k, 127).astype(np.int64)
+    code = np.where(v < 0, -kk - 1, kk).astype(np.int8)
+    return code, L, bool((~ok).any())

@@ -6,7 +6,8 @@ sys.path.insert(0, ROOT)
 PKG = os.path.join(ROOT, "unbiased-quantization-distributed-mean-estimation_amd")
 SRC = os.path.join(PKG, "csrc", "uq_dme.hip")
 OUT = os.path.join(PKG, "_build", "abl")
-VARIANTS = {"base": [], "copy": ["-DUQ_ABL_COPY"], "no_nt": ["-DUQ_NO_NT"]}
+VARIANTS = {"base": [], "old_swz": ["-DUQ_OLD_SWZ"], "pf2": ["-DUQ_PF2"], "copy": ["-DUQ_ABL_COPY"],
+            "copy_pf2": ["-DUQ_ABL_COPY", "-DUQ_PF2"]}
 def build():
     sys.path.insert(0, PKG)
     import build_ext as be

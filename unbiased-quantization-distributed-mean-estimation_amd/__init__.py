@@ -9,7 +9,9 @@ from .rates import RATE_TABLE, rate_to_m
 from .quantizer import (
     Type_unbiased_quantize, quantize_dequantize, client_mean, quantize_mean,
     l1_torch_order, draw_uniforms, set_torch_threads, get_torch_threads, check_status,
+    quantize_encode, decode, codes_mean,
 )
+from .codes import TypeCodes
 from ._lib import UQError, load as load_library, library_path
 from .distributed import shard_range, sharded_client_mean, sharded_quantize_mean
 from .dme import DISTRIBUTIONS, nmse_simulation
@@ -18,5 +20,6 @@ __all__ = [
     "RATE_TABLE", "rate_to_m", "Type_unbiased_quantize", "quantize_dequantize", "client_mean",
     "quantize_mean", "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
     "check_status", "UQError", "load_library", "library_path", "shard_range", "sharded_client_mean",
-    "sharded_quantize_mean", "DISTRIBUTIONS", "nmse_simulation",
+    "sharded_quantize_mean", "DISTRIBUTIONS", "nmse_simulation", "quantize_encode", "decode", "codes_mean",
+    "TypeCodes",
 ]

@@ -37,9 +37,8 @@ constexpr uint64_t kCanonNaN = 0x7FF8000000000000ull;  // NaN aggregates are can
 constexpr int kQBlock = 256;               // threads per workgroup (4 waves)
 constexpr int kQItems = 16;                // contiguous elements per thread
 constexpr int kQTile = kQBlock * kQItems;  // 4096 elements per tile
-// LDS tile image: 256 rows of 16 floats (thread t owns row t).  Float4 column c of row r
-// lives at r*16 + 4*(c ^ ((r >> 2) & 3)): conflict-free for the per-row ds_read_b128 of
-// every lane group and for the coalesced staging writes, with no padding.
+// LDS tile image: 256 rows of 16 floats (thread t owns row t); float4 column c of row r
+// lives at swz(r, c) (XOR swizzle, see there): bank-conflict-free without padding.
 constexpr int64_t kStreamMinClients = 256; // >= this many clients: one workgroup per vector
 
 // ---- workspace layout --------------------------------------------------------------
@@ -315,7 +314,14 @@ __device__ bool look_back(const uint64_t* agg, const uint64_t* incl, int32_t til
     }
 }
 
+#ifdef UQ_OLD_SWZ
 __device__ __forceinline__ int swz(int r, int c) { return r * 16 + 4 * (c ^ ((r >> 2) & 3)); }
+#else
+// f(r) = ((r >> 2) ^ (r >> 1)) & 3 makes the 16-lane ds_read_b128 groups (banks mod 64)
+// AND the 8-lane ds_write_b128 groups (banks mod 32) conflict-free for row accesses,
+// staging writes and store reads alike.
+__device__ __forceinline__ int swz(int r, int c) { return r * 16 + 4 * (c ^ (((r >> 2) ^ (r >> 1)) & 3)); }
+#endif
 __device__ __forceinline__ int swz_elem(int i) { return swz(i >> 4, (i >> 2) & 3) + (i & 3); }
 
 struct TileRegs {
@@ -458,8 +464,21 @@ __device__ __forceinline__ void tile_pass1(float* s_x, float* s_fr, double* s_wa
     st.total = total;
 }
 
+// Wire code of one coordinate (type codes, see uq_dme.h): k = fl + r in [0, 127] ->
+// code = k for sign(v) >= 0 and -k-1 for sign(v) < 0 (so -0.0 outputs survive);
+// k > 127 or NaN -> saturated and reported through the per-client overflow flag.
+__device__ __forceinline__ uint32_t code_of(float fl_s, float kf, bool& ovf) {
+    const bool ok = kf <= 127.0f;                   // false for NaN too
+    ovf |= !ok;
+    const int k = ok ? (int)kf : 127;
+    const int c = (__float_as_uint(fl_s) >> 31) ? -k - 1 : k;
+    return (uint32_t)(c & 0xFF);
+}
+
+template <bool WQ, bool WC>
 __device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const float* s_tab, int tid, double P,
-                                           float L, float fm, float Xv, const TileState& st) {
+                                           float L, float fm, float Xv, const TileState& st, uint32_t (&cw)[4],
+                                           bool& ovf) {
     double s = P + st.texcl;
     float fprev = floorf((float)s - Xv);       // floor(c_{i-1} - X) of this thread's first element
 #pragma unroll
@@ -470,6 +489,7 @@ __device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const 
         const float fls[4] = {fl4.x, fl4.y, fl4.z, fl4.w};
         const float frs[4] = {fr4.x, fr4.y, fr4.z, fr4.w};
         float o[4];
+        uint32_t w = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             s += (double)frs[c];                               // AS:635 fp64 running sum
@@ -477,16 +497,40 @@ __device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const 
             const float r = (fcur - fprev == 1.0f) ? 1.0f : 0.0f;   // AS:636-637
             fprev = fcur;
             const float kf = fabsf(fls[c]) + r;                // fl + r
-            float ov;
-            if (__builtin_expect(kf < (float)kTab, 1)) {
-                ov = copysignf(s_tab[(int)kf], fls[c]);        // AS:640 via the table
-            } else {
-                ov = (copysignf(L, fls[c]) * kf) / fm;         // AS:640 ((L1*sign)*(fl+r))/m
+            if (WQ) {
+                float ov;
+                if (__builtin_expect(kf < (float)kTab, 1)) {
+                    ov = copysignf(s_tab[(int)kf], fls[c]);    // AS:640 via the table
+                } else {
+                    ov = (copysignf(L, fls[c]) * kf) / fm;     // AS:640 ((L1*sign)*(fl+r))/m
+                }
+                o[c] = ov;
             }
-            o[c] = ov;
+            if (WC) w |= code_of(fls[c], kf, ovf) << (8 * c);
         }
-        *reinterpret_cast<float4*>(&s_x[a]) = make_float4(o[0], o[1], o[2], o[3]);
+        if (WQ) *reinterpret_cast<float4*>(&s_x[a]) = make_float4(o[0], o[1], o[2], o[3]);
+        if (WC) cw[k4] = w;
     }
+}
+
+// Codes of this thread's 16 consecutive elements: one 16-byte store when the row is
+// full and aligned, bytes otherwise.
+template <bool CVEC>
+__device__ __forceinline__ void store_codes(int8_t* __restrict__ ct, const uint32_t (&cw)[4], int len, int tid) {
+    const int i0 = tid * kQItems;
+    if (CVEC && i0 + kQItems <= len) {
+        const uint4 v = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+        __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(ct + i0));
+        __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(ct + i0) + 1);
+        __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(ct + i0) + 2);
+        __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(ct + i0) + 3);
+    } else {
+        for (int k = 0; k < kQItems && i0 + k < len; ++k) ct[i0 + k] = (int8_t)((cw[k >> 2] >> (8 * (k & 3))) & 0xFF);
+    }
+}
+
+__device__ __forceinline__ void flag_overflow(bool ovf, int32_t* overflow, int64_t vec, int tid) {
+    if (__any(ovf) && (tid & (kWave - 1)) == 0) atomicOr(&overflow[vec], 1);
 }
 
 template <bool VEC4>
@@ -506,10 +550,11 @@ __device__ __forceinline__ void store_tile(const float* s_data, float* __restric
 // tile prefetched into registers; P_{t+1} = fl64(P_t + A_t) carried in the workgroup.
 // No inter-workgroup communication at all.  Used when there are enough clients to
 // fill the GPU (batched DME, the bench workload).
-template <bool VEC4>
+template <bool VEC4, bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock, 4)
-quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, int32_t tiles,
-                       float fm, const float* __restrict__ Xs, const float* __restrict__ l1) {
+quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
+                       int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
+                       const float* __restrict__ Xs, const float* __restrict__ l1) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
     __shared__ __attribute__((aligned(16))) float s_fr[kQTile];
     __shared__ float s_tab[kTab];
@@ -521,12 +566,21 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     const float Xv = Xs[vec];
     TileRegs pre;
     load_tile<VEC4>(pre, x, d, tiles, (uint32_t)(vec * tiles), tid);
+#ifdef UQ_PF2
+    TileRegs pre2;
+    if (tiles > 1) load_tile<VEC4>(pre2, x, d, tiles, (uint32_t)(vec * tiles + 1), tid);
+#endif
     build_table(s_tab, tid, L, fm);
     double P = 0.0;
     for (int32_t tile = 0; tile < tiles; ++tile) {
         stage_tile<VEC4>(pre, s_x, tid);
         __syncthreads();
+#ifdef UQ_PF2
+        pre = pre2;
+        if (tile + 2 < tiles) load_tile<VEC4>(pre2, x, d, tiles, (uint32_t)(vec * tiles + tile + 2), tid);
+#else
         if (tile + 1 < tiles) load_tile<VEC4>(pre, x, d, tiles, (uint32_t)(vec * tiles + tile + 1), tid);
+#endif
         const int64_t t0 = (int64_t)tile * kQTile;
         const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
         TileState st;
@@ -535,11 +589,17 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
             tile_pass1<true>(s_x, s_fr, s_wave, tid, len, den, fm, st);
         else
             tile_pass1<false>(s_x, s_fr, s_wave, tid, len, den, fm, st);
-        tile_pass2(s_x, s_fr, s_tab, tid, P, L, fm, Xv, st);
+        uint32_t cw[4];
+        bool ovf = false;
+        tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, P, L, fm, Xv, st, cw, ovf);
         P = P + st.total;                          // serial definition of the tile prefix
+        if (WC) {
+            store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
+            flag_overflow(ovf, overflow, vec, tid);
+        }
 #endif
         __syncthreads();
-        store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
+        if (WQ) store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
         __syncthreads();
     }
 }
@@ -547,9 +607,10 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
 // K2-lookback: persistent workgroups over ticketed tiles with the deterministic
 // decoupled look-back above.  Used when there are too few clients to fill the GPU
 // one-vector-per-workgroup (e.g. the per-client drop-in call).
-template <bool VEC4>
+template <bool VEC4, bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock)
-quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, int32_t tiles,
+quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
+                         int32_t* __restrict__ overflow, int64_t d, int32_t tiles,
                          uint32_t total_tiles, float fm, const float* __restrict__ Xs, const float* __restrict__ l1,
                          uint64_t* __restrict__ agg, uint64_t* __restrict__ incl, uint32_t* __restrict__ ctrl) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
@@ -604,9 +665,15 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
             }
         }
         __syncthreads();
-        tile_pass2(s_x, s_fr, s_tab, tid, s_prefix, L, fm, Xs[vec], st);
+        uint32_t cw[4];
+        bool ovf = false;
+        tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, s_prefix, L, fm, Xs[vec], st, cw, ovf);
+        if (WC) {
+            store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
+            flag_overflow(ovf, overflow, vec, tid);
+        }
         __syncthreads();
-        store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
+        if (WQ) store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
         if (nxt >= total_tiles) break;
         cur = nxt;
         slot ^= 1;
@@ -649,6 +716,112 @@ client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, int64_t ld
             for (int64_t j = 0; j < n; ++j) e += q[j * ld + col + k] / n_div;
             est[col + k] = e;
         }
+    }
+}
+
+// =====================================================================================
+// Type codes (the wire format, see uq_dme.h): decode and decode+mean.
+// For one client, |q| = tab[k] = RN(RN(L1*k)/f32(m)) and q carries the code's sign, so
+// decoding rebuilds q bit-for-bit (including -0.0).  For the mean, (-a)/n = -(a/n), so
+// a per-client table tabn[k] = RN(tab[k]/n_div) gives q/n_div exactly.
+// =====================================================================================
+constexpr int kDecChunk = 4096;   // elements per decode workgroup (256 threads x 16)
+constexpr int kMeanCols = 4096;   // columns per decode+mean workgroup (256 threads x 16)
+constexpr int kMeanClients = 32;  // clients whose tables are staged in LDS at a time
+
+__device__ __forceinline__ float decode_one(int8_t c, const float* tab) {
+    const int ci = (int)c;
+    const int k = ci < 0 ? -ci - 1 : ci;
+    const float v = tab[k];
+    return ci < 0 ? -v : v;
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(256)
+codes_decode_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, int64_t d, float fm,
+                    float* __restrict__ out) {
+    __shared__ float tab[128];
+    const int64_t vec = blockIdx.y;
+    const int tid = threadIdx.x;
+    const float L = l1[vec];
+    if (tid < 128) tab[tid] = (L * (float)tid) / fm;
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kDecChunk + (int64_t)tid * 16;
+    const int8_t* cr = codes + vec * d;
+    float* orow = out + vec * d;
+    if (VEC && i0 + 16 <= d) {
+        const uint4 w = *reinterpret_cast<const uint4*>(cr + i0);
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+            float o[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) o[c] = decode_one((int8_t)((ws[k4] >> (8 * c)) & 0xFF), tab);
+            *reinterpret_cast<float4*>(orow + i0 + 4 * k4) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+    } else {
+        for (int64_t i = i0; i < i0 + 16 && i < d; ++i) orow[i] = decode_one(cr[i], tab);
+    }
+}
+
+// est[i] (+)= q_j[i] / n_div for clients j in order, q decoded from codes.  One workgroup
+// owns kMeanCols columns; client tables are staged kMeanClients at a time.
+template <bool VEC>
+__global__ void __launch_bounds__(256)
+codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, int64_t n, int64_t d, float fm,
+                  float n_div, int accumulate, float* __restrict__ est) {
+    __shared__ float tabn[kMeanClients][128];
+    const int tid = threadIdx.x;
+    const int64_t i0 = (int64_t)blockIdx.x * kMeanCols + (int64_t)tid * 16;
+    const bool full = VEC && i0 + 16 <= d;
+    float e[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) e[k] = (accumulate && i0 + k < d) ? est[i0 + k] : 0.0f;
+    for (int64_t j0 = 0; j0 < n; j0 += kMeanClients) {
+        const int nb = (int)((n - j0) < kMeanClients ? (n - j0) : kMeanClients);
+        __syncthreads();
+        for (int t = tid; t < nb * 128; t += 256) {
+            const int jj = t >> 7, k = t & 127;
+            const float L = l1[j0 + jj];
+            tabn[jj][k] = ((L * (float)k) / fm) / n_div;
+        }
+        __syncthreads();
+        if (full) {
+            int jj = 0;
+            for (; jj + 4 <= nb; jj += 4) {
+                uint4 w[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(codes + (j0 + jj + u) * d + i0));
+                    w[u] = make_uint4(t.x, t.y, t.z, t.w);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) e[k] += decode_one((int8_t)((ws[k >> 2] >> (8 * (k & 3))) & 0xFF), tabn[jj + u]);
+                }
+            }
+            for (; jj < nb; ++jj) {
+                const uint4 w = *reinterpret_cast<const uint4*>(codes + (j0 + jj) * d + i0);
+                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int k = 0; k < 16; ++k) e[k] += decode_one((int8_t)((ws[k >> 2] >> (8 * (k & 3))) & 0xFF), tabn[jj]);
+            }
+        } else {
+            for (int jj = 0; jj < nb; ++jj)
+                for (int k = 0; k < 16; ++k)
+                    if (i0 + k < d) e[k] += decode_one(codes[(j0 + jj) * d + i0 + k], tabn[jj]);
+        }
+    }
+    if (full) {
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4)
+            *reinterpret_cast<float4*>(est + i0 + 4 * k4) = make_float4(e[4 * k4], e[4 * k4 + 1], e[4 * k4 + 2], e[4 * k4 + 3]);
+    } else {
+        for (int k = 0; k < 16; ++k)
+            if (i0 + k < d) est[i0 + k] = e[k];
     }
 }
 
@@ -719,8 +892,8 @@ int persistent_grid(bool vec4, int* out) {
         if (rc) return rc;
         for (int v = 0; v < 2; ++v) {
             int per = 0;
-            rc = hip_check(v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, quantize_lookback_kernel<true>, kQBlock, 0)
-                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, quantize_lookback_kernel<false>, kQBlock, 0),
+            rc = hip_check(v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, quantize_lookback_kernel<true, true, false, true>, kQBlock, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, quantize_lookback_kernel<false, true, false, true>, kQBlock, 0),
                            "occupancy");
             if (rc) return rc;
             cache_v[v] = std::max(1, per) * std::max(1, cus);
@@ -795,16 +968,18 @@ int uq_l1_torch_order_f32(const float* x, int64_t n, int64_t d, int32_t T, float
     return launch_l1(x, n, d, plan, part, l1_out, st);
 }
 
-int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m, const float* X,
-                         const float* l1, float* l1_out, int32_t T, void* ws, size_t ws_bytes,
-                         void* stream) {
+int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_t* overflow, int64_t n, int64_t d,
+                               int64_t m, const float* X, const float* l1, float* l1_out, int32_t T, void* ws,
+                               size_t ws_bytes, void* stream) {
     L1Plan plan;
     WsLayout w;
     int rc = check_common(x, n, d, T, ws, ws_bytes, &plan, &w);
     if (rc) return rc;
     if (m < 0) return fail(UQ_E_INVALID, "m must be >= 0");
     if (n == 0 || d == 0) return UQ_OK;
-    if (!out || !X) return fail(UQ_E_INVALID, "null out or X");
+    if (!X) return fail(UQ_E_INVALID, "null X");
+    if (!out && !codes) return fail(UQ_E_INVALID, "nothing to write: out and codes are both NULL");
+    if (codes && !overflow) return fail(UQ_E_INVALID, "codes need an overflow[n] array");
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     float* l1buf = (float*)(wsb + w.l1_off);
@@ -818,37 +993,98 @@ int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64
         rc = hip_check(hipMemcpyAsync(l1_out, l1use, n * sizeof(float), hipMemcpyDeviceToDevice, st), "copy l1");
         if (rc) return rc;
     }
+    if (codes) {
+        rc = hip_check(hipMemsetAsync(overflow, 0, n * sizeof(int32_t), st), "memset overflow");
+        if (rc) return rc;
+    }
+    const float fm = (float)m;   // torch casts the Python int to f32 for `m * p` and `/ m`
+    const bool vec4 = aligned16(x) && (!out || aligned16(out)) && (d % 4 == 0);
+    const bool cvec = !codes || (aligned16(codes) && d % 16 == 0);
+    const int wq = out ? 1 : 0, wc = codes ? 1 : 0;
+    const int sel = (vec4 ? 8 : 0) | (wq ? 4 : 0) | (wc ? 2 : 0) | (cvec ? 1 : 0);
+    if (n >= kStreamMinClients) {
+        // enough clients to fill the GPU: one workgroup per client vector
+#define UQ_STREAM(V, Q, C, CV)                                                                              \
+    case ((V) * 8 + (Q) * 4 + (C) * 2 + (CV)):                                                            \
+        hipLaunchKernelGGL((quantize_stream_kernel<V, Q, C, CV>), dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, \
+                           codes, overflow, d, w.tiles, fm, X, l1use);                                    \
+        break;
+        switch (sel) {
+            UQ_STREAM(1, 1, 0, 1) UQ_STREAM(1, 1, 1, 1) UQ_STREAM(1, 1, 1, 0) UQ_STREAM(1, 0, 1, 1)
+            UQ_STREAM(1, 0, 1, 0) UQ_STREAM(0, 1, 0, 1) UQ_STREAM(0, 1, 1, 1) UQ_STREAM(0, 1, 1, 0)
+            UQ_STREAM(0, 0, 1, 1) UQ_STREAM(0, 0, 1, 0)
+            default: return fail(UQ_E_INVALID, "internal: bad kernel selector");
+        }
+#undef UQ_STREAM
+        return hip_check(hipGetLastError(), "quantize_stream_kernel launch");
+    }
     rc = hip_check(hipMemsetAsync(wsb, 0, 2 * sizeof(uint32_t), st), "memset ticket/abort");
     if (rc) return rc;
     // agg and incl are contiguous: one fill of both look-back arrays
     rc = hip_check(hipMemsetAsync(wsb + w.agg_off, 0xFF, w.part_off - w.agg_off, st), "memset look-back");
     if (rc) return rc;
-    const float fm = (float)m;   // torch casts the Python int to f32 for `m * p` and `/ m`
-    const bool vec4 = aligned16(x) && aligned16(out) && (d % 4 == 0);
     const uint32_t total = (uint32_t)(w.tiles * n);
-    if (n >= kStreamMinClients) {
-        // enough clients to fill the GPU: one workgroup per client vector
-        if (vec4)
-            hipLaunchKernelGGL(quantize_stream_kernel<true>, dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, d,
-                               w.tiles, fm, X, l1use);
-        else
-            hipLaunchKernelGGL(quantize_stream_kernel<false>, dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, d,
-                               w.tiles, fm, X, l1use);
-        return hip_check(hipGetLastError(), "quantize_stream_kernel launch");
-    }
     int grid_cap = 0;
     rc = persistent_grid(vec4, &grid_cap);
     if (rc) return rc;
     dim3 grid((unsigned)std::min<int64_t>(total, grid_cap));
     uint64_t* agg = (uint64_t*)(wsb + w.agg_off);
     uint64_t* incl = (uint64_t*)(wsb + w.incl_off);
-    if (vec4)
-        hipLaunchKernelGGL(quantize_lookback_kernel<true>, grid, dim3(kQBlock), 0, st, x, out, d, w.tiles, total, fm,
-                           X, l1use, agg, incl, (uint32_t*)wsb);
-    else
-        hipLaunchKernelGGL(quantize_lookback_kernel<false>, grid, dim3(kQBlock), 0, st, x, out, d, w.tiles, total,
-                           fm, X, l1use, agg, incl, (uint32_t*)wsb);
+#define UQ_LOOK(V, Q, C, CV)                                                                                  \
+    case ((V) * 8 + (Q) * 4 + (C) * 2 + (CV)):                                                              \
+        hipLaunchKernelGGL((quantize_lookback_kernel<V, Q, C, CV>), grid, dim3(kQBlock), 0, st, x, out, codes,  \
+                           overflow, d, w.tiles, total, fm, X, l1use, agg, incl, (uint32_t*)wsb);             \
+        break;
+    switch (sel) {
+        UQ_LOOK(1, 1, 0, 1) UQ_LOOK(1, 1, 1, 1) UQ_LOOK(1, 1, 1, 0) UQ_LOOK(1, 0, 1, 1)
+        UQ_LOOK(1, 0, 1, 0) UQ_LOOK(0, 1, 0, 1) UQ_LOOK(0, 1, 1, 1) UQ_LOOK(0, 1, 1, 0)
+        UQ_LOOK(0, 0, 1, 1) UQ_LOOK(0, 0, 1, 0)
+        default: return fail(UQ_E_INVALID, "internal: bad kernel selector");
+    }
+#undef UQ_LOOK
     return hip_check(hipGetLastError(), "quantize_lookback_kernel launch");
+}
+
+int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m, const float* X,
+                         const float* l1, float* l1_out, int32_t T, void* ws, size_t ws_bytes,
+                         void* stream) {
+    if (n > 0 && d > 0 && !out) return fail(UQ_E_INVALID, "null out");
+    return uq_type_unbiased_codes_f32(x, out, nullptr, nullptr, n, d, m, X, l1, l1_out, T, ws, ws_bytes, stream);
+}
+
+int uq_codes_decode_f32(const int8_t* codes, const float* l1, int64_t n, int64_t d, int64_t m, float* out,
+                        void* stream) {
+    if (n < 0 || d < 0 || m < 0) return fail(UQ_E_INVALID, "n, d and m must be >= 0");
+    if (n == 0 || d == 0) return UQ_OK;
+    if (!codes || !l1 || !out) return fail(UQ_E_INVALID, "null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t chunks = (d + kDecChunk - 1) / kDecChunk;
+    if (chunks > 0x7FFFFFFF) return fail(UQ_E_INVALID, "d too large");
+    const bool vec = aligned16(codes) && aligned16(out) && d % 16 == 0;
+    dim3 grid((unsigned)chunks, (unsigned)n);
+    if (vec)
+        hipLaunchKernelGGL(codes_decode_kernel<true>, grid, dim3(256), 0, st, codes, l1, d, (float)m, out);
+    else
+        hipLaunchKernelGGL(codes_decode_kernel<false>, grid, dim3(256), 0, st, codes, l1, d, (float)m, out);
+    return hip_check(hipGetLastError(), "codes_decode_kernel launch");
+}
+
+int uq_codes_mean_f32(const int8_t* codes, const float* l1, int64_t n, int64_t d, int64_t m, float n_div,
+                      int32_t accumulate, float* est, void* stream) {
+    if (n < 0 || d < 0 || m < 0) return fail(UQ_E_INVALID, "n, d and m must be >= 0");
+    if (d == 0) return UQ_OK;
+    if (!est || (n > 0 && (!codes || !l1))) return fail(UQ_E_INVALID, "null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const bool vec = (n == 0 || aligned16(codes)) && aligned16(est) && d % 16 == 0;
+    const int64_t blocks = (d + kMeanCols - 1) / kMeanCols;
+    if (blocks > 0x7FFFFFFF) return fail(UQ_E_INVALID, "d too large");
+    if (vec)
+        hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, n, d,
+                           (float)m, n_div, accumulate, est);
+    else
+        hipLaunchKernelGGL(codes_mean_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, n, d,
+                           (float)m, n_div, accumulate, est);
+    return hip_check(hipGetLastError(), "codes_mean_kernel launch");
 }
 
 int uq_client_mean_f32(const float* q, int64_t n, int64_t d, int64_t ld, float n_div, int32_t accumulate,

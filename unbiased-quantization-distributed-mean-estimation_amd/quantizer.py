@@ -28,7 +28,8 @@ from . import _lib
 from .rates import RATE_TABLE, rate_to_m
 
 __all__ = [
-    "Type_unbiased_quantize", "quantize_dequantize", "client_mean", "quantize_mean",
+    "Type_unbiased_quantize", "quantize_dequantize", "client_mean", "quantize_mean", "quantize_encode", "decode",
+    "codes_mean",
     "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
 ]
 
@@ -151,6 +152,64 @@ def quantize_dequantize(x, bits_per_dimension=1, X=None, *, m: int | None = None
                                                 T, _ptr(ws), ws.numel(), _stream_ptr(dev)),
                "uq_type_unbiased_f32")
     return (out, l1_out) if return_l1 else out
+
+
+def quantize_encode(x, bits_per_dimension=1, X=None, *, m: int | None = None, torch_threads: int | None = None,
+                    l1=None, return_q: bool = False, generator: torch.Generator | None = None):
+    """Quantize a batch and emit type codes (codes.TypeCodes); optionally also q.
+
+    Same numerics as quantize_dequantize: decode(codes) == q bit-for-bit."""
+    from .codes import TypeCodes
+    dev = _device()
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    mm = _resolve_m(bits_per_dimension, m, d)
+    T = get_torch_threads() if torch_threads is None else int(torch_threads)
+    if X is None:
+        X = draw_uniforms(n, generator)
+    X = torch.as_tensor(X, dtype=torch.float32).reshape(-1).to(dev)
+    if X.numel() != n:
+        raise ValueError("X must have one draw per row")
+    if l1 is not None:
+        l1 = torch.as_tensor(l1, dtype=torch.float32).reshape(-1).to(dev).contiguous()
+    codes = torch.empty((n, d), dtype=torch.int8, device=dev)
+    overflow = torch.zeros(n, dtype=torch.int32, device=dev)
+    l1_out = torch.empty(n, dtype=torch.float32, device=dev)
+    q = torch.empty_like(x) if return_q else None
+    nb = _ws_bytes(n, d, T)
+    ws = _workspace(dev, nb)
+    _lib.check(_lib.load().uq_type_unbiased_codes_f32(_ptr(x), _ptr(q), _ptr(codes), _ptr(overflow), n, d, mm,
+                                                      _ptr(X), _ptr(l1), _ptr(l1_out), T, _ptr(ws), ws.numel(),
+                                                      _stream_ptr(dev)), "uq_type_unbiased_codes_f32")
+    tc = TypeCodes(codes=codes, l1=l1_out, m=mm, overflow=overflow)
+    return (tc, q) if return_q else tc
+
+
+def decode(tc) -> torch.Tensor:
+    """Rebuild the dequantized batch from type codes (bit-identical to quantize_dequantize)."""
+    dev = _device()
+    codes = tc.codes.to(dev).contiguous()
+    l1 = tc.l1.to(device=dev, dtype=torch.float32).contiguous()
+    n, d = codes.shape
+    out = torch.empty((n, d), dtype=torch.float32, device=dev)
+    _lib.check(_lib.load().uq_codes_decode_f32(_ptr(codes), _ptr(l1), n, d, int(tc.m), _ptr(out), _stream_ptr(dev)),
+               "uq_codes_decode_f32")
+    return out
+
+
+def codes_mean(tc, n_div, est=None, accumulate: bool = False) -> torch.Tensor:
+    """ND:137-138 from type codes: est (+)= decode(codes)[j] / n_div over clients j in order,
+    bit-identical to client_mean(decode(tc), n_div)."""
+    dev = _device()
+    codes = tc.codes.to(dev).contiguous()
+    l1 = tc.l1.to(device=dev, dtype=torch.float32).contiguous()
+    n, d = codes.shape
+    if est is None:
+        est = torch.empty(d, dtype=torch.float32, device=dev)
+        accumulate = False
+    _lib.check(_lib.load().uq_codes_mean_f32(_ptr(codes), _ptr(l1), n, d, int(tc.m), float(n_div),
+                                             int(bool(accumulate)), _ptr(est), _stream_ptr(dev)), "uq_codes_mean_f32")
+    return est
 
 
 def client_mean(q, n_div, est=None, accumulate: bool = False) -> torch.Tensor:
