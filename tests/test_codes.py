@@ -54,8 +54,10 @@ def test_message_roundtrip_host():
     assert len(buf) == 32 + 12 + 3 * 37
     back = uqdme.TypeCodes.from_bytes(buf)
     assert torch.equal(back.codes, codes) and torch.equal(back.l1, tc.l1) and back.m == 7
+    kk = np.where(codes.numpy() < 0, -codes.numpy().astype(np.int32) - 1, codes.numpy().astype(np.int32))
+    assert np.array_equal(back.overflow.numpy(), kk.max(axis=1))
     with pytest.raises(ValueError):
         uqdme.TypeCodes.from_bytes(buf[:-1])
-    tc.overflow[1] = 1
+    tc.overflow[1] = 128
     with pytest.raises(OverflowError):
         tc.to_bytes()

@@ -6,8 +6,7 @@ sys.path.insert(0, ROOT)
 PKG = os.path.join(ROOT, "unbiased-quantization-distributed-mean-estimation_amd")
 SRC = os.path.join(PKG, "csrc", "uq_dme.hip")
 OUT = os.path.join(PKG, "_build", "abl")
-VARIANTS = {"base": [], "old_swz": ["-DUQ_OLD_SWZ"], "pf2": ["-DUQ_PF2"], "copy": ["-DUQ_ABL_COPY"],
-            "copy_pf2": ["-DUQ_ABL_COPY", "-DUQ_PF2"]}
+VARIANTS = {"base": [], "copy": ["-DUQ_ABL_COPY"]}
 def build():
     sys.path.insert(0, PKG)
     import build_ext as be
@@ -31,13 +30,21 @@ def run():
         f.argtypes = [ctypes.c_void_p]*2 + [ctypes.c_int64]*3 + [ctypes.c_void_p]*3 + [ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         sp = torch.cuda.current_stream().cuda_stream
         call = lambda: f(x.data_ptr(), q.data_ptr(), n, d, 224426, X.data_ptr(), l1.data_ptr(), None, 1, ws.data_ptr(), b.value, sp)
-        for _ in range(3): assert call() == 0
-        torch.cuda.synchronize()
-        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(10): call()
-        e1.record(); torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 10
-        print(f"{k:12s} {ms:8.3f} ms  {8*d*n/ms/1e6:8.1f} GB/s", flush=True)
+        calls = {"q": (call, 8)}
+        if hasattr(L, "uq_type_unbiased_codes_f32"):
+            g = L.uq_type_unbiased_codes_f32
+            g.argtypes = [ctypes.c_void_p]*4 + [ctypes.c_int64]*3 + [ctypes.c_void_p]*3 + [ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+            codes = torch.empty((n, d), dtype=torch.int8, device="cuda"); km = torch.zeros(n, dtype=torch.int32, device="cuda")
+            calls["q+codes"] = (lambda: g(x.data_ptr(), q.data_ptr(), codes.data_ptr(), km.data_ptr(), n, d, 224426, X.data_ptr(), l1.data_ptr(), None, 1, ws.data_ptr(), b.value, sp), 9)
+            calls["codes"] = (lambda: g(x.data_ptr(), None, codes.data_ptr(), km.data_ptr(), n, d, 224426, X.data_ptr(), l1.data_ptr(), None, 1, ws.data_ptr(), b.value, sp), 5)
+        for cname, (fn, bpe) in calls.items():
+            for _ in range(3): assert fn() == 0
+            torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10): fn()
+            e1.record(); torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 10
+            print(f"{k:12s} {cname:8s} {ms:8.3f} ms  {bpe*d*n/ms/1e6:8.1f} GB/s", flush=True)
 if __name__ == "__main__":
     build() if sys.argv[1] == "build" else run()

@@ -3,6 +3,7 @@ pmc_<tag>.json with per-launch HBM bytes for the quantize kernel (gfx950 correct
 FETCH_SIZE reads half the bytes of wide coalesced streaming loads -> x2; MI355X_MICROARCH.md)."""
 import csv, glob, json, os, shutil, sys
 src, tag = sys.argv[1], sys.argv[2]
+pipeline = sys.argv[3] if len(sys.argv) > 3 else "codes"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -18,7 +19,7 @@ def per_kernel(kind, counter):
         vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     return vals
 fetch, write = per_kernel("fetch", "FETCH_SIZE"), per_kernel("write", "WRITE_SIZE")
-out = {"tag": tag, "d": 1 << 20, "clients": 1024, "units": "bytes per launch",
+out = {"tag": tag, "d": 1 << 20, "clients": 1024, "pipeline": pipeline, "units": "bytes per launch",
        "method": "rocprofv3 --kernel-trace --pmc, one counter per pass; FETCH_SIZE (KB) x2 (gfx950 wide-load correction) + WRITE_SIZE (KB), x1024",
        "kernels": {}}
 for k in fetch:

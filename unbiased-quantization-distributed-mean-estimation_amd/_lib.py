@@ -31,7 +31,7 @@ SIGNATURES = {
     "uq_check_status": (ctypes.c_int, [_p, _p]),
     "uq_type_unbiased_codes_f32": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _i32, _p, _sz, _p]),
     "uq_codes_decode_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _p, _p]),
-    "uq_codes_mean_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _f32, _i32, _p, _p]),
+    "uq_codes_mean_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _f32, _i32, _p, _p]),
 }
 
 

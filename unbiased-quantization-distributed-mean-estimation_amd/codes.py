@@ -20,6 +20,7 @@ format is fixed-length and does not reach it -- parity unpinned (the reference h
 
 Serialized message (little endian):
     b"UQT1" | u32 version=1 | i64 n | i64 d | i64 m | f32 l1[n] | i8 codes[n*d]
+(the per-client max count is recomputed from the codes on receipt)
 """
 from __future__ import annotations
 
@@ -39,7 +40,7 @@ class TypeCodes:
     codes: torch.Tensor      # int8 [n, d] (device or host)
     l1: torch.Tensor         # f32 [n]
     m: int                   # lattice sum (AS:623)
-    overflow: torch.Tensor   # int32 [n], nonzero where a count saturated
+    overflow: torch.Tensor   # int32 [n]: the client's largest count k; 128 = a count > 127 saturated
 
     @property
     def n(self) -> int:
@@ -51,7 +52,7 @@ class TypeCodes:
 
     def check(self) -> None:
         """Raise if any client's counts did not fit the 8-bit code (synchronises)."""
-        bad = int(torch.count_nonzero(self.overflow).item())
+        bad = int(torch.count_nonzero(self.overflow > 127).item())
         if bad:
             raise OverflowError(f"{bad} client(s) have lattice counts > 127; send them as floats")
 
@@ -74,5 +75,7 @@ class TypeCodes:
         if off + n * d != len(buf):
             raise ValueError("truncated or oversized UQT1 message")
         dev = device or "cpu"
+        k = np.where(codes < 0, -(codes.astype(np.int32)) - 1, codes.astype(np.int32))
+        kmax = k.max(axis=1) if d else np.zeros(n, np.int32)
         return cls(codes=torch.from_numpy(codes.copy()).to(dev), l1=torch.from_numpy(l1).to(dev), m=int(m),
-                   overflow=torch.zeros(n, dtype=torch.int32, device=dev))
+                   overflow=torch.from_numpy(kmax.astype(np.int32)).to(dev))

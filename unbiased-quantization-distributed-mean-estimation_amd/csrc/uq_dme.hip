@@ -393,6 +393,41 @@ __device__ __forceinline__ void stage_tile(const TileRegs& r, float* s_x, int ti
     }
 }
 
+// Buffer descriptors for the stream kernel (guide T8/T20): built from wave-uniform values
+// only (readfirstlane on the inputs), 32-bit per-lane byte offsets, hardware range check
+// (out-of-range loads return 0, out-of-range stores are dropped: ragged last tiles need no
+// branches).  aux = 2: non-temporal (x and q are touched once per call).
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t b = (uint64_t)(uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    void* p = (void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr int kAuxNT = 2;
+
+__device__ __forceinline__ void load_tile_buf(TileRegs& r, __amdgpu_buffer_rsrc_t rx, uint32_t t0_bytes, int tid) {
+#pragma unroll
+    for (int j = 0; j < kQItems / 4; ++j) {
+        const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(rx, t0_bytes + (uint32_t)(tid + j * kQBlock) * 16u, 0,
+                                                               kAuxNT);
+        r.v[j] = make_float4(v.x, v.y, v.z, v.w);
+    }
+}
+
+__device__ __forceinline__ void store_tile_buf(const float* s_data, __amdgpu_buffer_rsrc_t ro, uint32_t t0_bytes,
+                                               int tid) {
+#pragma unroll
+    for (int j = 0; j < kQTile / 4 / kQBlock; ++j) {
+        const int q = tid + j * kQBlock;
+        const float4 v = *reinterpret_cast<const float4*>(&s_data[swz(q >> 2, q & 3)]);
+        const f32x4v w = {v.x, v.y, v.z, v.w};
+        __builtin_amdgcn_raw_buffer_store_b128(w, ro, t0_bytes + (uint32_t)q * 16u, 0, kAuxNT);
+    }
+}
+
 // Per-tile compute shared by both K2 kernels.  The tile (kQTile elements, zero-padded)
 // is staged in LDS as 256 rows of 16 (+4 pad) floats; thread `tid` owns row `tid`.
 //   pass 1: x -> v = x/den, p = |v|, mp = fm*p, fl = floor(mp), fr = mp - fl
@@ -465,22 +500,24 @@ __device__ __forceinline__ void tile_pass1(float* s_x, float* s_fr, double* s_wa
 }
 
 // Wire code of one coordinate (type codes, see uq_dme.h): k = fl + r in [0, 127] ->
-// code = k for sign(v) >= 0 and -k-1 for sign(v) < 0 (so -0.0 outputs survive);
-// k > 127 or NaN -> saturated and reported through the per-client overflow flag.
-__device__ __forceinline__ uint32_t code_of(float fl_s, float kf, bool& ovf) {
+// code = k for sign(v) >= 0 and ~k = -k-1 for sign(v) < 0 (keeps the reference's -0.0
+// outputs); k > 127 or NaN saturates and kmax = 128 flags the client.
+__device__ __forceinline__ uint32_t code_of(float fl_s, float kf, int& kmax) {
     const bool ok = kf <= 127.0f;                   // false for NaN too
-    ovf |= !ok;
     const int k = ok ? (int)kf : 127;
-    const int c = (__float_as_uint(fl_s) >> 31) ? -k - 1 : k;
+    kmax = max(kmax, ok ? k : 128);
+    const int c = (int)(__float_as_uint(fl_s) >> 31) ? ~k : k;
     return (uint32_t)(c & 0xFF);
 }
 
+// pass 2; WQ: outputs into the LDS image, WC: this thread's 16 codes into cw.
 template <bool WQ, bool WC>
 __device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const float* s_tab, int tid, double P,
                                            float L, float fm, float Xv, const TileState& st, uint32_t (&cw)[4],
-                                           bool& ovf) {
+                                           int& kmax, int len) {
     double s = P + st.texcl;
     float fprev = floorf((float)s - Xv);       // floor(c_{i-1} - X) of this thread's first element
+    const int i0 = tid * kQItems;
 #pragma unroll
     for (int k4 = 0; k4 < kQItems / 4; ++k4) {
         const int a = swz(tid, k4);
@@ -506,31 +543,32 @@ __device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const 
                 }
                 o[c] = ov;
             }
-            if (WC) w |= code_of(fls[c], kf, ovf) << (8 * c);
+            if (WC) {
+                int km = 0;
+                w |= code_of(fls[c], kf, km) << (8 * c);
+                if (i0 + 4 * k4 + c < len) kmax = max(kmax, km);
+            }
         }
         if (WQ) *reinterpret_cast<float4*>(&s_x[a]) = make_float4(o[0], o[1], o[2], o[3]);
         if (WC) cw[k4] = w;
     }
 }
 
-// Codes of this thread's 16 consecutive elements: one 16-byte store when the row is
-// full and aligned, bytes otherwise.
 template <bool CVEC>
 __device__ __forceinline__ void store_codes(int8_t* __restrict__ ct, const uint32_t (&cw)[4], int len, int tid) {
     const int i0 = tid * kQItems;
     if (CVEC && i0 + kQItems <= len) {
-        const uint4 v = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-        __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(ct + i0));
-        __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(ct + i0) + 1);
-        __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(ct + i0) + 2);
-        __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(ct + i0) + 3);
+        const u32x4v v = {cw[0], cw[1], cw[2], cw[3]};
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(ct + i0));
     } else {
         for (int k = 0; k < kQItems && i0 + k < len; ++k) ct[i0 + k] = (int8_t)((cw[k >> 2] >> (8 * (k & 3))) & 0xFF);
     }
 }
 
-__device__ __forceinline__ void flag_overflow(bool ovf, int32_t* overflow, int64_t vec, int tid) {
-    if (__any(ovf) && (tid & (kWave - 1)) == 0) atomicOr(&overflow[vec], 1);
+__device__ __forceinline__ void publish_kmax(int kmax, int32_t* kmaxv, int64_t vec, int tid) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o, kWave));
+    if ((tid & (kWave - 1)) == 0) atomicMax(&kmaxv[vec], kmax);
 }
 
 template <bool VEC4>
@@ -549,8 +587,9 @@ __device__ __forceinline__ void store_tile(const float* s_data, float* __restric
 // K2-stream: one workgroup streams one whole client vector, tiles in order, the next
 // tile prefetched into registers; P_{t+1} = fl64(P_t + A_t) carried in the workgroup.
 // No inter-workgroup communication at all.  Used when there are enough clients to
-// fill the GPU (batched DME, the bench workload).
-template <bool VEC4, bool WQ, bool WC, bool CVEC>
+// fill the GPU (batched DME, the bench workload).  Requires d % 4 == 0 and 4*d < 2^31
+// (buffer addressing); the host falls back to the look-back kernel otherwise.
+template <bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock, 4)
 quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                        int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
@@ -564,23 +603,18 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     const float L = l1[vec];
     const float den = L + 1e-12f;                  // AS:625 (f32 add)
     const float Xv = Xs[vec];
+    const uint32_t row_bytes = (uint32_t)(d * 4);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, row_bytes);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(WQ ? out + vec * d : x, row_bytes);
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(WC ? (const void*)(codes + vec * d) : (const void*)x, (uint32_t)d);
     TileRegs pre;
-    load_tile<VEC4>(pre, x, d, tiles, (uint32_t)(vec * tiles), tid);
-#ifdef UQ_PF2
-    TileRegs pre2;
-    if (tiles > 1) load_tile<VEC4>(pre2, x, d, tiles, (uint32_t)(vec * tiles + 1), tid);
-#endif
+    load_tile_buf(pre, rx, 0u, tid);
     build_table(s_tab, tid, L, fm);
     double P = 0.0;
     for (int32_t tile = 0; tile < tiles; ++tile) {
-        stage_tile<VEC4>(pre, s_x, tid);
+        stage_tile<true>(pre, s_x, tid);
         __syncthreads();
-#ifdef UQ_PF2
-        pre = pre2;
-        if (tile + 2 < tiles) load_tile<VEC4>(pre2, x, d, tiles, (uint32_t)(vec * tiles + tile + 2), tid);
-#else
-        if (tile + 1 < tiles) load_tile<VEC4>(pre, x, d, tiles, (uint32_t)(vec * tiles + tile + 1), tid);
-#endif
+        if (tile + 1 < tiles) load_tile_buf(pre, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
         const int64_t t0 = (int64_t)tile * kQTile;
         const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
         TileState st;
@@ -590,16 +624,21 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         else
             tile_pass1<false>(s_x, s_fr, s_wave, tid, len, den, fm, st);
         uint32_t cw[4];
-        bool ovf = false;
-        tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, P, L, fm, Xv, st, cw, ovf);
+        int kmax = 0;
+        tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, P, L, fm, Xv, st, cw, kmax, len);
         P = P + st.total;                          // serial definition of the tile prefix
         if (WC) {
-            store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
-            flag_overflow(ovf, overflow, vec, tid);
+            if (CVEC) {
+                const u32x4v v = {cw[0], cw[1], cw[2], cw[3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, rc, (uint32_t)(t0 + tid * kQItems), 0, kAuxNT);   // beyond d: dropped
+            } else {
+                store_codes<false>(codes + vec * d + t0, cw, len, tid);
+            }
+            publish_kmax(kmax, overflow, vec, tid);
         }
 #endif
         __syncthreads();
-        if (WQ) store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
+        if (WQ) store_tile_buf(s_x, ro, (uint32_t)t0 * 4u, tid);   // beyond d: dropped by the range check
         __syncthreads();
     }
 }
@@ -666,11 +705,11 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
         }
         __syncthreads();
         uint32_t cw[4];
-        bool ovf = false;
-        tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, s_prefix, L, fm, Xs[vec], st, cw, ovf);
+        int kmax = 0;
+        tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, s_prefix, L, fm, Xs[vec], st, cw, kmax, len);
         if (WC) {
             store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
-            flag_overflow(ovf, overflow, vec, tid);
+            publish_kmax(kmax, overflow, vec, tid);
         }
         __syncthreads();
         if (WQ) store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
@@ -726,14 +765,12 @@ client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, int64_t ld
 // a per-client table tabn[k] = RN(tab[k]/n_div) gives q/n_div exactly.
 // =====================================================================================
 constexpr int kDecChunk = 4096;   // elements per decode workgroup (256 threads x 16)
-constexpr int kMeanCols = 4096;   // columns per decode+mean workgroup (256 threads x 16)
 constexpr int kMeanClients = 32;  // clients whose tables are staged in LDS at a time
 
 __device__ __forceinline__ float decode_one(int8_t c, const float* tab) {
     const int ci = (int)c;
-    const int k = ci < 0 ? -ci - 1 : ci;
-    const float v = tab[k];
-    return ci < 0 ? -v : v;
+    const int k = ci ^ (ci >> 31);                 // ci < 0 ? -ci-1 : ci
+    return __uint_as_float(__float_as_uint(tab[k]) ^ ((uint32_t)ci & 0x80000000u));
 }
 
 template <bool VEC>
@@ -764,63 +801,62 @@ codes_decode_kernel(const int8_t* __restrict__ codes, const float* __restrict__ 
     }
 }
 
-// est[i] (+)= q_j[i] / n_div for clients j in order, q decoded from codes.  One workgroup
-// owns kMeanCols columns; client tables are staged kMeanClients at a time.
+// est[i] (+)= q_j[i] / n_div for clients j in order, q decoded from codes.  Each thread
+// owns 4 consecutive columns (one 4-byte code load per client); client tables
+// tabn[j][k] = RN(RN(RN(L1_j*k)/m)/n_div) for k <= kmax_j are staged kMeanClients at a
+// time (kmax_j from the encoder keeps them tiny: ~8 entries at R = 1).
 template <bool VEC>
 __global__ void __launch_bounds__(256)
-codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, int64_t n, int64_t d, float fm,
-                  float n_div, int accumulate, float* __restrict__ est) {
+codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, const int32_t* __restrict__ kmaxv,
+                  int64_t n, int64_t d, float fm, float n_div, int accumulate, float* __restrict__ est) {
     __shared__ float tabn[kMeanClients][128];
+    __shared__ int s_kmax[kMeanClients];
     const int tid = threadIdx.x;
-    const int64_t i0 = (int64_t)blockIdx.x * kMeanCols + (int64_t)tid * 16;
-    const bool full = VEC && i0 + 16 <= d;
-    float e[16];
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + tid) * 4;
+    const bool full = VEC && i0 + 4 <= d;
+    float e[4];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) e[k] = (accumulate && i0 + k < d) ? est[i0 + k] : 0.0f;
+    for (int k = 0; k < 4; ++k) e[k] = (accumulate && i0 + k < d) ? est[i0 + k] : 0.0f;
     for (int64_t j0 = 0; j0 < n; j0 += kMeanClients) {
         const int nb = (int)((n - j0) < kMeanClients ? (n - j0) : kMeanClients);
         __syncthreads();
+        if (tid < nb) s_kmax[tid] = min(127, max(0, kmaxv[j0 + tid]));
+        __syncthreads();
         for (int t = tid; t < nb * 128; t += 256) {
             const int jj = t >> 7, k = t & 127;
-            const float L = l1[j0 + jj];
-            tabn[jj][k] = ((L * (float)k) / fm) / n_div;
+            if (k <= s_kmax[jj]) {
+                const float L = l1[j0 + jj];
+                tabn[jj][k] = ((L * (float)k) / fm) / n_div;
+            }
         }
         __syncthreads();
         if (full) {
             int jj = 0;
-            for (; jj + 4 <= nb; jj += 4) {
-                uint4 w[4];
+            for (; jj + 8 <= nb; jj += 8) {
+                uint32_t w[8];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(codes + (j0 + jj + u) * d + i0));
-                    w[u] = make_uint4(t.x, t.y, t.z, t.w);
-                }
+                for (int u = 0; u < 8; ++u)
+                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(codes + (j0 + jj + u) * d + i0));
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+                for (int u = 0; u < 8; ++u)
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) e[k] += decode_one((int8_t)((ws[k >> 2] >> (8 * (k & 3))) & 0xFF), tabn[jj + u]);
-                }
+                    for (int k = 0; k < 4; ++k) e[k] += decode_one((int8_t)((w[u] >> (8 * k)) & 0xFF), tabn[jj + u]);
             }
             for (; jj < nb; ++jj) {
-                const uint4 w = *reinterpret_cast<const uint4*>(codes + (j0 + jj) * d + i0);
-                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+                const uint32_t w = *reinterpret_cast<const uint32_t*>(codes + (j0 + jj) * d + i0);
 #pragma unroll
-                for (int k = 0; k < 16; ++k) e[k] += decode_one((int8_t)((ws[k >> 2] >> (8 * (k & 3))) & 0xFF), tabn[jj]);
+                for (int k = 0; k < 4; ++k) e[k] += decode_one((int8_t)((w >> (8 * k)) & 0xFF), tabn[jj]);
             }
         } else {
             for (int jj = 0; jj < nb; ++jj)
-                for (int k = 0; k < 16; ++k)
+                for (int k = 0; k < 4; ++k)
                     if (i0 + k < d) e[k] += decode_one(codes[(j0 + jj) * d + i0 + k], tabn[jj]);
         }
     }
     if (full) {
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4)
-            *reinterpret_cast<float4*>(est + i0 + 4 * k4) = make_float4(e[4 * k4], e[4 * k4 + 1], e[4 * k4 + 2], e[4 * k4 + 3]);
+        *reinterpret_cast<float4*>(est + i0) = make_float4(e[0], e[1], e[2], e[3]);
     } else {
-        for (int k = 0; k < 16; ++k)
+        for (int k = 0; k < 4; ++k)
             if (i0 + k < d) est[i0 + k] = e[k];
     }
 }
@@ -979,7 +1015,7 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
     if (n == 0 || d == 0) return UQ_OK;
     if (!X) return fail(UQ_E_INVALID, "null X");
     if (!out && !codes) return fail(UQ_E_INVALID, "nothing to write: out and codes are both NULL");
-    if (codes && !overflow) return fail(UQ_E_INVALID, "codes need an overflow[n] array");
+    if (codes && !overflow) return fail(UQ_E_INVALID, "codes need a kmax[n] array");
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     float* l1buf = (float*)(wsb + w.l1_off);
@@ -994,7 +1030,7 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
         if (rc) return rc;
     }
     if (codes) {
-        rc = hip_check(hipMemsetAsync(overflow, 0, n * sizeof(int32_t), st), "memset overflow");
+        rc = hip_check(hipMemsetAsync(overflow, 0, n * sizeof(int32_t), st), "memset kmax");
         if (rc) return rc;
     }
     const float fm = (float)m;   // torch casts the Python int to f32 for `m * p` and `/ m`
@@ -1002,17 +1038,15 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
     const bool cvec = !codes || (aligned16(codes) && d % 16 == 0);
     const int wq = out ? 1 : 0, wc = codes ? 1 : 0;
     const int sel = (vec4 ? 8 : 0) | (wq ? 4 : 0) | (wc ? 2 : 0) | (cvec ? 1 : 0);
-    if (n >= kStreamMinClients) {
+    if (n >= kStreamMinClients && vec4 && d <= ((int64_t)1 << 29)) {
         // enough clients to fill the GPU: one workgroup per client vector
-#define UQ_STREAM(V, Q, C, CV)                                                                              \
-    case ((V) * 8 + (Q) * 4 + (C) * 2 + (CV)):                                                            \
-        hipLaunchKernelGGL((quantize_stream_kernel<V, Q, C, CV>), dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, \
+#define UQ_STREAM(Q, C, CV)                                                                                 \
+    case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
+        hipLaunchKernelGGL((quantize_stream_kernel<Q, C, CV>), dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, \
                            codes, overflow, d, w.tiles, fm, X, l1use);                                    \
         break;
-        switch (sel) {
-            UQ_STREAM(1, 1, 0, 1) UQ_STREAM(1, 1, 1, 1) UQ_STREAM(1, 1, 1, 0) UQ_STREAM(1, 0, 1, 1)
-            UQ_STREAM(1, 0, 1, 0) UQ_STREAM(0, 1, 0, 1) UQ_STREAM(0, 1, 1, 1) UQ_STREAM(0, 1, 1, 0)
-            UQ_STREAM(0, 0, 1, 1) UQ_STREAM(0, 0, 1, 0)
+        switch (sel & 7) {
+            UQ_STREAM(1, 0, 1) UQ_STREAM(1, 1, 1) UQ_STREAM(1, 1, 0) UQ_STREAM(0, 1, 1) UQ_STREAM(0, 1, 0)
             default: return fail(UQ_E_INVALID, "internal: bad kernel selector");
         }
 #undef UQ_STREAM
@@ -1069,20 +1103,20 @@ int uq_codes_decode_f32(const int8_t* codes, const float* l1, int64_t n, int64_t
     return hip_check(hipGetLastError(), "codes_decode_kernel launch");
 }
 
-int uq_codes_mean_f32(const int8_t* codes, const float* l1, int64_t n, int64_t d, int64_t m, float n_div,
-                      int32_t accumulate, float* est, void* stream) {
+int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax, int64_t n, int64_t d, int64_t m,
+                      float n_div, int32_t accumulate, float* est, void* stream) {
     if (n < 0 || d < 0 || m < 0) return fail(UQ_E_INVALID, "n, d and m must be >= 0");
     if (d == 0) return UQ_OK;
-    if (!est || (n > 0 && (!codes || !l1))) return fail(UQ_E_INVALID, "null pointer");
+    if (!est || (n > 0 && (!codes || !l1 || !kmax))) return fail(UQ_E_INVALID, "null pointer");
     hipStream_t st = (hipStream_t)stream;
     const bool vec = (n == 0 || aligned16(codes)) && aligned16(est) && d % 16 == 0;
-    const int64_t blocks = (d + kMeanCols - 1) / kMeanCols;
+    const int64_t blocks = (d + 1023) / 1024;
     if (blocks > 0x7FFFFFFF) return fail(UQ_E_INVALID, "d too large");
     if (vec)
-        hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, n, d,
+        hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, kmax, n, d,
                            (float)m, n_div, accumulate, est);
     else
-        hipLaunchKernelGGL(codes_mean_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, n, d,
+        hipLaunchKernelGGL(codes_mean_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, kmax, n, d,
                            (float)m, n_div, accumulate, est);
     return hip_check(hipGetLastError(), "codes_mean_kernel launch");
 }

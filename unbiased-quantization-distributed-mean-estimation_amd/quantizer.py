@@ -173,7 +173,7 @@ def quantize_encode(x, bits_per_dimension=1, X=None, *, m: int | None = None, to
     if l1 is not None:
         l1 = torch.as_tensor(l1, dtype=torch.float32).reshape(-1).to(dev).contiguous()
     codes = torch.empty((n, d), dtype=torch.int8, device=dev)
-    overflow = torch.zeros(n, dtype=torch.int32, device=dev)
+    overflow = torch.zeros(n, dtype=torch.int32, device=dev)     # per-client kmax (128 = overflow)
     l1_out = torch.empty(n, dtype=torch.float32, device=dev)
     q = torch.empty_like(x) if return_q else None
     nb = _ws_bytes(n, d, T)
@@ -207,7 +207,8 @@ def codes_mean(tc, n_div, est=None, accumulate: bool = False) -> torch.Tensor:
     if est is None:
         est = torch.empty(d, dtype=torch.float32, device=dev)
         accumulate = False
-    _lib.check(_lib.load().uq_codes_mean_f32(_ptr(codes), _ptr(l1), n, d, int(tc.m), float(n_div),
+    kmax = tc.overflow.to(device=dev, dtype=torch.int32).contiguous()
+    _lib.check(_lib.load().uq_codes_mean_f32(_ptr(codes), _ptr(l1), _ptr(kmax), n, d, int(tc.m), float(n_div),
                                              int(bool(accumulate)), _ptr(est), _stream_ptr(dev)), "uq_codes_mean_f32")
     return est
 
