@@ -4,6 +4,8 @@ FETCH_SIZE reads half the bytes of wide coalesced streaming loads -> x2; MI355X_
 import csv, glob, json, os, shutil, sys
 src, tag = sys.argv[1], sys.argv[2]
 pipeline = sys.argv[3] if len(sys.argv) > 3 else "codes"
+# quantize_stream_kernel<WQ, WC, CVEC> instance used by each bench pipeline
+VARIANT = {"q": "<true, false, true>", "codes": "<true, true, true>", "encode": "<false, true, true>"}
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -25,13 +27,14 @@ out = {"tag": tag, "d": 1 << 20, "clients": 1024, "pipeline": pipeline, "units":
 for k in fetch:
     f = sum(fetch[k]) / len(fetch[k]); w = sum(write.get(k, [0])) / max(1, len(write.get(k, [0])))
     out["kernels"][k[:80]] = {"fetch_kb_raw": f, "write_kb": w, "hbm_bytes": (2 * f + w) * 1024}
-    if "quantize_stream_kernel" in k:
+    if "quantize_stream_kernel" in k and VARIANT[pipeline] in k:
         out["quantize_bytes_per_launch"] = (2 * f + w) * 1024
+        out["quantize_kernel"] = k[:120]
 sq = glob.glob(os.path.join(src, "sq", "**", "*counter_collection.csv"), recursive=True)
 if sq:
     agg = {}
     for r in csv.DictReader(open(sq[0])):
-        if "quantize_stream_kernel" in r["Kernel_Name"]:
+        if "quantize_stream_kernel" in r["Kernel_Name"] and VARIANT[pipeline] in r["Kernel_Name"]:
             agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     out["quantize_sq"] = {c: sum(v) / len(v) for c, v in agg.items()}
 json.dump(out, open(os.path.join(prof, f"pmc_{tag}.json"), "w"), indent=1)

@@ -499,25 +499,25 @@ __device__ __forceinline__ void tile_pass1(float* s_x, float* s_fr, double* s_wa
     st.total = total;
 }
 
-// Wire code of one coordinate (type codes, see uq_dme.h): k = fl + r in [0, 127] ->
+// Wire code of one coordinate (type codes, see uq_dme.h): k = fl + r ->
 // code = k for sign(v) >= 0 and ~k = -k-1 for sign(v) < 0 (keeps the reference's -0.0
-// outputs); k > 127 or NaN saturates and kmax = 128 flags the client.
-__device__ __forceinline__ uint32_t code_of(float fl_s, float kf, int& kmax) {
-    const bool ok = kf <= 127.0f;                   // false for NaN too
-    const int k = ok ? (int)kf : 127;
-    kmax = max(kmax, ok ? k : 128);
-    const int c = (int)(__float_as_uint(fl_s) >> 31) ? ~k : k;
-    return (uint32_t)(c & 0xFF);
+// outputs).  kmax (float) tracks the largest k; a client whose kmax > 127 is flagged as
+// overflow (its codes are meaningless).  fl is finite whenever L1 is finite, and a
+// non-finite L1 flags the client separately (publish_kmax).
+__device__ __forceinline__ uint32_t code_of(float fl_s, float kf, float& kmax) {
+    kmax = fmaxf(kmax, kf);
+    const int mask = (int)__float_as_uint(fl_s) >> 31;      // 0 or -1
+    return (uint32_t)(((int)kf ^ mask) & 0xFF);
 }
 
 // pass 2; WQ: outputs into the LDS image, WC: this thread's 16 codes into cw.
 template <bool WQ, bool WC>
 __device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const float* s_tab, int tid, double P,
                                            float L, float fm, float Xv, const TileState& st, uint32_t (&cw)[4],
-                                           int& kmax, int len) {
+                                           float& kmax, int len) {
     double s = P + st.texcl;
     float fprev = floorf((float)s - Xv);       // floor(c_{i-1} - X) of this thread's first element
-    const int i0 = tid * kQItems;
+    (void)len;
 #pragma unroll
     for (int k4 = 0; k4 < kQItems / 4; ++k4) {
         const int a = swz(tid, k4);
@@ -543,11 +543,7 @@ __device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const 
                 }
                 o[c] = ov;
             }
-            if (WC) {
-                int km = 0;
-                w |= code_of(fls[c], kf, km) << (8 * c);
-                if (i0 + 4 * k4 + c < len) kmax = max(kmax, km);
-            }
+            if (WC) w |= code_of(fls[c], kf, kmax) << (8 * c);   // padding elements: fl = 0, r = 0
         }
         if (WQ) *reinterpret_cast<float4*>(&s_x[a]) = make_float4(o[0], o[1], o[2], o[3]);
         if (WC) cw[k4] = w;
@@ -565,7 +561,8 @@ __device__ __forceinline__ void store_codes(int8_t* __restrict__ ct, const uint3
     }
 }
 
-__device__ __forceinline__ void publish_kmax(int kmax, int32_t* kmaxv, int64_t vec, int tid) {
+__device__ __forceinline__ void publish_kmax(float kmaxf, float L, int32_t* kmaxv, int64_t vec, int tid) {
+    int kmax = (kmaxf <= 127.0f && isfinite(L)) ? (int)kmaxf : 128;     // 128 = overflow / not codable
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o, kWave));
     if ((tid & (kWave - 1)) == 0) atomicMax(&kmaxv[vec], kmax);
@@ -624,7 +621,7 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         else
             tile_pass1<false>(s_x, s_fr, s_wave, tid, len, den, fm, st);
         uint32_t cw[4];
-        int kmax = 0;
+        float kmax = 0.0f;
         tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, P, L, fm, Xv, st, cw, kmax, len);
         P = P + st.total;                          // serial definition of the tile prefix
         if (WC) {
@@ -634,7 +631,7 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
             } else {
                 store_codes<false>(codes + vec * d + t0, cw, len, tid);
             }
-            publish_kmax(kmax, overflow, vec, tid);
+            publish_kmax(kmax, L, overflow, vec, tid);
         }
 #endif
         __syncthreads();
@@ -705,11 +702,11 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
         }
         __syncthreads();
         uint32_t cw[4];
-        int kmax = 0;
+        float kmax = 0.0f;
         tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, s_prefix, L, fm, Xs[vec], st, cw, kmax, len);
         if (WC) {
             store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
-            publish_kmax(kmax, overflow, vec, tid);
+            publish_kmax(kmax, L, overflow, vec, tid);
         }
         __syncthreads();
         if (WQ) store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
@@ -802,21 +799,24 @@ codes_decode_kernel(const int8_t* __restrict__ codes, const float* __restrict__ 
 }
 
 // est[i] (+)= q_j[i] / n_div for clients j in order, q decoded from codes.  Each thread
-// owns 4 consecutive columns (one 4-byte code load per client); client tables
-// tabn[j][k] = RN(RN(RN(L1_j*k)/m)/n_div) for k <= kmax_j are staged kMeanClients at a
-// time (kmax_j from the encoder keeps them tiny: ~8 entries at R = 1).
+// owns kMeanCpt consecutive columns (one 8-byte code load per client); 16 clients of
+// loads are kept in flight.  Client tables tabn[j][k] = RN(RN(RN(L1_j*k)/m)/n_div) for
+// k <= kmax_j are staged kMeanClients at a time (kmax_j from the encoder keeps them tiny:
+// ~8 entries at R = 1).
+constexpr int kMeanCpt = 8;
+constexpr int kMeanUnroll = 16;
 template <bool VEC>
 __global__ void __launch_bounds__(256)
 codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, const int32_t* __restrict__ kmaxv,
                   int64_t n, int64_t d, float fm, float n_div, int accumulate, float* __restrict__ est) {
-    __shared__ float tabn[kMeanClients][128];
+    __shared__ float tabn[kMeanClients][256];     // indexed by the raw code byte, sign included
     __shared__ int s_kmax[kMeanClients];
     const int tid = threadIdx.x;
-    const int64_t i0 = ((int64_t)blockIdx.x * 256 + tid) * 4;
-    const bool full = VEC && i0 + 4 <= d;
-    float e[4];
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + tid) * kMeanCpt;
+    const bool full = VEC && i0 + kMeanCpt <= d;
+    float e[kMeanCpt];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) e[k] = (accumulate && i0 + k < d) ? est[i0 + k] : 0.0f;
+    for (int k = 0; k < kMeanCpt; ++k) e[k] = (accumulate && i0 + k < d) ? est[i0 + k] : 0.0f;
     for (int64_t j0 = 0; j0 < n; j0 += kMeanClients) {
         const int nb = (int)((n - j0) < kMeanClients ? (n - j0) : kMeanClients);
         __syncthreads();
@@ -826,37 +826,50 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
             const int jj = t >> 7, k = t & 127;
             if (k <= s_kmax[jj]) {
                 const float L = l1[j0 + jj];
-                tabn[jj][k] = ((L * (float)k) / fm) / n_div;
+                const float v = ((L * (float)k) / fm) / n_div;
+                tabn[jj][k] = v;            // code k
+                tabn[jj][255 - k] = -v;     // code ~k = -k-1 -> byte 255-k; (-a)/n = -(a/n)
             }
         }
         __syncthreads();
         if (full) {
+            const int8_t* cp = codes + j0 * d + i0;
             int jj = 0;
-            for (; jj + 8 <= nb; jj += 8) {
-                uint32_t w[8];
+            for (; jj + kMeanUnroll <= nb; jj += kMeanUnroll) {
+                uint2 w[kMeanUnroll];
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(codes + (j0 + jj + u) * d + i0));
+                for (int u = 0; u < kMeanUnroll; ++u) {
+                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                    const u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(cp + (int64_t)(jj + u) * d));
+                    w[u] = make_uint2(t.x, t.y);
+                }
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
+                for (int u = 0; u < kMeanUnroll; ++u) {
+                    const float* tb = tabn[jj + u];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) e[k] += decode_one((int8_t)((w[u] >> (8 * k)) & 0xFF), tabn[jj + u]);
+                    for (int k = 0; k < 4; ++k) e[k] += tb[(w[u].x >> (8 * k)) & 0xFF];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) e[4 + k] += tb[(w[u].y >> (8 * k)) & 0xFF];
+                }
             }
             for (; jj < nb; ++jj) {
-                const uint32_t w = *reinterpret_cast<const uint32_t*>(codes + (j0 + jj) * d + i0);
+                const uint2 w = *reinterpret_cast<const uint2*>(cp + (int64_t)jj * d);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) e[k] += decode_one((int8_t)((w >> (8 * k)) & 0xFF), tabn[jj]);
+                for (int k = 0; k < 4; ++k) e[k] += tabn[jj][(w.x >> (8 * k)) & 0xFF];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) e[4 + k] += tabn[jj][(w.y >> (8 * k)) & 0xFF];
             }
         } else {
             for (int jj = 0; jj < nb; ++jj)
-                for (int k = 0; k < 4; ++k)
-                    if (i0 + k < d) e[k] += decode_one(codes[(j0 + jj) * d + i0 + k], tabn[jj]);
+                for (int k = 0; k < kMeanCpt; ++k)
+                    if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[(j0 + jj) * d + i0 + k]];
         }
     }
     if (full) {
         *reinterpret_cast<float4*>(est + i0) = make_float4(e[0], e[1], e[2], e[3]);
+        *reinterpret_cast<float4*>(est + i0 + 4) = make_float4(e[4], e[5], e[6], e[7]);
     } else {
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < kMeanCpt; ++k)
             if (i0 + k < d) est[i0 + k] = e[k];
     }
 }
@@ -1110,7 +1123,7 @@ int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax,
     if (!est || (n > 0 && (!codes || !l1 || !kmax))) return fail(UQ_E_INVALID, "null pointer");
     hipStream_t st = (hipStream_t)stream;
     const bool vec = (n == 0 || aligned16(codes)) && aligned16(est) && d % 16 == 0;
-    const int64_t blocks = (d + 1023) / 1024;
+    const int64_t blocks = (d + 256 * kMeanCpt - 1) / (256 * kMeanCpt);
     if (blocks > 0x7FFFFFFF) return fail(UQ_E_INVALID, "d too large");
     if (vec)
         hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, kmax, n, d,
