@@ -106,6 +106,30 @@ int uq_codes_decode_f32(const int8_t* codes, const float* l1, int64_t n, int64_t
 int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax, int64_t n, int64_t d,
                       int64_t m, float n_div, int32_t accumulate, float* est, void* stream);
 
+/* ---- biased type quantizer (Reznik rounding) ------------------------------------------
+ * NMSE_Results/Codes/All_Schemes.py:669-687 Type_biased_quantize and :644-666 Reznik for
+ * a batch: out[j] = Type_biased_quantize(x[j], ·) with m = the lattice sum (AS:684).
+ *   k' = floor(m p + 0.5), m' = sum k' (torch CPU order for torch_threads), Delta = int(m' - m);
+ *   the |Delta| coordinates with the largest delta' = k' - m p (Delta > 0: k' -= 1) or the
+ *   smallest (Delta < 0: k' += 1) are adjusted; out = (L1 * sign(x)) * (k' / m).
+ * tie_policy decides which of several coordinates with the same delta' at the selection
+ * threshold are taken (torch.topk compares values only):
+ *   UQ_TIES_TORCH         the coordinates torch CPU's topk returns (libstdc++
+ *                         nth_element / partial_sort replayed on the GPU): bit-identical
+ *                         to the reference on every input
+ *   UQ_TIES_LOWEST_INDEX  the lowest indices (cheaper; identical whenever no tie straddles
+ *                         the threshold, i.e. info flag 1 is clear)
+ * l1_out [n] f32 or NULL.  info [n][2] int32 or NULL: {Delta, flags}; flags bit0 = a tie
+ * straddled the threshold, bit1 = m' not finite (the reference raises; output is NaN-laden),
+ * bit2 = |Delta| > d (the reference's topk raises), bit3 = torch tie choice replayed.
+ * Workspace: uq_biased_workspace_bytes (need not be zero-filled). */
+#define UQ_TIES_TORCH 0
+#define UQ_TIES_LOWEST_INDEX 1
+int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t torch_threads, size_t* bytes_out);
+int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m,
+                       int32_t torch_threads, int32_t tie_policy, float* l1_out, int32_t* info,
+                       void* ws, size_t ws_bytes, void* stream);
+
 /* After the stream has been synchronised: UQ_OK, or UQ_E_TIMEOUT if any
  * inter-workgroup wait in a previous call on this workspace gave up. Clears it. */
 int uq_check_status(void* ws, void* stream);

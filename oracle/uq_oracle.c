@@ -82,6 +82,22 @@ static float chunk_sum(const float* x, int64_t s) {
     return acc;
 }
 
+/* torch CPU f32 `sum` of a contiguous vector for `torch_threads` intra-op threads. */
+float uqo_torch_sum(const float* v, int64_t d, int torch_threads) {
+    if (d <= 0) return 0.0f;
+    int T = torch_threads < 1 ? 1 : torch_threads;
+    if (d < TORCH_GRAIN || T == 1) return chunk_sum(v, d);
+    int64_t nt = (d + TORCH_GRAIN - 1) / TORCH_GRAIN;
+    if (nt > T) nt = T;
+    int64_t cs = (d + nt - 1) / nt;
+    float acc = 0.0f;
+    for (int64_t c = 0; c < nt; ++c) {
+        int64_t b = c * cs, e = b + cs < d ? b + cs : d;
+        if (e > b) acc += chunk_sum(v + b, e - b);
+    }
+    return acc;
+}
+
 /* |x| into scratch, then torch's chunking by intra-op thread count. */
 float uqo_l1_torch_order(const float* x, int64_t d, int torch_threads, float* scratch) {
     if (d <= 0) return 0.0f;

@@ -33,6 +33,10 @@ def lib():
         L.uqo_quantize_batch.argtypes = [p, p, i64, i64, i64, p, ctypes.c_int, p, p]
         L.uqo_client_mean.restype = None
         L.uqo_client_mean.argtypes = [p, i64, i64, f, p]
+        L.uqo_torch_sum.restype = f
+        L.uqo_torch_sum.argtypes = [p, i64, ctypes.c_int]
+        L.uqo_biased_quantize.restype = ctypes.c_int
+        L.uqo_biased_quantize.argtypes = [p, p, i64, i64, ctypes.c_int, ctypes.c_int, p, p, p]
         _lib = L
     return _lib
 
@@ -72,3 +76,26 @@ def client_mean(q2d, n_div):
     est = np.empty(d, np.float32)
     lib().uqo_client_mean(_ptr(q2d), n, d, np.float32(n_div), _ptr(est))
     return est
+
+
+def torch_sum(v, torch_threads: int = 1):
+    v = np.ascontiguousarray(v, dtype=np.float32).reshape(-1)
+    return np.float32(lib().uqo_torch_sum(_ptr(v), v.shape[0], torch_threads))
+
+
+def biased_quantize(x, m: int, torch_threads: int = 1, tie_mode: int = 0):
+    """Type_biased_quantize (AS:669-687).  tie_mode 0: torch's topk choice among equal
+    values at the threshold; 1: lowest indices.  Returns (out, L1, Delta, ambiguous);
+    raises like the reference (ValueError / RuntimeError)."""
+    x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1)
+    out = np.empty_like(x)
+    L = np.zeros(1, np.float32)
+    D = np.zeros(1, np.int64)
+    A = np.zeros(1, np.int32)
+    rc = lib().uqo_biased_quantize(_ptr(x), _ptr(out), x.shape[0], m, torch_threads, tie_mode, _ptr(L), _ptr(D),
+                                   _ptr(A))
+    if rc == -1:
+        raise ValueError("cannot convert float NaN to integer (m' not finite, AS:656)")
+    if rc == -2:
+        raise RuntimeError("selected index k out of range (AS:660)")
+    return out, np.float32(L[0]), int(D[0]), bool(A[0])

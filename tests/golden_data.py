@@ -42,9 +42,25 @@ def spec_gen(sp) -> np.ndarray:
         v = rs.choice(np.arange(2), size=d, p=[0.3, 0.7]).astype(np.float64)
     elif kind == "lognormal":
         v = rs.lognormal(mean=1, sigma=2, size=d)
+    elif kind == "rounded":            # tie-heavy: many equal |x|
+        v = np.round(rs.normal(loc=0, scale=1, size=d) * 4) / 4
+    elif kind == "smallint":           # signed small integers: massive ties
+        v = rs.randint(-3, 4, size=d).astype(np.float64)
     else:
         raise ValueError(kind)
     return v.astype(f32)
+
+
+def biased_vectors():
+    """Fixtures of Type_biased_quantize (AS:669-687) made by make_golden_biased.py.
+    Yields (spec, x, expected_or_None, expected_sha)."""
+    z = np.load(os.path.join(GOLDEN, "biased_vectors.npz"))
+    specs = json.load(open(os.path.join(GOLDEN, "biased_vectors.json")))
+    for sp in specs:
+        i = sp["idx"]
+        x = z[f"x{i}"] if f"x{i}" in z.files else spec_gen(sp)
+        q = z[f"q{i}"] if f"q{i}" in z.files else None
+        yield sp, x, q, sp.get("sha")
 
 
 def spec_vectors(large=None):

@@ -1,0 +1,112 @@
+"""GPU parity of the biased type quantizer (AS:669-687) through the C-ABI, against the
+reference's fixtures and the C++ oracle (bit-exact; NaN positions compared as NaN)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import uq_oracle_c as C
+from oracle.uq_oracle import rate_to_m
+from tests import golden_data as G
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def uq(gpu_ready):
+    import uqdme
+    C.build()
+    return uqdme
+
+
+@pytest.fixture(scope="module")
+def cases():
+    return list(G.biased_vectors())
+
+
+def run(uq, x, R, T, ties):
+    xd = torch.as_tensor(np.ascontiguousarray(x, f32)).cuda().view(1, -1)
+    m = rate_to_m(R, x.shape[0])
+    out, info = uq.biased_quantize(xd, m=m, torch_threads=T, ties=ties, return_info=True)
+    return out.view(-1).cpu().numpy(), info.cpu().numpy()[0]
+
+
+def test_fixtures_lowest_rule(uq, cases):
+    """ties='lowest': bit-exact with the reference wherever no tie straddles the threshold,
+    and bit-exact with the oracle's lowest-index rule everywhere."""
+    bad = []
+    for sp, x, q, h in cases:
+        if sp.get("raises"):
+            continue
+        out, info = run(uq, x, sp["R"], sp["threads"], "lowest")
+        assert info[0] == sp["delta"], sp["idx"]
+        assert bool(info[1] & 1) == sp["ambiguous"], sp["idx"]
+        if not sp["ambiguous"]:
+            ok = G.bits_equal(out, q) if q is not None else G.sha(out) == h
+        else:
+            with np.errstate(all="ignore"):
+                exp, *_ = C.biased_quantize(x, rate_to_m(sp["R"], x.shape[0]), sp["threads"], 1)
+            ok = G.bits_equal(out, exp)
+        if not ok:
+            bad.append(sp["idx"])
+    assert not bad, f"GPU differs on fixtures {bad}"
+
+
+def test_raising_cases(uq, cases):
+    for sp, x, q, h in cases:
+        if not sp.get("raises"):
+            continue
+        out, info = run(uq, x, sp["R"], sp["threads"], "lowest")
+        assert info[1] & 4, sp["idx"]           # |Delta| > d: torch.topk raises
+        with pytest.raises(RuntimeError):
+            uq.Type_biased_quantize(torch.as_tensor(x), sp["R"])
+
+
+def test_batch_rows_independent(uq):
+    rng = np.random.default_rng(11)
+    n, d = 37, 3001
+    x = rng.standard_normal((n, d)).astype(f32)
+    x[5] = np.round(x[5] * 2) / 2          # some tie-heavy rows
+    x[17] = rng.integers(-2, 3, d)
+    m = rate_to_m(1, d)
+    out = uq.biased_quantize(torch.as_tensor(x).cuda(), m=m, torch_threads=1, ties="lowest").cpu().numpy()
+    for j in range(n):
+        exp, *_ = C.biased_quantize(x[j], m, 1, 1)
+        assert G.bits_equal(out[j], exp), j
+
+
+def test_large_batch_vs_oracle(uq):
+    """n = 64 clients at d = 2^18: the multi-workgroup histogram / tile paths."""
+    rng = np.random.default_rng(12)
+    n, d = 64, 1 << 18
+    x = rng.standard_normal((n, d)).astype(f32)
+    x[::4] = np.round(x[::4] * 3) / 3
+    for R in (1, 4):
+        m = rate_to_m(R, d)
+        out = uq.biased_quantize(torch.as_tensor(x).cuda(), m=m, torch_threads=8, ties="lowest").cpu().numpy()
+        for j in range(0, n, 7):
+            exp, *_ = C.biased_quantize(x[j], m, 8, 1)
+            assert G.bits_equal(out[j], exp), (R, j)
+
+
+def test_unaligned_and_ragged(uq):
+    rng = np.random.default_rng(13)
+    for d in (1, 3, 7, 31, 4097, 16385, 70001):
+        base = torch.as_tensor(rng.standard_normal(d + 1).astype(f32)).cuda()
+        xv = base[1:].view(1, d)           # 4-byte offset: scalar paths
+        m = rate_to_m(2, d)
+        out = uq.biased_quantize(xv, m=m, torch_threads=1, ties="lowest").cpu().numpy()[0]
+        exp, *_ = C.biased_quantize(xv.cpu().numpy()[0], m, 1, 1)
+        assert G.bits_equal(out, exp), d
+
+
+def test_drop_in_semantics(uq):
+    x = torch.randn(1000)
+    with pytest.raises(KeyError):
+        uq.Type_biased_quantize(x, 3.3)
+    state = torch.get_rng_state()
+    y = uq.Type_biased_quantize(x, 1)
+    assert torch.equal(state, torch.get_rng_state())     # the biased quantizer draws nothing
+    assert y.is_cuda and y.dtype == torch.float32 and y.shape == (1000,)
+    assert uq.Type_biased_quantize.__name__ == "Type_biased_quantize"
+    assert uq.Type_biased_quantize(torch.empty(0), 1).numel() == 0

@@ -1,8 +1,9 @@
 """MI355X-native unbiased L1-ball type quantizer for distributed mean estimation.
 
 Reference: Ritesh622/Unbiased-Quantization-Distributed-Mean-Estimation,
-`Type_unbiased_quantize` (NMSE_Results/Codes/All_Schemes.py:609-641) and the client
-mean around it (NMSE_Results/Codes/Normal_dist.py:133-138).  Import through the
+`Type_unbiased_quantize` (NMSE_Results/Codes/All_Schemes.py:609-641), the client
+mean around it (NMSE_Results/Codes/Normal_dist.py:133-138) and the biased variant
+`Type_biased_quantize` (All_Schemes.py:644-687).  Import through the
 top-level alias `uqdme` (this directory name is not a Python identifier).
 """
 from .rates import RATE_TABLE, rate_to_m
@@ -12,6 +13,7 @@ from .quantizer import (
     quantize_encode, decode, codes_mean,
 )
 from .codes import TypeCodes
+from .biased import Type_biased_quantize, biased_quantize
 from ._lib import UQError, load as load_library, library_path
 from .distributed import shard_range, sharded_client_mean, sharded_quantize_mean
 from .dme import DISTRIBUTIONS, nmse_simulation
@@ -21,5 +23,5 @@ __all__ = [
     "quantize_mean", "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
     "check_status", "UQError", "load_library", "library_path", "shard_range", "sharded_client_mean",
     "sharded_quantize_mean", "DISTRIBUTIONS", "nmse_simulation", "quantize_encode", "decode", "codes_mean",
-    "TypeCodes",
+    "TypeCodes", "Type_biased_quantize", "biased_quantize",
 ]

@@ -1,0 +1,105 @@
+"""Biased type quantizer (Reznik rounding) on the GPU — SURVEY §8(f) row 1.
+
+Drop-in:
+    Type_biased_quantize(input_vector, bits_per_dimension=1)
+        == NMSE_Results/Codes/All_Schemes.py:669-687 (with Reznik, AS:644-666): same name,
+        argument meaning, return type (new f32 tensor of shape (d,) on the GPU), no RNG,
+        KeyError for an unknown rate (AS:684).
+
+Batched:
+    biased_quantize(x[n, d], bits | m=, ties="torch" | "lowest") -> out[n, d]
+
+Numerics (all f32, as torch CPU): k' = floor(m*p + 0.5), m' = k'.sum() in torch CPU order
+for `torch_threads`, Delta = int(m' - m), the |Delta| extreme delta' = k' - m*p adjusted by
+-+1, out = (L1 * sign(x)) * (k' / m).  torch.topk picks among equal delta' values by what
+libstdc++'s nth_element / partial_sort leave in front; ties="lowest" takes the lowest
+indices instead (identical whenever info flag 1 is clear; see include/uq_dme.h).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .quantizer import (_as_device_f32_2d, _device, _ptr, _resolve_m, _stream_ptr, _workspace,
+                        get_torch_threads)
+from .rates import RATE_TABLE
+
+__all__ = ["Type_biased_quantize", "biased_quantize", "TIES_TORCH", "TIES_LOWEST_INDEX",
+           "FLAG_AMBIGUOUS", "FLAG_NONFINITE", "FLAG_RANGE", "FLAG_TORCH_TIES"]
+
+TIES_TORCH = 0            # UQ_TIES_TORCH
+TIES_LOWEST_INDEX = 1     # UQ_TIES_LOWEST_INDEX
+FLAG_AMBIGUOUS = 1
+FLAG_NONFINITE = 2
+FLAG_RANGE = 4
+FLAG_TORCH_TIES = 8
+
+_TIES = {"torch": TIES_TORCH, "lowest": TIES_LOWEST_INDEX, TIES_TORCH: TIES_TORCH,
+         TIES_LOWEST_INDEX: TIES_LOWEST_INDEX}
+
+
+def _biased_ws_bytes(n: int, d: int, T: int) -> int:
+    out = ctypes.c_size_t(0)
+    _lib.check(_lib.load().uq_biased_workspace_bytes(n, d, T, ctypes.byref(out)), "uq_biased_workspace_bytes")
+    return int(out.value)
+
+
+def biased_quantize(x, bits_per_dimension=1, *, m: int | None = None, torch_threads: int | None = None,
+                    ties="torch", out=None, return_l1: bool = False, return_info: bool = False):
+    """Batched Type_biased_quantize over the rows of x [n, d].
+
+    return_info adds an int32 [n, 2] tensor {Delta, flags} per row (flags: 1 a tie
+    straddled the threshold, 2 m' not finite, 4 |Delta| > d, 8 torch tie choice replayed)."""
+    dev = _device()
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    mm = _resolve_m(bits_per_dimension, m, d)
+    T = get_torch_threads() if torch_threads is None else int(torch_threads)
+    if ties not in _TIES:
+        raise ValueError("ties must be 'torch' or 'lowest'")
+    if out is None:
+        out = torch.empty_like(x)
+    elif out.shape != x.shape or out.dtype != torch.float32 or out.device != x.device or not out.is_contiguous():
+        raise ValueError("out must be a contiguous f32 tensor like x")
+    l1_out = torch.empty(n, dtype=torch.float32, device=dev) if return_l1 else None
+    info = torch.empty((n, 2), dtype=torch.int32, device=dev) if return_info else None
+    ws = _workspace(dev, _biased_ws_bytes(n, d, T))
+    _lib.check(_lib.load().uq_type_biased_f32(_ptr(x), _ptr(out), n, d, mm, T, _TIES[ties], _ptr(l1_out),
+                                              _ptr(info), _ptr(ws), ws.numel(), _stream_ptr(dev)),
+               "uq_type_biased_f32")
+    res = [out]
+    if return_l1:
+        res.append(l1_out)
+    if return_info:
+        res.append(info)
+    return res[0] if len(res) == 1 else tuple(res)
+
+
+def Type_biased_quantize(input_vector, bits_per_dimension=1):
+    """Drop-in for NMSE_Results/Codes/All_Schemes.py:669 (same name for FLM:177's
+    directory naming).  Copies the input (AS:671), KeyError for an unknown rate
+    (AS:684), bit-identical to the reference on torch CPU with the same intra-op
+    thread count, ties included.  The reference raises when m' is not finite (AS:656);
+    so does this."""
+    dev = _device()
+    l_rate = RATE_TABLE[bits_per_dimension]
+    if torch.is_tensor(input_vector):
+        v = input_vector.detach().to(device=dev, dtype=torch.float32).clone()
+    else:
+        v = torch.tensor(np.asarray(input_vector), dtype=torch.float32, device=dev)
+    if v.dim() != 1:
+        raise RuntimeError("Type_biased_quantize expects a 1-D vector")
+    d = v.numel()
+    m = int(l_rate * d)
+    if d == 0:
+        return v
+    out, info = biased_quantize(v.view(1, d), m=m, ties="torch", return_info=True)
+    flags = int(info[0, 1].item())
+    if flags & FLAG_NONFINITE:
+        raise ValueError("cannot convert float NaN to integer (m' is not finite, AS:656)")
+    if flags & FLAG_RANGE:
+        raise RuntimeError("selected index k out of range (AS:660)")
+    return out.view(d)

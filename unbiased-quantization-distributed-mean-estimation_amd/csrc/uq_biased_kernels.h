@@ -1,0 +1,330 @@
+// uq_biased_kernels.h — device code of the biased type quantizer (Reznik rounding).
+// Included by uq_dme.hip inside its anonymous namespace (shares the K1 cascade).
+//
+// Reference (paths relative to the reference root):
+//   NMSE_Results/Codes/All_Schemes.py:669-687  Type_biased_quantize
+//   NMSE_Results/Codes/All_Schemes.py:644-666  Reznik
+//
+// Per client j (one row of x):
+//   KB1  L1 = |x|.sum()                  K1 cascade, AbsOp           (AS:680)
+//   KB2  m' = k'.sum(), k' = floor(m p + 0.5)  K1 cascade, RezKOp    (AS:648-649)
+//   KB3  Delta = int(m' - m) -> |Delta| selections                    (AS:651-656)
+//   KB4  radix select (3 passes, 11/11/10-bit digits) of the |Delta|-th largest key of
+//        +delta' (Delta > 0) or -delta' (Delta < 0), delta' = k' - m p  (AS:655-665)
+//   KB5  (ambiguous clients only) tie counts per tile, for the index-order tie rank
+//   KB6  out = (L1 * sign(x)) * (k'' / m), k'' = k' -+ 1 on the selected set (AS:661/665/687)
+// torch.topk compares values (as doubles): equal values are ties whatever their index.
+// When the threshold value occurs more often than it is selected ("ambiguous"), torch's
+// choice is the one libstdc++'s nth_element / partial_sort makes; KB6 takes the lowest
+// indices instead, and the torch choice is replayed by uq_biased_torch_ties.h.
+
+constexpr int kRadixBins = 2048;
+constexpr int kHistItems = 64;                      // elements per thread in a histogram pass
+constexpr int kHistSpan = 256 * kHistItems;         // 16384 elements per workgroup
+constexpr int kSelItems = 16;                       // contiguous elements per thread (KB5/KB6)
+constexpr int kSelTile = 256 * kSelItems;           // 4096 elements per tile
+
+enum RezFlags : int32_t {
+    kRezAmbiguous = 1,     // threshold value shared by selected and unselected coordinates
+    kRezNonFinite = 2,     // m' is NaN/inf: the reference raises in int(m' - m) (AS:656)
+    kRezRange = 4,         // |Delta| > d: torch.topk raises (cannot happen for finite input)
+    kRezTorchTies = 8,     // selection set replayed with torch's tie choice (KB7)
+};
+
+struct RezState {          // 32 bytes per client; (delta, flags) are the public info pair
+    int32_t delta;         // AS:656; 0 when m' == m (AS:651) or on error
+    int32_t flags;         // RezFlags
+    float mprime;          // AS:649
+    uint32_t prefix;       // threshold key bits decided so far
+    uint32_t kleft;        // selections still to place at/below the prefix
+    uint32_t eq;           // keys equal to the threshold (after the last pass)
+    uint32_t need;         // how many of those are selected
+    uint32_t pad;
+};
+
+// Order-preserving u32 image of the selection value (+delta' for Delta > 0, -delta'
+// otherwise): larger value -> larger key.  -0 folds onto +0 (torch: -0 == +0 is a
+// tie) and NaNs onto one key above +inf (ATen's topk comparator puts NaN first).
+__device__ __forceinline__ uint32_t rez_key_of(float dp, bool up) {
+    float v = up ? dp : -dp;
+    v = v + 0.0f;
+    uint32_t u = __float_as_uint(v);
+    if (v != v) u = 0x7FC00000u;
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// k' and the key of one coordinate, exactly the reference's f32 ops (no contraction):
+// p = |x| / (L1 + 1e-12) (AS:681), mp = m * p, k' = floor(mp + 0.5) (AS:648),
+// delta' = k' - mp (AS:655).
+__device__ __forceinline__ uint32_t rez_elem(float xv, float den, float fm, bool up, float& kp) {
+    const float mp = fm * (fabsf(xv) / den);
+    kp = floorf(mp + 0.5f);
+    return rez_key_of(kp - mp, up);
+}
+
+template <int PASS> struct RadixPass;
+template <> struct RadixPass<0> { static constexpr int shift = 21; static constexpr uint32_t dmask = 0x7FF, hmask = 0u; };
+template <> struct RadixPass<1> { static constexpr int shift = 10; static constexpr uint32_t dmask = 0x7FF, hmask = 0xFFE00000u; };
+template <> struct RadixPass<2> { static constexpr int shift = 0; static constexpr uint32_t dmask = 0x3FF, hmask = 0xFFFFFC00u; };
+
+// Block-wide exclusive scan of one u32 per thread (256 threads); returns the exclusive
+// prefix, writes the total.  `lds` needs 4 u32.
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* lds, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, kWave);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) lds[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t t = lds[k];
+        base += (k < w) ? t : 0u;
+        all += t;
+    }
+    __syncthreads();
+    *total = all;
+    return base + inc - v;
+}
+
+// KB3: Delta and the selection count per client.
+__global__ void __launch_bounds__(256)
+rez_setup_kernel(const float* __restrict__ msum, float fm, int64_t d, int64_t n, RezState* __restrict__ st) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    RezState s{};
+    s.mprime = msum[i];
+    if (!(s.mprime == fm)) {                       // AS:651
+        if (!isfinite(s.mprime)) {
+            s.flags |= kRezNonFinite;
+        } else {
+            const float df = s.mprime - fm;        // AS:656 f32 subtract, int() truncates
+            const long long D = (long long)df;
+            const long long K = D > 0 ? D : -D;
+            if (K > d) {
+                s.flags |= kRezRange;
+            } else {
+                s.delta = (int32_t)D;
+                s.kleft = (uint32_t)K;
+            }
+        }
+    }
+    st[i] = s;
+}
+
+// KB4a: histogram of the PASS-th digit over keys matching the prefix.
+template <int PASS, bool VEC4>
+__global__ void __launch_bounds__(256)
+rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
+                const RezState* __restrict__ st, uint32_t* __restrict__ hist) {
+    using RP = RadixPass<PASS>;
+    const int64_t vec = blockIdx.y;
+    const uint32_t kleft = st[vec].kleft;
+    if (kleft == 0) return;
+    const uint32_t prefix = st[vec].prefix;
+    const bool up = st[vec].delta > 0;
+    __shared__ uint32_t h[kRadixBins];
+    const int tid = threadIdx.x;
+    for (int b = tid; b < kRadixBins; b += 256) h[b] = 0u;
+    __syncthreads();
+    const float den = l1[vec] + 1e-12f;
+    const float* xv = x + vec * d;
+    const int64_t b0 = (int64_t)blockIdx.x * kHistSpan;
+    auto visit = [&](float v) {
+        float kp;
+        const uint32_t key = rez_elem(v, den, fm, up, kp);
+        if ((key & RP::hmask) == prefix) atomicAdd(&h[(key >> RP::shift) & RP::dmask], 1u);
+    };
+    if (VEC4) {
+        const float4* x4 = reinterpret_cast<const float4*>(xv + b0);
+        const int64_t n4 = (std::min<int64_t>(d - b0, kHistSpan)) / 4;
+#pragma unroll 4
+        for (int j = 0; j < kHistItems / 4; ++j) {
+            const int64_t q = (int64_t)j * 256 + tid;
+            if (q < n4) {
+                const float4 t = x4[q];
+                visit(t.x); visit(t.y); visit(t.z); visit(t.w);
+            }
+        }
+    } else {
+        for (int j = 0; j < kHistItems; ++j) {
+            const int64_t i = b0 + (int64_t)j * 256 + tid;
+            if (i < d) visit(xv[i]);
+        }
+    }
+    __syncthreads();
+    uint32_t* g = hist + ((size_t)vec * 3 + PASS) * kRadixBins;
+    for (int b = tid; b < kRadixBins; b += 256)
+        if (h[b]) atomicAdd(&g[b], h[b]);
+}
+
+// KB4b: pick the digit holding the kleft-th largest key (one workgroup per client).
+template <int PASS>
+__global__ void __launch_bounds__(256)
+rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist) {
+    using RP = RadixPass<PASS>;
+    constexpr int nb = (int)RP::dmask + 1;
+    constexpr int per = nb / 256;
+    const int64_t vec = blockIdx.x;
+    const uint32_t kleft = st[vec].kleft;
+    if (kleft == 0) return;
+    __shared__ uint32_t lds[4];
+    const int tid = threadIdx.x;
+    const uint32_t* h = hist + ((size_t)vec * 3 + PASS) * kRadixBins;
+    // thread t owns bins [nb - (t+1)*per, nb - t*per): thread 0 the highest digits
+    const int hi = nb - tid * per;
+    uint32_t c[per], sum = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+        c[k] = h[hi - 1 - k];
+        sum += c[k];
+    }
+    uint32_t total;
+    uint32_t above = block_excl_scan_u32(sum, lds, &total);
+    if (above < kleft && above + sum >= kleft) {
+#pragma unroll
+        for (int k = 0; k < per; ++k) {
+            if (above + c[k] >= kleft) {
+                const uint32_t digit = (uint32_t)(hi - 1 - k);
+                RezState s = st[vec];
+                s.prefix |= digit << RP::shift;
+                s.kleft = kleft - above;
+                if (PASS == 2) {
+                    s.eq = c[k];
+                    s.need = s.kleft;
+                    if (s.eq > s.need) s.flags |= kRezAmbiguous;
+                }
+                st[vec] = s;
+                break;
+            }
+            above += c[k];
+        }
+    }
+}
+
+// KB5: keys equal to the threshold per tile (ambiguous clients only).
+template <bool VEC4>
+__global__ void __launch_bounds__(256)
+rez_tiecount_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
+                    const RezState* __restrict__ st, uint32_t* __restrict__ tilecnt, int32_t tiles) {
+    const int64_t vec = blockIdx.y;
+    if (!(st[vec].flags & kRezAmbiguous)) return;
+    const uint32_t tau = st[vec].prefix;
+    const bool up = st[vec].delta > 0;
+    const float den = l1[vec] + 1e-12f;
+    const float* xv = x + vec * d;
+    const int tid = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * kSelTile + (int64_t)tid * kSelItems;
+    uint32_t cnt = 0;
+    float kp;
+    if (VEC4 && e0 + kSelItems <= d) {
+        const float4* x4 = reinterpret_cast<const float4*>(xv + e0);
+#pragma unroll
+        for (int j = 0; j < kSelItems / 4; ++j) {
+            const float4 t = x4[j];
+            cnt += rez_elem(t.x, den, fm, up, kp) == tau;
+            cnt += rez_elem(t.y, den, fm, up, kp) == tau;
+            cnt += rez_elem(t.z, den, fm, up, kp) == tau;
+            cnt += rez_elem(t.w, den, fm, up, kp) == tau;
+        }
+    } else {
+        for (int j = 0; j < kSelItems; ++j)
+            if (e0 + j < d) cnt += rez_elem(xv[e0 + j], den, fm, up, kp) == tau;
+    }
+    __shared__ uint32_t lds[4];
+    uint32_t total;
+    (void)block_excl_scan_u32(cnt, lds, &total);
+    if (tid == 0) tilecnt[vec * tiles + blockIdx.x] = total;
+}
+
+__device__ __forceinline__ float torch_signf(float v) {
+    return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f);
+}
+
+// KB6: apply the selection and dequantize.  Selected = key > tau, or key == tau and
+// (all ties are selected | rank among ties in index order < need | marked by KB7).
+template <bool VEC4>
+__global__ void __launch_bounds__(256)
+rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, const float* __restrict__ l1,
+                  float fm, const RezState* __restrict__ st, const uint32_t* __restrict__ tilecnt, int32_t tiles,
+                  const uint32_t* __restrict__ tie_bits) {
+    const int64_t vec = blockIdx.y;
+    const RezState s = st[vec];
+    const bool on = s.kleft != 0;
+    const bool amb = on && (s.flags & kRezAmbiguous);
+    const bool replay = amb && (s.flags & kRezTorchTies);
+    const bool up = s.delta > 0;
+    const float L = l1[vec];
+    const float den = L + 1e-12f;
+    const float adj = up ? -1.f : 1.f;
+    const uint32_t tau = s.prefix;
+    const float* xv = x + vec * d;
+    float* ov = out + vec * d;
+    const int tid = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * kSelTile + (int64_t)tid * kSelItems;
+    const bool full = VEC4 && e0 + kSelItems <= d;
+    float v[kSelItems];
+    if (full) {
+        const float4* x4 = reinterpret_cast<const float4*>(xv + e0);
+#pragma unroll
+        for (int j = 0; j < kSelItems / 4; ++j) {
+            const float4 t = x4[j];
+            v[4 * j] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kSelItems; ++j) v[j] = (e0 + j < d) ? xv[e0 + j] : 0.f;
+    }
+    float kp[kSelItems];
+    uint32_t key[kSelItems];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < kSelItems; ++j) {
+        key[j] = rez_elem(v[j], den, fm, up, kp[j]);
+        cnt += (key[j] == tau && e0 + j < d);
+    }
+    uint32_t rank = 0;
+    if (amb && !replay) {              // block-uniform
+        __shared__ uint32_t lds[4];
+        __shared__ uint32_t tile_base;
+        uint32_t part = 0;
+        for (int t = tid; t < (int)blockIdx.x; t += 256) part += tilecnt[vec * tiles + t];
+        uint32_t ptot;
+        (void)block_excl_scan_u32(part, lds, &ptot);
+        if (tid == 0) tile_base = ptot;
+        uint32_t ctot;
+        rank = block_excl_scan_u32(cnt, lds, &ctot);
+        rank += tile_base;
+    }
+    // KB7's replayed set: one bit per coordinate, rows of ceil(d/32) words
+    const uint32_t* tbv = tie_bits + vec * ((d + 31) / 32);
+    float q[kSelItems];
+#pragma unroll
+    for (int j = 0; j < kSelItems; ++j) {
+        bool sel = false;
+        if (on) {
+            if (key[j] > tau) {
+                sel = true;
+            } else if (key[j] == tau) {
+                if (!amb) sel = true;
+                else if (replay) sel = (tbv[(e0 + j) >> 5] >> ((e0 + j) & 31)) & 1u;
+                else sel = (rank++ < s.need);
+            }
+        }
+        const float k2 = sel ? kp[j] + adj : kp[j];
+        q[j] = (L * torch_signf(v[j])) * (k2 / fm);      // AS:687 (L1 * signs) * (k'' / m)
+    }
+    if (full) {
+        float4* o4 = reinterpret_cast<float4*>(ov + e0);
+#pragma unroll
+        for (int j = 0; j < kSelItems / 4; ++j) o4[j] = make_float4(q[4 * j], q[4 * j + 1], q[4 * j + 2], q[4 * j + 3]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < kSelItems; ++j)
+            if (e0 + j < d) ov[e0 + j] = q[j];
+    }
+}

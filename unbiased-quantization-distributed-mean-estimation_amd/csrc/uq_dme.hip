@@ -117,16 +117,33 @@ __device__ __forceinline__ uint32_t ld_relaxed_agent32(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Element transforms summed by the K1 cascade.  The cascade itself (order of f32 adds)
+// is the torch CPU `sum` order whatever is summed.
+struct AbsOp {            // AS:624  input_vector.abs().sum()
+    float den, fm;
+    __device__ static AbsOp make(const float*, float, int64_t) { return AbsOp{0.f, 0.f}; }
+    __device__ float operator()(float v) const { return fabsf(v); }
+};
+struct RezKOp {           // AS:648-649  k' = floor(m * p + 0.5), p = |x| / (L1 + 1e-12)
+    float den, fm;
+    __device__ static RezKOp make(const float* l1, float fm, int64_t vec) {
+        return RezKOp{l1[vec] + 1e-12f, fm};
+    }
+    __device__ float operator()(float v) const { return floorf(fm * (fabsf(v) / den) + 0.5f); }
+};
+
 // =====================================================================================
-// K1a: level-1 block sums of |x| in torch cascade order.
+// K1a: level-1 block sums of op(x) in torch cascade order.
 // One workgroup = one level-1 group = step leaves x step rows x 32 streams.
 // Thread (leaf b, quad q) sums rows [b*step, (b+1)*step) of streams 4q..4q+3
 // sequentially (ATen level 0); then 32 threads add the step leaves in order (level 1).
 // =====================================================================================
-template <bool VEC4>
+template <bool VEC4, class Op>
 __global__ void __launch_bounds__(256)
-l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __restrict__ part) {
+l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __restrict__ part,
+                  const float* __restrict__ l1, float fm) {
     const int64_t vec = blockIdx.y;
+    const Op op = Op::make(l1, fm, vec);
     int32_t G = blockIdx.x;
     int c = 0;
     while (c + 1 < plan.nchunks && G >= plan.gbase[c + 1]) ++c;
@@ -151,7 +168,7 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
                 const float* pr = p + (int64_t)r * 32;
                 v0 = pr[0]; v1 = pr[1]; v2 = pr[2]; v3 = pr[3];
             }
-            a0 += fabsf(v0); a1 += fabsf(v1); a2 += fabsf(v2); a3 += fabsf(v3);
+            a0 += op(v0); a1 += op(v1); a2 += op(v2); a3 += op(v3);
         }
         float* l = leaf + b * 32 + 4 * q;
         l[0] = a0; l[1] = a1; l[2] = a2; l[3] = a3;
@@ -164,10 +181,11 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
     }
 }
 
-// Sequential sum of `nrows` rows of stream `a` starting at element `start` (|x|).
-__device__ float seq_rows(const float* __restrict__ xv, int64_t start, int64_t nrows, int a) {
+// Sequential sum of `nrows` rows of stream `a` starting at element `start`.
+template <class Op>
+__device__ float seq_rows(const Op& op, const float* __restrict__ xv, int64_t start, int64_t nrows, int a) {
     float acc = 0.f;
-    for (int64_t r = 0; r < nrows; ++r) acc += fabsf(xv[start + r * 32 + a]);
+    for (int64_t r = 0; r < nrows; ++r) acc += op(xv[start + r * 32 + a]);
     return acc;
 }
 
@@ -178,10 +196,13 @@ __device__ float seq_rows(const float* __restrict__ xv, int64_t start, int64_t n
 // then the ILP/lane/tail combination of ATen row_sum / vectorized_inner_sum, then the
 // chunk results in chunk order (torch parallel_reduce).
 // =====================================================================================
+template <class Op>
 __global__ void __launch_bounds__(64)
 l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
-                   const float* __restrict__ part, float* __restrict__ l1_out) {
+                   const float* __restrict__ part, float* __restrict__ l1_out,
+                   const float* __restrict__ l1, float fm) {
     const int64_t vec = blockIdx.x;
+    const Op op = Op::make(l1, fm, vec);
     const int lane = threadIdx.x;
     const float* xv = x + vec * d;
     __shared__ float fin[32];
@@ -194,8 +215,8 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
             // ATen scalar row_sum (ILP 4, rows < step -> all rows land in acc0).
             float p[4] = {0.f, 0.f, 0.f, 0.f};
             if (s >= 4)
-                for (int k = 0; k < 4; ++k) p[k] = 0.f + fabsf(xv[off + k]);
-            for (int64_t k = (s >= 4 ? 4 : 0); k < s; ++k) p[0] += fabsf(xv[off + k]);
+                for (int k = 0; k < 4; ++k) p[k] = 0.f + op(xv[off + k]);
+            for (int64_t k = (s >= 4 ? 4 : 0); k < s; ++k) p[0] += op(xv[off + k]);
             chunk_sum = ((p[0] + p[1]) + p[2]) + p[3];
         } else {
             const int64_t vs = s / 8, rows = vs / 4;
@@ -216,8 +237,8 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
                 for (int64_t k = ng2 * step; k < ng1; ++k) acc2 += pp[k * 32];
                 float acc1 = 0.f;
                 for (int64_t b = ng1 * step; b < nleaf; ++b)
-                    acc1 += seq_rows(xv, off + b * step * 32, step, lane);
-                float acc0 = seq_rows(xv, off + nleaf * step * 32, rows - nleaf * step, lane);
+                    acc1 += seq_rows(op, xv, off + b * step * 32, step, lane);
+                float acc0 = seq_rows(op, xv, off + nleaf * step * 32, rows - nleaf * step, lane);
                 fin[lane] = ((acc0 + acc1) + acc2) + acc3;
             }
             __syncthreads();
@@ -225,11 +246,11 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
                 float p0[8];
                 for (int l = 0; l < 8; ++l) p0[l] = fin[l];
                 for (int64_t v = rows * 4; v < vs; ++v)
-                    for (int l = 0; l < 8; ++l) p0[l] += fabsf(xv[off + v * 8 + l]);
+                    for (int l = 0; l < 8; ++l) p0[l] += op(xv[off + v * 8 + l]);
                 for (int k = 1; k < 4; ++k)
                     for (int l = 0; l < 8; ++l) p0[l] += fin[k * 8 + l];
                 float acc = 0.f;
-                for (int64_t k = vs * 8; k < s; ++k) acc += fabsf(xv[off + k]);
+                for (int64_t k = vs * 8; k < s; ++k) acc += op(xv[off + k]);
                 for (int l = 0; l < 8; ++l) acc += p0[l];
                 fin[0] = acc;
             }
@@ -874,6 +895,8 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
     }
 }
 
+#include "uq_biased_kernels.h"
+
 // ---- host-side helpers ---------------------------------------------------------------
 thread_local std::string g_err;
 
@@ -907,8 +930,9 @@ WsLayout layout(int64_t n, int64_t d, const L1Plan& plan) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-int launch_l1(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* part, float* l1_out,
-              hipStream_t st) {
+template <class Op>
+int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* part, float* sum_out,
+                   const float* l1, float fm, hipStream_t st) {
     if (plan.total_groups > 0) {
         bool vec4 = aligned16(x) && (d % 4 == 0);
         for (int c = 0; c < plan.nchunks; ++c) vec4 = vec4 && (plan.off[c] % 4 == 0);
@@ -918,14 +942,19 @@ int launch_l1(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* p
         dim3 grid(plan.total_groups, (unsigned)n);
         dim3 block(8 * maxstep);
         if (vec4)
-            hipLaunchKernelGGL(l1_partial_kernel<true>, grid, block, 0, st, x, d, plan, part);
+            hipLaunchKernelGGL((l1_partial_kernel<true, Op>), grid, block, 0, st, x, d, plan, part, l1, fm);
         else
-            hipLaunchKernelGGL(l1_partial_kernel<false>, grid, block, 0, st, x, d, plan, part);
+            hipLaunchKernelGGL((l1_partial_kernel<false, Op>), grid, block, 0, st, x, d, plan, part, l1, fm);
         int rc = hip_check(hipGetLastError(), "l1_partial_kernel launch");
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(l1_finalize_kernel, dim3((unsigned)n), dim3(64), 0, st, x, d, plan, part, l1_out);
+    hipLaunchKernelGGL(l1_finalize_kernel<Op>, dim3((unsigned)n), dim3(64), 0, st, x, d, plan, part, sum_out, l1, fm);
     return hip_check(hipGetLastError(), "l1_finalize_kernel launch");
+}
+
+int launch_l1(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* part, float* l1_out,
+              hipStream_t st) {
+    return launch_cascade<AbsOp>(x, n, d, plan, part, l1_out, nullptr, 0.f, st);
 }
 
 // Persistent grid for K2: (resident workgroups per CU) x CUs, from the occupancy API
@@ -967,6 +996,33 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
         if (ws_bytes < w->total) return fail(UQ_E_WORKSPACE, "workspace too small");
     }
     return UQ_OK;
+}
+
+// Biased-quantizer workspace: [ctrl 256][K1 parts][l1 n][m' n][state n x 32B]
+// [hist n x 3 x 2048 u32][tie counts n x tiles u32][tie bits n x ceil(d/32) u32]
+struct BiasedLayout {
+    size_t part_off, l1_off, msum_off, st_off, hist_off, tcnt_off, bits_off, total;
+    int32_t tiles;
+};
+
+BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
+    BiasedLayout w{};
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    w.tiles = (int32_t)((d + kSelTile - 1) / kSelTile);
+    w.part_off = kCtrlBytes;
+    w.l1_off = up(w.part_off + (size_t)n * plan.total_groups * 32 * sizeof(float));
+    w.msum_off = up(w.l1_off + (size_t)n * sizeof(float));
+    w.st_off = up(w.msum_off + (size_t)n * sizeof(float));
+    w.hist_off = up(w.st_off + (size_t)n * sizeof(RezState));
+    w.tcnt_off = up(w.hist_off + (size_t)n * 3 * kRadixBins * sizeof(uint32_t));
+    w.bits_off = up(w.tcnt_off + (size_t)n * w.tiles * sizeof(uint32_t));
+    w.total = up(w.bits_off + (size_t)n * ((d + 31) / 32) * sizeof(uint32_t));
+    return w;
+}
+
+int launch_torch_ties(const float*, int64_t, int64_t, const float*, float, RezState*, uint32_t*, char*,
+                      const BiasedLayout&, hipStream_t) {
+    return fail(UQ_E_INVALID, "tie_policy UQ_TIES_TORCH is not available in this build");
 }
 
 }  // namespace
@@ -1174,6 +1230,97 @@ int uq_check_status(void* ws, void* stream) {
         return fail(UQ_E_TIMEOUT, "inter-workgroup wait timed out");
     }
     return UQ_OK;
+}
+
+int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t T, size_t* bytes_out) {
+    if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
+    L1Plan plan;
+    if (n < 0 || d < 0 || T < 1 || T > kMaxChunks) return fail(UQ_E_INVALID, "bad n/d/torch_threads");
+    if (!make_plan(d, T, &plan)) return fail(UQ_E_INVALID, "cannot build L1 plan");
+    *bytes_out = biased_layout(n, d, plan).total;
+    return UQ_OK;
+}
+
+int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m, int32_t T,
+                       int32_t tie_policy, float* l1_out, int32_t* info, void* ws, size_t ws_bytes,
+                       void* stream) {
+    if (n < 0 || d < 0) return fail(UQ_E_INVALID, "n and d must be >= 0");
+    if (m < 0) return fail(UQ_E_INVALID, "m must be >= 0");
+    if (d >= ((int64_t)1 << 31)) return fail(UQ_E_INVALID, "d must be < 2^31");
+    if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 clients per call");
+    if (T < 1 || T > kMaxChunks) return fail(UQ_E_INVALID, "torch_threads must be in [1, 64]");
+    if (tie_policy != UQ_TIES_LOWEST_INDEX && tie_policy != UQ_TIES_TORCH)
+        return fail(UQ_E_INVALID, "unknown tie_policy");
+    L1Plan plan;
+    if (!make_plan(d, T, &plan)) return fail(UQ_E_INVALID, "cannot build L1 plan for this d/torch_threads");
+    const BiasedLayout w = biased_layout(n, d, plan);
+    if (n == 0) return UQ_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (d == 0) {
+        int rc = UQ_OK;
+        if (l1_out) rc = hip_check(hipMemsetAsync(l1_out, 0, n * sizeof(float), st), "memset l1");
+        if (!rc && info) rc = hip_check(hipMemsetAsync(info, 0, n * 2 * sizeof(int32_t), st), "memset info");
+        return rc;
+    }
+    if (!x || !out) return fail(UQ_E_INVALID, "null x or out");
+    if (!ws) return fail(UQ_E_INVALID, "null workspace");
+    if (ws_bytes < w.total) return fail(UQ_E_WORKSPACE, "workspace too small");
+    char* wsb = (char*)ws;
+    float* part = (float*)(wsb + w.part_off);
+    float* l1buf = (float*)(wsb + w.l1_off);
+    float* msum = (float*)(wsb + w.msum_off);
+    RezState* state = (RezState*)(wsb + w.st_off);
+    uint32_t* hist = (uint32_t*)(wsb + w.hist_off);
+    uint32_t* tcnt = (uint32_t*)(wsb + w.tcnt_off);
+    uint32_t* bits = (uint32_t*)(wsb + w.bits_off);
+    const float fm = (float)m;
+    int rc = launch_l1(x, n, d, plan, part, l1buf, st);                                   // AS:680
+    if (rc) return rc;
+    rc = launch_cascade<RezKOp>(x, n, d, plan, part, msum, l1buf, fm, st);               // AS:648-649
+    if (rc) return rc;
+    hipLaunchKernelGGL(rez_setup_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, msum, fm, d, n, state);
+    rc = hip_check(hipGetLastError(), "rez_setup_kernel launch");
+    if (rc) return rc;
+    rc = hip_check(hipMemsetAsync(hist, 0, (size_t)n * 3 * kRadixBins * sizeof(uint32_t), st), "memset hist");
+    if (rc) return rc;
+    const bool vec4 = aligned16(x) && aligned16(out) && d % 4 == 0;
+    const dim3 hgrid((unsigned)((d + kHistSpan - 1) / kHistSpan), (unsigned)n);
+    const dim3 tgrid((unsigned)w.tiles, (unsigned)n);
+#define UQ_RADIX(P)                                                                                          \
+    if (vec4)                                                                                                \
+        hipLaunchKernelGGL((rez_hist_kernel<P, true>), hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist); \
+    else                                                                                                     \
+        hipLaunchKernelGGL((rez_hist_kernel<P, false>), hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist); \
+    hipLaunchKernelGGL(rez_select_kernel<P>, dim3((unsigned)n), dim3(256), 0, st, state, hist);
+    UQ_RADIX(0) UQ_RADIX(1) UQ_RADIX(2)
+#undef UQ_RADIX
+    rc = hip_check(hipGetLastError(), "radix select launch");
+    if (rc) return rc;
+    if (tie_policy == UQ_TIES_TORCH) {
+        rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, st);
+        if (rc) return rc;
+    } else {
+        if (vec4)
+            hipLaunchKernelGGL(rez_tiecount_kernel<true>, tgrid, dim3(256), 0, st, x, d, l1buf, fm, state, tcnt, w.tiles);
+        else
+            hipLaunchKernelGGL(rez_tiecount_kernel<false>, tgrid, dim3(256), 0, st, x, d, l1buf, fm, state, tcnt, w.tiles);
+        rc = hip_check(hipGetLastError(), "rez_tiecount_kernel launch");
+        if (rc) return rc;
+    }
+    if (vec4)
+        hipLaunchKernelGGL(rez_output_kernel<true>, tgrid, dim3(256), 0, st, x, out, d, l1buf, fm, state, tcnt, w.tiles, bits);
+    else
+        hipLaunchKernelGGL(rez_output_kernel<false>, tgrid, dim3(256), 0, st, x, out, d, l1buf, fm, state, tcnt, w.tiles, bits);
+    rc = hip_check(hipGetLastError(), "rez_output_kernel launch");
+    if (rc) return rc;
+    if (l1_out) {
+        rc = hip_check(hipMemcpyAsync(l1_out, l1buf, n * sizeof(float), hipMemcpyDeviceToDevice, st), "copy l1");
+        if (rc) return rc;
+    }
+    if (info)
+        rc = hip_check(hipMemcpy2DAsync(info, 2 * sizeof(int32_t), state, sizeof(RezState), 2 * sizeof(int32_t), n,
+                                        hipMemcpyDeviceToDevice, st), "copy info");
+    return rc;
 }
 
 }  // extern "C"
