@@ -110,3 +110,82 @@ def test_drop_in_semantics(uq):
     assert y.is_cuda and y.dtype == torch.float32 and y.shape == (1000,)
     assert uq.Type_biased_quantize.__name__ == "Type_biased_quantize"
     assert uq.Type_biased_quantize(torch.empty(0), 1).numel() == 0
+
+
+def test_fixtures_torch_ties_bit_exact(uq, cases):
+    """ties='torch' (the default, KB7 replaying libstdc++'s nth_element / partial_sort):
+    bit-exact with the reference on every fixture, ambiguous ties included."""
+    bad, replayed = [], 0
+    for sp, x, q, h in cases:
+        if sp.get("raises"):
+            continue
+        out, info = run(uq, x, sp["R"], sp["threads"], "torch")
+        replayed += bool(info[1] & 8)
+        assert bool(info[1] & 8) == sp["ambiguous"], sp["idx"]
+        ok = G.bits_equal(out, q) if q is not None else G.sha(out) == h
+        if not ok:
+            bad.append(sp["idx"])
+    uq.check_status()
+    assert not bad, f"GPU differs from the reference on fixtures {bad}"
+    assert replayed >= 50
+
+
+def _heap_cases():
+    """Tie-heavy vectors whose topk takes partial_sort (k * 64 <= d) with a tie at the threshold."""
+    out = []
+    for d, scale, R in ((5000, 8, 8), (5000, 16, 2), (20000, 2, 8), (20000, 16, 4), (100000, 8, 2),
+                        (100000, 16, 8)):
+        x = (np.round(np.random.default_rng(d * 100 + scale + R).standard_normal(d) * scale) / scale).astype(f32)
+        out.append((x, R))
+    return out
+
+
+def test_torch_ties_heap_and_select_paths(uq):
+    hits = {"heap": 0, "nth": 0}
+    for x, R in _heap_cases():
+        d = x.shape[0]
+        m = rate_to_m(R, d)
+        exp, _, D, A = C.biased_quantize(x, m, 1, 0)
+        out, info = run(uq, x, R, 1, "torch")
+        assert info[0] == D
+        assert G.bits_equal(out, exp), (d, R)
+        if A:
+            hits["heap" if abs(D) * 64 <= d else "nth"] += 1
+    uq.check_status()
+    assert hits["heap"] >= 2, hits
+
+
+def test_torch_ties_many_clients(uq):
+    """More ambiguous clients than KB7 slots (64): workgroups loop over clients."""
+    rng = np.random.default_rng(21)
+    n, d = 150, 6007
+    x = rng.integers(-3, 4, (n, d)).astype(f32)
+    x[1::3] = rng.standard_normal((len(range(1, n, 3)), d)).astype(f32)     # some unambiguous rows
+    for R in (1, 4):
+        m = rate_to_m(R, d)
+        out, info = uq.biased_quantize(torch.as_tensor(x).cuda(), m=m, torch_threads=1, ties="torch",
+                                       return_info=True)
+        out = out.cpu().numpy()
+        info = info.cpu().numpy()
+        for j in range(n):
+            exp, _, D, A = C.biased_quantize(x[j], m, 1, 0)
+            assert info[j, 0] == D and bool(info[j, 1] & 1) == A, j
+            assert G.bits_equal(out[j], exp), (R, j)
+    uq.check_status()
+
+
+def test_drop_in_matches_reference_fixtures(uq, cases):
+    """The drop-in itself (1-D, torch ties) on the small fixtures, incl. the raising ones."""
+    for sp, x, q, h in cases:
+        if x.shape[0] > 8192 or sp["threads"] != 1:
+            continue
+        uq.set_torch_threads(1)
+        try:
+            if sp.get("raises"):
+                with pytest.raises(RuntimeError):
+                    uq.Type_biased_quantize(torch.as_tensor(x), sp["R"])
+                continue
+            y = uq.Type_biased_quantize(torch.as_tensor(x), sp["R"]).cpu().numpy()
+        finally:
+            uq.set_torch_threads(None)
+        assert G.bits_equal(y, q), sp["idx"]

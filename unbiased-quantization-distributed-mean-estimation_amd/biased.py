@@ -24,7 +24,7 @@ import torch
 
 from . import _lib
 from .quantizer import (_as_device_f32_2d, _device, _ptr, _resolve_m, _stream_ptr, _workspace,
-                        get_torch_threads)
+                        check_status, get_torch_threads)
 from .rates import RATE_TABLE
 
 __all__ = ["Type_biased_quantize", "biased_quantize", "TIES_TORCH", "TIES_LOWEST_INDEX",
@@ -98,6 +98,7 @@ def Type_biased_quantize(input_vector, bits_per_dimension=1):
         return v
     out, info = biased_quantize(v.view(1, d), m=m, ties="torch", return_info=True)
     flags = int(info[0, 1].item())
+    check_status()
     if flags & FLAG_NONFINITE:
         raise ValueError("cannot convert float NaN to integer (m' is not finite, AS:656)")
     if flags & FLAG_RANGE:

@@ -212,7 +212,8 @@ __global__ void __launch_bounds__(256)
 rez_tiecount_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
                     const RezState* __restrict__ st, uint32_t* __restrict__ tilecnt, int32_t tiles) {
     const int64_t vec = blockIdx.y;
-    if (!(st[vec].flags & kRezAmbiguous)) return;
+    const int32_t fl = st[vec].flags;
+    if (!(fl & kRezAmbiguous) || (fl & kRezTorchTies)) return;
     const uint32_t tau = st[vec].prefix;
     const bool up = st[vec].delta > 0;
     const float den = l1[vec] + 1e-12f;

@@ -896,6 +896,7 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
 }
 
 #include "uq_biased_kernels.h"
+#include "uq_biased_torch_ties.h"
 
 // ---- host-side helpers ---------------------------------------------------------------
 thread_local std::string g_err;
@@ -1000,9 +1001,11 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
 
 // Biased-quantizer workspace: [ctrl 256][K1 parts][l1 n][m' n][state n x 32B]
 // [hist n x 3 x 2048 u32][tie counts n x tiles u32][tie bits n x ceil(d/32) u32]
+// [KB7 slots: pairs S x d u64][KB7 positions S x 2d u32], S = min(n, kTieSlots)
 struct BiasedLayout {
-    size_t part_off, l1_off, msum_off, st_off, hist_off, tcnt_off, bits_off, total;
+    size_t part_off, l1_off, msum_off, st_off, hist_off, tcnt_off, bits_off, pairs_off, pos_off, total;
     int32_t tiles;
+    int32_t slots;
 };
 
 BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
@@ -1016,13 +1019,20 @@ BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.hist_off = up(w.st_off + (size_t)n * sizeof(RezState));
     w.tcnt_off = up(w.hist_off + (size_t)n * 3 * kRadixBins * sizeof(uint32_t));
     w.bits_off = up(w.tcnt_off + (size_t)n * w.tiles * sizeof(uint32_t));
-    w.total = up(w.bits_off + (size_t)n * ((d + 31) / 32) * sizeof(uint32_t));
+    w.slots = (int32_t)std::min<int64_t>(n, kTieSlots);
+    w.pairs_off = up(w.bits_off + (size_t)n * ((d + 31) / 32) * sizeof(uint32_t));
+    w.pos_off = up(w.pairs_off + (size_t)w.slots * d * sizeof(uint64_t));
+    w.total = up(w.pos_off + (size_t)w.slots * 2 * d * sizeof(uint32_t));
     return w;
 }
 
-int launch_torch_ties(const float*, int64_t, int64_t, const float*, float, RezState*, uint32_t*, char*,
-                      const BiasedLayout&, hipStream_t) {
-    return fail(UQ_E_INVALID, "tie_policy UQ_TIES_TORCH is not available in this build");
+int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, float fm, RezState* state,
+                      uint32_t* bits, char* wsb, const BiasedLayout& w, hipStream_t st) {
+    int rc = hip_check(hipMemsetAsync(bits, 0, (size_t)n * ((d + 31) / 32) * sizeof(uint32_t), st), "memset tie bits");
+    if (rc) return rc;
+    hipLaunchKernelGGL(rez_ties_kernel, dim3((unsigned)w.slots), dim3(256), 0, st, x, d, l1, fm, state, bits,
+                       (uint64_t*)(wsb + w.pairs_off), (uint32_t*)(wsb + w.pos_off), n, (uint32_t*)wsb);
+    return hip_check(hipGetLastError(), "rez_ties_kernel launch");
 }
 
 }  // namespace
@@ -1227,6 +1237,7 @@ int uq_check_status(void* ws, void* stream) {
     if (status) {
         (void)hipMemsetAsync((char*)ws + 8, 0, 4, st);
         (void)hipStreamSynchronize(st);
+        if (status == 2) return fail(UQ_E_TIMEOUT, "torch tie replay inconsistent (internal error)");
         return fail(UQ_E_TIMEOUT, "inter-workgroup wait timed out");
     }
     return UQ_OK;
@@ -1299,14 +1310,14 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     if (tie_policy == UQ_TIES_TORCH) {
         rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, st);
         if (rc) return rc;
-    } else {
-        if (vec4)
-            hipLaunchKernelGGL(rez_tiecount_kernel<true>, tgrid, dim3(256), 0, st, x, d, l1buf, fm, state, tcnt, w.tiles);
-        else
-            hipLaunchKernelGGL(rez_tiecount_kernel<false>, tgrid, dim3(256), 0, st, x, d, l1buf, fm, state, tcnt, w.tiles);
-        rc = hip_check(hipGetLastError(), "rez_tiecount_kernel launch");
-        if (rc) return rc;
     }
+    // index-order tie ranks (used by ambiguous clients that KB7 did not replay)
+    if (vec4)
+        hipLaunchKernelGGL(rez_tiecount_kernel<true>, tgrid, dim3(256), 0, st, x, d, l1buf, fm, state, tcnt, w.tiles);
+    else
+        hipLaunchKernelGGL(rez_tiecount_kernel<false>, tgrid, dim3(256), 0, st, x, d, l1buf, fm, state, tcnt, w.tiles);
+    rc = hip_check(hipGetLastError(), "rez_tiecount_kernel launch");
+    if (rc) return rc;
     if (vec4)
         hipLaunchKernelGGL(rez_output_kernel<true>, tgrid, dim3(256), 0, st, x, out, d, l1buf, fm, state, tcnt, w.tiles, bits);
     else
