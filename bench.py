@@ -198,6 +198,7 @@ def main():
                 ms = time_pipeline(pl, max(3, args.steps // 2))
                 side[pl] = {"ms_per_step": round(ms, 4), "value": round(n_total / ms / 1e3, 6)}
         _lib.check(lib.uq_check_status(P(ws), sp), "status after side pipelines")
+        side["biased"] = time_biased(uqdme, x, q, args.bits, T, max(3, args.steps // 2))
         if int(torch.count_nonzero(ovf > 127)):
             raise RuntimeError("type-code overflow in the bench workload")
 
@@ -227,6 +228,25 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def time_biased(uqdme, x, q, bits, T, steps):
+    """Side line: the biased type quantizer (AS:669-687, torch tie policy) on the same
+    resident batch, one uq_type_biased_f32 call per step (x -> q)."""
+    n, d = x.shape
+    m = uqdme.rate_to_m(bits, d)
+    for _ in range(2):
+        uqdme.biased_quantize(x, m=m, torch_threads=T, ties="torch", out=q)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        uqdme.biased_quantize(x, m=m, torch_threads=T, ties="torch", out=q)
+    e1.record()
+    torch.cuda.synchronize()
+    uqdme.check_status()
+    ms = e0.elapsed_time(e1) / steps
+    return {"ms_per_step": round(ms, 4), "value": round(n / ms / 1e3, 6), "what": "Type_biased_quantize batch, no mean"}
 
 
 def ctypes_size(lib, n, d, T):

@@ -37,7 +37,9 @@ def hipcc() -> str:
 def needs_build() -> bool:
     if not os.path.exists(SO):
         return True
-    src_m = max(os.path.getmtime(SRC), os.path.getmtime(os.path.join(PKG_DIR, "..", "include", "uq_dme.h")))
+    deps = [os.path.join(PKG_DIR, "csrc", f) for f in os.listdir(os.path.join(PKG_DIR, "csrc"))]
+    deps.append(os.path.join(PKG_DIR, "..", "include", "uq_dme.h"))
+    src_m = max(os.path.getmtime(f) for f in deps)
     return os.path.getmtime(SO) < src_m
 
 

@@ -20,63 +20,102 @@
 //     that beats the heap top replaces it (pop_heap).  Sequential by nature; one wave
 //     skips 64 non-candidates per ballot, lane 0 runs the heap moves.
 // The heap routines restate libstdc++'s __make_heap / __adjust_heap / __push_heap.
-// Each workgroup owns one scratch slot (pairs[d] + two position lists) and walks the
-// clients blockIdx.x, +gridDim.x, ...; clients without an ambiguous tie are skipped.
+// Each workgroup owns one scratch slot (keys[d], indices[d] = the queue in SoA form, plus
+// two position lists) and walks the clients blockIdx.x, +gridDim.x, ...; clients without
+// an ambiguous tie are skipped.  Ranges of <= kTieLdsPairs finish in LDS.
 
-constexpr int kTieSlots = 64;        // workgroups (and scratch slots) of KB7
-constexpr int kTieItems = 16;        // pairs per thread per partition chunk
-constexpr int kTieChunk = 256 * kTieItems;
+constexpr int kTieSlots = 256;       // workgroups (and scratch slots) of KB7: one per CU
+constexpr int kTieThreads = 1024;    // 16 waves per client
+constexpr int kTieWaves = kTieThreads / kWave;
+constexpr int kTieU = 8;             // independent loads in flight per lane
+constexpr int kTieLdsPairs = 4096;   // ranges this short finish in LDS
+
+#ifdef UQ_TIE_PROF
+// phase timers (wall_clock64 ticks, 100 MHz) accumulated by thread 0 into g_tie_prof[]:
+// 0 fill, 1 stop lists, 2 search, 3 swaps, 4 pivot, 5 lds phase, 6 mark, 7 levels (count)
+__device__ uint64_t* g_tie_prof;
+#define TT_DECL() uint64_t _tt0 = 0; (void)_tt0
+#define TT_T0() _tt0 = wall_clock64()
+#define TT_ACC(k) do { if (threadIdx.x == 0 && g_tie_prof) { uint64_t _t = wall_clock64(); atomicAdd((unsigned long long*)&g_tie_prof[k], (unsigned long long)(_t - _tt0)); _tt0 = _t; } } while (0)
+#else
+#define TT_DECL() do {} while (0)
+#define TT_T0() do {} while (0)
+#define TT_ACC(k) do {} while (0)
+#endif
+
+struct TieShared {
+    uint32_t wl[kTieWaves], wr[kTieWaves];   // per-wave stop counts of one partition
+    int64_t first, last;
+    int depth;
+    uint32_t piv;
+    uint32_t marked;
+};
+
+// The (value, index) queue in SoA form; element i = (K[i], I[i]).  The same code runs on
+// the global slot and on the LDS copy of a short range.
+struct Queue {
+    uint32_t* K;
+    uint32_t* I;
+    __device__ uint32_t key(int64_t i) const { return K[i]; }
+    __device__ uint64_t get(int64_t i) const { return ((uint64_t)K[i] << 32) | I[i]; }
+    __device__ void set(int64_t i, uint64_t v) const { K[i] = (uint32_t)(v >> 32); I[i] = (uint32_t)v; }
+    __device__ void swap(int64_t a, int64_t b) const {
+        const uint32_t ka = K[a], ia = I[a];
+        K[a] = K[b]; I[a] = I[b];
+        K[b] = ka; I[b] = ia;
+    }
+};
 
 __device__ __forceinline__ uint32_t pkey(uint64_t p) { return (uint32_t)(p >> 32); }
 
-__device__ void tt_adjust_heap(uint64_t* A, int64_t f, int64_t hole, int64_t len, uint64_t value) {
+__device__ void tt_adjust_heap(const Queue& A, int64_t f, int64_t hole, int64_t len, uint64_t value) {
     const int64_t top = hole;
     int64_t second = hole;
     while (second < (len - 1) / 2) {
         second = 2 * (second + 1);
-        if (pkey(A[f + second]) > pkey(A[f + second - 1])) second--;
-        A[f + hole] = A[f + second];
+        if (A.key(f + second) > A.key(f + second - 1)) second--;
+        A.set(f + hole, A.get(f + second));
         hole = second;
     }
     if ((len & 1) == 0 && second == (len - 2) / 2) {
         second = 2 * (second + 1);
-        A[f + hole] = A[f + second - 1];
+        A.set(f + hole, A.get(f + second - 1));
         hole = second - 1;
     }
     int64_t parent = (hole - 1) / 2;
-    while (hole > top && pkey(A[f + parent]) > pkey(value)) {
-        A[f + hole] = A[f + parent];
+    while (hole > top && A.key(f + parent) > pkey(value)) {
+        A.set(f + hole, A.get(f + parent));
         hole = parent;
         parent = (hole - 1) / 2;
     }
-    A[f + hole] = value;
+    A.set(f + hole, value);
 }
 
-__device__ void tt_make_heap(uint64_t* A, int64_t f, int64_t len) {
+__device__ void tt_make_heap(const Queue& A, int64_t f, int64_t len) {
     if (len < 2) return;
     for (int64_t parent = (len - 2) / 2;; --parent) {
-        tt_adjust_heap(A, f, parent, len, A[f + parent]);
+        tt_adjust_heap(A, f, parent, len, A.get(f + parent));
         if (parent == 0) break;
     }
 }
 
 // heap_select(A + f, A + m, A + l) by one wave (lanes 0..63 of the caller).
-__device__ void tt_heap_select_wave(uint64_t* A, int64_t f, int64_t m, int64_t l, int lane) {
+__device__ void tt_heap_select_wave(const Queue& A, int64_t f, int64_t m, int64_t l, int lane) {
     if (lane == 0) tt_make_heap(A, f, m - f);
-    uint32_t top = __shfl(lane == 0 ? pkey(A[f]) : 0u, 0, kWave);
+    uint32_t top = __shfl(lane == 0 ? A.key(f) : 0u, 0, kWave);
     for (int64_t base = m; base < l; base += kWave) {
         const int64_t i = base + lane;
-        const uint32_t ki = i < l ? pkey(A[i]) : 0u;
         const bool cand = i < l;
+        const uint32_t ki = cand ? A.key(i) : 0u;
         uint64_t mask = __ballot(cand && ki > top);
         while (mask) {
             const int j = __builtin_ctzll(mask);
             uint32_t nt = 0;
             if (lane == 0) {                       // pop_heap(f, m, base + j)
-                const uint64_t v = A[base + j];
-                A[base + j] = A[f];
+                const uint64_t v = A.get(base + j);
+                A.set(base + j, A.get(f));
                 tt_adjust_heap(A, f, 0, m - f, v);
-                nt = pkey(A[f]);
+                nt = A.key(f);
             }
             top = __shfl(nt, 0, kWave);
             const uint64_t later = (j == 63) ? 0ull : (~0ull << (j + 1));
@@ -85,37 +124,31 @@ __device__ void tt_heap_select_wave(uint64_t* A, int64_t f, int64_t m, int64_t l
     }
 }
 
-__device__ __forceinline__ void tt_swap(uint64_t* A, int64_t a, int64_t b) {
-    const uint64_t t = A[a];
-    A[a] = A[b];
-    A[b] = t;
-}
-
-__device__ void tt_move_median_to_first(uint64_t* A, int64_t r, int64_t a, int64_t b, int64_t c) {
-    const uint32_t ka = pkey(A[a]), kb = pkey(A[b]), kc = pkey(A[c]);
+__device__ void tt_move_median_to_first(const Queue& A, int64_t r, int64_t a, int64_t b, int64_t c) {
+    const uint32_t ka = A.key(a), kb = A.key(b), kc = A.key(c);
     if (ka > kb) {
-        if (kb > kc) tt_swap(A, r, b);
-        else if (ka > kc) tt_swap(A, r, c);
-        else tt_swap(A, r, a);
-    } else if (ka > kc) tt_swap(A, r, a);
-    else if (kb > kc) tt_swap(A, r, c);
-    else tt_swap(A, r, b);
+        if (kb > kc) A.swap(r, b);
+        else if (ka > kc) A.swap(r, c);
+        else A.swap(r, a);
+    } else if (ka > kc) A.swap(r, a);
+    else if (kb > kc) A.swap(r, c);
+    else A.swap(r, b);
 }
 
-__device__ void tt_insertion_sort(uint64_t* A, int64_t f, int64_t l) {
+__device__ void tt_insertion_sort(const Queue& A, int64_t f, int64_t l) {
     if (f == l) return;
     for (int64_t i = f + 1; i != l; ++i) {
-        const uint64_t v = A[i];
-        if (pkey(v) > pkey(A[f])) {
-            for (int64_t j = i; j > f; --j) A[j] = A[j - 1];
-            A[f] = v;
+        const uint64_t v = A.get(i);
+        if (pkey(v) > A.key(f)) {
+            for (int64_t j = i; j > f; --j) A.set(j, A.get(j - 1));
+            A.set(f, v);
         } else {
             int64_t j = i;
-            while (pkey(v) > pkey(A[j - 1])) {
-                A[j] = A[j - 1];
+            while (pkey(v) > A.key(j - 1)) {
+                A.set(j, A.get(j - 1));
                 --j;
             }
-            A[j] = v;
+            A.set(j, v);
         }
     }
 }
@@ -126,108 +159,210 @@ __device__ __forceinline__ int floor_log2_i64(int64_t n) {
     return r;
 }
 
-// std::nth_element(A, A + nth, A + d) by the whole workgroup.  Returns false on an
-// internal inconsistency (never expected; reported through the status word).
-__device__ bool tt_introselect(uint64_t* A, uint32_t* Lpos, uint32_t* Rpos, int64_t d, int64_t nth) {
-    __shared__ int64_t s_first, s_last, s_cut, s_J;
-    __shared__ int s_depth, s_bad;
-    __shared__ uint32_t s_piv;
-    __shared__ uint32_t lds[4];
-    const int tid = threadIdx.x;
-    if (tid == 0) {
-        s_first = 0;
-        s_last = d;
-        s_depth = 2 * floor_log2_i64(d);
-        s_bad = 0;
+// Stops of [s0, s1) (one wave's segment) in index order: FN(i, left, right) per element,
+// lanes own i = b + u*64 + lane, kTieU loads in flight.
+template <class FN>
+__device__ __forceinline__ void tt_scan_segment(const Queue& A, int64_t first, int64_t s0, int64_t s1, uint32_t piv,
+                                                int lane, FN&& fn) {
+    for (int64_t b = s0; b < s1; b += (int64_t)kWave * kTieU) {
+        uint32_t k[kTieU];
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int64_t i = b + (int64_t)u * kWave + lane;
+            k[u] = i < s1 ? A.key(i) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int64_t i = b + (int64_t)u * kWave + lane;
+            const bool valid = i < s1;
+            fn(i, valid && i > first && k[u] <= piv,      // left stop:  !comp(A[i], pivot)
+               valid && k[u] >= piv);                     // right stop: !comp(pivot, A[i])
+        }
+    }
+}
+
+// One unguarded Hoare partition of [first+1, last) around the pivot at `first` (indices
+// relative to the queue view; positions listed as PosT).  Each wave lists the stops of
+// its contiguous segment: one counting pass, a 16-entry prefix, one listing pass.
+// Returns the cut, or -1 on an internal inconsistency.
+template <typename PosT>
+__device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t first, int64_t last,
+                                uint32_t piv, TieShared& sh) {
+    TT_DECL();
+    TT_T0();
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int64_t seg = (((last - first) + kTieWaves - 1) / kTieWaves + kWave - 1) & ~(int64_t)(kWave - 1);
+    const int64_t s0 = std::min<int64_t>(last, first + (int64_t)w * seg);
+    const int64_t s1 = std::min<int64_t>(last, s0 + seg);
+    uint32_t cl = 0, cr = 0;
+    tt_scan_segment(A, first, s0, s1, piv, lane, [&](int64_t, bool lf, bool rf) {
+        cl += (uint32_t)__popcll(__ballot(lf));
+        cr += (uint32_t)__popcll(__ballot(rf));
+    });
+    if (lane == 0) {
+        sh.wl[w] = cl;
+        sh.wr[w] = cr;
     }
     __syncthreads();
-    for (;;) {
-        const int64_t first = s_first, last = s_last;
-        const int depth = s_depth;
-        if (last - first <= 3) break;
-        if (depth == 0) {                                   // introselect's heap fallback
-            if (tid < kWave) tt_heap_select_wave(A, first, nth + 1, last, tid);
-            __syncthreads();
-            if (tid == 0) tt_swap(A, first, nth);
-            __syncthreads();
-            return true;
+    uint32_t ol = 0, orr = 0, nL = 0, nR = 0;
+#pragma unroll
+    for (int q = 0; q < kTieWaves; ++q) {
+        const uint32_t a = sh.wl[q], b = sh.wr[q];
+        ol += q < w ? a : 0u;
+        orr += q < w ? b : 0u;
+        nL += a;
+        nR += b;
+    }
+    tt_scan_segment(A, first, s0, s1, piv, lane, [&](int64_t i, bool lf, bool rf) {
+        const uint64_t ml = __ballot(lf), mr = __ballot(rf);
+        if (lf) Lpos[ol + __popcll(ml & lt)] = (PosT)i;
+        if (rf) Rpos[orr + __popcll(mr & lt)] = (PosT)i;
+        ol += (uint32_t)__popcll(ml);
+        orr += (uint32_t)__popcll(mr);
+    });
+    __syncthreads();
+    TT_ACC(1);
+    // J = number of swaps = largest J with L_J < R_J (1-based; R counted from the right),
+    // found by a block-parallel search (the predicate holds for a prefix of J).
+    int64_t lo = 0, hi = nL < nR ? nL : nR;
+    while (lo < hi) {
+        const int64_t step = (hi - lo + kTieThreads - 1) / kTieThreads;
+        const int64_t cand = lo + (int64_t)(tid + 1) * step;
+        const bool f = cand <= hi && (int64_t)Lpos[cand - 1] < (int64_t)Rpos[nR - cand];
+        const int cnt = __syncthreads_count(f);
+        if (cnt == 0) {
+            hi = lo + step - 1;
+        } else {
+            lo = lo + (int64_t)cnt * step;
+            hi = std::min<int64_t>(hi, lo + step - 1);
         }
+    }
+    TT_ACC(2);
+    const int64_t J = lo;
+    int64_t cut = INT64_MAX;
+    if (J < (int64_t)nL) cut = (int64_t)Lpos[J];
+    if (J > 0) cut = std::min<int64_t>(cut, (int64_t)Rpos[nR - J]);
+    // the J swaps are disjoint pairs: kTieU of them per lane, independent loads
+    for (int64_t j0 = 0; j0 < J; j0 += (int64_t)kTieThreads * kTieU) {
+        int64_t a[kTieU], b[kTieU];
+        uint32_t ka[kTieU], kb[kTieU], ia[kTieU], ib[kTieU];
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int64_t j = j0 + (int64_t)u * kTieThreads + tid;
+            a[u] = j < J ? (int64_t)Lpos[j] : -1;
+            b[u] = j < J ? (int64_t)Rpos[nR - 1 - j] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u)
+            if (a[u] >= 0) {
+                ka[u] = A.K[a[u]]; ia[u] = A.I[a[u]];
+                kb[u] = A.K[b[u]]; ib[u] = A.I[b[u]];
+            }
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u)
+            if (a[u] >= 0) {
+                A.K[a[u]] = kb[u]; A.I[a[u]] = ib[u];
+                A.K[b[u]] = ka[u]; A.I[b[u]] = ia[u];
+            }
+    }
+    __syncthreads();
+    TT_ACC(3);
+#ifdef UQ_TIE_PROF
+    if (threadIdx.x == 0 && g_tie_prof) atomicAdd((unsigned long long*)&g_tie_prof[7], 1ull);
+#endif
+    return (cut <= first || cut >= last) ? -1 : cut;
+}
+
+// introselect's main loop on the queue view (element i of the vector at view index i - o)
+// while the range is longer than `stop`.  Returns 0 (range now <= stop), 1 (finished
+// through the heap fallback) or -1 (internal inconsistency).
+template <typename PosT>
+__device__ int tt_select_loop(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t o, int64_t nth, int64_t stop,
+                              TieShared& sh) {
+    TT_DECL();
+    const int tid = threadIdx.x;
+    for (;;) {
+        const int64_t first = sh.first - o, last = sh.last - o;
+        const int depth = sh.depth;
+        if (last - first <= stop) return 0;
+        if (depth == 0) {                                   // heap_select(first, nth+1, last)
+            if (tid < kWave) tt_heap_select_wave(A, first, nth - o + 1, last, tid);
+            __syncthreads();
+            if (tid == 0) A.swap(first, nth - o);
+            __syncthreads();
+            return 1;
+        }
+        __syncthreads();
+        TT_T0();
         if (tid == 0) {
             const int64_t mid = first + (last - first) / 2;
             tt_move_median_to_first(A, first, first + 1, mid, last - 1);
-            s_piv = pkey(A[first]);
+            sh.piv = A.key(first);
         }
         __syncthreads();
-        const uint32_t piv = s_piv;
-        // stops of both scans in index order, positions listed in Lpos / Rpos
-        uint32_t nL = 0, nR = 0;
-        for (int64_t c0 = first; c0 < last; c0 += kTieChunk) {
-            const int64_t i0 = c0 + (int64_t)tid * kTieItems;
-            uint32_t flags = 0, cl = 0, cr = 0;
-#pragma unroll
-            for (int j = 0; j < kTieItems; ++j) {
-                const int64_t i = i0 + j;
-                if (i < last) {
-                    const uint32_t k = pkey(A[i]);
-                    const bool lf = i > first && k <= piv;      // !comp(A[i], pivot)
-                    const bool rf = k >= piv;                   // !comp(pivot, A[i])
-                    flags |= (lf ? 1u : 0u) << j;
-                    flags |= (rf ? 1u : 0u) << (16 + j);
-                    cl += lf;
-                    cr += rf;
-                }
-            }
-            uint32_t tot;
-            const uint32_t ex = block_excl_scan_u32(cl | (cr << 16), lds, &tot);
-            uint32_t pl = nL + (ex & 0xFFFFu), pr = nR + (ex >> 16);
-#pragma unroll
-            for (int j = 0; j < kTieItems; ++j) {
-                if (flags & (1u << j)) Lpos[pl++] = (uint32_t)(i0 + j);
-                if (flags & (1u << (16 + j))) Rpos[pr++] = (uint32_t)(i0 + j);
-            }
-            nL += tot & 0xFFFFu;
-            nR += tot >> 16;
-        }
-        __syncthreads();
+        TT_ACC(4);
+        const int64_t cut = tt_partition<PosT>(A, Lpos, Rpos, first, last, sh.piv, sh);
+        if (cut < 0) return -1;
         if (tid == 0) {
-            // J = number of swaps: largest J with L_J < R_J (1-based; R counted from the right)
-            int64_t lo = 0, hi = nL < nR ? nL : nR;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi + 1) / 2;
-                if (Lpos[mid - 1] < Rpos[nR - mid]) lo = mid; else hi = mid - 1;
-            }
-            int64_t cut = INT64_MAX;
-            if (lo < (int64_t)nL) cut = Lpos[lo];
-            if (lo > 0) cut = std::min<int64_t>(cut, Rpos[nR - lo]);
-            if (cut <= first || cut >= last) s_bad = 1;
-            s_J = lo;
-            s_cut = cut;
-        }
-        __syncthreads();
-        if (s_bad) return false;
-        const int64_t J = s_J;
-        for (int64_t j = tid; j < J; j += 256) tt_swap(A, Lpos[j], Rpos[nR - 1 - j]);
-        __syncthreads();
-        if (tid == 0) {
-            if (s_cut <= nth) s_first = s_cut; else s_last = s_cut;
-            s_depth = depth - 1;
+            if (cut + o <= nth) sh.first = cut + o; else sh.last = cut + o;
+            sh.depth = depth - 1;
         }
         __syncthreads();
     }
-    if (tid == 0) tt_insertion_sort(A, s_first, s_last);
+}
+
+// std::nth_element(A, A + nth, A + d) by the whole workgroup (false on an inconsistency).
+__device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, int64_t d, int64_t nth,
+                               TieShared& sh, uint32_t* lK, uint32_t* lI, uint16_t* lL, uint16_t* lR) {
+    TT_DECL();
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        sh.first = 0;
+        sh.last = d;
+        sh.depth = 2 * floor_log2_i64(d);
+    }
+    __syncthreads();
+    int r = tt_select_loop<uint32_t>(A, Lpos, Rpos, 0, nth, kTieLdsPairs, sh);
+    if (r < 0) return false;
+    TT_T0();
+    if (r == 0 && sh.last - sh.first > 3) {                // finish the short range in LDS
+        const int64_t f0 = sh.first, len = sh.last - sh.first;
+        for (int64_t i = tid; i < len; i += kTieThreads) {
+            lK[i] = A.K[f0 + i];
+            lI[i] = A.I[f0 + i];
+        }
+        __syncthreads();
+        const Queue L{lK, lI};
+        r = tt_select_loop<uint16_t>(L, lL, lR, f0, nth, 3, sh);
+        __syncthreads();
+        for (int64_t i = tid; i < len; i += kTieThreads) {
+            A.K[f0 + i] = lK[i];
+            A.I[f0 + i] = lI[i];
+        }
+        __syncthreads();
+        if (r < 0) return false;
+    }
+    TT_ACC(5);
+    if (r == 0 && tid == 0) tt_insertion_sort(A, sh.first, sh.last);
     __syncthreads();
     return true;
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kTieThreads)
 rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
-                RezState* __restrict__ st, uint32_t* __restrict__ tie_bits, uint64_t* __restrict__ pairs,
+                RezState* __restrict__ st, uint32_t* __restrict__ tie_bits, uint32_t* __restrict__ qbuf,
                 uint32_t* __restrict__ pos, int64_t n, uint32_t* __restrict__ ctrl) {
-    uint64_t* A = pairs + (size_t)blockIdx.x * d;
+    TT_DECL();
+    const int64_t dpad = (d + 3) & ~(int64_t)3;              // 16-byte aligned K and I rows
+    const Queue A{qbuf + (size_t)blockIdx.x * 2 * dpad, qbuf + (size_t)blockIdx.x * 2 * dpad + dpad};
     uint32_t* Lpos = pos + (size_t)blockIdx.x * 2 * d;
     uint32_t* Rpos = Lpos + d;
     const int tid = threadIdx.x;
-    __shared__ uint32_t s_marked;
+    __shared__ TieShared sh;
+    __shared__ __attribute__((aligned(16))) uint32_t lK[kTieLdsPairs + 4];
+    __shared__ uint32_t lI[kTieLdsPairs];
+    __shared__ uint16_t lL[kTieLdsPairs], lR[kTieLdsPairs];
     for (int64_t vec = blockIdx.x; vec < n; vec += gridDim.x) {
         const RezState s = st[vec];
         if (s.kleft == 0 || !(s.flags & kRezAmbiguous)) continue;
@@ -235,35 +370,83 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         const int64_t k = up ? s.delta : -(int64_t)s.delta;
         const float den = l1[vec] + 1e-12f;
         const float* xv = x + vec * d;
-        for (int64_t i = tid; i < d; i += 256) {           // queue[j] = (value, j) (TopKImpl.h)
-            float kp;
-            A[i] = ((uint64_t)rez_elem(xv[i], den, fm, up, kp) << 32) | (uint64_t)i;
+        TT_T0();
+        // queue[j] = (value, j) (TopKImpl.h); 4 coordinates per lane and load
+        const bool xv4 = ((uintptr_t)xv & 15u) == 0;
+        for (int64_t i0 = 0; i0 < d; i0 += (int64_t)kTieThreads * 4 * kTieU) {
+            float4 v[kTieU];
+#pragma unroll
+            for (int u = 0; u < kTieU; ++u) {
+                const int64_t i = i0 + 4 * ((int64_t)u * kTieThreads + tid);
+                if (xv4 && i + 3 < d) {
+                    v[u] = *reinterpret_cast<const float4*>(xv + i);
+                } else {
+                    v[u].x = i < d ? xv[i] : 0.f;
+                    v[u].y = i + 1 < d ? xv[i + 1] : 0.f;
+                    v[u].z = i + 2 < d ? xv[i + 2] : 0.f;
+                    v[u].w = i + 3 < d ? xv[i + 3] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kTieU; ++u) {
+                const int64_t i = i0 + 4 * ((int64_t)u * kTieThreads + tid);
+                if (i >= d) continue;
+                float kp;
+                uint4 kk, ii;
+                kk.x = rez_elem(v[u].x, den, fm, up, kp);
+                kk.y = rez_elem(v[u].y, den, fm, up, kp);
+                kk.z = rez_elem(v[u].z, den, fm, up, kp);
+                kk.w = rez_elem(v[u].w, den, fm, up, kp);
+                ii = make_uint4((uint32_t)i, (uint32_t)i + 1, (uint32_t)i + 2, (uint32_t)i + 3);
+                if (i + 3 < d) {
+                    *reinterpret_cast<uint4*>(A.K + i) = kk;
+                    *reinterpret_cast<uint4*>(A.I + i) = ii;
+                } else {
+                    const uint32_t ka[4] = {kk.x, kk.y, kk.z, kk.w};
+                    for (int c = 0; i + c < d; ++c) {
+                        A.K[i + c] = ka[c];
+                        A.I[i + c] = (uint32_t)(i + c);
+                    }
+                }
+            }
         }
-        if (tid == 0) s_marked = 0;
+        if (tid == 0) sh.marked = 0;
         __syncthreads();
+        TT_ACC(0);
         bool ok = true;
         if (k * 64 <= d) {                                  // std::partial_sort's selection
             if (tid < kWave) tt_heap_select_wave(A, 0, k, d, tid);
             __syncthreads();
         } else {                                            // std::nth_element
-            ok = tt_introselect(A, Lpos, Rpos, d, k - 1);
+            ok = tt_introselect(A, Lpos, Rpos, d, k - 1, sh, lK, lI, lL, lR);
         }
         uint32_t* bits = tie_bits + vec * ((d + 31) / 32);
+        TT_T0();
         if (ok) {
             uint32_t mine = 0;
-            for (int64_t p = tid; p < k; p += 256) {
-                const uint64_t e = A[p];
-                if (pkey(e) == s.prefix) {
-                    const uint32_t idx = (uint32_t)e;
-                    atomicOr(&bits[idx >> 5], 1u << (idx & 31));
-                    ++mine;
+            for (int64_t p0 = 0; p0 < k; p0 += (int64_t)kTieThreads * kTieU) {
+                uint32_t kk[kTieU], ii[kTieU];
+#pragma unroll
+                for (int u = 0; u < kTieU; ++u) {
+                    const int64_t p = p0 + (int64_t)u * kTieThreads + tid;
+                    kk[u] = p < k ? A.K[p] : 0u;
+                    ii[u] = p < k ? A.I[p] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < kTieU; ++u) {
+                    const int64_t p = p0 + (int64_t)u * kTieThreads + tid;
+                    if (p < k && kk[u] == s.prefix) {
+                        atomicOr(&bits[ii[u] >> 5], 1u << (ii[u] & 31));
+                        ++mine;
+                    }
                 }
             }
-            atomicAdd(&s_marked, mine);
+            if (mine) atomicAdd(&sh.marked, mine);
         }
         __syncthreads();
+        TT_ACC(6);
         if (tid == 0) {
-            if (ok && s_marked == s.need) {
+            if (ok && sh.marked == s.need) {
                 st[vec].flags = s.flags | kRezTorchTies;
             } else {
                 __hip_atomic_store(ctrl + 2, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -1001,7 +1001,7 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
 
 // Biased-quantizer workspace: [ctrl 256][K1 parts][l1 n][m' n][state n x 32B]
 // [hist n x 3 x 2048 u32][tie counts n x tiles u32][tie bits n x ceil(d/32) u32]
-// [KB7 slots: pairs S x d u64][KB7 positions S x 2d u32], S = min(n, kTieSlots)
+// [KB7 slots: keys + indices S x 2d u32][KB7 positions S x 2d u32], S = min(n, kTieSlots)
 struct BiasedLayout {
     size_t part_off, l1_off, msum_off, st_off, hist_off, tcnt_off, bits_off, pairs_off, pos_off, total;
     int32_t tiles;
@@ -1021,7 +1021,7 @@ BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.bits_off = up(w.tcnt_off + (size_t)n * w.tiles * sizeof(uint32_t));
     w.slots = (int32_t)std::min<int64_t>(n, kTieSlots);
     w.pairs_off = up(w.bits_off + (size_t)n * ((d + 31) / 32) * sizeof(uint32_t));
-    w.pos_off = up(w.pairs_off + (size_t)w.slots * d * sizeof(uint64_t));
+    w.pos_off = up(w.pairs_off + (size_t)w.slots * 2 * ((d + 3) & ~(int64_t)3) * sizeof(uint32_t) + 16);
     w.total = up(w.pos_off + (size_t)w.slots * 2 * d * sizeof(uint32_t));
     return w;
 }
@@ -1030,8 +1030,8 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
                       uint32_t* bits, char* wsb, const BiasedLayout& w, hipStream_t st) {
     int rc = hip_check(hipMemsetAsync(bits, 0, (size_t)n * ((d + 31) / 32) * sizeof(uint32_t), st), "memset tie bits");
     if (rc) return rc;
-    hipLaunchKernelGGL(rez_ties_kernel, dim3((unsigned)w.slots), dim3(256), 0, st, x, d, l1, fm, state, bits,
-                       (uint64_t*)(wsb + w.pairs_off), (uint32_t*)(wsb + w.pos_off), n, (uint32_t*)wsb);
+    hipLaunchKernelGGL(rez_ties_kernel, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm, state, bits,
+                       (uint32_t*)(wsb + w.pairs_off), (uint32_t*)(wsb + w.pos_off), n, (uint32_t*)wsb);
     return hip_check(hipGetLastError(), "rez_ties_kernel launch");
 }
 
@@ -1242,6 +1242,12 @@ int uq_check_status(void* ws, void* stream) {
     }
     return UQ_OK;
 }
+
+#ifdef UQ_TIE_PROF
+int uq_debug_set_tie_prof(void* dev_counters) {
+    return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_tie_prof), &dev_counters, sizeof(void*)), "set tie prof");
+}
+#endif
 
 int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t T, size_t* bytes_out) {
     if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
