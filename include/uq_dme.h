@@ -131,6 +131,32 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
                        int32_t torch_threads, int32_t tie_policy, float* l1_out, int32_t* info,
                        void* ws, size_t ws_bytes, void* stream);
 
+/* ---- EDEN with the randomized Hadamard transform (baseline) -------
+ * NMSE_Results/Codes/All_Schemes.py:95-153 (RHT), :324-413 (EdenSender / EdenReceiver),
+ * :792-811 (EDEN_quantize_Hadamard).  D = dim rounded up to a power of two.
+ *
+ * uq_rht_signs: the RHT diagonal of AS:117-120 for each seed: signs[r][i] = +-1 (int8) as
+ *   2 * torch.bernoulli(1/2, generator seeded with seeds[r]) - 1 on torch's CPU generator
+ *   (MT19937).  Callers cache rows per (seed, D); seeds is a device int32 [rows].
+ * uq_eden_compress_f32: bins [n][D] u8 and scale [n] f32 of EdenSender.compress for integer
+ *   nbits (1 or 2, the tables the reference defines); client j uses diagonal row
+ *   sign_row[j] (device int32 [n]).  Rotation, norm (torch CPU order) and bins are
+ *   bit-identical to the reference; scale's dot product is accumulated in fp64 (the
+ *   reference's MKL sdot order is CPU-dependent): scale within 1e-6 relative.
+ * uq_eden_decompress_f32: out [n][dim] = scale * RHT^-1(centroids[bins])[:dim].
+ * uq_eden_f32: both (EDEN_quantize_Hadamard for a batch); scale_out [n] or NULL.
+ * Workspace: uq_eden_workspace_bytes. */
+int uq_rht_signs(const int32_t* seeds, int64_t rows, int64_t D, int8_t* signs, void* stream);
+int uq_eden_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out);
+int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
+                         const int32_t* sign_row, uint8_t* bins, float* scale, void* ws, size_t ws_bytes,
+                         void* stream);
+int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, int64_t dim, int32_t nbits,
+                           const int8_t* signs, const int32_t* sign_row, float* out, void* ws, size_t ws_bytes,
+                           void* stream);
+int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
+                const int32_t* sign_row, float* scale_out, void* ws, size_t ws_bytes, void* stream);
+
 /* After the stream has been synchronised: UQ_OK, or UQ_E_TIMEOUT if any
  * inter-workgroup wait in a previous call on this workspace gave up. Clears it. */
 int uq_check_status(void* ws, void* stream);

@@ -99,3 +99,15 @@ def n_mismatch(a, b) -> int:
     na, nb = np.isnan(a), np.isnan(b)
     bad = (na != nb) | (~na & ~nb & (a.view(np.uint32) != b.view(np.uint32)))
     return int(bad.sum())
+
+
+def eden():
+    """EDEN fixtures (make_golden_eden.py): (meta dict, npz)."""
+    z = np.load(os.path.join(GOLDEN, "eden_vectors.npz"))
+    meta = json.load(open(os.path.join(GOLDEN, "eden_vectors.json")))
+    return meta, z
+
+
+def eden_input(case, z):
+    i = case["idx"]
+    return z[f"x{i}"] if f"x{i}" in z.files else spec_gen(case)

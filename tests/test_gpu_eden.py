@@ -1,0 +1,82 @@
+"""GPU parity of EDEN + RHT (AS:95-153, 324-413, 792-811) through the C-ABI: diagonal and
+bins bit-exact with the reference fixtures, scale / outputs within 1e-6 relative (the
+reference's MKL dot order), and bit-exact with the oracle wherever the fp64 dot rounds to
+the same f32 scale."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import uq_eden as E
+from tests import golden_data as G
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def uq(gpu_ready):
+    import uqdme
+    return uqdme
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return G.eden()
+
+
+def test_rht_signs_known_answers(uq, fx):
+    meta, z = fx
+    for dg in meta["diag"]:
+        got = uq.rht_signs([dg["seed"]], dg["D"]).cpu().numpy()[0]
+        assert np.array_equal(got, z[f"diag_{dg['seed']}_{dg['D']}"]), dg
+
+
+def test_eden_vs_reference_fixtures(uq, fx):
+    meta, z = fx
+    for case in meta["cases"]:
+        x = torch.as_tensor(G.eden_input(case, z)).cuda().view(1, -1)
+        msg = uq.eden_compress(x, case["nbits"], seeds=[case["rseed"]])
+        bins = msg.bins.cpu().numpy()[0]
+        assert bins.shape[0] == case["D"]
+        assert G.sha(bins) == case["bins_sha"], case["idx"]
+        sc = float(msg.scale.cpu()[0])
+        assert abs(sc - case["scale"]) <= RTOL * abs(case["scale"]), case["idx"]
+        out = uq.eden_decompress(msg).cpu().numpy()[0]
+        full = uq.eden_quantize(x, case["nbits"], seeds=[case["rseed"]]).cpu().numpy()[0]
+        assert G.bits_equal(out, full)
+        i = case["idx"]
+        if f"out{i}" in z.files:
+            np.testing.assert_allclose(out, z[f"out{i}"], rtol=RTOL, atol=0)
+        else:
+            np.testing.assert_allclose(out[z[f"pos{i}"]], z[f"outs{i}"], rtol=RTOL, atol=0)
+
+
+def test_eden_batch_vs_oracle(uq):
+    rng = np.random.default_rng(3)
+    n, d = 12, 3000
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    seeds = [0, 5, 99, 5, 1234, 7, 0, 42, 64, 99, 3, 100]     # repeats and seeds outside 0..99
+    for nbits in (1, 2):
+        out, scale = uq.eden_quantize(torch.as_tensor(x).cuda(), nbits, seeds=seeds, return_scale=True)
+        out = out.cpu().numpy()
+        scale = scale.cpu().numpy()
+        for j in range(n):
+            bins, sc, _, _ = E.eden_compress(x[j], nbits, seeds[j])
+            assert abs(float(scale[j]) - float(sc)) <= 2 * np.spacing(np.float32(abs(sc))), j
+            exp = E.eden_decompress(bins, scale[j], nbits, seeds[j], d)     # same scale -> bit-exact
+            assert G.bits_equal(out[j], exp), (nbits, j)
+
+
+def test_drop_in(uq, fx):
+    meta, z = fx
+    for dd in meta["dropin"]:
+        x = z[f"dx{dd['tseed']}_{dd['nbits']}"]
+        torch.manual_seed(dd["tseed"])
+        y = uq.EDEN_quantize_Hadamard(torch.as_tensor(x), dd["nbits"])
+        assert isinstance(y, np.ndarray) and y.dtype == np.float32 and y.shape == x.shape
+        np.testing.assert_allclose(y, z[f"dout{dd['tseed']}_{dd['nbits']}"], rtol=RTOL, atol=0)
+        # exactly one randint(0, 100) draw was consumed
+        torch.manual_seed(dd["tseed"])
+        assert int(torch.randint(0, 100, (1,))) == dd["drawn_seed"]
+    with pytest.raises(ValueError):
+        uq.EDEN_quantize_Hadamard(torch.randn(64), 3)

@@ -14,6 +14,7 @@ from .quantizer import (
 )
 from .codes import TypeCodes
 from .biased import Type_biased_quantize, biased_quantize
+from .eden import EDEN_quantize_Hadamard, eden_quantize, eden_compress, eden_decompress, EdenMessage, rht_signs
 from ._lib import UQError, load as load_library, library_path
 from .distributed import shard_range, sharded_client_mean, sharded_quantize_mean
 from .dme import DISTRIBUTIONS, nmse_simulation
@@ -23,5 +24,6 @@ __all__ = [
     "quantize_mean", "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
     "check_status", "UQError", "load_library", "library_path", "shard_range", "sharded_client_mean",
     "sharded_quantize_mean", "DISTRIBUTIONS", "nmse_simulation", "quantize_encode", "decode", "codes_mean",
-    "TypeCodes", "Type_biased_quantize", "biased_quantize",
+    "TypeCodes", "Type_biased_quantize", "biased_quantize", "EDEN_quantize_Hadamard", "eden_quantize",
+    "eden_compress", "eden_decompress", "EdenMessage", "rht_signs",
 ]

@@ -897,6 +897,7 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
 
 #include "uq_biased_kernels.h"
 #include "uq_biased_torch_ties.h"
+#include "uq_eden_kernels.h"
 
 // ---- host-side helpers ---------------------------------------------------------------
 thread_local std::string g_err;
@@ -1024,6 +1025,90 @@ BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.pos_off = up(w.pairs_off + (size_t)w.slots * 2 * ((d + 3) & ~(int64_t)3) * sizeof(uint32_t) + 16);
     w.total = up(w.pos_off + (size_t)w.slots * 2 * d * sizeof(uint32_t));
     return w;
+}
+
+// ---- EDEN host helpers ------------------------------------------------------------------
+bool eden_tables(int nbits, EdenTables* t) {
+    // AS:302-315: centroids (-c reversed, c) as f32; boundaries = midpoints of neighbours
+    std::memset(t, 0, sizeof(*t));
+    double pos[2];
+    int np = 0;
+    if (nbits == 1) { pos[0] = 0.7978845608028654; np = 1; }
+    else if (nbits == 2) { pos[0] = 0.4527800398860679; pos[1] = 1.5104176087114887; np = 2; }
+    else return false;
+    double c[4];
+    for (int i = 0; i < np; ++i) { c[i] = -pos[np - 1 - i]; c[np + i] = pos[i]; }
+    for (int i = 0; i < 2 * np; ++i) t->c[i] = (float)c[i];
+    // the reference forms the midpoints from the f32 tensor elements, in double, then
+    // stores them as f32 (torch.Tensor of Python floats)
+    for (int i = 0; i + 1 < 2 * np; ++i) t->b[i] = (float)(((double)t->c[i] + (double)t->c[i + 1]) / 2.0);
+    t->nb = 2 * np - 1;
+    return true;
+}
+
+int ilog2_pow2(int64_t D) {
+    int p = 0;
+    while (((int64_t)1 << p) < D) ++p;
+    return p;
+}
+
+struct EdenLayout {
+    size_t vec_off, nrm_off, part_off, bins_off, scale_off, total;
+    int64_t D;
+    int32_t tiles;
+};
+
+EdenLayout eden_layout(int64_t n, int64_t dim) {
+    EdenLayout w{};
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    w.D = dim <= 1 ? 1 : ((int64_t)1 << ilog2_pow2(dim));
+    w.tiles = (int32_t)((w.D + kEdenTile - 1) / kEdenTile);
+    w.vec_off = kCtrlBytes;
+    w.nrm_off = up(w.vec_off + (size_t)n * w.D * sizeof(float));
+    w.part_off = up(w.nrm_off + (size_t)n * sizeof(float));
+    w.bins_off = up(w.part_off + (size_t)n * w.tiles * sizeof(double));
+    w.scale_off = up(w.bins_off + (size_t)n * w.D);
+    w.total = up(w.scale_off + (size_t)n * sizeof(float));
+    return w;
+}
+
+// Runs the FWHT passes of one transform.  MODE of the first pass: 1 sender, 2 receiver.
+int launch_fwht(FwhtArgs a, int64_t n, bool receiver, float* buf, float* out, hipStream_t st) {
+    const int p = ilog2_pow2(a.D);
+    int lo = 0, k = std::min(p, kFwhtLowBits);
+    bool first = true;
+    for (;;) {
+        const bool last = lo + k >= p;
+        const int cols = lo == 0 ? 1 : kFwhtCols;
+        const int64_t tiles = a.D / (((int64_t)1 << k) * cols);
+        FwhtArgs b = a;
+        b.out = (last && receiver) ? out : buf;
+        if (!first) b.in = buf;
+        const dim3 grid((unsigned)tiles, (unsigned)n);
+#define UQ_FWHT(M, L, R) hipLaunchKernelGGL((fwht_pass_kernel<M, L, R>), grid, dim3(kFwhtT), 0, st, b, lo, k)
+        if (first && !receiver) { if (last) UQ_FWHT(1, true, false); else UQ_FWHT(1, false, false); }
+        else if (first && receiver) { if (last) UQ_FWHT(2, true, true); else UQ_FWHT(2, false, false); }
+        else if (last && receiver) UQ_FWHT(0, true, true);
+        else if (last) UQ_FWHT(0, true, false);
+        else UQ_FWHT(0, false, false);
+#undef UQ_FWHT
+        int rc = hip_check(hipGetLastError(), "fwht_pass_kernel launch");
+        if (rc) return rc;
+        if (last) break;
+        first = false;
+        lo += k;
+        k = std::min(p - lo, kFwhtHighBits);
+    }
+    return UQ_OK;
+}
+
+int eden_check(int64_t n, int64_t dim, int32_t nbits, const int8_t* signs, EdenTables* tab) {
+    if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
+    if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 clients per call");
+    if (dim > ((int64_t)1 << 28)) return fail(UQ_E_INVALID, "dim must be <= 2^28");
+    if (!eden_tables(nbits, tab)) return fail(UQ_E_INVALID, "EDEN nbits must be 1 or 2 (the reference's tables)");
+    if (n > 0 && dim > 0 && !signs) return fail(UQ_E_INVALID, "null signs");
+    return UQ_OK;
 }
 
 int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, float fm, RezState* state,
@@ -1338,6 +1423,92 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         rc = hip_check(hipMemcpy2DAsync(info, 2 * sizeof(int32_t), state, sizeof(RezState), 2 * sizeof(int32_t), n,
                                         hipMemcpyDeviceToDevice, st), "copy info");
     return rc;
+}
+
+// ---- EDEN + RHT ------------------------------------------------------------------------
+int uq_rht_signs(const int32_t* seeds, int64_t rows, int64_t D, int8_t* signs, void* stream) {
+    if (rows < 0 || D < 0) return fail(UQ_E_INVALID, "rows and D must be >= 0");
+    if (rows == 0 || D == 0) return UQ_OK;
+    if (rows > 65535) return fail(UQ_E_INVALID, "at most 65535 rows per call");
+    if (!seeds || !signs) return fail(UQ_E_INVALID, "null pointer");
+    hipLaunchKernelGGL(rht_signs_kernel, dim3((unsigned)rows), dim3(640), 0, (hipStream_t)stream, seeds, D, signs);
+    return hip_check(hipGetLastError(), "rht_signs_kernel launch");
+}
+
+int uq_eden_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
+    if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
+    if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
+    *bytes_out = eden_layout(n, dim).total;
+    return UQ_OK;
+}
+
+int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
+                         const int32_t* sign_row, uint8_t* bins, float* scale, void* ws, size_t ws_bytes,
+                         void* stream) {
+    EdenTables tab;
+    int rc = eden_check(n, dim, nbits, signs, &tab);
+    if (rc) return rc;
+    if (n == 0 || dim == 0) return UQ_OK;
+    if (!x || !bins || !scale) return fail(UQ_E_INVALID, "null pointer");
+    const EdenLayout w = eden_layout(n, dim);
+    if (!ws || ws_bytes < w.total) return fail(UQ_E_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* wsb = (char*)ws;
+    float* vec = (float*)(wsb + w.vec_off);
+    float* nrm = (float*)(wsb + w.nrm_off);
+    double* part = (double*)(wsb + w.part_off);
+    FwhtArgs a{};
+    a.in = x;
+    a.signs = signs;
+    a.sign_row = sign_row;
+    a.D = w.D;
+    a.dim = dim;
+    a.sqrtD = (float)std::sqrt((double)w.D);                 // np.sqrt(d) -> f32 operand
+    a.tab = tab;
+    rc = launch_fwht(a, n, false, vec, nullptr, st);                               // AS:123-141
+    if (rc) return rc;
+    hipLaunchKernelGGL(eden_norm_kernel, dim3((unsigned)((n + 7) / 8)), dim3(64), 0, st, vec, n, w.D, nrm);
+    rc = hip_check(hipGetLastError(), "eden_norm_kernel launch");                  // AS:329 torch.norm
+    if (rc) return rc;
+    hipLaunchKernelGGL(eden_bins_kernel, dim3((unsigned)w.tiles, (unsigned)n), dim3(256), 0, st, vec, w.D, a.sqrtD,
+                       nrm, tab, bins, part, w.tiles);
+    rc = hip_check(hipGetLastError(), "eden_bins_kernel launch");                  // AS:329-335
+    if (rc) return rc;
+    hipLaunchKernelGGL(eden_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, w.tiles, nrm, n,
+                       scale);
+    return hip_check(hipGetLastError(), "eden_scale_kernel launch");
+}
+
+int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, int64_t dim, int32_t nbits,
+                           const int8_t* signs, const int32_t* sign_row, float* out, void* ws, size_t ws_bytes,
+                           void* stream) {
+    EdenTables tab;
+    int rc = eden_check(n, dim, nbits, signs, &tab);
+    if (rc) return rc;
+    if (n == 0 || dim == 0) return UQ_OK;
+    if (!bins || !scale || !out) return fail(UQ_E_INVALID, "null pointer");
+    const EdenLayout w = eden_layout(n, dim);
+    if (!ws || ws_bytes < w.total) return fail(UQ_E_WORKSPACE, "workspace too small");
+    FwhtArgs a{};
+    a.in = bins;
+    a.signs = signs;
+    a.sign_row = sign_row;
+    a.scale = scale;
+    a.D = w.D;
+    a.dim = dim;
+    a.sqrtD = (float)std::sqrt((double)w.D);
+    a.tab = tab;
+    return launch_fwht(a, n, true, (float*)((char*)ws + w.vec_off), out, (hipStream_t)stream);   // AS:378-413
+}
+
+int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
+                const int32_t* sign_row, float* scale_out, void* ws, size_t ws_bytes, void* stream) {
+    const EdenLayout w = eden_layout(n < 0 ? 0 : n, dim < 0 ? 0 : dim);
+    uint8_t* bins = (uint8_t*)((char*)ws + w.bins_off);
+    float* scale = scale_out ? scale_out : (float*)((char*)ws + w.scale_off);
+    int rc = uq_eden_compress_f32(x, n, dim, nbits, signs, sign_row, bins, scale, ws, ws_bytes, stream);
+    if (rc) return rc;
+    return uq_eden_decompress_f32(bins, scale, n, dim, nbits, signs, sign_row, out, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

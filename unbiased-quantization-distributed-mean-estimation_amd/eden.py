@@ -1,0 +1,162 @@
+"""EDEN with the randomized Hadamard transform on the GPU — SURVEY §8(f) row 2 (baseline).
+
+Drop-in:
+    EDEN_quantize_Hadamard(input_vector, bits_per_dimension=1)
+        == NMSE_Results/Codes/All_Schemes.py:792-811: one torch.randint(0, 100) draw of the
+        global CPU generator per call (the rotation seed, AS:797), EdenSender.compress then
+        EdenReceiver.decompress, returns a NumPy f32 array of length d (AS:811).
+
+Batched:
+    eden_quantize(x[n, d], bits, seeds[n])              -> out[n, d]
+    eden_compress(x[n, d], bits, seeds[n])              -> EdenMessage(bins u8 [n, D], scale[n], seeds, d)
+    eden_decompress(msg)                                -> out[n, d]
+
+Numerics: rotation (MT19937 diagonal, f32 butterflies a+b / (a+b)-2b, / f32(sqrt(D))), the
+norm (torch CPU order) and the bins are bit-identical to the reference; the scale's dot
+product is accumulated in fp64 because the reference's (MKL sdot) order is CPU-dependent,
+so outputs agree to 1e-6 relative.  Only the 1- and 2-bit tables exist in the reference.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from .quantizer import _as_device_f32_2d, _device, _ptr, _stream_ptr, _workspace
+
+__all__ = ["EDEN_quantize_Hadamard", "eden_quantize", "eden_compress", "eden_decompress", "EdenMessage",
+           "rht_signs", "padded_dim"]
+
+_SEEDS = 100                       # AS:797 torch.randint(0, 100)
+_cache_lock = threading.Lock()
+_sign_cache: dict = {}
+
+
+def padded_dim(d: int) -> int:
+    """AS:128 / AS:359: the next power of two (d itself when it is one)."""
+    return 1 if d <= 1 else 1 << (int(d) - 1).bit_length()
+
+
+def rht_signs(seeds, D: int, device=None) -> torch.Tensor:
+    """int8 [len(seeds), D] RHT diagonals (AS:117-120) generated on the GPU."""
+    dev = device or _device()
+    s = torch.as_tensor(seeds, dtype=torch.int32).reshape(-1).to(dev)
+    out = torch.empty((s.numel(), D), dtype=torch.int8, device=dev)
+    _lib.check(_lib.load().uq_rht_signs(_ptr(s), s.numel(), D, _ptr(out), _stream_ptr(dev)), "uq_rht_signs")
+    return out
+
+
+def _sign_rows(seeds: torch.Tensor, D: int, dev):
+    """(table, row index per client).  Seeds 0..99 (the reference's range) share one cached
+    table per (device, D); other seeds get rows generated for this call."""
+    seeds_cpu = seeds.to("cpu", torch.int64)
+    if bool(((seeds_cpu >= 0) & (seeds_cpu < _SEEDS)).all()):
+        key = (dev.index, D)
+        with _cache_lock:
+            tab = _sign_cache.get(key)
+            if tab is None:
+                tab = rht_signs(torch.arange(_SEEDS), D, dev)
+                _sign_cache[key] = tab
+        return tab, seeds_cpu.to(torch.int32).to(dev)
+    uniq, inv = torch.unique(seeds_cpu, return_inverse=True)
+    return rht_signs(uniq, D, dev), inv.to(torch.int32).to(dev)
+
+
+def _ws(n, d, dev):
+    b = ctypes.c_size_t(0)
+    _lib.check(_lib.load().uq_eden_workspace_bytes(n, d, ctypes.byref(b)), "uq_eden_workspace_bytes")
+    return _workspace(dev, int(b.value))
+
+
+def _seeds(seeds, n, generator=None):
+    if seeds is None:
+        return torch.randint(0, _SEEDS, (n,), generator=generator)     # n successive AS:797 draws
+    s = torch.as_tensor(seeds, dtype=torch.int64).reshape(-1)
+    if s.numel() != n:
+        raise ValueError("one seed per row")
+    return s
+
+
+def _bits(bits):
+    if bits not in (1, 2):
+        raise ValueError("EDEN supports 1 and 2 bits (the reference's centroid tables, AS:302-306)")
+    return int(bits)
+
+
+@dataclass
+class EdenMessage:
+    bins: torch.Tensor      # u8 [n, D]
+    scale: torch.Tensor     # f32 [n]
+    seeds: torch.Tensor     # int64 [n] (rotation seeds)
+    nbits: int
+    dim: int
+
+
+def eden_compress(x, bits_per_dimension=1, seeds=None, *, generator=None) -> EdenMessage:
+    """EdenSender.compress (AS:355-376) for every row of x [n, d]."""
+    dev = _device()
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    nb = _bits(bits_per_dimension)
+    s = _seeds(seeds, n, generator)
+    D = padded_dim(d)
+    bins = torch.empty((n, D), dtype=torch.uint8, device=dev)
+    scale = torch.empty(n, dtype=torch.float32, device=dev)
+    if n and d:
+        tab, rows = _sign_rows(s, D, dev)
+        ws = _ws(n, d, dev)
+        _lib.check(_lib.load().uq_eden_compress_f32(_ptr(x), n, d, nb, _ptr(tab), _ptr(rows), _ptr(bins), _ptr(scale),
+                                                    _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_eden_compress_f32")
+    return EdenMessage(bins=bins, scale=scale, seeds=s, nbits=nb, dim=d)
+
+
+def eden_decompress(msg: EdenMessage) -> torch.Tensor:
+    """EdenReceiver.decompress (AS:383-413) for every row."""
+    dev = _device()
+    bins = msg.bins.to(dev).contiguous()
+    scale = msg.scale.to(device=dev, dtype=torch.float32).contiguous()
+    n = bins.shape[0]
+    d = msg.dim
+    out = torch.empty((n, d), dtype=torch.float32, device=dev)
+    if n and d:
+        tab, rows = _sign_rows(torch.as_tensor(msg.seeds), bins.shape[1], dev)
+        ws = _ws(n, d, dev)
+        _lib.check(_lib.load().uq_eden_decompress_f32(_ptr(bins), _ptr(scale), n, d, msg.nbits, _ptr(tab), _ptr(rows),
+                                                      _ptr(out), _ptr(ws), ws.numel(), _stream_ptr(dev)),
+                   "uq_eden_decompress_f32")
+    return out
+
+
+def eden_quantize(x, bits_per_dimension=1, seeds=None, *, return_scale: bool = False, generator=None):
+    """EDEN_quantize_Hadamard for every row of x [n, d] (rotation seed per row)."""
+    dev = _device()
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    nb = _bits(bits_per_dimension)
+    s = _seeds(seeds, n, generator)
+    out = torch.empty((n, d), dtype=torch.float32, device=dev)
+    scale = torch.empty(n, dtype=torch.float32, device=dev)
+    if n and d:
+        tab, rows = _sign_rows(s, padded_dim(d), dev)
+        ws = _ws(n, d, dev)
+        _lib.check(_lib.load().uq_eden_f32(_ptr(x), _ptr(out), n, d, nb, _ptr(tab), _ptr(rows), _ptr(scale), _ptr(ws),
+                                           ws.numel(), _stream_ptr(dev)), "uq_eden_f32")
+    return (out, scale) if return_scale else out
+
+
+def EDEN_quantize_Hadamard(input_vector, bits_per_dimension=1):
+    """Drop-in for AS:792 (same name for the drivers' result keys).  Draws the rotation
+    seed from torch's global CPU generator like the CPU reference (AS:797) and returns a
+    NumPy f32 array (AS:811)."""
+    dev = _device()
+    if torch.is_tensor(input_vector):
+        v = input_vector.detach().to(device=dev, dtype=torch.float32).reshape(-1)
+    else:
+        v = torch.tensor(np.asarray(input_vector), dtype=torch.float32, device=dev).reshape(-1)
+    seed = int(torch.randint(0, _SEEDS, (1,)).item())
+    out = eden_quantize(v.view(1, -1), bits_per_dimension, seeds=[seed])
+    return out.view(-1).cpu().numpy()
