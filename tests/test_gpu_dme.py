@@ -65,3 +65,23 @@ def test_sharded_mean_single_rank_nccl(uq):
             assert torch.equal(est, ref), mode
     finally:
         dist.destroy_process_group()
+
+
+def test_multi_scheme_nmse_known_answers(gpu_ready):
+    """EDEN 1/2, unbiased 1/2 and biased 1/2 in the driver's call order against the
+    reference's own loop (tests/golden/nd_nmse_schemes.json): within 1e-6 relative."""
+    import json
+    import os
+    import uqdme
+    from tests.golden_data import GOLDEN
+    ref = json.load(open(os.path.join(GOLDEN, "nd_nmse_schemes.json")))
+    for dist, rows in ref["rows"].items():
+        res = uqdme.nmse_simulation(dist, dim=ref["dim"], users=(1, 6), num_instances=2,
+                                    schemes=("eden", "unbiased", "biased"), torch_threads=1)
+        for row in rows:
+            ui = (1, 6).index(row["n"])
+            for sc in ("eden", "unbiased", "biased"):
+                for r in (1, 2):
+                    got = float(res[(sc, r)]["script"][ui, row["inst"]])
+                    exp = row[f"{sc}{r}"]
+                    assert abs(got - exp) <= 1e-6 * exp, (dist, row["n"], row["inst"], sc, r, got, exp)

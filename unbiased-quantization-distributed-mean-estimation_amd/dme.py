@@ -12,16 +12,24 @@ Semantics kept from the reference (ND = Normal_dist.py):
   ND:151-157  NMSE = ||est - emp||^2 / (num_trials * vec_norm_squared * n)   ("script" NMSE,
               scales as 1/n^3); the standard NMSE = script * num_trials * n^2 is also returned
   ND:193-221  max / mean over instances
-The reference also calls 12 other schemes in the same loop; they consume the global torch
-RNG, so the shipped drivers' X stream differs from this unbiased-only loop (results agree
-statistically).
+The reference also calls other schemes in the same loop (ND:133-147), consuming the
+global torch RNG in client-major, scheme-minor order.  `schemes` selects which of the
+implemented ones run, in the reference's call order: EDEN_quantize_Hadamard (ND:135-136,
+one randint(0, 100) per call), Type_unbiased_quantize (ND:137-138, one rand(1) per call),
+Type_biased_quantize (ND:139-140, no draws).  DRIVE / QUIC-FL / Kashin / Scalar are not
+built (the shipped drivers crash at QUIC-FL, ND:141, whose sender tables are missing), so
+the draw stream equals that of a driver calling only the selected schemes.
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
 
+from .biased import biased_quantize
+from .eden import eden_quantize
 from .quantizer import client_mean, quantize_dequantize
+
+SCHEME_ORDER = ("eden", "unbiased", "biased")     # ND:135-140 call order
 
 __all__ = ["DISTRIBUTIONS", "draw_vectors", "nmse_simulation", "USERS_ND"]
 
@@ -54,29 +62,52 @@ def draw_vectors(dist: str, n: int, dim: int, rs=np.random):
 
 def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_instances: int = 50,
                     num_trials: int = 50, rates=(1, 2), seed: int = 42, torch_threads: int = 1,
-                    device=None):
-    """Returns {rate: {"script": [len(users), num_instances] array, "avg", "max",
-    "standard_avg", "standard_max"}} with the reference's normalisation."""
+                    device=None, schemes=("unbiased",)):
+    """NMSE curves of the selected schemes with the reference's normalisation.
+
+    Returns {rate: {...}} for the default unbiased-only run, else {(scheme, rate): {...}};
+    each value holds "script" ([len(users), num_instances]), "avg", "max", "standard_avg",
+    "standard_max"."""
     device = device or torch.device("cuda", torch.cuda.current_device())
+    schemes = tuple(schemes)
+    for sc in schemes:
+        if sc not in SCHEME_ORDER:
+            raise ValueError(f"unknown scheme {sc!r}")
+    order = [sc for sc in SCHEME_ORDER if sc in schemes]
     rs = np.random.RandomState(seed)                 # legacy stream == np.random.seed(seed)
     gen = torch.Generator().manual_seed(seed)        # == torch.manual_seed(seed) CPU stream
-    R = len(rates)
-    script = {r: np.zeros((len(users), num_instances), np.float64) for r in rates}
+    keys = [(sc, r) for sc in order for r in rates]
+    script = {k: np.zeros((len(users), num_instances), np.float64) for k in keys}
     for ui, n in enumerate(users):
         for inst in range(num_instances):
             vecs, vns = draw_vectors(dist, n, dim, rs)
             xs = torch.stack([torch.as_tensor(v, dtype=torch.float32) for v in vecs])     # ND:91
             emp = xs.sum(dim=0) / n                                                        # ND:95 (CPU)
-            X = torch.rand(R * n, generator=gen)                                           # AS:634 draws
+            draws = {k: [] for k in keys}
+            for _ in range(n):                        # ND:133-140: client-major, scheme/rate-minor
+                for sc in order:
+                    for r in rates:
+                        if sc == "eden":
+                            draws[(sc, r)].append(int(torch.randint(0, 100, (1,), generator=gen)))   # AS:797
+                        elif sc == "unbiased":
+                            draws[(sc, r)].append(float(torch.rand(1, generator=gen)))               # AS:634
             xd = xs.to(device)
-            for k, r in enumerate(rates):
-                q = quantize_dequantize(xd, r, X=X[k::R], torch_threads=torch_threads)
+            for sc, r in keys:
+                if sc == "unbiased":
+                    q = quantize_dequantize(xd, r, X=torch.tensor(draws[(sc, r)], dtype=torch.float32),
+                                            torch_threads=torch_threads)
+                elif sc == "biased":
+                    q = biased_quantize(xd, r, torch_threads=torch_threads)
+                else:
+                    q = eden_quantize(xd, r, seeds=draws[(sc, r)])
                 est = client_mean(q, n).cpu()
-                script[r][ui, inst] = float(torch.norm(est - emp).pow(2) / (num_trials * vns * n))   # ND:155
+                script[(sc, r)][ui, inst] = float(torch.norm(est - emp).pow(2) / (num_trials * vns * n))   # ND:155
     out = {}
-    for r in rates:
-        s = script[r].astype(np.float32)              # the reference stores NMSE in f32 tensors
-        std = s.astype(np.float64) * num_trials * np.asarray(users, np.float64)[:, None] ** 2
-        out[r] = {"script": s, "avg": s.mean(axis=1), "max": s.max(axis=1),
+    for k in keys:
+        sv = script[k].astype(np.float32)             # the reference stores NMSE in f32 tensors
+        std = sv.astype(np.float64) * num_trials * np.asarray(users, np.float64)[:, None] ** 2
+        out[k] = {"script": sv, "avg": sv.mean(axis=1), "max": sv.max(axis=1),
                   "standard_avg": std.mean(axis=1), "standard_max": std.max(axis=1)}
+    if schemes == ("unbiased",):
+        return {r: out[("unbiased", r)] for r in rates}
     return out
