@@ -199,6 +199,7 @@ def main():
                 side[pl] = {"ms_per_step": round(ms, 4), "value": round(n_total / ms / 1e3, 6)}
         _lib.check(lib.uq_check_status(P(ws), sp), "status after side pipelines")
         side["biased"] = time_biased(uqdme, x, q, args.bits, T, max(3, args.steps // 2))
+        side["eden"] = time_eden(uqdme, x, q, max(3, args.steps // 2))
         if int(torch.count_nonzero(ovf > 127)):
             raise RuntimeError("type-code overflow in the bench workload")
 
@@ -247,6 +248,25 @@ def time_biased(uqdme, x, q, bits, T, steps):
     uqdme.check_status()
     ms = e0.elapsed_time(e1) / steps
     return {"ms_per_step": round(ms, 4), "value": round(n / ms / 1e3, 6), "what": "Type_biased_quantize batch, no mean"}
+
+
+def time_eden(uqdme, x, q, steps):
+    """Side line: EDEN + RHT baseline (AS:792-811, 1 bit) on the same resident batch,
+    one compress + decompress per step, rotation seeds as the reference draws them."""
+    n, d = x.shape
+    seeds = torch.randint(0, 100, (n,), generator=torch.Generator().manual_seed(5))
+    for _ in range(2):
+        out = uqdme.eden_quantize(x, 1, seeds=seeds)
+    del out
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        uqdme.eden_quantize(x, 1, seeds=seeds)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    return {"ms_per_step": round(ms, 4), "value": round(n / ms / 1e3, 6), "what": "EDEN 1-bit batch (RHT, bins, scale, inverse RHT), no mean"}
 
 
 def ctypes_size(lib, n, d, T):

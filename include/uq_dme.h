@@ -147,6 +147,13 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
  * uq_eden_f32: both (EDEN_quantize_Hadamard for a batch); scale_out [n] or NULL.
  * Workspace: uq_eden_workspace_bytes. */
 int uq_rht_signs(const int32_t* seeds, int64_t rows, int64_t D, int8_t* signs, void* stream);
+/* The randomized Hadamard transform itself, for a batch (workspace: uq_eden_workspace_bytes):
+ *   inverse = 0: out [n][D] = H(pad(x[j], D) * diag) (HadamardSender.randomized_hadamard_transform,
+ *                AS:123-141); x rows have length dim
+ *   inverse = 1: out [n][D] = H(x[j]) * diag (HadamardReceiver, AS:146-153); dim must be D
+ * bit-identical to the reference (f32 butterflies a + b, (a + b) - 2b; / f32(sqrt(D))). */
+int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inverse, const int8_t* signs,
+               const int32_t* sign_row, void* ws, size_t ws_bytes, void* stream);
 int uq_eden_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out);
 int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
                          const int32_t* sign_row, uint8_t* bins, float* scale, void* ws, size_t ws_bytes,

@@ -36,7 +36,17 @@ def main():
     S = AS.EdenSender(device="cpu")
     R = AS.EdenReceiver(device="cpu")
     H = AS.Hadamard(device="cpu")
-    arrs, meta = {}, {"diag": [], "cases": [], "dropin": []}
+    arrs, meta = {}, {"diag": [], "cases": [], "dropin": [], "rht": []}
+    HS = AS.HadamardSender(device="cpu")
+    HR = AS.HadamardReceiver(device="cpu")
+    for k, (dim, seed) in enumerate(((1, 3), (5, 0), (1000, 42), (4096, 99), (5000, 7), (1 << 16, 11), (1 << 20, 123))):
+        x = spec_gen({"dist": "normal", "d": dim, "seed": 700 + k})
+        fwd = HS.randomized_hadamard_transform(torch.from_numpy(x.copy()), seed).numpy().astype(f32)
+        inv = HR.randomized_inverse_hadamard_transform(torch.from_numpy(fwd.copy()), seed).numpy().astype(f32)
+        meta["rht"].append({"k": k, "dim": dim, "seed": seed, "fwd_sha": sha(fwd), "inv_sha": sha(inv)})
+        if dim <= 8192:
+            arrs[f"rfwd{k}"] = fwd
+            arrs[f"rinv{k}"] = inv
     for seed, D in ((0, 4096), (17, 1000), (99, 624 * 3 + 5), (123, 64)):
         dg = H.random_diagonal(D, seed).numpy().astype(np.int8)
         arrs[f"diag_{seed}_{D}"] = dg

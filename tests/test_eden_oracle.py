@@ -52,3 +52,14 @@ def test_hadamard_is_an_involution_up_to_rounding():
     v = rng.standard_normal(1 << 12).astype(np.float32)
     w = E.hadamard(E.hadamard(v))
     np.testing.assert_allclose(w, v, rtol=1e-4, atol=1e-5)
+
+
+def test_rht_oracle_vs_reference(fx):
+    meta, z = fx
+    for r in meta["rht"]:
+        if r["dim"] > 70000:
+            continue
+        x = G.spec_gen({"dist": "normal", "d": r["dim"], "seed": 700 + r["k"]})
+        f = E.rht(x, r["seed"])
+        assert G.sha(f) == r["fwd_sha"], r
+        assert G.sha(E.inverse_rht(f, r["seed"])) == r["inv_sha"], r

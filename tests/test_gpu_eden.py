@@ -80,3 +80,17 @@ def test_drop_in(uq, fx):
         assert int(torch.randint(0, 100, (1,))) == dd["drawn_seed"]
     with pytest.raises(ValueError):
         uq.EDEN_quantize_Hadamard(torch.randn(64), 3)
+
+
+def test_rht_forward_inverse_vs_reference(uq, fx):
+    meta, z = fx
+    from tests.golden_data import spec_gen
+    for r in meta["rht"]:
+        x = spec_gen({"dist": "normal", "d": r["dim"], "seed": 700 + r["k"]})
+        fwd = uq.randomized_hadamard_transform(torch.as_tensor(x).cuda().view(1, -1), [r["seed"]])
+        inv = uq.randomized_inverse_hadamard_transform(fwd, [r["seed"]])
+        f, i = fwd.cpu().numpy()[0], inv.cpu().numpy()[0]
+        assert G.sha(f) == r["fwd_sha"], r
+        assert G.sha(i) == r["inv_sha"], r
+        if f"rfwd{r['k']}" in z.files:
+            assert G.bits_equal(f, z[f"rfwd{r['k']}"])

@@ -14,7 +14,8 @@ from .quantizer import (
 )
 from .codes import TypeCodes
 from .biased import Type_biased_quantize, biased_quantize
-from .eden import EDEN_quantize_Hadamard, eden_quantize, eden_compress, eden_decompress, EdenMessage, rht_signs
+from .eden import (EDEN_quantize_Hadamard, eden_quantize, eden_compress, eden_decompress, EdenMessage, rht_signs,
+                   randomized_hadamard_transform, randomized_inverse_hadamard_transform)
 from ._lib import UQError, load as load_library, library_path
 from .distributed import shard_range, sharded_client_mean, sharded_quantize_mean
 from .dme import DISTRIBUTIONS, nmse_simulation
@@ -25,5 +26,6 @@ __all__ = [
     "check_status", "UQError", "load_library", "library_path", "shard_range", "sharded_client_mean",
     "sharded_quantize_mean", "DISTRIBUTIONS", "nmse_simulation", "quantize_encode", "decode", "codes_mean",
     "TypeCodes", "Type_biased_quantize", "biased_quantize", "EDEN_quantize_Hadamard", "eden_quantize",
-    "eden_compress", "eden_decompress", "EdenMessage", "rht_signs",
+    "eden_compress", "eden_decompress", "EdenMessage", "rht_signs", "randomized_hadamard_transform",
+    "randomized_inverse_hadamard_transform",
 ]

@@ -1072,6 +1072,18 @@ EdenLayout eden_layout(int64_t n, int64_t dim) {
     return w;
 }
 
+// One FWHT pass: the register-radix kernels for the 4096-element low pass and the
+// 256 x 32 high pass, the generic LDS kernel otherwise (same stages, same bits).
+template <int M, bool L, bool R>
+void fwht_dispatch(dim3 grid, const FwhtArgs& b, int lo, int k, hipStream_t st) {
+    if (lo == 0 && k == kFwhtLowBits && (M != 2 || (b.D % 16) == 0))
+        hipLaunchKernelGGL((fwht_low4096_kernel<M, L, R>), grid, dim3(256), 0, st, b);
+    else if (lo > 0 && k == kFwhtHighBits && M == 0)
+        hipLaunchKernelGGL((fwht_high256_kernel<L, R>), grid, dim3(256), 0, st, b, lo);
+    else
+        hipLaunchKernelGGL((fwht_pass_kernel<M, L, R>), grid, dim3(kFwhtT), 0, st, b, lo, k);
+}
+
 // Runs the FWHT passes of one transform.  MODE of the first pass: 1 sender, 2 receiver.
 int launch_fwht(FwhtArgs a, int64_t n, bool receiver, float* buf, float* out, hipStream_t st) {
     const int p = ilog2_pow2(a.D);
@@ -1085,13 +1097,19 @@ int launch_fwht(FwhtArgs a, int64_t n, bool receiver, float* buf, float* out, hi
         b.out = (last && receiver) ? out : buf;
         if (!first) b.in = buf;
         const dim3 grid((unsigned)tiles, (unsigned)n);
-#define UQ_FWHT(M, L, R) hipLaunchKernelGGL((fwht_pass_kernel<M, L, R>), grid, dim3(kFwhtT), 0, st, b, lo, k)
-        if (first && !receiver) { if (last) UQ_FWHT(1, true, false); else UQ_FWHT(1, false, false); }
-        else if (first && receiver) { if (last) UQ_FWHT(2, true, true); else UQ_FWHT(2, false, false); }
-        else if (last && receiver) UQ_FWHT(0, true, true);
-        else if (last) UQ_FWHT(0, true, false);
-        else UQ_FWHT(0, false, false);
-#undef UQ_FWHT
+        if (first && !receiver) {
+            if (last) fwht_dispatch<1, true, false>(grid, b, lo, k, st);
+            else fwht_dispatch<1, false, false>(grid, b, lo, k, st);
+        } else if (first && receiver) {
+            if (last) fwht_dispatch<2, true, true>(grid, b, lo, k, st);
+            else fwht_dispatch<2, false, false>(grid, b, lo, k, st);
+        } else if (last && receiver) {
+            fwht_dispatch<0, true, true>(grid, b, lo, k, st);
+        } else if (last) {
+            fwht_dispatch<0, true, false>(grid, b, lo, k, st);
+        } else {
+            fwht_dispatch<0, false, false>(grid, b, lo, k, st);
+        }
         int rc = hip_check(hipGetLastError(), "fwht_pass_kernel launch");
         if (rc) return rc;
         if (last) break;
@@ -1435,6 +1453,55 @@ int uq_rht_signs(const int32_t* seeds, int64_t rows, int64_t D, int8_t* signs, v
     return hip_check(hipGetLastError(), "rht_signs_kernel launch");
 }
 
+int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inverse, const int8_t* signs,
+               const int32_t* sign_row, void* ws, size_t ws_bytes, void* stream) {
+    if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
+    if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 clients per call");
+    if (n == 0 || dim == 0) return UQ_OK;
+    if (!x || !out || !signs) return fail(UQ_E_INVALID, "null pointer");
+    const EdenLayout w = eden_layout(n, dim);
+    if (inverse && dim != w.D) return fail(UQ_E_INVALID, "inverse RHT input length must be a power of two");
+    if (!ws || ws_bytes < w.total) return fail(UQ_E_WORKSPACE, "workspace too small");
+    FwhtArgs a{};
+    a.in = x;
+    a.signs = signs;
+    a.sign_row = sign_row;
+    a.scale = nullptr;
+    a.D = w.D;
+    a.dim = inverse ? w.D : dim;
+    a.sqrtD = (float)std::sqrt((double)w.D);
+    hipStream_t st = (hipStream_t)stream;
+    float* buf = (float*)((char*)ws + w.vec_off);
+    if (!inverse) {                                           // AS:123-141: pad, * diag, H
+        int rc = launch_fwht(a, n, false, buf, nullptr, st);
+        if (rc) return rc;
+        return hip_check(hipMemcpyAsync(out, buf, (size_t)n * w.D * sizeof(float), hipMemcpyDeviceToDevice, st),
+                         "copy rht");
+    }
+    // AS:146-153: H, then * diag (the receiver's last pass with no scale)
+    const int p = ilog2_pow2(w.D);
+    int lo = 0, k = std::min(p, kFwhtLowBits);
+    bool first = true;
+    for (;;) {
+        const bool last = lo + k >= p;
+        const int cols = lo == 0 ? 1 : kFwhtCols;
+        const int64_t tiles = w.D / (((int64_t)1 << k) * cols);
+        FwhtArgs b = a;
+        b.in = first ? (const void*)x : (const void*)buf;
+        b.out = last ? out : buf;
+        const dim3 grid((unsigned)tiles, (unsigned)n);
+        if (last) fwht_dispatch<0, true, true>(grid, b, lo, k, st);
+        else fwht_dispatch<0, false, false>(grid, b, lo, k, st);
+        int rc = hip_check(hipGetLastError(), "fwht_pass_kernel launch");
+        if (rc) return rc;
+        if (last) break;
+        first = false;
+        lo += k;
+        k = std::min(p - lo, kFwhtHighBits);
+    }
+    return UQ_OK;
+}
+
 int uq_eden_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
     if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
     if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
@@ -1467,7 +1534,8 @@ int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, 
     a.tab = tab;
     rc = launch_fwht(a, n, false, vec, nullptr, st);                               // AS:123-141
     if (rc) return rc;
-    hipLaunchKernelGGL(eden_norm_kernel, dim3((unsigned)((n + 7) / 8)), dim3(64), 0, st, vec, n, w.D, nrm);
+    hipLaunchKernelGGL(eden_norm_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads), 0, st,
+                       vec, n, w.D, nrm);
     rc = hip_check(hipGetLastError(), "eden_norm_kernel launch");                  // AS:329 torch.norm
     if (rc) return rc;
     hipLaunchKernelGGL(eden_bins_kernel, dim3((unsigned)w.tiles, (unsigned)n), dim3(256), 0, st, vec, w.D, a.sqrtD,

@@ -155,7 +155,7 @@ fwht_pass_kernel(FwhtArgs a, int lo, int k) {
         if (RECV_LAST) {
             if (i < a.dim) {
                 v = v * (float)sg[i];                           // AS:152 * diag
-                a.out[vec * a.dim + i] = a.scale[vec] * v;      // AS:413 scale * vec, [:dim]
+                a.out[vec * a.dim + i] = a.scale ? a.scale[vec] * v : v;   // AS:413 scale * vec, [:dim]
             }
         } else {
             a.out[vec * D + i] = v;
@@ -163,35 +163,267 @@ fwht_pass_kernel(FwhtArgs a, int lo, int k) {
     }
 }
 
-// ---- KE2: torch.norm(v, 2) -------------------------------------------------------------
-// 8 clients per 64-thread block, lane l of a client accumulates v[8i + l] with fma in
-// order; the 8 lane sums are added 0..7, then sqrt (f32).  D is a power of two >= 8 or
-// smaller (then the scalar tail path applies to all of it).
-__global__ void __launch_bounds__(64)
-eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __restrict__ nrm) {
-    const int l = threadIdx.x & 7;
-    const int64_t vec = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 3);
-    const bool live = vec < n;
-    const float* p = v + (live ? vec : 0) * D;
-    const int64_t nv = D - D % 8;
-    float acc = 0.f;
-    if (live) {
-        int64_t i = l;
-        for (; i + 8 * 15 < nv; i += 8 * 16) {
-            float t[16];
+// ---- KE1': register-radix passes for the two common shapes -----------------------------
+// Same stages in the same order as fwht_pass_kernel (so the same bits), with 16 (low pass)
+// or 32 (high pass) elements per thread in registers and padded LDS transposes between
+// rounds of register-local stages.
+__device__ __forceinline__ void bfly(float& a, float& b) {   // AS:109-110
+    const float na = a + b;
+    b = na - 2.f * b;
+    a = na;
+}
+
+// stages over the 4 bits of a 16-element register array (index bit j of i)
+__device__ __forceinline__ void stages16(float* v) {
 #pragma unroll
-            for (int u = 0; u < 16; ++u) t[u] = p[i + 8 * u];
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int u = 0; u < 16; ++u) acc = fmaf(t[u], t[u], acc);
+        for (int i = 0; i < 16; ++i)
+            if (!(i & (1 << j))) bfly(v[i], v[i | (1 << j)]);
+}
+
+__device__ __forceinline__ int pad17(int e) { return e + (e >> 4); }
+
+// Low pass over 4096 contiguous elements, index e = b0 + 16 b1 + 256 b2: round 1 thread
+// (b1, b2) holds b0 = 0..15 (bits 0-3), round 2 thread (b0, b2) holds b1 (bits 4-7),
+// round 3 thread (b0, b1) holds b2 (bits 8-11).
+template <int MODE, bool LAST, bool RECV_LAST>
+__global__ void __launch_bounds__(256)
+fwht_low4096_kernel(FwhtArgs a) {
+    __shared__ float s[4096 + 256];
+    const int64_t vec = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int64_t D = a.D;
+    const int64_t base = (int64_t)blockIdx.x * 4096;
+    const int8_t* sg = a.signs + (int64_t)(a.sign_row ? a.sign_row[vec] : 0) * D;
+    float v[16];
+    {   // round-1 layout: 16 contiguous elements
+        const int64_t i0 = base + (int64_t)tid * 16;
+        if (MODE == 1) {
+            const float* x = (const float*)a.in + vec * a.dim;
+            const bool full = i0 + 16 <= a.dim && (((uintptr_t)(x + i0)) & 15) == 0;
+            if (full) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 t = *reinterpret_cast<const float4*>(x + i0 + 4 * q);
+                    v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = (i0 + i < a.dim) ? x[i0 + i] : 0.f;
+            }
+            const int4 sgv = *reinterpret_cast<const int4*>(sg + i0);       // 16 signs
+            const int8_t* sb = reinterpret_cast<const int8_t*>(&sgv);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = v[i] * (float)sb[i];            // AS:132/137 * diag
+        } else if (MODE == 2) {
+            const int4 bv = *reinterpret_cast<const int4*>((const uint8_t*)a.in + vec * D + i0);
+            const uint8_t* bb = reinterpret_cast<const uint8_t*>(&bv);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = a.tab.c[bb[i]];                  // AS:383
+        } else {
+            const float* p = (const float*)a.in + vec * D + i0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
+                v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+            }
         }
-        for (; i < nv; i += 8) acc = fmaf(p[i], p[i], acc);
     }
-    // lanes 0..7 in order, then the scalar tail
-    float tot = __shfl(acc, (threadIdx.x & ~7), kWave);
-    for (int j = 1; j < 8; ++j) tot = tot + __shfl(acc, (threadIdx.x & ~7) + j, kWave);
-    if (live && l == 0) {
-        for (int64_t i = nv; i < D; ++i) tot = tot + p[i] * p[i];
-        nrm[vec] = sqrtf(tot);
+    stages16(v);                                                   // bits 0-3
+    const int b1r1 = tid & 15, b2r1 = tid >> 4;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[pad17(i + 16 * b1r1 + 256 * b2r1)] = v[i];
+    __syncthreads();
+    const int b0 = tid & 15, b2 = tid >> 4;                        // round 2: (b0, b2)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = s[pad17(b0 + 16 * i + 256 * b2)];
+    stages16(v);                                                   // bits 4-7
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[pad17(b0 + 16 * i + 256 * b2)] = v[i];
+    __syncthreads();
+    const int b1 = tid >> 4;                                       // round 3: (b0, b1)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = s[pad17(b0 + 16 * b1 + 256 * i)];
+    stages16(v);                                                   // bits 8-11
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t gi = base + b0 + 16 * b1 + 256 * i;          // lanes: consecutive b0 + 16 b1
+        float r = v[i];
+        if (LAST) r = r / a.sqrtD;                                 // AS:114
+        if (RECV_LAST) {
+            if (gi < a.dim) {
+                r = r * (float)sg[gi];                             // AS:152
+                a.out[vec * a.dim + gi] = a.scale ? a.scale[vec] * r : r;
+            }
+        } else {
+            a.out[vec * D + gi] = r;
+        }
+    }
+}
+
+// High pass: 256 rows (index bits lo..lo+7) x 32 columns.  Round 1: thread (c, g), c = tid % 32,
+// g = tid / 32, holds rows 32 g + m (m = 0..31; row bits 0-4).  Round 2: thread (c, h)
+// holds rows a + 32 u for a in 4h..4h+3, u = 0..7 (row bits 5-7).
+template <bool LAST, bool RECV_LAST>
+__global__ void __launch_bounds__(256)
+fwht_high256_kernel(FwhtArgs a, int lo) {
+    __shared__ float s[256 * 33];
+    __shared__ int8_t sgl[RECV_LAST ? 256 * 32 : 1];            // the tile's diagonal, row-major
+    const int64_t vec = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int64_t D = a.D;
+    const int64_t lowspan = (int64_t)1 << lo;
+    const int64_t col_groups = lowspan / kFwhtCols;
+    const int64_t t = blockIdx.x;
+    const int64_t hi = (t / col_groups) << (lo + 8);
+    const int64_t c0 = (t % col_groups) * kFwhtCols;
+    const int8_t* sg = a.signs + (int64_t)(a.sign_row ? a.sign_row[vec] : 0) * D;
+    const int c = tid & 31, g = tid >> 5;
+    const float* in = (const float*)a.in + vec * D;
+    if (RECV_LAST) {      // row `tid` of the tile: 32 contiguous sign bytes, two 16-byte loads
+        const int8_t* sr = sg + hi + ((int64_t)tid << lo) + c0;
+        *reinterpret_cast<int4*>(sgl + 32 * tid) = *reinterpret_cast<const int4*>(sr);
+        *reinterpret_cast<int4*>(sgl + 32 * tid + 16) = *reinterpret_cast<const int4*>(sr + 16);
+    }
+    float v[32];
+#pragma unroll
+    for (int m = 0; m < 32; ++m) v[m] = in[hi + ((int64_t)(32 * g + m) << lo) + c0 + c];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int m = 0; m < 32; ++m)
+            if (!(m & (1 << j))) bfly(v[m], v[m | (1 << j)]);
+#pragma unroll
+    for (int m = 0; m < 32; ++m) s[(32 * g + m) * 33 + c] = v[m];
+    __syncthreads();
+    const int h = g;
+#pragma unroll
+    for (int aa = 0; aa < 4; ++aa)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[aa * 8 + u] = s[(4 * h + aa + 32 * u) * 33 + c];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int aa = 0; aa < 4; ++aa)
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (!(u & (1 << j))) bfly(v[aa * 8 + u], v[aa * 8 + (u | (1 << j))]);
+#pragma unroll
+    for (int aa = 0; aa < 4; ++aa)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int row = 4 * h + aa + 32 * u;
+            const int64_t gi = hi + ((int64_t)row << lo) + c0 + c;
+            float r = v[aa * 8 + u];
+            if (LAST) r = r / a.sqrtD;                             // AS:114
+            if (RECV_LAST) {
+                if (gi < a.dim) {
+                    r = r * (float)sgl[32 * row + c];              // AS:152
+                    a.out[vec * a.dim + gi] = a.scale ? a.scale[vec] * r : r;
+                }
+            } else {
+                a.out[vec * D + gi] = r;
+            }
+        }
+}
+
+// ---- KE2: torch.norm(v, 2) -------------------------------------------------------------
+// torch CPU order: 8 interleaved lanes, acc_l = fma(v[8i + l], v[8i + l], acc_l) in i order,
+// then acc_0 + acc_1 + ... + acc_7, the scalar tail, sqrt (f32).  One workgroup serves 4
+// clients: wave 0 runs the 32 chains (client k = lane / 8, torch lane l = lane % 8) and never
+// touches global memory; waves 1-4 stream 1024-float chunks of the 4 clients into a
+// triple-buffered LDS image laid out [client][l][i], so a chain lane reads 4 consecutive
+// steps with one ds_read_b128.
+constexpr int kNormClients = 4;
+constexpr int kNormChunk = 1024;                    // floats per client per chunk
+constexpr int kNormRow = kNormChunk / 8 + 4;        // one torch lane's 128 steps (+4 pad)
+constexpr int kNormClientStride = 8 * kNormRow;
+constexpr int kNormBuf = kNormClients * kNormClientStride;
+constexpr int kNormThreads = 64 + 256;
+__global__ void __launch_bounds__(kNormThreads)
+eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __restrict__ nrm) {
+    __shared__ __attribute__((aligned(16))) float s[3][kNormBuf];
+    const int tid = threadIdx.x;
+    const int64_t v0 = (int64_t)blockIdx.x * kNormClients;
+    const int64_t nv = D - D % 8;
+    const int64_t nchunks = (nv + kNormChunk - 1) / kNormChunk;
+    const bool chain = tid < kWave;
+    // loaders: thread t' = tid - 64 owns client k = t' / 64 and float4 slots (t' % 64) + 64 q
+    const int lt = tid - kWave, lk = lt >> 6, lj = lt & 63;
+    const bool lvalid = !chain && v0 + lk < n;
+    const float* lp = v + (lvalid ? v0 + lk : 0) * D;
+    constexpr int kLQ = kNormChunk / 256;             // float4 per loader thread
+    float4 nx[kLQ];
+    auto load = [&](int64_t ch) {
+#pragma unroll
+        for (int q = 0; q < kLQ; ++q) {
+            const int64_t i = ch * kNormChunk + 4 * (lj + 64 * q);
+            if (lvalid && i + 3 < nv) {
+                nx[q] = *reinterpret_cast<const float4*>(lp + i);
+            } else {
+                nx[q].x = (lvalid && i < nv) ? lp[i] : 0.f;
+                nx[q].y = (lvalid && i + 1 < nv) ? lp[i + 1] : 0.f;
+                nx[q].z = (lvalid && i + 2 < nv) ? lp[i + 2] : 0.f;
+                nx[q].w = (lvalid && i + 3 < nv) ? lp[i + 3] : 0.f;
+            }
+        }
+    };
+    auto store = [&](float* sb) {      // element e = 8 i + l of the chunk -> [k][l][i]
+        if (chain) return;
+#pragma unroll
+        for (int q = 0; q < kLQ; ++q) {
+            const int e = 4 * (lj + 64 * q);
+            const int i = e >> 3, l = e & 7;
+            float* base = sb + lk * kNormClientStride + i;
+            base[(l + 0) * kNormRow] = nx[q].x;
+            base[(l + 1) * kNormRow] = nx[q].y;
+            base[(l + 2) * kNormRow] = nx[q].z;
+            base[(l + 3) * kNormRow] = nx[q].w;
+        }
+    };
+    const int ck = (tid >> 3) & (kNormClients - 1), cl = tid & 7;   // lanes >= 32 mirror 0..31
+    float acc = 0.f;
+    if (nchunks > 0) {
+        if (!chain) load(0);
+        store(s[0]);
+        if (!chain && nchunks > 1) load(1);
+    }
+    __syncthreads();
+    for (int64_t ch = 0; ch < nchunks; ++ch) {
+        if (chain) {
+            const int cnt = (int)(std::min<int64_t>(kNormChunk, nv - ch * kNormChunk) / 8);
+            const float* row = s[ch % 3] + ck * kNormClientStride + cl * kNormRow;
+            int i = 0;
+            for (; i + 16 <= cnt; i += 16) {
+                float4 t[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const float4*>(row + i + 4 * u);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc = fmaf(t[u].x, t[u].x, acc);
+                    acc = fmaf(t[u].y, t[u].y, acc);
+                    acc = fmaf(t[u].z, t[u].z, acc);
+                    acc = fmaf(t[u].w, t[u].w, acc);
+                }
+            }
+            for (; i < cnt; ++i) acc = fmaf(row[i], row[i], acc);
+        } else if (ch + 1 < nchunks) {
+            store(s[(ch + 1) % 3]);
+            if (ch + 2 < nchunks) load(ch + 2);
+        }
+        __syncthreads();
+    }
+    if (chain) {
+        const int base = tid & ~7;
+        float tot = __shfl(acc, base, kWave);
+        for (int j = 1; j < 8; ++j) tot = tot + __shfl(acc, base + j, kWave);
+        const int64_t vec = v0 + ck;
+        if (tid < 8 * kNormClients && cl == 0 && vec < n) {
+            const float* p = v + vec * D;
+            for (int64_t i = nv; i < D; ++i) tot = tot + p[i] * p[i];
+            nrm[vec] = sqrtf(tot);
+        }
     }
 }
 
@@ -204,15 +436,34 @@ eden_bins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const floa
     const float nv = nrm[vec];
     const float* p = v + vec * D;
     uint8_t* bp = bins + vec * D;
+    const int64_t i0 = (int64_t)blockIdx.x * kEdenTile + (int64_t)tid * 16;
     double dot = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kEdenTile + tid; i < std::min<int64_t>(D, (int64_t)(blockIdx.x + 1) * kEdenTile);
-         i += 256) {
-        const float x = p[i];
-        const float z = (x * sqrtD) / nv;                   // AS:329 vec * sqrt(D) / norm
-        int b = 0;
-        for (int j = 0; j < tab.nb; ++j) b += (tab.b[j] < z) ? 1 : 0;    // bucketize, right=False
-        bp[i] = (uint8_t)b;
-        dot += (double)tab.c[b] * (double)x;                // AS:335 dot(centroids[bins], vec)
+    if (i0 + 16 <= D) {
+        float x[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 t = *reinterpret_cast<const float4*>(p + i0 + 4 * q);
+            x[4 * q] = t.x; x[4 * q + 1] = t.y; x[4 * q + 2] = t.z; x[4 * q + 3] = t.w;
+        }
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float z = (x[i] * sqrtD) / nv;                   // AS:329 vec * sqrt(D) / norm
+            int b = 0;
+            for (int j = 0; j < tab.nb; ++j) b += (tab.b[j] < z) ? 1 : 0;   // bucketize, right=False
+            w[i >> 2] |= (uint32_t)b << (8 * (i & 3));
+            dot += (double)tab.c[b] * (double)x[i];                // AS:335 dot(centroids[bins], vec)
+        }
+        *reinterpret_cast<uint4*>(bp + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (int64_t i = i0; i < std::min<int64_t>(D, i0 + 16); ++i) {
+            const float x = p[i];
+            const float z = (x * sqrtD) / nv;
+            int b = 0;
+            for (int j = 0; j < tab.nb; ++j) b += (tab.b[j] < z) ? 1 : 0;
+            bp[i] = (uint8_t)b;
+            dot += (double)tab.c[b] * (double)x;
+        }
     }
     __shared__ double red[256];
     red[tid] = dot;

@@ -29,7 +29,7 @@ from . import _lib
 from .quantizer import _as_device_f32_2d, _device, _ptr, _stream_ptr, _workspace
 
 __all__ = ["EDEN_quantize_Hadamard", "eden_quantize", "eden_compress", "eden_decompress", "EdenMessage",
-           "rht_signs", "padded_dim"]
+           "rht_signs", "padded_dim", "randomized_hadamard_transform", "randomized_inverse_hadamard_transform"]
 
 _SEEDS = 100                       # AS:797 torch.randint(0, 100)
 _cache_lock = threading.Lock()
@@ -146,6 +146,36 @@ def eden_quantize(x, bits_per_dimension=1, seeds=None, *, return_scale: bool = F
         _lib.check(_lib.load().uq_eden_f32(_ptr(x), _ptr(out), n, d, nb, _ptr(tab), _ptr(rows), _ptr(scale), _ptr(ws),
                                            ws.numel(), _stream_ptr(dev)), "uq_eden_f32")
     return (out, scale) if return_scale else out
+
+
+def _rht(x, seeds, inverse: bool):
+    dev = _device()
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    D = padded_dim(d)
+    if inverse and d != D:
+        raise ValueError("the inverse transform takes power-of-two rows (AS:146-153)")
+    s = torch.as_tensor(seeds, dtype=torch.int64).reshape(-1)
+    if s.numel() != n:
+        raise ValueError("one seed per row")
+    out = torch.empty((n, D), dtype=torch.float32, device=dev)
+    if n and d:
+        tab, rows = _sign_rows(s, D, dev)
+        ws = _ws(n, D, dev)
+        _lib.check(_lib.load().uq_rht_f32(_ptr(x), _ptr(out), n, d, int(inverse), _ptr(tab), _ptr(rows), _ptr(ws),
+                                          ws.numel(), _stream_ptr(dev)), "uq_rht_f32")
+    return out
+
+
+def randomized_hadamard_transform(x, seeds) -> torch.Tensor:
+    """HadamardSender.randomized_hadamard_transform (AS:123-141) per row: zero-pad to a
+    power of two, multiply by the seeded diagonal, normalized Walsh-Hadamard transform."""
+    return _rht(x, seeds, False)
+
+
+def randomized_inverse_hadamard_transform(x, seeds) -> torch.Tensor:
+    """HadamardReceiver.randomized_inverse_hadamard_transform (AS:146-153) per row."""
+    return _rht(x, seeds, True)
 
 
 def EDEN_quantize_Hadamard(input_vector, bits_per_dimension=1):
