@@ -1,0 +1,95 @@
+"""Reproduce the reference's DME NMSE curves on the GPU (config C1-style harness).
+
+    python tools/nmse_curves.py --out gpurun_out/nmse_curves.json
+
+Runs dme.nmse_simulation (ND:77-221 semantics: legacy np.random seed 42 vectors, torch seed-42
+draws in the drivers' per-client call order, script NMSE, avg/max over 50 instances) for the
+five reference distributions at d = 2048, n = 1, 6, ..., 101 (96 for Bernoulli/Laplace/Gamma
+as their drivers use arange(1, 101, 5)), for the unbiased, biased and EDEN schemes, and
+compares the unbiased curves with the values decoded from the reference's published plots
+(BASELINE.md §2a).  The published runs interleave 12 more schemes on the same torch RNG,
+so agreement is statistical, not bitwise."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# (dist, stat, R) -> {n: value}; last column is n=101 (n=96 for bernoulli)
+PUBLISHED = {
+    ("normal", "avg", 1): [3.980e-2, 1.832e-4, 2.974e-5, 2.977e-7, 3.832e-8],
+    ("normal", "avg", 2): [5.244e-3, 2.413e-5, 3.920e-6, 3.927e-8, 5.132e-9],
+    ("normal", "max", 1): [4.191e-2, 1.962e-4, 3.242e-5, 3.223e-7, 4.083e-8],
+    ("normal", "max", 2): [5.550e-3, 2.586e-5, 4.283e-6, 4.176e-8, 5.543e-9],
+    ("laplace", "avg", 1): [3.177e-2, 1.457e-4, 2.364e-5, 2.377e-7, 3.062e-8],
+    ("laplace", "avg", 2): [4.544e-3, 2.095e-5, 3.399e-6, 3.407e-8, 4.345e-9],
+    ("laplace", "max", 1): [3.386e-2, 1.567e-4, 2.561e-5, 2.569e-7, 3.269e-8],
+    ("laplace", "max", 2): [4.933e-3, 2.303e-5, 3.604e-6, 3.678e-8, 4.636e-9],
+    ("gamma", "avg", 1): [4.250e-2, 1.963e-4, 3.190e-5, 3.200e-7, 4.155e-8],
+    ("gamma", "avg", 2): [5.915e-3, 2.766e-5, 4.450e-6, 4.503e-8, 5.762e-9],
+    ("gamma", "max", 1): [4.448e-2, 2.089e-4, 3.456e-5, 3.516e-7, 4.492e-8],
+    ("gamma", "max", 2): [6.334e-3, 2.957e-5, 4.744e-6, 4.980e-8, 6.070e-9],
+    ("bernoulli", "avg", 1): [4.541e-2, 2.130e-4, 3.392e-5, 3.457e-7, 5.150e-8],
+    ("bernoulli", "avg", 2): [1.955e-3, 9.235e-6, 1.477e-6, 1.494e-8, 2.244e-9],
+    ("bernoulli", "max", 1): [4.785e-2, 2.351e-4, 3.639e-5, 3.760e-7, 5.459e-8],
+    ("bernoulli", "max", 2): [2.774e-3, 1.088e-5, 1.683e-6, 1.629e-8, 2.417e-9],
+    ("lognormal", "avg", 1): [1.222e-3, 4.047e-6, 5.988e-7, 4.834e-9, 5.981e-10],
+    ("lognormal", "avg", 2): [2.147e-4, 7.112e-7, 1.065e-7, 8.555e-10, 1.065e-10],
+    ("lognormal", "max", 1): [2.315e-3, 7.211e-6, 1.017e-6, 6.947e-09, 8.900e-10],
+    ("lognormal", "max", 2): [3.789e-4, 1.304e-6, 1.793e-7, 1.224e-9, 1.613e-10],
+}
+# The published plots' user grids: 21 points (n = 1..101) except Bernoulli (20 points, n = 1..96).
+# Note: the shipped Laplace_dist.py:43 and Gamma_dist.py:40 use arange(1, 101, 5) (last n = 96),
+# but their published plots end at n = 101 -- our n = 96 value is (101/96)^3 = 1.165 times the
+# published last point, the 1/n^3 scaling of the script NMSE -- so those plots came from a
+# 21-point run; the comparison uses the published grid.
+USERS = {"normal": range(1, 102, 5), "lognormal": range(1, 102, 5), "laplace": range(1, 102, 5),
+         "gamma": range(1, 102, 5), "bernoulli": range(1, 101, 5)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dists", default="normal,laplace,gamma,bernoulli,lognormal")
+    ap.add_argument("--dim", type=int, default=2048)
+    ap.add_argument("--instances", type=int, default=50)
+    ap.add_argument("--schemes", default="eden,unbiased,biased")
+    ap.add_argument("--out", default="gpurun_out/nmse_curves.json")
+    a = ap.parse_args()
+    import uqdme
+    schemes = tuple(a.schemes.split(","))
+    res = {"dim": a.dim, "instances": a.instances, "schemes": schemes, "curves": {}, "vs_published": {}}
+    for dist in a.dists.split(","):
+        users = tuple(USERS[dist])
+        t0 = time.time()
+        out = uqdme.nmse_simulation(dist, dim=a.dim, users=users, num_instances=a.instances, schemes=schemes,
+                                    torch_threads=1)
+        if schemes == ("unbiased",):
+            out = {("unbiased", r): v for r, v in out.items()}
+        for (sc, r), v in out.items():
+            res["curves"][f"{dist}/{sc}/R{r}"] = {"users": list(users), "avg": [float(x) for x in v["avg"]],
+                                                  "max": [float(x) for x in v["max"]]}
+        cols = [users.index(u) for u in (1, 6, 11, 51)] + [len(users) - 1]
+        for stat in ("avg", "max"):
+            for r in (1, 2):
+                if ("unbiased", r) not in out:
+                    continue
+                got = np.asarray(out[("unbiased", r)][stat])[cols]
+                pub = np.asarray(PUBLISHED[(dist, stat, r)])
+                rel = (got - pub) / pub
+                res["vs_published"][f"{dist}/{stat}/R{r}"] = {"users": [users[c] for c in cols],
+                                                              "gpu": [float(x) for x in got],
+                                                              "published": [float(x) for x in pub],
+                                                              "rel_diff": [round(float(x), 4) for x in rel]}
+        print(f"{dist}: {time.time() - t0:.1f} s", flush=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    worst = max(abs(x) for v in res["vs_published"].values() for x in v["rel_diff"])
+    print(json.dumps({"tool": "nmse_curves", "worst_abs_rel_diff_vs_published": worst}))
+
+
+if __name__ == "__main__":
+    main()
