@@ -252,11 +252,14 @@ template <bool VEC4>
 __global__ void __launch_bounds__(256)
 rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, const float* __restrict__ l1,
                   float fm, const RezState* __restrict__ st, const uint32_t* __restrict__ tilecnt, int32_t tiles,
-                  const uint32_t* __restrict__ tie_bits) {
+                  const uint32_t* __restrict__ tie_bits, int part) {
     const int64_t vec = blockIdx.y;
     const RezState s = st[vec];
     const bool on = s.kleft != 0;
     const bool amb = on && (s.flags & kRezAmbiguous);
+    // part 0: every client; 1: clients without a tie at the threshold (run while KB7 replays
+    // the others on a side stream); 2: only those with one (after KB7)
+    if ((part == 1 && amb) || (part == 2 && !amb)) return;
     const bool replay = amb && (s.flags & kRezTorchTies);
     const bool up = s.delta > 0;
     const float L = l1[vec];

@@ -174,7 +174,7 @@ __device__ __forceinline__ void tt_scan_segment(const Queue& A, int64_t first, i
 #pragma unroll
         for (int u = 0; u < kTieU; ++u) {
             const int64_t i = b + (int64_t)u * kWave + lane;
-            const bool valid = i < s1;
+            const bool valid = i < s1 && i >= first;
             fn(i, valid && i > first && k[u] <= piv,      // left stop:  !comp(A[i], pivot)
                valid && k[u] >= piv);                     // right stop: !comp(pivot, A[i])
         }
@@ -192,14 +192,41 @@ __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t 
     TT_T0();
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int64_t seg = (((last - first) + kTieWaves - 1) / kTieWaves + kWave - 1) & ~(int64_t)(kWave - 1);
-    const int64_t s0 = std::min<int64_t>(last, first + (int64_t)w * seg);
+    // segments start at multiples of 4 (16-byte aligned in the 16-byte aligned view); indices
+    // below `first` belong to no stop list
+    const int64_t a0 = first & ~(int64_t)3;
+    const int64_t seg = ((((last - a0) + kTieWaves - 1) / kTieWaves) + 4 * kWave - 1) & ~(int64_t)(4 * kWave - 1);
+    const int64_t s0 = std::min<int64_t>(last, a0 + (int64_t)w * seg);
     const int64_t s1 = std::min<int64_t>(last, s0 + seg);
     uint32_t cl = 0, cr = 0;
-    tt_scan_segment(A, first, s0, s1, piv, lane, [&](int64_t, bool lf, bool rf) {
-        cl += (uint32_t)__popcll(__ballot(lf));
-        cr += (uint32_t)__popcll(__ballot(rf));
-    });
+    {   // counting pass: 4 keys per lane and load, lane-local counts, one wave reduction
+        constexpr int kCU = 4;
+        for (int64_t b = s0; b < s1; b += (int64_t)kWave * 4 * kCU) {
+            uint4 kv[kCU];
+#pragma unroll
+            for (int u = 0; u < kCU; ++u) {
+                const int64_t q = b + 4 * ((int64_t)u * kWave + lane);
+                kv[u] = q < s1 ? *reinterpret_cast<const uint4*>(A.K + q) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < kCU; ++u) {
+                const int64_t q = b + 4 * ((int64_t)u * kWave + lane);
+                const uint32_t k4[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int64_t i = q + c;
+                    const bool in = i < s1 && i >= first;
+                    cl += (in && i > first && k4[c] <= piv) ? 1u : 0u;
+                    cr += (in && k4[c] >= piv) ? 1u : 0u;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) {
+            cl += __shfl_xor(cl, o, kWave);
+            cr += __shfl_xor(cr, o, kWave);
+        }
+    }
     if (lane == 0) {
         sh.wl[w] = cl;
         sh.wr[w] = cr;

@@ -1129,6 +1129,33 @@ int eden_check(int64_t n, int64_t dim, int32_t nbits, const int8_t* signs, EdenT
     return UQ_OK;
 }
 
+// A second stream per device and thread (plus fork / join events) for work that can run
+// beside the caller's stream inside one call; joined back before the call returns.
+struct SideStream {
+    hipStream_t s;
+    hipEvent_t fork, join;
+};
+
+int side_stream(SideStream** out) {
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc) return rc;
+    static thread_local SideStream cache[64];
+    static thread_local bool made[64] = {};
+    if (dev < 0 || dev >= 64) return fail(UQ_E_INVALID, "device index out of range");
+    if (!made[dev]) {
+        rc = hip_check(hipStreamCreateWithFlags(&cache[dev].s, hipStreamNonBlocking), "create side stream");
+        if (rc) return rc;
+        rc = hip_check(hipEventCreateWithFlags(&cache[dev].fork, hipEventDisableTiming), "create event");
+        if (rc) return rc;
+        rc = hip_check(hipEventCreateWithFlags(&cache[dev].join, hipEventDisableTiming), "create event");
+        if (rc) return rc;
+        made[dev] = true;
+    }
+    *out = &cache[dev];
+    return UQ_OK;
+}
+
 int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, float fm, RezState* state,
                       uint32_t* bits, char* wsb, const BiasedLayout& w, hipStream_t st) {
     int rc = hip_check(hipMemsetAsync(bits, 0, (size_t)n * ((d + 31) / 32) * sizeof(uint32_t), st), "memset tie bits");
@@ -1416,23 +1443,51 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
 #undef UQ_RADIX
     rc = hip_check(hipGetLastError(), "radix select launch");
     if (rc) return rc;
+    auto output = [&](hipStream_t os, int part) {
+        if (vec4)
+            hipLaunchKernelGGL(rez_output_kernel<true>, tgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
+                               w.tiles, bits, part);
+        else
+            hipLaunchKernelGGL(rez_output_kernel<false>, tgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
+                               w.tiles, bits, part);
+        return hip_check(hipGetLastError(), "rez_output_kernel launch");
+    };
+    auto tiecount = [&](hipStream_t ts) {
+        // index-order tie ranks (ambiguous clients that KB7 did not replay)
+        if (vec4)
+            hipLaunchKernelGGL(rez_tiecount_kernel<true>, tgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles);
+        else
+            hipLaunchKernelGGL(rez_tiecount_kernel<false>, tgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles);
+        return hip_check(hipGetLastError(), "rez_tiecount_kernel launch");
+    };
     if (tie_policy == UQ_TIES_TORCH) {
-        rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, st);
+        // fork: KB7 (few workgroups, latency-bound) on the side stream while KB6 writes the
+        // clients without a threshold tie on the caller's stream; join, then the rest
+        SideStream* sb = nullptr;
+        rc = side_stream(&sb);
+        if (rc) return rc;
+        rc = hip_check(hipEventRecord(sb->fork, st), "record fork");
+        if (rc) return rc;
+        rc = hip_check(hipStreamWaitEvent(sb->s, sb->fork, 0), "wait fork");
+        if (rc) return rc;
+        rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s);
+        if (rc) return rc;
+        rc = tiecount(sb->s);
+        if (rc) return rc;
+        rc = hip_check(hipEventRecord(sb->join, sb->s), "record join");
+        if (rc) return rc;
+        rc = output(st, 1);
+        if (rc) return rc;
+        rc = hip_check(hipStreamWaitEvent(st, sb->join, 0), "wait join");
+        if (rc) return rc;
+        rc = output(st, 2);
+        if (rc) return rc;
+    } else {
+        rc = tiecount(st);
+        if (rc) return rc;
+        rc = output(st, 0);
         if (rc) return rc;
     }
-    // index-order tie ranks (used by ambiguous clients that KB7 did not replay)
-    if (vec4)
-        hipLaunchKernelGGL(rez_tiecount_kernel<true>, tgrid, dim3(256), 0, st, x, d, l1buf, fm, state, tcnt, w.tiles);
-    else
-        hipLaunchKernelGGL(rez_tiecount_kernel<false>, tgrid, dim3(256), 0, st, x, d, l1buf, fm, state, tcnt, w.tiles);
-    rc = hip_check(hipGetLastError(), "rez_tiecount_kernel launch");
-    if (rc) return rc;
-    if (vec4)
-        hipLaunchKernelGGL(rez_output_kernel<true>, tgrid, dim3(256), 0, st, x, out, d, l1buf, fm, state, tcnt, w.tiles, bits);
-    else
-        hipLaunchKernelGGL(rez_output_kernel<false>, tgrid, dim3(256), 0, st, x, out, d, l1buf, fm, state, tcnt, w.tiles, bits);
-    rc = hip_check(hipGetLastError(), "rez_output_kernel launch");
-    if (rc) return rc;
     if (l1_out) {
         rc = hip_check(hipMemcpyAsync(l1_out, l1buf, n * sizeof(float), hipMemcpyDeviceToDevice, st), "copy l1");
         if (rc) return rc;
