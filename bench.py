@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--bits", type=float, default=1)
     ap.add_argument("--torch-threads", type=int, default=1)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--dist", choices=["normal", "laplace", "uniform"], default="normal",
+                    help="client vectors: N(0,1) (C2), Laplace(1,2) as Laplace_dist.py:89 or U(-1,1) (C3 sweeps)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/pmc_*.json)")
@@ -106,7 +108,16 @@ def main():
 
     # ---- synthetic inputs resident in HBM (generation is outside the timed region) ----
     g = torch.Generator(device=dev).manual_seed(args.seed + 7919 * rank)
-    x = torch.randn(n, d, generator=g, device=dev, dtype=torch.float32)
+    if args.dist == "normal":
+        x = torch.randn(n, d, generator=g, device=dev, dtype=torch.float32)
+    elif args.dist == "laplace":        # loc 1, scale 2 by inversion of a uniform draw
+        # u in (-1/2, 1/2) strictly (|u| = 1/2 would invert to -inf): clamp to 1/2 - 2^-25
+        lim = 0.5 - 2.0 ** -25
+        u = (torch.rand(n, d, generator=g, device=dev, dtype=torch.float32) - 0.5).clamp_(-lim, lim)
+        x = 1.0 - 2.0 * torch.sign(u) * torch.log1p(-2.0 * u.abs())
+        del u
+    else:
+        x = torch.rand(n, d, generator=g, device=dev, dtype=torch.float32) * 2.0 - 1.0
     X_cpu = torch.rand(n_total, generator=torch.Generator().manual_seed(args.seed))[rank * n:(rank + 1) * n]
     X = X_cpu.to(dev)
     q = torch.empty_like(x)
@@ -209,9 +220,15 @@ def main():
             "metric": METRIC, "value": round(value, 6), "unit": "M-vectors/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: i.i.d. N(0,1) f32 per client (torch CUDA generator), X ~ U[0,1) from a CPU generator",
-            "config": {"workload": "C2 (BASELINE.json configs[1]): 1024 clients/GPU x d=2^20, Gaussian, R=1, "
-                                   "unbiased L1 type quantizer + client-ordered mean" + (" + RCCL reduce" if world > 1 else ""),
+            "data": {"normal": "synthetic: i.i.d. N(0,1) f32 per client (torch CUDA generator)",
+                     "laplace": "synthetic: i.i.d. Laplace(1,2) f32 per client (torch CUDA generator, inversion)",
+                     "uniform": "synthetic: i.i.d. U(-1,1) f32 per client (torch CUDA generator)"}[args.dist]
+                    + ", X ~ U[0,1) from a CPU generator",
+            "config": {"workload": ("C2 (BASELINE.json configs[1]): 1024 clients/GPU x d=2^20, Gaussian, R=1, "
+                                    if args.dist == "normal" else
+                                    f"C3-style sweep (BASELINE.json configs[2]): {n} clients/GPU x d=2^20, {args.dist}, R=1, ")
+                                   + "unbiased L1 type quantizer + client-ordered mean" + (" + RCCL reduce" if world > 1 else ""),
+                       "dist": args.dist,
                        "clients_per_gpu": n, "d": d, "bits_per_dimension": args.bits, "m": m,
                        "torch_threads_l1_order": T, "parallelism": f"client-sharded x{world}",
                        "mean_mode": args.mean_mode if world > 1 else "single", "pipeline": args.pipeline},
