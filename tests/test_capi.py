@@ -76,3 +76,29 @@ def test_drop_in_signature_and_name():
     sig = inspect.signature(f)
     assert list(sig.parameters) == ["input_vector", "bits_per_dimension"]
     assert sig.parameters["bits_per_dimension"].default == 1
+
+
+def test_biased_and_eden_argument_errors(lib):
+    """Host-side validation of the biased / EDEN / RHT entry points (no kernel launched)."""
+    import ctypes
+    from uqdme_amd import _lib as L
+    for name, (res, args) in L.SIGNATURES.items():
+        getattr(lib, name).restype = res
+        getattr(lib, name).argtypes = args
+    b = ctypes.c_size_t(0)
+    assert lib.uq_biased_workspace_bytes(4, 1000, 1, ctypes.byref(b)) == 0 and b.value > 0
+    assert lib.uq_biased_workspace_bytes(-1, 1000, 1, ctypes.byref(b)) < 0
+    assert lib.uq_eden_workspace_bytes(4, 1000, ctypes.byref(b)) == 0 and b.value > 0
+    # bad n / m / torch_threads / tie policy are rejected before any device work
+    assert lib.uq_type_biased_f32(None, None, -1, 10, 2, 1, 0, None, None, None, 0, None) < 0
+    assert lib.uq_type_biased_f32(None, None, 1, 10, -2, 1, 0, None, None, None, 0, None) < 0
+    assert lib.uq_type_biased_f32(None, None, 1, 10, 2, 0, 0, None, None, None, 0, None) < 0
+    assert lib.uq_type_biased_f32(None, None, 1, 10, 2, 1, 7, None, None, None, 0, None) < 0
+    assert b"tie_policy" in lib.uq_last_error()
+    assert lib.uq_type_biased_f32(None, None, 0, 10, 2, 1, 0, None, None, None, 0, None) == 0   # n = 0: no-op
+    # EDEN: only the reference's 1- and 2-bit tables
+    assert lib.uq_eden_compress_f32(None, 1, 16, 3, None, None, None, None, None, 0, None) < 0
+    assert b"nbits" in lib.uq_last_error()
+    assert lib.uq_eden_f32(None, None, 0, 16, 1, None, None, None, None, 0, None) == 0
+    assert lib.uq_rht_f32(None, None, -1, 16, 0, None, None, None, 0, None) < 0
+    assert lib.uq_rht_signs(None, -1, 16, None, None) < 0
