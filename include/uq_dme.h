@@ -121,7 +121,8 @@ int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax,
  *                         the threshold, i.e. info flag 1 is clear)
  * l1_out [n] f32 or NULL.  info [n][2] int32 or NULL: {Delta, flags}; flags bit0 = a tie
  * straddled the threshold, bit1 = m' not finite (the reference raises; output is NaN-laden),
- * bit2 = |Delta| > d (the reference's topk raises), bit3 = torch tie choice replayed.
+ * bit2 = |Delta| > d (the reference's topk raises), bit3 = torch tie choice replayed,
+ * bit4 = threshold digits 2-3 found on the compacted first-digit bucket (informational).
  * Workspace: uq_biased_workspace_bytes; zero-filled once before first use (it holds the
  * status word of uq_check_status, which reports an inconsistent tie replay). */
 #define UQ_TIES_TORCH 0

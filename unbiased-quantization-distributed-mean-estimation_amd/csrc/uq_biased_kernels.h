@@ -29,6 +29,7 @@ enum RezFlags : int32_t {
     kRezNonFinite = 2,     // m' is NaN/inf: the reference raises in int(m' - m) (AS:656)
     kRezRange = 4,         // |Delta| > d: torch.topk raises (cannot happen for finite input)
     kRezTorchTies = 8,     // selection set replayed with torch's tie choice (KB7)
+    kRezCompact = 16,      // threshold digits 2-3 found on the compacted first-digit bucket
 };
 
 struct RezState {          // 32 bytes per client; (delta, flags) are the public info pair
@@ -124,7 +125,7 @@ rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
     using RP = RadixPass<PASS>;
     const int64_t vec = blockIdx.y;
     const uint32_t kleft = st[vec].kleft;
-    if (kleft == 0) return;
+    if (kleft == 0 || (st[vec].flags & kRezCompact)) return;
     const uint32_t prefix = st[vec].prefix;
     const bool up = st[vec].delta > 0;
     __shared__ uint32_t h[kRadixBins];
@@ -163,24 +164,42 @@ rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
 }
 
 // KB4b: pick the digit holding the kleft-th largest key (one workgroup per client).
+// Pass 0 reads the histogram of +delta' made inside the k' sum (KB2) and mirrors it for
+// Delta < 0 (key(-v) = ~key(v) except for v = 0 and NaN, counted apart in zn).  When the
+// chosen first-digit bucket holds at most `cap` keys the client switches to candidate
+// compaction (KB4c/KB4d) instead of passes 1-2.
 template <int PASS>
 __global__ void __launch_bounds__(256)
-rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist) {
+rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ zn,
+                  uint32_t cap) {
     using RP = RadixPass<PASS>;
     constexpr int nb = (int)RP::dmask + 1;
     constexpr int per = nb / 256;
     const int64_t vec = blockIdx.x;
     const uint32_t kleft = st[vec].kleft;
     if (kleft == 0) return;
+    if (PASS > 0 && (st[vec].flags & kRezCompact)) return;
     __shared__ uint32_t lds[4];
     const int tid = threadIdx.x;
     const uint32_t* h = hist + ((size_t)vec * 3 + PASS) * kRadixBins;
+    const bool mirror = PASS == 0 && st[vec].delta < 0;
+    const uint32_t z = PASS == 0 ? zn[vec * 2] : 0u, nn = PASS == 0 ? zn[vec * 2 + 1] : 0u;
+    auto count = [&](int b) -> uint32_t {
+        if (!mirror) return h[b];
+        const int src = nb - 1 - b;              // top digit of ~key
+        uint32_t c = h[src];
+        if (src == 1024) c -= z;                 // zeros and NaNs do not move
+        if (src == 2046) c -= nn;
+        if (b == 1024) c += z;
+        if (b == 2046) c += nn;
+        return c;
+    };
     // thread t owns bins [nb - (t+1)*per, nb - t*per): thread 0 the highest digits
     const int hi = nb - tid * per;
     uint32_t c[per], sum = 0;
 #pragma unroll
     for (int k = 0; k < per; ++k) {
-        c[k] = h[hi - 1 - k];
+        c[k] = count(hi - 1 - k);
         sum += c[k];
     }
     uint32_t total;
@@ -193,6 +212,10 @@ rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist) 
                 RezState s = st[vec];
                 s.prefix |= digit << RP::shift;
                 s.kleft = kleft - above;
+                if (PASS == 0 && c[k] <= cap) {
+                    s.flags |= kRezCompact;
+                    s.eq = c[k];                 // keys in the bucket = candidates to compact
+                }
                 if (PASS == 2) {
                     s.eq = c[k];
                     s.need = s.kleft;
@@ -204,6 +227,114 @@ rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist) 
             above += c[k];
         }
     }
+}
+
+// KB4c: compact the keys of the chosen first-digit bucket (compact-mode clients).  Each
+// thread keeps its 64 keys in registers (16 float4 loads, coalesced), counts the matches,
+// one block scan + one atomic per workgroup reserves the output range.
+template <bool VEC4>
+__global__ void __launch_bounds__(256)
+rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
+                   const RezState* __restrict__ st, uint32_t* __restrict__ cand, uint32_t* __restrict__ cand_n,
+                   uint32_t cap) {
+    const int64_t vec = blockIdx.y;
+    if (st[vec].kleft == 0 || !(st[vec].flags & kRezCompact)) return;
+    const uint32_t prefix = st[vec].prefix;
+    const bool up = st[vec].delta > 0;
+    const float den = l1[vec] + 1e-12f;
+    const float* xv = x + vec * d;
+    const int tid = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * kHistSpan;
+    __shared__ uint32_t lds[4];
+    __shared__ uint32_t s_base;
+    uint32_t key[kHistItems];
+    uint64_t match = 0;
+#pragma unroll
+    for (int j = 0; j < kHistItems / 4; ++j) {
+        const int64_t i = b0 + 4 * ((int64_t)j * 256 + tid);          // elements i .. i+3
+        float v[4];
+        if (VEC4 && i + 3 < d) {
+            const float4 t = *reinterpret_cast<const float4*>(xv + i);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = (i + c < d) ? xv[i + c] : 0.f;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float kp;
+            key[4 * j + c] = rez_elem(v[c], den, fm, up, kp);
+            if (i + c < d && (key[4 * j + c] & 0xFFE00000u) == prefix) match |= 1ull << (4 * j + c);
+        }
+    }
+    uint32_t tot;
+    uint32_t off = block_excl_scan_u32((uint32_t)__popcll(match), lds, &tot);
+    if (tid == 0) s_base = tot ? atomicAdd(&cand_n[vec], tot) : 0u;
+    __syncthreads();
+    off += s_base;
+    uint32_t* cv = cand + (size_t)vec * cap;
+#pragma unroll
+    for (int e = 0; e < kHistItems; ++e)
+        if (((match >> e) & 1ull) && off < cap) cv[off++] = key[e];
+}
+
+// KB4d: digits 2 and 3 on the candidates (one workgroup per compact-mode client).
+__global__ void __launch_bounds__(256)
+rez_cand_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ cand,
+                       const uint32_t* __restrict__ cand_n, uint32_t cap) {
+    const int64_t vec = blockIdx.x;
+    if (st[vec].kleft == 0 || !(st[vec].flags & kRezCompact)) return;
+    __shared__ uint32_t h[kRadixBins];
+    __shared__ uint32_t lds[4];
+    const int tid = threadIdx.x;
+    const uint32_t nc = std::min(cand_n[vec], cap);
+    const uint32_t* cv = cand + (size_t)vec * cap;
+    RezState s = st[vec];
+    for (int pass = 1; pass <= 2; ++pass) {
+        const int shift = pass == 1 ? 10 : 0;
+        const uint32_t dmask = pass == 1 ? 0x7FFu : 0x3FFu;
+        const uint32_t hmask = pass == 1 ? 0xFFE00000u : 0xFFFFFC00u;
+        const int nb = (int)dmask + 1;
+        for (int b = tid; b < kRadixBins; b += 256) h[b] = 0u;
+        __syncthreads();
+        for (uint32_t i = tid; i < nc; i += 256) {
+            const uint32_t key = cv[i];
+            if ((key & hmask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
+        }
+        __syncthreads();
+        const int per = nb / 256;
+        const int hi = nb - tid * per;
+        uint32_t c[8], sum = 0;
+        for (int k = 0; k < per; ++k) {
+            c[k] = h[hi - 1 - k];
+            sum += c[k];
+        }
+        __shared__ uint32_t s_digit, s_above, s_eq;
+        if (tid == 0) { s_digit = 0u; s_above = 0u; s_eq = 0u; }
+        uint32_t total;
+        uint32_t above = block_excl_scan_u32(sum, lds, &total);
+        if (above < s.kleft && above + sum >= s.kleft) {
+            for (int k = 0; k < per; ++k) {
+                if (above + c[k] >= s.kleft) {
+                    s_digit = (uint32_t)(hi - 1 - k);
+                    s_above = above;
+                    s_eq = c[k];
+                    break;
+                }
+                above += c[k];
+            }
+        }
+        __syncthreads();
+        s.prefix |= s_digit << shift;
+        s.kleft -= s_above;
+        if (pass == 2) {
+            s.eq = s_eq;
+            s.need = s.kleft;
+            if (s.eq > s.need) s.flags |= kRezAmbiguous;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) st[vec] = s;
 }
 
 // KB5: keys equal to the threshold per tile (ambiguous clients only).

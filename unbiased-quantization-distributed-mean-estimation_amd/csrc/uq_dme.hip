@@ -120,16 +120,44 @@ __device__ __forceinline__ uint32_t ld_relaxed_agent32(const uint32_t* p) {
 // Element transforms summed by the K1 cascade.  The cascade itself (order of f32 adds)
 // is the torch CPU `sum` order whatever is summed.
 struct AbsOp {            // AS:624  input_vector.abs().sum()
+    static constexpr bool kHist = false;   // no radix-digit histogram (see RezKHistOp)
     float den, fm;
-    __device__ static AbsOp make(const float*, float, int64_t) { return AbsOp{0.f, 0.f}; }
+    uint32_t *h, *zn;
+    __device__ static AbsOp make(const float*, float, int64_t) { return AbsOp{0.f, 0.f, nullptr, nullptr}; }
     __device__ float operator()(float v) const { return fabsf(v); }
 };
 struct RezKOp {           // AS:648-649  k' = floor(m * p + 0.5), p = |x| / (L1 + 1e-12)
+    static constexpr bool kHist = false;
     float den, fm;
+    uint32_t *h, *zn;
     __device__ static RezKOp make(const float* l1, float fm, int64_t vec) {
-        return RezKOp{l1[vec] + 1e-12f, fm};
+        return RezKOp{l1[vec] + 1e-12f, fm, nullptr, nullptr};
     }
     __device__ float operator()(float v) const { return floorf(fm * (fabsf(v) / den) + 0.5f); }
+};
+// RezKOp that also counts the top 11 bits of the order key of +delta' = k' - m p into
+// h[2048] (the biased quantizer's first radix digit, KB4 pass 0), and delta' == 0 / NaN
+// elements into zn[0] / zn[1] so that the histogram of -delta' can be mirrored from it.
+// h / zn point to LDS in K1a (flushed per workgroup) and to global memory in K1b.
+struct RezKHistOp {
+    static constexpr bool kHist = true;
+    float den, fm;
+    uint32_t *h, *zn;
+    __device__ static RezKHistOp make(const float* l1, float fm, int64_t vec) {
+        return RezKHistOp{l1[vec] + 1e-12f, fm, nullptr, nullptr};
+    }
+    __device__ float operator()(float v) const {
+        const float mp = fm * (fabsf(v) / den);
+        const float kp = floorf(mp + 0.5f);
+        float dp = (kp - mp) + 0.0f;
+        uint32_t u = __float_as_uint(dp);
+        if (dp != dp) u = 0x7FC00000u;
+        const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        atomicAdd(&h[key >> 21], 1u);
+        if (key == 0x80000000u) atomicAdd(&zn[0], 1u);
+        else if (key == 0xFFC00000u) atomicAdd(&zn[1], 1u);
+        return kp;
+    }
 };
 
 // =====================================================================================
@@ -141,9 +169,16 @@ struct RezKOp {           // AS:648-649  k' = floor(m * p + 0.5), p = |x| / (L1 
 template <bool VEC4, class Op>
 __global__ void __launch_bounds__(256)
 l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __restrict__ part,
-                  const float* __restrict__ l1, float fm) {
+                  const float* __restrict__ l1, float fm, uint32_t* __restrict__ hist_g, uint32_t* __restrict__ zn_g) {
     const int64_t vec = blockIdx.y;
-    const Op op = Op::make(l1, fm, vec);
+    Op op = Op::make(l1, fm, vec);
+    __shared__ uint32_t hs[Op::kHist ? 2048 + 2 : 1];
+    if (Op::kHist) {
+        for (int b = threadIdx.x; b < 2048 + 2; b += blockDim.x) hs[b] = 0u;
+        __syncthreads();
+        op.h = hs;
+        op.zn = hs + 2048;
+    }
     int32_t G = blockIdx.x;
     int c = 0;
     while (c + 1 < plan.nchunks && G >= plan.gbase[c + 1]) ++c;
@@ -179,6 +214,11 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
         for (int b = 0; b < step; ++b) acc += leaf[b * 32 + tid];
         part[(vec * plan.total_groups + G) * 32 + tid] = acc;
     }
+    if (Op::kHist) {
+        for (int b = tid; b < 2048; b += blockDim.x)
+            if (hs[b]) atomicAdd(&hist_g[(size_t)vec * 3 * 2048 + b], hs[b]);
+        if (tid < 2 && hs[2048 + tid]) atomicAdd(&zn_g[vec * 2 + tid], hs[2048 + tid]);
+    }
 }
 
 // Sequential sum of `nrows` rows of stream `a` starting at element `start`.
@@ -200,9 +240,14 @@ template <class Op>
 __global__ void __launch_bounds__(64)
 l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
                    const float* __restrict__ part, float* __restrict__ l1_out,
-                   const float* __restrict__ l1, float fm) {
+                   const float* __restrict__ l1, float fm, uint32_t* __restrict__ hist_g,
+                   uint32_t* __restrict__ zn_g) {
     const int64_t vec = blockIdx.x;
-    const Op op = Op::make(l1, fm, vec);
+    Op op = Op::make(l1, fm, vec);
+    if (Op::kHist) {                   // the few elements outside full level-1 groups
+        op.h = hist_g + (size_t)vec * 3 * 2048;
+        op.zn = zn_g + vec * 2;
+    }
     const int lane = threadIdx.x;
     const float* xv = x + vec * d;
     __shared__ float fin[32];
@@ -934,7 +979,7 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 template <class Op>
 int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* part, float* sum_out,
-                   const float* l1, float fm, hipStream_t st) {
+                   const float* l1, float fm, hipStream_t st, uint32_t* hist = nullptr, uint32_t* zn = nullptr) {
     if (plan.total_groups > 0) {
         bool vec4 = aligned16(x) && (d % 4 == 0);
         for (int c = 0; c < plan.nchunks; ++c) vec4 = vec4 && (plan.off[c] % 4 == 0);
@@ -944,13 +989,14 @@ int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, flo
         dim3 grid(plan.total_groups, (unsigned)n);
         dim3 block(8 * maxstep);
         if (vec4)
-            hipLaunchKernelGGL((l1_partial_kernel<true, Op>), grid, block, 0, st, x, d, plan, part, l1, fm);
+            hipLaunchKernelGGL((l1_partial_kernel<true, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn);
         else
-            hipLaunchKernelGGL((l1_partial_kernel<false, Op>), grid, block, 0, st, x, d, plan, part, l1, fm);
+            hipLaunchKernelGGL((l1_partial_kernel<false, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn);
         int rc = hip_check(hipGetLastError(), "l1_partial_kernel launch");
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(l1_finalize_kernel<Op>, dim3((unsigned)n), dim3(64), 0, st, x, d, plan, part, sum_out, l1, fm);
+    hipLaunchKernelGGL(l1_finalize_kernel<Op>, dim3((unsigned)n), dim3(64), 0, st, x, d, plan, part, sum_out, l1, fm,
+                       hist, zn);
     return hip_check(hipGetLastError(), "l1_finalize_kernel launch");
 }
 
@@ -1001,12 +1047,15 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
 }
 
 // Biased-quantizer workspace: [ctrl 256][K1 parts][l1 n][m' n][state n x 32B]
-// [hist n x 3 x 2048 u32][tie counts n x tiles u32][tie bits n x ceil(d/32) u32]
+// [hist n x 3 x 2048 u32][zero/NaN counts n x 2][candidate counts n][candidates n x cap u32]
+// [tie counts n x tiles u32][tie bits n x ceil(d/32) u32]
 // [KB7 slots: keys + indices S x 2d u32][KB7 positions S x 2d u32], S = min(n, kTieSlots)
 struct BiasedLayout {
-    size_t part_off, l1_off, msum_off, st_off, hist_off, tcnt_off, bits_off, pairs_off, pos_off, total;
+    size_t part_off, l1_off, msum_off, st_off, hist_off, zn_off, cn_off, cand_off, tcnt_off, bits_off, pairs_off,
+        pos_off, total;
     int32_t tiles;
     int32_t slots;
+    uint32_t cap;      // candidate capacity per client (compaction of the first-digit bucket)
 };
 
 BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
@@ -1018,7 +1067,11 @@ BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.msum_off = up(w.l1_off + (size_t)n * sizeof(float));
     w.st_off = up(w.msum_off + (size_t)n * sizeof(float));
     w.hist_off = up(w.st_off + (size_t)n * sizeof(RezState));
-    w.tcnt_off = up(w.hist_off + (size_t)n * 3 * kRadixBins * sizeof(uint32_t));
+    w.cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(d, 1), std::max<int64_t>(4096, d / 8));
+    w.zn_off = up(w.hist_off + (size_t)n * 3 * kRadixBins * sizeof(uint32_t));
+    w.cn_off = w.zn_off + (size_t)n * 2 * sizeof(uint32_t);           // zn and cand_n adjacent
+    w.cand_off = up(w.cn_off + (size_t)n * sizeof(uint32_t));
+    w.tcnt_off = up(w.cand_off + (size_t)n * w.cap * sizeof(uint32_t));
     w.bits_off = up(w.tcnt_off + (size_t)n * w.tiles * sizeof(uint32_t));
     w.slots = (int32_t)std::min<int64_t>(n, kTieSlots);
     w.pairs_off = up(w.bits_off + (size_t)n * ((d + 31) / 32) * sizeof(uint32_t));
@@ -1423,23 +1476,35 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     const float fm = (float)m;
     int rc = launch_l1(x, n, d, plan, part, l1buf, st);                                   // AS:680
     if (rc) return rc;
-    rc = launch_cascade<RezKOp>(x, n, d, plan, part, msum, l1buf, fm, st);               // AS:648-649
+    uint32_t* zn = (uint32_t*)(wsb + w.zn_off);
+    uint32_t* cand_n = (uint32_t*)(wsb + w.cn_off);
+    uint32_t* cand = (uint32_t*)(wsb + w.cand_off);
+    rc = hip_check(hipMemsetAsync(hist, 0, w.cand_off - w.hist_off, st), "memset hist/zn/cand_n");
+    if (rc) return rc;
+    // AS:648-649 m' = sum k' in torch order, with the first radix digit's histogram (KB2 + KB4 pass 0)
+    rc = launch_cascade<RezKHistOp>(x, n, d, plan, part, msum, l1buf, fm, st, hist, zn);
     if (rc) return rc;
     hipLaunchKernelGGL(rez_setup_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, msum, fm, d, n, state);
     rc = hip_check(hipGetLastError(), "rez_setup_kernel launch");
     if (rc) return rc;
-    rc = hip_check(hipMemsetAsync(hist, 0, (size_t)n * 3 * kRadixBins * sizeof(uint32_t), st), "memset hist");
-    if (rc) return rc;
     const bool vec4 = aligned16(x) && aligned16(out) && d % 4 == 0;
     const dim3 hgrid((unsigned)((d + kHistSpan - 1) / kHistSpan), (unsigned)n);
     const dim3 tgrid((unsigned)w.tiles, (unsigned)n);
+    hipLaunchKernelGGL(rez_select_kernel<0>, dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.cap);
+    // compact-mode clients: the chosen bucket's keys, then digits 2-3 on them
+    if (vec4)
+        hipLaunchKernelGGL(rez_compact_kernel<true>, hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
+    else
+        hipLaunchKernelGGL(rez_compact_kernel<false>, hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
+    hipLaunchKernelGGL(rez_cand_select_kernel, dim3((unsigned)n), dim3(256), 0, st, state, cand, cand_n, w.cap);
+    // the others: full-vector histogram passes for digits 2-3
 #define UQ_RADIX(P)                                                                                          \
     if (vec4)                                                                                                \
         hipLaunchKernelGGL((rez_hist_kernel<P, true>), hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist); \
     else                                                                                                     \
         hipLaunchKernelGGL((rez_hist_kernel<P, false>), hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist); \
-    hipLaunchKernelGGL(rez_select_kernel<P>, dim3((unsigned)n), dim3(256), 0, st, state, hist);
-    UQ_RADIX(0) UQ_RADIX(1) UQ_RADIX(2)
+    hipLaunchKernelGGL(rez_select_kernel<P>, dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.cap);
+    UQ_RADIX(1) UQ_RADIX(2)
 #undef UQ_RADIX
     rc = hip_check(hipGetLastError(), "radix select launch");
     if (rc) return rc;
