@@ -189,3 +189,18 @@ def test_drop_in_matches_reference_fixtures(uq, cases):
         finally:
             uq.set_torch_threads(None)
         assert G.bits_equal(y, q), sp["idx"]
+
+
+def test_c4_size_2pow22_vs_oracle(uq):
+    """Config C4's d = 2^22, torch ties: Gaussian (compaction path) and tie-heavy integers
+    (full radix passes + KB7 replay) bit-exact against the oracle's libstdc++ replay."""
+    rng = np.random.default_rng(42)
+    d = 1 << 22
+    for x in (rng.standard_normal(d).astype(f32), rng.integers(-3, 4, d).astype(f32)):
+        for R in (1, 2):
+            m = rate_to_m(R, d)
+            exp, _, D, A = C.biased_quantize(x, m, 1, 0)
+            out, info = run(uq, x, R, 1, "torch")
+            assert info[0] == D and bool(info[1] & 1) == A
+            assert G.bits_equal(out, exp), (R, G.n_mismatch(out, exp))
+    uq.check_status()

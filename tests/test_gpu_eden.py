@@ -94,3 +94,18 @@ def test_rht_forward_inverse_vs_reference(uq, fx):
         assert G.sha(i) == r["inv_sha"], r
         if f"rfwd{r['k']}" in z.files:
             assert G.bits_equal(f, z[f"rfwd{r['k']}"])
+
+
+def test_eden_c4_size_2pow22_vs_oracle(uq):
+    """d = 2^22 (three FWHT passes: 12 + 8 + 2 bits) and a padded d = 2^22 - 3."""
+    rng = np.random.default_rng(9)
+    for d in (1 << 22, (1 << 22) - 3):
+        x = rng.standard_normal(d).astype(np.float32)
+        for nbits in (1, 2):
+            out, scale = uq.eden_quantize(torch.as_tensor(x).cuda().view(1, -1), nbits, seeds=[37],
+                                          return_scale=True)
+            bins, sc, _, _ = E.eden_compress(x, nbits, 37)
+            sg = float(scale.cpu()[0])
+            assert abs(sg - float(sc)) <= 2 * np.spacing(np.float32(abs(sc)))
+            exp = E.eden_decompress(bins, np.float32(sg), nbits, 37, d)
+            assert G.bits_equal(out.cpu().numpy()[0], exp), (d, nbits)
