@@ -176,6 +176,10 @@ def main():
         return e0.elapsed_time(e1) / steps
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    for _ in range(args.warmup):                  # W untimed warmup steps
+        step()
+    torch.cuda.synchronize()
+    _lib.check(lib.uq_check_status(P(ws), sp), "status after warmup")
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -202,6 +206,10 @@ def main():
     alg_bytes = float(d * n) * (4 + (4 if args.pipeline in ("q", "codes") else 0) + (1 if args.pipeline != "q" else 0))
     achieved = alg_bytes / (q_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(args.traffic_json, d, n, args.pipeline)
+    # CPU baseline + parity sample on the timed steps' own output q (before any side line)
+    base = parity = None
+    if world == 1 and not args.no_cpu_baseline:
+        base, parity = cpu_baseline(args, x, X_cpu, q, m, T)
     side = {}
     if args.side_pipelines and world == 1:
         for pl in ("q", "codes", "encode"):
@@ -209,7 +217,7 @@ def main():
                 ms = time_pipeline(pl, max(3, args.steps // 2))
                 side[pl] = {"ms_per_step": round(ms, 4), "value": round(n_total / ms / 1e3, 6)}
         _lib.check(lib.uq_check_status(P(ws), sp), "status after side pipelines")
-        side["biased"] = time_biased(uqdme, x, q, args.bits, T, max(3, args.steps // 2))
+        side["biased"] = time_biased(uqdme, x, args.bits, T, max(3, args.steps // 2))
         side["eden"] = time_eden(uqdme, x, q, max(3, args.steps // 2))
         if int(torch.count_nonzero(ovf > 127)):
             raise RuntimeError("type-code overflow in the bench workload")
@@ -240,18 +248,19 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes},
         }
-        if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"], result["parity_sample"] = cpu_baseline(args, x, X_cpu, q, m, T)
+        if base is not None:
+            result["cpu_baseline"], result["parity_sample"] = base, parity
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def time_biased(uqdme, x, q, bits, T, steps):
+def time_biased(uqdme, x, bits, T, steps):
     """Side line: the biased type quantizer (AS:669-687, torch tie policy) on the same
-    resident batch, one uq_type_biased_f32 call per step (x -> q)."""
+    resident batch, one uq_type_biased_f32 call per step (into its own output buffer)."""
     n, d = x.shape
+    q = torch.empty_like(x)
     m = uqdme.rate_to_m(bits, d)
     for _ in range(2):
         uqdme.biased_quantize(x, m=m, torch_threads=T, ties="torch", out=q)
