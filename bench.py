@@ -7,15 +7,17 @@
 Workload (BASELINE.json configs[1], "C2"): per GPU, n=1024 client vectors of d=2^20
 i.i.d. N(0,1) f32, resident in HBM before timing; rate R=1 (m = 224426); L1 in the
 torch-CPU order of 1 thread.  One step = one pass of the hot path over the batch:
-    K1 torch-order L1 (AS:624)  ->  K2 fused quantize/dequantize (AS:625-640, writes q)
-    ->  K3 client-ordered mean (ND:137-138)  ->  [N>1] one RCCL reduce of est to rank 0.
+    K1 torch-order L1 (AS:624)  ->  K2 fused quantize/dequantize (AS:625-640; writes the
+    dequantized q and the int8 type codes)  ->  K3c client-ordered mean from the codes
+    (ND:137-138, bit-identical to the mean of q)  ->  [N>1] one RCCL reduce of est to rank 0.
+(--pipeline q: K2 writes q only and K3 reads q; --pipeline encode: codes only.)
 Clients shard across GPUs with no data-path collective except that final reduce
 (weak scaling: 1024 clients per GPU).  value = all clients processed / max-over-ranks
 time, in M-vectors/s.
 
 Rank 0 prints ONE JSON line.  `roofline` is computed for K2 from HIP events recorded
-around its launches inside the timed region (algorithmic bytes = 8*d per vector: read
-x + write q).  `cpu_baseline` times the C restatement of the reference path (oracle/,
+around its launches inside the timed region (algorithmic bytes = 9*d per vector: read x,
+write q, write codes; 8*d for --pipeline q, 5*d for encode).  W warmup steps run first.  `cpu_baseline` times the C restatement of the reference path (oracle/,
 the checker) on this host for a bounded sample of the same clients, and the same
 sample doubles as a bit-parity and NMSE check of the GPU output.
 """
