@@ -591,7 +591,8 @@ __device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const 
         const float4 fr4 = *reinterpret_cast<const float4*>(&s_fr[a]);
         const float fls[4] = {fl4.x, fl4.y, fl4.z, fl4.w};
         const float frs[4] = {fr4.x, fr4.y, fr4.z, fr4.w};
-        float o[4];
+        float o[4], kfs[4];
+        bool off_table = false;
         uint32_t w = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -600,16 +601,19 @@ __device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const 
             const float r = (fcur - fprev == 1.0f) ? 1.0f : 0.0f;   // AS:636-637
             fprev = fcur;
             const float kf = fabsf(fls[c]) + r;                // fl + r
+            kfs[c] = kf;
             if (WQ) {
-                float ov;
-                if (__builtin_expect(kf < (float)kTab, 1)) {
-                    ov = copysignf(s_tab[(int)kf], fls[c]);    // AS:640 via the table
-                } else {
-                    ov = (copysignf(L, fls[c]) * kf) / fm;     // AS:640 ((L1*sign)*(fl+r))/m
-                }
-                o[c] = ov;
+                // AS:640 via the table; the index is clamped so the four LDS reads issue
+                // together, and k >= kTab / NaN are recomputed below (rare)
+                o[c] = copysignf(s_tab[(int)fminf(kf, (float)(kTab - 1))], fls[c]);
+                off_table |= !(kf < (float)kTab);
             }
             if (WC) w |= code_of(fls[c], kf, kmax) << (8 * c);   // padding elements: fl = 0, r = 0
+        }
+        if (WQ && __builtin_expect(off_table, 0)) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (!(kfs[c] < (float)kTab)) o[c] = (copysignf(L, fls[c]) * kfs[c]) / fm;   // ((L1*sign)*(fl+r))/m
         }
         if (WQ) *reinterpret_cast<float4*>(&s_x[a]) = make_float4(o[0], o[1], o[2], o[3]);
         if (WC) cw[k4] = w;
