@@ -229,3 +229,15 @@ def test_client_mean_order_and_accumulate(uq):
         if n // 2 + 1 < n:
             est = uq.client_mean(dev(q[n // 2 + 1:]), n, est=est, accumulate=True)
         assert G.bits_equal(est.cpu().numpy(), C.client_mean(q, n)), (n, d, "split")
+
+
+def test_single_row_ragged_d_vector_path_and_many_threads(uq):
+    """n = 1 uses the vector loads for any d (the row is 16-byte aligned); the ragged end
+    must not read past d.  torch_threads > 64 is accepted while the chunk count is <= 64."""
+    rng = np.random.default_rng(77)
+    for d in (172554, 4097, 8195, 1 << 16 | 3):
+        x = rng.standard_normal(d).astype(f32)
+        for T in (1, 8, 128):
+            q = uq.quantize_dequantize(dev(x).view(1, d), 1, X=[0.37], torch_threads=T).cpu().numpy()[0]
+            exp = C.quantize_batch(x[None], O.rate_to_m(1, d), np.array([0.37], f32), T)[0][0]
+            assert G.bits_equal(q, exp), (d, T, G.n_mismatch(q, exp))

@@ -425,7 +425,14 @@ __device__ __forceinline__ void load_tile(TileRegs& r, const float* __restrict__
 #pragma unroll
         for (int j = 0; j < kQItems / 4; ++j) {
             const int64_t e = (int64_t)(tid + j * kQBlock) * 4;
-            r.v[j] = e < rem ? reinterpret_cast<const float4*>(xt)[tid + j * kQBlock] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e + 3 < rem) {
+                r.v[j] = reinterpret_cast<const float4*>(xt)[tid + j * kQBlock];
+            } else {                              // ragged end of the row: never read past d
+                r.v[j].x = e < rem ? xt[e] : 0.f;
+                r.v[j].y = e + 1 < rem ? xt[e + 1] : 0.f;
+                r.v[j].z = e + 2 < rem ? xt[e + 2] : 0.f;
+                r.v[j].w = 0.f;
+            }
         }
     } else {
 #pragma unroll
@@ -985,7 +992,7 @@ template <class Op>
 int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* part, float* sum_out,
                    const float* l1, float fm, hipStream_t st, uint32_t* hist = nullptr, uint32_t* zn = nullptr) {
     if (plan.total_groups > 0) {
-        bool vec4 = aligned16(x) && (d % 4 == 0);
+        bool vec4 = aligned16(x) && (d % 4 == 0 || n == 1);
         for (int c = 0; c < plan.nchunks; ++c) vec4 = vec4 && (plan.off[c] % 4 == 0);
         int maxstep = 16;
         for (int c = 0; c < plan.nchunks; ++c) maxstep = std::max(maxstep, 1 << plan.lp[c]);
@@ -1038,8 +1045,8 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
                  L1Plan* plan, WsLayout* w) {
     if (n < 0 || d < 0) return fail(UQ_E_INVALID, "n and d must be >= 0");
     if (n > (int64_t)1 << 31 || d > (int64_t)1 << 40) return fail(UQ_E_INVALID, "n or d too large");
-    if (T < 1 || T > kMaxChunks) return fail(UQ_E_INVALID, "torch_threads must be in [1, 64]");
-    if (!make_plan(d, T, plan)) return fail(UQ_E_INVALID, "cannot build L1 plan for this d/torch_threads");
+    if (T < 1) return fail(UQ_E_INVALID, "torch_threads must be >= 1");
+    if (!make_plan(d, T, plan)) return fail(UQ_E_INVALID, "more than 64 torch-order sum chunks (min(torch_threads, ceil(d/32768)) > 64) unsupported");
     *w = layout(n, d, *plan);
     if ((int64_t)w->tiles * n > 0xFFFFFFFFll) return fail(UQ_E_INVALID, "batch too large for one call");
     if (n > 0 && d > 0) {
@@ -1250,7 +1257,7 @@ int uq_rate_to_m(double bits, int64_t d, int64_t* m_out) {
 int uq_workspace_bytes(int64_t n, int64_t d, int32_t T, size_t* bytes_out) {
     if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
     L1Plan plan;
-    if (n < 0 || d < 0 || T < 1 || T > kMaxChunks) return fail(UQ_E_INVALID, "bad n/d/torch_threads");
+    if (n < 0 || d < 0 || T < 1) return fail(UQ_E_INVALID, "bad n/d/torch_threads");
     if (!make_plan(d, T, &plan)) return fail(UQ_E_INVALID, "cannot build L1 plan");
     *bytes_out = layout(n, d, plan).total;
     return UQ_OK;
@@ -1300,7 +1307,8 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
         if (rc) return rc;
     }
     const float fm = (float)m;   // torch casts the Python int to f32 for `m * p` and `/ m`
-    const bool vec4 = aligned16(x) && (!out || aligned16(out)) && (d % 4 == 0);
+    // rows are 16-byte aligned when d % 4 == 0, or when there is only one row
+    const bool vec4 = aligned16(x) && (!out || aligned16(out)) && (d % 4 == 0 || n == 1);
     const bool cvec = !codes || (aligned16(codes) && d % 16 == 0);
     const int wq = out ? 1 : 0, wc = codes ? 1 : 0;
     const int sel = (vec4 ? 8 : 0) | (wq ? 4 : 0) | (wc ? 2 : 0) | (cvec ? 1 : 0);
@@ -1439,7 +1447,7 @@ int uq_debug_set_tie_prof(void* dev_counters) {
 int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t T, size_t* bytes_out) {
     if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
     L1Plan plan;
-    if (n < 0 || d < 0 || T < 1 || T > kMaxChunks) return fail(UQ_E_INVALID, "bad n/d/torch_threads");
+    if (n < 0 || d < 0 || T < 1) return fail(UQ_E_INVALID, "bad n/d/torch_threads");
     if (!make_plan(d, T, &plan)) return fail(UQ_E_INVALID, "cannot build L1 plan");
     *bytes_out = biased_layout(n, d, plan).total;
     return UQ_OK;
@@ -1452,7 +1460,7 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     if (m < 0) return fail(UQ_E_INVALID, "m must be >= 0");
     if (d >= ((int64_t)1 << 31)) return fail(UQ_E_INVALID, "d must be < 2^31");
     if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 clients per call");
-    if (T < 1 || T > kMaxChunks) return fail(UQ_E_INVALID, "torch_threads must be in [1, 64]");
+    if (T < 1) return fail(UQ_E_INVALID, "torch_threads must be >= 1");
     if (tie_policy != UQ_TIES_LOWEST_INDEX && tie_policy != UQ_TIES_TORCH)
         return fail(UQ_E_INVALID, "unknown tie_policy");
     L1Plan plan;
