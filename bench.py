@@ -67,15 +67,24 @@ def parse():
     return ap.parse_args()
 
 
+# RCCL (backend "nccl") is the product path.  UQDME_BENCH_BACKEND=gloo is a rehearsal knob
+# that lets several ranks share one GPU; it stages the one reduce through host memory.
+BACKEND = os.environ.get("UQDME_BENCH_BACKEND", "nccl")
+
+
 def dist_init(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+        local = local % max(1, torch.cuda.device_count())    # one rank per GPU; wraps if fewer GPUs
         torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:    # rehearsal only: ranks sharing one GPU (RCCL refuses duplicate devices)
+            dist.init_process_group("gloo")
         return dist, rank, world, local
     torch.cuda.set_device(0)
     return None, 0, 1, 0
@@ -157,7 +166,12 @@ def main():
             ev[3].record(stream)
         if dist is not None:
             if args.mean_mode == "reduce":
-                dist.reduce(est, dst=0, op=dist.ReduceOp.SUM)      # the one RCCL collective
+                if BACKEND == "nccl":
+                    dist.reduce(est, dst=0, op=dist.ReduceOp.SUM)      # the one RCCL collective
+                else:
+                    est_h = est.cpu()
+                    dist.reduce(est_h, dst=0, op=dist.ReduceOp.SUM)
+                    est.copy_(est_h)
             else:
                 if pipeline != "q":
                     _lib.check(lib.uq_codes_decode_f32(P(codes), P(l1), n, d, m, P(q), sp), "decode")
@@ -194,7 +208,7 @@ def main():
     elapsed = time.perf_counter() - t0
     _lib.check(lib.uq_check_status(P(ws), sp), "status after timed steps")
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if BACKEND == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -237,11 +251,12 @@ def main():
             "config": {"workload": ("C2 (BASELINE.json configs[1]): 1024 clients/GPU x d=2^20, Gaussian, R=1, "
                                     if args.dist == "normal" else
                                     f"C3-style sweep (BASELINE.json configs[2]): {n} clients/GPU x d=2^20, {args.dist}, R=1, ")
-                                   + "unbiased L1 type quantizer + client-ordered mean" + (" + RCCL reduce" if world > 1 else ""),
+                                   + "unbiased L1 type quantizer + client-ordered mean" + ((" + RCCL reduce" if BACKEND == "nccl" else " + host-staged gloo reduce (rehearsal)") if world > 1 else ""),
                        "dist": args.dist,
                        "clients_per_gpu": n, "d": d, "bits_per_dimension": args.bits, "m": m,
                        "torch_threads_l1_order": T, "parallelism": f"client-sharded x{world}",
-                       "mean_mode": args.mean_mode if world > 1 else "single", "pipeline": args.pipeline},
+                       "mean_mode": args.mean_mode if world > 1 else "single",
+                       **({"backend": BACKEND} if world > 1 and BACKEND != "nccl" else {}), "pipeline": args.pipeline},
             "kernel_ms": {"l1": round(float(seg_ms[0]), 4), "quantize": round(q_ms, 4),
                           "client_mean": round(float(seg_ms[2]), 4), "reduce": round(float(seg_ms[3]), 4)},
             "pipelines": side,
