@@ -241,3 +241,47 @@ def test_single_row_ragged_d_vector_path_and_many_threads(uq):
             q = uq.quantize_dequantize(dev(x).view(1, d), 1, X=[0.37], torch_threads=T).cpu().numpy()[0]
             exp = C.quantize_batch(x[None], O.rate_to_m(1, d), np.array([0.37], f32), T)[0][0]
             assert G.bits_equal(q, exp), (d, T, G.n_mismatch(q, exp))
+
+
+def _division_guard_batch(n, d, rng):
+    """Rows that drive every branch of the kernels' x / den (div_plan / div4): ordinary
+    rows (fast path), rows with tiny, subnormal, huge and non-finite elements (per-element
+    IEEE fallback), zero-heavy rows (zeros stay on the fast path), a row with L1 >= 2^40
+    (whole client on the IEEE division), an all-zero row (den = 1e-12) and rows whose
+    quotients all fall under the guard threshold."""
+    x = rng.standard_normal((n, d)).astype(f32)
+    for j in range(n):
+        kind = j % 8
+        idx = rng.integers(0, d, size=max(1, d // 64))
+        if kind == 1:
+            x[j, idx] *= np.float32(1e-40)                        # subnormal elements
+        elif kind == 2:
+            x[j, idx] = (rng.standard_normal(idx.size) * 1e-25).astype(f32)   # tiny normals
+        elif kind == 3:
+            x[j] *= np.float32(1e10)                              # L1 >= 2^40: IEEE path per client
+        elif kind == 4:
+            x[j, rng.random(d) < 0.9] = 0.0                       # sparse: zeros on the fast path
+        elif kind == 5:
+            x[j] *= np.float32(1e-30)                             # every quotient under the threshold
+        elif kind == 6:
+            x[j, idx[:3]] = [np.inf, -np.inf, np.nan][: min(3, idx.size)]
+        elif kind == 7:
+            x[j, idx] *= np.float32(1e30)                         # huge elements, q still finite
+    x[n // 2] = 0.0                                               # den = 1e-12 exactly
+    return x
+
+
+@pytest.mark.parametrize("n,d", [(264, 4100), (3, 70001)])
+def test_division_guards_stream_and_lookback(uq, n, d):
+    """x / den is computed with a per-client reciprocal and two fma corrections; every
+    guard branch must give the IEEE quotient's bits (n >= 256: stream kernel, one
+    workgroup per client; n = 3: look-back kernel)."""
+    rng = np.random.default_rng(4242 + n)
+    x = _division_guard_batch(n, d, rng)
+    assert float(np.abs(x[3 % n]).astype(np.float64).sum()) >= 2.0 ** 40 or n < 4
+    X = rng.random(n).astype(f32)
+    for R in (1, 4):
+        m = O.rate_to_m(R, d)
+        got = uq.quantize_dequantize(dev(x), m=m, X=X, torch_threads=1).cpu().numpy()
+        ref, _ = C.quantize_batch(x, m, X, 1)
+        assert G.n_mismatch(got, ref) == 0, (n, d, R, [G.n_mismatch(got[j], ref[j]) for j in range(n)][:16])

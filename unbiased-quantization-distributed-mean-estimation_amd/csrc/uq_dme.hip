@@ -529,33 +529,91 @@ struct TileState {
     double total;        // tile aggregate A_t (same value in every thread)
 };
 
+// v = x / den (AS:625) without the IEEE division sequence (~10 VALU per element).  den is
+// one per client, so y = RN(1/den) is computed once (IEEE) and each quotient takes a
+// product and two residual corrections (Markstein):
+//     q0 = RN(x*y);  q1 = RN(q0 + RN(x - den*q0)*y)    (faithful)
+//                    q2 = RN(q1 + RN(x - den*q1)*y)    (= RN(x/den): y correctly rounded,
+//                                                       q1 faithful, no underflow)
+// as packed fma pairs.  No underflow: den = L1 + 1e-12 >= 2^-39.9 always and den < 2^40 is
+// required per client (else the IEEE division is used throughout), and elements with
+// |q2| < 2^-59/den (covers every 0 < |x| < 2^-60) or q2 NaN (x = inf/NaN, overflow) are
+// recomputed with the IEEE division.  x = +-0 gives q = +-0 in either sign, which is
+// immaterial (only v < 0 and |v| are used).  tools/markstein_check.c checks this exact
+// function against IEEE division over every finite f32 x for divisors across the range.
+struct DivPlan {
+    float den, y, thr;
+    bool fast;
+};
+__device__ __forceinline__ DivPlan div_plan(float L) {
+    DivPlan p;
+    p.den = L + 1e-12f;                  // AS:625 (f32 add)
+    p.fast = p.den < 0x1p40f;            // false for NaN / inf
+    p.y = 1.0f / p.den;
+    p.thr = 0x1p-59f / p.den;
+    return p;
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void div4(const float (&xs)[4], const DivPlan& dp, float (&vs)[4]) {
+    if (dp.fast) {
+        const f32x2 Y = {dp.y, dp.y}, B = {-dp.den, -dp.den};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x2 a = {xs[2 * h], xs[2 * h + 1]};
+            f32x2 q = a * Y;
+            f32x2 r = __builtin_elementwise_fma(B, q, a);
+            q = __builtin_elementwise_fma(r, Y, q);
+            r = __builtin_elementwise_fma(B, q, a);
+            q = __builtin_elementwise_fma(r, Y, q);
+            vs[2 * h] = q.x;
+            vs[2 * h + 1] = q.y;
+        }
+        bool bad = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bad |= !(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f;
+        if (__builtin_expect(bad, 0)) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (!(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f) vs[c] = xs[c] / dp.den;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) vs[c] = xs[c] / dp.den;
+    }
+}
+
+// fl (signed, see above) and fr of this thread's kQItems elements stay in registers
+// between the passes: a thread only ever reads back its own row.
+struct TileVals {
+    float fl[kQItems];
+    float fr[kQItems];
+};
+
 template <bool FULL>
-__device__ __forceinline__ void tile_pass1(float* s_x, float* s_fr, double* s_wave, int tid, int len, float den,
-                                           float fm, TileState& st) {
+__device__ __forceinline__ void tile_pass1(const float* s_x, TileVals& tv, double* s_wave, int tid, int len,
+                                           const DivPlan& dp, float fm, TileState& st) {
     const int lane = tid & (kWave - 1);
     const int wid = tid / kWave;
     const int i0 = tid * kQItems;
     double tsum = 0.0;
 #pragma unroll
     for (int k4 = 0; k4 < kQItems / 4; ++k4) {
-        const int a = swz(tid, k4);
-        const float4 xv4 = *reinterpret_cast<const float4*>(&s_x[a]);
+        const float4 xv4 = *reinterpret_cast<const float4*>(&s_x[swz(tid, k4)]);
         const float xs[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
-        float fls[4], frs[4];
+        float vs[4];
+        div4(xs, dp, vs);                       // AS:625 x / den, correctly rounded
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const float v = xs[c] / den;        // AS:625 IEEE f32 division
+            const float v = vs[c];
             const float p = fabsf(v);           // AS:626
             const float mp = fm * p;            // AS:629
             const float fl = floorf(mp);        // AS:630
             float fr = mp - fl;                 // AS:631
             if (!FULL && i0 + 4 * k4 + c >= len) fr = 0.0f;
-            fls[c] = v < 0.0f ? -fl : fl;
-            frs[c] = fr;
+            tv.fl[4 * k4 + c] = v < 0.0f ? -fl : fl;
+            tv.fr[4 * k4 + c] = fr;
             tsum += (double)fr;
         }
-        *reinterpret_cast<float4*>(&s_x[a]) = make_float4(fls[0], fls[1], fls[2], fls[3]);
-        *reinterpret_cast<float4*>(&s_fr[a]) = make_float4(frs[0], frs[1], frs[2], frs[3]);
     }
     const double incl_w = wave_incl_scan(tsum, lane);
     double wexcl = __shfl_up(incl_w, 1, kWave);
@@ -583,46 +641,42 @@ __device__ __forceinline__ uint32_t code_of(float fl_s, float kf, float& kmax) {
     return (uint32_t)(((int)kf ^ mask) & 0xFF);
 }
 
-// pass 2; WQ: outputs into the LDS image, WC: this thread's 16 codes into cw.
+// pass 2; WQ: outputs into the LDS image s_o, WC: this thread's 16 codes into cw.
 template <bool WQ, bool WC>
-__device__ __forceinline__ void tile_pass2(float* s_x, const float* s_fr, const float* s_tab, int tid, double P,
+__device__ __forceinline__ void tile_pass2(float* s_o, const TileVals& tv, const float* s_tab, int tid, double P,
                                            float L, float fm, float Xv, const TileState& st, uint32_t (&cw)[4],
-                                           float& kmax, int len) {
+                                           float& kmax) {
     double s = P + st.texcl;
     float fprev = floorf((float)s - Xv);       // floor(c_{i-1} - X) of this thread's first element
-    (void)len;
 #pragma unroll
     for (int k4 = 0; k4 < kQItems / 4; ++k4) {
-        const int a = swz(tid, k4);
-        const float4 fl4 = *reinterpret_cast<const float4*>(&s_x[a]);
-        const float4 fr4 = *reinterpret_cast<const float4*>(&s_fr[a]);
-        const float fls[4] = {fl4.x, fl4.y, fl4.z, fl4.w};
-        const float frs[4] = {fr4.x, fr4.y, fr4.z, fr4.w};
         float o[4], kfs[4];
         bool off_table = false;
         uint32_t w = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            s += (double)frs[c];                               // AS:635 fp64 running sum
+            const float fl = tv.fl[4 * k4 + c];
+            s += (double)tv.fr[4 * k4 + c];                    // AS:635 fp64 running sum
             const float fcur = floorf((float)s - Xv);          // AS:636 floor(c_i - X)
             const float r = (fcur - fprev == 1.0f) ? 1.0f : 0.0f;   // AS:636-637
             fprev = fcur;
-            const float kf = fabsf(fls[c]) + r;                // fl + r
+            const float kf = fabsf(fl) + r;                    // fl + r
             kfs[c] = kf;
             if (WQ) {
                 // AS:640 via the table; the index is clamped so the four LDS reads issue
                 // together, and k >= kTab / NaN are recomputed below (rare)
-                o[c] = copysignf(s_tab[(int)fminf(kf, (float)(kTab - 1))], fls[c]);
+                o[c] = copysignf(s_tab[(int)fminf(kf, (float)(kTab - 1))], fl);
                 off_table |= !(kf < (float)kTab);
             }
-            if (WC) w |= code_of(fls[c], kf, kmax) << (8 * c);   // padding elements: fl = 0, r = 0
+            if (WC) w |= code_of(fl, kf, kmax) << (8 * c);     // padding elements: fl = 0, r = 0
         }
         if (WQ && __builtin_expect(off_table, 0)) {
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-                if (!(kfs[c] < (float)kTab)) o[c] = (copysignf(L, fls[c]) * kfs[c]) / fm;   // ((L1*sign)*(fl+r))/m
+                if (!(kfs[c] < (float)kTab))
+                    o[c] = (copysignf(L, tv.fl[4 * k4 + c]) * kfs[c]) / fm;   // ((L1*sign)*(fl+r))/m
         }
-        if (WQ) *reinterpret_cast<float4*>(&s_x[a]) = make_float4(o[0], o[1], o[2], o[3]);
+        if (WQ) *reinterpret_cast<float4*>(&s_o[swz(tid, k4)]) = make_float4(o[0], o[1], o[2], o[3]);
         if (WC) cw[k4] = w;
     }
 }
@@ -635,6 +689,20 @@ __device__ __forceinline__ void store_codes(int8_t* __restrict__ ct, const uint3
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(ct + i0));
     } else {
         for (int k = 0; k < kQItems && i0 + k < len; ++k) ct[i0 + k] = (int8_t)((cw[k >> 2] >> (8 * (k & 3))) & 0xFF);
+    }
+}
+
+// codes of tile t0 (element offset) of one row: one 16-byte buffer store per thread
+// (beyond d: dropped by the range check), or bytewise when d % 16 != 0.
+template <bool CVEC>
+__device__ __forceinline__ void store_codes_buf(__amdgpu_buffer_rsrc_t rc, int8_t* __restrict__ crow,
+                                                const uint32_t (&cw)[4], uint32_t t0, int64_t d, int tid) {
+    if (CVEC) {
+        const u32x4v v = {cw[0], cw[1], cw[2], cw[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rc, t0 + (uint32_t)(tid * kQItems), 0, kAuxNT);
+    } else {
+        const int64_t rem = d - (int64_t)t0;
+        store_codes<false>(crow + t0, cw, (int)(rem < kQTile ? rem : kQTile), tid);
     }
 }
 
@@ -663,19 +731,25 @@ __device__ __forceinline__ void store_tile(const float* s_data, float* __restric
 // No inter-workgroup communication at all.  Used when there are enough clients to
 // fill the GPU (batched DME, the bench workload).  Requires d % 4 == 0 and 4*d < 2^31
 // (buffer addressing); the host falls back to the look-back kernel otherwise.
+//
+// Order of the vector-memory operations per iteration t: stores of tile t-1 (q from the
+// LDS image s_o, codes from registers), THEN the loads of tile t+1.  vmcnt counts stores
+// too and retires in issue order, so with the loads last the wait before staging tile
+// t+1 never waits on a store acknowledgement, and stores and loads both overlap the
+// whole compute of tile t.
 template <bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock, 4)
 quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                        int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
                        const float* __restrict__ Xs, const float* __restrict__ l1) {
-    __shared__ __attribute__((aligned(16))) float s_x[kQTile];
-    __shared__ __attribute__((aligned(16))) float s_fr[kQTile];
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image of tile t
+    __shared__ __attribute__((aligned(16))) float s_o[kQTile];     // output image of tile t-1 / t
     __shared__ float s_tab[kTab];
     __shared__ double s_wave[kQBlock / kWave];
     const int tid = threadIdx.x;
     const int64_t vec = blockIdx.x;
     const float L = l1[vec];
-    const float den = L + 1e-12f;                  // AS:625 (f32 add)
+    const DivPlan dp = div_plan(L);
     const float Xv = Xs[vec];
     const uint32_t row_bytes = (uint32_t)(d * 4);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, row_bytes);
@@ -685,35 +759,35 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     load_tile_buf(pre, rx, 0u, tid);
     build_table(s_tab, tid, L, fm);
     double P = 0.0;
+    uint32_t cw[4] = {0u, 0u, 0u, 0u};
+    float kmax = 0.0f;
     for (int32_t tile = 0; tile < tiles; ++tile) {
         stage_tile<true>(pre, s_x, tid);
-        __syncthreads();
+        __syncthreads();                           // s_x(t) staged; s_o(t-1) complete
+        if (tile > 0) {
+            const uint32_t tp = (uint32_t)(tile - 1) * (uint32_t)kQTile;
+            if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);      // beyond d: dropped by the range check
+            if (WC) store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
+        }
         if (tile + 1 < tiles) load_tile_buf(pre, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
         const int64_t t0 = (int64_t)tile * kQTile;
         const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
         TileState st;
-#ifndef UQ_ABL_COPY
+        TileVals tv;
+        // pass 1's barrier also orders the s_o reads above before pass 2's s_o writes
         if (len == kQTile)
-            tile_pass1<true>(s_x, s_fr, s_wave, tid, len, den, fm, st);
+            tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
         else
-            tile_pass1<false>(s_x, s_fr, s_wave, tid, len, den, fm, st);
-        uint32_t cw[4];
-        float kmax = 0.0f;
-        tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, P, L, fm, Xv, st, cw, kmax, len);
+            tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
+        tile_pass2<WQ, WC>(s_o, tv, s_tab, tid, P, L, fm, Xv, st, cw, kmax);
         P = P + st.total;                          // serial definition of the tile prefix
-        if (WC) {
-            if (CVEC) {
-                const u32x4v v = {cw[0], cw[1], cw[2], cw[3]};
-                __builtin_amdgcn_raw_buffer_store_b128(v, rc, (uint32_t)(t0 + tid * kQItems), 0, kAuxNT);   // beyond d: dropped
-            } else {
-                store_codes<false>(codes + vec * d + t0, cw, len, tid);
-            }
-            publish_kmax(kmax, L, overflow, vec, tid);
-        }
-#endif
-        __syncthreads();
-        if (WQ) store_tile_buf(s_x, ro, (uint32_t)t0 * 4u, tid);   // beyond d: dropped by the range check
-        __syncthreads();
+    }
+    __syncthreads();
+    const uint32_t tp = (uint32_t)(tiles - 1) * (uint32_t)kQTile;
+    if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);
+    if (WC) {
+        store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
+        publish_kmax(kmax, L, overflow, vec, tid);
     }
 }
 
@@ -726,8 +800,7 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
                          int32_t* __restrict__ overflow, int64_t d, int32_t tiles,
                          uint32_t total_tiles, float fm, const float* __restrict__ Xs, const float* __restrict__ l1,
                          uint64_t* __restrict__ agg, uint64_t* __restrict__ incl, uint32_t* __restrict__ ctrl) {
-    __shared__ __attribute__((aligned(16))) float s_x[kQTile];
-    __shared__ __attribute__((aligned(16))) float s_fr[kQTile];
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image, then output image
     __shared__ double s_wave[kQBlock / kWave];
     __shared__ float s_tab[kTab];
     __shared__ double s_prefix;
@@ -758,13 +831,14 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
         const int64_t t0 = (int64_t)tile * kQTile;
         const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
         const float L = l1[vec];
-        const float den = L + 1e-12f;              // AS:625 (f32 add)
+        const DivPlan dp = div_plan(L);
         if (s_tabvec != vec) build_table(s_tab, tid, L, fm);   // uniform; tab read after pass 1's barrier
         TileState st;
+        TileVals tv;
         if (len == kQTile)
-            tile_pass1<true>(s_x, s_fr, s_wave, tid, len, den, fm, st);
+            tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
         else
-            tile_pass1<false>(s_x, s_fr, s_wave, tid, len, den, fm, st);
+            tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
         uint64_t* aggv = agg + vec * tiles;
         uint64_t* inclv = incl + vec * tiles;
         if (tid == 0) s_tabvec = vec;              // every thread has tested s_tabvec before pass 1's barrier
@@ -780,7 +854,7 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
         __syncthreads();
         uint32_t cw[4];
         float kmax = 0.0f;
-        tile_pass2<WQ, WC>(s_x, s_fr, s_tab, tid, s_prefix, L, fm, Xs[vec], st, cw, kmax, len);
+        tile_pass2<WQ, WC>(s_x, tv, s_tab, tid, s_prefix, L, fm, Xs[vec], st, cw, kmax);   // s_x free after pass 1
         if (WC) {
             store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
             publish_kmax(kmax, L, overflow, vec, tid);
