@@ -75,3 +75,20 @@ def test_wire_roundtrip_through_bytes(uq):
     msg = tc.to_bytes()
     back = uq.TypeCodes.from_bytes(msg, device="cuda")
     assert G.bits_equal(uq.decode(back).cpu().numpy(), q.cpu().numpy())
+
+
+@pytest.mark.parametrize("d", [4112, 1000])
+def test_codes_mean_group_boundaries(uq, d):
+    """codes_mean stages client tables 32 at a time and double-buffers code loads in
+    batches of 16: client counts on either side of every boundary, vector and bytewise
+    columns (d = 4112: a tail workgroup whose last threads go bytewise; d = 1000: all
+    bytewise), against the float-path client mean."""
+    rng = np.random.default_rng(d)
+    x = rng.laplace(1, 2, (97, d)).astype(f32)
+    X = rng.random(97).astype(f32)
+    tc, q = uq.quantize_encode(torch.from_numpy(x).cuda(), 2, X=X, torch_threads=1, return_q=True)
+    for n in (15, 16, 17, 31, 32, 33, 47, 48, 49, 63, 64, 65, 80, 95, 96, 97):
+        sub = uq.TypeCodes(codes=tc.codes[:n].contiguous(), l1=tc.l1[:n], m=tc.m, overflow=tc.overflow[:n])
+        est = uq.codes_mean(sub, 97).cpu().numpy()
+        ref = uq.client_mean(q[:n].contiguous(), 97).cpu().numpy()
+        assert G.bits_equal(est, ref), (n, d, G.n_mismatch(est, ref))

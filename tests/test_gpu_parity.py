@@ -285,3 +285,33 @@ def test_division_guards_stream_and_lookback(uq, n, d):
         got = uq.quantize_dequantize(dev(x), m=m, X=X, torch_threads=1).cpu().numpy()
         ref, _ = C.quantize_batch(x, m, X, 1)
         assert G.n_mismatch(got, ref) == 0, (n, d, R, [G.n_mismatch(got[j], ref[j]) for j in range(n)][:16])
+
+
+@pytest.mark.parametrize("n,d", [(6, 1 << 20), (6, (1 << 20) + 3), (50, 100004)])
+def test_k2_forms_agree_stream_phased_lookback(uq, n, d):
+    """The three K2 forms -- stream (n >= 256, one workgroup per client), phased (a few
+    clients with >= 1024 tiles: tile aggregates, per-client fold, outputs; segmented
+    stream for aligned rows -- (50, 100004): 13 segments of 2 tiles, the last one a single
+    ragged tile -- and one workgroup per tile otherwise) and look-back (n = 1) -- carry the
+    same serial tile-prefix recursion, so the same client gives the same bits whichever
+    form runs; two rows also against the C oracle."""
+    rng = np.random.default_rng(d % 1000 + n)
+    x = rng.laplace(1, 2, (n, d)).astype(f32)
+    X = rng.random(n).astype(f32)
+    m = O.rate_to_m(2, d)
+    xd = dev(x)
+    phased = uq.quantize_dequantize(xd, m=m, X=X, torch_threads=1).cpu().numpy()
+    for j in range(n):
+        one = uq.quantize_dequantize(xd[j:j + 1].contiguous(), m=m, X=X[j:j + 1], torch_threads=1).cpu().numpy()[0]
+        assert G.n_mismatch(one, phased[j]) == 0, ("look-back vs phased", j)
+    if d % 4 == 0:
+        filler = torch.randn(256 - n, d, device="cuda")
+        big = torch.cat([xd, filler])
+        Xb = np.concatenate([X, rng.random(256 - n).astype(f32)])
+        stream = uq.quantize_dequantize(big, m=m, X=Xb, torch_threads=1)[:n].cpu().numpy()
+        assert G.n_mismatch(stream, phased) == 0, "stream vs phased"
+    ref, _ = C.quantize_batch(x[:2], m, X[:2], 1)
+    assert G.n_mismatch(phased[:2], ref) == 0
+    tc, q = uq.quantize_encode(xd, m=m, X=X, torch_threads=1, return_q=True)
+    assert G.bits_equal(q.cpu().numpy(), phased)
+    assert G.bits_equal(uq.decode(tc).cpu().numpy(), phased)

@@ -40,6 +40,7 @@ constexpr int kQTile = kQBlock * kQItems;  // 4096 elements per tile
 // LDS tile image: 256 rows of 16 floats (thread t owns row t); float4 column c of row r
 // lives at swz(r, c) (XOR swizzle, see there): bank-conflict-free without padding.
 constexpr int64_t kStreamMinClients = 256; // >= this many clients: one workgroup per vector
+constexpr int64_t kPhasedMinTiles = 1024;   // fewer clients but >= this many tiles: K2-phased
 
 // ---- workspace layout --------------------------------------------------------------
 // [0,256)            control: u32 ticket, u32 abort (both reset by every call),
@@ -314,8 +315,9 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
 // Persistent workgroups walk 4096-element tiles in ticket order (one atomic counter):
 // a workgroup only ever waits on tiles with smaller tickets, which are either done or
 // owned by a running workgroup that will finish them first, so there is no residency
-// assumption and no deadlock.  While a tile is processed, the next ticket's tile is
-// already in flight into registers (prefetch), so HBM traffic overlaps the scan wait.
+// assumption and no deadlock.  A workgroup takes its next ticket once the current
+// tile's look-back has resolved (it has no waits left) and prefetches that tile into
+// registers during pass 2 and the stores.
 //
 // Scan (AS:635): torch CPU cumsum of f32 accumulates sequentially in fp64 and rounds
 // each prefix to f32.  Each thread adds its 16 fractional parts sequentially in fp64
@@ -737,17 +739,24 @@ __device__ __forceinline__ void store_tile(const float* s_data, float* __restric
 // too and retires in issue order, so with the loads last the wait before staging tile
 // t+1 never waits on a store acknowledgement, and stores and loads both overlap the
 // whole compute of tile t.
+//
+// Segments: workgroup b takes client b / nseg, tiles [s*seg_tiles, (s+1)*seg_tiles) with
+// s = b % nseg, starting from P = pre[first tile] (the per-client fold of the phased
+// form) -- or from P = 0 over the whole vector when nseg == 1 (pre == nullptr).
 template <bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock, 4)
 quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                        int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
-                       const float* __restrict__ Xs, const float* __restrict__ l1) {
+                       const float* __restrict__ Xs, const float* __restrict__ l1, int32_t seg_tiles, int32_t nseg,
+                       const uint64_t* __restrict__ pre) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image of tile t
     __shared__ __attribute__((aligned(16))) float s_o[kQTile];     // output image of tile t-1 / t
     __shared__ float s_tab[kTab];
     __shared__ double s_wave[kQBlock / kWave];
     const int tid = threadIdx.x;
-    const int64_t vec = blockIdx.x;
+    const int64_t vec = blockIdx.x / (uint32_t)nseg;
+    const int32_t tb = (int32_t)(blockIdx.x % (uint32_t)nseg) * seg_tiles;
+    const int32_t te = min(tiles, tb + seg_tiles);
     const float L = l1[vec];
     const DivPlan dp = div_plan(L);
     const float Xv = Xs[vec];
@@ -755,21 +764,21 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, row_bytes);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(WQ ? out + vec * d : x, row_bytes);
     const __amdgpu_buffer_rsrc_t rc = make_rsrc(WC ? (const void*)(codes + vec * d) : (const void*)x, (uint32_t)d);
-    TileRegs pre;
-    load_tile_buf(pre, rx, 0u, tid);
+    TileRegs pre_x;
+    load_tile_buf(pre_x, rx, (uint32_t)tb * (uint32_t)(kQTile * 4), tid);
     build_table(s_tab, tid, L, fm);
-    double P = 0.0;
+    double P = pre ? __longlong_as_double((long long)pre[vec * tiles + tb]) : 0.0;
     uint32_t cw[4] = {0u, 0u, 0u, 0u};
     float kmax = 0.0f;
-    for (int32_t tile = 0; tile < tiles; ++tile) {
-        stage_tile<true>(pre, s_x, tid);
+    for (int32_t tile = tb; tile < te; ++tile) {
+        stage_tile<true>(pre_x, s_x, tid);
         __syncthreads();                           // s_x(t) staged; s_o(t-1) complete
-        if (tile > 0) {
+        if (tile > tb) {
             const uint32_t tp = (uint32_t)(tile - 1) * (uint32_t)kQTile;
             if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);      // beyond d: dropped by the range check
             if (WC) store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
         }
-        if (tile + 1 < tiles) load_tile_buf(pre, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
+        if (tile + 1 < te) load_tile_buf(pre_x, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
         const int64_t t0 = (int64_t)tile * kQTile;
         const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
         TileState st;
@@ -783,11 +792,42 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         P = P + st.total;                          // serial definition of the tile prefix
     }
     __syncthreads();
-    const uint32_t tp = (uint32_t)(tiles - 1) * (uint32_t)kQTile;
+    const uint32_t tp = (uint32_t)(te - 1) * (uint32_t)kQTile;
     if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);
     if (WC) {
         store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
         publish_kmax(kmax, L, overflow, vec, tid);
+    }
+}
+
+// Phase 1 of the segmented (phased) form: tile aggregates A_t over a segment, streamed
+// with the same prefetch as the stream kernel (pass 1 only; 4 B per element read).
+__global__ void __launch_bounds__(kQBlock, 4)
+agg_stream_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
+                  int32_t seg_tiles, int32_t nseg, uint64_t* __restrict__ agg) {
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];
+    __shared__ double s_wave[kQBlock / kWave];
+    const int tid = threadIdx.x;
+    const int64_t vec = blockIdx.x / (uint32_t)nseg;
+    const int32_t tb = (int32_t)(blockIdx.x % (uint32_t)nseg) * seg_tiles;
+    const int32_t te = min(tiles, tb + seg_tiles);
+    const DivPlan dp = div_plan(l1[vec]);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, (uint32_t)(d * 4));
+    TileRegs pre_x;
+    load_tile_buf(pre_x, rx, (uint32_t)tb * (uint32_t)(kQTile * 4), tid);
+    for (int32_t tile = tb; tile < te; ++tile) {
+        stage_tile<true>(pre_x, s_x, tid);
+        __syncthreads();
+        if (tile + 1 < te) load_tile_buf(pre_x, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
+        const int64_t t0 = (int64_t)tile * kQTile;
+        const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+        TileState st;
+        TileVals tv;
+        if (len == kQTile)
+            tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
+        else
+            tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
+        if (tid == 0) agg[vec * tiles + tile] = (uint64_t)__double_as_longlong(st.total);
     }
 }
 
@@ -804,28 +844,24 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
     __shared__ double s_wave[kQBlock / kWave];
     __shared__ float s_tab[kTab];
     __shared__ double s_prefix;
-    __shared__ uint32_t s_ticket[2];
+    __shared__ uint32_t s_ticket;
     __shared__ int64_t s_tabvec;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wid = tid / kWave;
 
     if (tid == 0) {
-        s_ticket[0] = atomicAdd(ctrl, 1u);
+        s_ticket = atomicAdd(ctrl, 1u);
         s_tabvec = -1;
     }
     __syncthreads();
-    uint32_t cur = s_ticket[0];
+    uint32_t cur = s_ticket;
     if (cur >= total_tiles) return;
     TileRegs pre;
     load_tile<VEC4>(pre, x, d, tiles, cur, tid);
-    int slot = 0;
     for (;;) {
-        if (tid == 0) s_ticket[slot ^ 1] = atomicAdd(ctrl, 1u);
         stage_tile<VEC4>(pre, s_x, tid);
         __syncthreads();
-        const uint32_t nxt = s_ticket[slot ^ 1];
-        if (nxt < total_tiles) load_tile<VEC4>(pre, x, d, tiles, nxt, tid);
         const int64_t vec = cur / (uint32_t)tiles;
         const int32_t tile = cur % (uint32_t)tiles;
         const int64_t t0 = (int64_t)tile * kQTile;
@@ -849,9 +885,16 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
             if (lane == 0) {
                 st_relaxed_agent(&inclv[tile], canon_bits(P + st.total));
                 s_prefix = P;
+                // the next ticket only now: from here this workgroup never waits again, so
+                // the aggregate of the ticket it takes is published within about one tile
+                // time.  (Taken earlier, a held ticket's aggregate would wait on this
+                // tile's look-back, and look-back waits would chain.)
+                s_ticket = atomicAdd(ctrl, 1u);
             }
         }
         __syncthreads();
+        const uint32_t nxt = s_ticket;
+        if (nxt < total_tiles) load_tile<VEC4>(pre, x, d, tiles, nxt, tid);   // overlaps pass 2 + stores
         uint32_t cw[4];
         float kmax = 0.0f;
         tile_pass2<WQ, WC>(s_x, tv, s_tab, tid, s_prefix, L, fm, Xs[vec], st, cw, kmax);   // s_x free after pass 1
@@ -863,9 +906,93 @@ quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, i
         if (WQ) store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
         if (nxt >= total_tiles) break;
         cur = nxt;
-        slot ^= 1;
         __syncthreads();
     }
+}
+
+// K2-phased: few clients with many tiles (1 < n < kStreamMinClients).  Three launches,
+// no inter-workgroup waits at all:
+//   tile_agg_kernel    one workgroup per tile: pass 1 -> tile aggregate A_t (the same
+//                      fixed tree as every other K2 form)
+//   tile_prefix_kernel one thread per client: P_0 = 0, P_{t+1} = fl64(P_t + A_t) -- the
+//                      serial recursion the stream kernel carries and the look-back
+//                      reproduces, so all three forms give the same bits
+//   tile_out_kernel    one workgroup per tile: pass 1 again, pass 2 from P_t, stores.
+// x is read twice (plus K1); at these batch sizes the second read mostly hits the MALL.
+template <bool VEC4>
+__global__ void __launch_bounds__(kQBlock)
+tile_agg_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
+                uint64_t* __restrict__ agg) {
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];
+    __shared__ double s_wave[kQBlock / kWave];
+    const int tid = threadIdx.x;
+    const int32_t tile = blockIdx.x;
+    const int64_t vec = blockIdx.y;
+    TileRegs r;
+    load_tile<VEC4>(r, x, d, tiles, (uint32_t)(vec * tiles + tile), tid);
+    stage_tile<VEC4>(r, s_x, tid);
+    __syncthreads();
+    const int64_t t0 = (int64_t)tile * kQTile;
+    const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+    const DivPlan dp = div_plan(l1[vec]);
+    TileState st;
+    TileVals tv;
+    if (len == kQTile)
+        tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
+    else
+        tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
+    if (tid == 0) agg[vec * tiles + tile] = (uint64_t)__double_as_longlong(st.total);
+}
+
+__global__ void __launch_bounds__(256)
+tile_prefix_kernel(const uint64_t* __restrict__ agg, uint64_t* __restrict__ pre, int64_t n, int32_t tiles) {
+    const int64_t vec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (vec >= n) return;
+    const uint64_t* a = agg + vec * tiles;
+    uint64_t* p = pre + vec * tiles;
+    double P = 0.0;
+    for (int32_t t = 0; t < tiles; ++t) {
+        p[t] = (uint64_t)__double_as_longlong(P);
+        P = P + __longlong_as_double((long long)a[t]);
+    }
+}
+
+template <bool VEC4, bool WQ, bool WC, bool CVEC>
+__global__ void __launch_bounds__(kQBlock)
+tile_out_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
+                int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm, const float* __restrict__ Xs,
+                const float* __restrict__ l1, const uint64_t* __restrict__ pre) {
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image, then output image
+    __shared__ double s_wave[kQBlock / kWave];
+    __shared__ float s_tab[kTab];
+    const int tid = threadIdx.x;
+    const int32_t tile = blockIdx.x;
+    const int64_t vec = blockIdx.y;
+    TileRegs r;
+    load_tile<VEC4>(r, x, d, tiles, (uint32_t)(vec * tiles + tile), tid);
+    const float L = l1[vec];
+    build_table(s_tab, tid, L, fm);                 // read after pass 1's barrier
+    stage_tile<VEC4>(r, s_x, tid);
+    __syncthreads();
+    const int64_t t0 = (int64_t)tile * kQTile;
+    const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+    const DivPlan dp = div_plan(L);
+    TileState st;
+    TileVals tv;
+    if (len == kQTile)
+        tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
+    else
+        tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
+    const double P = __longlong_as_double((long long)pre[vec * tiles + tile]);
+    uint32_t cw[4];
+    float kmax = 0.0f;
+    tile_pass2<WQ, WC>(s_x, tv, s_tab, tid, P, L, fm, Xs[vec], st, cw, kmax);   // s_x free after pass 1
+    if (WC) {
+        store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
+        publish_kmax(kmax, L, overflow, vec, tid);
+    }
+    __syncthreads();
+    if (WQ) store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
 }
 
 // =====================================================================================
@@ -950,70 +1077,111 @@ codes_decode_kernel(const int8_t* __restrict__ codes, const float* __restrict__ 
 }
 
 // est[i] (+)= q_j[i] / n_div for clients j in order, q decoded from codes.  Each thread
-// owns kMeanCpt consecutive columns (one 8-byte code load per client); 16 clients of
-// loads are kept in flight.  Client tables tabn[j][k] = RN(RN(RN(L1_j*k)/m)/n_div) for
-// k <= kmax_j are staged kMeanClients at a time (kmax_j from the encoder keeps them tiny:
-// ~8 entries at R = 1).
+// owns kMeanCpt consecutive columns (one 8-byte code load per client).  Client tables
+// tabn[j][k] = RN(RN(RN(L1_j*k)/m)/n_div) for k <= kmax_j are staged kMeanClients at a
+// time (kmax_j from the encoder keeps them tiny: ~8 entries at R = 1); each wave builds
+// whole clients' tables from wave-uniform SCALAR loads of L1_j and kmax_j, so the table
+// build never waits on the vector-memory counter.  Code loads go in batches of
+// kMeanUnroll clients, double-buffered: batch b+1 (crossing group boundaries) is in
+// flight while batch b is summed.
 constexpr int kMeanCpt = 8;
 constexpr int kMeanUnroll = 16;
+static_assert(kMeanClients == 2 * kMeanUnroll, "two code batches per table group");
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void mean_load_batch(uint2 (&w)[kMeanUnroll], const int8_t* cp, int64_t d) {
+#pragma unroll
+    for (int u = 0; u < kMeanUnroll; ++u) {
+        const u32x2v t = __builtin_nontemporal_load(reinterpret_cast<const u32x2v*>(cp + (int64_t)u * d));
+        w[u] = make_uint2(t.x, t.y);
+    }
+}
+
+__device__ __forceinline__ void mean_add_batch(float (&e)[kMeanCpt], const uint2 (&w)[kMeanUnroll],
+                                               const float (*tabn)[256], int jj) {
+#pragma unroll
+    for (int u = 0; u < kMeanUnroll; ++u) {
+        const float* tb = tabn[jj + u];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] += tb[(w[u].x >> (8 * k)) & 0xFF];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[4 + k] += tb[(w[u].y >> (8 * k)) & 0xFF];
+    }
+}
+
+// Tables of clients j0 .. j0+nb-1 into tabn (callers bracket it with barriers).
+__device__ __forceinline__ void mean_build_tables(float (*tabn)[256], const float* __restrict__ l1,
+                                                  const int32_t* __restrict__ kmaxv, int64_t j0, int nb, int wid,
+                                                  int lane, float fm, float n_div) {
+    for (int jj = wid; jj < nb; jj += 256 / kWave) {
+        const float L = l1[j0 + jj];                // wave-uniform: scalar loads
+        const int km = min(127, max(0, kmaxv[j0 + jj]));
+        for (int k = lane; k <= km; k += kWave) {
+            const float v = ((L * (float)k) / fm) / n_div;
+            tabn[jj][k] = v;                        // code k
+            tabn[jj][255 - k] = -v;                 // code ~k = -k-1 -> byte 255-k; (-a)/n = -(a/n)
+        }
+    }
+}
+
+// ragged / unaligned columns: bytewise, clients j0 .. j0+nb-1 in order
+__device__ __forceinline__ void mean_add_bytes(float (&e)[kMeanCpt], const int8_t* __restrict__ codes,
+                                               const float (*tabn)[256], int64_t j0, int nb, int64_t i0, int64_t d) {
+    for (int jj = 0; jj < nb; ++jj)
+        for (int k = 0; k < kMeanCpt; ++k)
+            if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[(j0 + jj) * d + i0 + k]];
+}
+
 template <bool VEC>
 __global__ void __launch_bounds__(256)
 codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, const int32_t* __restrict__ kmaxv,
                   int64_t n, int64_t d, float fm, float n_div, int accumulate, float* __restrict__ est) {
     __shared__ float tabn[kMeanClients][256];     // indexed by the raw code byte, sign included
-    __shared__ int s_kmax[kMeanClients];
     const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);
     const int64_t i0 = ((int64_t)blockIdx.x * 256 + tid) * kMeanCpt;
     const bool full = VEC && i0 + kMeanCpt <= d;
     float e[kMeanCpt];
 #pragma unroll
     for (int k = 0; k < kMeanCpt; ++k) e[k] = (accumulate && i0 + k < d) ? est[i0 + k] : 0.0f;
-    for (int64_t j0 = 0; j0 < n; j0 += kMeanClients) {
-        const int nb = (int)((n - j0) < kMeanClients ? (n - j0) : kMeanClients);
+    // full groups of kMeanClients: straight-line, unconditional loads (the prefetch of the
+    // group after the last one is clamped to a valid row and never used), so the waits
+    // before each batch cover that batch only
+    const int64_t groups = n / kMeanClients;
+    const int8_t* cbase = codes + (full ? i0 : 0);
+    uint2 wa[kMeanUnroll], wb[kMeanUnroll];
+    if (VEC && groups > 0) mean_load_batch(wa, cbase, d);
+    for (int64_t g = 0; g < groups; ++g) {
+        const int64_t j0 = g * kMeanClients;
+        __syncthreads();                            // previous group's tables no longer read
+        mean_build_tables(tabn, l1, kmaxv, j0, kMeanClients, wid, lane, fm, n_div);
         __syncthreads();
-        if (tid < nb) s_kmax[tid] = min(127, max(0, kmaxv[j0 + tid]));
-        __syncthreads();
-        for (int t = tid; t < nb * 128; t += 256) {
-            const int jj = t >> 7, k = t & 127;
-            if (k <= s_kmax[jj]) {
-                const float L = l1[j0 + jj];
-                const float v = ((L * (float)k) / fm) / n_div;
-                tabn[jj][k] = v;            // code k
-                tabn[jj][255 - k] = -v;     // code ~k = -k-1 -> byte 255-k; (-a)/n = -(a/n)
-            }
+        if (VEC) {
+            mean_load_batch(wb, cbase + (j0 + kMeanUnroll) * d, d);
+            if (full) mean_add_batch(e, wa, tabn, 0);
+            const int64_t jn = (j0 + kMeanClients + kMeanUnroll <= n) ? j0 + kMeanClients : n - kMeanUnroll;
+            mean_load_batch(wa, cbase + jn * d, d);
+            if (full) mean_add_batch(e, wb, tabn, kMeanUnroll);
         }
+        if (!full) mean_add_bytes(e, codes, tabn, j0, kMeanClients, i0, d);
+    }
+    const int64_t jr = groups * kMeanClients;
+    const int nr = (int)(n - jr);
+    if (nr > 0) {                                   // the last n % kMeanClients clients
+        __syncthreads();
+        mean_build_tables(tabn, l1, kmaxv, jr, nr, wid, lane, fm, n_div);
         __syncthreads();
         if (full) {
-            const int8_t* cp = codes + j0 * d + i0;
-            int jj = 0;
-            for (; jj + kMeanUnroll <= nb; jj += kMeanUnroll) {
-                uint2 w[kMeanUnroll];
-#pragma unroll
-                for (int u = 0; u < kMeanUnroll; ++u) {
-                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-                    const u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(cp + (int64_t)(jj + u) * d));
-                    w[u] = make_uint2(t.x, t.y);
-                }
-#pragma unroll
-                for (int u = 0; u < kMeanUnroll; ++u) {
-                    const float* tb = tabn[jj + u];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) e[k] += tb[(w[u].x >> (8 * k)) & 0xFF];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) e[4 + k] += tb[(w[u].y >> (8 * k)) & 0xFF];
-                }
-            }
-            for (; jj < nb; ++jj) {
-                const uint2 w = *reinterpret_cast<const uint2*>(cp + (int64_t)jj * d);
+            for (int jj = 0; jj < nr; ++jj) {
+                const uint2 w = *reinterpret_cast<const uint2*>(codes + (jr + jj) * d + i0);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) e[k] += tabn[jj][(w.x >> (8 * k)) & 0xFF];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) e[4 + k] += tabn[jj][(w.y >> (8 * k)) & 0xFF];
             }
         } else {
-            for (int jj = 0; jj < nb; ++jj)
-                for (int k = 0; k < kMeanCpt; ++k)
-                    if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[(j0 + jj) * d + i0 + k]];
+            mean_add_bytes(e, codes, tabn, jr, nr, i0, d);
         }
     }
     if (full) {
@@ -1112,6 +1280,23 @@ int persistent_grid(bool vec4, int* out) {
         cache_dev = dev;
     }
     *out = cache_v[vec4 ? 1 : 0];
+    return UQ_OK;
+}
+
+// Resident stream-kernel workgroups on this device: 4 per CU (launch bounds).
+int stream_slots(int* out) {
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc) return rc;
+    static thread_local int cache_dev = -1, cache_slots = 0;
+    if (cache_dev != dev) {
+        int cus = 0;
+        rc = hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
+        if (rc) return rc;
+        cache_slots = 4 * std::max(1, cus);
+        cache_dev = dev;
+    }
+    *out = cache_slots;
     return UQ_OK;
 }
 
@@ -1391,7 +1576,7 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
 #define UQ_STREAM(Q, C, CV)                                                                                 \
     case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
         hipLaunchKernelGGL((quantize_stream_kernel<Q, C, CV>), dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, \
-                           codes, overflow, d, w.tiles, fm, X, l1use);                                    \
+                           codes, overflow, d, w.tiles, fm, X, l1use, w.tiles, 1, nullptr);              \
         break;
         switch (sel & 7) {
             UQ_STREAM(1, 0, 1) UQ_STREAM(1, 1, 1) UQ_STREAM(1, 1, 0) UQ_STREAM(0, 1, 1) UQ_STREAM(0, 1, 0)
@@ -1399,6 +1584,63 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
         }
 #undef UQ_STREAM
         return hip_check(hipGetLastError(), "quantize_stream_kernel launch");
+    }
+    if (n > 1 && n <= 65535 && n * (int64_t)w.tiles >= kPhasedMinTiles && n * (int64_t)w.tiles < ((int64_t)1 << 32)) {
+        // several clients, enough tiles to fill the GPU: the three-phase form (no waits)
+        uint64_t* agg = (uint64_t*)(wsb + w.agg_off);
+        uint64_t* pre = (uint64_t*)(wsb + w.incl_off);
+        if (vec4 && d <= ((int64_t)1 << 29)) {
+            // segmented stream: runs of R tiles per workgroup, ~4 resident workgroups per CU
+            int slots = 0;
+            rc = stream_slots(&slots);
+            if (rc) return rc;
+            const int64_t total_tiles = n * (int64_t)w.tiles;
+            const int32_t R = (int32_t)std::max<int64_t>(1, (total_tiles + slots - 1) / slots);
+            const int32_t nseg = (w.tiles + R - 1) / R;
+            const dim3 sgrid((unsigned)(n * nseg));
+            hipLaunchKernelGGL(agg_stream_kernel, sgrid, dim3(kQBlock), 0, st, x, d, w.tiles, fm, l1use, R, nseg, agg);
+            rc = hip_check(hipGetLastError(), "agg_stream_kernel launch");
+            if (rc) return rc;
+            hipLaunchKernelGGL(tile_prefix_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, agg, pre, n,
+                               w.tiles);
+            rc = hip_check(hipGetLastError(), "tile_prefix_kernel launch");
+            if (rc) return rc;
+#define UQ_SEG(Q, C, CV)                                                                                    \
+    case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
+        hipLaunchKernelGGL((quantize_stream_kernel<Q, C, CV>), sgrid, dim3(kQBlock), 0, st, x, out, codes, overflow, \
+                           d, w.tiles, fm, X, l1use, R, nseg, pre);                                         \
+        break;
+            switch (sel & 7) {
+                UQ_SEG(1, 0, 1) UQ_SEG(1, 1, 1) UQ_SEG(1, 1, 0) UQ_SEG(0, 1, 1) UQ_SEG(0, 1, 0)
+                default: return fail(UQ_E_INVALID, "internal: bad kernel selector");
+            }
+#undef UQ_SEG
+            return hip_check(hipGetLastError(), "quantize_stream_kernel (segments) launch");
+        }
+        const dim3 grid((unsigned)w.tiles, (unsigned)n);
+        if (vec4)
+            hipLaunchKernelGGL(tile_agg_kernel<true>, grid, dim3(kQBlock), 0, st, x, d, w.tiles, fm, l1use, agg);
+        else
+            hipLaunchKernelGGL(tile_agg_kernel<false>, grid, dim3(kQBlock), 0, st, x, d, w.tiles, fm, l1use, agg);
+        rc = hip_check(hipGetLastError(), "tile_agg_kernel launch");
+        if (rc) return rc;
+        hipLaunchKernelGGL(tile_prefix_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, agg, pre, n,
+                           w.tiles);
+        rc = hip_check(hipGetLastError(), "tile_prefix_kernel launch");
+        if (rc) return rc;
+#define UQ_PHASED(V, Q, C, CV)                                                                                \
+    case ((V) * 8 + (Q) * 4 + (C) * 2 + (CV)):                                                              \
+        hipLaunchKernelGGL((tile_out_kernel<V, Q, C, CV>), grid, dim3(kQBlock), 0, st, x, out, codes, overflow, d, \
+                           w.tiles, fm, X, l1use, pre);                                                       \
+        break;
+        switch (sel) {
+            UQ_PHASED(1, 1, 0, 1) UQ_PHASED(1, 1, 1, 1) UQ_PHASED(1, 1, 1, 0) UQ_PHASED(1, 0, 1, 1)
+            UQ_PHASED(1, 0, 1, 0) UQ_PHASED(0, 1, 0, 1) UQ_PHASED(0, 1, 1, 1) UQ_PHASED(0, 1, 1, 0)
+            UQ_PHASED(0, 0, 1, 1) UQ_PHASED(0, 0, 1, 0)
+            default: return fail(UQ_E_INVALID, "internal: bad kernel selector");
+        }
+#undef UQ_PHASED
+        return hip_check(hipGetLastError(), "tile_out_kernel launch");
     }
     rc = hip_check(hipMemsetAsync(wsb, 0, 2 * sizeof(uint32_t), st), "memset ticket/abort");
     if (rc) return rc;
