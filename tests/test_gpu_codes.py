@@ -1,4 +1,4 @@
-"""GPU: type codes from the quantize kernels (stream and look-back paths), decode, and the
+"""GPU: type codes from the quantize kernels (stream and small-batch paths), decode, and the
 mean from codes -- all bit-exact against the oracle / the float path."""
 import numpy as np
 import pytest

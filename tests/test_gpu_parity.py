@@ -272,10 +272,10 @@ def _division_guard_batch(n, d, rng):
 
 
 @pytest.mark.parametrize("n,d", [(264, 4100), (3, 70001)])
-def test_division_guards_stream_and_lookback(uq, n, d):
+def test_division_guards_stream_and_small_batch(uq, n, d):
     """x / den is computed with a per-client reciprocal and two fma corrections; every
     guard branch must give the IEEE quotient's bits (n >= 256: stream kernel, one
-    workgroup per client; n = 3: look-back kernel)."""
+    workgroup per client; n = 3: the small-batch kernels)."""
     rng = np.random.default_rng(4242 + n)
     x = _division_guard_batch(n, d, rng)
     assert float(np.abs(x[3 % n]).astype(np.float64).sum()) >= 2.0 ** 40 or n < 4
@@ -288,12 +288,11 @@ def test_division_guards_stream_and_lookback(uq, n, d):
 
 
 @pytest.mark.parametrize("n,d", [(6, 1 << 20), (6, (1 << 20) + 3), (50, 100004)])
-def test_k2_forms_agree_stream_phased_lookback(uq, n, d):
-    """The three K2 forms -- stream (n >= 256, one workgroup per client), phased (a few
-    clients with >= 1024 tiles: tile aggregates, per-client fold, outputs; segmented
-    stream for aligned rows -- (50, 100004): 13 segments of 2 tiles, the last one a single
-    ragged tile -- and one workgroup per tile otherwise) and look-back (n = 1) -- carry the
-    same serial tile-prefix recursion, so the same client gives the same bits whichever
+def test_k2_forms_agree_stream_segmented_per_tile(uq, n, d):
+    """The K2 forms -- stream (n >= 256, one workgroup per client), segmented stream (a
+    few aligned clients with >= 1024 tiles; (50, 100004): 13 segments of 2 tiles, the last
+    one a single ragged tile) and one workgroup per tile (n = 1, unaligned rows) -- all
+    reproduce the sequential fp64 cumsum, so the same client gives the same bits whichever
     form runs; two rows also against the C oracle."""
     rng = np.random.default_rng(d % 1000 + n)
     x = rng.laplace(1, 2, (n, d)).astype(f32)
@@ -303,7 +302,7 @@ def test_k2_forms_agree_stream_phased_lookback(uq, n, d):
     phased = uq.quantize_dequantize(xd, m=m, X=X, torch_threads=1).cpu().numpy()
     for j in range(n):
         one = uq.quantize_dequantize(xd[j:j + 1].contiguous(), m=m, X=X[j:j + 1], torch_threads=1).cpu().numpy()[0]
-        assert G.n_mismatch(one, phased[j]) == 0, ("look-back vs phased", j)
+        assert G.n_mismatch(one, phased[j]) == 0, ("n = 1 vs batch", j)
     if d % 4 == 0:
         filler = torch.randn(256 - n, d, device="cuda")
         big = torch.cat([xd, filler])

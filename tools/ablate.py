@@ -6,7 +6,8 @@ sys.path.insert(0, ROOT)
 PKG = os.path.join(ROOT, "unbiased-quantization-distributed-mean-estimation_amd")
 SRC = os.path.join(PKG, "csrc", "uq_dme.hip")
 OUT = os.path.join(PKG, "_build", "abl")
-VARIANTS = {"base": [], "copy": ["-DUQ_ABL_COPY"]}
+VARIANTS = {"base": [], "copy": ["-DUQ_ABL_COPY"],
+            "noties": ["-DUQ_EXP_NOTIES"], "noirrties": ["-DUQ_EXP_NOIRR", "-DUQ_EXP_NOTIES"]}
 def build():
     sys.path.insert(0, PKG)
     import build_ext as be

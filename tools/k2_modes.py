@@ -1,4 +1,4 @@
-"""K2 per-element cost in its two forms at scale: the look-back kernel (n < 256 clients,
+"""K2 per-element cost in its two forms at scale: the small-batch kernels (n < 256 clients,
 several workgroups per client) against the stream kernel (n >= 256, one workgroup per
 client), d = 2^20, q + codes outputs.  Also times the L1 pass.
 

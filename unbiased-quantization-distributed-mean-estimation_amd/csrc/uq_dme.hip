@@ -30,8 +30,6 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kGrain = 32768;     // at::internal::GRAIN_SIZE (torch CPU intra-op split)
 constexpr int kMaxChunks = 64;    // torch_threads supported by the L1 plan
-constexpr uint64_t kEmpty = ~0ull;                   // "aggregate not yet published"
-constexpr uint64_t kCanonNaN = 0x7FF8000000000000ull;  // NaN aggregates are canonicalised
 
 // ---- quantize tile geometry --------------------------------------------------------
 constexpr int kQBlock = 256;               // threads per workgroup (4 waves)
@@ -40,14 +38,16 @@ constexpr int kQTile = kQBlock * kQItems;  // 4096 elements per tile
 // LDS tile image: 256 rows of 16 floats (thread t owns row t); float4 column c of row r
 // lives at swz(r, c) (XOR swizzle, see there): bank-conflict-free without padding.
 constexpr int64_t kStreamMinClients = 256; // >= this many clients: one workgroup per vector
-constexpr int64_t kPhasedMinTiles = 1024;   // fewer clients but >= this many tiles: K2-phased
+constexpr int64_t kSegMinTiles = 1024;     // fewer clients but >= this many tiles: segmented stream
+constexpr int64_t kMaxGridY = 65535;       // clients per launch of the per-tile kernels
 
 // ---- workspace layout --------------------------------------------------------------
 // [0,256)            control: u32 ticket, u32 abort (both reset by every call),
 //                    u32 sticky error word (set on timeout; cleared by uq_check_status).
 //                    A new workspace must be zero-filled once before first use.
-// [256, ...)         u64 agg[n][tiles]           (look-back: tile aggregates A_t)
-// then               u64 incl[n][tiles]          (look-back: inclusive prefixes P_{t+1})
+// [256, ...)         u64 agg[n][tiles]           (small batches: tile sums A_t, then map m0)
+// then               u64 incl[n][tiles]          (small batches: prefixes P'_t, then exact P_t)
+// then               u64 map1[n][tiles]          (small batches: map m1)
 // then               f32 l1part[n][groups][32]  (level-1 block sums)
 // then               f32 l1[n]                  (computed norms)
 constexpr size_t kCtrlBytes = 256;
@@ -312,23 +312,28 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
 // =====================================================================================
 // K2: fused normalize / floor / fp64 scan / crossing / dequantize.
 //
-// Persistent workgroups walk 4096-element tiles in ticket order (one atomic counter):
-// a workgroup only ever waits on tiles with smaller tickets, which are either done or
-// owned by a running workgroup that will finish them first, so there is no residency
-// assumption and no deadlock.  A workgroup takes its next ticket once the current
-// tile's look-back has resolved (it has no waits left) and prefetches that tile into
-// registers during pass 2 and the stores.
+// Scan (AS:635): torch CPU cumsum of f32 accumulates SEQUENTIALLY in fp64 and rounds
+// each prefix to f32.  K2 reproduces every fp64 prefix bit-for-bit, in parallel:
 //
-// Scan (AS:635): torch CPU cumsum of f32 accumulates sequentially in fp64 and rounds
-// each prefix to f32.  Each thread adds its 16 fractional parts sequentially in fp64
-// from base = P_t + (thread-exclusive prefix in the tile).  The tile prefix P_t is
-// defined SERIALLY: P_0 = 0, P_{t+1} = fl64(P_t + A_t) with A_t the tile aggregate.
-// Tile t publishes A_t (agg[t]) as soon as it is known and P_{t+1} (incl[t]) once its
-// look-back is done.  Looking back, tile t takes the nearest published incl[j] and
-// re-applies A_{j+1}..A_{t-1} in forward order, which reproduces the serial recursion
-// bit-for-bit whichever j it found: the result does not depend on timing.
-// Every published value is one 8-byte relaxed agent-scope store that is its own ready
-// flag (sentinel = all ones; NaN aggregates are canonicalised), read with sc1 loads.
+//   While the running sum S stays in one fp64 binade [2^E, 2^(E+1)) (spacing G =
+//   2^(E-52)), the add S + f rounds to a multiple of G, and the result depends on S
+//   only through S mod 2G (round-half-even looks at the parity of S/G).  So a thread
+//   runs its 16 adds twice, from B0 = 2^E (parity 0) and B1 = 2^E + G (parity 1):
+//   T_p = chain_p - B_p is its EXACT increment for a start of parity p.  All T are
+//   multiples of G, so the block scan of T0 is exact in any order.  Threads with
+//   T0 != T1 ("ties": an element with remainder exactly G/2) are resolved in order
+//   from their exact start parity (the lowest mantissa bit of the start).  A tile is
+//   "regular" when its exact start P >= 32 and P + total + 1 < 2^(E+1); otherwise
+//   (tile 0, binade crossings: about log2(d) tiles per vector) each thread takes the
+//   binade of its approximate start, threads near a binade edge add their 16 values
+//   one by one, and one lane walks the threads in order.
+//
+// Forms: the stream kernel carries the exact P from tile to tile (one workgroup per
+// client).  Batches of fewer clients fold per client: approximate tile sums ->
+// approximate prefixes P' (binade of each tile) -> exact tile maps (T for a start of
+// parity 0 / 1, ties resolved for both) -> exact serial fold (irregular tiles are
+// recomputed from their exact start) -> outputs from the exact P.  Every form gives
+// the sequential cumsum's bits, hence the same bits.
 // =====================================================================================
 __device__ __forceinline__ double wave_incl_scan(double v, int lane) {
 #pragma unroll
@@ -339,48 +344,32 @@ __device__ __forceinline__ double wave_incl_scan(double v, int lane) {
     return v;
 }
 
-__device__ __forceinline__ uint64_t canon_bits(double v) {
-    return v != v ? kCanonNaN : (uint64_t)__double_as_longlong(v);
+// Chain bases of the binade holding s: b0 = 2^E, b1 = 2^E + G (odd: lowest mantissa bit
+// set), top = 2^(E+1).  Below 32 (and for NaN / huge s) the E = 5 bases: such tiles and
+// threads are never "regular", the bases then only serve approximate sums.
+struct Binade {
+    double b0, b1, top;
+};
+__device__ __forceinline__ Binade binade_of(double s) {
+    const uint64_t e = (s >= 32.0 && s < 0x1p1000) ? ((uint64_t)__double_as_longlong(s) >> 52) : (uint64_t)(1023 + 5);
+    Binade b;
+    b.b0 = __longlong_as_double((long long)(e << 52));
+    b.b1 = __longlong_as_double((long long)((e << 52) | 1ull));
+    b.top = __longlong_as_double((long long)((e + 1) << 52));
+    return b;
 }
-
-// Wave 0 of the workgroup: P_t for tile `tile` of the vector whose slots start at
-// agg/incl.  Returns false on timeout (the abort word is then set).
-__device__ bool look_back(const uint64_t* agg, const uint64_t* incl, int32_t tile, int lane,
-                          uint32_t* ctrl, double* out_prefix) {
-    if (tile == 0) {
-        *out_prefix = 0.0;
-        return true;
-    }
-    uint32_t spins = 0;
-    for (;;) {
-        const int32_t j = tile - 1 - lane;          // lane 0 = nearest predecessor
-        const bool valid = j >= 0;
-        const uint64_t ib = valid ? ld_relaxed_agent(&incl[j]) : kEmpty;
-        const uint64_t ab = valid ? ld_relaxed_agent(&agg[j]) : kEmpty;
-        const uint64_t have_incl = __ballot(ib != kEmpty);
-        if (have_incl) {
-            const int L = __builtin_ctzll(have_incl);         // nearest published incl
-            const uint64_t need = (L == 0) ? 0ull : ((1ull << L) - 1ull);
-            const uint64_t have_agg = __ballot(ab != kEmpty);
-            if ((have_agg & need) == need) {
-                double P = __longlong_as_double(__shfl(ib, L, kWave));
-                for (int k = L - 1; k >= 0; --k)             // forward order: j0+1 .. t-1
-                    P = P + __longlong_as_double(__shfl(ab, k, kWave));
-                *out_prefix = P;
-                return true;
-            }
-        }
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 20) || ld_relaxed_agent32(ctrl + 1) != 0u) {
-            if (lane == 0) {
-                __hip_atomic_store(ctrl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            *out_prefix = 0.0;
-            return false;
-        }
-    }
+// A block-uniform double moved to scalar registers (keeps B and P out of VGPRs).
+__device__ __forceinline__ double uniform_d(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+// parity of s/G for s in its own binade: the lowest mantissa bit
+__device__ __forceinline__ bool lowbit(double s) { return ((uint32_t)__double_as_longlong(s) & 1u) != 0u; }
+// relative margin between an approximate prefix and a binade edge (covers the distance
+// between the sequential fp64 sum and any approximation of it for d < 2^31)
+constexpr double kEdge = 0x1p-20;
 
 #ifdef UQ_OLD_SWZ
 __device__ __forceinline__ int swz(int r, int c) { return r * 16 + 4 * (c ^ ((r >> 2) & 3)); }
@@ -527,8 +516,9 @@ __device__ __forceinline__ void build_table(float* s_tab, int tid, float L, floa
 // its own: v = +-0 gives fr = 0, hence r = 0 and out = (L1*0)*0/m = +0 = tab[0]; v = NaN
 // makes fl NaN and out NaN either way (AS:640).
 struct TileState {
-    double texcl;        // fp64 exclusive prefix of this thread's first element within the tile
-    double total;        // tile aggregate A_t (same value in every thread)
+    double texcl;        // exclusive prefix of t0 over the tile's threads (exact in a regular tile)
+    double total;        // sum of t0 over the tile (same value in every thread)
+    double t0, t1;       // this thread's increment from a start of parity 0 / 1 in the binade
 };
 
 // v = x / den (AS:625) without the IEEE division sequence (~10 VALU per element).  den is
@@ -584,20 +574,42 @@ __device__ __forceinline__ void div4(const float (&xs)[4], const DivPlan& dp, fl
     }
 }
 
-// fl (signed, see above) and fr of this thread's kQItems elements stay in registers
-// between the passes: a thread only ever reads back its own row.
+// mp = m*p of this thread's kQItems elements stays in registers between the passes, with
+// sign(v) folded in (v < 0 -> -mp; -0.0 marks a negative coordinate whose floor is 0); fl
+// and fr are re-derived from it (floor / subtract: the same f32 ops, so the same bits) --
+// one register per element instead of two.
 struct TileVals {
-    float fl[kQItems];
-    float fr[kQItems];
+    float mps[kQItems];
+};
+__device__ __forceinline__ float fr_of(float mps) {
+    const float mp = fabsf(mps);
+    return mp - floorf(mp);                     // AS:631
+}
+
+// LDS of the tile scan and the exact resolution (besides the scratch slots, see
+// resolve_exact)
+struct ScanLds {
+    double wave[kQBlock / kWave];        // wave sums of t0
+    uint64_t tmask[kQBlock / kWave];     // tie threads (pass 1); events (irregular tiles)
+    uint64_t kmask[kQBlock / kWave];     // constant parity transfer (pass 1)
+    uint64_t vmask[kQBlock / kWave];     // its value, else the flip bit (pass 1)
+    uint64_t cmask[kQBlock / kWave];     // clean threads (irregular tiles)
+    double rsum[kQBlock / kWave];        // irregular tiles: sum of the run ending the wave
+    uint32_t rhead[kQBlock / kWave];     // irregular tiles: that run starts inside the wave
+    double misc[2];
+    double aux[kQBlock];                 // t1 - t0 of tie threads (pass 1); run sums (irregular)
 };
 
-template <bool FULL>
-__device__ __forceinline__ void tile_pass1(const float* s_x, TileVals& tv, double* s_wave, int tid, int len,
-                                           const DivPlan& dp, float fm, TileState& st) {
+// pass 1.  TIES: run the parity-1 chain too and publish, before the barrier, the tie mask,
+// each thread's parity transfer in B's binade and t1 - t0 of tie threads; otherwise
+// t1 = t0 (approximate tile sums).
+template <bool FULL, bool TIES>
+__device__ __forceinline__ void tile_pass1(const float* s_x, TileVals& tv, ScanLds& sl, int tid, int len,
+                                           const DivPlan& dp, float fm, const Binade& B, TileState& st) {
     const int lane = tid & (kWave - 1);
     const int wid = tid / kWave;
     const int i0 = tid * kQItems;
-    double tsum = 0.0;
+    double c0 = B.b0, c1 = B.b1;
 #pragma unroll
     for (int k4 = 0; k4 < kQItems / 4; ++k4) {
         const float4 xv4 = *reinterpret_cast<const float4*>(&s_x[swz(tid, k4)]);
@@ -611,25 +623,347 @@ __device__ __forceinline__ void tile_pass1(const float* s_x, TileVals& tv, doubl
             const float mp = fm * p;            // AS:629
             const float fl = floorf(mp);        // AS:630
             float fr = mp - fl;                 // AS:631
-            if (!FULL && i0 + 4 * k4 + c >= len) fr = 0.0f;
-            tv.fl[4 * k4 + c] = v < 0.0f ? -fl : fl;
-            tv.fr[4 * k4 + c] = fr;
-            tsum += (double)fr;
+            float mps = v < 0.0f ? -mp : mp;
+            if (!FULL && i0 + 4 * k4 + c >= len) fr = mps = 0.0f;
+            tv.mps[4 * k4 + c] = mps;
+            c0 += (double)fr;                   // AS:635, from a parity-0 start
+            if (TIES) c1 += (double)fr;         // ... and from a parity-1 start
         }
     }
-    const double incl_w = wave_incl_scan(tsum, lane);
+    st.t0 = c0 - B.b0;                          // exact (Sterbenz)
+    st.t1 = TIES ? c1 - B.b1 : st.t0;
+    const double incl_w = wave_incl_scan(st.t0, lane);
     double wexcl = __shfl_up(incl_w, 1, kWave);
     if (lane == 0) wexcl = 0.0;
-    if (lane == kWave - 1) s_wave[wid] = incl_w;
+    if (lane == kWave - 1) sl.wave[wid] = incl_w;
+    if (TIES) {
+        // parity transfer (regular tiles): a start of parity 0 ends on parity e0 = par(t0),
+        // one of parity 1 on e1 = 1 ^ par(t1); par(t) = lowest mantissa bit of t + 2^E
+        const bool tie = st.t0 != st.t1;
+        const bool e0 = lowbit(st.t0 + B.b0);
+        const bool e1 = !lowbit(st.t1 + B.b0);
+        const uint64_t tm = __ballot(tie);
+        const uint64_t km = __ballot(e0 == e1);
+        const uint64_t vm = __ballot(e0);
+        if (lane == 0) {
+            sl.tmask[wid] = tm;
+            sl.kmask[wid] = km;
+            sl.vmask[wid] = vm;
+        }
+        if (tie) sl.aux[tid] = st.t1 - st.t0;
+    }
     __syncthreads();
     double wbase = 0.0, total = 0.0;
 #pragma unroll
     for (int w = 0; w < kQBlock / kWave; ++w) {
-        if (w < wid) wbase += s_wave[w];
-        total += s_wave[w];
+        if (w < wid) wbase += sl.wave[w];
+        total += sl.wave[w];
     }
     st.texcl = wbase + wexcl;
-    st.total = total;
+    st.total = uniform_d(total);
+}
+
+__device__ __forceinline__ double* slot_of(float* s_scr, int t) { return reinterpret_cast<double*>(s_scr + t * kQItems); }
+
+// Cumulative tie correction of the last tie thread before `tid` (slot[3]), 0 if none.
+__device__ __forceinline__ double tie_corr(float* s_scr, const ScanLds& sl, int tid) {
+    const int lane = tid & (kWave - 1);
+    int w = tid / kWave;
+    uint64_t mk = sl.tmask[w] & ((1ull << lane) - 1ull);
+    while (mk == 0ull && w > 0) mk = sl.tmask[--w];
+    if (mk == 0ull) return 0.0;
+    return slot_of(s_scr, w * kWave + 63 - __builtin_clzll(mk))[3];
+}
+
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+constexpr int kFastTies = 32;   // ties per regular tile resolved from the parity transfers
+
+// Parity of the running sum at the start of each thread of a regular tile whose start
+// has parity pP: the threads' parity transfers composed in order.  Each is a constant (a
+// tie thread whose two chains end on the same parity) or an xor with a fixed bit, so a
+// thread's start parity is the last constant before it xor the flips after that.  The
+// masks and the four wave-start parities live in scalar registers (built once per tile).
+struct ParityCtx {
+    uint64_t km[kQBlock / kWave], vm[kQBlock / kWave];
+    bool pw[kQBlock / kWave];
+};
+__device__ __forceinline__ void parity_ctx(const ScanLds& sl, bool pP, ParityCtx& c) {
+    bool p = pP;
+#pragma unroll
+    for (int w = 0; w < kQBlock / kWave; ++w) {
+        const uint64_t km = uniform_u64(sl.kmask[w]), vm = uniform_u64(sl.vmask[w]);
+        c.km[w] = km;
+        c.vm[w] = vm;
+        c.pw[w] = p;
+        if (km) {
+            const int j = 63 - __builtin_clzll(km);
+            p = (((vm >> j) & 1ull) != 0ull) != ((__builtin_popcountll(~km & vm & ~((2ull << j) - 1ull)) & 1) != 0);
+        } else {
+            p = p != ((__builtin_popcountll(vm) & 1) != 0);
+        }
+    }
+}
+// start parity of lane b of wave W (W a compile-time index after unrolling)
+template <int W>
+__device__ __forceinline__ bool parity_in(const ParityCtx& c, int b) {
+    const uint64_t lim = (1ull << b) - 1ull;
+    const uint64_t cc = c.km[W] & lim;
+    const uint64_t x = ~c.km[W] & c.vm[W] & lim;
+    if (cc) {
+        const int j = 63 - __builtin_clzll(cc);
+        return (((c.vm[W] >> j) & 1ull) != 0ull) != ((__builtin_popcountll(x & ~((2ull << j) - 1ull)) & 1) != 0);
+    }
+    return c.pw[W] != ((__builtin_popcountll(x) & 1) != 0);
+}
+
+// Sum of t1 - t0 over the tie threads of wave W whose start is odd: all of them (Dt) and
+// those before thread `tid` (Db).
+template <int W>
+__device__ __forceinline__ void tie_sums(const ScanLds& sl, const ParityCtx& c, int tid, double& Db, double& Dt) {
+    uint64_t mk = uniform_u64(sl.tmask[W]);
+    while (mk) {
+        const int b = __builtin_ctzll(mk);
+        mk &= mk - 1ull;
+        if (parity_in<W>(c, b)) {
+            const double dd = sl.aux[W * kWave + b];
+            Dt = Dt + dd;
+            if (W * kWave + b < tid) Db = Db + dd;
+        }
+    }
+}
+
+// Exact thread base (prefix before this thread's first element) and exact P_{t+1}, from
+// the exact tile start P.  s_scr: the tile's LDS image after pass 1 (thread t's row =
+// floats [16t, 16t+16) is its scratch slot).  Ends with a barrier whenever it used the
+// scratch, so the caller may rewrite the image right after.
+__device__ double resolve_exact(double P, const Binade& B, const TileState& st, const TileVals& tv, float* s_scr,
+                                ScanLds& sl, int tid, double& pnext) {
+    double* slot = slot_of(s_scr, tid);
+    if (P >= 32.0 && (P + st.total) + 1.0 < B.top) {            // regular (uniform)
+        int nt = 0;
+#pragma unroll
+        for (int w = 0; w < kQBlock / kWave; ++w) nt += __builtin_popcountll(uniform_u64(sl.tmask[w]));
+        if (nt == 0
+#ifdef UQ_EXP_NOTIES
+            || true
+#endif
+        ) {
+            pnext = P + st.total;                                // exact: multiples of G in the binade
+            return P + st.texcl;
+        }
+        if (nt <= kFastTies) {
+            // a tie thread adds t1 - t0 when its start is odd: no barrier, no walk
+            ParityCtx pc;
+            parity_ctx(sl, lowbit(P), pc);
+            double Db = 0.0, Dt = 0.0;
+            tie_sums<0>(sl, pc, tid, Db, Dt);
+            tie_sums<1>(sl, pc, tid, Db, Dt);
+            tie_sums<2>(sl, pc, tid, Db, Dt);
+            tie_sums<3>(sl, pc, tid, Db, Dt);
+            pnext = (P + st.total) + Dt;
+            return (P + st.texcl) + Db;
+        }
+        if (st.t0 != st.t1) {
+            slot[0] = st.texcl;
+            slot[1] = st.t0;
+            slot[2] = st.t1;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double D = 0.0;
+            for (int w = 0; w < kQBlock / kWave; ++w) {
+                uint64_t mk = sl.tmask[w];
+                while (mk) {
+                    double* q = slot_of(s_scr, w * kWave + __builtin_ctzll(mk));
+                    mk &= mk - 1ull;
+                    const double t0 = q[1], t1 = q[2];
+                    const double Sk = (P + q[0]) + D;            // exact start of the tie thread
+                    D = D + ((lowbit(Sk) ? t1 : t0) - t0);
+                    q[3] = D;
+                }
+            }
+            sl.misc[0] = D;
+        }
+        __syncthreads();
+        const double corr = tie_corr(s_scr, sl, tid);
+        const double D = sl.misc[0];
+        __syncthreads();
+        pnext = (P + st.total) + D;
+        return (P + st.texcl) + corr;
+    }
+#ifdef UQ_EXP_NOIRR
+    pnext = P + st.total; return P + st.texcl;
+#endif
+    // irregular tile: each thread in the binade of its approximate start
+    const int lane = tid & (kWave - 1);
+    const double sa = P + st.texcl;
+    const Binade bt = binade_of(sa);
+    const bool clean = sa >= 32.0 && sa >= bt.b0 * (1.0 + kEdge) && (sa + st.t0) + 1.0 < bt.top;
+    double t0c = 0.0, t1c = 0.0;
+    if (clean) {
+        double c0 = bt.b0, c1 = bt.b1;
+#pragma unroll
+        for (int k = 0; k < kQItems; ++k) {
+            const double f = (double)fr_of(tv.mps[k]);
+            c0 += f;
+            c1 += f;
+        }
+        t0c = c0 - bt.b0;
+        t1c = c1 - bt.b1;
+        slot[0] = t0c;
+        slot[1] = t1c;
+    } else {
+#pragma unroll
+        for (int k4 = 0; k4 < kQItems / 4; ++k4)
+            reinterpret_cast<float4*>(slot)[k4] = make_float4(fr_of(tv.mps[4 * k4]), fr_of(tv.mps[4 * k4 + 1]),
+                                                              fr_of(tv.mps[4 * k4 + 2]), fr_of(tv.mps[4 * k4 + 3]));
+    }
+    // Events: threads whose increment is not a fixed multiple of their run's G -- not clean
+    // (added one by one from their exact start) or a clean tie (t0 != t1).  Between events,
+    // clean threads form runs inside one binade (consecutive clean threads cannot straddle
+    // an edge: each ends 1 below it); their t0 are multiples of that G and a run sums to
+    // less than 2^E, so a SEGMENTED scan of t0 (a run starts after each event) is exact in
+    // any order.  One lane then walks the events only.
+    const int wid = tid / kWave;
+    const bool event = !clean || t0c != t1c;
+    const double v = event ? 0.0 : t0c;
+    const uint64_t em = __ballot(event);
+    const uint64_t cm = __ballot(clean);
+    bool f = tid == 0 || (lane > 0 && ((em >> (lane - 1)) & 1ull) != 0ull);   // run head, in-wave view
+    double x = v;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {                       // segmented inclusive scan, wave level
+        const double xu = __shfl_up(x, o, kWave);
+        const int fu = __shfl_up((int)f, o, kWave);
+        if (lane >= o) {
+            if (!f) x = xu + x;
+            f = f || fu != 0;
+        }
+    }
+    if (lane == kWave - 1) {
+        sl.rsum[wid] = x;                                      // sum of the run that ends the wave
+        sl.rhead[wid] = f ? 1u : 0u;                           // that run starts inside the wave
+    }
+    if (lane == 0) {
+        sl.tmask[wid] = em;
+        sl.cmask[wid] = cm;
+    }
+    __syncthreads();
+    if (!f) {                                                  // the run comes from earlier waves
+        for (int w = wid - 1; w >= 0; --w) {
+            if ((sl.tmask[w] >> (kWave - 1)) & 1ull) break;    // wave w ends with an event
+            x = sl.rsum[w] + x;
+            if (sl.rhead[w]) break;
+        }
+    }
+    sl.aux[tid] = x;                                           // inclusive run sum
+    __syncthreads();
+    if (tid == 0) {
+        double S = P;                                          // exact value at the current run head
+        for (int w = 0; w < kQBlock / kWave; ++w) {
+            uint64_t mk = sl.tmask[w];
+            while (mk) {
+                const int b = __builtin_ctzll(mk);
+                const int k = w * kWave + b;
+                mk &= mk - 1ull;
+                double* q = slot_of(s_scr, k);
+                S = S + sl.aux[k];                             // exact start of event k (its own v is 0)
+                sl.aux[k] = S;
+                if ((sl.cmask[w] >> b) & 1ull) {
+                    const double t0 = q[0], t1 = q[1];
+                    S = S + (lowbit(S) ? t1 : t0);
+                } else {
+                    for (int k4 = 0; k4 < kQItems / 4; ++k4) {
+                        const float4 f4 = reinterpret_cast<const float4*>(q)[k4];
+                        S = (((S + (double)f4.x) + (double)f4.y) + (double)f4.z) + (double)f4.w;
+                    }
+                }
+                q[6] = S;                                      // value at the head of the next run
+            }
+        }
+        const bool last_event = (sl.tmask[kQBlock / kWave - 1] >> (kWave - 1)) & 1ull;
+        sl.misc[0] = last_event ? S : S + sl.aux[kQBlock - 1];
+    }
+    __syncthreads();
+    double base;
+    if (event) {
+        base = sl.aux[tid];
+    } else {
+        int w = wid;                                           // the last event before this thread
+        uint64_t mk = sl.tmask[w] & ((1ull << lane) - 1ull);
+        while (mk == 0ull && w > 0) mk = sl.tmask[--w];
+        const double start = mk ? slot_of(s_scr, w * kWave + 63 - __builtin_clzll(mk))[6] : P;
+        base = start + (x - v);                                // + exclusive run sum (exact)
+    }
+    pnext = sl.misc[0];
+    __syncthreads();
+    return base;
+}
+
+// Tile map from an APPROXIMATE start Pg (the per-client fold of the small-batch forms):
+// if the exact start is certainly in Pg's binade and the tile stays in it, the tile's
+// exact increment for a start of parity p is m[p] (ties resolved for both parities).
+// Returns false for an irregular tile (resolved later from its exact start).
+__device__ bool resolve_map(double Pg, const Binade& B, const TileState& st, float* s_scr, ScanLds& sl, int tid,
+                            double& m0, double& m1) {
+    if (!(Pg >= 32.0 && Pg >= B.b0 * (1.0 + kEdge) && (Pg + st.total) + 1.0 < B.top)) return false;   // uniform
+    int nt = 0;
+#pragma unroll
+    for (int w = 0; w < kQBlock / kWave; ++w) nt += __builtin_popcountll(uniform_u64(sl.tmask[w]));
+    if (nt == 0) {
+        m0 = m1 = st.total;
+        return true;
+    }
+    if (nt <= kFastTies) {
+        ParityCtx p0, p1;
+        parity_ctx(sl, false, p0);
+        parity_ctx(sl, true, p1);
+        double D0 = 0.0, D1 = 0.0, unused = 0.0;
+        tie_sums<0>(sl, p0, 0, unused, D0);
+        tie_sums<1>(sl, p0, 0, unused, D0);
+        tie_sums<2>(sl, p0, 0, unused, D0);
+        tie_sums<3>(sl, p0, 0, unused, D0);
+        tie_sums<0>(sl, p1, 0, unused, D1);
+        tie_sums<1>(sl, p1, 0, unused, D1);
+        tie_sums<2>(sl, p1, 0, unused, D1);
+        tie_sums<3>(sl, p1, 0, unused, D1);
+        m0 = st.total + D0;
+        m1 = st.total + D1;
+        return true;
+    }
+    double* slot = slot_of(s_scr, tid);
+    if (st.t0 != st.t1) {
+        slot[0] = st.texcl;
+        slot[1] = st.t0;
+        slot[2] = st.t1;
+    }
+    __syncthreads();
+    if (tid < 2) {
+        // start parity p = tid: the parity at a tie thread is p xor parity((texcl + D)/G),
+        // read off (texcl + D) + 2^E (exact: texcl + D < 2^E is a multiple of G)
+        const bool p = tid != 0;
+        double D = 0.0;
+        for (int w = 0; w < kQBlock / kWave; ++w) {
+            uint64_t mk = sl.tmask[w];
+            while (mk) {
+                const double* q = slot_of(s_scr, w * kWave + __builtin_ctzll(mk));
+                mk &= mk - 1ull;
+                const double t0 = q[1], t1 = q[2];
+                const bool par = p != lowbit((q[0] + D) + B.b0);
+                D = D + ((par ? t1 : t0) - t0);
+            }
+        }
+        sl.misc[tid] = D;
+    }
+    __syncthreads();
+    m0 = st.total + sl.misc[0];
+    m1 = st.total + sl.misc[1];
+    __syncthreads();
+    return true;
 }
 
 // Wire code of one coordinate (type codes, see uq_dme.h): k = fl + r ->
@@ -637,46 +971,47 @@ __device__ __forceinline__ void tile_pass1(const float* s_x, TileVals& tv, doubl
 // outputs).  kmax (float) tracks the largest k; a client whose kmax > 127 is flagged as
 // overflow (its codes are meaningless).  fl is finite whenever L1 is finite, and a
 // non-finite L1 flags the client separately (publish_kmax).
-__device__ __forceinline__ uint32_t code_of(float fl_s, float kf, float& kmax) {
-    kmax = fmaxf(kmax, kf);
-    const int mask = (int)__float_as_uint(fl_s) >> 31;      // 0 or -1
+__device__ __forceinline__ uint32_t code_of(float mps, float kf) {
+    const int mask = (int)__float_as_uint(mps) >> 31;       // 0 or -1: sign(v) < 0
     return (uint32_t)(((int)kf ^ mask) & 0xFF);
 }
 
 // pass 2; WQ: outputs into the LDS image s_o, WC: this thread's 16 codes into cw.
 template <bool WQ, bool WC>
-__device__ __forceinline__ void tile_pass2(float* s_o, const TileVals& tv, const float* s_tab, int tid, double P,
-                                           float L, float fm, float Xv, const TileState& st, uint32_t (&cw)[4],
-                                           float& kmax) {
-    double s = P + st.texcl;
+__device__ __forceinline__ void tile_pass2(float* s_o, const TileVals& tv, const float* s_tab, int tid, double base,
+                                           float L, float fm, float Xv, uint32_t (&cw)[4], float& kmax) {
+    double s = base;                           // exact prefix before this thread's first element
     float fprev = floorf((float)s - Xv);       // floor(c_{i-1} - X) of this thread's first element
+    // k = fl + r can only be NaN when L1 is not finite: such a client takes the arithmetic
+    // path for every element; otherwise a running max of k bounds the table reads
+    const bool arith = !(fabsf(L) <= 3.40282347e38f);
 #pragma unroll
     for (int k4 = 0; k4 < kQItems / 4; ++k4) {
         float o[4], kfs[4];
-        bool off_table = false;
+        float m4 = 0.0f;
         uint32_t w = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const float fl = tv.fl[4 * k4 + c];
-            s += (double)tv.fr[4 * k4 + c];                    // AS:635 fp64 running sum
+            const float mps = tv.mps[4 * k4 + c];
+            const float mp = fabsf(mps);
+            const float fla = floorf(mp);                      // AS:630
+            s += (double)(mp - fla);                           // AS:631, AS:635 fp64 running sum
             const float fcur = floorf((float)s - Xv);          // AS:636 floor(c_i - X)
             const float r = (fcur - fprev == 1.0f) ? 1.0f : 0.0f;   // AS:636-637
             fprev = fcur;
-            const float kf = fabsf(fl) + r;                    // fl + r
+            const float kf = fla + r;                          // fl + r
             kfs[c] = kf;
-            if (WQ) {
-                // AS:640 via the table; the index is clamped so the four LDS reads issue
-                // together, and k >= kTab / NaN are recomputed below (rare)
-                o[c] = copysignf(s_tab[(int)fminf(kf, (float)(kTab - 1))], fl);
-                off_table |= !(kf < (float)kTab);
-            }
-            if (WC) w |= code_of(fl, kf, kmax) << (8 * c);     // padding elements: fl = 0, r = 0
+            m4 = fmaxf(m4, kf);
+            // AS:640 via the table, sign(v) from mps; k >= kTab is recomputed below (rare)
+            if (WQ) o[c] = copysignf(s_tab[(int)kf & (kTab - 1)], mps);
+            if (WC) w |= code_of(mps, kf) << (8 * c);          // padding elements: mps = 0, r = 0
         }
-        if (WQ && __builtin_expect(off_table, 0)) {
+        if (WC) kmax = fmaxf(kmax, m4);
+        if (WQ && __builtin_expect(!(m4 < (float)kTab) || arith, 0)) {
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-                if (!(kfs[c] < (float)kTab))
-                    o[c] = (copysignf(L, tv.fl[4 * k4 + c]) * kfs[c]) / fm;   // ((L1*sign)*(fl+r))/m
+                if (!(kfs[c] < (float)kTab) || arith)
+                    o[c] = (copysignf(L, tv.mps[4 * k4 + c]) * kfs[c]) / fm;   // ((L1*sign)*(fl+r))/m
         }
         if (WQ) *reinterpret_cast<float4*>(&s_o[swz(tid, k4)]) = make_float4(o[0], o[1], o[2], o[3]);
         if (WC) cw[k4] = w;
@@ -729,10 +1064,10 @@ __device__ __forceinline__ void store_tile(const float* s_data, float* __restric
 }
 
 // K2-stream: one workgroup streams one whole client vector, tiles in order, the next
-// tile prefetched into registers; P_{t+1} = fl64(P_t + A_t) carried in the workgroup.
-// No inter-workgroup communication at all.  Used when there are enough clients to
-// fill the GPU (batched DME, the bench workload).  Requires d % 4 == 0 and 4*d < 2^31
-// (buffer addressing); the host falls back to the look-back kernel otherwise.
+// tile prefetched into registers; the exact prefix P is carried in the workgroup.  No
+// inter-workgroup communication at all.  Used when there are enough clients to fill
+// the GPU (batched DME, the bench workload).  Requires d % 4 == 0 and 4*d < 2^31
+// (buffer addressing); the host uses the per-tile form otherwise.
 //
 // Order of the vector-memory operations per iteration t: stores of tile t-1 (q from the
 // LDS image s_o, codes from registers), THEN the loads of tile t+1.  vmcnt counts stores
@@ -741,18 +1076,18 @@ __device__ __forceinline__ void store_tile(const float* s_data, float* __restric
 // whole compute of tile t.
 //
 // Segments: workgroup b takes client b / nseg, tiles [s*seg_tiles, (s+1)*seg_tiles) with
-// s = b % nseg, starting from P = pre[first tile] (the per-client fold of the phased
-// form) -- or from P = 0 over the whole vector when nseg == 1 (pre == nullptr).
+// s = b % nseg, starting from the exact P = pre[first tile] (the per-client fold of the
+// small-batch form) -- or from P = 0 over the whole vector when nseg == 1 (pre == nullptr).
 template <bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock, 4)
 quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                        int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
                        const float* __restrict__ Xs, const float* __restrict__ l1, int32_t seg_tiles, int32_t nseg,
                        const uint64_t* __restrict__ pre) {
-    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image of tile t
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image of tile t (then scratch)
     __shared__ __attribute__((aligned(16))) float s_o[kQTile];     // output image of tile t-1 / t
     __shared__ float s_tab[kTab];
-    __shared__ double s_wave[kQBlock / kWave];
+    __shared__ ScanLds sl;
     const int tid = threadIdx.x;
     const int64_t vec = blockIdx.x / (uint32_t)nseg;
     const int32_t tb = (int32_t)(blockIdx.x % (uint32_t)nseg) * seg_tiles;
@@ -760,10 +1095,14 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     const float L = l1[vec];
     const DivPlan dp = div_plan(L);
     const float Xv = Xs[vec];
+#ifdef UQ_ABL_NOIO
+    const uint32_t row_bytes = 0;              // timing-only ablation: every access dropped
+#else
     const uint32_t row_bytes = (uint32_t)(d * 4);
+#endif
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, row_bytes);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(WQ ? out + vec * d : x, row_bytes);
-    const __amdgpu_buffer_rsrc_t rc = make_rsrc(WC ? (const void*)(codes + vec * d) : (const void*)x, (uint32_t)d);
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(WC ? (const void*)(codes + vec * d) : (const void*)x, row_bytes / 4u);
     TileRegs pre_x;
     load_tile_buf(pre_x, rx, (uint32_t)tb * (uint32_t)(kQTile * 4), tid);
     build_table(s_tab, tid, L, fm);
@@ -781,15 +1120,27 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         if (tile + 1 < te) load_tile_buf(pre_x, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
         const int64_t t0 = (int64_t)tile * kQTile;
         const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+#ifdef UQ_ABL_COPY
+        // timing-only ablation: the tile's memory traffic without the arithmetic
+        __syncthreads();
+#pragma unroll
+        for (int k4 = 0; k4 < kQItems / 4; ++k4)
+            *reinterpret_cast<float4*>(&s_o[swz(tid, k4)]) = *reinterpret_cast<const float4*>(&s_x[swz(tid, k4)]);
+#else
         TileState st;
         TileVals tv;
+        P = uniform_d(P);
+        const Binade B = binade_of(P);
         // pass 1's barrier also orders the s_o reads above before pass 2's s_o writes
         if (len == kQTile)
-            tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
+            tile_pass1<true, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
         else
-            tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
-        tile_pass2<WQ, WC>(s_o, tv, s_tab, tid, P, L, fm, Xv, st, cw, kmax);
-        P = P + st.total;                          // serial definition of the tile prefix
+            tile_pass1<false, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
+        double pnext;
+        const double base = resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);
+        tile_pass2<WQ, WC>(s_o, tv, s_tab, tid, base, L, fm, Xv, cw, kmax);
+        P = pnext;
+#endif
     }
     __syncthreads();
     const uint32_t tp = (uint32_t)(te - 1) * (uint32_t)kQTile;
@@ -800,19 +1151,28 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     }
 }
 
-// Phase 1 of the segmented (phased) form: tile aggregates A_t over a segment, streamed
-// with the same prefetch as the stream kernel (pass 1 only; 4 B per element read).
+// ---- small-batch forms (fewer clients than fill the GPU one workgroup per client) ----
+//   approximate tile sums A_t (agg_stream_kernel over segments, or tile_agg_kernel)
+//   tile_prefix_kernel   per client P'_t = sum of A_j, j < t (approximate prefixes)
+//   tile_map_kernel      per tile, in the binade of P'_t: exact map (m0, m1), or NaN
+//   exact_fold_kernel    per client, serial: P_0 = 0, P_{t+1} = P_t + m[parity(P_t)];
+//                        irregular tiles recomputed from their exact P_t
+//   outputs              quantize_stream_kernel over segments / tile_out_kernel from P_t
+// Maps and prefixes are stored as raw fp64 bits in u64 arrays.
+
+// Approximate tile sums over a segment, streamed with the stream kernel's prefetch.
 __global__ void __launch_bounds__(kQBlock, 4)
 agg_stream_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
                   int32_t seg_tiles, int32_t nseg, uint64_t* __restrict__ agg) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
-    __shared__ double s_wave[kQBlock / kWave];
+    __shared__ ScanLds sl;
     const int tid = threadIdx.x;
     const int64_t vec = blockIdx.x / (uint32_t)nseg;
     const int32_t tb = (int32_t)(blockIdx.x % (uint32_t)nseg) * seg_tiles;
     const int32_t te = min(tiles, tb + seg_tiles);
     const DivPlan dp = div_plan(l1[vec]);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, (uint32_t)(d * 4));
+    const Binade B = binade_of(0.0);
     TileRegs pre_x;
     load_tile_buf(pre_x, rx, (uint32_t)tb * (uint32_t)(kQTile * 4), tid);
     for (int32_t tile = tb; tile < te; ++tile) {
@@ -824,107 +1184,20 @@ agg_stream_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
         TileState st;
         TileVals tv;
         if (len == kQTile)
-            tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
+            tile_pass1<true, false>(s_x, tv, sl, tid, len, dp, fm, B, st);
         else
-            tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
+            tile_pass1<false, false>(s_x, tv, sl, tid, len, dp, fm, B, st);
         if (tid == 0) agg[vec * tiles + tile] = (uint64_t)__double_as_longlong(st.total);
     }
 }
 
-// K2-lookback: persistent workgroups over ticketed tiles with the deterministic
-// decoupled look-back above.  Used when there are too few clients to fill the GPU
-// one-vector-per-workgroup (e.g. the per-client drop-in call).
-template <bool VEC4, bool WQ, bool WC, bool CVEC>
-__global__ void __launch_bounds__(kQBlock)
-quantize_lookback_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
-                         int32_t* __restrict__ overflow, int64_t d, int32_t tiles,
-                         uint32_t total_tiles, float fm, const float* __restrict__ Xs, const float* __restrict__ l1,
-                         uint64_t* __restrict__ agg, uint64_t* __restrict__ incl, uint32_t* __restrict__ ctrl) {
-    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image, then output image
-    __shared__ double s_wave[kQBlock / kWave];
-    __shared__ float s_tab[kTab];
-    __shared__ double s_prefix;
-    __shared__ uint32_t s_ticket;
-    __shared__ int64_t s_tabvec;
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wid = tid / kWave;
-
-    if (tid == 0) {
-        s_ticket = atomicAdd(ctrl, 1u);
-        s_tabvec = -1;
-    }
-    __syncthreads();
-    uint32_t cur = s_ticket;
-    if (cur >= total_tiles) return;
-    TileRegs pre;
-    load_tile<VEC4>(pre, x, d, tiles, cur, tid);
-    for (;;) {
-        stage_tile<VEC4>(pre, s_x, tid);
-        __syncthreads();
-        const int64_t vec = cur / (uint32_t)tiles;
-        const int32_t tile = cur % (uint32_t)tiles;
-        const int64_t t0 = (int64_t)tile * kQTile;
-        const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
-        const float L = l1[vec];
-        const DivPlan dp = div_plan(L);
-        if (s_tabvec != vec) build_table(s_tab, tid, L, fm);   // uniform; tab read after pass 1's barrier
-        TileState st;
-        TileVals tv;
-        if (len == kQTile)
-            tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
-        else
-            tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
-        uint64_t* aggv = agg + vec * tiles;
-        uint64_t* inclv = incl + vec * tiles;
-        if (tid == 0) s_tabvec = vec;              // every thread has tested s_tabvec before pass 1's barrier
-        if (wid == 0) {
-            if (lane == 0 && tile > 0) st_relaxed_agent(&aggv[tile], canon_bits(st.total));
-            double P = 0.0;
-            look_back(aggv, inclv, tile, lane, ctrl, &P);
-            if (lane == 0) {
-                st_relaxed_agent(&inclv[tile], canon_bits(P + st.total));
-                s_prefix = P;
-                // the next ticket only now: from here this workgroup never waits again, so
-                // the aggregate of the ticket it takes is published within about one tile
-                // time.  (Taken earlier, a held ticket's aggregate would wait on this
-                // tile's look-back, and look-back waits would chain.)
-                s_ticket = atomicAdd(ctrl, 1u);
-            }
-        }
-        __syncthreads();
-        const uint32_t nxt = s_ticket;
-        if (nxt < total_tiles) load_tile<VEC4>(pre, x, d, tiles, nxt, tid);   // overlaps pass 2 + stores
-        uint32_t cw[4];
-        float kmax = 0.0f;
-        tile_pass2<WQ, WC>(s_x, tv, s_tab, tid, s_prefix, L, fm, Xs[vec], st, cw, kmax);   // s_x free after pass 1
-        if (WC) {
-            store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
-            publish_kmax(kmax, L, overflow, vec, tid);
-        }
-        __syncthreads();
-        if (WQ) store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
-        if (nxt >= total_tiles) break;
-        cur = nxt;
-        __syncthreads();
-    }
-}
-
-// K2-phased: few clients with many tiles (1 < n < kStreamMinClients).  Three launches,
-// no inter-workgroup waits at all:
-//   tile_agg_kernel    one workgroup per tile: pass 1 -> tile aggregate A_t (the same
-//                      fixed tree as every other K2 form)
-//   tile_prefix_kernel one thread per client: P_0 = 0, P_{t+1} = fl64(P_t + A_t) -- the
-//                      serial recursion the stream kernel carries and the look-back
-//                      reproduces, so all three forms give the same bits
-//   tile_out_kernel    one workgroup per tile: pass 1 again, pass 2 from P_t, stores.
-// x is read twice (plus K1); at these batch sizes the second read mostly hits the MALL.
+// Approximate tile sums, one workgroup per tile (any row alignment).
 template <bool VEC4>
 __global__ void __launch_bounds__(kQBlock)
 tile_agg_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
                 uint64_t* __restrict__ agg) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
-    __shared__ double s_wave[kQBlock / kWave];
+    __shared__ ScanLds sl;
     const int tid = threadIdx.x;
     const int32_t tile = blockIdx.x;
     const int64_t vec = blockIdx.y;
@@ -935,15 +1208,17 @@ tile_agg_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
     const int64_t t0 = (int64_t)tile * kQTile;
     const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
     const DivPlan dp = div_plan(l1[vec]);
+    const Binade B = binade_of(0.0);
     TileState st;
     TileVals tv;
     if (len == kQTile)
-        tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
+        tile_pass1<true, false>(s_x, tv, sl, tid, len, dp, fm, B, st);
     else
-        tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
+        tile_pass1<false, false>(s_x, tv, sl, tid, len, dp, fm, B, st);
     if (tid == 0) agg[vec * tiles + tile] = (uint64_t)__double_as_longlong(st.total);
 }
 
+// One thread per client: approximate prefixes P'_t (they only choose each tile's binade).
 __global__ void __launch_bounds__(256)
 tile_prefix_kernel(const uint64_t* __restrict__ agg, uint64_t* __restrict__ pre, int64_t n, int32_t tiles) {
     const int64_t vec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -957,14 +1232,108 @@ tile_prefix_kernel(const uint64_t* __restrict__ agg, uint64_t* __restrict__ pre,
     }
 }
 
+// Exact tile maps in the binade of P'_t: map0[t] = m0 (NaN: irregular), map1[t] = m1.
+template <bool VEC4>
+__global__ void __launch_bounds__(kQBlock)
+tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
+                const uint64_t* __restrict__ pre_approx, uint64_t* __restrict__ map0, uint64_t* __restrict__ map1) {
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];
+    __shared__ ScanLds sl;
+    const int tid = threadIdx.x;
+    const int32_t tile = blockIdx.x;
+    const int64_t vec = blockIdx.y;
+    const int64_t idx = vec * tiles + tile;
+    const double Pg = __longlong_as_double((long long)pre_approx[idx]);
+    const Binade B = binade_of(Pg);
+    if (!(Pg >= 32.0 && Pg >= B.b0 * (1.0 + kEdge))) {          // certainly irregular: skip the work
+        if (tid == 0) {
+            map0[idx] = (uint64_t)__double_as_longlong(__builtin_nan(""));
+            map1[idx] = 0ull;
+        }
+        return;
+    }
+    TileRegs r;
+    load_tile<VEC4>(r, x, d, tiles, (uint32_t)idx, tid);
+    stage_tile<VEC4>(r, s_x, tid);
+    __syncthreads();
+    const int64_t t0 = (int64_t)tile * kQTile;
+    const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+    const DivPlan dp = div_plan(l1[vec]);
+    TileState st;
+    TileVals tv;
+    if (len == kQTile)
+        tile_pass1<true, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
+    else
+        tile_pass1<false, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
+    double m0 = 0.0, m1 = 0.0;
+    const bool ok = resolve_map(Pg, B, st, s_x, sl, tid, m0, m1);
+    if (tid == 0) {
+        map0[idx] = (uint64_t)__double_as_longlong(ok ? m0 : __builtin_nan(""));
+        map1[idx] = (uint64_t)__double_as_longlong(m1);
+    }
+}
+
+constexpr int kFoldChunk = 1024;   // tile maps staged in LDS at a time
+
+// One workgroup per client: the exact serial fold over its tile maps; irregular tiles are
+// loaded and resolved from their exact start.  pre[t] = exact P_t.
+template <bool VEC4>
+__global__ void __launch_bounds__(kQBlock)
+exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
+                  const uint64_t* __restrict__ map0, const uint64_t* __restrict__ map1, uint64_t* __restrict__ pre) {
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];
+    __shared__ ScanLds sl;
+    const int tid = threadIdx.x;
+    const int64_t vec = blockIdx.x;
+    const DivPlan dp = div_plan(l1[vec]);
+    __shared__ double s_m0[kFoldChunk], s_m1[kFoldChunk];
+    double P = 0.0;
+    for (int32_t tile = 0; tile < tiles; ++tile) {
+        const int64_t idx = vec * tiles + tile;
+        const int ci = tile % kFoldChunk;
+        if (ci == 0) {                                         // stage the next chunk of maps
+            __syncthreads();
+            for (int i = tid; i < kFoldChunk && tile + i < tiles; i += kQBlock) {
+                s_m0[i] = __longlong_as_double((long long)map0[idx + i]);
+                s_m1[i] = __longlong_as_double((long long)map1[idx + i]);
+            }
+            __syncthreads();
+        }
+        if (tid == 0) pre[idx] = (uint64_t)__double_as_longlong(P);
+        const double m0 = s_m0[ci];
+        if (m0 == m0) {                                        // regular: P stays in the map's binade
+            P = P + (lowbit(P) ? s_m1[ci] : m0);
+            continue;
+        }
+        TileRegs r;
+        load_tile<VEC4>(r, x, d, tiles, (uint32_t)idx, tid);
+        stage_tile<VEC4>(r, s_x, tid);
+        __syncthreads();
+        const int64_t t0 = (int64_t)tile * kQTile;
+        const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+        const Binade B = binade_of(P);
+        TileState st;
+        TileVals tv;
+        if (len == kQTile)
+            tile_pass1<true, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
+        else
+            tile_pass1<false, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
+        double pnext;
+        (void)resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);
+        __syncthreads();                                       // s_x / sl reused by the next irregular tile
+        P = pnext;
+    }
+}
+
+// Outputs, one workgroup per tile, from the exact tile prefix pre[t] (any row alignment).
 template <bool VEC4, bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock)
 tile_out_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                 int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm, const float* __restrict__ Xs,
                 const float* __restrict__ l1, const uint64_t* __restrict__ pre) {
-    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image, then output image
-    __shared__ double s_wave[kQBlock / kWave];
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image, scratch, then output image
     __shared__ float s_tab[kTab];
+    __shared__ ScanLds sl;
     const int tid = threadIdx.x;
     const int32_t tile = blockIdx.x;
     const int64_t vec = blockIdx.y;
@@ -977,16 +1346,19 @@ tile_out_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __
     const int64_t t0 = (int64_t)tile * kQTile;
     const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
     const DivPlan dp = div_plan(L);
+    const double P = __longlong_as_double((long long)pre[vec * tiles + tile]);
+    const Binade B = binade_of(P);
     TileState st;
     TileVals tv;
     if (len == kQTile)
-        tile_pass1<true>(s_x, tv, s_wave, tid, len, dp, fm, st);
+        tile_pass1<true, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
     else
-        tile_pass1<false>(s_x, tv, s_wave, tid, len, dp, fm, st);
-    const double P = __longlong_as_double((long long)pre[vec * tiles + tile]);
+        tile_pass1<false, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
+    double pnext;
+    const double base = resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);   // barrier-terminated if it used s_x
     uint32_t cw[4];
     float kmax = 0.0f;
-    tile_pass2<WQ, WC>(s_x, tv, s_tab, tid, P, L, fm, Xs[vec], st, cw, kmax);   // s_x free after pass 1
+    tile_pass2<WQ, WC>(s_x, tv, s_tab, tid, base, L, fm, Xs[vec], cw, kmax);   // each thread rewrites its own row
     if (WC) {
         store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
         publish_kmax(kmax, L, overflow, vec, tid);
@@ -1211,7 +1583,7 @@ int hip_check(hipError_t e, const char* what) {
 }
 
 struct WsLayout {
-    size_t agg_off, incl_off, part_off, l1_off, total;
+    size_t agg_off, incl_off, map1_off, part_off, l1_off, total;
     int32_t tiles;
 };
 
@@ -1222,7 +1594,8 @@ WsLayout layout(int64_t n, int64_t d, const L1Plan& plan) {
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
     w.agg_off = kCtrlBytes;
     w.incl_off = up(w.agg_off + (size_t)n * tiles * sizeof(uint64_t));
-    w.part_off = up(w.incl_off + (size_t)n * tiles * sizeof(uint64_t));
+    w.map1_off = up(w.incl_off + (size_t)n * tiles * sizeof(uint64_t));
+    w.part_off = up(w.map1_off + (size_t)n * tiles * sizeof(uint64_t));
     w.l1_off = up(w.part_off + (size_t)n * plan.total_groups * 32 * sizeof(float));
     w.total = up(w.l1_off + (size_t)n * sizeof(float));
     return w;
@@ -1256,31 +1629,6 @@ int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, flo
 int launch_l1(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* part, float* l1_out,
               hipStream_t st) {
     return launch_cascade<AbsOp>(x, n, d, plan, part, l1_out, nullptr, 0.f, st);
-}
-
-// Persistent grid for K2: (resident workgroups per CU) x CUs, from the occupancy API
-// (correctness never depends on it: tiles are ticketed).
-int persistent_grid(bool vec4, int* out) {
-    int dev = 0;
-    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
-    if (rc) return rc;
-    static thread_local int cache_dev = -1, cache_v[2] = {0, 0};
-    if (cache_dev != dev) {
-        int cus = 0;
-        rc = hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
-        if (rc) return rc;
-        for (int v = 0; v < 2; ++v) {
-            int per = 0;
-            rc = hip_check(v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, quantize_lookback_kernel<true, true, false, true>, kQBlock, 0)
-                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, quantize_lookback_kernel<false, true, false, true>, kQBlock, 0),
-                           "occupancy");
-            if (rc) return rc;
-            cache_v[v] = std::max(1, per) * std::max(1, cus);
-        }
-        cache_dev = dev;
-    }
-    *out = cache_v[vec4 ? 1 : 0];
-    return UQ_OK;
 }
 
 // Resident stream-kernel workgroups on this device: 4 per CU (launch bounds).
@@ -1585,53 +1933,77 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
 #undef UQ_STREAM
         return hip_check(hipGetLastError(), "quantize_stream_kernel launch");
     }
-    if (n > 1 && n <= 65535 && n * (int64_t)w.tiles >= kPhasedMinTiles && n * (int64_t)w.tiles < ((int64_t)1 << 32)) {
-        // several clients, enough tiles to fill the GPU: the three-phase form (no waits)
-        uint64_t* agg = (uint64_t*)(wsb + w.agg_off);
-        uint64_t* pre = (uint64_t*)(wsb + w.incl_off);
-        if (vec4 && d <= ((int64_t)1 << 29)) {
+    // Small batches: approximate sums -> approximate prefixes -> exact maps -> exact fold
+    // -> outputs (see "small-batch forms").  Clients go in chunks of at most kMaxGridY.
+    for (int64_t j0 = 0; j0 < n; j0 += kMaxGridY) {
+        const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
+        const float* xj = x + j0 * d;
+        float* outj = out ? out + j0 * d : nullptr;
+        int8_t* codesj = codes ? codes + j0 * d : nullptr;
+        int32_t* ovj = codes ? overflow + j0 : nullptr;
+        const float* Xj = X + j0;
+        const float* l1j = l1use + j0;
+        uint64_t* agg = (uint64_t*)(wsb + w.agg_off) + j0 * w.tiles;
+        uint64_t* pre = (uint64_t*)(wsb + w.incl_off) + j0 * w.tiles;
+        uint64_t* map1 = (uint64_t*)(wsb + w.map1_off) + j0 * w.tiles;
+        const int64_t total_tiles = nj * (int64_t)w.tiles;
+        const bool seg = vec4 && d <= ((int64_t)1 << 29) && total_tiles >= kSegMinTiles;
+        const dim3 tgrid((unsigned)w.tiles, (unsigned)nj);
+        int32_t R = 1, nseg = 1;
+        if (seg) {
             // segmented stream: runs of R tiles per workgroup, ~4 resident workgroups per CU
             int slots = 0;
             rc = stream_slots(&slots);
             if (rc) return rc;
-            const int64_t total_tiles = n * (int64_t)w.tiles;
-            const int32_t R = (int32_t)std::max<int64_t>(1, (total_tiles + slots - 1) / slots);
-            const int32_t nseg = (w.tiles + R - 1) / R;
-            const dim3 sgrid((unsigned)(n * nseg));
-            hipLaunchKernelGGL(agg_stream_kernel, sgrid, dim3(kQBlock), 0, st, x, d, w.tiles, fm, l1use, R, nseg, agg);
-            rc = hip_check(hipGetLastError(), "agg_stream_kernel launch");
+            R = (int32_t)std::max<int64_t>(1, (total_tiles + slots - 1) / slots);
+            nseg = (w.tiles + R - 1) / R;
+            hipLaunchKernelGGL(agg_stream_kernel, dim3((unsigned)(nj * nseg)), dim3(kQBlock), 0, st, xj, d, w.tiles, fm,
+                               l1j, R, nseg, agg);
+        } else if (vec4) {
+            hipLaunchKernelGGL(tile_agg_kernel<true>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg);
+        } else {
+            hipLaunchKernelGGL(tile_agg_kernel<false>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg);
+        }
+        rc = hip_check(hipGetLastError(), "tile sums launch");
+        if (rc) return rc;
+        hipLaunchKernelGGL(tile_prefix_kernel, dim3((unsigned)((nj + 255) / 256)), dim3(256), 0, st, agg, pre, nj,
+                           w.tiles);
+        rc = hip_check(hipGetLastError(), "tile_prefix_kernel launch");
+        if (rc) return rc;
+        if (vec4) {
+            hipLaunchKernelGGL(tile_map_kernel<true>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, pre, agg, map1);
+            rc = hip_check(hipGetLastError(), "tile_map_kernel launch");
             if (rc) return rc;
-            hipLaunchKernelGGL(tile_prefix_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, agg, pre, n,
-                               w.tiles);
-            rc = hip_check(hipGetLastError(), "tile_prefix_kernel launch");
+            hipLaunchKernelGGL(exact_fold_kernel<true>, dim3((unsigned)nj), dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j,
+                               agg, map1, pre);
+        } else {
+            hipLaunchKernelGGL(tile_map_kernel<false>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, pre, agg, map1);
+            rc = hip_check(hipGetLastError(), "tile_map_kernel launch");
             if (rc) return rc;
+            hipLaunchKernelGGL(exact_fold_kernel<false>, dim3((unsigned)nj), dim3(kQBlock), 0, st, xj, d, w.tiles, fm,
+                               l1j, agg, map1, pre);
+        }
+        rc = hip_check(hipGetLastError(), "exact_fold_kernel launch");
+        if (rc) return rc;
+        if (seg) {
 #define UQ_SEG(Q, C, CV)                                                                                    \
     case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
-        hipLaunchKernelGGL((quantize_stream_kernel<Q, C, CV>), sgrid, dim3(kQBlock), 0, st, x, out, codes, overflow, \
-                           d, w.tiles, fm, X, l1use, R, nseg, pre);                                         \
+        hipLaunchKernelGGL((quantize_stream_kernel<Q, C, CV>), dim3((unsigned)(nj * nseg)), dim3(kQBlock), 0, st, xj, \
+                           outj, codesj, ovj, d, w.tiles, fm, Xj, l1j, R, nseg, pre);                      \
         break;
             switch (sel & 7) {
                 UQ_SEG(1, 0, 1) UQ_SEG(1, 1, 1) UQ_SEG(1, 1, 0) UQ_SEG(0, 1, 1) UQ_SEG(0, 1, 0)
                 default: return fail(UQ_E_INVALID, "internal: bad kernel selector");
             }
 #undef UQ_SEG
-            return hip_check(hipGetLastError(), "quantize_stream_kernel (segments) launch");
+            rc = hip_check(hipGetLastError(), "quantize_stream_kernel (segments) launch");
+            if (rc) return rc;
+            continue;
         }
-        const dim3 grid((unsigned)w.tiles, (unsigned)n);
-        if (vec4)
-            hipLaunchKernelGGL(tile_agg_kernel<true>, grid, dim3(kQBlock), 0, st, x, d, w.tiles, fm, l1use, agg);
-        else
-            hipLaunchKernelGGL(tile_agg_kernel<false>, grid, dim3(kQBlock), 0, st, x, d, w.tiles, fm, l1use, agg);
-        rc = hip_check(hipGetLastError(), "tile_agg_kernel launch");
-        if (rc) return rc;
-        hipLaunchKernelGGL(tile_prefix_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, agg, pre, n,
-                           w.tiles);
-        rc = hip_check(hipGetLastError(), "tile_prefix_kernel launch");
-        if (rc) return rc;
 #define UQ_PHASED(V, Q, C, CV)                                                                                \
     case ((V) * 8 + (Q) * 4 + (C) * 2 + (CV)):                                                              \
-        hipLaunchKernelGGL((tile_out_kernel<V, Q, C, CV>), grid, dim3(kQBlock), 0, st, x, out, codes, overflow, d, \
-                           w.tiles, fm, X, l1use, pre);                                                       \
+        hipLaunchKernelGGL((tile_out_kernel<V, Q, C, CV>), tgrid, dim3(kQBlock), 0, st, xj, outj, codesj, ovj, d, \
+                           w.tiles, fm, Xj, l1j, pre);                                                        \
         break;
         switch (sel) {
             UQ_PHASED(1, 1, 0, 1) UQ_PHASED(1, 1, 1, 1) UQ_PHASED(1, 1, 1, 0) UQ_PHASED(1, 0, 1, 1)
@@ -1640,33 +2012,10 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
             default: return fail(UQ_E_INVALID, "internal: bad kernel selector");
         }
 #undef UQ_PHASED
-        return hip_check(hipGetLastError(), "tile_out_kernel launch");
+        rc = hip_check(hipGetLastError(), "tile_out_kernel launch");
+        if (rc) return rc;
     }
-    rc = hip_check(hipMemsetAsync(wsb, 0, 2 * sizeof(uint32_t), st), "memset ticket/abort");
-    if (rc) return rc;
-    // agg and incl are contiguous: one fill of both look-back arrays
-    rc = hip_check(hipMemsetAsync(wsb + w.agg_off, 0xFF, w.part_off - w.agg_off, st), "memset look-back");
-    if (rc) return rc;
-    const uint32_t total = (uint32_t)(w.tiles * n);
-    int grid_cap = 0;
-    rc = persistent_grid(vec4, &grid_cap);
-    if (rc) return rc;
-    dim3 grid((unsigned)std::min<int64_t>(total, grid_cap));
-    uint64_t* agg = (uint64_t*)(wsb + w.agg_off);
-    uint64_t* incl = (uint64_t*)(wsb + w.incl_off);
-#define UQ_LOOK(V, Q, C, CV)                                                                                  \
-    case ((V) * 8 + (Q) * 4 + (C) * 2 + (CV)):                                                              \
-        hipLaunchKernelGGL((quantize_lookback_kernel<V, Q, C, CV>), grid, dim3(kQBlock), 0, st, x, out, codes,  \
-                           overflow, d, w.tiles, total, fm, X, l1use, agg, incl, (uint32_t*)wsb);             \
-        break;
-    switch (sel) {
-        UQ_LOOK(1, 1, 0, 1) UQ_LOOK(1, 1, 1, 1) UQ_LOOK(1, 1, 1, 0) UQ_LOOK(1, 0, 1, 1)
-        UQ_LOOK(1, 0, 1, 0) UQ_LOOK(0, 1, 0, 1) UQ_LOOK(0, 1, 1, 1) UQ_LOOK(0, 1, 1, 0)
-        UQ_LOOK(0, 0, 1, 1) UQ_LOOK(0, 0, 1, 0)
-        default: return fail(UQ_E_INVALID, "internal: bad kernel selector");
-    }
-#undef UQ_LOOK
-    return hip_check(hipGetLastError(), "quantize_lookback_kernel launch");
+    return UQ_OK;
 }
 
 int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m, const float* X,
