@@ -108,16 +108,6 @@ bool make_plan(int64_t d, int32_t T, L1Plan* p) {
     return true;
 }
 
-__device__ __forceinline__ uint64_t ld_relaxed_agent(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_relaxed_agent(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_relaxed_agent32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Element transforms summed by the K1 cascade.  The cascade itself (order of f32 adds)
 // is the torch CPU `sum` order whatever is summed.
 struct AbsOp {            // AS:624  input_vector.abs().sum()
@@ -128,7 +118,6 @@ struct AbsOp {            // AS:624  input_vector.abs().sum()
     __device__ float operator()(float v) const { return fabsf(v); }
 };
 struct RezKOp {           // AS:648-649  k' = floor(m * p + 0.5), p = |x| / (L1 + 1e-12)
-    static constexpr bool kHist = false;
     float den, fm;
     uint32_t *h, *zn;
     __device__ static RezKOp make(const float* l1, float fm, int64_t vec) {
@@ -736,6 +725,84 @@ __device__ __forceinline__ void tie_sums(const ScanLds& sl, const ParityCtx& c, 
     }
 }
 
+// Irregular tile, up to the walk: each thread takes the binade of its approximate start
+// Ps + texcl (Ps: the exact start, or P' when a map kernel records the tile), writes its
+// scratch slot (t0, t1 of a clean thread, else its 16 fractions), the event / clean masks
+// (tmask / cmask) and its inclusive run sum (aux).
+// Events: threads whose increment is not a fixed multiple of their run's G -- not clean
+// (added one by one from their exact start) or a clean tie (t0 != t1).  Between events,
+// clean threads form runs inside one binade (consecutive clean threads cannot straddle an
+// edge: each ends 1 below it); their t0 are multiples of that G and a run sums to less than
+// 2^E, so a SEGMENTED scan of t0 (a run starts after each event) is exact in any order.
+struct IrrThread {
+    bool event;
+    double v, x;         // own run value (0 for an event), inclusive run sum
+};
+__device__ void irregular_prep(double Ps, const TileState& st, const TileVals& tv, float* s_scr, ScanLds& sl, int tid,
+                               IrrThread& it) {
+    double* slot = slot_of(s_scr, tid);
+    const int wid = tid / kWave;
+    const int lane = tid & (kWave - 1);
+    const double sa = Ps + st.texcl;
+    const Binade bt = binade_of(sa);
+    const bool clean = sa >= 32.0 && sa >= bt.b0 * (1.0 + kEdge) && (sa + st.t0) + 1.0 < bt.top;
+    double t0c = 0.0, t1c = 0.0;
+    if (clean) {
+        double c0 = bt.b0, c1 = bt.b1;
+#pragma unroll
+        for (int k = 0; k < kQItems; ++k) {
+            const double f = (double)fr_of(tv.mps[k]);
+            c0 += f;
+            c1 += f;
+        }
+        t0c = c0 - bt.b0;
+        t1c = c1 - bt.b1;
+        slot[0] = t0c;
+        slot[1] = t1c;
+    } else {
+#pragma unroll
+        for (int k4 = 0; k4 < kQItems / 4; ++k4)
+            reinterpret_cast<float4*>(slot)[k4] = make_float4(fr_of(tv.mps[4 * k4]), fr_of(tv.mps[4 * k4 + 1]),
+                                                              fr_of(tv.mps[4 * k4 + 2]), fr_of(tv.mps[4 * k4 + 3]));
+    }
+    const bool event = !clean || t0c != t1c;
+    const double v = event ? 0.0 : t0c;
+    it.event = event;
+    it.v = v;
+    const uint64_t em = __ballot(event);
+    const uint64_t cm = __ballot(clean);
+    bool f = tid == 0 || (lane > 0 && ((em >> (lane - 1)) & 1ull) != 0ull);   // run head, in-wave view
+    double x = v;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {                       // segmented inclusive scan, wave level
+        const double xu = __shfl_up(x, o, kWave);
+        const int fu = __shfl_up((int)f, o, kWave);
+        if (lane >= o) {
+            if (!f) x = xu + x;
+            f = f || fu != 0;
+        }
+    }
+    if (lane == kWave - 1) {
+        sl.rsum[wid] = x;                                      // sum of the run that ends the wave
+        sl.rhead[wid] = f ? 1u : 0u;                           // that run starts inside the wave
+    }
+    if (lane == 0) {
+        sl.tmask[wid] = em;
+        sl.cmask[wid] = cm;
+    }
+    __syncthreads();
+    if (!f) {                                                  // the run comes from earlier waves
+        for (int w = wid - 1; w >= 0; --w) {
+            if ((sl.tmask[w] >> (kWave - 1)) & 1ull) break;    // wave w ends with an event
+            x = sl.rsum[w] + x;
+            if (sl.rhead[w]) break;
+        }
+    }
+    sl.aux[tid] = x;                                           // inclusive run sum
+    it.x = x;
+    __syncthreads();
+}
+
 // Exact thread base (prefix before this thread's first element) and exact P_{t+1}, from
 // the exact tile start P.  s_scr: the tile's LDS image after pass 1 (thread t's row =
 // floats [16t, 16t+16) is its scratch slot).  Ends with a barrier whenever it used the
@@ -798,70 +865,11 @@ __device__ double resolve_exact(double P, const Binade& B, const TileState& st, 
 #ifdef UQ_EXP_NOIRR
     pnext = P + st.total; return P + st.texcl;
 #endif
-    // irregular tile: each thread in the binade of its approximate start
+    // irregular tile: the events walked by one lane from the exact start
+    IrrThread it;
+    irregular_prep(P, st, tv, s_scr, sl, tid, it);
     const int lane = tid & (kWave - 1);
-    const double sa = P + st.texcl;
-    const Binade bt = binade_of(sa);
-    const bool clean = sa >= 32.0 && sa >= bt.b0 * (1.0 + kEdge) && (sa + st.t0) + 1.0 < bt.top;
-    double t0c = 0.0, t1c = 0.0;
-    if (clean) {
-        double c0 = bt.b0, c1 = bt.b1;
-#pragma unroll
-        for (int k = 0; k < kQItems; ++k) {
-            const double f = (double)fr_of(tv.mps[k]);
-            c0 += f;
-            c1 += f;
-        }
-        t0c = c0 - bt.b0;
-        t1c = c1 - bt.b1;
-        slot[0] = t0c;
-        slot[1] = t1c;
-    } else {
-#pragma unroll
-        for (int k4 = 0; k4 < kQItems / 4; ++k4)
-            reinterpret_cast<float4*>(slot)[k4] = make_float4(fr_of(tv.mps[4 * k4]), fr_of(tv.mps[4 * k4 + 1]),
-                                                              fr_of(tv.mps[4 * k4 + 2]), fr_of(tv.mps[4 * k4 + 3]));
-    }
-    // Events: threads whose increment is not a fixed multiple of their run's G -- not clean
-    // (added one by one from their exact start) or a clean tie (t0 != t1).  Between events,
-    // clean threads form runs inside one binade (consecutive clean threads cannot straddle
-    // an edge: each ends 1 below it); their t0 are multiples of that G and a run sums to
-    // less than 2^E, so a SEGMENTED scan of t0 (a run starts after each event) is exact in
-    // any order.  One lane then walks the events only.
     const int wid = tid / kWave;
-    const bool event = !clean || t0c != t1c;
-    const double v = event ? 0.0 : t0c;
-    const uint64_t em = __ballot(event);
-    const uint64_t cm = __ballot(clean);
-    bool f = tid == 0 || (lane > 0 && ((em >> (lane - 1)) & 1ull) != 0ull);   // run head, in-wave view
-    double x = v;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {                       // segmented inclusive scan, wave level
-        const double xu = __shfl_up(x, o, kWave);
-        const int fu = __shfl_up((int)f, o, kWave);
-        if (lane >= o) {
-            if (!f) x = xu + x;
-            f = f || fu != 0;
-        }
-    }
-    if (lane == kWave - 1) {
-        sl.rsum[wid] = x;                                      // sum of the run that ends the wave
-        sl.rhead[wid] = f ? 1u : 0u;                           // that run starts inside the wave
-    }
-    if (lane == 0) {
-        sl.tmask[wid] = em;
-        sl.cmask[wid] = cm;
-    }
-    __syncthreads();
-    if (!f) {                                                  // the run comes from earlier waves
-        for (int w = wid - 1; w >= 0; --w) {
-            if ((sl.tmask[w] >> (kWave - 1)) & 1ull) break;    // wave w ends with an event
-            x = sl.rsum[w] + x;
-            if (sl.rhead[w]) break;
-        }
-    }
-    sl.aux[tid] = x;                                           // inclusive run sum
-    __syncthreads();
     if (tid == 0) {
         double S = P;                                          // exact value at the current run head
         for (int w = 0; w < kQBlock / kWave; ++w) {
@@ -890,14 +898,14 @@ __device__ double resolve_exact(double P, const Binade& B, const TileState& st, 
     }
     __syncthreads();
     double base;
-    if (event) {
+    if (it.event) {
         base = sl.aux[tid];
     } else {
         int w = wid;                                           // the last event before this thread
         uint64_t mk = sl.tmask[w] & ((1ull << lane) - 1ull);
         while (mk == 0ull && w > 0) mk = sl.tmask[--w];
         const double start = mk ? slot_of(s_scr, w * kWave + 63 - __builtin_clzll(mk))[6] : P;
-        base = start + (x - v);                                // + exclusive run sum (exact)
+        base = start + (it.x - it.v);                                // + exclusive run sum (exact)
     }
     pnext = sl.misc[0];
     __syncthreads();
@@ -1153,8 +1161,9 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
 
 // ---- small-batch forms (fewer clients than fill the GPU one workgroup per client) ----
 //   approximate tile sums A_t (agg_stream_kernel over segments, or tile_agg_kernel)
-//   tile_prefix_kernel   per client P'_t = sum of A_j, j < t (approximate prefixes)
-//   tile_map_kernel      per tile, in the binade of P'_t: exact map (m0, m1), or NaN
+//   tile_map_kernel      per tile: P'_t = the sums before it (approximate prefix), then in
+//                        the binade of P'_t the exact map (m0, m1), or an irregular tile's
+//                        event record
 //   exact_fold_kernel    per client, serial: P_0 = 0, P_{t+1} = P_t + m[parity(P_t)];
 //                        irregular tiles recomputed from their exact P_t
 //   outputs              quantize_stream_kernel over segments / tile_out_kernel from P_t
@@ -1218,42 +1227,53 @@ tile_agg_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
     if (tid == 0) agg[vec * tiles + tile] = (uint64_t)__double_as_longlong(st.total);
 }
 
-// One thread per client: approximate prefixes P'_t (they only choose each tile's binade).
-__global__ void __launch_bounds__(256)
-tile_prefix_kernel(const uint64_t* __restrict__ agg, uint64_t* __restrict__ pre, int64_t n, int32_t tiles) {
-    const int64_t vec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (vec >= n) return;
-    const uint64_t* a = agg + vec * tiles;
-    uint64_t* p = pre + vec * tiles;
-    double P = 0.0;
-    for (int32_t t = 0; t < tiles; ++t) {
-        p[t] = (uint64_t)__double_as_longlong(P);
-        P = P + __longlong_as_double((long long)a[t]);
-    }
-}
+// Irregular tiles of the small-batch forms are recorded by the map kernel as their event
+// list (classified from P', valid for the exact start by the kEdge margin): per event the
+// run sum before it, then a clean tie's (t0, t1) or an edge thread's 16 fractions, and the
+// run sum after the last event.  The fold walks a record in LDS instead of loading and
+// resolving the tile.  Tiles with more events, or beyond a client's record budget, or of
+// clients past kRecClients, are resolved from the data as before.
+constexpr int kRecEvents = 48;          // events per record
+constexpr int kRecPerClient = 32;       // records per client
+constexpr int kRecClients = 256;        // clients per launch chunk with records
+struct EvEntry {
+    double run;                         // run sum between the previous event and this one
+    double t0, t1;                      // clean tie
+    uint32_t tie;                       // 1: clean tie, 0: edge thread (fr)
+    uint32_t pad;
+    float fr[kQItems];
+};
+struct TileRec {
+    uint32_t count;
+    uint32_t pad;
+    double last_run;                    // run sum after the last event
+    EvEntry ev[kRecEvents];
+};
 
-// Exact tile maps in the binade of P'_t: map0[t] = m0 (NaN: irregular), map1[t] = m1.
+// Exact tile maps in the binade of P'_t: map0[t] = m0 (NaN: irregular), map1[t] = m1, or for
+// an irregular tile its record number + 1 (0: no record).
 template <bool VEC4>
 __global__ void __launch_bounds__(kQBlock)
 tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
-                const uint64_t* __restrict__ pre_approx, uint64_t* __restrict__ map0, uint64_t* __restrict__ map1) {
+                const uint64_t* __restrict__ agg, uint64_t* __restrict__ map0, uint64_t* __restrict__ map1,
+                TileRec* __restrict__ recs, uint32_t* __restrict__ reccnt) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
     __shared__ ScanLds sl;
     const int tid = threadIdx.x;
     const int32_t tile = blockIdx.x;
     const int64_t vec = blockIdx.y;
     const int64_t idx = vec * tiles + tile;
-    const double Pg = __longlong_as_double((long long)pre_approx[idx]);
-    const Binade B = binade_of(Pg);
-    if (!(Pg >= 32.0 && Pg >= B.b0 * (1.0 + kEdge))) {          // certainly irregular: skip the work
-        if (tid == 0) {
-            map0[idx] = (uint64_t)__double_as_longlong(__builtin_nan(""));
-            map1[idx] = 0ull;
-        }
-        return;
-    }
     TileRegs r;
     load_tile<VEC4>(r, x, d, tiles, (uint32_t)idx, tid);
+    // P'_t = the approximate tile sums before t, in any order (it only picks the binade)
+    double acc = 0.0;
+    for (int32_t j = tid; j < tile; j += kQBlock) acc += __longlong_as_double((long long)agg[vec * tiles + j]);
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
+    if ((tid & (kWave - 1)) == 0) sl.wave[tid / kWave] = acc;
+    __syncthreads();
+    const double Pg = uniform_d(((sl.wave[0] + sl.wave[1]) + sl.wave[2]) + sl.wave[3]);
+    const Binade B = binade_of(Pg);
     stage_tile<VEC4>(r, s_x, tid);
     __syncthreads();
     const int64_t t0 = (int64_t)tile * kQTile;
@@ -1266,45 +1286,243 @@ tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
     else
         tile_pass1<false, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
     double m0 = 0.0, m1 = 0.0;
-    const bool ok = resolve_map(Pg, B, st, s_x, sl, tid, m0, m1);
+    if (resolve_map(Pg, B, st, s_x, sl, tid, m0, m1)) {
+        if (tid == 0) {
+            map0[idx] = (uint64_t)__double_as_longlong(m0);
+            map1[idx] = (uint64_t)__double_as_longlong(m1);
+        }
+        return;
+    }
+    // irregular: record the events (classified from P')
+    IrrThread it;
+    irregular_prep(Pg, st, tv, s_x, sl, tid, it);
+    int ne = 0;
+#pragma unroll
+    for (int w = 0; w < kQBlock / kWave; ++w) ne += __builtin_popcountll(uniform_u64(sl.tmask[w]));
     if (tid == 0) {
-        map0[idx] = (uint64_t)__double_as_longlong(ok ? m0 : __builtin_nan(""));
-        map1[idx] = (uint64_t)__double_as_longlong(m1);
+        uint32_t rn = 0;
+        if (ne <= kRecEvents && vec < kRecClients) {
+            const uint32_t slotno = atomicAdd(&reccnt[vec], 1u);
+            rn = slotno < (uint32_t)kRecPerClient ? slotno + 1u : 0u;
+        }
+        sl.misc[0] = (double)rn;
+    }
+    __syncthreads();
+    const uint32_t rno = (uint32_t)sl.misc[0];
+    if (tid == 0) {
+        map0[idx] = (uint64_t)__double_as_longlong(__builtin_nan(""));
+        map1[idx] = rno;
+    }
+    if (rno == 0u) return;
+    TileRec* rec = recs + (vec * kRecPerClient + (rno - 1u));
+    if (it.event) {
+        const int lane = tid & (kWave - 1), wid = tid / kWave;
+        int e = __builtin_popcountll(sl.tmask[wid] & ((1ull << lane) - 1ull));
+        for (int w = 0; w < wid; ++w) e += __builtin_popcountll(sl.tmask[w]);
+        EvEntry& ev = rec->ev[e];
+        const double* q = slot_of(s_x, tid);
+        ev.run = it.x;                                         // inclusive run sum; own v is 0
+        const bool tie = (sl.cmask[wid] >> lane) & 1ull;
+        ev.tie = tie ? 1u : 0u;
+        if (tie) {
+            ev.t0 = q[0];
+            ev.t1 = q[1];
+        } else {
+#pragma unroll
+            for (int k = 0; k < kQItems; ++k) ev.fr[k] = reinterpret_cast<const float*>(q)[k];
+        }
+    }
+    if (tid == kQBlock - 1) {
+        rec->count = (uint32_t)ne;
+        rec->last_run = it.event ? 0.0 : it.x;
     }
 }
 
 constexpr int kFoldChunk = 1024;   // tile maps staged in LDS at a time
+constexpr int kFoldEvents = 256;   // record events prefetched into LDS (24 KB)
 
 // One workgroup per client: the exact serial fold over its tile maps; irregular tiles are
 // loaded and resolved from their exact start.  pre[t] = exact P_t.
 template <bool VEC4>
 __global__ void __launch_bounds__(kQBlock)
 exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
-                  const uint64_t* __restrict__ map0, const uint64_t* __restrict__ map1, uint64_t* __restrict__ pre) {
+                  const uint64_t* map0, const uint64_t* __restrict__ map1, uint64_t* pre,
+                  const TileRec* __restrict__ recs, const uint32_t* __restrict__ reccnt) {
+    // (map0 and pre may alias: pre overwrites maps already staged in LDS)
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
     __shared__ ScanLds sl;
+    __shared__ double s_m0[kFoldChunk], s_m1[kFoldChunk], s_pre[kFoldChunk];
+    __shared__ EvEntry s_ev[kFoldEvents];                  // the client's records, prefetched
+    __shared__ uint32_t s_roff[kRecPerClient], s_rcnt[kRecPerClient];
+    __shared__ double s_rlast[kRecPerClient];
     const int tid = threadIdx.x;
     const int64_t vec = blockIdx.x;
     const DivPlan dp = div_plan(l1[vec]);
-    __shared__ double s_m0[kFoldChunk], s_m1[kFoldChunk];
+#ifdef UQ_FOLD_PROF
+    uint64_t pt0 = wall_clock64(), pmap = 0, prec = 0, pfb = 0;
+    int nfb = 0, nrw = 0;
+#endif
+    // prefetch every record of this client that fits (two dependent round trips in all)
+    const int nrec = vec < kRecClients ? (int)min(reccnt[vec], (uint32_t)kRecPerClient) : 0;
+    if (tid < nrec) {
+        s_rcnt[tid] = recs[vec * kRecPerClient + tid].count;
+        s_rlast[tid] = recs[vec * kRecPerClient + tid].last_run;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t off = 0;
+        for (int r = 0; r < nrec; ++r) {
+            const bool fits = off + s_rcnt[r] <= (uint32_t)kFoldEvents;
+            s_roff[r] = fits ? off : ~0u;
+            if (fits) off += s_rcnt[r];
+        }
+    }
+    __syncthreads();
+    for (int r = 0; r < nrec; ++r) {
+        if (s_roff[r] == ~0u) continue;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(recs[vec * kRecPerClient + r].ev);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(s_ev + s_roff[r]);
+        const int nw = (int)(s_rcnt[r] * (sizeof(EvEntry) / 4));
+        for (int i = tid; i < nw; i += kQBlock) dst[i] = src[i];
+    }
+    __syncthreads();
+#ifdef UQ_FOLD_PROF
+    const uint64_t pt1 = wall_clock64();
+#endif
     double P = 0.0;
     for (int32_t tile = 0; tile < tiles; ++tile) {
-        const int64_t idx = vec * tiles + tile;
-        const int ci = tile % kFoldChunk;
+        int ci = tile % kFoldChunk;
         if (ci == 0) {                                         // stage the next chunk of maps
             __syncthreads();
+            const int64_t b = vec * tiles + tile;
             for (int i = tid; i < kFoldChunk && tile + i < tiles; i += kQBlock) {
-                s_m0[i] = __longlong_as_double((long long)map0[idx + i]);
-                s_m1[i] = __longlong_as_double((long long)map1[idx + i]);
+                s_m0[i] = __longlong_as_double((long long)map0[b + i]);
+                s_m1[i] = __longlong_as_double((long long)map1[b + i]);
             }
             __syncthreads();
         }
+        {   // a run of regular maps (P stays in their binade): one lane, maps read one ahead
+#ifdef UQ_FOLD_PROF
+            const uint64_t q0 = wall_clock64();
+#endif
+            const int cend = min(kFoldChunk, tiles - (tile - ci));
+            if (tid == 0) {
+                double Pl = P;
+                int c = ci;
+                // maps read a group of 4 ahead; both candidate sums formed before the parity
+                // select, so the dependent chain per tile is one add and one select
+                double a0[4], a1[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int cn = min(c + u, cend - 1);
+                    a0[u] = s_m0[cn];
+                    a1[u] = s_m1[cn];
+                }
+                bool more = true;
+                while (more) {
+                    double b0[4], b1[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int cn = min(c + 4 + u, cend - 1);
+                        b0[u] = s_m0[cn];
+                        b1[u] = s_m1[cn];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (more && !(a0[u] == a0[u])) more = false;      // irregular tile: stop
+                        if (more) {
+                            s_pre[c] = Pl;                             // copied to pre[] below
+                            const double q0 = Pl + a0[u], q1 = Pl + a1[u];
+                            Pl = lowbit(Pl) ? q1 : q0;
+                            if (++c == cend) more = false;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        a0[u] = b0[u];
+                        a1[u] = b1[u];
+                    }
+                }
+                sl.misc[0] = Pl;
+                sl.misc[1] = (double)c;
+            }
+            __syncthreads();
+            P = sl.misc[0];
+            const int c = (int)sl.misc[1];
+            {
+                const int64_t base = vec * tiles + (tile - ci);
+                for (int i = ci + tid; i < c; i += kQBlock) pre[base + i] = (uint64_t)__double_as_longlong(s_pre[i]);
+            }
+            __syncthreads();
+            tile += c - ci;
+            ci = c;
+#ifdef UQ_FOLD_PROF
+            pmap += wall_clock64() - q0;
+#endif
+            if (ci == cend) {                                  // chunk folded: stage the next one
+                --tile;
+                continue;
+            }
+        }
+        const int64_t idx = vec * tiles + tile;                // an irregular tile
         if (tid == 0) pre[idx] = (uint64_t)__double_as_longlong(P);
-        const double m0 = s_m0[ci];
-        if (m0 == m0) {                                        // regular: P stays in the map's binade
-            P = P + (lowbit(P) ? s_m1[ci] : m0);
+        const uint32_t rid = (uint32_t)__double_as_longlong(s_m1[ci]);
+        if (rid != 0u && s_roff[rid - 1u] != ~0u) {            // recorded and prefetched: walk it
+#ifdef UQ_FOLD_PROF
+            const uint64_t q0 = wall_clock64();
+            ++nrw;
+#endif
+            if (tid == 0) {
+                const EvEntry* ev0 = s_ev + s_roff[rid - 1u];
+                double S = P;
+                for (uint32_t e = 0; e < s_rcnt[rid - 1u]; ++e) {
+                    const EvEntry& ev = ev0[e];
+                    S = S + ev.run;                            // exact start of the event
+                    if (ev.tie) {
+                        S = S + (lowbit(S) ? ev.t1 : ev.t0);
+                    } else {
+                        for (int k = 0; k < kQItems; ++k) S = S + (double)ev.fr[k];
+                    }
+                }
+                sl.misc[0] = S + s_rlast[rid - 1u];
+            }
+            __syncthreads();
+            P = sl.misc[0];
+            __syncthreads();
+#ifdef UQ_FOLD_PROF
+            prec += wall_clock64() - q0;
+#endif
             continue;
         }
+        if (rid != 0u) {                                       // recorded: walk its events from LDS
+            const TileRec* rec = recs + (vec * kRecPerClient + (rid - 1u));
+            uint32_t* dst = reinterpret_cast<uint32_t*>(s_x);
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(rec);
+            for (int i = tid; i < (int)(sizeof(TileRec) / 4); i += kQBlock) dst[i] = src[i];
+            __syncthreads();
+            if (tid == 0) {
+                const TileRec* lr = reinterpret_cast<const TileRec*>(s_x);
+                double S = P;
+                for (uint32_t e = 0; e < lr->count; ++e) {
+                    const EvEntry& ev = lr->ev[e];
+                    S = S + ev.run;                            // exact start of the event
+                    if (ev.tie) {
+                        S = S + (lowbit(S) ? ev.t1 : ev.t0);
+                    } else {
+                        for (int k = 0; k < kQItems; ++k) S = S + (double)ev.fr[k];
+                    }
+                }
+                sl.misc[0] = S + lr->last_run;
+            }
+            __syncthreads();
+            P = sl.misc[0];
+            __syncthreads();
+            continue;
+        }
+#ifdef UQ_FOLD_PROF
+        const uint64_t qf = wall_clock64();
+        ++nfb;
+#endif
         TileRegs r;
         load_tile<VEC4>(r, x, d, tiles, (uint32_t)idx, tid);
         stage_tile<VEC4>(r, s_x, tid);
@@ -1322,7 +1540,16 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
         (void)resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);
         __syncthreads();                                       // s_x / sl reused by the next irregular tile
         P = pnext;
+#ifdef UQ_FOLD_PROF
+        pfb += wall_clock64() - qf;
+#endif
     }
+#ifdef UQ_FOLD_PROF
+    if (tid == 0 && vec == 0)
+        printf("fold: prefetch %llu map %llu rec %llu (%d) fallback %llu (%d) total %llu ticks (100 MHz)\n",
+               (unsigned long long)(pt1 - pt0), (unsigned long long)pmap, (unsigned long long)prec, nrw,
+               (unsigned long long)pfb, nfb, (unsigned long long)(wall_clock64() - pt0));
+#endif
 }
 
 // Outputs, one workgroup per tile, from the exact tile prefix pre[t] (any row alignment).
@@ -1583,7 +1810,7 @@ int hip_check(hipError_t e, const char* what) {
 }
 
 struct WsLayout {
-    size_t agg_off, incl_off, map1_off, part_off, l1_off, total;
+    size_t agg_off, incl_off, map1_off, rec_off, cnt_off, part_off, l1_off, total;
     int32_t tiles;
 };
 
@@ -1595,7 +1822,10 @@ WsLayout layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.agg_off = kCtrlBytes;
     w.incl_off = up(w.agg_off + (size_t)n * tiles * sizeof(uint64_t));
     w.map1_off = up(w.incl_off + (size_t)n * tiles * sizeof(uint64_t));
-    w.part_off = up(w.map1_off + (size_t)n * tiles * sizeof(uint64_t));
+    const size_t rec_clients = (size_t)std::min<int64_t>(n, kRecClients);
+    w.rec_off = up(w.map1_off + (size_t)n * tiles * sizeof(uint64_t));
+    w.cnt_off = up(w.rec_off + rec_clients * kRecPerClient * sizeof(TileRec));
+    w.part_off = up(w.cnt_off + rec_clients * sizeof(uint32_t));
     w.l1_off = up(w.part_off + (size_t)n * plan.total_groups * 32 * sizeof(float));
     w.total = up(w.l1_off + (size_t)n * sizeof(float));
     return w;
@@ -1946,6 +2176,11 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
         uint64_t* agg = (uint64_t*)(wsb + w.agg_off) + j0 * w.tiles;
         uint64_t* pre = (uint64_t*)(wsb + w.incl_off) + j0 * w.tiles;
         uint64_t* map1 = (uint64_t*)(wsb + w.map1_off) + j0 * w.tiles;
+        TileRec* recs = (TileRec*)(wsb + w.rec_off);
+        uint32_t* reccnt = (uint32_t*)(wsb + w.cnt_off);
+        rc = hip_check(hipMemsetAsync(reccnt, 0, std::min<int64_t>(nj, kRecClients) * sizeof(uint32_t), st),
+                       "memset record counters");
+        if (rc) return rc;
         const int64_t total_tiles = nj * (int64_t)w.tiles;
         const bool seg = vec4 && d <= ((int64_t)1 << 29) && total_tiles >= kSegMinTiles;
         const dim3 tgrid((unsigned)w.tiles, (unsigned)nj);
@@ -1966,22 +2201,20 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
         }
         rc = hip_check(hipGetLastError(), "tile sums launch");
         if (rc) return rc;
-        hipLaunchKernelGGL(tile_prefix_kernel, dim3((unsigned)((nj + 255) / 256)), dim3(256), 0, st, agg, pre, nj,
-                           w.tiles);
-        rc = hip_check(hipGetLastError(), "tile_prefix_kernel launch");
-        if (rc) return rc;
         if (vec4) {
-            hipLaunchKernelGGL(tile_map_kernel<true>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, pre, agg, map1);
+            hipLaunchKernelGGL(tile_map_kernel<true>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg, pre, map1, recs,
+                               reccnt);
             rc = hip_check(hipGetLastError(), "tile_map_kernel launch");
             if (rc) return rc;
             hipLaunchKernelGGL(exact_fold_kernel<true>, dim3((unsigned)nj), dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j,
-                               agg, map1, pre);
+                               pre, map1, pre, recs, reccnt);
         } else {
-            hipLaunchKernelGGL(tile_map_kernel<false>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, pre, agg, map1);
+            hipLaunchKernelGGL(tile_map_kernel<false>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg, pre, map1, recs,
+                               reccnt);
             rc = hip_check(hipGetLastError(), "tile_map_kernel launch");
             if (rc) return rc;
             hipLaunchKernelGGL(exact_fold_kernel<false>, dim3((unsigned)nj), dim3(kQBlock), 0, st, xj, d, w.tiles, fm,
-                               l1j, agg, map1, pre);
+                               l1j, pre, map1, pre, recs, reccnt);
         }
         rc = hip_check(hipGetLastError(), "exact_fold_kernel launch");
         if (rc) return rc;
