@@ -7,7 +7,7 @@ PKG = os.path.join(ROOT, "unbiased-quantization-distributed-mean-estimation_amd"
 SRC = os.path.join(PKG, "csrc", "uq_dme.hip")
 OUT = os.path.join(PKG, "_build", "abl")
 VARIANTS = {"base": [], "copy": ["-DUQ_ABL_COPY"],
-            "noties": ["-DUQ_EXP_NOTIES"], "noirrties": ["-DUQ_EXP_NOIRR", "-DUQ_EXP_NOTIES"]}
+            "k1default": ["-DUQ_K1_NO_NT"]}
 def build():
     sys.path.insert(0, PKG)
     import build_ext as be
@@ -38,6 +38,14 @@ def run():
             codes = torch.empty((n, d), dtype=torch.int8, device="cuda"); km = torch.zeros(n, dtype=torch.int32, device="cuda")
             calls["q+codes"] = (lambda: g(x.data_ptr(), q.data_ptr(), codes.data_ptr(), km.data_ptr(), n, d, 224426, X.data_ptr(), l1.data_ptr(), None, 1, ws.data_ptr(), b.value, sp), 9)
             calls["codes"] = (lambda: g(x.data_ptr(), None, codes.data_ptr(), km.data_ptr(), n, d, 224426, X.data_ptr(), l1.data_ptr(), None, 1, ws.data_ptr(), b.value, sp), 5)
+        h = L.uq_l1_torch_order_f32
+        h.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                      ctypes.c_size_t, ctypes.c_void_p]
+        l1o = torch.empty(n, device="cuda")
+        calls["l1"] = (lambda: h(x.data_ptr(), n, d, 1, l1o.data_ptr(), ws.data_ptr(), b.value, sp), 4)
+        if "q+codes" in calls:
+            qc = calls["q+codes"][0]
+            calls["l1,q+codes"] = (lambda: h(x.data_ptr(), n, d, 1, l1o.data_ptr(), ws.data_ptr(), b.value, sp) or qc(), 13)
         for cname, (fn, bpe) in calls.items():
             for _ in range(3): assert fn() == 0
             torch.cuda.synchronize()

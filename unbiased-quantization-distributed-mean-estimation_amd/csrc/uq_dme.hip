@@ -187,7 +187,13 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
         for (int r = 0; r < step; ++r) {
             float v0, v1, v2, v3;
             if (VEC4) {
+#ifndef UQ_K1_NO_NT            // x is streamed once per pass: non-temporal (measured 8.7 % faster)
+                typedef float k1x4 __attribute__((ext_vector_type(4)));
+                const k1x4 tv = __builtin_nontemporal_load(reinterpret_cast<const k1x4*>(p + (int64_t)r * 32));
+                const float4 t = make_float4(tv.x, tv.y, tv.z, tv.w);
+#else
                 const float4 t = *reinterpret_cast<const float4*>(p + (int64_t)r * 32);
+#endif
                 v0 = t.x; v1 = t.y; v2 = t.z; v3 = t.w;
             } else {
                 const float* pr = p + (int64_t)r * 32;
