@@ -314,3 +314,21 @@ def test_k2_forms_agree_stream_segmented_per_tile(uq, n, d):
     tc, q = uq.quantize_encode(xd, m=m, X=X, torch_threads=1, return_q=True)
     assert G.bits_equal(q.cpu().numpy(), phased)
     assert G.bits_equal(uq.decode(tc).cpu().numpy(), phased)
+
+
+@pytest.mark.parametrize("R", [0.5, 6.5, 10])
+def test_stream_form_all_rates_and_ragged_rows(uq, R):
+    """n >= 256 (stream kernel) at low and high rates: k >= 256 takes the arithmetic output
+    path (the running-max bound on the table), heavy tails make large k, and d is not a
+    multiple of the tile."""
+    rng = np.random.default_rng(int(R * 10))
+    n, d = 256, 3 * 4096 + 20
+    x = rng.laplace(1, 2, (n, d)).astype(f32)
+    x[::7] *= np.float32(50.0)
+    X = rng.random(n).astype(f32)
+    m = O.rate_to_m(R, d)
+    got = uq.quantize_dequantize(dev(x), m=m, X=X, torch_threads=1).cpu().numpy()
+    ref, _ = C.quantize_batch(x, m, X, 1)
+    assert G.n_mismatch(got, ref) == 0
+    tc, q = uq.quantize_encode(dev(x), m=m, X=X, torch_threads=1, return_q=True)
+    assert G.bits_equal(q.cpu().numpy(), ref)
