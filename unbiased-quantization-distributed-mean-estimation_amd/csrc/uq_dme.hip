@@ -1256,8 +1256,10 @@ struct TileRec {
     EvEntry ev[kRecEvents];
 };
 
-// Exact tile maps in the binade of P'_t: map0[t] = m0 (NaN: irregular), map1[t] = m1, or for
-// an irregular tile its record number + 1 (0: no record).
+// Exact tile maps in the binade E of P'_t, in units of G = 2^(E-52): map0[t] = m0/G | (E+1023)
+// << 53 and map1[t] = m1/G (both < 2^52); an irregular tile has map0 = kIrrMap and map1 = its
+// record number + 1 (0: no record).
+constexpr uint64_t kIrrMap = ~0ull;
 template <bool VEC4>
 __global__ void __launch_bounds__(kQBlock)
 tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
@@ -1293,9 +1295,11 @@ tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
         tile_pass1<false, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
     double m0 = 0.0, m1 = 0.0;
     if (resolve_map(Pg, B, st, s_x, sl, tid, m0, m1)) {
-        if (tid == 0) {
-            map0[idx] = (uint64_t)__double_as_longlong(m0);
-            map1[idx] = (uint64_t)__double_as_longlong(m1);
+        if (tid == 0) {                                        // in units of G, with the binade
+            const uint64_t eb = (uint64_t)__double_as_longlong(B.b0) >> 52;
+            const int sh = 52 - ((int)eb - 1023);
+            map0[idx] = (uint64_t)ldexp(m0, sh) | (eb << 53);
+            map1[idx] = (uint64_t)ldexp(m1, sh);
         }
         return;
     }
@@ -1316,7 +1320,7 @@ tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
     __syncthreads();
     const uint32_t rno = (uint32_t)sl.misc[0];
     if (tid == 0) {
-        map0[idx] = (uint64_t)__double_as_longlong(__builtin_nan(""));
+        map0[idx] = kIrrMap;
         map1[idx] = rno;
     }
     if (rno == 0u) return;
@@ -1344,25 +1348,32 @@ tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
     }
 }
 
-constexpr int kFoldChunk = 1024;   // tile maps staged in LDS at a time
 constexpr int kFoldEvents = 256;   // record events prefetched into LDS (24 KB)
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // One workgroup per client: the exact serial fold over its tile maps; irregular tiles are
-// loaded and resolved from their exact start.  pre[t] = exact P_t.
+// walked from their event records, or loaded and resolved from their exact start.
+// pre[t] = exact P_t.  A run of regular maps is walked in integer units of its binade's G
+// (P stays in the binade): a parity select and a 64-bit add per tile on uniform values,
+// maps read 8 ahead.
 template <bool VEC4>
 __global__ void __launch_bounds__(kQBlock)
 exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
-                  const uint64_t* map0, const uint64_t* __restrict__ map1, uint64_t* pre,
+                  const uint64_t* __restrict__ map0, const uint64_t* __restrict__ map1, uint64_t* __restrict__ pre,
                   const TileRec* __restrict__ recs, const uint32_t* __restrict__ reccnt) {
-    // (map0 and pre may alias: pre overwrites maps already staged in LDS)
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
     __shared__ ScanLds sl;
-    __shared__ double s_m0[kFoldChunk], s_m1[kFoldChunk], s_pre[kFoldChunk];
     __shared__ EvEntry s_ev[kFoldEvents];                  // the client's records, prefetched
     __shared__ uint32_t s_roff[kRecPerClient], s_rcnt[kRecPerClient];
     __shared__ double s_rlast[kRecPerClient];
     const int tid = threadIdx.x;
     const int64_t vec = blockIdx.x;
+    const int64_t base = vec * tiles;
     const DivPlan dp = div_plan(l1[vec]);
 #ifdef UQ_FOLD_PROF
     uint64_t pt0 = wall_clock64(), pmap = 0, prec = 0, pfb = 0;
@@ -1395,87 +1406,53 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
 #ifdef UQ_FOLD_PROF
     const uint64_t pt1 = wall_clock64();
 #endif
-    double P = 0.0;
-    for (int32_t tile = 0; tile < tiles; ++tile) {
-        int ci = tile % kFoldChunk;
-        if (ci == 0) {                                         // stage the next chunk of maps
-            __syncthreads();
-            const int64_t b = vec * tiles + tile;
-            for (int i = tid; i < kFoldChunk && tile + i < tiles; i += kQBlock) {
-                s_m0[i] = __longlong_as_double((long long)map0[b + i]);
-                s_m1[i] = __longlong_as_double((long long)map1[b + i]);
-            }
-            __syncthreads();
-        }
-        {   // a run of regular maps (P stays in their binade): one lane, maps read one ahead
+    constexpr uint64_t kMant = (1ull << 52) - 1ull;
+    uint64_t Pb = 0;                                           // bits of the exact P (P_0 = 0)
+    int32_t tile = 0;
+    while (tile < tiles) {
 #ifdef UQ_FOLD_PROF
-            const uint64_t q0 = wall_clock64();
+        const uint64_t q0 = wall_clock64();
 #endif
-            const int cend = min(kFoldChunk, tiles - (tile - ci));
-            if (tid == 0) {
-                double Pl = P;
-                int c = ci;
-                // maps read a group of 4 ahead; both candidate sums formed before the parity
-                // select, so the dependent chain per tile is one add and one select
-                double a0[4], a1[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int cn = min(c + u, cend - 1);
-                    a0[u] = s_m0[cn];
-                    a1[u] = s_m1[cn];
+        // a run of regular maps; lane l holds the maps of tile blk + l, the next 64 are
+        // loaded while this block is walked, and the walk reads them with readlane
+        const int lane = tid & (kWave - 1);
+        bool go = true;
+        int32_t blk = tile;
+        uint64_t am = map0[base + min(blk + lane, tiles - 1)], bm = map1[base + min(blk + lane, tiles - 1)];
+        while (go) {
+            const int32_t nb = blk + kWave;
+            uint64_t pv = 0;                                   // lane u: P of tile blk + u
+            const uint64_t an = map0[base + min(nb + lane, tiles - 1)], bn = map1[base + min(nb + lane, tiles - 1)];
+            for (int u = 0; u < kWave && go; ++u) {
+                const uint64_t au = readlane64(am, u), bu = readlane64(bm, u);
+                const uint64_t eb = au >> 53;                  // the map's binade (biased exponent)
+                if (tile >= tiles || au == kIrrMap || (Pb >> 52) != eb) {
+                    go = false;
+                } else {
+                    if (lane == u) pv = Pb;                        // stored per block below
+                    uint64_t Pi = (Pb & kMant) | (1ull << 52);     // P / G
+                    Pi += (Pi & 1ull) ? bu : (au & ((1ull << 53) - 1ull));
+                    Pb = (Pi & kMant) | (eb << 52);
+                    ++tile;
                 }
-                bool more = true;
-                while (more) {
-                    double b0[4], b1[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int cn = min(c + 4 + u, cend - 1);
-                        b0[u] = s_m0[cn];
-                        b1[u] = s_m1[cn];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        if (more && !(a0[u] == a0[u])) more = false;      // irregular tile: stop
-                        if (more) {
-                            s_pre[c] = Pl;                             // copied to pre[] below
-                            const double q0 = Pl + a0[u], q1 = Pl + a1[u];
-                            Pl = lowbit(Pl) ? q1 : q0;
-                            if (++c == cend) more = false;
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        a0[u] = b0[u];
-                        a1[u] = b1[u];
-                    }
-                }
-                sl.misc[0] = Pl;
-                sl.misc[1] = (double)c;
             }
-            __syncthreads();
-            P = sl.misc[0];
-            const int c = (int)sl.misc[1];
-            {
-                const int64_t base = vec * tiles + (tile - ci);
-                for (int i = ci + tid; i < c; i += kQBlock) pre[base + i] = (uint64_t)__double_as_longlong(s_pre[i]);
-            }
-            __syncthreads();
-            tile += c - ci;
-            ci = c;
-#ifdef UQ_FOLD_PROF
-            pmap += wall_clock64() - q0;
-#endif
-            if (ci == cend) {                                  // chunk folded: stage the next one
-                --tile;
-                continue;
-            }
+            if (tid < tile - blk) pre[base + blk + tid] = pv;  // wave 0, one coalesced store
+            blk = nb;
+            am = an;
+            bm = bn;
         }
-        const int64_t idx = vec * tiles + tile;                // an irregular tile
-        if (tid == 0) pre[idx] = (uint64_t)__double_as_longlong(P);
-        const uint32_t rid = (uint32_t)__double_as_longlong(s_m1[ci]);
+#ifdef UQ_FOLD_PROF
+        pmap += wall_clock64() - q0;
+#endif
+        if (tile >= tiles) break;
+        // an irregular tile (or a map whose binade P is not in: resolved from the data)
+        double P = __longlong_as_double((long long)Pb);
+        const int64_t idx = base + tile;
+        if (tid == 0) pre[idx] = Pb;
+        const uint32_t rid = map0[idx] == kIrrMap ? (uint32_t)map1[idx] : 0u;
         if (rid != 0u && s_roff[rid - 1u] != ~0u) {            // recorded and prefetched: walk it
 #ifdef UQ_FOLD_PROF
-            const uint64_t q0 = wall_clock64();
+            const uint64_t q1 = wall_clock64();
             ++nrw;
 #endif
             if (tid == 0) {
@@ -1496,11 +1473,9 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
             P = sl.misc[0];
             __syncthreads();
 #ifdef UQ_FOLD_PROF
-            prec += wall_clock64() - q0;
+            prec += wall_clock64() - q1;
 #endif
-            continue;
-        }
-        if (rid != 0u) {                                       // recorded: walk its events from LDS
+        } else if (rid != 0u) {                                // recorded: copy it, walk it
             const TileRec* rec = recs + (vec * kRecPerClient + (rid - 1u));
             uint32_t* dst = reinterpret_cast<uint32_t*>(s_x);
             const uint32_t* src = reinterpret_cast<const uint32_t*>(rec);
@@ -1511,7 +1486,7 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
                 double S = P;
                 for (uint32_t e = 0; e < lr->count; ++e) {
                     const EvEntry& ev = lr->ev[e];
-                    S = S + ev.run;                            // exact start of the event
+                    S = S + ev.run;
                     if (ev.tie) {
                         S = S + (lowbit(S) ? ev.t1 : ev.t0);
                     } else {
@@ -1523,32 +1498,34 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
             __syncthreads();
             P = sl.misc[0];
             __syncthreads();
-            continue;
+        } else {                                               // from the data
+#ifdef UQ_FOLD_PROF
+            const uint64_t qf = wall_clock64();
+            ++nfb;
+#endif
+            TileRegs r;
+            load_tile<VEC4>(r, x, d, tiles, (uint32_t)idx, tid);
+            stage_tile<VEC4>(r, s_x, tid);
+            __syncthreads();
+            const int64_t t0 = (int64_t)tile * kQTile;
+            const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
+            const Binade B = binade_of(P);
+            TileState st;
+            TileVals tv;
+            if (len == kQTile)
+                tile_pass1<true, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
+            else
+                tile_pass1<false, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
+            double pnext;
+            (void)resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);
+            __syncthreads();                                   // s_x / sl reused by the next irregular tile
+            P = pnext;
+#ifdef UQ_FOLD_PROF
+            pfb += wall_clock64() - qf;
+#endif
         }
-#ifdef UQ_FOLD_PROF
-        const uint64_t qf = wall_clock64();
-        ++nfb;
-#endif
-        TileRegs r;
-        load_tile<VEC4>(r, x, d, tiles, (uint32_t)idx, tid);
-        stage_tile<VEC4>(r, s_x, tid);
-        __syncthreads();
-        const int64_t t0 = (int64_t)tile * kQTile;
-        const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
-        const Binade B = binade_of(P);
-        TileState st;
-        TileVals tv;
-        if (len == kQTile)
-            tile_pass1<true, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
-        else
-            tile_pass1<false, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
-        double pnext;
-        (void)resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);
-        __syncthreads();                                       // s_x / sl reused by the next irregular tile
-        P = pnext;
-#ifdef UQ_FOLD_PROF
-        pfb += wall_clock64() - qf;
-#endif
+        Pb = (uint64_t)__double_as_longlong(P);
+        ++tile;
     }
 #ifdef UQ_FOLD_PROF
     if (tid == 0 && vec == 0)
@@ -2213,17 +2190,18 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
             rc = hip_check(hipGetLastError(), "tile_map_kernel launch");
             if (rc) return rc;
             hipLaunchKernelGGL(exact_fold_kernel<true>, dim3((unsigned)nj), dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j,
-                               pre, map1, pre, recs, reccnt);
+                               pre, map1, agg, recs, reccnt);
         } else {
             hipLaunchKernelGGL(tile_map_kernel<false>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg, pre, map1, recs,
                                reccnt);
             rc = hip_check(hipGetLastError(), "tile_map_kernel launch");
             if (rc) return rc;
             hipLaunchKernelGGL(exact_fold_kernel<false>, dim3((unsigned)nj), dim3(kQBlock), 0, st, xj, d, w.tiles, fm,
-                               l1j, pre, map1, pre, recs, reccnt);
+                               l1j, pre, map1, agg, recs, reccnt);
         }
         rc = hip_check(hipGetLastError(), "exact_fold_kernel launch");
         if (rc) return rc;
+        pre = agg;                                             // the fold's exact prefixes
         if (seg) {
 #define UQ_SEG(Q, C, CV)                                                                                    \
     case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
