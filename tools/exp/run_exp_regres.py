@@ -1,0 +1,81 @@
+"""Times tools/exp/exp_regres.hip (register-resident fused K1+K2 data flow: x read once)
+against K1 + K2 on the C2 batch (1024 x 2^20).
+Build: cd tools/exp && hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -o libexp_regres.so exp_regres.hip"""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import uqdme
+    from uqdme_amd import _lib
+    lib = _lib.load()
+    ex = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp_regres.so"))
+    ex.exp_regres.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                              ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                              ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+    n, d = 1024, 1 << 20
+    m = uqdme.rate_to_m(1, d)
+    dev = torch.device("cuda")
+    x = torch.randn(n, d, device=dev)
+    q = torch.empty_like(x)
+    codes = torch.empty((n, d), dtype=torch.int8, device=dev)
+    ovf = torch.zeros(n, dtype=torch.int32, device=dev)
+    X = torch.rand(n, device=dev)
+    l1 = torch.empty(n, device=dev)
+    b = ctypes.c_size_t()
+    lib.uq_workspace_bytes(n, d, 1, ctypes.byref(b))
+    ws = torch.zeros(max(b.value, 64 << 20), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def base():
+        _lib.check(lib.uq_l1_torch_order_f32(x.data_ptr(), n, d, 1, l1.data_ptr(), ws.data_ptr(), b.value, st), "l1")
+        _lib.check(lib.uq_type_unbiased_codes_f32(x.data_ptr(), q.data_ptr(), codes.data_ptr(), ovf.data_ptr(), n, d, m,
+                                                  X.data_ptr(), l1.data_ptr(), None, 1, ws.data_ptr(), b.value, st), "k2")
+
+    used = ctypes.c_int()
+
+    def fused(E, slots, mode):
+        def f():
+            rc = ex.exp_regres(x.data_ptr(), q.data_ptr(), codes.data_ptr(), n, d, float(m), E, slots, ws.data_ptr(),
+                               mode, st, ctypes.byref(used))
+            assert rc == 0, rc
+        return f
+
+    def timeit(f, k=10):
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(k):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        return round(e0.elapsed_time(e1) / k, 4)
+
+    res = {"k1+k2": timeit(base)}
+    for E in (64, 32):
+        for slots in (0, 8):
+            for mode in (0, 1):
+                t = timeit(fused(E, slots, mode))
+                S = d // (E * 1024)
+                errw = int(ws[(n * S + 2 * n) * 4:(n * S + 2 * n) * 4 + 4].view(torch.int32).item())
+                res[f"E{E}_slots{slots or 'max'}_chain{mode}"] = {"ms": t, "slots_x1000_plus_wg_per_cu": used.value,
+                                                                  "err": errw}
+                print(json.dumps({k: v for k, v in res.items()}), flush=True)
+    # check the stand-in output is what the data flow computed (x * m / L1 with L1 ~ sum |x|)
+    j = 5
+    ref = x[j] * (m / x[j].abs().sum())
+    res["check_maxrel"] = float(((q[j] - ref).abs().max() / ref.abs().max()).item())
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
