@@ -17,6 +17,7 @@
  *
  *   gcc -O2 -mfma -fopenmp -ffp-contract=off tools/markstein_check.c -o /tmp/mk -lm
  *   /tmp/mk [n_divisors=14]        # ~13 s per divisor on 8 cores
+ *   /tmp/mk 13 m                   # the biased dequantize divisors m (div_plan_m)
  * Round-1 run: 14 divisors, 59,894,661,120 quotients, 0 mismatches.  An earlier variant
  * without the guard showed the failures it removes: |x| <= 2^-87 (residual underflow).
  */
@@ -39,7 +40,14 @@ static inline float kernel_div(float a, float den, float y, float thr) {
     return q;
 }
 
+/* "m" mode: the biased dequantize step k''/m (div_plan_m: den = f32(m), no 1e-12 term)
+ * for the m values of the configs (C1, C2/C3, C4, C5, CIFAR-10 at R=1,2) plus
+ * 1, 3 and f32(2^24+1), every finite x as above. */
+static const float kM[] = {219.f, 652.f, 224426.f, 668488.f, 897706.f, 2673952.f, 36931.f, 110006.f,
+                           26245.f, 78176.f, 1.f, 3.f, 16777217.f};
+
 int main(int argc, char** argv) {
+    const int mmode = argc > 2 && strcmp(argv[2], "m") == 0;
     const int nb = argc > 1 ? atoi(argv[1]) : 14;
     uint64_t s = 12345;
     long long bad = 0, total = 0;
@@ -50,6 +58,10 @@ int main(int argc, char** argv) {
         if (ib == 0) den = 1e-12f;
         if (ib == 1) den = nextafterf(0x1p40f, 0.0f);
         if (ib == 2) den = 1e-12f + 1e-12f * 0x1p-20f;
+        if (mmode) {
+            if (ib >= (int)(sizeof kM / sizeof kM[0])) break;
+            den = kM[ib];
+        }
         const float y = 1.0f / den, thr = 0x1p-59f / den;
         long long lb = 0;
 #pragma omp parallel for reduction(+ : lb) schedule(static, 1 << 16)

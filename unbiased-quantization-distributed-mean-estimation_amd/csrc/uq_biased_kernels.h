@@ -57,10 +57,25 @@ __device__ __forceinline__ uint32_t rez_key_of(float dp, bool up) {
 // k' and the key of one coordinate, exactly the reference's f32 ops (no contraction):
 // p = |x| / (L1 + 1e-12) (AS:681), mp = m * p, k' = floor(mp + 0.5) (AS:648),
 // delta' = k' - mp (AS:655).
-__device__ __forceinline__ uint32_t rez_elem(float xv, float den, float fm, bool up, float& kp) {
-    const float mp = fm * (fabsf(xv) / den);
+__device__ __forceinline__ uint32_t rez_elem(float xv, const DivPlan& dp, float fm, bool up, float& kp) {
+    const float mp = fm * div1(fabsf(xv), dp);      // RN(|x| / den), reciprocal + Markstein
     kp = floorf(mp + 0.5f);
     return rez_key_of(kp - mp, up);
+}
+
+// Four at a time: packed reciprocal division with one guard test per four (div4).
+__device__ __forceinline__ void rez_elem4(const float (&xv)[4], const DivPlan& dp, float fm, bool up, float (&kp)[4],
+                                          uint32_t (&key)[4]) {
+    float a[4], p[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a[c] = fabsf(xv[c]);
+    div4(a, dp, p);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float mp = fm * p[c];
+        kp[c] = floorf(mp + 0.5f);
+        key[c] = rez_key_of(kp[c] - mp, up);
+    }
 }
 
 template <int PASS> struct RadixPass;
@@ -132,12 +147,12 @@ rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
     const int tid = threadIdx.x;
     for (int b = tid; b < kRadixBins; b += 256) h[b] = 0u;
     __syncthreads();
-    const float den = l1[vec] + 1e-12f;
+    const DivPlan dp = div_plan(l1[vec]);
     const float* xv = x + vec * d;
     const int64_t b0 = (int64_t)blockIdx.x * kHistSpan;
     auto visit = [&](float v) {
         float kp;
-        const uint32_t key = rez_elem(v, den, fm, up, kp);
+        const uint32_t key = rez_elem(v, dp, fm, up, kp);
         if ((key & RP::hmask) == prefix) atomicAdd(&h[(key >> RP::shift) & RP::dmask], 1u);
     };
     if (VEC4) {
@@ -241,7 +256,7 @@ rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restri
     if (st[vec].kleft == 0 || !(st[vec].flags & kRezCompact)) return;
     const uint32_t prefix = st[vec].prefix;
     const bool up = st[vec].delta > 0;
-    const float den = l1[vec] + 1e-12f;
+    const DivPlan dp = div_plan(l1[vec]);
     const float* xv = x + vec * d;
     const int tid = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * kHistSpan;
@@ -254,17 +269,20 @@ rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restri
         const int64_t i = b0 + 4 * ((int64_t)j * 256 + tid);          // elements i .. i+3
         float v[4];
         if (VEC4 && i + 3 < d) {
-            const float4 t = *reinterpret_cast<const float4*>(xv + i);
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(xv + i));
             v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
         } else {
 #pragma unroll
             for (int c = 0; c < 4; ++c) v[c] = (i + c < d) ? xv[i + c] : 0.f;
         }
+        float kp[4];
+        uint32_t k4[4];
+        rez_elem4(v, dp, fm, up, kp, k4);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            float kp;
-            key[4 * j + c] = rez_elem(v[c], den, fm, up, kp);
-            if (i + c < d && (key[4 * j + c] & 0xFFE00000u) == prefix) match |= 1ull << (4 * j + c);
+            key[4 * j + c] = k4[c];
+            if (i + c < d && (k4[c] & 0xFFE00000u) == prefix) match |= 1ull << (4 * j + c);
         }
     }
     uint32_t tot;
@@ -347,7 +365,7 @@ rez_tiecount_kernel(const float* __restrict__ x, int64_t d, const float* __restr
     if (!(fl & kRezAmbiguous) || (fl & kRezTorchTies)) return;
     const uint32_t tau = st[vec].prefix;
     const bool up = st[vec].delta > 0;
-    const float den = l1[vec] + 1e-12f;
+    const DivPlan dp = div_plan(l1[vec]);
     const float* xv = x + vec * d;
     const int tid = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * kSelTile + (int64_t)tid * kSelItems;
@@ -358,14 +376,14 @@ rez_tiecount_kernel(const float* __restrict__ x, int64_t d, const float* __restr
 #pragma unroll
         for (int j = 0; j < kSelItems / 4; ++j) {
             const float4 t = x4[j];
-            cnt += rez_elem(t.x, den, fm, up, kp) == tau;
-            cnt += rez_elem(t.y, den, fm, up, kp) == tau;
-            cnt += rez_elem(t.z, den, fm, up, kp) == tau;
-            cnt += rez_elem(t.w, den, fm, up, kp) == tau;
+            cnt += rez_elem(t.x, dp, fm, up, kp) == tau;
+            cnt += rez_elem(t.y, dp, fm, up, kp) == tau;
+            cnt += rez_elem(t.z, dp, fm, up, kp) == tau;
+            cnt += rez_elem(t.w, dp, fm, up, kp) == tau;
         }
     } else {
         for (int j = 0; j < kSelItems; ++j)
-            if (e0 + j < d) cnt += rez_elem(xv[e0 + j], den, fm, up, kp) == tau;
+            if (e0 + j < d) cnt += rez_elem(xv[e0 + j], dp, fm, up, kp) == tau;
     }
     __shared__ uint32_t lds[4];
     uint32_t total;
@@ -394,13 +412,51 @@ rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t 
     const bool replay = amb && (s.flags & kRezTorchTies);
     const bool up = s.delta > 0;
     const float L = l1[vec];
-    const float den = L + 1e-12f;
+    const DivPlan dp = div_plan(L);
+    const DivPlan dpm = div_plan_m(fm);
     const float adj = up ? -1.f : 1.f;
     const uint32_t tau = s.prefix;
     const float* xv = x + vec * d;
     float* ov = out + vec * d;
     const int tid = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * kSelTile + (int64_t)tid * kSelItems;
+    const int64_t tb = (int64_t)blockIdx.x * kSelTile;
+    if (VEC4 && !(amb && !replay) && tb + kSelTile <= d) {
+        // no index-order rank needed (block-uniform): lane-interleaved float4s, one
+        // coalesced 1 KB row per wave per load, non-temporal loads and stores
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v* x4 = reinterpret_cast<const f4v*>(xv + tb);
+        f4v* o4 = reinterpret_cast<f4v*>(ov + tb);
+        const uint32_t* tbw = tie_bits + vec * ((d + 31) / 32);
+        f4v a[kSelItems / 4];
+#pragma unroll
+        for (int j = 0; j < kSelItems / 4; ++j) a[j] = __builtin_nontemporal_load(x4 + j * 256 + tid);
+#pragma unroll
+        for (int j = 0; j < kSelItems / 4; ++j) {
+            const float v4[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
+            float k4[4], r4[4];
+            uint32_t y4[4];
+            rez_elem4(v4, dp, fm, up, k4, y4);
+            const int64_t i0 = tb + 4 * ((int64_t)j * 256 + tid);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                bool sel = false;
+                if (on) {
+                    if (y4[c] > tau) sel = true;
+                    else if (y4[c] == tau) sel = !amb || ((tbw[(i0 + c) >> 5] >> ((i0 + c) & 31)) & 1u);
+                }
+                k4[c] = sel ? k4[c] + adj : k4[c];             // k''
+            }
+            div4(k4, dpm, r4);                                 // RN(k'' / m)
+            f4v o;
+            o.x = (L * torch_signf(v4[0])) * r4[0];            // AS:687 (L1 * signs) * (k'' / m)
+            o.y = (L * torch_signf(v4[1])) * r4[1];
+            o.z = (L * torch_signf(v4[2])) * r4[2];
+            o.w = (L * torch_signf(v4[3])) * r4[3];
+            __builtin_nontemporal_store(o, o4 + j * 256 + tid);
+        }
+        return;
+    }
+    const int64_t e0 = tb + (int64_t)tid * kSelItems;
     const bool full = VEC4 && e0 + kSelItems <= d;
     float v[kSelItems];
     if (full) {
@@ -418,10 +474,19 @@ rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t 
     uint32_t key[kSelItems];
     uint32_t cnt = 0;
 #pragma unroll
-    for (int j = 0; j < kSelItems; ++j) {
-        key[j] = rez_elem(v[j], den, fm, up, kp[j]);
-        cnt += (key[j] == tau && e0 + j < d);
+    for (int j = 0; j < kSelItems / 4; ++j) {
+        const float v4[4] = {v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
+        float k4[4];
+        uint32_t y4[4];
+        rez_elem4(v4, dp, fm, up, k4, y4);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            kp[4 * j + c] = k4[c];
+            key[4 * j + c] = y4[c];
+        }
     }
+#pragma unroll
+    for (int j = 0; j < kSelItems; ++j) cnt += (key[j] == tau && e0 + j < d);
     uint32_t rank = 0;
     if (amb && !replay) {              // block-uniform
         __shared__ uint32_t lds[4];
@@ -450,8 +515,16 @@ rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t 
                 else sel = (rank++ < s.need);
             }
         }
-        const float k2 = sel ? kp[j] + adj : kp[j];
-        q[j] = (L * torch_signf(v[j])) * (k2 / fm);      // AS:687 (L1 * signs) * (k'' / m)
+        q[j] = sel ? kp[j] + adj : kp[j];                 // k''
+    }
+#pragma unroll
+    for (int j = 0; j < kSelItems / 4; ++j) {
+        const float k4[4] = {q[4 * j], q[4 * j + 1], q[4 * j + 2], q[4 * j + 3]};
+        float r4[4];
+        div4(k4, dpm, r4);                                 // RN(k'' / m)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            q[4 * j + c] = (L * torch_signf(v[4 * j + c])) * r4[c];   // AS:687 (L1 * signs) * (k'' / m)
     }
     if (full) {
         float4* o4 = reinterpret_cast<float4*>(ov + e0);

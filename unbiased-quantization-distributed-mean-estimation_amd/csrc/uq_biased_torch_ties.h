@@ -395,7 +395,7 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         if (s.kleft == 0 || !(s.flags & kRezAmbiguous)) continue;
         const bool up = s.delta > 0;
         const int64_t k = up ? s.delta : -(int64_t)s.delta;
-        const float den = l1[vec] + 1e-12f;
+        const DivPlan dp = div_plan(l1[vec]);
         const float* xv = x + vec * d;
         TT_T0();
         // queue[j] = (value, j) (TopKImpl.h); 4 coordinates per lane and load
@@ -420,10 +420,10 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
                 if (i >= d) continue;
                 float kp;
                 uint4 kk, ii;
-                kk.x = rez_elem(v[u].x, den, fm, up, kp);
-                kk.y = rez_elem(v[u].y, den, fm, up, kp);
-                kk.z = rez_elem(v[u].z, den, fm, up, kp);
-                kk.w = rez_elem(v[u].w, den, fm, up, kp);
+                kk.x = rez_elem(v[u].x, dp, fm, up, kp);
+                kk.y = rez_elem(v[u].y, dp, fm, up, kp);
+                kk.z = rez_elem(v[u].z, dp, fm, up, kp);
+                kk.w = rez_elem(v[u].w, dp, fm, up, kp);
                 ii = make_uint4((uint32_t)i, (uint32_t)i + 1, (uint32_t)i + 2, (uint32_t)i + 3);
                 if (i + 3 < d) {
                     *reinterpret_cast<uint4*>(A.K + i) = kk;

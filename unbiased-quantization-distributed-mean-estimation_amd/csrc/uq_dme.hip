@@ -108,6 +108,81 @@ bool make_plan(int64_t d, int32_t T, L1Plan* p) {
     return true;
 }
 
+// v = x / den (AS:625) without the IEEE division sequence (~10 VALU per element).  den is
+// one per client, so y = RN(1/den) is computed once (IEEE) and each quotient takes a
+// product and two residual corrections (Markstein):
+//     q0 = RN(x*y);  q1 = RN(q0 + RN(x - den*q0)*y)    (faithful)
+//                    q2 = RN(q1 + RN(x - den*q1)*y)    (= RN(x/den): y correctly rounded,
+//                                                       q1 faithful, no underflow)
+// as packed fma pairs.  No underflow: den = L1 + 1e-12 >= 2^-39.9 always and den < 2^40 is
+// required per client (else the IEEE division is used throughout), and elements with
+// |q2| < 2^-59/den (covers every 0 < |x| < 2^-60) or q2 NaN (x = inf/NaN, overflow) are
+// recomputed with the IEEE division.  x = +-0 gives q = +-0 in either sign, which is
+// immaterial (only v < 0 and |v| are used).  tools/markstein_check.c checks this exact
+// function against IEEE division over every finite f32 x for divisors across the range.
+struct DivPlan {
+    float den, y, thr;
+    bool fast;
+};
+__device__ __forceinline__ DivPlan div_plan(float L) {
+    DivPlan p;
+    p.den = L + 1e-12f;                  // AS:625 (f32 add)
+    p.fast = p.den < 0x1p40f;            // false for NaN / inf
+    p.y = 1.0f / p.den;
+    p.thr = 0x1p-59f / p.den;
+    return p;
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void div4(const float (&xs)[4], const DivPlan& dp, float (&vs)[4]) {
+    if (dp.fast) {
+        const f32x2 Y = {dp.y, dp.y}, B = {-dp.den, -dp.den};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x2 a = {xs[2 * h], xs[2 * h + 1]};
+            f32x2 q = a * Y;
+            f32x2 r = __builtin_elementwise_fma(B, q, a);
+            q = __builtin_elementwise_fma(r, Y, q);
+            r = __builtin_elementwise_fma(B, q, a);
+            q = __builtin_elementwise_fma(r, Y, q);
+            vs[2 * h] = q.x;
+            vs[2 * h + 1] = q.y;
+        }
+        bool bad = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bad |= !(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f;
+        if (__builtin_expect(bad, 0)) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (!(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f) vs[c] = xs[c] / dp.den;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) vs[c] = xs[c] / dp.den;
+    }
+}
+// One quotient, the same operations as div4 (so the same bits).
+__device__ __forceinline__ float div1(float x, const DivPlan& dp) {
+    if (!dp.fast) return x / dp.den;
+    float q = x * dp.y;
+    float r = fmaf(-dp.den, q, x);
+    q = fmaf(r, dp.y, q);
+    r = fmaf(-dp.den, q, x);
+    q = fmaf(r, dp.y, q);
+    if (__builtin_expect(!(fabsf(q) >= dp.thr) && x != 0.0f, 0)) q = x / dp.den;
+    return q;
+}
+// RN(k / m) for the dequantize step (m >= 1 is exact in f32 up to 2^24 and below 2^40
+// always): the same Markstein sequence with den = m itself (no 1e-12 term).
+__device__ __forceinline__ DivPlan div_plan_m(float fm) {
+    DivPlan p;
+    p.den = fm;
+    p.fast = fm >= 1.0f && fm < 0x1p40f;
+    p.y = 1.0f / fm;
+    p.thr = 0x1p-59f / fm;
+    return p;
+}
+
+
 // Element transforms summed by the K1 cascade.  The cascade itself (order of f32 adds)
 // is the torch CPU `sum` order whatever is summed.
 struct AbsOp {            // AS:624  input_vector.abs().sum()
@@ -118,12 +193,13 @@ struct AbsOp {            // AS:624  input_vector.abs().sum()
     __device__ float operator()(float v) const { return fabsf(v); }
 };
 struct RezKOp {           // AS:648-649  k' = floor(m * p + 0.5), p = |x| / (L1 + 1e-12)
-    float den, fm;
+    DivPlan dp;
+    float fm;
     uint32_t *h, *zn;
     __device__ static RezKOp make(const float* l1, float fm, int64_t vec) {
-        return RezKOp{l1[vec] + 1e-12f, fm, nullptr, nullptr};
+        return RezKOp{div_plan(l1[vec]), fm, nullptr, nullptr};
     }
-    __device__ float operator()(float v) const { return floorf(fm * (fabsf(v) / den) + 0.5f); }
+    __device__ float operator()(float v) const { return floorf(fm * div1(fabsf(v), dp) + 0.5f); }
 };
 // RezKOp that also counts the top 11 bits of the order key of +delta' = k' - m p into
 // h[2048] (the biased quantizer's first radix digit, KB4 pass 0), and delta' == 0 / NaN
@@ -131,13 +207,14 @@ struct RezKOp {           // AS:648-649  k' = floor(m * p + 0.5), p = |x| / (L1 
 // h / zn point to LDS in K1a (flushed per workgroup) and to global memory in K1b.
 struct RezKHistOp {
     static constexpr bool kHist = true;
-    float den, fm;
+    DivPlan dp;
+    float fm;
     uint32_t *h, *zn;
     __device__ static RezKHistOp make(const float* l1, float fm, int64_t vec) {
-        return RezKHistOp{l1[vec] + 1e-12f, fm, nullptr, nullptr};
+        return RezKHistOp{div_plan(l1[vec]), fm, nullptr, nullptr};
     }
     __device__ float operator()(float v) const {
-        const float mp = fm * (fabsf(v) / den);
+        const float mp = fm * div1(fabsf(v), dp);
         const float kp = floorf(mp + 0.5f);
         float dp = (kp - mp) + 0.0f;
         uint32_t u = __float_as_uint(dp);
@@ -515,59 +592,6 @@ struct TileState {
     double total;        // sum of t0 over the tile (same value in every thread)
     double t0, t1;       // this thread's increment from a start of parity 0 / 1 in the binade
 };
-
-// v = x / den (AS:625) without the IEEE division sequence (~10 VALU per element).  den is
-// one per client, so y = RN(1/den) is computed once (IEEE) and each quotient takes a
-// product and two residual corrections (Markstein):
-//     q0 = RN(x*y);  q1 = RN(q0 + RN(x - den*q0)*y)    (faithful)
-//                    q2 = RN(q1 + RN(x - den*q1)*y)    (= RN(x/den): y correctly rounded,
-//                                                       q1 faithful, no underflow)
-// as packed fma pairs.  No underflow: den = L1 + 1e-12 >= 2^-39.9 always and den < 2^40 is
-// required per client (else the IEEE division is used throughout), and elements with
-// |q2| < 2^-59/den (covers every 0 < |x| < 2^-60) or q2 NaN (x = inf/NaN, overflow) are
-// recomputed with the IEEE division.  x = +-0 gives q = +-0 in either sign, which is
-// immaterial (only v < 0 and |v| are used).  tools/markstein_check.c checks this exact
-// function against IEEE division over every finite f32 x for divisors across the range.
-struct DivPlan {
-    float den, y, thr;
-    bool fast;
-};
-__device__ __forceinline__ DivPlan div_plan(float L) {
-    DivPlan p;
-    p.den = L + 1e-12f;                  // AS:625 (f32 add)
-    p.fast = p.den < 0x1p40f;            // false for NaN / inf
-    p.y = 1.0f / p.den;
-    p.thr = 0x1p-59f / p.den;
-    return p;
-}
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void div4(const float (&xs)[4], const DivPlan& dp, float (&vs)[4]) {
-    if (dp.fast) {
-        const f32x2 Y = {dp.y, dp.y}, B = {-dp.den, -dp.den};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const f32x2 a = {xs[2 * h], xs[2 * h + 1]};
-            f32x2 q = a * Y;
-            f32x2 r = __builtin_elementwise_fma(B, q, a);
-            q = __builtin_elementwise_fma(r, Y, q);
-            r = __builtin_elementwise_fma(B, q, a);
-            q = __builtin_elementwise_fma(r, Y, q);
-            vs[2 * h] = q.x;
-            vs[2 * h + 1] = q.y;
-        }
-        bool bad = false;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) bad |= !(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f;
-        if (__builtin_expect(bad, 0)) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (!(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f) vs[c] = xs[c] / dp.den;
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) vs[c] = xs[c] / dp.den;
-    }
-}
 
 // mp = m*p of this thread's kQItems elements stays in registers between the passes, with
 // sign(v) folded in (v < 0 -> -mp; -0.0 marks a negative coordinate whose floor is 0); fl
