@@ -1981,13 +1981,14 @@ EdenLayout eden_layout(int64_t n, int64_t dim) {
 }
 
 // One FWHT pass: the register-radix kernels for the 4096-element low pass and the
-// 256 x 32 high pass, the generic LDS kernel otherwise (same stages, same bits).
+// 256 x 64 high pass, the generic LDS kernel otherwise (same stages, same bits).
 template <int M, bool L, bool R>
 void fwht_dispatch(dim3 grid, const FwhtArgs& b, int lo, int k, hipStream_t st) {
     if (lo == 0 && k == kFwhtLowBits && (M != 2 || (b.D % 16) == 0))
         hipLaunchKernelGGL((fwht_low4096_kernel<M, L, R>), grid, dim3(256), 0, st, b);
-    else if (lo > 0 && k == kFwhtHighBits && M == 0)
-        hipLaunchKernelGGL((fwht_high256_kernel<L, R>), grid, dim3(256), 0, st, b, lo);
+    else if (lo > 0 && k == kFwhtHighBits && M == 0 && ((int64_t)1 << lo) % kHighCols == 0)
+        hipLaunchKernelGGL((fwht_high256_kernel<L, R>), dim3(grid.x * kFwhtCols / kHighCols, grid.y), dim3(kHighT), 0, st,
+                           b, lo);
     else
         hipLaunchKernelGGL((fwht_pass_kernel<M, L, R>), grid, dim3(kFwhtT), 0, st, b, lo, k);
 }

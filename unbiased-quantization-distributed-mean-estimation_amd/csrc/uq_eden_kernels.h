@@ -262,46 +262,61 @@ fwht_low4096_kernel(FwhtArgs a) {
     }
 }
 
-// High pass: 256 rows (index bits lo..lo+7) x 32 columns.  Round 1: thread (c, g), c = tid % 32,
-// g = tid / 32, holds rows 32 g + m (m = 0..31; row bits 0-4).  Round 2: thread (c, h)
-// holds rows a + 32 u for a in 4h..4h+3, u = 0..7 (row bits 5-7).
+// High pass: 256 rows (index bits lo..lo+7) x 64 columns, 512 threads (a wave reads one
+// row's 64 contiguous floats, 256 B).  Round 1: thread (c, g), c = tid % 64, g = tid / 64,
+// holds rows 32 g + m (m = 0..31; row bits 0-4).  Round 2: thread (c, h) holds rows
+// a + 32 u for a in 4h..4h+3, u = 0..7 (row bits 5-7).
+constexpr int kHighCols = 64;
+constexpr int kHighT = 512;
 template <bool LAST, bool RECV_LAST>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kHighT)
 fwht_high256_kernel(FwhtArgs a, int lo) {
-    __shared__ float s[256 * 33];
-    __shared__ int8_t sgl[RECV_LAST ? 256 * 32 : 1];            // the tile's diagonal, row-major
+    __shared__ float s[256 * (kHighCols + 1)];
     const int64_t vec = blockIdx.y;
     const int tid = threadIdx.x;
     const int64_t D = a.D;
     const int64_t lowspan = (int64_t)1 << lo;
-    const int64_t col_groups = lowspan / kFwhtCols;
+    const int64_t col_groups = lowspan / kHighCols;
     const int64_t t = blockIdx.x;
     const int64_t hi = (t / col_groups) << (lo + 8);
-    const int64_t c0 = (t % col_groups) * kFwhtCols;
+    const int64_t c0 = (t % col_groups) * kHighCols;
     const int8_t* sg = a.signs + (int64_t)(a.sign_row ? a.sign_row[vec] : 0) * D;
-    const int c = tid & 31, g = tid >> 5;
+    const int c = tid & (kHighCols - 1), g = tid / kHighCols;
     const float* in = (const float*)a.in + vec * D;
-    if (RECV_LAST) {      // row `tid` of the tile: 32 contiguous sign bytes, two 16-byte loads
-        const int8_t* sr = sg + hi + ((int64_t)tid << lo) + c0;
-        *reinterpret_cast<int4*>(sgl + 32 * tid) = *reinterpret_cast<const int4*>(sr);
-        *reinterpret_cast<int4*>(sgl + 32 * tid + 16) = *reinterpret_cast<const int4*>(sr + 16);
+    const float sc = (RECV_LAST && a.scale) ? a.scale[vec] : 1.0f;
+    // the tile's diagonal as sign bits (2 KB of LDS keeps two workgroups per CU): thread
+    // tid packs the 32 sign bytes of half a row
+    __shared__ uint32_t sgb[RECV_LAST ? 2 * 256 : 1];
+    if (RECV_LAST) {
+        const int row = tid >> 1, half = tid & 1;
+        const int4* sr = reinterpret_cast<const int4*>(sg + hi + ((int64_t)row << lo) + c0 + 32 * half);
+        const int4 w0 = sr[0], w1 = sr[1];
+        const uint32_t wv[8] = {(uint32_t)w0.x, (uint32_t)w0.y, (uint32_t)w0.z, (uint32_t)w0.w,
+                                (uint32_t)w1.x, (uint32_t)w1.y, (uint32_t)w1.z, (uint32_t)w1.w};
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t w = wv[k];
+            bits |= (((w >> 7) & 1u) | ((w >> 14) & 2u) | ((w >> 21) & 4u) | ((w >> 28) & 8u)) << (4 * k);
+        }
+        sgb[tid] = bits;
     }
     float v[32];
 #pragma unroll
-    for (int m = 0; m < 32; ++m) v[m] = in[hi + ((int64_t)(32 * g + m) << lo) + c0 + c];
+    for (int m = 0; m < 32; ++m) v[m] = __builtin_nontemporal_load(in + hi + ((int64_t)(32 * g + m) << lo) + c0 + c);
 #pragma unroll
     for (int j = 0; j < 5; ++j)
 #pragma unroll
         for (int m = 0; m < 32; ++m)
             if (!(m & (1 << j))) bfly(v[m], v[m | (1 << j)]);
 #pragma unroll
-    for (int m = 0; m < 32; ++m) s[(32 * g + m) * 33 + c] = v[m];
+    for (int m = 0; m < 32; ++m) s[(32 * g + m) * (kHighCols + 1) + c] = v[m];
     __syncthreads();
     const int h = g;
 #pragma unroll
     for (int aa = 0; aa < 4; ++aa)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[aa * 8 + u] = s[(4 * h + aa + 32 * u) * 33 + c];
+        for (int u = 0; u < 8; ++u) v[aa * 8 + u] = s[(4 * h + aa + 32 * u) * (kHighCols + 1) + c];
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -319,11 +334,11 @@ fwht_high256_kernel(FwhtArgs a, int lo) {
             if (LAST) r = r / a.sqrtD;                             // AS:114
             if (RECV_LAST) {
                 if (gi < a.dim) {
-                    r = r * (float)sgl[32 * row + c];              // AS:152
-                    a.out[vec * a.dim + gi] = a.scale ? a.scale[vec] * r : r;
+                    r = r * (((sgb[2 * row + (c >> 5)] >> (c & 31)) & 1u) ? -1.0f : 1.0f);   // AS:152 (diag = +-1)
+                    __builtin_nontemporal_store(a.scale ? sc * r : r, a.out + vec * a.dim + gi);
                 }
             } else {
-                a.out[vec * D + gi] = r;
+                __builtin_nontemporal_store(r, a.out + vec * D + gi);
             }
         }
 }
