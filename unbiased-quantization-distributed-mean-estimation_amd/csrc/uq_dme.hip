@@ -295,10 +295,19 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
 }
 
 // Sequential sum of `nrows` rows of stream `a` starting at element `start`.
+// Loads go out 16 at a time ahead of the (ordered) adds: one memory round trip per 16 rows.
 template <class Op>
 __device__ float seq_rows(const Op& op, const float* __restrict__ xv, int64_t start, int64_t nrows, int a) {
     float acc = 0.f;
-    for (int64_t r = 0; r < nrows; ++r) acc += op(xv[start + r * 32 + a]);
+    int64_t r = 0;
+    for (; r + 16 <= nrows; r += 16) {
+        float t[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) t[u] = xv[start + (r + u) * 32 + a];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += op(t[u]);
+    }
+    for (; r < nrows; ++r) acc += op(xv[start + r * 32 + a]);
     return acc;
 }
 
@@ -309,6 +318,7 @@ __device__ float seq_rows(const Op& op, const float* __restrict__ xv, int64_t st
 // then the ILP/lane/tail combination of ATen row_sum / vectorized_inner_sum, then the
 // chunk results in chunk order (torch parallel_reduce).
 // =====================================================================================
+constexpr int kFinStage = 256;      // level-1 block sums staged in LDS at a time (32 KB)
 template <class Op>
 __global__ void __launch_bounds__(64)
 l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
@@ -324,6 +334,8 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
     const int lane = threadIdx.x;
     const float* xv = x + vec * d;
     __shared__ float fin[32];
+    __shared__ __attribute__((aligned(16))) float s_stage[kFinStage * 32];
+    __shared__ float s_tail[64];
     float total = 0.f;
     for (int c = 0; c < plan.nchunks; ++c) {
         const int64_t off = plan.off[c];
@@ -343,32 +355,57 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
             const int64_t nleaf = rows / step;
             const int64_t ng1 = plan.ng1[c];
             const int64_t ng2 = ng1 / step;
-            if (lane < 32) {
-                const float* pp = part + (vec * plan.total_groups + plan.gbase[c]) * 32 + lane;
-                float acc3 = 0.f;
-                for (int64_t h = 0; h < ng2; ++h) {
-                    float b2 = 0.f;
-                    for (int64_t k = 0; k < step; ++k) b2 += pp[(h * step + k) * 32];
-                    acc3 += b2;
+            // level-2/3 over the ng1 block sums in order: groups [h*step, (h+1)*step) for
+            // h < ng2 into b2 then acc3, the rest into acc2.  The block sums are staged
+            // through LDS by the whole wave (coalesced, all loads in flight), so the
+            // sequential adds read LDS instead of one dependent global load each.
+            const float* pc = part + (vec * plan.total_groups + plan.gbase[c]) * 32;
+            float acc3 = 0.f, acc2 = 0.f, b2 = 0.f;
+            const int64_t n3 = ng2 * step;
+            for (int64_t k0 = 0; k0 < ng1; k0 += kFinStage) {
+                const int nk = (int)std::min<int64_t>(kFinStage, ng1 - k0);
+                __syncthreads();
+                const float4* src = reinterpret_cast<const float4*>(pc + k0 * 32);
+                float4* dst = reinterpret_cast<float4*>(s_stage);
+                for (int i = lane; i < nk * 8; i += 64) dst[i] = src[i];
+                __syncthreads();
+                if (lane < 32) {
+                    for (int kk = 0; kk < nk; ++kk) {
+                        const int64_t k = k0 + kk;
+                        const float v = s_stage[kk * 32 + lane];
+                        if (k < n3) {
+                            b2 += v;
+                            if ((k + 1) % step == 0) {
+                                acc3 += b2;
+                                b2 = 0.f;
+                            }
+                        } else {
+                            acc2 += v;
+                        }
+                    }
                 }
-                float acc2 = 0.f;
-                for (int64_t k = ng2 * step; k < ng1; ++k) acc2 += pp[k * 32];
+            }
+            if (lane < 32) {
                 float acc1 = 0.f;
                 for (int64_t b = ng1 * step; b < nleaf; ++b)
                     acc1 += seq_rows(op, xv, off + b * step * 32, step, lane);
                 float acc0 = seq_rows(op, xv, off + nleaf * step * 32, rows - nleaf * step, lane);
                 fin[lane] = ((acc0 + acc1) + acc2) + acc3;
             }
+            // the < 40 elements after the 32-stream rows, one load per lane, into LDS
+            const int64_t t0 = rows * 32;
+            const int nt = (int)(s - t0);
+            if (lane < nt) s_tail[lane] = xv[off + t0 + lane];
             __syncthreads();
             if (lane == 0) {
                 float p0[8];
                 for (int l = 0; l < 8; ++l) p0[l] = fin[l];
                 for (int64_t v = rows * 4; v < vs; ++v)
-                    for (int l = 0; l < 8; ++l) p0[l] += op(xv[off + v * 8 + l]);
+                    for (int l = 0; l < 8; ++l) p0[l] += op(s_tail[v * 8 + l - t0]);
                 for (int k = 1; k < 4; ++k)
                     for (int l = 0; l < 8; ++l) p0[l] += fin[k * 8 + l];
                 float acc = 0.f;
-                for (int64_t k = vs * 8; k < s; ++k) acc += op(xv[off + k]);
+                for (int64_t k = vs * 8; k < s; ++k) acc += op(s_tail[k - t0]);
                 for (int l = 0; l < 8; ++l) acc += p0[l];
                 fin[0] = acc;
             }
@@ -1374,6 +1411,10 @@ tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
 
 constexpr int kFoldEvents = 256;   // record events prefetched into LDS (24 KB)
 
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
+    const uint32_t lo = __shfl_up((uint32_t)v, o, kWave), hi = __shfl_up((uint32_t)(v >> 32), o, kWave);
+    return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
@@ -1437,30 +1478,45 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
 #ifdef UQ_FOLD_PROF
         const uint64_t q0 = wall_clock64();
 #endif
-        // a run of regular maps; lane l holds the maps of tile blk + l, the next 64 are
-        // loaded while this block is walked, and the walk reads them with readlane
+        // a run of regular maps, 64 tiles at a time: lane l holds the map of tile blk + l
+        // (the next 64 are loaded meanwhile).  A map in units of G is P -> P + d[P & 1];
+        // two maps compose to the same form, (F then g).d[p] = F.d[p] + g.d[p ^ (F.d[p] & 1)],
+        // so a wave scan gives every tile's exact start at once.  The run ends at the first
+        // irregular map or map of another binade (P stays in its binade along a run).
         const int lane = tid & (kWave - 1);
         bool go = true;
         int32_t blk = tile;
         uint64_t am = map0[base + min(blk + lane, tiles - 1)], bm = map1[base + min(blk + lane, tiles - 1)];
         while (go) {
             const int32_t nb = blk + kWave;
-            uint64_t pv = 0;                                   // lane u: P of tile blk + u
             const uint64_t an = map0[base + min(nb + lane, tiles - 1)], bn = map1[base + min(nb + lane, tiles - 1)];
-            for (int u = 0; u < kWave && go; ++u) {
-                const uint64_t au = readlane64(am, u), bu = readlane64(bm, u);
-                const uint64_t eb = au >> 53;                  // the map's binade (biased exponent)
-                if (tile >= tiles || au == kIrrMap || (Pb >> 52) != eb) {
-                    go = false;
-                } else {
-                    if (lane == u) pv = Pb;                        // stored per block below
-                    uint64_t Pi = (Pb & kMant) | (1ull << 52);     // P / G
-                    Pi += (Pi & 1ull) ? bu : (au & ((1ull << 53) - 1ull));
-                    Pb = (Pi & kMant) | (eb << 52);
-                    ++tile;
+            const uint64_t E0 = Pb >> 52;
+            const bool valid = blk + lane < tiles && am != kIrrMap && (am >> 53) == E0;
+            const uint64_t inv = __ballot(!valid);
+            const int f = inv ? (int)__builtin_ctzll(inv) : kWave;        // tiles in the run here
+            uint64_t d0 = lane < f ? (am & ((1ull << 53) - 1ull)) : 0ull, d1 = lane < f ? bm : 0ull;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {               // inclusive scan of the maps
+                const uint64_t f0 = shfl_up64(d0, o), f1 = shfl_up64(d1, o);
+                if (lane >= o) {
+                    const uint64_t n0 = f0 + ((f0 & 1ull) ? d1 : d0);
+                    const uint64_t n1 = f1 + ((f1 & 1ull) ? d0 : d1);
+                    d0 = n0;
+                    d1 = n1;
                 }
             }
-            if (tid < tile - blk) pre[base + blk + tid] = pv;  // wave 0, one coalesced store
+            const uint64_t Pi0 = (Pb & kMant) | (1ull << 52);   // P / G
+            const bool odd = (Pi0 & 1ull) != 0ull;
+            uint64_t e0 = shfl_up64(d0, 1), e1 = shfl_up64(d1, 1);
+            if (lane == 0) e0 = e1 = 0ull;
+            const uint64_t st = Pi0 + (odd ? e1 : e0);            // exact start of tile blk + lane
+            if (tid < f) pre[base + blk + tid] = (st & kMant) | (E0 << 52);   // wave 0, coalesced
+            if (f > 0) {
+                const uint64_t inc = odd ? readlane64(d1, f - 1) : readlane64(d0, f - 1);
+                Pb = ((Pi0 + inc) & kMant) | (E0 << 52);
+            }
+            tile += f;
+            go = f == kWave;
             blk = nb;
             am = an;
             bm = bn;
