@@ -318,9 +318,16 @@ __device__ float seq_rows(const Op& op, const float* __restrict__ xv, int64_t st
 // then the ILP/lane/tail combination of ATen row_sum / vectorized_inner_sum, then the
 // chunk results in chunk order (torch parallel_reduce).
 // =====================================================================================
-constexpr int kFinStage = 256;      // level-1 block sums staged in LDS at a time (32 KB)
+constexpr int kFinStage = 64;       // level-1 block sums staged in LDS per wave at a time (8 KB)
+constexpr int kFinWaves = 8;        // chunks are finished by different waves, summed in order
+// LDS written and read back by lanes of the same wave: a wave-level barrier suffices.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 template <class Op>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64 * kFinWaves)
 l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
                    const float* __restrict__ part, float* __restrict__ l1_out,
                    const float* __restrict__ l1, float fm, uint32_t* __restrict__ hist_g,
@@ -331,13 +338,16 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
         op.h = hist_g + (size_t)vec * 3 * 2048;
         op.zn = zn_g + vec * 2;
     }
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const float* xv = x + vec * d;
-    __shared__ float fin[32];
-    __shared__ __attribute__((aligned(16))) float s_stage[kFinStage * 32];
-    __shared__ float s_tail[64];
-    float total = 0.f;
-    for (int c = 0; c < plan.nchunks; ++c) {
+    __shared__ float fin_w[kFinWaves][32];
+    __shared__ __attribute__((aligned(16))) float s_stage_w[kFinWaves][kFinStage * 32];
+    __shared__ float s_tail_w[kFinWaves][64];
+    __shared__ float s_chunk[64];
+    float* fin = fin_w[wv];
+    float* s_stage = s_stage_w[wv];
+    float* s_tail = s_tail_w[wv];
+    for (int c = wv; c < plan.nchunks; c += kFinWaves) {
         const int64_t off = plan.off[c];
         const int64_t s = plan.size[c];
         float chunk_sum;
@@ -364,11 +374,11 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
             const int64_t n3 = ng2 * step;
             for (int64_t k0 = 0; k0 < ng1; k0 += kFinStage) {
                 const int nk = (int)std::min<int64_t>(kFinStage, ng1 - k0);
-                __syncthreads();
+                wave_sync();
                 const float4* src = reinterpret_cast<const float4*>(pc + k0 * 32);
                 float4* dst = reinterpret_cast<float4*>(s_stage);
                 for (int i = lane; i < nk * 8; i += 64) dst[i] = src[i];
-                __syncthreads();
+                wave_sync();
                 if (lane < 32) {
                     for (int kk = 0; kk < nk; ++kk) {
                         const int64_t k = k0 + kk;
@@ -396,7 +406,7 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
             const int64_t t0 = rows * 32;
             const int nt = (int)(s - t0);
             if (lane < nt) s_tail[lane] = xv[off + t0 + lane];
-            __syncthreads();
+            wave_sync();
             if (lane == 0) {
                 float p0[8];
                 for (int l = 0; l < 8; ++l) p0[l] = fin[l];
@@ -409,13 +419,18 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
                 for (int l = 0; l < 8; ++l) acc += p0[l];
                 fin[0] = acc;
             }
-            __syncthreads();
+            wave_sync();
             chunk_sum = fin[0];
-            __syncthreads();
+            wave_sync();
         }
-        total += chunk_sum;
+        if (lane == 0) s_chunk[c] = chunk_sum;
     }
-    if (lane == 0) l1_out[vec] = total;
+    __syncthreads();
+    if (threadIdx.x == 0) {             // chunk results in chunk order (torch parallel_reduce)
+        float total = 0.f;
+        for (int c = 0; c < plan.nchunks; ++c) total += s_chunk[c];
+        l1_out[vec] = total;
+    }
 }
 
 // =====================================================================================
@@ -1914,7 +1929,7 @@ int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, flo
         int rc = hip_check(hipGetLastError(), "l1_partial_kernel launch");
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(l1_finalize_kernel<Op>, dim3((unsigned)n), dim3(64), 0, st, x, d, plan, part, sum_out, l1, fm,
+    hipLaunchKernelGGL(l1_finalize_kernel<Op>, dim3((unsigned)n), dim3(64 * kFinWaves), 0, st, x, d, plan, part, sum_out, l1, fm,
                        hist, zn);
     return hip_check(hipGetLastError(), "l1_finalize_kernel launch");
 }
