@@ -459,14 +459,27 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
 // recomputed from their exact start) -> outputs from the exact P.  Every form gives
 // the sequential cumsum's bits, hence the same bits.
 // =====================================================================================
-__device__ __forceinline__ double wave_incl_scan(double v, int lane) {
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const double t = __shfl_up(v, o, kWave);
-        if (lane >= o) v = t + v;
-    }
+// 64-bit DPP move (two 32-bit halves); lanes without a source (or outside ROWMASK) read 0.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_d(double v) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)u, CTRL, ROWMASK, 0xF, true);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(u >> 32), CTRL, ROWMASK, 0xF, true);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// Inclusive wave scan by DPP (row_shr 1/2/4/8, then row_bcast 15/31): no LDS round trips.
+// Only used on sums that are exact in any order (multiples of one G below 2^E).
+__device__ __forceinline__ double wave_incl_scan(double v, int) {
+    v = v + dpp_d<0x111, 0xF>(v);                  // row_shr:1
+    v = v + dpp_d<0x112, 0xF>(v);                  // row_shr:2
+    v = v + dpp_d<0x114, 0xF>(v);                  // row_shr:4
+    v = v + dpp_d<0x118, 0xF>(v);                  // row_shr:8
+    v = v + dpp_d<0x142, 0xA>(v);                  // row_bcast:15 -> rows 1, 3
+    v = v + dpp_d<0x143, 0xC>(v);                  // row_bcast:31 -> rows 2, 3
     return v;
 }
+// value of the previous lane (0 in lane 0): wave_shr:1
+__device__ __forceinline__ double wave_prev(double v) { return dpp_d<0x138, 0xF>(v); }
 
 // Chain bases of the binade holding s: b0 = 2^E, b1 = 2^E + G (odd: lowest mantissa bit
 // set), top = 2^(E+1).  Below 32 (and for NaN / huge s) the E = 5 bases: such tiles and
@@ -704,8 +717,7 @@ __device__ __forceinline__ void tile_pass1(const float* s_x, TileVals& tv, ScanL
     st.t0 = c0 - B.b0;                          // exact (Sterbenz)
     st.t1 = TIES ? c1 - B.b1 : st.t0;
     const double incl_w = wave_incl_scan(st.t0, lane);
-    double wexcl = __shfl_up(incl_w, 1, kWave);
-    if (lane == 0) wexcl = 0.0;
+    const double wexcl = wave_prev(incl_w);
     if (lane == kWave - 1) sl.wave[wid] = incl_w;
     if (TIES) {
         // parity transfer (regular tiles): a start of parity 0 ends on parity e0 = par(t0),
