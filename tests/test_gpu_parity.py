@@ -243,6 +243,25 @@ def test_single_row_ragged_d_vector_path_and_many_threads(uq):
             assert G.bits_equal(q, exp), (d, T, G.n_mismatch(q, exp))
 
 
+def test_l1_many_chunks_over_finalize_waves(uq):
+    """K1b finishes torch chunks on 8 waves (chunk c on wave c % 8) and adds the chunk
+    results in chunk order: more than 8 chunks (16, 33) and ragged chunk sizes must keep the
+    torch CPU cascade bits (ATen: min(T, ceil(d / 32768)) chunks)."""
+    rng = np.random.default_rng(78)
+    d = (1 << 20) + 5
+    x = rng.standard_normal((2, d)).astype(f32)
+    m = O.rate_to_m(1, d)
+    X = np.array([0.61, 0.05], f32)
+    for T in (16, 37):
+        q = uq.quantize_dequantize(dev(x), m=m, X=X, torch_threads=T).cpu().numpy()
+        exp = C.quantize_batch(x, m, X, T)[0]
+        assert G.bits_equal(q, exp), (T, G.n_mismatch(q, exp))
+    # the biased quantizer's m' (k' summed by the same cascade, with its radix histogram)
+    qb = uq.biased_quantize(dev(x[:1]), m=m, torch_threads=16, ties="torch").cpu().numpy()[0]
+    eb, *_ = C.biased_quantize(x[0], m, 16, 0)
+    assert G.bits_equal(qb, eb), G.n_mismatch(qb, eb)
+
+
 def _division_guard_batch(n, d, rng):
     """Rows that drive every branch of the kernels' x / den (div_plan / div4): ordinary
     rows (fast path), rows with tiny, subnormal, huge and non-finite elements (per-element
