@@ -147,10 +147,9 @@ __device__ __forceinline__ void div4(const float (&xs)[4], const DivPlan& dp, fl
             vs[2 * h] = q.x;
             vs[2 * h + 1] = q.y;
         }
-        bool bad = false;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) bad |= !(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f;
-        if (__builtin_expect(bad, 0)) {
+        // one test per four: the smallest |q| (q is finite here: den >= |x| and finite)
+        const float mn = fminf(fminf(fabsf(vs[0]), fabsf(vs[1])), fminf(fabsf(vs[2]), fabsf(vs[3])));
+        if (__builtin_expect(!(mn >= dp.thr), 0)) {
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 if (!(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f) vs[c] = xs[c] / dp.den;
