@@ -607,6 +607,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
     return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 constexpr int kAuxNT = 2;
+#ifndef UQ_CODES_AUX
+#define UQ_CODES_AUX kAuxNT    // cache policy of the code stores (timing ablation switch)
+#endif
 
 __device__ __forceinline__ void load_tile_buf(TileRegs& r, __amdgpu_buffer_rsrc_t rx, uint32_t t0_bytes, int tid) {
 #pragma unroll
@@ -1137,7 +1140,7 @@ __device__ __forceinline__ void store_codes_buf(__amdgpu_buffer_rsrc_t rc, int8_
                                                 const uint32_t (&cw)[4], uint32_t t0, int64_t d, int tid) {
     if (CVEC) {
         const u32x4v v = {cw[0], cw[1], cw[2], cw[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rc, t0 + (uint32_t)(tid * kQItems), 0, kAuxNT);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rc, t0 + (uint32_t)(tid * kQItems), 0, UQ_CODES_AUX);
     } else {
         const int64_t rem = d - (int64_t)t0;
         store_codes<false>(crow + t0, cw, (int)(rem < kQTile ? rem : kQTile), tid);
