@@ -245,8 +245,41 @@ rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist, 
 }
 
 // KB4c: compact the keys of the chosen first-digit bucket (compact-mode clients).  Each
-// thread keeps its 64 keys in registers (16 float4 loads, coalesced), counts the matches,
-// one block scan + one atomic per workgroup reserves the output range.
+// thread keeps its 64 keys in registers (16 float4 loads, coalesced, non-temporal), counts
+// the matches; one block scan + one atomic per workgroup reserves the output range.  The
+// matches are staged in LDS (branch-free: a non-match goes to the thread's junk slot) and
+// copied out coalesced; a workgroup with more than kCompactStage matches (tie-heavy data)
+// writes them straight from registers.
+constexpr int kCompactStage = 4096;
+template <bool CHECK>
+__device__ __forceinline__ uint64_t compact_keys(const float* __restrict__ xv, int64_t d, int64_t b0, int tid,
+                                                 const DivPlan& dp, float fm, bool up, uint32_t prefix,
+                                                 uint32_t (&key)[kHistItems]) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    uint64_t match = 0;
+#pragma unroll
+    for (int j = 0; j < kHistItems / 4; ++j) {
+        const int64_t i = b0 + 4 * ((int64_t)j * 256 + tid);          // elements i .. i+3
+        float v[4];
+        if (!CHECK) {
+            const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(xv + i));
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = (i + c < d) ? xv[i + c] : 0.f;
+        }
+        float kp[4];
+        uint32_t k4[4];
+        rez_elem4(v, dp, fm, up, kp, k4);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            key[4 * j + c] = k4[c];
+            if ((!CHECK || i + c < d) && (k4[c] & 0xFFE00000u) == prefix) match |= 1ull << (4 * j + c);
+        }
+    }
+    return match;
+}
+
 template <bool VEC4>
 __global__ void __launch_bounds__(256)
 rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
@@ -262,38 +295,34 @@ rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restri
     const int64_t b0 = (int64_t)blockIdx.x * kHistSpan;
     __shared__ uint32_t lds[4];
     __shared__ uint32_t s_base;
+    __shared__ uint32_t s_cand[kCompactStage + 256];             // staged matches + junk slots
     uint32_t key[kHistItems];
-    uint64_t match = 0;
-#pragma unroll
-    for (int j = 0; j < kHistItems / 4; ++j) {
-        const int64_t i = b0 + 4 * ((int64_t)j * 256 + tid);          // elements i .. i+3
-        float v[4];
-        if (VEC4 && i + 3 < d) {
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(xv + i));
-            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-        } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) v[c] = (i + c < d) ? xv[i + c] : 0.f;
-        }
-        float kp[4];
-        uint32_t k4[4];
-        rez_elem4(v, dp, fm, up, kp, k4);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            key[4 * j + c] = k4[c];
-            if (i + c < d && (k4[c] & 0xFFE00000u) == prefix) match |= 1ull << (4 * j + c);
-        }
-    }
+    const uint64_t match = (VEC4 && b0 + kHistSpan <= d)
+                               ? compact_keys<false>(xv, d, b0, tid, dp, fm, up, prefix, key)
+                               : compact_keys<true>(xv, d, b0, tid, dp, fm, up, prefix, key);
     uint32_t tot;
     uint32_t off = block_excl_scan_u32((uint32_t)__popcll(match), lds, &tot);
     if (tid == 0) s_base = tot ? atomicAdd(&cand_n[vec], tot) : 0u;
-    __syncthreads();
-    off += s_base;
     uint32_t* cv = cand + (size_t)vec * cap;
+    if (tot <= (uint32_t)kCompactStage) {                        // block-uniform
+        const uint32_t junk = kCompactStage + tid;
 #pragma unroll
-    for (int e = 0; e < kHistItems; ++e)
-        if (((match >> e) & 1ull) && off < cap) cv[off++] = key[e];
+        for (int e = 0; e < kHistItems; ++e) {
+            const uint32_t bit = (uint32_t)(match >> e) & 1u;
+            s_cand[bit ? off : junk] = key[e];
+            off += bit;
+        }
+        __syncthreads();
+        const uint32_t base = s_base;
+        for (uint32_t k = tid; k < tot; k += 256)
+            if (base + k < cap) cv[base + k] = s_cand[k];
+    } else {
+        __syncthreads();
+        off += s_base;
+#pragma unroll
+        for (int e = 0; e < kHistItems; ++e)
+            if (((match >> e) & 1ull) && off < cap) cv[off++] = key[e];
+    }
 }
 
 // KB4d: digits 2 and 3 on the candidates (one workgroup per compact-mode client).
