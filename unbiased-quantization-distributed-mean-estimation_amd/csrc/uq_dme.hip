@@ -610,6 +610,9 @@ constexpr int kAuxNT = 2;
 #ifndef UQ_CODES_AUX
 #define UQ_CODES_AUX kAuxNT    // cache policy of the code stores (timing ablation switch)
 #endif
+#ifndef UQ_Q_AUX
+#define UQ_Q_AUX kAuxNT        // cache policy of the q stores (timing ablation switch)
+#endif
 
 __device__ __forceinline__ void load_tile_buf(TileRegs& r, __amdgpu_buffer_rsrc_t rx, uint32_t t0_bytes, int tid) {
 #pragma unroll
@@ -627,7 +630,7 @@ __device__ __forceinline__ void store_tile_buf(const float* s_data, __amdgpu_buf
         const int q = tid + j * kQBlock;
         const float4 v = *reinterpret_cast<const float4*>(&s_data[swz(q >> 2, q & 3)]);
         const f32x4v w = {v.x, v.y, v.z, v.w};
-        __builtin_amdgcn_raw_buffer_store_b128(w, ro, t0_bytes + (uint32_t)q * 16u, 0, kAuxNT);
+        __builtin_amdgcn_raw_buffer_store_b128(w, ro, t0_bytes + (uint32_t)q * 16u, 0, UQ_Q_AUX);
     }
 }
 
@@ -1218,8 +1221,13 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         __syncthreads();                           // s_x(t) staged; s_o(t-1) complete
         if (tile > tb) {
             const uint32_t tp = (uint32_t)(tile - 1) * (uint32_t)kQTile;
+#ifdef UQ_CODES_FIRST           // timing ablation: code stores before the q stores
+            if (WC) store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
+            if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);
+#else
             if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);      // beyond d: dropped by the range check
             if (WC) store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
+#endif
         }
         if (tile + 1 < te) load_tile_buf(pre_x, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
         const int64_t t0 = (int64_t)tile * kQTile;
