@@ -344,7 +344,17 @@ rez_cand_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ c
         const int nb = (int)dmask + 1;
         for (int b = tid; b < kRadixBins; b += 256) h[b] = 0u;
         __syncthreads();
-        for (uint32_t i = tid; i < nc; i += 256) {
+        // 8 independent candidate loads in flight per thread, then their LDS atomics
+        uint32_t i = tid;
+        for (; i + 7 * 256 < nc; i += 8 * 256) {
+            uint32_t kk[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kk[u] = __builtin_nontemporal_load(cv + i + u * 256);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if ((kk[u] & hmask) == s.prefix) atomicAdd(&h[(kk[u] >> shift) & dmask], 1u);
+        }
+        for (; i < nc; i += 256) {
             const uint32_t key = cv[i];
             if ((key & hmask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
         }
