@@ -155,6 +155,17 @@ int uq_rht_signs(const int32_t* seeds, int64_t rows, int64_t D, int8_t* signs, v
  * bit-identical to the reference (f32 butterflies a + b, (a + b) - 2b; / f32(sqrt(D))). */
 int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inverse, const int8_t* signs,
                const int32_t* sign_row, void* ws, size_t ws_bytes, void* stream);
+/* uq_quicfl_prepare_f32: QuicFLReceiver.decompress (AS:526-532) up to its inverse RHT, for a
+ * batch: out [n][D] = (exact ? exact_vals : recv_table[X * h_len + h]) / scale[j], with
+ * h = torch.randint(0, h_len, (D,)) of a CPU generator seeded with prng_seeds[j] (MT19937
+ * word % h_len).  X [n][D] int32 in [0, table_rows); recv_table [table_rows][h_len] f32
+ * (<= 1024 entries: the reference tables <b>_X_<s>_h_256_q_recv_table.pt); exact_mask u8 [n][D] and
+ * exact_vals f32 [n][D] (dense) or both NULL; scale [n] f32.  The inverse RHT is uq_rht_f32
+ * (inverse = 1).  The sender (AS:429-505) is not provided: its tables are not in the
+ * reference. */
+int uq_quicfl_prepare_f32(const int32_t* X, int64_t n, int64_t D, const float* recv_table, int32_t table_rows,
+                          int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask, const float* exact_vals,
+                          const float* scale, float* out, void* stream);
 int uq_eden_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out);
 int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
                          const int32_t* sign_row, uint8_t* bins, float* scale, void* ws, size_t ws_bytes,

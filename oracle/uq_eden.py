@@ -161,3 +161,18 @@ def eden_quantize(x: np.ndarray, nbits: int, seed: int) -> np.ndarray:
     x = np.asarray(x, f32)
     bins, scale, _, _ = eden_compress(x, nbits, seed)
     return eden_decompress(bins, scale, nbits, seed, x.shape[0])
+
+
+def quicfl_decompress(X: np.ndarray, recv_table: np.ndarray, h_len: int, prng_seed: int, exact_mask, exact_values,
+                      scale, rotation_seed: int, dim: int) -> np.ndarray:
+    """QuicFLReceiver.decompress (AS:526-535): h = torch.randint(0, h_len, (D,)) from a CPU
+    generator seeded with prng_seed (= MT19937 word % h_len), v = recv_table.take(X * h_len + h),
+    exact coordinates overwritten in index order, v / scale (f32), inverse RHT, [:dim]."""
+    X = np.asarray(X, np.int64).reshape(-1)
+    h = (mt19937(int(prng_seed), X.size) % np.uint32(h_len)).astype(np.int64)
+    v = np.asarray(recv_table, f32).reshape(-1)[X * h_len + h].copy()
+    if exact_mask is not None:
+        m = np.asarray(exact_mask, bool).reshape(-1)
+        v[m] = np.asarray(exact_values, f32).reshape(-1)
+    v = (v / f32(scale)).astype(f32)
+    return inverse_rht(v, rotation_seed)[:dim]

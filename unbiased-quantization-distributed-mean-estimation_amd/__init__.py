@@ -16,11 +16,13 @@ from .codes import TypeCodes
 from .biased import Type_biased_quantize, biased_quantize
 from .eden import (EDEN_quantize_Hadamard, eden_quantize, eden_compress, eden_decompress, EdenMessage, rht_signs,
                    randomized_hadamard_transform, randomized_inverse_hadamard_transform)
+from .quicfl import QuicFLReceiver, quicfl_decompress
 from ._lib import UQError, load as load_library, library_path
 from .distributed import shard_range, sharded_client_mean, sharded_quantize_mean
 from .dme import DISTRIBUTIONS, nmse_simulation
 
 __all__ = [
+    "QuicFLReceiver", "quicfl_decompress",
     "RATE_TABLE", "rate_to_m", "Type_unbiased_quantize", "quantize_dequantize", "client_mean",
     "quantize_mean", "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
     "check_status", "UQError", "load_library", "library_path", "shard_range", "sharded_client_mean",

@@ -36,6 +36,7 @@ SIGNATURES = {
     "uq_type_biased_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _sz, _p]),
     "uq_rht_signs": (ctypes.c_int, [_p, _i64, _i64, _p, _p]),
     "uq_rht_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _sz, _p]),
+    "uq_quicfl_prepare_f32": (ctypes.c_int, [_p, _i64, _i64, _p, _i32, _i32, _p, _p, _p, _p, _p, _p]),
     "uq_eden_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
     "uq_eden_compress_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _sz, _p]),
     "uq_eden_decompress_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _sz, _p]),

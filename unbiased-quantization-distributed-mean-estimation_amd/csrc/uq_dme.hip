@@ -2585,6 +2585,21 @@ int uq_rht_signs(const int32_t* seeds, int64_t rows, int64_t D, int8_t* signs, v
     return hip_check(hipGetLastError(), "rht_signs_kernel launch");
 }
 
+int uq_quicfl_prepare_f32(const int32_t* X, int64_t n, int64_t D, const float* recv_table, int32_t table_rows,
+                          int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask, const float* exact_vals,
+                          const float* scale, float* out, void* stream) {
+    if (n < 0 || D < 0) return fail(UQ_E_INVALID, "n and D must be >= 0");
+    if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 clients per call");
+    if (n == 0 || D == 0) return UQ_OK;
+    if (!X || !recv_table || !prng_seeds || !scale || !out) return fail(UQ_E_INVALID, "null pointer");
+    if ((exact_mask == nullptr) != (exact_vals == nullptr)) return fail(UQ_E_INVALID, "exact_mask and exact_vals go together");
+    if (h_len < 1 || table_rows < 1 || (int64_t)h_len * table_rows > kQflTab)
+        return fail(UQ_E_INVALID, "receiver table must hold 1..1024 entries");
+    hipLaunchKernelGGL(quicfl_prepare_kernel, dim3((unsigned)n), dim3(640), 0, (hipStream_t)stream, X, D, recv_table,
+                       table_rows * h_len, h_len, prng_seeds, exact_mask, exact_vals, scale, out);
+    return hip_check(hipGetLastError(), "quicfl_prepare_kernel launch");
+}
+
 int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inverse, const int8_t* signs,
                const int32_t* sign_row, void* ws, size_t ws_bytes, void* stream) {
     if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
