@@ -14,6 +14,7 @@
  *   NMSE_Results/Codes/Normal_dist.py:137-138  est += q / n
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -82,37 +83,36 @@ static float chunk_sum(const float* x, int64_t s) {
     return acc;
 }
 
-/* torch CPU f32 `sum` of a contiguous vector for `torch_threads` intra-op threads. */
+/* torch CPU f32 `sum` of a contiguous vector for `torch_threads` intra-op threads
+ * (ATen TensorIteratorBase::parallel_reduce).  d < GRAIN or T == 1: one cascade.
+ * Otherwise two_pass_reduction: nt = min(T, ceil(d/GRAIN)) chunks of ceil(d/nt)
+ * (invoke_parallel), thread t adds its chunk's cascade sum into buffer[t] of a T-element
+ * zero buffer, and the result is 0 + the cascade sum of that buffer (checked against
+ * torch 2.10 for T = 1..39, 47, 63..65, 96, 128, 200, 256; the chunk sums are NOT added
+ * sequentially unless T is 1, 2, 3, 4 or 8). */
 float uqo_torch_sum(const float* v, int64_t d, int torch_threads) {
     if (d <= 0) return 0.0f;
     int T = torch_threads < 1 ? 1 : torch_threads;
-    if (d < TORCH_GRAIN || T == 1) return chunk_sum(v, d);
+    if (d < TORCH_GRAIN || T == 1) return 0.0f + chunk_sum(v, d);
     int64_t nt = (d + TORCH_GRAIN - 1) / TORCH_GRAIN;
     if (nt > T) nt = T;
     int64_t cs = (d + nt - 1) / nt;
-    float acc = 0.0f;
+    float* buf = (float*)calloc((size_t)T, sizeof(float));
+    if (!buf) return NAN;
     for (int64_t c = 0; c < nt; ++c) {
         int64_t b = c * cs, e = b + cs < d ? b + cs : d;
-        if (e > b) acc += chunk_sum(v + b, e - b);
+        if (e > b) buf[c] = 0.0f + chunk_sum(v + b, e - b);
     }
-    return acc;
+    float r = 0.0f + chunk_sum(buf, T);
+    free(buf);
+    return r;
 }
 
 /* |x| into scratch, then torch's chunking by intra-op thread count. */
 float uqo_l1_torch_order(const float* x, int64_t d, int torch_threads, float* scratch) {
     if (d <= 0) return 0.0f;
     for (int64_t i = 0; i < d; ++i) scratch[i] = fabsf(x[i]);
-    int T = torch_threads < 1 ? 1 : torch_threads;
-    if (d < TORCH_GRAIN || T == 1) return chunk_sum(scratch, d);
-    int64_t nt = (d + TORCH_GRAIN - 1) / TORCH_GRAIN;
-    if (nt > T) nt = T;
-    int64_t cs = (d + nt - 1) / nt;
-    float acc = 0.0f;
-    for (int64_t c = 0; c < nt; ++c) {
-        int64_t b = c * cs, e = b + cs < d ? b + cs : d;
-        if (e > b) acc += chunk_sum(scratch + b, e - b);
-    }
-    return acc;
+    return uqo_torch_sum(scratch, d, torch_threads);
 }
 
 static inline float torch_sign(float v) {
@@ -152,6 +152,26 @@ void uqo_quantize_batch(const float* x, float* out, int64_t n, int64_t d, int64_
         float L = uqo_quantize(x + j * d, out + j * d, d, m, X[j], torch_threads, 0, 0.0f, scratch);
         if (l1_out) l1_out[j] = L;
     }
+}
+
+/* The same batch with clients spread over `nthreads` OpenMP threads (each client is
+ * independent, AS:609-641): the all-cores CPU baseline.  Returns the threads used. */
+int uqo_quantize_batch_mt(const float* x, float* out, int64_t n, int64_t d, int64_t m,
+                          const float* X, int torch_threads, float* l1_out, int nthreads) {
+    int used = 1;
+#pragma omp parallel num_threads(nthreads)
+    {
+#pragma omp single
+        used = omp_get_num_threads();
+        float* scratch = (float*)malloc((size_t)(d > 0 ? d : 1) * sizeof(float));
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t j = 0; j < n; ++j) {
+            float L = uqo_quantize(x + j * d, out + j * d, d, m, X[j], torch_threads, 0, 0.0f, scratch);
+            if (l1_out) l1_out[j] = L;
+        }
+        free(scratch);
+    }
+    return used;
 }
 
 /* Normal_dist.py:137 — est += q / n, client order, f32. */

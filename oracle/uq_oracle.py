@@ -135,22 +135,32 @@ def _chunk_sum(x: np.ndarray) -> f32:
 def l1_torch_order(x: np.ndarray, torch_threads: int = 1) -> f32:
     """AS:624 `input_vector.abs().sum()` with torch CPU's exact f32 summation order.
 
-    With T intra-op threads and d >= GRAIN the vector is split into
-    nt = min(T, ceil(d/GRAIN)) chunks of ceil(d/nt); chunk sums are added in
-    chunk order onto 0."""
-    a = np.abs(np.asarray(x, dtype=f32))
+    With T intra-op threads and d >= GRAIN, ATen's two_pass_reduction
+    (TensorIteratorBase::parallel_reduce) splits the vector into
+    nt = min(T, ceil(d/GRAIN)) chunks of ceil(d/nt); thread t adds its chunk's sum
+    into buffer[t] of a T-element zero buffer, and the result is 0 + the same cascade
+    sum over that buffer.  Checked against torch 2.10 for T = 1..39, 47, 63..65, 96,
+    128, 200, 256 at five sizes (tests/golden/l1_threads.json); the chunk sums are not
+    added sequentially unless T is 1, 2, 3, 4 or 8."""
+    return torch_sum(np.abs(np.asarray(x, dtype=f32)), torch_threads)
+
+
+def torch_sum(a: np.ndarray, torch_threads: int = 1) -> f32:
+    """torch CPU f32 `Tensor.sum()` of a contiguous vector (see l1_torch_order)."""
+    a = np.asarray(a, dtype=f32)
     d = a.shape[0]
     if d == 0:
         return f32(0)
     T = max(1, int(torch_threads))
     if d < TORCH_GRAIN or T == 1:
-        return _chunk_sum(a)
+        return f32(f32(0) + _chunk_sum(a))
     nt = min(T, -(-d // TORCH_GRAIN))
     cs = -(-d // nt)
-    acc = f32(0)
+    buf = np.zeros(T, f32)
     for c in range(nt):
-        acc = f32(acc + _chunk_sum(a[c * cs:(c + 1) * cs]))
-    return acc
+        if c * cs < d:
+            buf[c] = f32(f32(0) + _chunk_sum(a[c * cs:(c + 1) * cs]))
+    return f32(f32(0) + _chunk_sum(buf))
 
 
 def fractional_parts(x: np.ndarray, m: int, l1: f32):

@@ -31,6 +31,8 @@ def lib():
         L.uqo_quantize.argtypes = [p, p, i64, i64, f, ctypes.c_int, ctypes.c_int, f, p]
         L.uqo_quantize_batch.restype = None
         L.uqo_quantize_batch.argtypes = [p, p, i64, i64, i64, p, ctypes.c_int, p, p]
+        L.uqo_quantize_batch_mt.restype = ctypes.c_int
+        L.uqo_quantize_batch_mt.argtypes = [p, p, i64, i64, i64, p, ctypes.c_int, p, ctypes.c_int]
         L.uqo_client_mean.restype = None
         L.uqo_client_mean.argtypes = [p, i64, i64, f, p]
         L.uqo_torch_sum.restype = f
@@ -60,6 +62,17 @@ def quantize_batch(x2d, m: int, X, torch_threads: int = 1):
     scratch = np.empty(max(1, d), np.float32)
     lib().uqo_quantize_batch(_ptr(x2d), _ptr(out), n, d, m, _ptr(X), torch_threads, _ptr(l1), _ptr(scratch))
     return out, l1
+
+
+def quantize_batch_mt(x2d, m: int, X, torch_threads: int = 1, nthreads: int = 1):
+    """quantize_batch with clients spread over OpenMP threads; returns (out, l1, threads used)."""
+    x2d = np.ascontiguousarray(x2d, dtype=np.float32)
+    n, d = x2d.shape
+    X = np.ascontiguousarray(X, dtype=np.float32).reshape(n)
+    out = np.empty_like(x2d)
+    l1 = np.empty(n, np.float32)
+    used = lib().uqo_quantize_batch_mt(_ptr(x2d), _ptr(out), n, d, m, _ptr(X), torch_threads, _ptr(l1), nthreads)
+    return out, l1, int(used)
 
 
 def quantize_with_l1(x, m: int, X: float, l1: float):

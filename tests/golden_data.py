@@ -111,3 +111,16 @@ def eden():
 def eden_input(case, z):
     i = case["idx"]
     return z[f"x{i}"] if f"x{i}" in z.files else spec_gen(case)
+
+
+def l1_threads():
+    """torch's AS:624 L1 at many intra-op thread counts (make_golden_threads.py).
+    Yields (record, x)."""
+    recs = json.load(open(os.path.join(GOLDEN, "l1_threads.json")))["records"]
+    cache = {}
+    for r in recs:
+        key = (r["seed"], r["d"], r["scale"])
+        if key not in cache:
+            cache.clear()
+            cache[key] = (np.random.default_rng(r["seed"]).standard_normal(r["d"]) * r["scale"]).astype(f32)
+        yield r, cache[key]

@@ -65,11 +65,13 @@ def test_workspace_and_argument_errors(lib):
     assert lib.uq_type_unbiased_f32(ctypes.c_void_p(16), ctypes.c_void_p(16), 4, 100, -5, ctypes.c_void_p(16),
                                     None, None, 1, ctypes.c_void_p(16), 1 << 30, None) == -1
     assert lib.uq_l1_torch_order_f32(ctypes.c_void_p(16), 4, 100, 0, None, ctypes.c_void_p(16), 1 << 30, None) == -1
-    # any torch thread count: torch splits a sum into min(T, ceil(d/32768)) chunks, and only
-    # more than 64 chunks is unsupported
+    # any torch thread count up to 4096: torch splits a sum into min(T, ceil(d/32768))
+    # chunks summed through a T-element buffer
     assert lib.uq_workspace_bytes(4, 100, 128, ctypes.byref(b)) == 0
     assert lib.uq_workspace_bytes(4, 1 << 21, 128, ctypes.byref(b)) == 0          # 64 chunks
-    assert lib.uq_workspace_bytes(4, 1 << 23, 128, ctypes.byref(b)) == -1         # 128 chunks
+    assert lib.uq_workspace_bytes(4, 1 << 23, 128, ctypes.byref(b)) == 0          # 128 chunks
+    assert lib.uq_workspace_bytes(4, 1 << 23, 4096, ctypes.byref(b)) == 0         # 256 chunks
+    assert lib.uq_workspace_bytes(4, 1 << 23, 4097, ctypes.byref(b)) == -1        # beyond the plan
     assert lib.uq_client_mean_f32(None, 3, 10, 10, 3.0, 0, None, None) == -1
     assert lib.uq_client_mean_f32(ctypes.c_void_p(16), 3, 10, 9, 3.0, 0, ctypes.c_void_p(16), None) == -1
 

@@ -80,7 +80,7 @@ def test_spec_vectors_large_bit_exact(uq):
         assert G.sha(got) == sp["q_sha256"], (sp["dist"], sp["d"], sp["R"], sp["threads"])
 
 
-@pytest.mark.parametrize("T", [1, 2, 3, 8])
+@pytest.mark.parametrize("T", [1, 2, 3, 5, 7, 8, 16, 64, 65, 128, 256])
 def test_l1_torch_order_sweep(uq, T):
     rng = np.random.default_rng(100 + T)
     sizes = [1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 32, 33, 63, 64, 65, 511, 512, 513, 8191, 8192, 8193,
@@ -233,7 +233,7 @@ def test_client_mean_order_and_accumulate(uq):
 
 def test_single_row_ragged_d_vector_path_and_many_threads(uq):
     """n = 1 uses the vector loads for any d (the row is 16-byte aligned); the ragged end
-    must not read past d.  torch_threads > 64 is accepted while the chunk count is <= 64."""
+    must not read past d; any torch_threads (here up to 128) is accepted."""
     rng = np.random.default_rng(77)
     for d in (172554, 4097, 8195, 1 << 16 | 3):
         x = rng.standard_normal(d).astype(f32)
@@ -351,3 +351,57 @@ def test_stream_form_all_rates_and_ragged_rows(uq, R):
     assert G.n_mismatch(got, ref) == 0
     tc, q = uq.quantize_encode(dev(x), m=m, X=X, torch_threads=1, return_q=True)
     assert G.bits_equal(q.cpu().numpy(), ref)
+
+
+def test_l1_thread_counts_match_torch_fixture(uq):
+    """K1 at T = 1..256 torch threads against torch's own L1 bits (tests/golden/l1_threads.json):
+    the two-pass reduction's per-thread buffer is summed by the same cascade."""
+    by_vec = {}
+    for r, x in G.l1_threads():
+        key = (r["seed"], r["d"])
+        if key not in by_vec:
+            by_vec[key] = (dev(x).view(1, -1), [])
+        by_vec[key][1].append(r)
+    n = 0
+    for xd, recs in by_vec.values():
+        for r in recs:
+            got = uq.l1_torch_order(xd, r["threads"]).cpu().numpy()[0]
+            assert got.view(np.uint32) == np.uint32(r["l1_bits"]), (r["d"], r["threads"], got, r["l1"])
+            n += 1
+    assert n >= 140
+
+
+@pytest.mark.parametrize("T", [64, 65, 128, 256])
+def test_c4_size_many_torch_threads_bit_exact(uq, T):
+    """d = 2^22 (config C4) with as many torch threads as a many-core host gives: 128 chunks
+    at T >= 128.  Unbiased and biased quantizers bit-exact against the C oracle."""
+    rng = np.random.default_rng(T)
+    d = 1 << 22
+    x = rng.standard_normal((2, d)).astype(f32)
+    X = np.array([0.41, 0.93], f32)
+    m = O.rate_to_m(1, d)
+    q = uq.quantize_dequantize(dev(x), m=m, X=X, torch_threads=T).cpu().numpy()
+    ref, _ = C.quantize_batch(x, m, X, T)
+    assert G.n_mismatch(q, ref) == 0, T
+    qb = uq.biased_quantize(dev(x[:1]), m=m, torch_threads=T, ties="torch").cpu().numpy()[0]
+    eb, *_ = C.biased_quantize(x[0], m, T, 0)
+    assert G.bits_equal(qb, eb), G.n_mismatch(qb, eb)
+
+
+def test_drop_in_default_torch_threads_c4_size(uq):
+    """The drop-in with the host's default torch thread count (whatever this box gives,
+    often > 64 on a many-core host) at d = 2^22: same bits as the C oracle with that T."""
+    uq.set_torch_threads(None)
+    T = uq.get_torch_threads()
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal(1 << 22).astype(f32)
+    torch.manual_seed(123)
+    got = uq.Type_unbiased_quantize(x, 1).cpu().numpy()
+    torch.manual_seed(123)
+    X = torch.rand(1).item()
+    ref = C.quantize_batch(x[None], O.rate_to_m(1, x.shape[0]), np.array([X], f32), T)[0][0]
+    assert G.n_mismatch(got, ref) == 0, T
+    torch.manual_seed(123)
+    gb = uq.Type_biased_quantize(x, 1).cpu().numpy()
+    eb, *_ = C.biased_quantize(x, O.rate_to_m(1, x.shape[0]), T, 0)
+    assert G.bits_equal(gb, eb), (T, G.n_mismatch(gb, eb))

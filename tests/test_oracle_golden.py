@@ -142,3 +142,18 @@ def test_rate_table_matches_survey_m():
     assert O.rate_to_m(1, 172554) == 36931 and O.rate_to_m(2, 172554) == 110006
     with pytest.raises(KeyError):
         O.rate_to_m(3.3, 10)
+
+
+def test_l1_thread_counts_match_torch_fixture():
+    """AS:624 at T = 1..256 torch threads: torch reduces in two passes (per-thread chunk
+    sums into a T-element buffer, then the same cascade over the buffer), pinned by
+    tests/golden/l1_threads.json (torch's own results).  C oracle everywhere, the NumPy
+    restatement on the sizes it finishes quickly."""
+    n = 0
+    for r, x in G.l1_threads():
+        want = np.uint32(r["l1_bits"]).view(f32)
+        assert C.l1_torch_order(x, r["threads"]) == want, (r["d"], r["threads"])
+        if r["d"] <= 65537:
+            assert O.l1_torch_order(x, r["threads"]) == want, (r["d"], r["threads"])
+        n += 1
+    assert n >= 140

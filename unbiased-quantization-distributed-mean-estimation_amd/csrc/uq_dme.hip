@@ -29,7 +29,7 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kGrain = 32768;     // at::internal::GRAIN_SIZE (torch CPU intra-op split)
-constexpr int kMaxChunks = 64;    // torch_threads supported by the L1 plan
+constexpr int kMaxThreads = 4096; // torch_threads supported by the L1 plan (per-thread buffer in LDS)
 
 // ---- quantize tile geometry --------------------------------------------------------
 constexpr int kQBlock = 256;               // threads per workgroup (4 waves)
@@ -52,59 +52,79 @@ constexpr int64_t kMaxGridY = 65535;       // clients per launch of the per-tile
 // then               f32 l1[n]                  (computed norms)
 constexpr size_t kCtrlBytes = 256;
 
+// torch CPU `sum` of a contiguous f32 vector with T intra-op threads (ATen
+// TensorIteratorBase::parallel_reduce -> two_pass_reduction, SumKernel cascade_sum):
+//   d < GRAIN or T == 1: one cascade over the whole vector.
+//   else: nt = min(T, ceil(d/GRAIN)) chunks of cs = ceil(d/nt) (ATen invoke_parallel); thread
+//   t < nt sums chunk t into buffer[t] (buffer of T zeros), and the result is the SAME cascade
+//   sum over the T-element buffer -- not a sequential add of the chunk sums (verified against
+//   torch 2.10 for T = 1..39, 47, 63..65, 96, 128, 200, 256 at five sizes; T in {1,2,3,4,8}
+//   happen to coincide with sequential order).
+// Chunks are uniform except the last, so two geometries describe them all.
+struct ChunkGeo {
+    int64_t size;                    // chunk length
+    int32_t lp;                      // log2(step) of its cascade
+    int32_t ng1;                     // full level-1 groups in the chunk
+};
 struct L1Plan {
-    int32_t nchunks;
+    int32_t nchunks;                 // nt
+    int32_t nbuf;                    // T (length of the per-thread buffer), 1 in the one-chunk case
     int32_t total_groups;            // level-1 groups per vector, all chunks
-    int64_t off[kMaxChunks];         // chunk offset (elements)
-    int64_t size[kMaxChunks];        // chunk length
-    int32_t lp[kMaxChunks];          // log2(step)
-    int32_t ng1[kMaxChunks];         // full level-1 groups in chunk
-    int32_t gbase[kMaxChunks];       // first group index of chunk
+    int64_t cs;                      // chunk stride (size of every chunk but the last)
+    ChunkGeo full, last;             // chunks 0 .. nt-2, chunk nt-1
+    __host__ __device__ int64_t off(int c) const { return (int64_t)c * cs; }
+    __host__ __device__ const ChunkGeo& geo(int c) const { return c + 1 < nchunks ? full : last; }
+    __host__ __device__ int32_t gbase(int c) const { return c * full.ng1; }
+    __host__ __device__ int chunk_of_group(int32_t G) const {
+        const int32_t nfull = (nchunks - 1) * full.ng1;
+        return G < nfull ? G / full.ng1 : nchunks - 1;
+    }
 };
 
-inline int ceil_log2_i64(int64_t x) {
+__host__ __device__ inline int ceil_log2_i64(int64_t x) {
     if (x <= 1) return 0;
     int r = 0;
     uint64_t v = (uint64_t)(x - 1);
     while (v) { ++r; v >>= 1; }
     return r;
 }
+__device__ inline int ceil_log2_dev(int64_t x) { return ceil_log2_i64(x); }
 
-// Mirrors torch CPU: d < GRAIN or T == 1 -> one chunk; else nt = min(T, ceil(d/GRAIN))
-// chunks of ceil(d/nt), reduced independently and added in chunk order.
+bool chunk_geo(int64_t s, ChunkGeo* g) {
+    const int64_t rows = (s / 8) / 4;   // rows of 32 floats (8 lanes x 4 ILP)
+    int lp = ceil_log2_i64(rows) / 4;
+    if (lp < 4) lp = 4;
+    if (lp > 8) return false;
+    const int64_t step = (int64_t)1 << lp;
+    const int64_t ng1 = (rows / step) / step;
+    if (ng1 > (int64_t)1 << 28) return false;
+    g->size = s;
+    g->lp = lp;
+    g->ng1 = (int32_t)ng1;
+    return true;
+}
+
 bool make_plan(int64_t d, int32_t T, L1Plan* p) {
     std::memset(p, 0, sizeof(*p));
     if (T < 1) T = 1;
+    if (T > kMaxThreads) return false;
     int64_t nt = 1, cs = d;
     if (!(d < kGrain || T == 1)) {
         nt = (d + kGrain - 1) / kGrain;
         if (nt > T) nt = T;
         cs = (d + nt - 1) / nt;
+        nt = (d + cs - 1) / cs;        // chunks past d are empty (their buffer slots stay 0)
+        p->nbuf = T;
+    } else {
+        p->nbuf = 1;
     }
-    if (nt > kMaxChunks) return false;
-    int32_t g = 0, c = 0;
-    for (int64_t k = 0; k < nt; ++k) {
-        int64_t b = k * cs, e = b + cs < d ? b + cs : d;
-        if (e <= b) continue;
-        int64_t s = e - b;
-        p->off[c] = b;
-        p->size[c] = s;
-        int64_t rows = (s / 8) / 4;   // rows of 32 floats (8 lanes x 4 ILP)
-        int lp = ceil_log2_i64(rows) / 4;
-        if (lp < 4) lp = 4;
-        if (lp > 8) return false;
-        int64_t step = (int64_t)1 << lp;
-        int64_t nleaf = rows / step;
-        int64_t ng1 = nleaf / step;
-        if (ng1 > (int64_t)1 << 28) return false;
-        p->lp[c] = lp;
-        p->ng1[c] = (int32_t)ng1;
-        p->gbase[c] = g;
-        g += (int32_t)ng1;
-        ++c;
-    }
-    p->nchunks = c;
-    p->total_groups = g;
+    p->nchunks = (int32_t)nt;
+    p->cs = cs;
+    if (!chunk_geo(nt > 1 ? cs : d, &p->full)) return false;
+    if (!chunk_geo(d - (nt - 1) * cs, &p->last)) return false;
+    const int64_t g = (nt - 1) * (int64_t)p->full.ng1 + p->last.ng1;
+    if (g > (int64_t)1 << 30) return false;
+    p->total_groups = (int32_t)g;
     return true;
 }
 
@@ -246,15 +266,14 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
         op.zn = hs + 2048;
     }
     int32_t G = blockIdx.x;
-    int c = 0;
-    while (c + 1 < plan.nchunks && G >= plan.gbase[c + 1]) ++c;
-    const int32_t g = G - plan.gbase[c];
-    const int lp = plan.lp[c];
+    const int c = plan.chunk_of_group(G);
+    const int32_t g = G - plan.gbase(c);
+    const int lp = plan.geo(c).lp;
     const int step = 1 << lp;
     const int tid = threadIdx.x;
     const int nthreads = 8 * step;            // 8 quads x step leaves
     __shared__ float leaf[256 * 4];           // [leaf][32] (step <= 32 -> <= 1024 floats)
-    const float* base = x + vec * d + plan.off[c] + (int64_t)g * step * step * 32;
+    const float* base = x + vec * d + plan.off(c) + (int64_t)g * step * step * 32;
     if (tid < nthreads) {
         const int q = tid & 7;
         const int b = tid >> 3;
@@ -325,6 +344,58 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// Column k of ATen multi_row_sum over R rows of width W (row stride W), f32 accumulate
+// (the same level structure as the K1a/K1b cascade, walked by one lane).
+__device__ float cascade_col(const float* a, int64_t R, int W, int k) {
+    int lp = ceil_log2_dev(R) / 4;
+    if (lp < 4) lp = 4;
+    const int64_t step = (int64_t)1 << lp, mask = step - 1;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int64_t i = 0;
+    for (; i + step <= R;) {
+        for (int64_t j = 0; j < step; ++j, ++i) a0 += a[i * W + k];
+        a1 += a0; a0 = 0.f;
+        if ((i & (mask << lp)) != 0) continue;
+        a2 += a1; a1 = 0.f;
+        if ((i & (mask << (2 * lp))) != 0) continue;
+        a3 += a2; a2 = 0.f;
+    }
+    for (; i < R; ++i) a0 += a[i * W + k];
+    return ((a0 + a1) + a2) + a3;
+}
+// torch cascade_sum of a[0..s) (ATen vectorized_inner_sum for s >= 8, scalar row_sum below),
+// computed by the lanes of one wave; the result is valid in lane 0.  Used on the two-pass
+// reduction's per-thread buffer (s = T <= kMaxThreads, so it is cheap).
+__device__ float lds_torch_sum(const float* a, int s, int lane) {
+    if (s < 8) {
+        float p[4] = {0.f, 0.f, 0.f, 0.f};
+        if (s >= 4)
+            for (int k = 0; k < 4; ++k) p[k] = 0.f + a[k];
+        for (int k = (s >= 4 ? 4 : 0); k < s; ++k) p[0] += a[k];
+        return ((p[0] + p[1]) + p[2]) + p[3];
+    }
+    const int vs = s / 8, nilp = vs / 4;
+    const float col = (lane < 32 && nilp) ? cascade_col(a, nilp, 32, lane) : 0.f;
+    float p[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) p[j] = __shfl(col, j, kWave);
+    float p0[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) p0[l] = p[l];
+    for (int v = nilp * 4; v < vs; ++v)
+#pragma unroll
+        for (int l = 0; l < 8; ++l) p0[l] += a[v * 8 + l];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+#pragma unroll
+        for (int l = 0; l < 8; ++l) p0[l] += p[k * 8 + l];
+    float acc = 0.f;
+    for (int k = vs * 8; k < s; ++k) acc += a[k];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) acc += p0[l];
+    return acc;
+}
+
 template <class Op>
 __global__ void __launch_bounds__(64 * kFinWaves)
 l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
@@ -342,13 +413,15 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
     __shared__ float fin_w[kFinWaves][32];
     __shared__ __attribute__((aligned(16))) float s_stage_w[kFinWaves][kFinStage * 32];
     __shared__ float s_tail_w[kFinWaves][64];
-    __shared__ float s_chunk[64];
+    __shared__ float s_chunk[kMaxThreads];      // the per-thread buffer of the two-pass reduction
     float* fin = fin_w[wv];
     float* s_stage = s_stage_w[wv];
     float* s_tail = s_tail_w[wv];
+    for (int t = plan.nchunks + (int)threadIdx.x; t < plan.nbuf; t += 64 * kFinWaves) s_chunk[t] = 0.0f;
     for (int c = wv; c < plan.nchunks; c += kFinWaves) {
-        const int64_t off = plan.off[c];
-        const int64_t s = plan.size[c];
+        const int64_t off = plan.off(c);
+        const ChunkGeo& geo = plan.geo(c);
+        const int64_t s = geo.size;
         float chunk_sum;
         if (s < 8) {
             // ATen scalar row_sum (ILP 4, rows < step -> all rows land in acc0).
@@ -359,16 +432,16 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
             chunk_sum = ((p[0] + p[1]) + p[2]) + p[3];
         } else {
             const int64_t vs = s / 8, rows = vs / 4;
-            const int lp = plan.lp[c];
+            const int lp = geo.lp;
             const int64_t step = (int64_t)1 << lp;
             const int64_t nleaf = rows / step;
-            const int64_t ng1 = plan.ng1[c];
+            const int64_t ng1 = geo.ng1;
             const int64_t ng2 = ng1 / step;
             // level-2/3 over the ng1 block sums in order: groups [h*step, (h+1)*step) for
             // h < ng2 into b2 then acc3, the rest into acc2.  The block sums are staged
             // through LDS by the whole wave (coalesced, all loads in flight), so the
             // sequential adds read LDS instead of one dependent global load each.
-            const float* pc = part + (vec * plan.total_groups + plan.gbase[c]) * 32;
+            const float* pc = part + (vec * plan.total_groups + plan.gbase(c)) * 32;
             float acc3 = 0.f, acc2 = 0.f, b2 = 0.f;
             const int64_t n3 = ng2 * step;
             for (int64_t k0 = 0; k0 < ng1; k0 += kFinStage) {
@@ -422,13 +495,13 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
             chunk_sum = fin[0];
             wave_sync();
         }
-        if (lane == 0) s_chunk[c] = chunk_sum;
+        if (lane == 0) s_chunk[c] = 0.0f + chunk_sum;     // buffer[t] = 0 + (thread t's chunk)
     }
     __syncthreads();
-    if (threadIdx.x == 0) {             // chunk results in chunk order (torch parallel_reduce)
-        float total = 0.f;
-        for (int c = 0; c < plan.nchunks; ++c) total += s_chunk[c];
-        l1_out[vec] = total;
+    // second pass of the two-pass reduction: out = 0 + cascade sum of the T-element buffer
+    if (wv == 0) {
+        const float total = lds_torch_sum(s_chunk, plan.nbuf, lane);
+        if (lane == 0) l1_out[vec] = 0.0f + total;
     }
 }
 
@@ -1938,9 +2011,9 @@ int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, flo
                    const float* l1, float fm, hipStream_t st, uint32_t* hist = nullptr, uint32_t* zn = nullptr) {
     if (plan.total_groups > 0) {
         bool vec4 = aligned16(x) && (d % 4 == 0 || n == 1);
-        for (int c = 0; c < plan.nchunks; ++c) vec4 = vec4 && (plan.off[c] % 4 == 0);
-        int maxstep = 16;
-        for (int c = 0; c < plan.nchunks; ++c) maxstep = std::max(maxstep, 1 << plan.lp[c]);
+        vec4 = vec4 && (plan.nchunks == 1 || plan.cs % 4 == 0);
+        int maxstep = std::max(16, 1 << plan.last.lp);
+        if (plan.nchunks > 1) maxstep = std::max(maxstep, 1 << plan.full.lp);
         if (maxstep > 32) return fail(UQ_E_INVALID, "L1 cascade step > 32 unsupported (d too large)");
         dim3 grid(plan.total_groups, (unsigned)n);
         dim3 block(8 * maxstep);
@@ -1983,7 +2056,7 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
     if (n < 0 || d < 0) return fail(UQ_E_INVALID, "n and d must be >= 0");
     if (n > (int64_t)1 << 31 || d > (int64_t)1 << 40) return fail(UQ_E_INVALID, "n or d too large");
     if (T < 1) return fail(UQ_E_INVALID, "torch_threads must be >= 1");
-    if (!make_plan(d, T, plan)) return fail(UQ_E_INVALID, "more than 64 torch-order sum chunks (min(torch_threads, ceil(d/32768)) > 64) unsupported");
+    if (!make_plan(d, T, plan)) return fail(UQ_E_INVALID, "torch_threads > 4096 (or d too large) unsupported by the L1 plan");
     *w = layout(n, d, *plan);
     if ((int64_t)w->tiles * n > 0xFFFFFFFFll) return fail(UQ_E_INVALID, "batch too large for one call");
     if (n > 0 && d > 0) {
