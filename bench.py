@@ -16,10 +16,15 @@ Clients shard across GPUs with no data-path collective except that final reduce
 time, in M-vectors/s.
 
 Rank 0 prints ONE JSON line.  `roofline` is computed for K2 from HIP events recorded
-around its launches inside the timed region (algorithmic bytes = 9*d per vector: read x,
-write q, write codes; 8*d for --pipeline q, 5*d for encode).  W warmup steps run first.  `cpu_baseline` times the C restatement of the reference path (oracle/,
-the checker) on this host for a bounded sample of the same clients, and the same
-sample doubles as a bit-parity and NMSE check of the GPU output.
+around its launches inside the timed region.  Algorithmic bytes follow SURVEY.md §8(d):
+8*d per vector for quantize+dequantize (read x, write q); the int8 code stream K2 also
+writes (1*d) is implementation traffic, reported apart (`impl_bytes_per_launch`) and never
+counted as achieved bandwidth; --pipeline encode (no q) counts 4*d.  `roofline.step` prices
+the whole step the same way (8*d per vector / ms_per_step) and sets the PMC traffic of all
+the step's kernels against it.  W warmup steps run first.  `cpu_baseline` times the C
+restatement of the reference path (oracle/, the checker) on this host: the whole batch
+with clients over all the host's allotted cores (OpenMP) and a bounded single-thread
+sample; the batch doubles as a bit-parity and NMSE check of the GPU output.
 """
 from __future__ import annotations
 
@@ -52,7 +57,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--dist", choices=["normal", "laplace", "uniform"], default="normal",
                     help="client vectors: N(0,1) (C2), Laplace(1,2) as Laplace_dist.py:89 or U(-1,1) (C3 sweeps)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="budget of the single-thread CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/pmc_*.json)")
     ap.add_argument("--mean-mode", choices=["reduce", "ordered"], default="reduce",
@@ -101,8 +106,23 @@ def load_traffic(path, d, n, pipeline):
             continue
         if (j.get("d") == d and j.get("clients") == n and j.get("pipeline", "q") == pipeline
                 and "quantize_bytes_per_launch" in j):
-            return float(j["quantize_bytes_per_launch"]), os.path.relpath(p, ROOT)
-    return None, None
+            # one launch each of the step's kernels (input generation and fills excluded)
+            step = sum(v["hbm_bytes"] for k, v in j.get("kernels", {}).items()
+                       if any(s in k for s in STEP_KERNELS)) or None
+            return float(j["quantize_bytes_per_launch"]), os.path.relpath(p, ROOT), step
+    return None, None, None
+
+
+PIPELINE_WHAT = {
+    "q": "drop-in equivalent: K2 writes the dequantized q only (what Type_unbiased_quantize returns), "
+         "the client mean reads q (ND:137-138)",
+    "codes": "K2 writes q and int8 type codes, the client mean decodes the codes (same est bits)",
+    "encode": "K2 writes int8 type codes only (no per-client q), the mean kernel dequantizes them",
+}
+
+# kernels launched once per bench step (tools/summarize_profile.py keeps one entry per name)
+STEP_KERNELS = ("l1_partial_kernel", "l1_finalize_kernel", "quantize_stream_kernel", "codes_mean_kernel",
+                "client_mean_kernel")
 
 
 def main():
@@ -218,10 +238,14 @@ def main():
     value = n_total * args.steps / elapsed / 1e6
 
     q_ms = float(seg_ms[1])
-    # algorithmic bytes per K2 launch: read x (4d) + write q (4d) and/or codes (1d)
-    alg_bytes = float(d * n) * (4 + (4 if args.pipeline in ("q", "codes") else 0) + (1 if args.pipeline != "q" else 0))
+    # algorithmic bytes per K2 launch: read x (4d) + write q (4d); the int8
+    # code stream (1d) is this design's own traffic and is reported apart, not as achieved
+    alg_bytes = float(d * n) * (8 if args.pipeline in ("q", "codes") else 4)
+    impl_bytes = float(d * n) * (1 if args.pipeline != "q" else 0)
     achieved = alg_bytes / (q_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(args.traffic_json, d, n, args.pipeline)
+    traffic, traffic_src, step_traffic = load_traffic(args.traffic_json, d, n, args.pipeline)
+    step_alg = float(d * n_total) * 8 / world      # quantize+dequantize bytes of one rank's clients
+    step_achieved = step_alg / (ms_per_step * 1e-3) / 1e9
     # CPU baseline + parity sample on the timed steps' own output q (before any side line)
     base = parity = None
     if world == 1 and not args.no_cpu_baseline:
@@ -231,7 +255,8 @@ def main():
         for pl in ("q", "codes", "encode"):
             if pl != args.pipeline:
                 ms = time_pipeline(pl, max(3, args.steps // 2))
-                side[pl] = {"ms_per_step": round(ms, 4), "value": round(n_total / ms / 1e3, 6)}
+                side[pl] = {"ms_per_step": round(ms, 4), "value": round(n_total / ms / 1e3, 6),
+                            "what": PIPELINE_WHAT[pl]}
         _lib.check(lib.uq_check_status(P(ws), sp), "status after side pipelines")
         side["biased"] = time_biased(uqdme, x, args.bits, T, max(3, args.steps // 2))
         side["eden"] = time_eden(uqdme, x, q, max(3, args.steps // 2))
@@ -263,7 +288,17 @@ def main():
             "roofline": {"kernel": "quantize_stream_kernel (K2)", "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes, "impl_bytes_per_launch": impl_bytes,
+                         "alg_bytes_rule": ("8*d per vector (read x, write q), SURVEY.md §8(d); the int8 codes "
+                                            "(1*d) K2 also writes are implementation traffic"
+                                            if args.pipeline != "encode" else "4*d per vector (read x); no q"),
+                         "step": {"alg_bytes": step_alg, "ms": round(ms_per_step, 4),
+                                  "achieved": round(step_achieved, 2),
+                                  "frac": round(step_achieved / HBM_PEAK_GBS, 4),
+                                  "traffic": step_traffic,
+                                  "traffic_over_alg": (round(step_traffic / step_alg, 3) if step_traffic else None),
+                                  "what": "whole step (L1 + quantize + mean [+ reduce]) priced at 8*d per vector; "
+                                          "traffic = PMC HBM bytes of all the step's kernels per step"}},
         }
         if base is not None:
             result["cpu_baseline"], result["parity_sample"] = base, parity
@@ -320,39 +355,51 @@ def ctypes_size(lib, n, d, T):
     return int(b.value)
 
 
+def host_threads() -> int:
+    """Cores this process may use: its CPU affinity, capped by OMP_NUM_THREADS when the
+    host sets it (the GPU box allots 16 per GPU although it shows many more)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(args, x, X_cpu, q, m, T):
-    """Time the C restatement of the reference path (oracle/, a checker) on host cores
-    for a bounded sample of the same clients; verify the GPU output on that sample."""
+    """Time the C restatement of the reference path (oracle/, a checker) on host cores:
+    the whole batch with clients spread over all allotted cores (OpenMP; primary entry),
+    and a bounded single-thread sample.  The whole-batch output doubles as a bit-parity
+    and NMSE check of the GPU's q from the timed steps."""
     from oracle import uq_oracle_c as C
     from oracle import uq_oracle as O
     n, d = x.shape
+    xh = x.cpu().numpy()
+    Xh = X_cpu.numpy()
+    # single thread: a bounded sample spread over the batch
     budget = args.cpu_seconds
+    t1 = 0.0
     done = 0
-    t_cpu = 0.0
-    mism = 0
-    outs = []
-    idx = []
-    # spread the sample over the batch
-    order = list(range(0, n, max(1, n // 64))) + [j for j in range(n) if j % max(1, n // 64)]
-    for j in order:
-        xj = x[j].cpu().numpy()[None]
+    for j in range(0, n, max(1, n // 64)):
         t0 = time.perf_counter()
-        ref, _ = C.quantize_batch(xj, m, X_cpu[j:j + 1].numpy(), T)
-        t_cpu += time.perf_counter() - t0
-        mism += int(np.count_nonzero(q[j].cpu().numpy().view(np.uint32) != ref[0].view(np.uint32)))
-        outs.append(ref[0])
-        idx.append(j)
+        C.quantize_batch(xh[j:j + 1], m, Xh[j:j + 1], T)
+        t1 += time.perf_counter() - t0
         done += 1
-        if t_cpu >= budget:
+        if t1 >= budget:
             break
-    # NMSE on the sample (script formula ND:151-157), GPU vs CPU restatement
-    xs = x[idx].cpu().numpy()
-    emp = (xs.sum(axis=0, dtype=np.float32) / np.float32(len(idx))).astype(np.float32)
-    vns = float(np.sum(xs.astype(np.float64) ** 2))
-    est_gpu = C.client_mean(q[idx].cpu().numpy(), len(idx))
-    est_cpu = C.client_mean(np.stack(outs), len(idx))
-    nmse_gpu = O.script_nmse(est_gpu, emp, vns, len(idx))
-    nmse_cpu = O.script_nmse(est_cpu, emp, vns, len(idx))
+    # all allotted cores: the whole batch (clients are independent, AS:609-641)
+    nth = host_threads()
+    t0 = time.perf_counter()
+    ref, _, used = C.quantize_batch_mt(xh, m, Xh, T, nth)
+    t_mt = time.perf_counter() - t0
+    qh = q.cpu().numpy()
+    mism = int(np.count_nonzero(qh.view(np.uint32) != ref.view(np.uint32)))
+    # NMSE on the batch (script formula ND:151-157), GPU vs CPU restatement
+    emp = (xh.sum(axis=0, dtype=np.float32) / np.float32(n)).astype(np.float32)
+    vns = float(sum(np.sum(np.square(xh[j:j + 64], dtype=np.float64)) for j in range(0, n, 64)))
+    nmse_gpu = O.script_nmse(C.client_mean(qh, n), emp, vns, n)
+    nmse_cpu = O.script_nmse(C.client_mean(ref, n), emp, vns, n)
+    del xh, qh, ref
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -361,11 +408,28 @@ def cpu_baseline(args, x, X_cpu, q, m, T):
                 break
     except OSError:
         pass
-    base = {"value": round(done / t_cpu / 1e6, 9), "unit": "M-vectors/s", "cores": 1, "kind": "port",
-            "sample": f"{done} of the {n} benchmark clients (d=2^20, R=1), single-threaded C restatement "
-                      f"oracle/uq_oracle.c, {t_cpu:.1f} s on '{cpu_model}' ({os.cpu_count()} logical CPUs visible)",
-            "ms_per_vector": round(t_cpu * 1e3 / done, 3)}
-    par = {"clients_checked": done, "bit_mismatches": mism, "nmse_gpu": nmse_gpu, "nmse_cpu": nmse_cpu,
+    ratio = None
+    try:
+        ratio = json.load(open(os.path.join(ROOT, "profiles", "r02_cpu_port_vs_reference.json")))
+    except (OSError, ValueError):
+        pass
+    base = {"value": round(n / t_mt / 1e6, 9), "unit": "M-vectors/s", "cores": used, "kind": "port",
+            "sample": f"all {n} benchmark clients (d=2^20, R=1), C restatement oracle/uq_oracle.c with clients "
+                      f"over {used} OpenMP threads (allotted cores; {os.cpu_count()} logical CPUs visible), "
+                      f"{t_mt:.2f} s on '{cpu_model}'",
+            "ms_per_vector": round(t_mt * 1e3 / n, 4),
+            "single_thread": {"value": round(done / t1 / 1e6, 9), "unit": "M-vectors/s", "cores": 1,
+                              "ms_per_vector": round(t1 * 1e3 / done, 3),
+                              "sample": f"{done} of the {n} clients, one thread, {t1:.1f} s"}}
+    if ratio:
+        base["port_vs_reference"] = {
+            "host": ratio.get("host_cpu"), "logical_cpus": ratio.get("logical_cpus"),
+            "source": "profiles/r02_cpu_port_vs_reference.json (tools/cpu_port_ratio.py: the reference's "
+                      "Type_unbiased_quantize and this port on the same vectors, one host)",
+            **{k: {kk: v[kk] for kk in ("reference_ms_per_vector", "port_ms_per_vector",
+                                        "port_speedup_over_reference", "bit_mismatches")}
+               for k, v in ratio.items() if k.startswith("threads_")}}
+    par = {"clients_checked": n, "bit_mismatches": mism, "nmse_gpu": nmse_gpu, "nmse_cpu": nmse_cpu,
            "nmse_rel_diff": abs(nmse_gpu - nmse_cpu) / max(nmse_cpu, 1e-300)}
     return base, par
 
