@@ -10,10 +10,13 @@ VARIANTS = {"base": [], "copy": ["-DUQ_ABL_COPY"],
             "k1default": ["-DUQ_K1_NO_NT"]}
 def build():
     sys.path.insert(0, PKG)
+    sys.path.insert(0, os.path.join(ROOT, "tools", "exp"))
     import build_ext as be
+    from ablation_src import patched_csrc           # the -D switches live in tools/exp/ablations.patch
+    src = os.path.join(patched_csrc(), "uq_dme.hip")
     os.makedirs(OUT, exist_ok=True)
     for k, fl in VARIANTS.items():
-        subprocess.run([be.hipcc(), *be.HIPCC_FLAGS, *fl, "-o", os.path.join(OUT, f"{k}.so"), SRC], check=True)
+        subprocess.run([be.hipcc(), *be.HIPCC_FLAGS, *fl, "-o", os.path.join(OUT, f"{k}.so"), src], check=True)
     for extra in sys.argv[2:]:          # name=path/to/alternative.hip
         k, src = extra.split("=", 1)
         subprocess.run([be.hipcc(), *be.HIPCC_FLAGS, "-I", os.path.join(PKG, "csrc"), "-o", os.path.join(OUT, f"{k}.so"), src], check=True)

@@ -14,10 +14,12 @@ VARIANTS = {"base": [], "nochain": ["-DUQ_NORM_ABL_NOCHAIN"], "noload": ["-DUQ_N
 def build():
     sys.path.insert(0, PKG)
     import build_ext as be
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from ablation_src import patched_csrc           # the switches live in tools/exp/ablations.patch
+    src = os.path.join(patched_csrc(), "uq_dme.hip")
     os.makedirs(OUT, exist_ok=True)
     for k, fl in VARIANTS.items():
-        subprocess.run([be.hipcc(), *be.HIPCC_FLAGS, *fl, "-o", os.path.join(OUT, f"{k}.so"),
-                        os.path.join(PKG, "csrc", "uq_dme.hip")], check=True)
+        subprocess.run([be.hipcc(), *be.HIPCC_FLAGS, *fl, "-o", os.path.join(OUT, f"{k}.so"), src], check=True)
 
 
 def run():

@@ -19,7 +19,10 @@ def build():
     sys.path.insert(0, PKG)
     import build_ext as be
     os.makedirs(os.path.dirname(SO), exist_ok=True)
-    subprocess.run([be.hipcc(), *be.HIPCC_FLAGS, "-DUQ_TIE_PROF", "-o", SO, be.SRC], check=True)
+    sys.path.insert(0, os.path.join(ROOT, "tools", "exp"))
+    from ablation_src import patched_csrc           # UQ_TIE_PROF lives in tools/exp/ablations.patch
+    subprocess.run([be.hipcc(), *be.HIPCC_FLAGS, "-DUQ_TIE_PROF", "-o", SO,
+                    os.path.join(patched_csrc(), "uq_dme.hip")], check=True)
 
 
 def run(dist, n):

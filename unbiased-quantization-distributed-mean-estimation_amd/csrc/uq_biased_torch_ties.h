@@ -30,18 +30,9 @@ constexpr int kTieWaves = kTieThreads / kWave;
 constexpr int kTieU = 8;             // independent loads in flight per lane
 constexpr int kTieLdsPairs = 4096;   // ranges this short finish in LDS
 
-#ifdef UQ_TIE_PROF
-// phase timers (wall_clock64 ticks, 100 MHz) accumulated by thread 0 into g_tie_prof[]:
-// 0 fill, 1 stop lists, 2 search, 3 swaps, 4 pivot, 5 lds phase, 6 mark, 7 levels (count)
-__device__ uint64_t* g_tie_prof;
-#define TT_DECL() uint64_t _tt0 = 0; (void)_tt0
-#define TT_T0() _tt0 = wall_clock64()
-#define TT_ACC(k) do { if (threadIdx.x == 0 && g_tie_prof) { uint64_t _t = wall_clock64(); atomicAdd((unsigned long long*)&g_tie_prof[k], (unsigned long long)(_t - _tt0)); _tt0 = _t; } } while (0)
-#else
 #define TT_DECL() do {} while (0)
 #define TT_T0() do {} while (0)
 #define TT_ACC(k) do {} while (0)
-#endif
 
 struct TieShared {
     uint32_t wl[kTieWaves], wr[kTieWaves];   // per-wave stop counts of one partition
@@ -295,9 +286,6 @@ __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t 
     }
     __syncthreads();
     TT_ACC(3);
-#ifdef UQ_TIE_PROF
-    if (threadIdx.x == 0 && g_tie_prof) atomicAdd((unsigned long long*)&g_tie_prof[7], 1ull);
-#endif
     return (cut <= first || cut >= last) ? -1 : cut;
 }
 

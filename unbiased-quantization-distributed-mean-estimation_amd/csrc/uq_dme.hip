@@ -282,13 +282,9 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
         for (int r = 0; r < step; ++r) {
             float v0, v1, v2, v3;
             if (VEC4) {
-#ifndef UQ_K1_NO_NT            // x is streamed once per pass: non-temporal (measured 8.7 % faster)
                 typedef float k1x4 __attribute__((ext_vector_type(4)));
                 const k1x4 tv = __builtin_nontemporal_load(reinterpret_cast<const k1x4*>(p + (int64_t)r * 32));
                 const float4 t = make_float4(tv.x, tv.y, tv.z, tv.w);
-#else
-                const float4 t = *reinterpret_cast<const float4*>(p + (int64_t)r * 32);
-#endif
                 v0 = t.x; v1 = t.y; v2 = t.z; v3 = t.w;
             } else {
                 const float* pr = p + (int64_t)r * 32;
@@ -580,14 +576,10 @@ __device__ __forceinline__ bool lowbit(double s) { return ((uint32_t)__double_as
 // between the sequential fp64 sum and any approximation of it for d < 2^31)
 constexpr double kEdge = 0x1p-20;
 
-#ifdef UQ_OLD_SWZ
-__device__ __forceinline__ int swz(int r, int c) { return r * 16 + 4 * (c ^ ((r >> 2) & 3)); }
-#else
 // f(r) = ((r >> 2) ^ (r >> 1)) & 3 makes the 16-lane ds_read_b128 groups (banks mod 64)
 // AND the 8-lane ds_write_b128 groups (banks mod 32) conflict-free for row accesses,
 // staging writes and store reads alike.
 __device__ __forceinline__ int swz(int r, int c) { return r * 16 + 4 * (c ^ (((r >> 2) ^ (r >> 1)) & 3)); }
-#endif
 __device__ __forceinline__ int swz_elem(int i) { return swz(i >> 4, (i >> 2) & 3) + (i & 3); }
 
 struct TileRegs {
@@ -595,8 +587,7 @@ struct TileRegs {
 };
 
 // x is read once and q written once per call: non-temporal loads/stores (measured ~4%
-// faster on the C2 batch than default-policy accesses).  -DUQ_NO_NT restores them.
-#ifndef UQ_NO_NT
+// faster on the C2 batch than default-policy accesses).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld_stream(const float4* p) {
     const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
@@ -606,10 +597,6 @@ __device__ __forceinline__ void st_stream(float4* p, float4 v) {
     const f32x4 t = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
 }
-#else
-__device__ __forceinline__ float4 ld_stream(const float4* p) { return *p; }
-__device__ __forceinline__ void st_stream(float4* p, float4 v) { *p = v; }
-#endif
 
 template <bool VEC4>
 __device__ __forceinline__ void load_tile(TileRegs& r, const float* __restrict__ x, int64_t d, int32_t tiles,
@@ -680,12 +667,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
     return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 constexpr int kAuxNT = 2;
-#ifndef UQ_CODES_AUX
-#define UQ_CODES_AUX kAuxNT    // cache policy of the code stores (timing ablation switch)
-#endif
-#ifndef UQ_Q_AUX
-#define UQ_Q_AUX kAuxNT        // cache policy of the q stores (timing ablation switch)
-#endif
 
 __device__ __forceinline__ void load_tile_buf(TileRegs& r, __amdgpu_buffer_rsrc_t rx, uint32_t t0_bytes, int tid) {
 #pragma unroll
@@ -703,7 +684,7 @@ __device__ __forceinline__ void store_tile_buf(const float* s_data, __amdgpu_buf
         const int q = tid + j * kQBlock;
         const float4 v = *reinterpret_cast<const float4*>(&s_data[swz(q >> 2, q & 3)]);
         const f32x4v w = {v.x, v.y, v.z, v.w};
-        __builtin_amdgcn_raw_buffer_store_b128(w, ro, t0_bytes + (uint32_t)q * 16u, 0, UQ_Q_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(w, ro, t0_bytes + (uint32_t)q * 16u, 0, kAuxNT);
     }
 }
 
@@ -986,11 +967,7 @@ __device__ double resolve_exact(double P, const Binade& B, const TileState& st, 
         int nt = 0;
 #pragma unroll
         for (int w = 0; w < kQBlock / kWave; ++w) nt += __builtin_popcountll(uniform_u64(sl.tmask[w]));
-        if (nt == 0
-#ifdef UQ_EXP_NOTIES
-            || true
-#endif
-        ) {
+        if (nt == 0) {
             pnext = P + st.total;                                // exact: multiples of G in the binade
             return P + st.texcl;
         }
@@ -1034,9 +1011,6 @@ __device__ double resolve_exact(double P, const Binade& B, const TileState& st, 
         pnext = (P + st.total) + D;
         return (P + st.texcl) + corr;
     }
-#ifdef UQ_EXP_NOIRR
-    pnext = P + st.total; return P + st.texcl;
-#endif
     // irregular tile: the events walked by one lane from the exact start
     IrrThread it;
     irregular_prep(P, st, tv, s_scr, sl, tid, it);
@@ -1216,7 +1190,7 @@ __device__ __forceinline__ void store_codes_buf(__amdgpu_buffer_rsrc_t rc, int8_
                                                 const uint32_t (&cw)[4], uint32_t t0, int64_t d, int tid) {
     if (CVEC) {
         const u32x4v v = {cw[0], cw[1], cw[2], cw[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rc, t0 + (uint32_t)(tid * kQItems), 0, UQ_CODES_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rc, t0 + (uint32_t)(tid * kQItems), 0, kAuxNT);
     } else {
         const int64_t rem = d - (int64_t)t0;
         store_codes<false>(crow + t0, cw, (int)(rem < kQTile ? rem : kQTile), tid);
@@ -1275,11 +1249,7 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     const float L = l1[vec];
     const DivPlan dp = div_plan(L);
     const float Xv = Xs[vec];
-#ifdef UQ_ABL_NOIO
-    const uint32_t row_bytes = 0;              // timing-only ablation: every access dropped
-#else
     const uint32_t row_bytes = (uint32_t)(d * 4);
-#endif
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, row_bytes);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(WQ ? out + vec * d : x, row_bytes);
     const __amdgpu_buffer_rsrc_t rc = make_rsrc(WC ? (const void*)(codes + vec * d) : (const void*)x, row_bytes / 4u);
@@ -1294,24 +1264,12 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         __syncthreads();                           // s_x(t) staged; s_o(t-1) complete
         if (tile > tb) {
             const uint32_t tp = (uint32_t)(tile - 1) * (uint32_t)kQTile;
-#ifdef UQ_CODES_FIRST           // timing ablation: code stores before the q stores
-            if (WC) store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
-            if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);
-#else
             if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);      // beyond d: dropped by the range check
             if (WC) store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
-#endif
         }
         if (tile + 1 < te) load_tile_buf(pre_x, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
         const int64_t t0 = (int64_t)tile * kQTile;
         const int len = (int)((d - t0) < kQTile ? (d - t0) : kQTile);
-#ifdef UQ_ABL_COPY
-        // timing-only ablation: the tile's memory traffic without the arithmetic
-        __syncthreads();
-#pragma unroll
-        for (int k4 = 0; k4 < kQItems / 4; ++k4)
-            *reinterpret_cast<float4*>(&s_o[swz(tid, k4)]) = *reinterpret_cast<const float4*>(&s_x[swz(tid, k4)]);
-#else
         TileState st;
         TileVals tv;
         P = uniform_d(P);
@@ -1325,7 +1283,6 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         const double base = resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);
         tile_pass2<WQ, WC>(s_o, tv, s_tab, tid, base, L, fm, Xv, cw, kmax);
         P = pnext;
-#endif
     }
     __syncthreads();
     const uint32_t tp = (uint32_t)(te - 1) * (uint32_t)kQTile;
@@ -1550,10 +1507,6 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
     const int64_t vec = blockIdx.x;
     const int64_t base = vec * tiles;
     const DivPlan dp = div_plan(l1[vec]);
-#ifdef UQ_FOLD_PROF
-    uint64_t pt0 = wall_clock64(), pmap = 0, prec = 0, pfb = 0;
-    int nfb = 0, nrw = 0;
-#endif
     // prefetch every record of this client that fits (two dependent round trips in all)
     const int nrec = vec < kRecClients ? (int)min(reccnt[vec], (uint32_t)kRecPerClient) : 0;
     if (tid < nrec) {
@@ -1578,16 +1531,10 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
         for (int i = tid; i < nw; i += kQBlock) dst[i] = src[i];
     }
     __syncthreads();
-#ifdef UQ_FOLD_PROF
-    const uint64_t pt1 = wall_clock64();
-#endif
     constexpr uint64_t kMant = (1ull << 52) - 1ull;
     uint64_t Pb = 0;                                           // bits of the exact P (P_0 = 0)
     int32_t tile = 0;
     while (tile < tiles) {
-#ifdef UQ_FOLD_PROF
-        const uint64_t q0 = wall_clock64();
-#endif
         // a run of regular maps, 64 tiles at a time: lane l holds the map of tile blk + l
         // (the next 64 are loaded meanwhile).  A map in units of G is P -> P + d[P & 1];
         // two maps compose to the same form, (F then g).d[p] = F.d[p] + g.d[p ^ (F.d[p] & 1)],
@@ -1631,9 +1578,6 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
             am = an;
             bm = bn;
         }
-#ifdef UQ_FOLD_PROF
-        pmap += wall_clock64() - q0;
-#endif
         if (tile >= tiles) break;
         // an irregular tile (or a map whose binade P is not in: resolved from the data)
         double P = __longlong_as_double((long long)Pb);
@@ -1641,10 +1585,6 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
         if (tid == 0) pre[idx] = Pb;
         const uint32_t rid = map0[idx] == kIrrMap ? (uint32_t)map1[idx] : 0u;
         if (rid != 0u && s_roff[rid - 1u] != ~0u) {            // recorded and prefetched: walk it
-#ifdef UQ_FOLD_PROF
-            const uint64_t q1 = wall_clock64();
-            ++nrw;
-#endif
             if (tid == 0) {
                 const EvEntry* ev0 = s_ev + s_roff[rid - 1u];
                 double S = P;
@@ -1662,9 +1602,6 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
             __syncthreads();
             P = sl.misc[0];
             __syncthreads();
-#ifdef UQ_FOLD_PROF
-            prec += wall_clock64() - q1;
-#endif
         } else if (rid != 0u) {                                // recorded: copy it, walk it
             const TileRec* rec = recs + (vec * kRecPerClient + (rid - 1u));
             uint32_t* dst = reinterpret_cast<uint32_t*>(s_x);
@@ -1689,10 +1626,6 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
             P = sl.misc[0];
             __syncthreads();
         } else {                                               // from the data
-#ifdef UQ_FOLD_PROF
-            const uint64_t qf = wall_clock64();
-            ++nfb;
-#endif
             TileRegs r;
             load_tile<VEC4>(r, x, d, tiles, (uint32_t)idx, tid);
             stage_tile<VEC4>(r, s_x, tid);
@@ -1710,19 +1643,10 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
             (void)resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);
             __syncthreads();                                   // s_x / sl reused by the next irregular tile
             P = pnext;
-#ifdef UQ_FOLD_PROF
-            pfb += wall_clock64() - qf;
-#endif
         }
         Pb = (uint64_t)__double_as_longlong(P);
         ++tile;
     }
-#ifdef UQ_FOLD_PROF
-    if (tid == 0 && vec == 0)
-        printf("fold: prefetch %llu map %llu rec %llu (%d) fallback %llu (%d) total %llu ticks (100 MHz)\n",
-               (unsigned long long)(pt1 - pt0), (unsigned long long)pmap, (unsigned long long)prec, nrw,
-               (unsigned long long)pfb, nfb, (unsigned long long)(wall_clock64() - pt0));
-#endif
 }
 
 // Outputs, one workgroup per tile, from the exact tile prefix pre[t] (any row alignment).
@@ -2511,11 +2435,6 @@ int uq_check_status(void* ws, void* stream) {
     return UQ_OK;
 }
 
-#ifdef UQ_TIE_PROF
-int uq_debug_set_tie_prof(void* dev_counters) {
-    return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_tie_prof), &dev_counters, sizeof(void*)), "set tie prof");
-}
-#endif
 
 int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t T, size_t* bytes_out) {
     if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");

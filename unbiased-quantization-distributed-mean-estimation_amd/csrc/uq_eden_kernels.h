@@ -374,13 +374,8 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
 #pragma unroll
         for (int q = 0; q < kLQ; ++q) {
             const int64_t i = ch * kNormChunk + 4 * (lj + 64 * q);
-#ifdef UQ_NORM_ABL_NOLOAD          // timing-only ablation (tools/exp/norm_abl.py): no global loads
-            if (true) {
-                nx[q] = make_float4(1.f, 1.f, 1.f, (float)i);
-#else
             if (lvalid && i + 3 < nv) {
                 nx[q] = *reinterpret_cast<const float4*>(lp + i);
-#endif
             } else {
                 nx[q].x = (lvalid && i < nv) ? lp[i] : 0.f;
                 nx[q].y = (lvalid && i + 1 < nv) ? lp[i + 1] : 0.f;
@@ -412,9 +407,6 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
     __syncthreads();
     for (int64_t ch = 0; ch < nchunks; ++ch) {
         if (chain) {
-#ifdef UQ_NORM_ABL_NOCHAIN         // timing-only ablation (tools/exp/norm_abl.py): no chain work
-            acc += s[ch % 3][tid];
-#else
             const int cnt = (int)(std::min<int64_t>(kNormChunk, nv - ch * kNormChunk) / 8);
             const float* row = s[ch % 3] + ck * kNormClientStride + cl * kNormRow;
             int i = 0;
@@ -431,7 +423,6 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
                 }
             }
             for (; i < cnt; ++i) acc = fmaf(row[i], row[i], acc);
-#endif
         } else if (ch + 1 < nchunks) {
             store(s[(ch + 1) % 3]);
             if (ch + 2 < nchunks) load(ch + 2);
