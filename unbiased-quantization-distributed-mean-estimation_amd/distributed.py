@@ -19,6 +19,9 @@ is the final mean:
 
 The per-rank compute is injected (`fold`), so the protocol runs unchanged on the
 gloo backend in CPU tests; on GPUs `fold` defaults to the HIP client-mean kernel.
+With a non-RCCL backend (gloo) and device tensors, every exchange is staged through host
+memory (gloo's point-to-point ops take host tensors); that is how several ranks sharing
+one GPU test the HIP path, while the product path on a node is RCCL with no staging.
 """
 from __future__ import annotations
 
@@ -38,6 +41,35 @@ def shard_range(n_total: int, world: int, rank: int) -> tuple:
     lo = rank * base + min(rank, extra)
     hi = lo + base + (1 if rank < extra else 0)
     return lo, hi
+
+
+def _staged(t: torch.Tensor, group) -> bool:
+    return t.is_cuda and dist.get_backend(group) != "nccl"
+
+
+def _reduce(est, dst, group):
+    if _staged(est, group):
+        h = est.cpu()
+        dist.reduce(h, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if dist.get_rank(group) == dst:
+            est.copy_(h)
+    else:
+        dist.reduce(est, dst=dst, op=dist.ReduceOp.SUM, group=group)
+
+
+def _recv(t, src, group):
+    if _staged(t, group):
+        h = torch.empty(t.shape, dtype=t.dtype)
+        dist.recv(h, src=src, group=group)
+        t.copy_(h)
+    else:
+        dist.recv(t, src=src, group=group)
+
+
+def _isend(t, dst, group):
+    """Returns (work, buffer): the buffer must live until the work completes."""
+    buf = t.cpu() if _staged(t, group) else t
+    return dist.isend(buf, dst=dst, group=group), buf
 
 
 def _default_fold(q: torch.Tensor, n_div: float, est: Optional[torch.Tensor]) -> torch.Tensor:
@@ -62,7 +94,7 @@ def sharded_client_mean(q_local: torch.Tensor, n_div: float, *, mode: str = "red
         else:
             est = torch.zeros(d, dtype=torch.float32, device=q_local.device)
         if world > 1:
-            dist.reduce(est, dst=dst, op=dist.ReduceOp.SUM, group=group)
+            _reduce(est, dst, group)
         return est if rank == dst else None
     if mode != "ordered":
         raise ValueError("mode must be 'reduce' or 'ordered'")
@@ -72,19 +104,19 @@ def sharded_client_mean(q_local: torch.Tensor, n_div: float, *, mode: str = "red
         c1 = min(d, c0 + block)
         blk = est[c0:c1]
         if rank > 0:
-            dist.recv(blk, src=rank - 1, group=group)
+            _recv(blk, rank - 1, group)
         if n_local:
             fold(q_local[:, c0:c1], n_div, blk)       # continues the client-ordered sum in place
         if rank < world - 1:
-            pending.append(dist.isend(blk, dst=rank + 1, group=group))
-    for p in pending:
-        p.wait()
+            pending.append(_isend(blk, rank + 1, group))
+    for work, _buf in pending:
+        work.wait()
     last = world - 1
     if dst != last:
         if rank == last:
-            dist.send(est, dst=dst, group=group)
+            dist.send(est.cpu() if _staged(est, group) else est, dst=dst, group=group)
         elif rank == dst:
-            dist.recv(est, src=last, group=group)
+            _recv(est, last, group)
     return est if rank == dst else None
 
 
