@@ -66,6 +66,8 @@ def parse():
                     help="q: K2 writes the dequantized q, mean reads q (the reference's drop-in semantics); "
                          "codes: K2 writes q AND type codes, mean decodes codes; "
                          "encode: K2 writes codes only, the mean kernel dequantizes (DME wire pipeline)")
+    ap.add_argument("--probe-candidates", type=int, default=6,
+                    help="output-buffer sets probed once before warmup (pipeline.py); <= 1: no probe")
     ap.add_argument("--side-pipelines", action="store_true", default=True,
                     help="also time the other pipelines (reported under 'pipelines')")
     ap.add_argument("--no-side-pipelines", dest="side_pipelines", action="store_false")
@@ -151,18 +153,15 @@ def main():
         x = torch.rand(n, d, generator=g, device=dev, dtype=torch.float32) * 2.0 - 1.0
     X_cpu = torch.rand(n_total, generator=torch.Generator().manual_seed(args.seed))[rank * n:(rank + 1) * n]
     X = X_cpu.to(dev)
-    q = torch.empty_like(x)
-    l1 = torch.empty(n, dtype=torch.float32, device=dev)
-    est = torch.empty(d, dtype=torch.float32, device=dev)
+    # resident buffers of the batched pipeline; the output placement is probed once (see
+    # pipeline.py: K2's speed follows where q and the codes land in physical memory)
+    pipe = uqdme.DMEPipeline(n, d, m=m, torch_threads=T)
+    probe = pipe.probe_outputs(x, X, candidates=args.probe_candidates) if args.probe_candidates > 1 else None
+    q, codes, ovf, l1, est, ws, nb = pipe.q, pipe.codes, pipe.kmax, pipe.l1, pipe.est, pipe.ws, pipe.ws_bytes
     lib = _lib.load()
-    nb = ctypes_size(lib, n, d, T)
-    ws = torch.zeros(nb, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     P = lambda t: t.data_ptr()  # noqa: E731
-
-    codes = torch.empty((n, d), dtype=torch.int8, device=dev)
-    ovf = torch.zeros(n, dtype=torch.int32, device=dev)
 
     def step(ev=None, pipeline=args.pipeline):
         if ev is not None:
@@ -285,6 +284,7 @@ def main():
             "kernel_ms": {"l1": round(float(seg_ms[0]), 4), "quantize": round(q_ms, 4),
                           "client_mean": round(float(seg_ms[2]), 4), "reduce": round(float(seg_ms[3]), 4)},
             "pipelines": side,
+            "output_placement_probe": probe,
             "roofline": {"kernel": "quantize_stream_kernel (K2)", "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
@@ -345,14 +345,6 @@ def time_eden(uqdme, x, q, steps):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     return {"ms_per_step": round(ms, 4), "value": round(n / ms / 1e3, 6), "what": "EDEN 1-bit batch (RHT, bins, scale, inverse RHT), no mean"}
-
-
-def ctypes_size(lib, n, d, T):
-    import ctypes
-    from uqdme_amd import _lib
-    b = ctypes.c_size_t()
-    _lib.check(lib.uq_workspace_bytes(n, d, T, ctypes.byref(b)), "workspace")
-    return int(b.value)
 
 
 def host_threads() -> int:

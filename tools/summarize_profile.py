@@ -12,6 +12,23 @@ os.makedirs(prof, exist_ok=True)
 st = glob.glob(os.path.join(src, "stats", "**", "*kernel_stats.csv"), recursive=True)
 if st:
     shutil.copy(st[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
+# The bench probes its output placement before warmup (extra K2 launches on candidate
+# buffers, pipeline.py), so the stats average mixes those in; the timed steps are the LAST
+# launches of each kernel.  Per-kernel averages over the last `steps` dispatches, from the
+# same pass's per-dispatch trace:
+STEPS = int(os.environ.get("PROFILE_STEPS", "10"))
+tr = glob.glob(os.path.join(src, "stats", "**", "*kernel_trace.csv"), recursive=True)
+timed = {}
+if tr:
+    per = {}
+    for r in csv.DictReader(open(tr[0])):
+        per.setdefault(r["Kernel_Name"], []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    for k, v in per.items():
+        last = v[-STEPS:]
+        timed[k[:100]] = {"calls_total": len(v), "timed_calls": len(last), "avg_ms_timed": sum(last) / len(last) / 1e6,
+                          "avg_ms_all": sum(v) / len(v) / 1e6}
+    json.dump({"tag": tag, "steps": STEPS, "kernels": timed}, open(os.path.join(prof, f"{tag}_kernel_timed.json"), "w"),
+              indent=1)
 def per_kernel(kind, counter):
     fs = glob.glob(os.path.join(src, kind, "**", "*counter_collection.csv"), recursive=True)
     vals = {}

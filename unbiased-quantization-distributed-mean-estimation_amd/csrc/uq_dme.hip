@@ -409,7 +409,9 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
     __shared__ float fin_w[kFinWaves][32];
     __shared__ __attribute__((aligned(16))) float s_stage_w[kFinWaves][kFinStage * 32];
     __shared__ float s_tail_w[kFinWaves][64];
-    __shared__ float s_chunk[kMaxThreads];      // the per-thread buffer of the two-pass reduction
+    // the per-thread buffer of the two-pass reduction: plan.nbuf floats of dynamic LDS (a
+    // static kMaxThreads buffer would halve the workgroups per CU for every T)
+    extern __shared__ float s_chunk[];
     float* fin = fin_w[wv];
     float* s_stage = s_stage_w[wv];
     float* s_tail = s_tail_w[wv];
@@ -1948,8 +1950,8 @@ int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, flo
         int rc = hip_check(hipGetLastError(), "l1_partial_kernel launch");
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(l1_finalize_kernel<Op>, dim3((unsigned)n), dim3(64 * kFinWaves), 0, st, x, d, plan, part, sum_out, l1, fm,
-                       hist, zn);
+    hipLaunchKernelGGL(l1_finalize_kernel<Op>, dim3((unsigned)n), dim3(64 * kFinWaves), (size_t)plan.nbuf * sizeof(float), st,
+                       x, d, plan, part, sum_out, l1, fm, hist, zn);
     return hip_check(hipGetLastError(), "l1_finalize_kernel launch");
 }
 

@@ -1,0 +1,124 @@
+"""Resident DME pipeline: the batched hot path with its buffers kept in HBM.
+
+    p = DMEPipeline(n, d, bits_per_dimension=1, torch_threads=1)
+    est = p.step(x, X, n_div)        # K1 L1 (AS:624) -> K2 quantize (AS:625-640, writes q and
+                                     # type codes) -> K3c client-ordered mean (ND:137-138)
+    p.q, p.codes, p.l1               # the step's per-client outputs (overwritten by the next step)
+
+Output placement.  K2 writes q (4*d B per client) and the int8 codes (1*d) while reading x.
+On MI355X its time depends on where the OUTPUT buffers land in physical memory: with x fixed
+and q + codes re-allocated ten times in one process K2 took 1.66-2.03 ms on the C2 batch, with
+q + codes fixed and x re-allocated ten times 1.67-1.73 ms (profiles/r02d_exp_placement_split.jsonl);
+the code layout does not matter (tile-major codes follow the same modes,
+profiles/r02c_exp_codes_layout.jsonl).  The pipeline's outputs are long-lived, so
+`probe_outputs` allocates a few candidate (q, codes) sets at once (each on its own pages),
+times K2 on each with the real batch, keeps the fastest and frees the rest: a one-time
+calibration like a workspace autotune.  Results do not depend on the buffers chosen.
+
+Every launch goes through the C-ABI (include/uq_dme.h); nothing here computes on the CPU."""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .rates import rate_to_m
+
+__all__ = ["DMEPipeline"]
+
+
+def _p(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+class DMEPipeline:
+    def __init__(self, n: int, d: int, bits_per_dimension=1, *, m: int | None = None, torch_threads: int = 1,
+                 write_q: bool = True, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("uqdme requires a ROCm GPU (no CPU fallback by design)")
+        self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.n, self.d = int(n), int(d)
+        self.m = int(m) if m is not None else rate_to_m(bits_per_dimension, d)
+        self.T = int(torch_threads)
+        self.write_q = bool(write_q)
+        self.lib = _lib.load()
+        b = ctypes.c_size_t()
+        _lib.check(self.lib.uq_workspace_bytes(self.n, self.d, self.T, ctypes.byref(b)), "uq_workspace_bytes")
+        self.ws_bytes = int(b.value)
+        self.ws = torch.zeros(max(self.ws_bytes, 1 << 16), dtype=torch.uint8, device=self.dev)
+        self.l1 = torch.empty(self.n, dtype=torch.float32, device=self.dev)
+        self.kmax = torch.zeros(self.n, dtype=torch.int32, device=self.dev)
+        self.est = torch.empty(self.d, dtype=torch.float32, device=self.dev)
+        self.q, self.codes = self._alloc_outputs()
+        self.probe_report = None
+
+    # ---- buffers ---------------------------------------------------------------------
+    def _alloc_outputs(self):
+        q = torch.empty((self.n, self.d), dtype=torch.float32, device=self.dev) if self.write_q else None
+        c = torch.empty((self.n, self.d), dtype=torch.int8, device=self.dev)
+        return q, c
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    # ---- the three launches ----------------------------------------------------------
+    def l1_norms(self, x):
+        _lib.check(self.lib.uq_l1_torch_order_f32(_p(x), self.n, self.d, self.T, _p(self.l1), _p(self.ws),
+                                                  self.ws_bytes, self._stream()), "uq_l1_torch_order_f32")
+
+    def quantize(self, x, X, q=None, codes=None):
+        q = self.q if q is None and self.write_q else q
+        codes = self.codes if codes is None else codes
+        _lib.check(self.lib.uq_type_unbiased_codes_f32(_p(x), _p(q), _p(codes), _p(self.kmax), self.n, self.d, self.m,
+                                                       _p(X), _p(self.l1), None, self.T, _p(self.ws), self.ws_bytes,
+                                                       self._stream()), "uq_type_unbiased_codes_f32")
+
+    def mean(self, n_div: float, accumulate: bool = False):
+        _lib.check(self.lib.uq_codes_mean_f32(_p(self.codes), _p(self.l1), _p(self.kmax), self.n, self.d, self.m,
+                                              float(n_div), int(bool(accumulate)), _p(self.est), self._stream()),
+                   "uq_codes_mean_f32")
+        return self.est
+
+    def step(self, x, X, n_div=None, accumulate: bool = False):
+        """One pass of the hot path over the resident batch x[n, d] (f32, contiguous, on the
+        device) with per-client uniforms X[n] (device f32).  Returns est (+)= sum_j q_j / n_div."""
+        self._check(x, X)
+        self.l1_norms(x)
+        self.quantize(x, X)
+        return self.mean(self.n if n_div is None else n_div, accumulate)
+
+    def _check(self, x, X):
+        if x.shape != (self.n, self.d) or x.dtype != torch.float32 or not x.is_contiguous() or x.device != self.dev:
+            raise ValueError(f"x must be a contiguous f32 [{self.n}, {self.d}] tensor on {self.dev}")
+        if X.numel() != self.n or X.dtype != torch.float32 or X.device != self.dev:
+            raise ValueError("X must hold one f32 draw per client on the device")
+
+    # ---- output placement ------------------------------------------------------------
+    def probe_outputs(self, x, X, candidates: int = 4, reps: int = 3):
+        """Time K2 on `candidates` output sets (the current one included), keep the fastest.
+        Needs the batch's L1 (runs K1 first).  Returns the report (ms per candidate)."""
+        self._check(x, X)
+        self.l1_norms(x)
+        sets = [(self.q, self.codes)] + [self._alloc_outputs() for _ in range(max(0, candidates - 1))]
+        times = []
+        for q, c in sets:
+            for _ in range(2):
+                self.quantize(x, X, q, c)
+            torch.cuda.synchronize(self.dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                self.quantize(x, X, q, c)
+            e1.record()
+            torch.cuda.synchronize(self.dev)
+            times.append(e0.elapsed_time(e1) / reps)
+        best = min(range(len(sets)), key=lambda i: times[i])
+        self.q, self.codes = sets[best]
+        del sets
+        torch.cuda.empty_cache()
+        self.probe_report = {"candidates": len(times), "k2_ms": [round(t, 4) for t in times], "chosen": best}
+        return self.probe_report
+
+    def check_status(self):
+        _lib.check(self.lib.uq_check_status(_p(self.ws), self._stream()), "uq_check_status")
