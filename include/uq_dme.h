@@ -106,6 +106,32 @@ int uq_codes_decode_f32(const int8_t* codes, const float* l1, int64_t n, int64_t
 int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax, int64_t n, int64_t d,
                       int64_t m, float n_div, int32_t accumulate, float* est, void* stream);
 
+/* ---- type messages "UQR1": entropy-coded type codes ---------------
+ * The reference has no wire format (parity unpinned); its client output is AS:640's
+ * dequantized vector, fully described by (L1, m, signed counts k) = the int8 codes above.
+ * One message per client: rANS over symbols s = 2k + neg with a per-client static model
+ * (frequencies quantized to 2^12), 32-bit states, 16-bit words, W = min(64, ceil(d/1024))
+ * interleaved states per chunk of W*1024 symbols, so ~R bits per coordinate at rate R.
+ * flags bit 0 (UQ_TC_EXACT_ZERO_SIGNS): keep the sign of zero counts (neg for k = 0), so
+ * the decoded q is bit-identical to AS:640 (-0.0 included); without it the sign of a zero
+ * count is dropped and q is value-identical (+0.0 where the reference has -0.0), at ~R bits.
+ * Byte layout: oracle/uq_codec.c (the CPU restatement the tests compare against).
+ *
+ * uq_tc_bound: the largest message of a client of length d (bytes).
+ * uq_tc_encode: codes [n][d] int8, l1 [n] f32 (device) -> messages packed back to back in
+ *   msgs (device, msgs_bytes >= n * bound), offsets [n+1] u64 (device): client j's message is
+ *   msgs[offsets[j] .. offsets[j+1]).  Workspace: uq_tc_workspace_bytes (no zero-fill needed).
+ * uq_tc_decode: messages (device, offsets [n+1]) -> codes [n][d], l1 [n], kmax [n]; status [n]
+ *   int32 (device) is 0 for a well-formed message, else bit 0 bad header / d mismatch, bit 1
+ *   bad frequency table, bit 2 word stream overrun or underrun, bit 3 wrong final state. */
+#define UQ_TC_EXACT_ZERO_SIGNS 1
+int uq_tc_bound(int64_t d, size_t* bytes_out);
+int uq_tc_workspace_bytes(int64_t n, int64_t d, size_t* bytes_out);
+int uq_tc_encode(const int8_t* codes, const float* l1, int64_t n, int64_t d, int64_t m, int32_t flags,
+                 uint8_t* msgs, size_t msgs_bytes, uint64_t* offsets, void* ws, size_t ws_bytes, void* stream);
+int uq_tc_decode(const uint8_t* msgs, const uint64_t* offsets, int64_t n, int64_t d, int8_t* codes, float* l1,
+                 int32_t* kmax, int32_t* status, void* stream);
+
 /* ---- biased type quantizer (Reznik rounding) ------------------------------------------
  * NMSE_Results/Codes/All_Schemes.py:669-687 Type_biased_quantize and :644-666 Reznik for
  * a batch: out[j] = Type_biased_quantize(x[j], ·) with m = the lattice sum (AS:684).

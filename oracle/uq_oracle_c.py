@@ -37,6 +37,12 @@ def lib():
         L.uqo_client_mean.argtypes = [p, i64, i64, f, p]
         L.uqo_torch_sum.restype = f
         L.uqo_torch_sum.argtypes = [p, i64, ctypes.c_int]
+        L.uqc_bound.restype = ctypes.c_uint64
+        L.uqc_bound.argtypes = [i64]
+        L.uqc_encode.restype = ctypes.c_uint64
+        L.uqc_encode.argtypes = [p, i64, i64, f, ctypes.c_int, p]
+        L.uqc_decode.restype = ctypes.c_int
+        L.uqc_decode.argtypes = [p, ctypes.c_uint64, p, i64, p, p]
         L.uqo_biased_quantize.restype = ctypes.c_int
         L.uqo_biased_quantize.argtypes = [p, p, i64, i64, ctypes.c_int, ctypes.c_int, p, p, p]
         _lib = L
@@ -112,3 +118,25 @@ def biased_quantize(x, m: int, torch_threads: int = 1, tie_mode: int = 0):
     if rc == -2:
         raise RuntimeError("selected index k out of range (AS:660)")
     return out, np.float32(L[0]), int(D[0]), bool(A[0])
+
+
+def codec_encode(codes, m: int, l1: float, exact: bool = False) -> bytes:
+    """One client's int8 type codes -> a UQR1 message (oracle/uq_codec.c)."""
+    c = np.ascontiguousarray(codes, dtype=np.int8).reshape(-1)
+    out = np.empty(int(lib().uqc_bound(c.shape[0])), np.uint8)
+    n = lib().uqc_encode(_ptr(c), c.shape[0], int(m), np.float32(l1), int(bool(exact)), _ptr(out))
+    if n == 0 and c.shape[0] > 0:
+        raise ValueError("uqc_encode failed")
+    return out[:n].tobytes()
+
+
+def codec_decode(msg: bytes, d: int):
+    """UQR1 message -> (codes int8 [d], l1 f32, m); raises on a malformed message."""
+    buf = np.frombuffer(msg, np.uint8).copy()
+    codes = np.empty(max(1, d), np.int8)
+    l1 = np.zeros(1, np.float32)
+    m = np.zeros(1, np.int64)
+    rc = lib().uqc_decode(_ptr(buf), buf.shape[0], _ptr(codes), int(d), _ptr(l1), _ptr(m))
+    if rc != 0:
+        raise ValueError(f"malformed UQR1 message ({rc})")
+    return codes[:d], np.float32(l1[0]), int(m[0])

@@ -12,7 +12,7 @@ from .quantizer import (
     l1_torch_order, draw_uniforms, set_torch_threads, get_torch_threads, check_status,
     quantize_encode, decode, codes_mean,
 )
-from .codes import TypeCodes
+from .codes import TypeCodes, TypeMessages, encode_messages, decode_messages
 from .biased import Type_biased_quantize, biased_quantize
 from .eden import (EDEN_quantize_Hadamard, eden_quantize, eden_compress, eden_decompress, EdenMessage, rht_signs,
                    randomized_hadamard_transform, randomized_inverse_hadamard_transform)
@@ -32,5 +32,5 @@ __all__ = [
     "TypeCodes", "Type_biased_quantize", "biased_quantize", "EDEN_quantize_Hadamard", "eden_quantize",
     "eden_compress", "eden_decompress", "EdenMessage", "rht_signs", "randomized_hadamard_transform",
     "randomized_inverse_hadamard_transform", "compute_nmse_stats_auto", "data_format", "round_nmse",
-    "DMEPipeline",
+    "DMEPipeline", "TypeMessages", "encode_messages", "decode_messages",
 ]

@@ -1,0 +1,412 @@
+// Type-message codec "UQR1": rANS over the int8 type codes.
+// Included by uq_dme.hip inside its anonymous namespace.  Format and symbol map: see the
+// header of include/uq_dme.h (uq_tc_*) and codes.py; oracle/uq_codec.c restates it on the CPU
+// byte for byte (tests compare whole messages).
+//
+//   KC1 tc_hist_kernel     symbol counts per client (LDS histogram per 64 Ki-symbol segment)
+//   KC2 tc_table_kernel    one wave per client: quantized frequencies (sum 2^12), cumulative
+//                          table, header size
+//   KC3 tc_encode_kernel   one wave per chunk (W interleaved rANS states x 1024 steps): steps
+//                          in reverse, renormalisation words pushed per step in lane order
+//                          (ballot + popcount), final states; words go to a scratch stack
+//   KC4 tc_layout_kernel   one wave per client: cumulative words per chunk, message size
+//   KC5 tc_scan_kernel     message offsets (exclusive scan over clients)
+//   KC6 tc_pack_kernel     header, tables, states and words into the packed messages
+//   KC7 tc_decode_kernel   one wave per chunk: LDS slot->symbol table, forward steps, words
+//                          read per step in lane order; checks the chunk ends exactly
+// Bytes: KC1 and KC3 read the codes (d per client each), KC3 writes <= 2 B per symbol of
+// scratch, KC6 copies the words; KC7 reads the message and writes d code bytes.
+constexpr int kTcProbBits = 12;
+constexpr uint32_t kTcM = 1u << kTcProbBits;
+constexpr uint32_t kTcL = 1u << 16;
+constexpr int kTcSteps = 1024;
+constexpr uint32_t kTcMagic = 0x31525155u;   // "UQR1"
+constexpr int kTcHistSeg = 65536;
+
+__host__ __device__ inline int tc_lanes(int64_t d) {
+    int64_t w = (d + kTcSteps - 1) / kTcSteps;
+    return (int)(w < 1 ? 1 : (w > 64 ? 64 : w));
+}
+__host__ __device__ inline int64_t tc_nchunks(int64_t d) {
+    const int64_t csz = (int64_t)tc_lanes(d) * kTcSteps;
+    return d > 0 ? (d + csz - 1) / csz : 0;
+}
+__host__ __device__ inline uint64_t tc_align4(uint64_t x) { return (x + 3u) & ~(uint64_t)3u; }
+__host__ __device__ inline uint64_t tc_table_off(int nsym) { return tc_align4(40 + 2 * (uint64_t)nsym); }
+__host__ __device__ inline uint64_t tc_header_bytes(int nsym, int64_t nch, int W) {
+    return tc_table_off(nsym) + 4 * (uint64_t)nch + 4 * (uint64_t)nch * (uint64_t)W;
+}
+__host__ __device__ inline uint64_t tc_bound(int64_t d) {
+    return tc_header_bytes(256, tc_nchunks(d), tc_lanes(d)) + tc_align4(2 * (uint64_t)d);
+}
+__device__ __forceinline__ int tc_sym(int c, bool exact) {       // c: the int8 code as int
+    const int k = c < 0 ? -c - 1 : c;
+    const int neg = c < 0 ? 1 : 0;
+    return 2 * k + (exact ? neg : (neg & (k > 0 ? 1 : 0)));
+}
+__device__ __forceinline__ int8_t tc_code(int s) {
+    const int k = s >> 1;
+    return (s & 1) ? (int8_t)(-k - 1) : (int8_t)k;
+}
+
+struct TcTable {            // per client, in the workspace
+    uint32_t nsym, hdr_bytes, total_words, pad;
+    uint32_t f[256];
+    uint32_t cum[256];
+};
+
+// KC1
+__global__ void __launch_bounds__(256)
+tc_hist_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    const int tid = threadIdx.x;
+    h[tid] = 0u;
+    __syncthreads();
+    const int64_t vec = blockIdx.y;
+    const int64_t b = (int64_t)blockIdx.x * kTcHistSeg;
+    const int64_t e = min(d, b + kTcHistSeg);
+    const int8_t* row = codes + vec * d;
+    const bool al = ((((uintptr_t)(row + b)) & 15u) == 0u);
+    if (al) {
+        int64_t i = b + (int64_t)tid * 16;
+        for (; i + 16 <= e; i += 256 * 16) {
+            const uint4 w = *reinterpret_cast<const uint4*>(row + i);
+            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                atomicAdd(&h[tc_sym((int)(int8_t)((ws[k >> 2] >> (8 * (k & 3))) & 0xFFu), exact != 0)], 1u);
+        }
+        for (; i < e; ++i) atomicAdd(&h[tc_sym((int)row[i], exact != 0)], 1u);   // ragged end: one thread
+    } else {
+        for (int64_t i = b + tid; i < e; i += 256) atomicAdd(&h[tc_sym((int)row[i], exact != 0)], 1u);
+    }
+    __syncthreads();
+    if (h[tid]) atomicAdd(&hist[vec * 256 + tid], h[tid]);
+}
+
+// KC2: one wave per client.
+__global__ void __launch_bounds__(64)
+tc_table_kernel(const uint32_t* __restrict__ hist, int64_t d, TcTable* __restrict__ tabs) {
+    const int64_t vec = blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint32_t* hc = hist + vec * 256;
+    uint32_t c[4], f[4];
+    int smax = -1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int s = lane + 64 * r;
+        c[r] = hc[s];
+        if (c[r]) smax = s;
+    }
+    for (int o = 32; o > 0; o >>= 1) smax = max(smax, __shfl_xor(smax, o, 64));
+    const int nsym = d > 0 ? 2 * (smax >> 1) + 2 : 0;
+    int64_t sum = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        f[r] = c[r] ? (uint32_t)(((uint64_t)c[r] * kTcM) / (uint64_t)d) : 0u;
+        if (c[r] && f[r] == 0u) f[r] = 1u;
+        sum += f[r];
+    }
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    // normalisation (oracle/uq_codec.c uqc_normalize): adjust the most frequent symbol
+    // (lowest index on ties) until the sum is M
+    while (d > 0 && sum != (int64_t)kTcM) {
+        uint32_t key = 0u;                         // (f << 8) | (255 - s): max = largest f, lowest s
+#pragma unroll
+        for (int r = 0; r < 4; ++r) key = max(key, (f[r] << 8) | (uint32_t)(255 - (lane + 64 * r)));
+        for (int o = 32; o > 0; o >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, o, 64));
+        const int best = 255 - (int)(key & 0xFFu);
+        const uint32_t fb = key >> 8;
+        int64_t delta;
+        if (sum < (int64_t)kTcM) {
+            delta = (int64_t)kTcM - sum;
+        } else {
+            delta = sum - (int64_t)kTcM;
+            if (delta > (int64_t)fb - 1) delta = (int64_t)fb - 1;
+            delta = -delta;
+        }
+        if ((best & 63) == lane) f[best >> 6] = (uint32_t)((int64_t)fb + delta);
+        sum += delta;
+    }
+    // cumulative frequencies: symbol s = lane + 64 r, scanned in symbol order
+    TcTable* t = tabs + vec;
+    uint32_t base = 0u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        uint32_t incl = f[r];
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        t->f[lane + 64 * r] = f[r];
+        t->cum[lane + 64 * r] = base + incl - f[r];
+        base += (uint32_t)__shfl((int)incl, 63, 64);
+    }
+    if (lane == 0) {
+        const int64_t nch = tc_nchunks(d);
+        t->nsym = (uint32_t)nsym;
+        t->hdr_bytes = (uint32_t)tc_header_bytes(nsym, nch, tc_lanes(d));
+    }
+}
+
+// KC3: one wave per chunk.  scratch: [n][nch][csz] u16 (the chunk's words end at csz);
+// cwords [n][nch] u32, states [n][nch][W] u32.
+__global__ void __launch_bounds__(64)
+tc_encode_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, const TcTable* __restrict__ tabs,
+                 uint16_t* __restrict__ scratch, uint32_t* __restrict__ cwords, uint32_t* __restrict__ states) {
+    __shared__ uint32_t sf[256], scum[256];
+    const int lane = threadIdx.x;
+    const int64_t vec = blockIdx.y;
+    const int64_t c = blockIdx.x;
+    const TcTable* t = tabs + vec;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sf[lane + 64 * r] = t->f[lane + 64 * r];
+        scum[lane + 64 * r] = t->cum[lane + 64 * r];
+    }
+    __syncthreads();
+    const int W = tc_lanes(d);
+    const int64_t nch = tc_nchunks(d);
+    const int64_t csz = (int64_t)W * kTcSteps;
+    const int64_t base = c * csz;
+    const int64_t len = min(csz, d - base);
+    const int64_t steps = (len + W - 1) / W;
+    const int8_t* row = codes + vec * d + base;
+    uint16_t* stk = scratch + (vec * nch + c) * csz;
+    uint32_t x = kTcL;
+    int64_t ptr = csz;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int64_t st = steps - 1; st >= 0; --st) {
+        const int64_t i = st * W + lane;
+        const bool act = lane < W && i < len;
+        int s = 0;
+        bool need = false;
+        if (act) {
+            s = tc_sym((int)row[i], exact != 0);
+            need = (uint64_t)x >= ((uint64_t)sf[s] << 20);        // ((L >> 12) << 16) * f
+        }
+        const uint64_t mk = __ballot(need);
+        const int k = __popcll(mk);
+        if (need) {
+            stk[ptr - k + __popcll(mk & below)] = (uint16_t)(x & 0xFFFFu);
+            x >>= 16;
+        }
+        ptr -= k;
+        if (act) {
+            const uint32_t fs = sf[s];
+            x = ((x / fs) << kTcProbBits) + (x % fs) + scum[s];
+        }
+    }
+    if (lane < W) states[(vec * nch + c) * W + lane] = x;
+    if (lane == 0) cwords[vec * nch + c] = (uint32_t)(csz - ptr);
+}
+
+// KC4: one wave per client: cumulative words per chunk (in place), total, message size.
+__global__ void __launch_bounds__(64)
+tc_layout_kernel(int64_t d, TcTable* __restrict__ tabs, uint32_t* __restrict__ cwords, uint64_t* __restrict__ sizes) {
+    const int64_t vec = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t nch = tc_nchunks(d);
+    uint32_t* cw = cwords + vec * nch;
+    uint32_t carry = 0u;
+    for (int64_t c0 = 0; c0 < nch; c0 += 64) {
+        const bool in = c0 + lane < nch;
+        uint32_t v = in ? cw[c0 + lane] : 0u;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)v, o, 64);
+            if (lane >= o) v += u;
+        }
+        if (in) cw[c0 + lane] = carry + v;               // words_end[c]
+        carry += (uint32_t)__shfl((int)v, 63, 64);
+    }
+    if (lane == 0) {
+        tabs[vec].total_words = carry;
+        sizes[vec] = (uint64_t)tabs[vec].hdr_bytes + tc_align4(2 * (uint64_t)carry);
+    }
+}
+
+// KC5: offsets[j] = sum of sizes before j, offsets[n] = total (one workgroup).
+__global__ void __launch_bounds__(1024)
+tc_scan_kernel(const uint64_t* __restrict__ sizes, int64_t n, uint64_t* __restrict__ offsets) {
+    __shared__ uint64_t s[1024];
+    __shared__ uint64_t carry;
+    const int tid = threadIdx.x;
+    if (tid == 0) carry = 0ull;
+    __syncthreads();
+    for (int64_t j0 = 0; j0 < n; j0 += 1024) {
+        const uint64_t v = j0 + tid < n ? sizes[j0 + tid] : 0ull;
+        s[tid] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const uint64_t u = tid >= o ? s[tid - o] : 0ull;
+            __syncthreads();
+            s[tid] += u;
+            __syncthreads();
+        }
+        if (j0 + tid < n) offsets[j0 + tid] = carry + s[tid] - v;
+        __syncthreads();
+        if (tid == 0) carry += s[1023];
+        __syncthreads();
+    }
+    if (tid == 0) offsets[n] = carry;
+}
+
+__device__ __forceinline__ void tc_put32(uint8_t* p, uint32_t v) {   // 4-byte aligned
+    *reinterpret_cast<uint32_t*>(p) = v;
+}
+
+// KC6: grid (nch, n), 256 threads.  Chunk c's workgroup writes words_end[c], its states and
+// its words; chunk 0's also the fixed header and the frequency table; the last chunk's the
+// padding word.
+__global__ void __launch_bounds__(256)
+tc_pack_kernel(int64_t d, int64_t m, int exact, const float* __restrict__ l1, const TcTable* __restrict__ tabs,
+               const uint16_t* __restrict__ scratch, const uint32_t* __restrict__ cwords,
+               const uint32_t* __restrict__ states, const uint64_t* __restrict__ offsets, uint8_t* __restrict__ msgs) {
+    const int tid = threadIdx.x;
+    const int64_t vec = blockIdx.y;
+    const int64_t c = blockIdx.x;
+    const TcTable* t = tabs + vec;
+    const int W = tc_lanes(d);
+    const int64_t nch = tc_nchunks(d);
+    const int64_t csz = (int64_t)W * kTcSteps;
+    const int nsym = (int)t->nsym;
+    uint8_t* msg = msgs + offsets[vec];
+    const uint64_t toff = tc_table_off(nsym);
+    uint32_t* wend = reinterpret_cast<uint32_t*>(msg + toff);
+    uint32_t* st = wend + nch;
+    uint16_t* words = reinterpret_cast<uint16_t*>(msg + t->hdr_bytes);
+    if (c < nch) {                                     // (d == 0: a header-only message)
+        const uint32_t* cw = cwords + vec * nch;
+        const uint32_t w0 = c ? cw[c - 1] : 0u, w1 = cw[c];
+        if (tid == 0) wend[c] = w1;
+        if (tid < W) st[c * W + tid] = states[(vec * nch + c) * W + tid];
+        const uint16_t* src = scratch + (vec * nch + c) * csz + (csz - (int64_t)(w1 - w0));
+        for (uint32_t k = tid; k < w1 - w0; k += 256) words[w0 + k] = src[k];
+        if (c == nch - 1 && tid == 0 && (t->total_words & 1u)) words[t->total_words] = 0;
+    }
+    if (c == 0) {
+        if (tid == 0) {
+            const uint64_t size = offsets[vec + 1] - offsets[vec];
+            tc_put32(msg + 0, kTcMagic);
+            tc_put32(msg + 4, 1u | ((uint32_t)(exact ? 1 : 0) << 16));
+            tc_put32(msg + 8, (uint32_t)(uint64_t)d);
+            tc_put32(msg + 12, (uint32_t)((uint64_t)d >> 32));
+            tc_put32(msg + 16, (uint32_t)(uint64_t)m);
+            tc_put32(msg + 20, (uint32_t)((uint64_t)m >> 32));
+            tc_put32(msg + 24, __float_as_uint(l1[vec]));
+            tc_put32(msg + 28, (uint32_t)nsym | ((uint32_t)kTcProbBits << 16) | ((uint32_t)W << 24));
+            tc_put32(msg + 32, (uint32_t)nch);
+            tc_put32(msg + 36, (uint32_t)size);
+        }
+        uint16_t* ft = reinterpret_cast<uint16_t*>(msg + 40);
+        for (int s = tid; s < nsym; s += 256) ft[s] = (uint16_t)t->f[s];
+        if (tid == 0 && (nsym & 1)) ft[nsym] = 0;
+    }
+}
+
+// KC7: grid (nch, n), one wave per chunk.  status[vec] |= 1 bad header, 2 table, 4 words
+// overrun / underrun, 8 final state.
+__global__ void __launch_bounds__(64)
+tc_decode_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offsets, int64_t d,
+                 int8_t* __restrict__ codes, float* __restrict__ l1, int32_t* __restrict__ kmax,
+                 int32_t* __restrict__ status) {
+    __shared__ uint8_t lut[kTcM];
+    __shared__ uint32_t sf[256], scum[257];
+    const int lane = threadIdx.x;
+    const int64_t vec = blockIdx.y;
+    const int64_t c = blockIdx.x;
+    const uint8_t* msg = msgs + offsets[vec];
+    const uint64_t size = offsets[vec + 1] - offsets[vec];
+    const uint32_t* h = reinterpret_cast<const uint32_t*>(msg);
+    const int W = tc_lanes(d);
+    const int64_t nch = tc_nchunks(d);
+    bool ok = size >= 40 && h[0] == kTcMagic && (h[1] & 0xFFFFu) == 1u &&
+              ((uint64_t)h[2] | ((uint64_t)h[3] << 32)) == (uint64_t)d && ((h[7] >> 16) & 0xFFu) == (uint32_t)kTcProbBits &&
+              (int)(h[7] >> 24) == W && (int64_t)h[8] == nch && (uint64_t)h[9] == size;
+    const int nsym = ok ? (int)(h[7] & 0xFFFFu) : 0;
+    ok = ok && nsym <= 256 && (d == 0 || nsym >= 2) && tc_header_bytes(nsym, nch, W) <= size;
+    if (!ok) {
+        if (lane == 0 && c == 0) atomicOr(&status[vec], 1);
+        return;
+    }
+    if (d == 0) {
+        if (lane == 0) {
+            l1[vec] = __uint_as_float(h[6]);
+            kmax[vec] = 0;
+        }
+        return;
+    }
+    const uint16_t* ft = reinterpret_cast<const uint16_t*>(msg + 40);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int s = lane + 64 * r;
+        sf[s] = s < nsym ? (uint32_t)ft[s] : 0u;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t a = 0u;
+        for (int s = 0; s < 256; ++s) {
+            scum[s] = a;
+            a += sf[s];
+        }
+        scum[256] = a;
+    }
+    __syncthreads();
+    if (scum[256] != kTcM) {
+        if (lane == 0) atomicOr(&status[vec], 2);
+        return;
+    }
+    // slot -> symbol: the s with cum[s] <= slot < cum[s+1] (binary search per slot)
+    for (uint32_t j = lane; j < kTcM; j += 64) {
+        int lo = 0, hi = 255;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (scum[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        lut[j] = (uint8_t)lo;
+    }
+    __syncthreads();
+    const uint64_t toff = tc_table_off(nsym);
+    const uint32_t* wend = reinterpret_cast<const uint32_t*>(msg + toff);
+    const uint32_t* st = wend + nch;
+    const uint16_t* words = reinterpret_cast<const uint16_t*>(msg + tc_header_bytes(nsym, nch, W));
+    const uint64_t wmax = (size - tc_header_bytes(nsym, nch, W)) / 2;
+    const int64_t csz = (int64_t)W * kTcSteps;
+    const int64_t base = c * csz;
+    const int64_t len = min(csz, d - base);
+    const int64_t steps = (len + W - 1) / W;
+    uint32_t r = c ? wend[c - 1] : 0u;
+    const uint32_t rend = wend[c];
+    bool bad = rend > wmax || r > rend;
+    uint32_t x = lane < W ? st[c * W + lane] : kTcL;
+    int8_t* row = codes + vec * d + base;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int64_t s0 = 0; s0 < steps && !bad; ++s0) {
+        const int64_t i = s0 * W + lane;
+        const bool act = lane < W && i < len;
+        if (act) {
+            const uint32_t slot = x & (kTcM - 1u);
+            const int s = lut[slot];
+            x = sf[s] * (x >> kTcProbBits) + slot - scum[s];
+            row[i] = tc_code(s);
+        }
+        const bool need = act && x < kTcL;
+        const uint64_t mk = __ballot(need);
+        const uint32_t k = (uint32_t)__popcll(mk);
+        if (r + k > rend) {
+            bad = true;
+            break;
+        }
+        if (need) x = (x << 16) | (uint32_t)words[r + __popcll(mk & below)];
+        r += k;
+    }
+    const bool endbad = __ballot(lane < W && x != kTcL) != 0ull;
+    if (lane == 0) {
+        if (bad || r != rend) atomicOr(&status[vec], 4);
+        else if (endbad) atomicOr(&status[vec], 8);
+        if (c == 0) {
+            l1[vec] = __uint_as_float(h[6]);
+            kmax[vec] = d > 0 ? (nsym - 2) / 2 : 0;
+        }
+    }
+}

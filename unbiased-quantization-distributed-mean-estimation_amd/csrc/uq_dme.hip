@@ -1894,6 +1894,7 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
 #include "uq_biased_kernels.h"
 #include "uq_biased_torch_ties.h"
 #include "uq_eden_kernels.h"
+#include "uq_codec_kernels.h"
 
 // ---- host-side helpers ---------------------------------------------------------------
 thread_local std::string g_err;
@@ -2170,7 +2171,7 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
 
 extern "C" {
 
-int uq_version(void) { return 100; }
+int uq_version(void) { return 101; }
 
 const char* uq_last_error(void) { return g_err.c_str(); }
 
@@ -2437,6 +2438,115 @@ int uq_check_status(void* ws, void* stream) {
     return UQ_OK;
 }
 
+
+// ---- type-message codec "UQR1" (uq_codec_kernels.h) -----------------------------------
+namespace {
+struct TcLayout {
+    size_t hist, tabs, cwords, states, sizes, scratch, total;
+};
+TcLayout tc_layout(int64_t n, int64_t d) {
+    const int64_t nch = tc_nchunks(d);
+    const int64_t csz = (int64_t)tc_lanes(d) * kTcSteps;
+    TcLayout L;
+    size_t o = 0;
+    auto take = [&](size_t b) { const size_t r = o; o += (b + 255) & ~(size_t)255; return r; };
+    L.hist = take((size_t)n * 256 * 4);
+    L.tabs = take((size_t)n * sizeof(TcTable));
+    L.cwords = take((size_t)(n * nch) * 4);
+    L.states = take((size_t)(n * nch) * 64 * 4);
+    L.sizes = take((size_t)n * 8);
+    L.scratch = take((size_t)(n * nch * csz) * 2);
+    L.total = o;
+    return L;
+}
+}  // namespace
+
+int uq_tc_bound(int64_t d, size_t* bytes_out) {
+    if (d < 0 || d > ((int64_t)1 << 31) || !bytes_out) return fail(UQ_E_INVALID, "bad d / null bytes_out");
+    *bytes_out = (size_t)tc_bound(d);
+    return UQ_OK;
+}
+
+int uq_tc_workspace_bytes(int64_t n, int64_t d, size_t* bytes_out) {
+    if (n < 0 || d < 0 || d > ((int64_t)1 << 31) || !bytes_out) return fail(UQ_E_INVALID, "bad n / d / null bytes_out");
+    *bytes_out = tc_layout(n, d).total;
+    return UQ_OK;
+}
+
+int uq_tc_encode(const int8_t* codes, const float* l1, int64_t n, int64_t d, int64_t m, int32_t flags, uint8_t* msgs,
+                 size_t msgs_bytes, uint64_t* offsets, void* ws, size_t ws_bytes, void* stream) {
+    if (n < 0 || d < 0 || d > ((int64_t)1 << 31) || m < 0) return fail(UQ_E_INVALID, "bad n / d / m");
+    if (flags & ~1) return fail(UQ_E_INVALID, "unknown codec flags");
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) return offsets ? hip_check(hipMemsetAsync(offsets, 0, 8, st), "offsets") : fail(UQ_E_INVALID, "null offsets");
+    if (!l1 || !msgs || !offsets || !ws || (d > 0 && !codes)) return fail(UQ_E_INVALID, "null pointer");
+    if (msgs_bytes < (size_t)n * tc_bound(d)) return fail(UQ_E_INVALID, "message buffer below n * uq_tc_bound(d)");
+    const TcLayout L = tc_layout(n, d);
+    if (ws_bytes < L.total) return fail(UQ_E_WORKSPACE, "workspace too small (uq_tc_workspace_bytes)");
+    char* w = (char*)ws;
+    uint32_t* hist = (uint32_t*)(w + L.hist);
+    TcTable* tabs = (TcTable*)(w + L.tabs);
+    uint32_t* cwords = (uint32_t*)(w + L.cwords);
+    uint32_t* states = (uint32_t*)(w + L.states);
+    uint64_t* sizes = (uint64_t*)(w + L.sizes);
+    uint16_t* scratch = (uint16_t*)(w + L.scratch);
+    const int64_t nch = tc_nchunks(d);
+    const int exact = flags & 1;
+    int rc = hip_check(hipMemsetAsync(hist, 0, (size_t)n * 256 * 4, st), "memset hist");
+    if (rc) return rc;
+    for (int64_t j0 = 0; j0 < n; j0 += kMaxGridY) {
+        const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
+        if (d > 0) {
+            hipLaunchKernelGGL(tc_hist_kernel, dim3((unsigned)((d + kTcHistSeg - 1) / kTcHistSeg), (unsigned)nj), dim3(256), 0,
+                               st, codes + j0 * d, d, exact, hist + j0 * 256);
+            if ((rc = hip_check(hipGetLastError(), "tc_hist_kernel launch"))) return rc;
+        }
+        hipLaunchKernelGGL(tc_table_kernel, dim3((unsigned)nj), dim3(64), 0, st, hist + j0 * 256, d, tabs + j0);
+        if ((rc = hip_check(hipGetLastError(), "tc_table_kernel launch"))) return rc;
+        if (nch > 0) {
+            hipLaunchKernelGGL(tc_encode_kernel, dim3((unsigned)nch, (unsigned)nj), dim3(64), 0, st, codes + j0 * d, d, exact,
+                               tabs + j0, scratch + j0 * nch * ((int64_t)tc_lanes(d) * kTcSteps), cwords + j0 * nch,
+                               states + j0 * nch * tc_lanes(d));
+            if ((rc = hip_check(hipGetLastError(), "tc_encode_kernel launch"))) return rc;
+        }
+        hipLaunchKernelGGL(tc_layout_kernel, dim3((unsigned)nj), dim3(64), 0, st, d, tabs + j0, cwords + j0 * nch, sizes + j0);
+        if ((rc = hip_check(hipGetLastError(), "tc_layout_kernel launch"))) return rc;
+    }
+    hipLaunchKernelGGL(tc_scan_kernel, dim3(1), dim3(1024), 0, st, sizes, n, offsets);
+    if ((rc = hip_check(hipGetLastError(), "tc_scan_kernel launch"))) return rc;
+    if (nch == 0) {
+        // d == 0: header-only messages, written by one "chunk" each
+        hipLaunchKernelGGL(tc_pack_kernel, dim3(1, (unsigned)std::min<int64_t>(n, kMaxGridY)), dim3(256), 0, st, d, m, exact,
+                           l1, tabs, scratch, cwords, states, offsets, msgs);
+        return hip_check(hipGetLastError(), "tc_pack_kernel launch");
+    }
+    for (int64_t j0 = 0; j0 < n; j0 += kMaxGridY) {
+        const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
+        hipLaunchKernelGGL(tc_pack_kernel, dim3((unsigned)nch, (unsigned)nj), dim3(256), 0, st, d, m, exact, l1 + j0,
+                           tabs + j0, scratch + j0 * nch * ((int64_t)tc_lanes(d) * kTcSteps), cwords + j0 * nch,
+                           states + j0 * nch * tc_lanes(d), offsets + j0, msgs);
+        if ((rc = hip_check(hipGetLastError(), "tc_pack_kernel launch"))) return rc;
+    }
+    return UQ_OK;
+}
+
+int uq_tc_decode(const uint8_t* msgs, const uint64_t* offsets, int64_t n, int64_t d, int8_t* codes, float* l1,
+                 int32_t* kmax, int32_t* status, void* stream) {
+    if (n < 0 || d < 0 || d > ((int64_t)1 << 31)) return fail(UQ_E_INVALID, "bad n / d");
+    if (n == 0) return UQ_OK;
+    if (!msgs || !offsets || !l1 || !kmax || !status || (d > 0 && !codes)) return fail(UQ_E_INVALID, "null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    int rc = hip_check(hipMemsetAsync(status, 0, (size_t)n * 4, st), "memset status");
+    if (rc) return rc;
+    const int64_t nch = std::max<int64_t>(1, tc_nchunks(d));
+    for (int64_t j0 = 0; j0 < n; j0 += kMaxGridY) {
+        const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
+        hipLaunchKernelGGL(tc_decode_kernel, dim3((unsigned)nch, (unsigned)nj), dim3(64), 0, st, msgs, offsets + j0, d,
+                           codes ? codes + j0 * d : codes, l1 + j0, kmax + j0, status + j0);
+        if ((rc = hip_check(hipGetLastError(), "tc_decode_kernel launch"))) return rc;
+    }
+    return UQ_OK;
+}
 
 int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t T, size_t* bytes_out) {
     if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
