@@ -259,6 +259,7 @@ def main():
         _lib.check(lib.uq_check_status(P(ws), sp), "status after side pipelines")
         side["biased"] = time_biased(uqdme, x, args.bits, T, max(3, args.steps // 2))
         side["eden"] = time_eden(uqdme, x, q, max(3, args.steps // 2))
+        side["codec"] = time_codec(uqdme, pipe, max(3, args.steps // 2))
         if int(torch.count_nonzero(ovf > 127)):
             raise RuntimeError("type-code overflow in the bench workload")
 
@@ -345,6 +346,49 @@ def time_eden(uqdme, x, q, steps):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     return {"ms_per_step": round(ms, 4), "value": round(n / ms / 1e3, 6), "what": "EDEN 1-bit batch (RHT, bins, scale, inverse RHT), no mean"}
+
+
+def time_codec(uqdme, pipe, steps):
+    """Side line: the UQR1 type-message codec (codes.py, uq_tc_*) on the timed steps' type
+    codes: encode (int8 codes -> one rANS message per client) and decode, per batch."""
+    import ctypes
+    from uqdme_amd import _lib
+    lib = _lib.load()
+    n, d = pipe.n, pipe.d
+    b, w = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.check(lib.uq_tc_bound(d, ctypes.byref(b)), "bound")
+    _lib.check(lib.uq_tc_workspace_bytes(n, d, ctypes.byref(w)), "ws")
+    data = torch.empty(n * b.value, dtype=torch.uint8, device="cuda")
+    off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    ws = torch.empty(w.value, dtype=torch.uint8, device="cuda")
+    codes = torch.empty_like(pipe.codes)
+    l1 = torch.empty_like(pipe.l1)
+    km = torch.empty_like(pipe.kmax)
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    sp = torch.cuda.current_stream().cuda_stream
+    P = lambda t: t.data_ptr()  # noqa: E731
+    enc = lambda: _lib.check(lib.uq_tc_encode(P(pipe.codes), P(pipe.l1), n, d, pipe.m, 0, P(data), data.numel(),  # noqa: E731
+                                              P(off), P(ws), ws.numel(), sp), "encode")
+    dec = lambda: _lib.check(lib.uq_tc_decode(P(data), P(off), n, d, P(codes), P(l1), P(km), P(status), sp),  # noqa: E731
+                             "decode")
+    res = {}
+    for name, f in (("encode", enc), ("decode", dec)):
+        f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        res[f"{name}_ms"] = round(e0.elapsed_time(e1) / steps, 4)
+    total = int(off[n].item())
+    ok = bool(torch.equal(codes, torch.where(pipe.codes == -1, torch.zeros_like(pipe.codes), pipe.codes))
+              and int(torch.count_nonzero(status).item()) == 0)
+    res.update({"bits_per_dim": round(8.0 * total / (n * d), 4), "bytes_per_client": round(total / n, 1),
+                "roundtrip_ok": ok, "what": "UQR1 rANS type messages (value mode) of the bench batch's codes, "
+                                            "encode and decode per 1024-client batch"})
+    return res
 
 
 def host_threads() -> int:
