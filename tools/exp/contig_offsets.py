@@ -9,6 +9,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 
 
+def _ok(rc):
+    """HIP return code check that python -O does not strip."""
+    if rc != 0:
+        raise RuntimeError(f"HIP call failed ({rc})")
+    return rc
+
+
 def main():
     import uqdme
     from uqdme_amd import _lib
@@ -20,7 +27,7 @@ def main():
     slack = 512 * MB
     total = 9 * GB + 2 * slack
     p = ctypes.c_void_p()
-    assert hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(total), ctypes.c_uint(0x4)) == 0
+    _ok(hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(total), ctypes.c_uint(0x4)))
     base = p.value
     src = torch.randn(n, d, device="cuda")
     X = torch.rand(n, device="cuda")
@@ -37,8 +44,9 @@ def main():
         x = base
         q = base + 4 * GB + qo
         c = base + 8 * GB + slack + co
-        assert qo < slack and co < slack and c + n * d <= base + total
-        assert hip.hipMemcpy(ctypes.c_void_p(x), ctypes.c_void_p(src.data_ptr()), ctypes.c_size_t(n * d * 4), 3) == 0
+        if not (qo < slack and co < slack and c + n * d <= base + total):
+            raise RuntimeError("carve-out outside the allocation")
+        _ok(hip.hipMemcpy(ctypes.c_void_p(x), ctypes.c_void_p(src.data_ptr()), ctypes.c_size_t(n * d * 4), 3))
         f = lambda: lib.uq_type_unbiased_codes_f32(x, q, c, ovf.data_ptr(), n, d, m, X.data_ptr(), l1.data_ptr(),
                                                    None, 1, ws.data_ptr(), b.value, st)
         for _ in range(2):

@@ -8,6 +8,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 
 
+def _ok(rc):
+    """HIP return code check that python -O does not strip."""
+    if rc != 0:
+        raise RuntimeError(f"HIP call failed ({rc})")
+    return rc
+
+
 def main():
     import uqdme
     from uqdme_amd import _lib
@@ -19,7 +26,7 @@ def main():
 
     def calloc(nbytes):
         p = ctypes.c_void_p()
-        assert hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(nbytes), ctypes.c_uint(0x4)) == 0
+        _ok(hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(nbytes), ctypes.c_uint(0x4)))
         return p.value
     src = torch.randn(n, d, device="cuda")
     X = torch.rand(n, device="cuda")
@@ -38,7 +45,7 @@ def main():
             sp = calloc(S * GB) if S else None
             q = calloc(5 * GB)
             c = q + 4 * GB
-            assert hip.hipMemcpy(ctypes.c_void_p(x), ctypes.c_void_p(src.data_ptr()), ctypes.c_size_t(n * d * 4), 3) == 0
+            _ok(hip.hipMemcpy(ctypes.c_void_p(x), ctypes.c_void_p(src.data_ptr()), ctypes.c_size_t(n * d * 4), 3))
             f = lambda: lib.uq_type_unbiased_codes_f32(x, q, c, ovf.data_ptr(), n, d, m, X.data_ptr(), l1.data_ptr(),
                                                        None, 1, ws.data_ptr(), b.value, st)
             for _ in range(2):

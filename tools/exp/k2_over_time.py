@@ -8,15 +8,35 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 
 
-def clocks():
+def _card():
+    """sysfs card of the active device: the one whose PCI bus id matches torch's device."""
+    try:
+        bus = torch.cuda.get_device_properties(torch.cuda.current_device()).pci_bus_id
+    except Exception:
+        bus = None
+    for p in sorted(glob.glob("/sys/class/drm/card*/device")):
+        try:
+            if bus is not None and os.path.basename(os.path.realpath(p)).endswith(f"{bus:02x}:00.0"):
+                return p
+        except OSError:
+            pass
+    return None
+
+
+def clocks(card):
+    """Current memory / system clock levels of the active device's card, as the flat keys of
+    profiles/r01g_exp_k2_over_time.jsonl (mclk0 / sclk0 = the line marked current).  That
+    file came from an earlier revision which always read card0; this one reads the card of
+    the device under test (empty when sysfs is not readable)."""
     out = {}
-    for f in ("pp_dpm_mclk", "pp_dpm_sclk", "pp_dpm_fclk"):
-        for p in glob.glob(f"/sys/class/drm/card*/device/{f}")[:8]:
-            try:
-                cur = [l.strip() for l in open(p) if l.strip().endswith("*")]
-                out.setdefault(f, []).append(cur[0] if cur else "?")
-            except OSError:
-                pass
+    if card is None:
+        return out
+    for key, f in (("mclk0", "pp_dpm_mclk"), ("sclk0", "pp_dpm_sclk")):
+        try:
+            cur = [l.strip() for l in open(os.path.join(card, f)) if l.strip().endswith("*")]
+            out[key] = cur[0] if cur else "?"
+        except OSError:
+            pass
     return out
 
 
@@ -39,6 +59,7 @@ def main():
     _lib.check(lib.uq_l1_torch_order_f32(x.data_ptr(), n, d, 1, l1.data_ptr(), ws.data_ptr(), b.value, st), "l1")
     f = lambda: lib.uq_type_unbiased_codes_f32(x.data_ptr(), q.data_ptr(), c.data_ptr(), ovf.data_ptr(), n, d, m,
                                                X.data_ptr(), l1.data_ptr(), None, 1, ws.data_ptr(), b.value, st)
+    card = _card()
     t0 = time.time()
     for trial in range(30):
         for _ in range(2):
@@ -51,7 +72,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         print(json.dumps({"trial": trial, "t_s": round(time.time() - t0, 2), "k2_ms": round(e0.elapsed_time(e1) / 5, 4),
-                          "clk": clocks()}), flush=True)
+                          **clocks(card)}), flush=True)
         time.sleep(0.25)
 
 

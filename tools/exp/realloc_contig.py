@@ -9,6 +9,13 @@ sys.path.insert(0, ROOT)
 FLAGS = {"malloc": None, "contig": 0x4}       # hipDeviceMallocContiguous (hip_runtime_api.h)
 
 
+def _ok(rc):
+    """HIP return code check that python -O does not strip."""
+    if rc != 0:
+        raise RuntimeError(f"HIP call failed ({rc})")
+    return rc
+
+
 def main():
     import uqdme
     from uqdme_amd import _lib
@@ -42,7 +49,7 @@ def main():
         except RuntimeError as e:
             print(json.dumps({"trial": trial, "kind": kind, "error": str(e)}), flush=True)
             continue
-        assert hip.hipMemcpy(ctypes.c_void_p(x), ctypes.c_void_p(src.data_ptr()), ctypes.c_size_t(n * d * 4), 3) == 0
+        _ok(hip.hipMemcpy(ctypes.c_void_p(x), ctypes.c_void_p(src.data_ptr()), ctypes.c_size_t(n * d * 4), 3))
         f = lambda: lib.uq_type_unbiased_codes_f32(x, q, c, ovf.data_ptr(), n, d, m, X.data_ptr(), l1.data_ptr(),
                                                    None, 1, ws.data_ptr(), b.value, st)
         for _ in range(2):
