@@ -109,3 +109,19 @@ def test_biased_and_eden_argument_errors(lib):
     assert lib.uq_eden_f32(None, None, 0, 16, 1, None, None, None, None, 0, None) == 0
     assert lib.uq_rht_f32(None, None, -1, 16, 0, None, None, None, 0, None) < 0
     assert lib.uq_rht_signs(None, -1, 16, None, None) < 0
+
+
+def test_codec_sizes_host_only(lib):
+    """uq_tc_bound agrees with the CPU restatement's bound; workspace sizes grow with n, d;
+    bad arguments are rejected (no kernel launched)."""
+    from oracle import uq_oracle_c as C
+    for d in (0, 1, 5, 1023, 1024, 1025, 65536, 65537, 172554, 1 << 20, 3000017):
+        b = ctypes.c_size_t()
+        assert lib.uq_tc_bound(d, ctypes.byref(b)) == 0
+        assert b.value == C.lib().uqc_bound(d), d
+    w1, w2 = ctypes.c_size_t(), ctypes.c_size_t()
+    assert lib.uq_tc_workspace_bytes(4, 1 << 20, ctypes.byref(w1)) == 0
+    assert lib.uq_tc_workspace_bytes(8, 1 << 20, ctypes.byref(w2)) == 0
+    assert w2.value > w1.value >= 4 * 2 * (1 << 20)         # the word scratch: 2 B per symbol
+    assert lib.uq_tc_bound(-1, ctypes.byref(w1)) != 0
+    assert lib.uq_tc_encode(None, None, 1, 10, 5, 2, None, 0, None, None, 0, None) != 0   # unknown flag
