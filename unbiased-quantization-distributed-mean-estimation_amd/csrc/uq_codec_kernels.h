@@ -22,6 +22,7 @@ constexpr uint32_t kTcL = 1u << 16;
 constexpr int kTcSteps = 1024;
 constexpr uint32_t kTcMagic = 0x31525155u;   // "UQR1"
 constexpr int kTcHistSeg = 65536;
+constexpr int kTcRing = 512;                 // decoder word-ring block (u16 words)
 
 __host__ __device__ inline int tc_lanes(int64_t d) {
     int64_t w = (d + kTcSteps - 1) / kTcSteps;
@@ -55,11 +56,16 @@ struct TcTable {            // per client, in the workspace
     uint32_t cum[256];
 };
 
-// KC1
+// KC1.  Symbols are heavily skewed (k = 0 for ~80 % of the coordinates at R = 1), so one LDS
+// atomic per symbol serialises on a few bins.  Symbols 0..7 (counts 0..3) are counted in two
+// registers of four 16-bit fields per lane (a lane sees <= 256 symbols per segment, a wave
+// <= 16384, so the fields never carry), summed over the wave by shuffles; the rare others go
+// to LDS atomics.
 __global__ void __launch_bounds__(256)
 tc_hist_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[256];
     const int tid = threadIdx.x;
+    const int lane = tid & 63;
     h[tid] = 0u;
     __syncthreads();
     const int64_t vec = blockIdx.y;
@@ -67,18 +73,32 @@ tc_hist_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, uint32_t*
     const int64_t e = min(d, b + kTcHistSeg);
     const int8_t* row = codes + vec * d;
     const bool al = ((((uintptr_t)(row + b)) & 15u) == 0u);
+    uint64_t lo = 0ull, hi = 0ull;                   // fields: symbols 0..3 / 4..7
+    auto count = [&](int s) {
+        const uint64_t one = 1ull << (16 * (s & 3));
+        if (s < 4) lo += one;
+        else if (s < 8) hi += one;
+        else atomicAdd(&h[s], 1u);
+    };
     if (al) {
         int64_t i = b + (int64_t)tid * 16;
         for (; i + 16 <= e; i += 256 * 16) {
             const uint4 w = *reinterpret_cast<const uint4*>(row + i);
             const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                atomicAdd(&h[tc_sym((int)(int8_t)((ws[k >> 2] >> (8 * (k & 3))) & 0xFFu), exact != 0)], 1u);
+            for (int k = 0; k < 16; ++k) count(tc_sym((int)(int8_t)((ws[k >> 2] >> (8 * (k & 3))) & 0xFFu), exact != 0));
         }
-        for (; i < e; ++i) atomicAdd(&h[tc_sym((int)row[i], exact != 0)], 1u);   // ragged end: one thread
+        for (; i < e; ++i) count(tc_sym((int)row[i], exact != 0));   // ragged end: one thread
     } else {
-        for (int64_t i = b + tid; i < e; i += 256) atomicAdd(&h[tc_sym((int)row[i], exact != 0)], 1u);
+        for (int64_t i = b + tid; i < e; i += 256) count(tc_sym((int)row[i], exact != 0));
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo += (uint64_t)__shfl_xor((long long)lo, o, 64);
+        hi += (uint64_t)__shfl_xor((long long)hi, o, 64);
+    }
+    if (lane < 8) {
+        const uint32_t c = (uint32_t)(((lane < 4 ? lo : hi) >> (16 * (lane & 3))) & 0xFFFFull);
+        if (c) atomicAdd(&h[lane], c);
     }
     __syncthreads();
     if (h[tid]) atomicAdd(&hist[vec * 256 + tid], h[tid]);
@@ -150,19 +170,39 @@ tc_table_kernel(const uint32_t* __restrict__ hist, int64_t d, TcTable* __restric
 }
 
 // KC3: one wave per chunk.  scratch: [n][nch][csz] u16 (the chunk's words end at csz);
-// cwords [n][nch] u32, states [n][nch][W] u32.
+// cwords [n][nch] u32, states [n][nch][W] u32.  Steps run in reverse in blocks of 16: each
+// lane loads its 16 code bytes of the next block while it encodes the current one.  x / f
+// is floor(x * RU(1/f)) in fp64: exact for x < 2^32 and f <= 2^12 (the product is >= x/f and
+// within 2^-20 of it, while a non-integer x/f is >= 2^-12 below the next integer).
+constexpr int kTcBlk = 16;
+
+__device__ __forceinline__ void tc_load_blk(uint32_t (&b)[kTcBlk], const int8_t* row, int64_t blk, int W, int lane,
+                                            int64_t len) {
+#pragma unroll
+    for (int t = 0; t < kTcBlk; ++t) {
+        const int64_t i = (blk * kTcBlk + t) * W + lane;
+        b[t] = (lane < W && i < len) ? (uint32_t)(uint8_t)row[i] : 0u;
+    }
+}
+
 __global__ void __launch_bounds__(64)
 tc_encode_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, const TcTable* __restrict__ tabs,
                  uint16_t* __restrict__ scratch, uint32_t* __restrict__ cwords, uint32_t* __restrict__ states) {
     __shared__ uint32_t sf[256], scum[256];
+    __shared__ double srcp[256];
     const int lane = threadIdx.x;
     const int64_t vec = blockIdx.y;
     const int64_t c = blockIdx.x;
     const TcTable* t = tabs + vec;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        sf[lane + 64 * r] = t->f[lane + 64 * r];
-        scum[lane + 64 * r] = t->cum[lane + 64 * r];
+        const int s = lane + 64 * r;
+        const uint32_t f = t->f[s];
+        sf[s] = f;
+        scum[s] = t->cum[s];
+        double rc = f ? 1.0 / (double)f : 0.0;                    // RU(1/f): bump an RN result below 1/f
+        if (f && fma(rc, (double)f, -1.0) < 0.0) rc = __longlong_as_double(__double_as_longlong(rc) + 1);
+        srcp[s] = rc;
     }
     __syncthreads();
     const int W = tc_lanes(d);
@@ -176,26 +216,37 @@ tc_encode_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, const T
     uint32_t x = kTcL;
     int64_t ptr = csz;
     const uint64_t below = (1ull << lane) - 1ull;
-    for (int64_t st = steps - 1; st >= 0; --st) {
-        const int64_t i = st * W + lane;
-        const bool act = lane < W && i < len;
-        int s = 0;
-        bool need = false;
-        if (act) {
-            s = tc_sym((int)row[i], exact != 0);
-            need = (uint64_t)x >= ((uint64_t)sf[s] << 20);        // ((L >> 12) << 16) * f
+    const int64_t nblk = (steps + kTcBlk - 1) / kTcBlk;
+    uint32_t cur[kTcBlk], nxt[kTcBlk];
+    tc_load_blk(cur, row, nblk - 1, W, lane, len);
+    for (int64_t blk = nblk - 1; blk >= 0; --blk) {
+        if (blk > 0) tc_load_blk(nxt, row, blk - 1, W, lane, len);
+#pragma unroll
+        for (int tt = kTcBlk - 1; tt >= 0; --tt) {
+            const int64_t st = blk * kTcBlk + tt;
+            if (st >= steps) continue;                                  // uniform
+            const bool act = lane < W && st * W + lane < len;
+            int s = 0;
+            bool need = false;
+            if (act) {
+                s = tc_sym((int)(int8_t)cur[tt], exact != 0);
+                need = (uint64_t)x >= ((uint64_t)sf[s] << 20);        // ((L >> 12) << 16) * f
+            }
+            const uint64_t mk = __ballot(need);
+            const int k = __popcll(mk);
+            if (need) {
+                stk[ptr - k + __popcll(mk & below)] = (uint16_t)(x & 0xFFFFu);
+                x >>= 16;
+            }
+            ptr -= k;
+            if (act) {
+                const uint32_t fs = sf[s];
+                const uint32_t qd = (uint32_t)((double)x * srcp[s]);  // floor(x / fs), exact
+                x = (qd << kTcProbBits) + (x - qd * fs) + scum[s];
+            }
         }
-        const uint64_t mk = __ballot(need);
-        const int k = __popcll(mk);
-        if (need) {
-            stk[ptr - k + __popcll(mk & below)] = (uint16_t)(x & 0xFFFFu);
-            x >>= 16;
-        }
-        ptr -= k;
-        if (act) {
-            const uint32_t fs = sf[s];
-            x = ((x / fs) << kTcProbBits) + (x % fs) + scum[s];
-        }
+#pragma unroll
+        for (int tt = 0; tt < kTcBlk; ++tt) cur[tt] = nxt[tt];
     }
     if (lane < W) states[(vec * nch + c) * W + lane] = x;
     if (lane == 0) cwords[vec * nch + c] = (uint32_t)(csz - ptr);
@@ -312,6 +363,7 @@ tc_decode_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ 
                  int32_t* __restrict__ status) {
     __shared__ uint8_t lut[kTcM];
     __shared__ uint32_t sf[256], scum[257];
+    __shared__ uint16_t ring[2 * kTcRing];           // the chunk's words, two blocks at a time
     const int lane = threadIdx.x;
     const int64_t vec = blockIdx.y;
     const int64_t c = blockIdx.x;
@@ -375,9 +427,32 @@ tc_decode_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ 
     const int64_t base = c * csz;
     const int64_t len = min(csz, d - base);
     const int64_t steps = (len + W - 1) / W;
-    uint32_t r = c ? wend[c - 1] : 0u;
+    const uint32_t r0 = c ? wend[c - 1] : 0u;
     const uint32_t rend = wend[c];
-    bool bad = rend > wmax || r > rend;
+    bool bad = rend > wmax || r0 > rend;
+    const uint32_t nw = bad ? 0u : rend - r0;        // the chunk's words: words[r0 .. rend)
+    const uint16_t* cwp = words + r0;
+    // words stream through an LDS ring of two kTcRing-word blocks: block b sits in slot b & 1;
+    // while the decoder reads blocks cb and cb + 1, block cb + 2 is in flight in registers
+    auto fetch = [&](uint32_t blk, uint16_t (&v)[kTcRing / 64]) {
+#pragma unroll
+        for (int j = 0; j < kTcRing / 64; ++j) {
+            const uint32_t u = blk * kTcRing + (uint32_t)(lane + 64 * j);
+            v[j] = u < nw ? cwp[u] : (uint16_t)0;
+        }
+    };
+    auto put = [&](uint32_t blk, const uint16_t (&v)[kTcRing / 64]) {
+#pragma unroll
+        for (int j = 0; j < kTcRing / 64; ++j) ring[(blk & 1u) * kTcRing + lane + 64 * j] = v[j];
+    };
+    uint16_t pf[kTcRing / 64];
+    fetch(0, pf);
+    put(0, pf);
+    fetch(1, pf);
+    put(1, pf);
+    fetch(2, pf);
+    __syncthreads();
+    uint32_t u = 0, cb = 0;                          // words consumed; the block holding u
     uint32_t x = lane < W ? st[c * W + lane] : kTcL;
     int8_t* row = codes + vec * d + base;
     const uint64_t below = (1ull << lane) - 1ull;
@@ -393,13 +468,24 @@ tc_decode_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ 
         const bool need = act && x < kTcL;
         const uint64_t mk = __ballot(need);
         const uint32_t k = (uint32_t)__popcll(mk);
-        if (r + k > rend) {
+        if (u + k > nw) {
             bad = true;
             break;
         }
-        if (need) x = (x << 16) | (uint32_t)words[r + __popcll(mk & below)];
-        r += k;
+        if (need) {
+            const uint32_t v = u + (uint32_t)__popcll(mk & below);
+            x = (x << 16) | (uint32_t)ring[((v / kTcRing) & 1u) * kTcRing + v % kTcRing];
+        }
+        u += k;
+        if (u / kTcRing != cb) {                     // entered block cb + 1: block cb + 2 into cb's slot
+            ++cb;
+            __syncthreads();                         // every lane is done with block cb - 1
+            put(cb + 1, pf);
+            fetch(cb + 2, pf);
+            __syncthreads();
+        }
     }
+    const uint32_t r = r0 + u;
     const bool endbad = __ballot(lane < W && x != kTcL) != 0ull;
     if (lane == 0) {
         if (bad || r != rend) atomicOr(&status[vec], 4);
