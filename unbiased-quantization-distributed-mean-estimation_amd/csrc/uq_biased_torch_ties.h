@@ -364,10 +364,45 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
     return true;
 }
 
+// The clients KB7 replays, in client order: list[0] = count, list[1 + i] = client.  With one
+// replay per workgroup (up to kTieSlots of them) no workgroup runs two replays back to back,
+// which a client-strided walk did whenever two ambiguous clients shared a residue mod the
+// grid.
+__global__ void __launch_bounds__(1024)
+rez_tie_list_kernel(const RezState* __restrict__ st, int64_t n, uint32_t* __restrict__ list) {
+    __shared__ uint32_t wc[16];
+    __shared__ uint32_t base;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) base = 0u;
+    __syncthreads();
+    for (int64_t j0 = 0; j0 < n; j0 += 1024) {
+        const int64_t j = j0 + tid;
+        bool f = false;
+        if (j < n) {
+            const RezState s = st[j];
+            f = s.kleft != 0 && (s.flags & kRezAmbiguous);
+        }
+        const uint64_t m = __ballot(f);
+        if (lane == 0) wc[w] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t off = base;
+        for (int q = 0; q < w; ++q) off += wc[q];
+        if (f) list[1 + off + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)j;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t t = 0u;
+            for (int q = 0; q < 16; ++q) t += wc[q];
+            base += t;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) list[0] = base;
+}
+
 __global__ void __launch_bounds__(kTieThreads)
 rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
                 RezState* __restrict__ st, uint32_t* __restrict__ tie_bits, uint32_t* __restrict__ qbuf,
-                uint32_t* __restrict__ pos, int64_t n, uint32_t* __restrict__ ctrl) {
+                uint32_t* __restrict__ pos, const uint32_t* __restrict__ list, uint32_t* __restrict__ ctrl) {
     TT_DECL();
     const int64_t dpad = (d + 3) & ~(int64_t)3;              // 16-byte aligned K and I rows
     const Queue A{qbuf + (size_t)blockIdx.x * 2 * dpad, qbuf + (size_t)blockIdx.x * 2 * dpad + dpad};
@@ -378,7 +413,9 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
     __shared__ __attribute__((aligned(16))) uint32_t lK[kTieLdsPairs + 4];
     __shared__ uint32_t lI[kTieLdsPairs];
     __shared__ uint16_t lL[kTieLdsPairs], lR[kTieLdsPairs];
-    for (int64_t vec = blockIdx.x; vec < n; vec += gridDim.x) {
+    const uint32_t nlist = list[0];
+    for (uint32_t li = blockIdx.x; li < nlist; li += gridDim.x) {
+        const int64_t vec = list[1 + li];
         const RezState s = st[vec];
         if (s.kleft == 0 || !(s.flags & kRezAmbiguous)) continue;
         const bool up = s.delta > 0;

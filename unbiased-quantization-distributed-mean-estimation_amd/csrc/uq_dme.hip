@@ -2000,7 +2000,7 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
 // [KB7 slots: keys + indices S x 2d u32][KB7 positions S x 2d u32], S = min(n, kTieSlots)
 struct BiasedLayout {
     size_t part_off, l1_off, msum_off, st_off, hist_off, zn_off, cn_off, cand_off, tcnt_off, bits_off, pairs_off,
-        pos_off, total;
+        pos_off, list_off, total;
     int32_t tiles;
     int32_t slots;
     uint32_t cap;      // candidate capacity per client (compaction of the first-digit bucket)
@@ -2024,7 +2024,8 @@ BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.slots = (int32_t)std::min<int64_t>(n, kTieSlots);
     w.pairs_off = up(w.bits_off + (size_t)n * ((d + 31) / 32) * sizeof(uint32_t));
     w.pos_off = up(w.pairs_off + (size_t)w.slots * 2 * ((d + 3) & ~(int64_t)3) * sizeof(uint32_t) + 16);
-    w.total = up(w.pos_off + (size_t)w.slots * 2 * d * sizeof(uint32_t));
+    w.list_off = up(w.pos_off + (size_t)w.slots * 2 * d * sizeof(uint32_t));
+    w.total = up(w.list_off + (size_t)(n + 1) * sizeof(uint32_t));      // KB7's client list
     return w;
 }
 
@@ -2162,8 +2163,12 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
                       uint32_t* bits, char* wsb, const BiasedLayout& w, hipStream_t st) {
     int rc = hip_check(hipMemsetAsync(bits, 0, (size_t)n * ((d + 31) / 32) * sizeof(uint32_t), st), "memset tie bits");
     if (rc) return rc;
+    uint32_t* list = (uint32_t*)(wsb + w.list_off);
+    hipLaunchKernelGGL(rez_tie_list_kernel, dim3(1), dim3(1024), 0, st, state, n, list);
+    rc = hip_check(hipGetLastError(), "rez_tie_list_kernel launch");
+    if (rc) return rc;
     hipLaunchKernelGGL(rez_ties_kernel, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm, state, bits,
-                       (uint32_t*)(wsb + w.pairs_off), (uint32_t*)(wsb + w.pos_off), n, (uint32_t*)wsb);
+                       (uint32_t*)(wsb + w.pairs_off), (uint32_t*)(wsb + w.pos_off), list, (uint32_t*)wsb);
     return hip_check(hipGetLastError(), "rez_ties_kernel launch");
 }
 
