@@ -327,15 +327,18 @@ __device__ int tt_select_loop(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t o,
     }
 }
 
-// std::nth_element(A, A + nth, A + d) by the whole workgroup (false on an inconsistency).
+// std::nth_element(A, A + nth, A + d) by the whole workgroup (false on an inconsistency),
+// from introselect's state (first, last, depth) -- (0, d, 2 floor(log2 d)) at the start, or
+// where the multi-workgroup levels (KB7a, below) left it.
 __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, int64_t d, int64_t nth,
-                               TieShared& sh, uint32_t* lK, uint32_t* lI, uint16_t* lL, uint16_t* lR) {
+                               TieShared& sh, uint32_t* lK, uint32_t* lI, uint16_t* lL, uint16_t* lR,
+                               int64_t first0, int64_t last0, int depth0) {
     TT_DECL();
     const int tid = threadIdx.x;
     if (tid == 0) {
-        sh.first = 0;
-        sh.last = d;
-        sh.depth = 2 * floor_log2_i64(d);
+        sh.first = first0;
+        sh.last = last0;
+        sh.depth = depth0;
     }
     __syncthreads();
     int r = tt_select_loop<uint32_t>(A, Lpos, Rpos, 0, nth, kTieLdsPairs, sh);
@@ -362,6 +365,269 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
     if (r == 0 && tid == 0) tt_insertion_sort(A, sh.first, sh.last);
     __syncthreads();
     return true;
+}
+
+// ---- KB7a: introselect's first levels over many workgroups ----------------------------
+// The long partitions (range > kTieLevelMin) of all replayed clients run level by level
+// as separate launches over (segments x slots), so every CU works on them instead of one
+// workgroup per client: queue fill; per level the pivot (median of 3 to `first`), stop
+// counts per segment, stop lists in index order, J and the cut, the J swaps.  The element
+// moves are those of tt_partition (the stop lists are defined by index order, not by who
+// scans), so rez_ties_kernel resumes from the saved (first, last, depth) with the same
+// queue it would have built itself.  Slot a serves list entry a (a < kTieSlots).
+constexpr int64_t kTieLevelMin = 65536;     // shorter ranges stay with rez_ties_kernel
+constexpr int kTieSegs = 256;               // segments per partition (one wave each)
+constexpr int kTieFillSegs = 64;            // workgroups per client for the queue fill
+
+struct TieLevelState {
+    int64_t first, last, nth;
+    int64_t J, nL, nR;
+    int32_t depth, active, filled, err;
+    uint32_t piv, pad;
+};
+
+__global__ void __launch_bounds__(256)
+kt_fill_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
+               const RezState* __restrict__ st, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ list,
+               TieLevelState* __restrict__ tls) {
+    const int64_t a = blockIdx.y;
+    const uint32_t nlist = list[0];
+    if (a >= (int64_t)nlist) {                         // unused slot: nothing stale may run
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            tls[a].filled = 0;
+            tls[a].active = 0;
+        }
+        return;
+    }
+    const int64_t vec = list[1 + a];
+    const RezState s = st[vec];
+    const bool up = s.delta > 0;
+    const int64_t k = up ? s.delta : -(int64_t)s.delta;
+    if (k * 64 <= d) {                                 // partial_sort's heap path: rez_ties_kernel alone
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            tls[a].filled = 0;
+            tls[a].active = 0;
+        }
+        return;
+    }
+    const int64_t dpad = (d + 3) & ~(int64_t)3;
+    uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+    uint32_t* I = K + dpad;
+    const DivPlan dp = div_plan(l1[vec]);
+    const float* xv = x + vec * d;
+    const int64_t seg = (((d + kTieFillSegs - 1) / kTieFillSegs) + 3) & ~(int64_t)3;
+    const int64_t b = (int64_t)blockIdx.x * seg, e = min(d, b + seg);
+    for (int64_t i = b + threadIdx.x; i < e; i += 256) {
+        float kp;
+        K[i] = rez_elem(xv[i], dp, fm, up, kp);
+        I[i] = (uint32_t)i;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        TieLevelState t{};
+        t.first = 0;
+        t.last = d;
+        t.nth = k - 1;
+        t.depth = 2 * floor_log2_i64(d);
+        t.filled = 1;
+        tls[a] = t;
+    }
+}
+
+// level step 1 (one thread per slot): the pivot, or retire the slot for this pass
+__global__ void __launch_bounds__(256)
+kt_pivot_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ list,
+                TieLevelState* __restrict__ tls, int slots) {
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= slots) return;
+    TieLevelState& t = tls[a];
+    if (a >= (int)list[0]) {
+        t.active = 0;
+        return;
+    }
+    t.active = t.filled && !t.err && t.depth > 0 && t.last - t.first > kTieLevelMin;
+    if (!t.active) return;
+    const int64_t dpad = (d + 3) & ~(int64_t)3;
+    const Queue A{qbuf + (size_t)a * 2 * dpad, qbuf + (size_t)a * 2 * dpad + dpad};
+    const int64_t mid = t.first + (t.last - t.first) / 2;
+    tt_move_median_to_first(A, t.first, t.first + 1, mid, t.last - 1);
+    t.piv = A.key(t.first);
+}
+
+// segment s of [first, last) for one wave
+__device__ __forceinline__ void kt_seg(const TieLevelState& t, int s, int64_t& s0, int64_t& s1) {
+    const int64_t len = t.last - t.first;
+    const int64_t seg = (((len + kTieSegs - 1) / kTieSegs) + 63) & ~(int64_t)63;
+    s0 = min(t.last, t.first + (int64_t)s * seg);
+    s1 = min(t.last, s0 + seg);
+}
+
+// level step 2: left / right stop counts per segment (cnt [slots][kTieSegs][2])
+__global__ void __launch_bounds__(64)
+kt_count_kernel(int64_t d, const uint32_t* __restrict__ qbuf, const TieLevelState* __restrict__ tls,
+                uint32_t* __restrict__ cnt) {
+    const int a = blockIdx.y, sg = blockIdx.x, lane = threadIdx.x;
+    const TieLevelState& t = tls[a];
+    if (!t.active) return;
+    const int64_t dpad = (d + 3) & ~(int64_t)3;
+    const uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+    int64_t s0, s1;
+    kt_seg(t, sg, s0, s1);
+    uint32_t cl = 0, cr = 0;
+    for (int64_t b = s0; b < s1; b += 64 * kTieU) {
+        uint32_t kk[kTieU];
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int64_t i = b + (int64_t)u * 64 + lane;
+            kk[u] = i < s1 ? K[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int64_t i = b + (int64_t)u * 64 + lane;
+            cl += (i < s1 && i > t.first && kk[u] <= t.piv) ? 1u : 0u;
+            cr += (i < s1 && kk[u] >= t.piv) ? 1u : 0u;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cl += __shfl_xor(cl, o, 64);
+        cr += __shfl_xor(cr, o, 64);
+    }
+    if (lane == 0) {
+        cnt[((size_t)a * kTieSegs + sg) * 2] = cl;
+        cnt[((size_t)a * kTieSegs + sg) * 2 + 1] = cr;
+    }
+}
+
+// level step 3: stop lists in index order
+__global__ void __launch_bounds__(64)
+kt_list_kernel(int64_t d, const uint32_t* __restrict__ qbuf, uint32_t* __restrict__ pos,
+               const TieLevelState* __restrict__ tls, const uint32_t* __restrict__ cnt) {
+    const int a = blockIdx.y, sg = blockIdx.x, lane = threadIdx.x;
+    const TieLevelState& t = tls[a];
+    if (!t.active) return;
+    const int64_t dpad = (d + 3) & ~(int64_t)3;
+    const uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+    uint32_t* Lpos = pos + (size_t)a * 2 * d;
+    uint32_t* Rpos = Lpos + d;
+    uint32_t ol = 0, orr = 0;
+    for (int q = lane; q < sg; q += 64) {
+        ol += cnt[((size_t)a * kTieSegs + q) * 2];
+        orr += cnt[((size_t)a * kTieSegs + q) * 2 + 1];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ol += __shfl_xor(ol, o, 64);
+        orr += __shfl_xor(orr, o, 64);
+    }
+    int64_t s0, s1;
+    kt_seg(t, sg, s0, s1);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int64_t b = s0; b < s1; b += 64 * kTieU) {
+        uint32_t kk[kTieU];
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int64_t i = b + (int64_t)u * 64 + lane;
+            kk[u] = i < s1 ? K[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int64_t i = b + (int64_t)u * 64 + lane;
+            const bool lf = i < s1 && i > t.first && kk[u] <= t.piv;
+            const bool rf = i < s1 && kk[u] >= t.piv;
+            const uint64_t ml = __ballot(lf), mr = __ballot(rf);
+            if (lf) Lpos[ol + __popcll(ml & lt)] = (uint32_t)i;
+            if (rf) Rpos[orr + __popcll(mr & lt)] = (uint32_t)i;
+            ol += (uint32_t)__popcll(ml);
+            orr += (uint32_t)__popcll(mr);
+        }
+    }
+}
+
+// level step 4 (one 256-thread workgroup per slot): J = the largest J with L_J < R_J (R
+// counted from the right), the cut, and introselect's next range -- as tt_partition /
+// tt_select_loop.  Small workgroups, so that the step is dispatched between KB6's
+// workgroups instead of waiting for a whole CU to drain (KB7a runs beside KB6).
+constexpr int kJcutThreads = 256;
+
+__global__ void __launch_bounds__(kJcutThreads)
+kt_jcut_kernel(int64_t d, const uint32_t* __restrict__ pos, TieLevelState* __restrict__ tls,
+               const uint32_t* __restrict__ cnt) {
+    constexpr int kW = kJcutThreads / kWave;
+    __shared__ uint32_t red[2][kW];
+    const int a = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    TieLevelState& t = tls[a];
+    if (!t.active) return;
+    const uint32_t* Lpos = pos + (size_t)a * 2 * d;
+    const uint32_t* Rpos = Lpos + d;
+    uint32_t cl = 0, cr = 0;
+    for (int q = tid; q < kTieSegs; q += kJcutThreads) {
+        cl += cnt[((size_t)a * kTieSegs + q) * 2];
+        cr += cnt[((size_t)a * kTieSegs + q) * 2 + 1];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cl += __shfl_xor(cl, o, 64);
+        cr += __shfl_xor(cr, o, 64);
+    }
+    if (lane == 0) {
+        red[0][w] = cl;
+        red[1][w] = cr;
+    }
+    __syncthreads();
+    uint32_t nL = 0, nR = 0;
+    for (int q = 0; q < kW; ++q) {
+        nL += red[0][q];
+        nR += red[1][q];
+    }
+    int64_t lo = 0, hi = nL < nR ? nL : nR;
+    while (lo < hi) {
+        const int64_t step = (hi - lo + kJcutThreads - 1) / kJcutThreads;
+        const int64_t cand = lo + (int64_t)(tid + 1) * step;
+        const bool f = cand <= hi && (int64_t)Lpos[cand - 1] < (int64_t)Rpos[nR - cand];
+        const int c = __syncthreads_count(f);
+        if (c == 0) {
+            hi = lo + step - 1;
+        } else {
+            lo = lo + (int64_t)c * step;
+            hi = std::min<int64_t>(hi, lo + step - 1);
+        }
+    }
+    if (tid == 0) {
+        const int64_t J = lo;
+        int64_t cut = INT64_MAX;
+        if (J < (int64_t)nL) cut = (int64_t)Lpos[J];
+        if (J > 0) cut = std::min<int64_t>(cut, (int64_t)Rpos[nR - J]);
+        t.J = J;
+        t.nL = nL;
+        t.nR = nR;
+        if (cut <= t.first || cut >= t.last) {
+            t.err = 1;
+        } else {
+            if (cut <= t.nth) t.first = cut; else t.last = cut;
+            t.depth -= 1;
+        }
+    }
+}
+
+// level step 5: the J disjoint swaps
+__global__ void __launch_bounds__(256)
+kt_swap_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ pos,
+               const TieLevelState* __restrict__ tls) {
+    const int a = blockIdx.y;
+    const TieLevelState& t = tls[a];
+    if (!t.active) return;
+    const int64_t dpad = (d + 3) & ~(int64_t)3;
+    uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+    uint32_t* I = K + dpad;
+    const uint32_t* Lpos = pos + (size_t)a * 2 * d;
+    const uint32_t* Rpos = Lpos + d;
+    const int64_t J = t.J, nR = t.nR;
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < J; j += (int64_t)gridDim.x * 256) {
+        const int64_t pa = Lpos[j], pb = Rpos[nR - 1 - j];
+        const uint32_t ka = K[pa], ia = I[pa], kb = K[pb], ib = I[pb];
+        K[pa] = kb; I[pa] = ib;
+        K[pb] = ka; I[pb] = ia;
+    }
 }
 
 // The clients KB7 replays, in client order: list[0] = count, list[1 + i] = client.  With one
@@ -402,7 +668,8 @@ rez_tie_list_kernel(const RezState* __restrict__ st, int64_t n, uint32_t* __rest
 __global__ void __launch_bounds__(kTieThreads)
 rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
                 RezState* __restrict__ st, uint32_t* __restrict__ tie_bits, uint32_t* __restrict__ qbuf,
-                uint32_t* __restrict__ pos, const uint32_t* __restrict__ list, uint32_t* __restrict__ ctrl) {
+                uint32_t* __restrict__ pos, const uint32_t* __restrict__ list, uint32_t* __restrict__ ctrl,
+                const TieLevelState* __restrict__ tls) {
     TT_DECL();
     const int64_t dpad = (d + 3) & ~(int64_t)3;              // 16-byte aligned K and I rows
     const Queue A{qbuf + (size_t)blockIdx.x * 2 * dpad, qbuf + (size_t)blockIdx.x * 2 * dpad + dpad};
@@ -423,9 +690,11 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         const DivPlan dp = div_plan(l1[vec]);
         const float* xv = x + vec * d;
         TT_T0();
+        // resumed: KB7a filled this slot's queue and ran introselect's first levels
+        const bool resumed = tls && li == blockIdx.x && tls[li].filled;
         // queue[j] = (value, j) (TopKImpl.h); 4 coordinates per lane and load
         const bool xv4 = ((uintptr_t)xv & 15u) == 0;
-        for (int64_t i0 = 0; i0 < d; i0 += (int64_t)kTieThreads * 4 * kTieU) {
+        for (int64_t i0 = 0; i0 < (resumed ? 0 : d); i0 += (int64_t)kTieThreads * 4 * kTieU) {
             float4 v[kTieU];
 #pragma unroll
             for (int u = 0; u < kTieU; ++u) {
@@ -470,7 +739,10 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
             if (tid < kWave) tt_heap_select_wave(A, 0, k, d, tid);
             __syncthreads();
         } else {                                            // std::nth_element
-            ok = tt_introselect(A, Lpos, Rpos, d, k - 1, sh, lK, lI, lL, lR);
+            if (resumed && tls[li].err) ok = false;
+            else if (resumed) ok = tt_introselect(A, Lpos, Rpos, d, k - 1, sh, lK, lI, lL, lR, tls[li].first, tls[li].last,
+                                                  tls[li].depth);
+            else ok = tt_introselect(A, Lpos, Rpos, d, k - 1, sh, lK, lI, lL, lR, 0, d, 2 * floor_log2_i64(d));
         }
         uint32_t* bits = tie_bits + vec * ((d + 31) / 32);
         TT_T0();

@@ -2000,7 +2000,7 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
 // [KB7 slots: keys + indices S x 2d u32][KB7 positions S x 2d u32], S = min(n, kTieSlots)
 struct BiasedLayout {
     size_t part_off, l1_off, msum_off, st_off, hist_off, zn_off, cn_off, cand_off, tcnt_off, bits_off, pairs_off,
-        pos_off, list_off, total;
+        pos_off, list_off, tls_off, tcnt2_off, total;
     int32_t tiles;
     int32_t slots;
     uint32_t cap;      // candidate capacity per client (compaction of the first-digit bucket)
@@ -2025,7 +2025,9 @@ BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.pairs_off = up(w.bits_off + (size_t)n * ((d + 31) / 32) * sizeof(uint32_t));
     w.pos_off = up(w.pairs_off + (size_t)w.slots * 2 * ((d + 3) & ~(int64_t)3) * sizeof(uint32_t) + 16);
     w.list_off = up(w.pos_off + (size_t)w.slots * 2 * d * sizeof(uint32_t));
-    w.total = up(w.list_off + (size_t)(n + 1) * sizeof(uint32_t));      // KB7's client list
+    w.tls_off = up(w.list_off + (size_t)(n + 1) * sizeof(uint32_t));    // KB7's client list
+    w.tcnt2_off = up(w.tls_off + (size_t)w.slots * sizeof(TieLevelState));
+    w.total = up(w.tcnt2_off + (size_t)w.slots * kTieSegs * 2 * sizeof(uint32_t));
     return w;
 }
 
@@ -2147,7 +2149,12 @@ int side_stream(SideStream** out) {
     static thread_local bool made[64] = {};
     if (dev < 0 || dev >= 64) return fail(UQ_E_INVALID, "device index out of range");
     if (!made[dev]) {
-        rc = hip_check(hipStreamCreateWithFlags(&cache[dev].s, hipStreamNonBlocking), "create side stream");
+        // the side stream carries short dependent chains (KB7) beside a bandwidth-bound kernel on
+        // the caller's stream: give it the highest priority so its workgroups dispatch first
+        int least = 0, greatest = 0;
+        rc = hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priority range");
+        if (rc) return rc;
+        rc = hip_check(hipStreamCreateWithPriority(&cache[dev].s, hipStreamNonBlocking, greatest), "create side stream");
         if (rc) return rc;
         rc = hip_check(hipEventCreateWithFlags(&cache[dev].fork, hipEventDisableTiming), "create event");
         if (rc) return rc;
@@ -2167,8 +2174,29 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     hipLaunchKernelGGL(rez_tie_list_kernel, dim3(1), dim3(1024), 0, st, state, n, list);
     rc = hip_check(hipGetLastError(), "rez_tie_list_kernel launch");
     if (rc) return rc;
+    uint32_t* qbuf = (uint32_t*)(wsb + w.pairs_off);
+    uint32_t* pos = (uint32_t*)(wsb + w.pos_off);
+    TieLevelState* tls = nullptr;
+    if (d > kTieLevelMin) {
+        // KB7a: introselect's long levels over (segments x slots) workgroups, level by level
+        tls = (TieLevelState*)(wsb + w.tls_off);
+        uint32_t* cnt = (uint32_t*)(wsb + w.tcnt2_off);
+        const unsigned S = (unsigned)w.slots;
+        hipLaunchKernelGGL(kt_fill_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, x, d, l1, fm, state, qbuf, list, tls);
+        if ((rc = hip_check(hipGetLastError(), "kt_fill_kernel launch"))) return rc;
+        int levels = 1;
+        for (int64_t r = d; r > kTieLevelMin; r >>= 1) ++levels;       // ranges roughly halve per level
+        for (int lv = 0; lv < levels; ++lv) {
+            hipLaunchKernelGGL(kt_pivot_kernel, dim3((S + 255) / 256), dim3(256), 0, st, d, qbuf, list, tls, (int)S);
+            hipLaunchKernelGGL(kt_count_kernel, dim3(kTieSegs, S), dim3(64), 0, st, d, qbuf, tls, cnt);
+            hipLaunchKernelGGL(kt_list_kernel, dim3(kTieSegs, S), dim3(64), 0, st, d, qbuf, pos, tls, cnt);
+            hipLaunchKernelGGL(kt_jcut_kernel, dim3(S), dim3(kJcutThreads), 0, st, d, pos, tls, cnt);
+            hipLaunchKernelGGL(kt_swap_kernel, dim3(64, S), dim3(256), 0, st, d, qbuf, pos, tls);
+            if ((rc = hip_check(hipGetLastError(), "KB7a level launch"))) return rc;
+        }
+    }
     hipLaunchKernelGGL(rez_ties_kernel, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm, state, bits,
-                       (uint32_t*)(wsb + w.pairs_off), (uint32_t*)(wsb + w.pos_off), list, (uint32_t*)wsb);
+                       qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)tls);
     return hip_check(hipGetLastError(), "rez_ties_kernel launch");
 }
 
