@@ -9,7 +9,11 @@ followed by the client mean from the codes.  Groups of >= 256 clients use K2's s
 workgroups per client, x read three times: tile sums, maps, outputs), whose re-reads of a
 group of <= 32 clients (<= 128 MiB) are the ones the cache could serve.  If the cache served
 K2's x, interleaved would beat separate at equal G.  Prints one JSON line per case; est is
-checked bit-equal across every arrangement."""
+checked bit-equal across every arrangement.
+
+    python tools/exp/mall_groups.py                 (the timing sweep)
+    python tools/exp/mall_groups.py --one G inter K (K steps of one case, for a --pmc pass:
+                                                      FETCH_SIZE of K2's kernels per step)"""
 import json
 import os
 import sys
@@ -82,6 +86,14 @@ def timeit(G, inter, reps=6):
     torch.cuda.synchronize()
     return a.elapsed_time(b) / reps
 
+
+if len(sys.argv) > 1 and sys.argv[1] == "--one":
+    G, inter, K = int(sys.argv[2]), bool(int(sys.argv[3])), int(sys.argv[4])
+    for _ in range(K):
+        step(G, inter)
+    torch.cuda.synchronize()
+    _lib.check(lib.uq_check_status(P(ws), sp), "status")
+    sys.exit(0)
 
 ref = None
 for G in (1024, 512, 256, 64, 32, 16):
