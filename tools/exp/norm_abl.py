@@ -32,7 +32,8 @@ def run():
     for k in VARIANTS:
         L = ctypes.CDLL(os.path.join(OUT, f"{k}.so"))
         b = ctypes.c_size_t()
-        assert L.uq_eden_workspace_bytes(ctypes.c_int64(n), ctypes.c_int64(d), ctypes.byref(b)) == 0
+        if (L.uq_eden_workspace_bytes(ctypes.c_int64(n), ctypes.c_int64(d), ctypes.byref(b))) != 0:
+            raise RuntimeError('L.uq_eden_workspace_bytes(ctypes.c_int64(n), ctypes.c_int64(d), ctypes.byref(b))' + ' failed')
         ws = torch.zeros(b.value, dtype=torch.uint8, device="cuda")
         signs = torch.ones(d, dtype=torch.int8, device="cuda")
         rows = torch.zeros(n, dtype=torch.int32, device="cuda")
@@ -42,7 +43,8 @@ def run():
         call = lambda: f(x.data_ptr(), n, d, 1, signs.data_ptr(), rows.data_ptr(), bins.data_ptr(), scale.data_ptr(),
                          ws.data_ptr(), b.value, sp)
         for _ in range(2):
-            assert call() == 0
+            if (call()) != 0:
+                raise RuntimeError('call()' + ' failed')
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

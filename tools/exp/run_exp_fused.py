@@ -40,7 +40,8 @@ def main():
         def f():
             rc = ex.exp_fused(P(x), P(q), P(codes), P(ovf), ctypes.c_int64(n), ctypes.c_int64(d), ctypes.c_int64(m),
                               P(X), P(ws), segs, grid, phases, ctypes.c_void_p(st))
-            assert rc == 0
+            if (rc) != 0:
+                raise RuntimeError('rc' + ' failed')
         return f
 
     def timeit(f, k=10):

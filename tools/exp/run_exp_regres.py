@@ -45,7 +45,8 @@ def main():
         def f():
             rc = ex.exp_regres(x.data_ptr(), q.data_ptr(), codes.data_ptr(), n, d, float(m), E, slots, ws.data_ptr(),
                                mode, st, ctypes.byref(used))
-            assert rc == 0, rc
+            if (rc) != 0:
+                raise RuntimeError('rc' + ' failed')
         return f
 
     def timeit(f, k=10):
