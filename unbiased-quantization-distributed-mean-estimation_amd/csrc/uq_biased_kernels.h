@@ -394,14 +394,25 @@ rez_cand_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ c
     if (tid == 0) st[vec] = s;
 }
 
-// KB5: keys equal to the threshold per tile (ambiguous clients only).
+// KB5: keys equal to the threshold per tile (ambiguous clients only).  `list` (torch ties:
+// KB7's client list, ascending; null otherwise): listed clients are replayed, so they need
+// no index-order rank (a failed replay is reported as an internal error).
 template <bool VEC4>
 __global__ void __launch_bounds__(256)
 rez_tiecount_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
-                    const RezState* __restrict__ st, uint32_t* __restrict__ tilecnt, int32_t tiles) {
+                    const RezState* __restrict__ st, uint32_t* __restrict__ tilecnt, int32_t tiles,
+                    const uint32_t* __restrict__ list) {
     const int64_t vec = blockIdx.y;
     const int32_t fl = st[vec].flags;
     if (!(fl & kRezAmbiguous) || (fl & kRezTorchTies)) return;
+    if (list) {                                          // binary search of the sorted list
+        uint32_t lo = 0, hi = list[0];
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (list[1 + mid] < (uint32_t)vec) lo = mid + 1; else hi = mid;
+        }
+        if (lo < list[0] && list[1 + lo] == (uint32_t)vec) return;
+    }
     const uint32_t tau = st[vec].prefix;
     const bool up = st[vec].delta > 0;
     const DivPlan dp = div_plan(l1[vec]);

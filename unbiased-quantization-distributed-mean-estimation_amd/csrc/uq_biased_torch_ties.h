@@ -25,7 +25,8 @@
 // an ambiguous tie are skipped.  Ranges of <= kTieLdsPairs finish in LDS.
 
 constexpr int kTieSlots = 256;       // workgroups (and scratch slots) of KB7: one per CU
-constexpr int kTieThreads = 1024;    // 16 waves per client
+constexpr int kTieThreads = 1024;    // 16 waves per client (full replays)
+constexpr int kTieThreadsLds = 256;  // LDS tails after KB7a: small enough to dispatch beside KB6
 constexpr int kTieWaves = kTieThreads / kWave;
 constexpr int kTieU = 8;             // independent loads in flight per lane
 constexpr int kTieLdsPairs = 4096;   // ranges this short finish in LDS
@@ -176,7 +177,7 @@ __device__ __forceinline__ void tt_scan_segment(const Queue& A, int64_t first, i
 // relative to the queue view; positions listed as PosT).  Each wave lists the stops of
 // its contiguous segment: one counting pass, a 16-entry prefix, one listing pass.
 // Returns the cut, or -1 on an internal inconsistency.
-template <typename PosT>
+template <typename PosT, int NT>
 __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t first, int64_t last,
                                 uint32_t piv, TieShared& sh) {
     TT_DECL();
@@ -186,7 +187,8 @@ __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t 
     // segments start at multiples of 4 (16-byte aligned in the 16-byte aligned view); indices
     // below `first` belong to no stop list
     const int64_t a0 = first & ~(int64_t)3;
-    const int64_t seg = ((((last - a0) + kTieWaves - 1) / kTieWaves) + 4 * kWave - 1) & ~(int64_t)(4 * kWave - 1);
+    constexpr int NW = NT / kWave;
+    const int64_t seg = ((((last - a0) + NW - 1) / NW) + 4 * kWave - 1) & ~(int64_t)(4 * kWave - 1);
     const int64_t s0 = std::min<int64_t>(last, a0 + (int64_t)w * seg);
     const int64_t s1 = std::min<int64_t>(last, s0 + seg);
     uint32_t cl = 0, cr = 0;
@@ -225,7 +227,7 @@ __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t 
     __syncthreads();
     uint32_t ol = 0, orr = 0, nL = 0, nR = 0;
 #pragma unroll
-    for (int q = 0; q < kTieWaves; ++q) {
+    for (int q = 0; q < NW; ++q) {
         const uint32_t a = sh.wl[q], b = sh.wr[q];
         ol += q < w ? a : 0u;
         orr += q < w ? b : 0u;
@@ -245,7 +247,7 @@ __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t 
     // found by a block-parallel search (the predicate holds for a prefix of J).
     int64_t lo = 0, hi = nL < nR ? nL : nR;
     while (lo < hi) {
-        const int64_t step = (hi - lo + kTieThreads - 1) / kTieThreads;
+        const int64_t step = (hi - lo + NT - 1) / NT;
         const int64_t cand = lo + (int64_t)(tid + 1) * step;
         const bool f = cand <= hi && (int64_t)Lpos[cand - 1] < (int64_t)Rpos[nR - cand];
         const int cnt = __syncthreads_count(f);
@@ -262,12 +264,12 @@ __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t 
     if (J < (int64_t)nL) cut = (int64_t)Lpos[J];
     if (J > 0) cut = std::min<int64_t>(cut, (int64_t)Rpos[nR - J]);
     // the J swaps are disjoint pairs: kTieU of them per lane, independent loads
-    for (int64_t j0 = 0; j0 < J; j0 += (int64_t)kTieThreads * kTieU) {
+    for (int64_t j0 = 0; j0 < J; j0 += (int64_t)NT * kTieU) {
         int64_t a[kTieU], b[kTieU];
         uint32_t ka[kTieU], kb[kTieU], ia[kTieU], ib[kTieU];
 #pragma unroll
         for (int u = 0; u < kTieU; ++u) {
-            const int64_t j = j0 + (int64_t)u * kTieThreads + tid;
+            const int64_t j = j0 + (int64_t)u * NT + tid;
             a[u] = j < J ? (int64_t)Lpos[j] : -1;
             b[u] = j < J ? (int64_t)Rpos[nR - 1 - j] : -1;
         }
@@ -292,7 +294,7 @@ __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t 
 // introselect's main loop on the queue view (element i of the vector at view index i - o)
 // while the range is longer than `stop`.  Returns 0 (range now <= stop), 1 (finished
 // through the heap fallback) or -1 (internal inconsistency).
-template <typename PosT>
+template <typename PosT, int NT>
 __device__ int tt_select_loop(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t o, int64_t nth, int64_t stop,
                               TieShared& sh) {
     TT_DECL();
@@ -317,7 +319,7 @@ __device__ int tt_select_loop(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t o,
         }
         __syncthreads();
         TT_ACC(4);
-        const int64_t cut = tt_partition<PosT>(A, Lpos, Rpos, first, last, sh.piv, sh);
+        const int64_t cut = tt_partition<PosT, NT>(A, Lpos, Rpos, first, last, sh.piv, sh);
         if (cut < 0) return -1;
         if (tid == 0) {
             if (cut + o <= nth) sh.first = cut + o; else sh.last = cut + o;
@@ -330,6 +332,7 @@ __device__ int tt_select_loop(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t o,
 // std::nth_element(A, A + nth, A + d) by the whole workgroup (false on an inconsistency),
 // from introselect's state (first, last, depth) -- (0, d, 2 floor(log2 d)) at the start, or
 // where the multi-workgroup levels (KB7a, below) left it.
+template <int NT>
 __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, int64_t d, int64_t nth,
                                TieShared& sh, uint32_t* lK, uint32_t* lI, uint16_t* lL, uint16_t* lR,
                                int64_t first0, int64_t last0, int depth0) {
@@ -341,20 +344,20 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
         sh.depth = depth0;
     }
     __syncthreads();
-    int r = tt_select_loop<uint32_t>(A, Lpos, Rpos, 0, nth, kTieLdsPairs, sh);
+    int r = tt_select_loop<uint32_t, NT>(A, Lpos, Rpos, 0, nth, kTieLdsPairs, sh);
     if (r < 0) return false;
     TT_T0();
     if (r == 0 && sh.last - sh.first > 3) {                // finish the short range in LDS
         const int64_t f0 = sh.first, len = sh.last - sh.first;
-        for (int64_t i = tid; i < len; i += kTieThreads) {
+        for (int64_t i = tid; i < len; i += NT) {
             lK[i] = A.K[f0 + i];
             lI[i] = A.I[f0 + i];
         }
         __syncthreads();
         const Queue L{lK, lI};
-        r = tt_select_loop<uint16_t>(L, lL, lR, f0, nth, 3, sh);
+        r = tt_select_loop<uint16_t, NT>(L, lL, lR, f0, nth, 3, sh);
         __syncthreads();
-        for (int64_t i = tid; i < len; i += kTieThreads) {
+        for (int64_t i = tid; i < len; i += NT) {
             A.K[f0 + i] = lK[i];
             A.I[f0 + i] = lI[i];
         }
@@ -375,7 +378,7 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
 // moves are those of tt_partition (the stop lists are defined by index order, not by who
 // scans), so rez_ties_kernel resumes from the saved (first, last, depth) with the same
 // queue it would have built itself.  Slot a serves list entry a (a < kTieSlots).
-constexpr int64_t kTieLevelMin = 65536;     // shorter ranges stay with rez_ties_kernel
+constexpr int64_t kTieLevelMin = kTieLdsPairs;   // shorter ranges finish in rez_ties_kernel's LDS
 constexpr int kTieSegs = 256;               // segments per partition (one wave each)
 constexpr int kTieFillSegs = 64;            // workgroups per client for the queue fill
 
@@ -383,7 +386,7 @@ struct TieLevelState {
     int64_t first, last, nth;
     int64_t J, nL, nR;
     int32_t depth, active, filled, err;
-    uint32_t piv, pad;
+    uint32_t piv, marked;       // marked: ties at the threshold in [0, first) (kt_mark_kernel)
 };
 
 __global__ void __launch_bounds__(256)
@@ -433,24 +436,39 @@ kt_fill_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__
     }
 }
 
-// level step 1 (one thread per slot): the pivot, or retire the slot for this pass
-__global__ void __launch_bounds__(256)
+// level step 1 (one workgroup, one thread per slot, slots <= kTieSlots): the pivot, or
+// retire the slot; the active slots are compacted into alist (alist[0] = count), so the
+// level's other launches spread over the active slots only and an idle level costs a few
+// short launches.
+constexpr int kTieGrid = 2048;              // workgroups of the per-level launches (4 waves each)
+__global__ void __launch_bounds__(kTieSlots)
 kt_pivot_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ list,
-                TieLevelState* __restrict__ tls, int slots) {
-    const int a = blockIdx.x * 256 + threadIdx.x;
-    if (a >= slots) return;
-    TieLevelState& t = tls[a];
-    if (a >= (int)list[0]) {
-        t.active = 0;
-        return;
+                TieLevelState* __restrict__ tls, int slots, uint32_t* __restrict__ alist) {
+    __shared__ uint32_t wc[kTieSlots / 64];
+    const int a = threadIdx.x, lane = a & 63, w = a >> 6;
+    bool act = false;
+    if (a < slots) {
+        TieLevelState& t = tls[a];
+        act = a < (int)list[0] && t.filled && !t.err && t.depth > 0 && t.last - t.first > kTieLevelMin;
+        t.active = act ? 1 : 0;
+        if (act) {
+            const int64_t dpad = (d + 3) & ~(int64_t)3;
+            const Queue A{qbuf + (size_t)a * 2 * dpad, qbuf + (size_t)a * 2 * dpad + dpad};
+            const int64_t mid = t.first + (t.last - t.first) / 2;
+            tt_move_median_to_first(A, t.first, t.first + 1, mid, t.last - 1);
+            t.piv = A.key(t.first);
+        }
     }
-    t.active = t.filled && !t.err && t.depth > 0 && t.last - t.first > kTieLevelMin;
-    if (!t.active) return;
-    const int64_t dpad = (d + 3) & ~(int64_t)3;
-    const Queue A{qbuf + (size_t)a * 2 * dpad, qbuf + (size_t)a * 2 * dpad + dpad};
-    const int64_t mid = t.first + (t.last - t.first) / 2;
-    tt_move_median_to_first(A, t.first, t.first + 1, mid, t.last - 1);
-    t.piv = A.key(t.first);
+    const uint64_t m = __ballot(act);
+    if (lane == 0) wc[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int q = 0; q < kTieSlots / 64; ++q) {
+        off += q < w ? wc[q] : 0u;
+        tot += wc[q];
+    }
+    if (act) alist[1 + off + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)a;
+    if (a == 0) alist[0] = tot;
 }
 
 // segment s of [first, last) for one wave
@@ -461,84 +479,92 @@ __device__ __forceinline__ void kt_seg(const TieLevelState& t, int s, int64_t& s
     s1 = min(t.last, s0 + seg);
 }
 
-// level step 2: left / right stop counts per segment (cnt [slots][kTieSegs][2])
-__global__ void __launch_bounds__(64)
+// level step 2: left / right stop counts per segment (cnt [slots][kTieSegs][2]); items
+// (active slot, segment) over the grid
+__global__ void __launch_bounds__(256)
 kt_count_kernel(int64_t d, const uint32_t* __restrict__ qbuf, const TieLevelState* __restrict__ tls,
-                uint32_t* __restrict__ cnt) {
-    const int a = blockIdx.y, sg = blockIdx.x, lane = threadIdx.x;
-    const TieLevelState& t = tls[a];
-    if (!t.active) return;
-    const int64_t dpad = (d + 3) & ~(int64_t)3;
-    const uint32_t* K = qbuf + (size_t)a * 2 * dpad;
-    int64_t s0, s1;
-    kt_seg(t, sg, s0, s1);
-    uint32_t cl = 0, cr = 0;
-    for (int64_t b = s0; b < s1; b += 64 * kTieU) {
-        uint32_t kk[kTieU];
+                uint32_t* __restrict__ cnt, const uint32_t* __restrict__ alist) {
+    const int lane = threadIdx.x & 63;
+    const int64_t items = (int64_t)alist[0] * kTieSegs;
+    for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < items; it += (int64_t)gridDim.x * 4) {
+        const int a = (int)alist[1 + it / kTieSegs], sg = (int)(it % kTieSegs);
+        const TieLevelState& t = tls[a];
+        const int64_t dpad = (d + 3) & ~(int64_t)3;
+        const uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+        int64_t s0, s1;
+        kt_seg(t, sg, s0, s1);
+        uint32_t cl = 0, cr = 0;
+        for (int64_t b = s0; b < s1; b += 64 * kTieU) {
+            uint32_t kk[kTieU];
 #pragma unroll
-        for (int u = 0; u < kTieU; ++u) {
-            const int64_t i = b + (int64_t)u * 64 + lane;
-            kk[u] = i < s1 ? K[i] : 0u;
+            for (int u = 0; u < kTieU; ++u) {
+                const int64_t i = b + (int64_t)u * 64 + lane;
+                kk[u] = i < s1 ? K[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kTieU; ++u) {
+                const int64_t i = b + (int64_t)u * 64 + lane;
+                cl += (i < s1 && i > t.first && kk[u] <= t.piv) ? 1u : 0u;
+                cr += (i < s1 && kk[u] >= t.piv) ? 1u : 0u;
+            }
         }
 #pragma unroll
-        for (int u = 0; u < kTieU; ++u) {
-            const int64_t i = b + (int64_t)u * 64 + lane;
-            cl += (i < s1 && i > t.first && kk[u] <= t.piv) ? 1u : 0u;
-            cr += (i < s1 && kk[u] >= t.piv) ? 1u : 0u;
+        for (int o = 32; o > 0; o >>= 1) {
+            cl += __shfl_xor(cl, o, 64);
+            cr += __shfl_xor(cr, o, 64);
         }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        cl += __shfl_xor(cl, o, 64);
-        cr += __shfl_xor(cr, o, 64);
-    }
-    if (lane == 0) {
-        cnt[((size_t)a * kTieSegs + sg) * 2] = cl;
-        cnt[((size_t)a * kTieSegs + sg) * 2 + 1] = cr;
+        if (lane == 0) {
+            cnt[((size_t)a * kTieSegs + sg) * 2] = cl;
+            cnt[((size_t)a * kTieSegs + sg) * 2 + 1] = cr;
+        }
     }
 }
 
 // level step 3: stop lists in index order
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(256)
 kt_list_kernel(int64_t d, const uint32_t* __restrict__ qbuf, uint32_t* __restrict__ pos,
-               const TieLevelState* __restrict__ tls, const uint32_t* __restrict__ cnt) {
-    const int a = blockIdx.y, sg = blockIdx.x, lane = threadIdx.x;
-    const TieLevelState& t = tls[a];
-    if (!t.active) return;
-    const int64_t dpad = (d + 3) & ~(int64_t)3;
-    const uint32_t* K = qbuf + (size_t)a * 2 * dpad;
-    uint32_t* Lpos = pos + (size_t)a * 2 * d;
-    uint32_t* Rpos = Lpos + d;
-    uint32_t ol = 0, orr = 0;
-    for (int q = lane; q < sg; q += 64) {
-        ol += cnt[((size_t)a * kTieSegs + q) * 2];
-        orr += cnt[((size_t)a * kTieSegs + q) * 2 + 1];
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        ol += __shfl_xor(ol, o, 64);
-        orr += __shfl_xor(orr, o, 64);
-    }
-    int64_t s0, s1;
-    kt_seg(t, sg, s0, s1);
+               const TieLevelState* __restrict__ tls, const uint32_t* __restrict__ cnt,
+               const uint32_t* __restrict__ alist) {
+    const int lane = threadIdx.x & 63;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int64_t b = s0; b < s1; b += 64 * kTieU) {
-        uint32_t kk[kTieU];
-#pragma unroll
-        for (int u = 0; u < kTieU; ++u) {
-            const int64_t i = b + (int64_t)u * 64 + lane;
-            kk[u] = i < s1 ? K[i] : 0u;
+    const int64_t items = (int64_t)alist[0] * kTieSegs;
+    for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < items; it += (int64_t)gridDim.x * 4) {
+        const int a = (int)alist[1 + it / kTieSegs], sg = (int)(it % kTieSegs);
+        const TieLevelState& t = tls[a];
+        const int64_t dpad = (d + 3) & ~(int64_t)3;
+        const uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+        uint32_t* Lpos = pos + (size_t)a * 2 * d;
+        uint32_t* Rpos = Lpos + d;
+        uint32_t ol = 0, orr = 0;
+        for (int q = lane; q < sg; q += 64) {
+            ol += cnt[((size_t)a * kTieSegs + q) * 2];
+            orr += cnt[((size_t)a * kTieSegs + q) * 2 + 1];
         }
 #pragma unroll
-        for (int u = 0; u < kTieU; ++u) {
-            const int64_t i = b + (int64_t)u * 64 + lane;
-            const bool lf = i < s1 && i > t.first && kk[u] <= t.piv;
-            const bool rf = i < s1 && kk[u] >= t.piv;
-            const uint64_t ml = __ballot(lf), mr = __ballot(rf);
-            if (lf) Lpos[ol + __popcll(ml & lt)] = (uint32_t)i;
-            if (rf) Rpos[orr + __popcll(mr & lt)] = (uint32_t)i;
-            ol += (uint32_t)__popcll(ml);
-            orr += (uint32_t)__popcll(mr);
+        for (int o = 32; o > 0; o >>= 1) {
+            ol += __shfl_xor(ol, o, 64);
+            orr += __shfl_xor(orr, o, 64);
+        }
+        int64_t s0, s1;
+        kt_seg(t, sg, s0, s1);
+        for (int64_t b = s0; b < s1; b += 64 * kTieU) {
+            uint32_t kk[kTieU];
+#pragma unroll
+            for (int u = 0; u < kTieU; ++u) {
+                const int64_t i = b + (int64_t)u * 64 + lane;
+                kk[u] = i < s1 ? K[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kTieU; ++u) {
+                const int64_t i = b + (int64_t)u * 64 + lane;
+                const bool lf = i < s1 && i > t.first && kk[u] <= t.piv;
+                const bool rf = i < s1 && kk[u] >= t.piv;
+                const uint64_t ml = __ballot(lf), mr = __ballot(rf);
+                if (lf) Lpos[ol + __popcll(ml & lt)] = (uint32_t)i;
+                if (rf) Rpos[orr + __popcll(mr & lt)] = (uint32_t)i;
+                ol += (uint32_t)__popcll(ml);
+                orr += (uint32_t)__popcll(mr);
+            }
         }
     }
 }
@@ -551,12 +577,12 @@ constexpr int kJcutThreads = 256;
 
 __global__ void __launch_bounds__(kJcutThreads)
 kt_jcut_kernel(int64_t d, const uint32_t* __restrict__ pos, TieLevelState* __restrict__ tls,
-               const uint32_t* __restrict__ cnt) {
+               const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ alist) {
     constexpr int kW = kJcutThreads / kWave;
     __shared__ uint32_t red[2][kW];
-    const int a = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (blockIdx.x >= alist[0]) return;
+    const int a = (int)alist[1 + blockIdx.x], tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     TieLevelState& t = tls[a];
-    if (!t.active) return;
     const uint32_t* Lpos = pos + (size_t)a * 2 * d;
     const uint32_t* Rpos = Lpos + d;
     uint32_t cl = 0, cr = 0;
@@ -612,21 +638,92 @@ kt_jcut_kernel(int64_t d, const uint32_t* __restrict__ pos, TieLevelState* __res
 // level step 5: the J disjoint swaps
 __global__ void __launch_bounds__(256)
 kt_swap_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ pos,
-               const TieLevelState* __restrict__ tls) {
-    const int a = blockIdx.y;
+               const TieLevelState* __restrict__ tls, const uint32_t* __restrict__ alist) {
+    // few VGPRs (u32 positions, 4 swaps in flight per lane): this runs beside KB6, whose
+    // 40-VGPR waves leave only small holes to dispatch into.  The grid is dealt out over the
+    // active slots (workgroup b serves slot b mod nA), so a workgroup reads its slot's state
+    // once and strides over that slot's swaps.
+    constexpr int kB = 4;
+    const uint32_t nA = alist[0];
+    if (blockIdx.x >= (gridDim.x / nA) * nA) return;             // also nA == 0
+    const int a = (int)alist[1 + blockIdx.x % nA];
+    const int64_t c = blockIdx.x / nA, C = gridDim.x / nA;
     const TieLevelState& t = tls[a];
-    if (!t.active) return;
     const int64_t dpad = (d + 3) & ~(int64_t)3;
     uint32_t* K = qbuf + (size_t)a * 2 * dpad;
     uint32_t* I = K + dpad;
     const uint32_t* Lpos = pos + (size_t)a * 2 * d;
     const uint32_t* Rpos = Lpos + d;
     const int64_t J = t.J, nR = t.nR;
-    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < J; j += (int64_t)gridDim.x * 256) {
-        const int64_t pa = Lpos[j], pb = Rpos[nR - 1 - j];
-        const uint32_t ka = K[pa], ia = I[pa], kb = K[pb], ib = I[pb];
-        K[pa] = kb; I[pa] = ib;
-        K[pb] = ka; I[pb] = ia;
+    const int tid = threadIdx.x;
+    for (int64_t j0 = c * 256 * kB; j0 < J; j0 += C * 256 * kB) {
+        uint32_t pa[kB], pb[kB], ka[kB], kb[kB], ia[kB], ib[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int64_t j = j0 + (int64_t)u * 256 + tid;
+            pa[u] = j < J ? Lpos[j] : 0u;
+            pb[u] = j < J ? Rpos[nR - 1 - j] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u)
+            if (j0 + (int64_t)u * 256 + tid < J) {
+                ka[u] = K[pa[u]]; ia[u] = I[pa[u]];
+                kb[u] = K[pb[u]]; ib[u] = I[pb[u]];
+            }
+#pragma unroll
+        for (int u = 0; u < kB; ++u)
+            if (j0 + (int64_t)u * 256 + tid < J) {
+                K[pa[u]] = kb[u]; I[pa[u]] = ib[u];
+                K[pb[u]] = ka[u]; I[pb[u]] = ia[u];
+            }
+    }
+}
+
+// After the levels, queue[0, first) is final (introselect only works inside [first, last)):
+// the ties at the threshold there are marked here over (segments x slots) workgroups, so the
+// LDS-tail replay marks only [first, k).
+__global__ void __launch_bounds__(256)
+kt_mark_kernel(int64_t d, const uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ list,
+               const RezState* __restrict__ st, TieLevelState* __restrict__ tls, uint32_t* __restrict__ tie_bits) {
+    __shared__ uint32_t wsum[4];
+    const int64_t a = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    TieLevelState& t = tls[a];
+    if (!t.filled || t.err) return;
+    const int64_t vec = list[1 + a];
+    const uint32_t tau = st[vec].prefix;
+    const int64_t dpad = (d + 3) & ~(int64_t)3;
+    const uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+    const uint32_t* I = K + dpad;
+    uint32_t* bits = tie_bits + vec * ((d + 31) / 32);
+    const int64_t end = t.first;
+    const int64_t seg = (((end + gridDim.x - 1) / gridDim.x) + 255) & ~(int64_t)255;
+    const int64_t b = min(end, (int64_t)blockIdx.x * seg), e = min(end, b + seg);
+    uint32_t mine = 0;
+    for (int64_t p0 = b; p0 < e; p0 += 256 * kTieU) {
+        uint32_t kk[kTieU];
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int64_t p = p0 + (int64_t)u * 256 + tid;
+            kk[u] = p < e ? K[p] : ~tau;
+        }
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int64_t p = p0 + (int64_t)u * 256 + tid;
+            if (p < e && kk[u] == tau) {
+                const uint32_t ii = I[p];
+                atomicOr(&bits[ii >> 5], 1u << (ii & 31));
+                ++mine;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (lane == 0) wsum[w] = mine;
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (tot) atomicAdd(&t.marked, tot);
     }
 }
 
@@ -665,11 +762,15 @@ rez_tie_list_kernel(const RezState* __restrict__ st, int64_t n, uint32_t* __rest
     if (tid == 0) list[0] = base;
 }
 
-__global__ void __launch_bounds__(kTieThreads)
+// NT threads per workgroup.  part 0: every listed client (slots walk the list).  With
+// KB7a's level state `tls`: part 1 finishes the clients KB7a resumed (slot a = list entry a,
+// LDS tails: NT = kTieThreadsLds), part 2 every other listed client.
+template <int NT>
+__global__ void __launch_bounds__(NT)
 rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
                 RezState* __restrict__ st, uint32_t* __restrict__ tie_bits, uint32_t* __restrict__ qbuf,
                 uint32_t* __restrict__ pos, const uint32_t* __restrict__ list, uint32_t* __restrict__ ctrl,
-                const TieLevelState* __restrict__ tls) {
+                const TieLevelState* __restrict__ tls, int part) {
     TT_DECL();
     const int64_t dpad = (d + 3) & ~(int64_t)3;              // 16-byte aligned K and I rows
     const Queue A{qbuf + (size_t)blockIdx.x * 2 * dpad, qbuf + (size_t)blockIdx.x * 2 * dpad + dpad};
@@ -692,13 +793,14 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         TT_T0();
         // resumed: KB7a filled this slot's queue and ran introselect's first levels
         const bool resumed = tls && li == blockIdx.x && tls[li].filled;
+        if ((part == 1 && !resumed) || (part == 2 && resumed)) continue;
         // queue[j] = (value, j) (TopKImpl.h); 4 coordinates per lane and load
         const bool xv4 = ((uintptr_t)xv & 15u) == 0;
-        for (int64_t i0 = 0; i0 < (resumed ? 0 : d); i0 += (int64_t)kTieThreads * 4 * kTieU) {
+        for (int64_t i0 = 0; i0 < (resumed ? 0 : d); i0 += (int64_t)NT * 4 * kTieU) {
             float4 v[kTieU];
 #pragma unroll
             for (int u = 0; u < kTieU; ++u) {
-                const int64_t i = i0 + 4 * ((int64_t)u * kTieThreads + tid);
+                const int64_t i = i0 + 4 * ((int64_t)u * NT + tid);
                 if (xv4 && i + 3 < d) {
                     v[u] = *reinterpret_cast<const float4*>(xv + i);
                 } else {
@@ -710,7 +812,7 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
             }
 #pragma unroll
             for (int u = 0; u < kTieU; ++u) {
-                const int64_t i = i0 + 4 * ((int64_t)u * kTieThreads + tid);
+                const int64_t i = i0 + 4 * ((int64_t)u * NT + tid);
                 if (i >= d) continue;
                 float kp;
                 uint4 kk, ii;
@@ -740,25 +842,27 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
             __syncthreads();
         } else {                                            // std::nth_element
             if (resumed && tls[li].err) ok = false;
-            else if (resumed) ok = tt_introselect(A, Lpos, Rpos, d, k - 1, sh, lK, lI, lL, lR, tls[li].first, tls[li].last,
+            else if (resumed) ok = tt_introselect<NT>(A, Lpos, Rpos, d, k - 1, sh, lK, lI, lL, lR, tls[li].first, tls[li].last,
                                                   tls[li].depth);
-            else ok = tt_introselect(A, Lpos, Rpos, d, k - 1, sh, lK, lI, lL, lR, 0, d, 2 * floor_log2_i64(d));
+            else ok = tt_introselect<NT>(A, Lpos, Rpos, d, k - 1, sh, lK, lI, lL, lR, 0, d, 2 * floor_log2_i64(d));
         }
         uint32_t* bits = tie_bits + vec * ((d + 31) / 32);
         TT_T0();
         if (ok) {
             uint32_t mine = 0;
-            for (int64_t p0 = 0; p0 < k; p0 += (int64_t)kTieThreads * kTieU) {
+            const int64_t pb = resumed ? tls[li].first : 0;   // [0, first) marked by kt_mark_kernel
+            if (resumed && tid == 0) atomicAdd(&sh.marked, tls[li].marked);
+            for (int64_t p0 = pb; p0 < k; p0 += (int64_t)NT * kTieU) {
                 uint32_t kk[kTieU], ii[kTieU];
 #pragma unroll
                 for (int u = 0; u < kTieU; ++u) {
-                    const int64_t p = p0 + (int64_t)u * kTieThreads + tid;
+                    const int64_t p = p0 + (int64_t)u * NT + tid;
                     kk[u] = p < k ? A.K[p] : 0u;
                     ii[u] = p < k ? A.I[p] : 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < kTieU; ++u) {
-                    const int64_t p = p0 + (int64_t)u * kTieThreads + tid;
+                    const int64_t p = p0 + (int64_t)u * NT + tid;
                     if (p < k && kk[u] == s.prefix) {
                         atomicOr(&bits[ii[u] >> 5], 1u << (ii[u] & 31));
                         ++mine;

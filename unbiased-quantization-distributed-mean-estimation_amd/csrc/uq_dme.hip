@@ -2000,7 +2000,7 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
 // [KB7 slots: keys + indices S x 2d u32][KB7 positions S x 2d u32], S = min(n, kTieSlots)
 struct BiasedLayout {
     size_t part_off, l1_off, msum_off, st_off, hist_off, zn_off, cn_off, cand_off, tcnt_off, bits_off, pairs_off,
-        pos_off, list_off, tls_off, tcnt2_off, total;
+        pos_off, list_off, tls_off, tcnt2_off, alist_off, total;
     int32_t tiles;
     int32_t slots;
     uint32_t cap;      // candidate capacity per client (compaction of the first-digit bucket)
@@ -2027,7 +2027,8 @@ BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.list_off = up(w.pos_off + (size_t)w.slots * 2 * d * sizeof(uint32_t));
     w.tls_off = up(w.list_off + (size_t)(n + 1) * sizeof(uint32_t));    // KB7's client list
     w.tcnt2_off = up(w.tls_off + (size_t)w.slots * sizeof(TieLevelState));
-    w.total = up(w.tcnt2_off + (size_t)w.slots * kTieSegs * 2 * sizeof(uint32_t));
+    w.alist_off = up(w.tcnt2_off + (size_t)w.slots * kTieSegs * 2 * sizeof(uint32_t));
+    w.total = up(w.alist_off + (size_t)(kTieSlots + 1) * sizeof(uint32_t));    // KB7a's active slots
     return w;
 }
 
@@ -2166,37 +2167,65 @@ int side_stream(SideStream** out) {
     return UQ_OK;
 }
 
-int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, float fm, RezState* state,
-                      uint32_t* bits, char* wsb, const BiasedLayout& w, hipStream_t st) {
+// KB7 on stream `st`.  Without KB7a (d <= kTieLevelMin) one launch replays every listed
+// client.  With KB7a, the replay's LDS tails run here in small workgroups (part 1) and
+// *tls_out is set: the caller then runs launch_torch_ties_rest (part 2: heap-path clients
+// and list entries beyond the slots) once the output kernel on its own stream is done.
+// KB7's client list and cleared tie bits (before launch_torch_ties and the tie counts).
+int torch_ties_prepare(int64_t n, int64_t d, RezState* state, uint32_t* bits, char* wsb, const BiasedLayout& w,
+                       hipStream_t st) {
     int rc = hip_check(hipMemsetAsync(bits, 0, (size_t)n * ((d + 31) / 32) * sizeof(uint32_t), st), "memset tie bits");
     if (rc) return rc;
+    hipLaunchKernelGGL(rez_tie_list_kernel, dim3(1), dim3(1024), 0, st, state, n, (uint32_t*)(wsb + w.list_off));
+    return hip_check(hipGetLastError(), "rez_tie_list_kernel launch");
+}
+
+int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, float fm, RezState* state,
+                      uint32_t* bits, char* wsb, const BiasedLayout& w, hipStream_t st, const TieLevelState** tls_out) {
+    *tls_out = nullptr;
+    int rc = UQ_OK;
     uint32_t* list = (uint32_t*)(wsb + w.list_off);
-    hipLaunchKernelGGL(rez_tie_list_kernel, dim3(1), dim3(1024), 0, st, state, n, list);
-    rc = hip_check(hipGetLastError(), "rez_tie_list_kernel launch");
-    if (rc) return rc;
     uint32_t* qbuf = (uint32_t*)(wsb + w.pairs_off);
     uint32_t* pos = (uint32_t*)(wsb + w.pos_off);
-    TieLevelState* tls = nullptr;
-    if (d > kTieLevelMin) {
-        // KB7a: introselect's long levels over (segments x slots) workgroups, level by level
-        tls = (TieLevelState*)(wsb + w.tls_off);
-        uint32_t* cnt = (uint32_t*)(wsb + w.tcnt2_off);
-        const unsigned S = (unsigned)w.slots;
-        hipLaunchKernelGGL(kt_fill_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, x, d, l1, fm, state, qbuf, list, tls);
-        if ((rc = hip_check(hipGetLastError(), "kt_fill_kernel launch"))) return rc;
-        int levels = 1;
-        for (int64_t r = d; r > kTieLevelMin; r >>= 1) ++levels;       // ranges roughly halve per level
-        for (int lv = 0; lv < levels; ++lv) {
-            hipLaunchKernelGGL(kt_pivot_kernel, dim3((S + 255) / 256), dim3(256), 0, st, d, qbuf, list, tls, (int)S);
-            hipLaunchKernelGGL(kt_count_kernel, dim3(kTieSegs, S), dim3(64), 0, st, d, qbuf, tls, cnt);
-            hipLaunchKernelGGL(kt_list_kernel, dim3(kTieSegs, S), dim3(64), 0, st, d, qbuf, pos, tls, cnt);
-            hipLaunchKernelGGL(kt_jcut_kernel, dim3(S), dim3(kJcutThreads), 0, st, d, pos, tls, cnt);
-            hipLaunchKernelGGL(kt_swap_kernel, dim3(64, S), dim3(256), 0, st, d, qbuf, pos, tls);
-            if ((rc = hip_check(hipGetLastError(), "KB7a level launch"))) return rc;
-        }
+    if (d <= kTieLevelMin) {
+        hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
+                           state, bits, qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)nullptr, 0);
+        return hip_check(hipGetLastError(), "rez_ties_kernel launch");
     }
-    hipLaunchKernelGGL(rez_ties_kernel, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm, state, bits,
-                       qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)tls);
+    // KB7a: introselect's levels over (segments x slots) workgroups, level by level, down to
+    // ranges that fit the LDS tail
+    TieLevelState* tls = (TieLevelState*)(wsb + w.tls_off);
+    uint32_t* cnt = (uint32_t*)(wsb + w.tcnt2_off);
+    const unsigned S = (unsigned)w.slots;
+    hipLaunchKernelGGL(kt_fill_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, x, d, l1, fm, state, qbuf, list, tls);
+    if ((rc = hip_check(hipGetLastError(), "kt_fill_kernel launch"))) return rc;
+    // a level keeps the side of the cut that holds nth (measured: ranges reach kTieLevelMin
+    // after ~8 levels from 2^20), so enough levels for 0.6 per level, plus two; an idle level
+    // costs five ~5 us launches, and a range still longer goes global in rez_ties_kernel
+    int levels = 2;
+    for (double r = (double)d; r > (double)kTieLevelMin; r *= 0.6) ++levels;
+    uint32_t* alist = (uint32_t*)(wsb + w.alist_off);
+    for (int lv = 0; lv < levels; ++lv) {
+        hipLaunchKernelGGL(kt_pivot_kernel, dim3(1), dim3(kTieSlots), 0, st, d, qbuf, list, tls, (int)S, alist);
+        hipLaunchKernelGGL(kt_count_kernel, dim3(kTieGrid), dim3(256), 0, st, d, qbuf, tls, cnt, alist);
+        hipLaunchKernelGGL(kt_list_kernel, dim3(kTieGrid), dim3(256), 0, st, d, qbuf, pos, tls, cnt, alist);
+        hipLaunchKernelGGL(kt_jcut_kernel, dim3(S), dim3(kJcutThreads), 0, st, d, pos, tls, cnt, alist);
+        hipLaunchKernelGGL(kt_swap_kernel, dim3(kTieGrid), dim3(256), 0, st, d, qbuf, pos, tls, alist);
+        if ((rc = hip_check(hipGetLastError(), "KB7a level launch"))) return rc;
+    }
+    hipLaunchKernelGGL(kt_mark_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, d, qbuf, list, state, tls, bits);
+    if ((rc = hip_check(hipGetLastError(), "kt_mark_kernel launch"))) return rc;
+    hipLaunchKernelGGL(rez_ties_kernel<kTieThreadsLds>, dim3(S), dim3(kTieThreadsLds), 0, st, x, d, l1, fm, state, bits,
+                       qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)tls, 1);
+    *tls_out = tls;
+    return hip_check(hipGetLastError(), "rez_ties_kernel launch");
+}
+
+int launch_torch_ties_rest(const float* x, int64_t d, const float* l1, float fm, RezState* state, uint32_t* bits,
+                           char* wsb, const BiasedLayout& w, const TieLevelState* tls, hipStream_t st) {
+    hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
+                       state, bits, (uint32_t*)(wsb + w.pairs_off), (uint32_t*)(wsb + w.pos_off),
+                       (const uint32_t*)(wsb + w.list_off), (uint32_t*)wsb, tls, 2);
     return hip_check(hipGetLastError(), "rez_ties_kernel launch");
 }
 
@@ -2666,12 +2695,14 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
                                w.tiles, bits, part);
         return hip_check(hipGetLastError(), "rez_output_kernel launch");
     };
-    auto tiecount = [&](hipStream_t ts) {
-        // index-order tie ranks (ambiguous clients that KB7 did not replay)
+    auto tiecount = [&](hipStream_t ts, const uint32_t* list) {
+        // index-order tie ranks (ambiguous clients that KB7 does not replay)
         if (vec4)
-            hipLaunchKernelGGL(rez_tiecount_kernel<true>, tgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles);
+            hipLaunchKernelGGL(rez_tiecount_kernel<true>, tgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles,
+                               list);
         else
-            hipLaunchKernelGGL(rez_tiecount_kernel<false>, tgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles);
+            hipLaunchKernelGGL(rez_tiecount_kernel<false>, tgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles,
+                               list);
         return hip_check(hipGetLastError(), "rez_tiecount_kernel launch");
     };
     if (tie_policy == UQ_TIES_TORCH) {
@@ -2684,20 +2715,30 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         if (rc) return rc;
         rc = hip_check(hipStreamWaitEvent(sb->s, sb->fork, 0), "wait fork");
         if (rc) return rc;
-        rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s);
+        // KB6 for the clients without a tie is enqueued first: the side chain below is ~60
+        // short launches, and the GPU must not idle while the host issues them
+        rc = output(st, 1);
         if (rc) return rc;
-        rc = tiecount(sb->s);
+        rc = torch_ties_prepare(n, d, state, bits, wsb, w, sb->s);
+        if (rc) return rc;
+        // tie counts of unlisted clients first: independent of the replays
+        rc = tiecount(sb->s, (const uint32_t*)(wsb + w.list_off));
+        if (rc) return rc;
+        const TieLevelState* tls = nullptr;
+        rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls);
         if (rc) return rc;
         rc = hip_check(hipEventRecord(sb->join, sb->s), "record join");
         if (rc) return rc;
-        rc = output(st, 1);
-        if (rc) return rc;
         rc = hip_check(hipStreamWaitEvent(st, sb->join, 0), "wait join");
         if (rc) return rc;
+        if (tls) {                       // replays KB7a did not take (full 1024-thread replays)
+            rc = launch_torch_ties_rest(x, d, l1buf, fm, state, bits, wsb, w, tls, st);
+            if (rc) return rc;
+        }
         rc = output(st, 2);
         if (rc) return rc;
     } else {
-        rc = tiecount(st);
+        rc = tiecount(st, nullptr);
         if (rc) return rc;
         rc = output(st, 0);
         if (rc) return rc;
