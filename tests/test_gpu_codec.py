@@ -25,7 +25,8 @@ def _batch(n, d, dist, seed):
 
 
 @pytest.mark.parametrize("n,d,R,dist", [(16, 1024, 1, "normal"), (3, 65537, 2, "laplace"), (5, 172554, 1, "normal"),
-                                        (2, 4099, 4, "normal"), (7, 1, 1, "normal"), (4, 100, 0.5, "laplace")])
+                                        (2, 4099, 4, "normal"), (7, 1, 1, "normal"), (4, 100, 0.5, "laplace"),
+                                        (2, 1 << 20, 1, "normal"), (2, 1 << 20, 2, "laplace")])
 def test_messages_match_cpu_restatement(gpu_ready, n, d, R, dist):
     import uqdme
     x, X = _batch(n, d, dist, n * d)

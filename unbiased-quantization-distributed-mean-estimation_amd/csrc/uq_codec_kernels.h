@@ -56,13 +56,17 @@ struct TcTable {            // per client, in the workspace
     uint32_t cum[256];
 };
 
-// KC1.  Symbols are heavily skewed (k = 0 for ~80 % of the coordinates at R = 1), so one LDS
-// atomic per symbol serialises on a few bins.  Symbols 0..7 (counts 0..3) are counted in two
-// registers of four 16-bit fields per lane (a lane sees <= 256 symbols per segment, a wave
-// <= 16384, so the fields never carry), summed over the wave by shuffles; the rare others go
-// to LDS atomics.
+// KC1: histogram of the int8 CODES (KC2 maps codes to symbols).  Codes are heavily skewed
+// (0 for ~80 % of the coordinates at R = 1, most of the rest in -4..3), so one LDS atomic per
+// byte would serialise on a few bins, and per-byte branches load the CU's one scalar unit.
+// Codes -4..3 are counted branch-free: a SWAR byte add maps them to 0..7, each byte adds
+// 1 << 4q to one of two nibble accumulators (even / odd bytes: <= 8 per pass, no carry),
+// unpacked after every 16 bytes into four registers of two 16-bit fields (bins q and q + 4;
+// a lane sees <= 256 bytes per segment, a wave <= 16384, so no field carries); they are
+// summed over the wave by shuffles.  A lane whose 16 bytes hold another code adds those to
+// LDS atomically (rare).
 __global__ void __launch_bounds__(256)
-tc_hist_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, uint32_t* __restrict__ hist) {
+tc_hist_kernel(const int8_t* __restrict__ codes, int64_t d, uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[256];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -73,32 +77,64 @@ tc_hist_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, uint32_t*
     const int64_t e = min(d, b + kTcHistSeg);
     const int8_t* row = codes + vec * d;
     const bool al = ((((uintptr_t)(row + b)) & 15u) == 0u);
-    uint64_t lo = 0ull, hi = 0ull;                   // fields: symbols 0..3 / 4..7
-    auto count = [&](int s) {
-        const uint64_t one = 1ull << (16 * (s & 3));
-        if (s < 4) lo += one;
-        else if (s < 8) hi += one;
-        else atomicAdd(&h[s], 1u);
+    uint32_t cq[4] = {0u, 0u, 0u, 0u};              // cq[j]: bins j (low half) and j + 4 (high)
+    auto rare_add = [&](uint32_t byte) {
+        if (((byte + 4u) & 0xFFu) >= 8u) atomicAdd(&h[byte], 1u);
+    };
+    auto pass = [&](const uint4& w) {
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+        uint32_t acc[2] = {0u, 0u};
+        uint32_t any = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t t = ((ws[k] & 0x7F7F7F7Fu) + 0x04040404u) ^ (ws[k] & 0x80808080u);   // bytes + 4
+            any |= t & 0xF8F8F8F8u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t q = (t >> (8 * j)) & 0xFFu;
+                acc[j & 1] += q < 8u ? (1u << (4 * q)) : 0u;
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cq[j] += (acc[a] >> (4 * j)) & 0x000F000Fu;
+        if (any) {
+#pragma unroll 1
+            for (int k = 0; k < 16; ++k) rare_add((ws[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+        }
     };
     if (al) {
         int64_t i = b + (int64_t)tid * 16;
-        for (; i + 16 <= e; i += 256 * 16) {
-            const uint4 w = *reinterpret_cast<const uint4*>(row + i);
-            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int k = 0; k < 16; ++k) count(tc_sym((int)(int8_t)((ws[k >> 2] >> (8 * (k & 3))) & 0xFFu), exact != 0));
+        for (; i + 256 * 16 + 16 <= e; i += 2 * 256 * 16) {         // two loads in flight
+            const uint4 w0 = *reinterpret_cast<const uint4*>(row + i);
+            const uint4 w1 = *reinterpret_cast<const uint4*>(row + i + 256 * 16);
+            pass(w0);
+            pass(w1);
         }
-        for (; i < e; ++i) count(tc_sym((int)row[i], exact != 0));   // ragged end: one thread
+        for (; i + 16 <= e; i += 256 * 16) pass(*reinterpret_cast<const uint4*>(row + i));
+        for (; i < e; ++i) {                                          // ragged end: one thread
+            const uint32_t byte = (uint32_t)(uint8_t)row[i];
+            const uint32_t q = (byte + 4u) & 0xFFu;
+            if (q < 8u) cq[q & 3u] += 1u << (16 * (q >> 2));
+            else atomicAdd(&h[byte], 1u);
+        }
     } else {
-        for (int64_t i = b + tid; i < e; i += 256) count(tc_sym((int)row[i], exact != 0));
+        for (int64_t i = b + tid; i < e; i += 256) {
+            const uint32_t byte = (uint32_t)(uint8_t)row[i];
+            const uint32_t q = (byte + 4u) & 0xFFu;
+            if (q < 8u) cq[q & 3u] += 1u << (16 * (q >> 2));
+            else atomicAdd(&h[byte], 1u);
+        }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        lo += (uint64_t)__shfl_xor((long long)lo, o, 64);
-        hi += (uint64_t)__shfl_xor((long long)hi, o, 64);
-    }
-    if (lane < 8) {
-        const uint32_t c = (uint32_t)(((lane < 4 ? lo : hi) >> (16 * (lane & 3))) & 0xFFFFull);
-        if (c) atomicAdd(&h[lane], c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        for (int o = 32; o > 0; o >>= 1) cq[j] += (uint32_t)__shfl_xor((int)cq[j], o, 64);
+    if (lane < 8) {                                   // bin q = lane <-> code q - 4
+        const uint32_t v = lane == 0 ? cq[0] : lane == 1 ? cq[1] : lane == 2 ? cq[2] : lane == 3 ? cq[3]
+                         : lane == 4 ? cq[0] : lane == 5 ? cq[1] : lane == 6 ? cq[2] : cq[3];
+        const uint32_t cnt = (v >> (16 * (lane >> 2))) & 0xFFFFu;
+        if (cnt) atomicAdd(&h[(lane - 4) & 0xFF], cnt);
     }
     __syncthreads();
     if (h[tid]) atomicAdd(&hist[vec * 256 + tid], h[tid]);
@@ -106,16 +142,27 @@ tc_hist_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, uint32_t*
 
 // KC2: one wave per client.
 __global__ void __launch_bounds__(64)
-tc_table_kernel(const uint32_t* __restrict__ hist, int64_t d, TcTable* __restrict__ tabs) {
+tc_table_kernel(const uint32_t* __restrict__ hist, int64_t d, int exact, TcTable* __restrict__ tabs) {
+    __shared__ uint32_t sc[256];
     const int64_t vec = blockIdx.x;
     const int lane = threadIdx.x;
-    const uint32_t* hc = hist + vec * 256;
+    const uint32_t* hc = hist + vec * 256;          // counts per code byte
     uint32_t c[4], f[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sc[lane + 64 * r] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {                   // symbol counts (value mode folds code -1 into 0)
+        const int b = lane + 64 * r;
+        const uint32_t n = hc[b];
+        if (n) atomicAdd(&sc[tc_sym((int)(int8_t)b, exact != 0)], n);
+    }
+    __syncthreads();
     int smax = -1;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int s = lane + 64 * r;
-        c[r] = hc[s];
+        c[r] = sc[s];
         if (c[r]) smax = s;
     }
     for (int o = 32; o > 0; o >>= 1) smax = max(smax, __shfl_xor(smax, o, 64));
@@ -185,37 +232,118 @@ __device__ __forceinline__ void tc_load_blk(uint32_t (&b)[kTcBlk], const int8_t*
     }
 }
 
-__global__ void __launch_bounds__(64)
+__device__ __forceinline__ void tc_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// KC3: grid (ceil(nch / kTcEncWaves), n), one wave per chunk; the waves of a workgroup share
+// the per-symbol constants, one 16-byte LDS entry {x_max, f | cum << 16, RU(1/f)}.  Full
+// chunks (W = 64 lanes x 1024 steps: every chunk of d >= 65536 but a ragged last one) take a
+// branch-free path: each block of 16 steps arrives as one 16-byte load per lane (1 KB per
+// wave, loaded a block ahead) staged in LDS and read back one byte per step; words go to a
+// per-wave LDS ring (non-renormalising lanes write a dummy slot instead of branching) and
+// leave as 8-byte stores per lane, 256 words at a time, tested every 4 steps.  The words,
+// their order and the final states are those of the generic path.
+struct alignas(16) TcEnc {
+    uint32_t xmax;      // renormalise while x > xmax: x >= f << 20 (f = 4096 never)
+    uint32_t fc;        // f | cum << 16
+    double rcp;         // RU(1 / f)
+};
+constexpr int kTcEncWaves = 8;
+constexpr int kTcRingW = 1024;              // encoder word ring per wave (u16), power of two
+constexpr int kTcFlush = 256;               // words per ring flush (one 8-byte store per lane)
+
+__global__ void __launch_bounds__(64 * kTcEncWaves)
 tc_encode_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, const TcTable* __restrict__ tabs,
                  uint16_t* __restrict__ scratch, uint32_t* __restrict__ cwords, uint32_t* __restrict__ states) {
-    __shared__ uint32_t sf[256], scum[256];
-    __shared__ double srcp[256];
-    const int lane = threadIdx.x;
+    __shared__ TcEnc se[256];
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf[kTcEncWaves][kTcBlk * 64];
+    __shared__ __attribute__((aligned(16))) uint16_t ring[kTcEncWaves][kTcRingW + 64];   // + dummy slots
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t vec = blockIdx.y;
-    const int64_t c = blockIdx.x;
     const TcTable* t = tabs + vec;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int s = lane + 64 * r;
-        const uint32_t f = t->f[s];
-        sf[s] = f;
-        scum[s] = t->cum[s];
+    for (int q = tid; q < 256; q += 64 * kTcEncWaves) {
+        const uint32_t f = t->f[q];
         double rc = f ? 1.0 / (double)f : 0.0;                    // RU(1/f): bump an RN result below 1/f
         if (f && fma(rc, (double)f, -1.0) < 0.0) rc = __longlong_as_double(__double_as_longlong(rc) + 1);
-        srcp[s] = rc;
+        TcEnc e;
+        e.xmax = f >= 4096u ? 0xFFFFFFFFu : (f << 20) - 1u;
+        e.fc = f | (t->cum[q] << 16);
+        e.rcp = rc;
+        se[q] = e;
     }
     __syncthreads();
     const int W = tc_lanes(d);
     const int64_t nch = tc_nchunks(d);
+    const int64_t c = (int64_t)blockIdx.x * kTcEncWaves + wv;
+    if (c >= nch) return;                                           // no workgroup barriers below
     const int64_t csz = (int64_t)W * kTcSteps;
     const int64_t base = c * csz;
     const int64_t len = min(csz, d - base);
-    const int64_t steps = (len + W - 1) / W;
     const int8_t* row = codes + vec * d + base;
     uint16_t* stk = scratch + (vec * nch + c) * csz;
     uint32_t x = kTcL;
-    int64_t ptr = csz;
     const uint64_t below = (1ull << lane) - 1ull;
+    if (W == 64 && len == csz) {
+        uint8_t* sb = sbuf[wv];
+        uint16_t* rg = ring[wv];
+        // block b holds steps 16b .. 16b+15: bytes [1024 b, 1024 b + 1024) of the chunk
+        const uint4* rv = reinterpret_cast<const uint4*>(row);
+        const bool al = (((uintptr_t)row) & 15u) == 0u;
+        auto load = [&](int b) -> uint4 {
+            if (al) return rv[b * 64 + lane];
+            const int8_t* p = row + (int64_t)b * 1024 + 16 * lane;
+            uint32_t w4[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                w4[q] = (uint32_t)(uint8_t)p[4 * q] | ((uint32_t)(uint8_t)p[4 * q + 1] << 8) |
+                        ((uint32_t)(uint8_t)p[4 * q + 2] << 16) | ((uint32_t)(uint8_t)p[4 * q + 3] << 24);
+            return make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        };
+        constexpr int nblk = kTcSteps / kTcBlk;                     // 64
+        int ptr = (int)csz, fl = (int)csz;                          // words [ptr, fl) are in the ring
+        uint4 nx = load(nblk - 1);
+        for (int b = nblk - 1; b >= 0; --b) {
+            tc_wave_sync();
+            reinterpret_cast<uint4*>(sb)[lane] = nx;
+            tc_wave_sync();
+            if (b > 0) nx = load(b - 1);
+#pragma unroll
+            for (int g = 3; g >= 0; --g) {
+#pragma unroll
+                for (int tt = 4 * g + 3; tt >= 4 * g; --tt) {
+                    const TcEnc e = se[tc_sym((int)(int8_t)sb[tt * 64 + lane], exact != 0)];
+                    const bool need = x > e.xmax;
+                    const uint64_t mk = __ballot(need);
+                    const int k = __popcll(mk);
+                    const int slot = need ? ((ptr - k + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u))) & (kTcRingW - 1))
+                                          : kTcRingW + lane;
+                    rg[slot] = (uint16_t)(x & 0xFFFFu);
+                    x = need ? x >> 16 : x;
+                    ptr -= k;
+                    const uint32_t f = e.fc & 0xFFFFu;
+                    const uint32_t qd = (uint32_t)((double)x * e.rcp);   // floor(x / f), exact
+                    x = (qd << kTcProbBits) + (x - qd * f) + (e.fc >> 16);
+                }
+                if (fl - ptr >= kTcFlush) {                           // uniform; pending <= 256 + 7 + 256
+                    tc_wave_sync();
+                    const int o = fl - kTcFlush;                      // multiple of 4: 8-byte aligned
+                    const uint2 w = *reinterpret_cast<const uint2*>(&rg[(o + 4 * lane) & (kTcRingW - 1)]);
+                    *reinterpret_cast<uint2*>(stk + o + 4 * lane) = w;
+                    fl = o;
+                }
+            }
+        }
+        tc_wave_sync();
+        for (int p = ptr + lane; p < fl; p += 64) stk[p] = rg[p & (kTcRingW - 1)];
+        states[(vec * nch + c) * W + lane] = x;
+        if (lane == 0) cwords[vec * nch + c] = (uint32_t)(csz - ptr);
+        return;
+    }
+    const int64_t steps = (len + W - 1) / W;
+    int64_t ptr = csz;
     const int64_t nblk = (steps + kTcBlk - 1) / kTcBlk;
     uint32_t cur[kTcBlk], nxt[kTcBlk];
     tc_load_blk(cur, row, nblk - 1, W, lane, len);
@@ -230,7 +358,7 @@ tc_encode_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, const T
             bool need = false;
             if (act) {
                 s = tc_sym((int)(int8_t)cur[tt], exact != 0);
-                need = (uint64_t)x >= ((uint64_t)sf[s] << 20);        // ((L >> 12) << 16) * f
+                need = x > se[s].xmax;
             }
             const uint64_t mk = __ballot(need);
             const int k = __popcll(mk);
@@ -240,9 +368,10 @@ tc_encode_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, const T
             }
             ptr -= k;
             if (act) {
-                const uint32_t fs = sf[s];
-                const uint32_t qd = (uint32_t)((double)x * srcp[s]);  // floor(x / fs), exact
-                x = (qd << kTcProbBits) + (x - qd * fs) + scum[s];
+                const TcEnc e = se[s];
+                const uint32_t f = e.fc & 0xFFFFu;
+                const uint32_t qd = (uint32_t)((double)x * e.rcp);  // floor(x / f), exact
+                x = (qd << kTcProbBits) + (x - qd * f) + (e.fc >> 16);
             }
         }
 #pragma unroll
@@ -355,69 +484,80 @@ tc_pack_kernel(int64_t d, int64_t m, int exact, const float* __restrict__ l1, co
     }
 }
 
-// KC7: grid (nch, n), one wave per chunk.  status[vec] |= 1 bad header, 2 table, 4 words
-// overrun / underrun, 8 final state.
-__global__ void __launch_bounds__(64)
+// KC7: grid (ceil(nch / kTcDecWaves), n), one wave per chunk; the waves of a workgroup
+// share the client's slot table.  status[vec] |= 1 bad header, 2 table, 4 words overrun /
+// underrun, 8 final state.
+//   Slot table: one u32 per slot = code | (f - 1) << 8 | (slot - cum[s]) << 20, so a step is
+//   one LDS read (x' = f (x >> 12) + slot - cum[s]) before the renormalisation read.
+//   Words: a per-wave LDS ring of kTcDecRing words (word v in slot v mod kTcDecRing),
+//   refilled 256 words at a time from registers loaded one refill ahead.  Full chunks (W =
+//   64, 1024 steps) run groups of 4 steps: before a group the ring holds every word it can
+//   take (<= 256) and the overrun test is made once; inside, no branches (the scalar unit,
+//   one per CU, bounded the branchy form).  Codes of 16 steps (1 KB) are staged in LDS and
+//   leave as one 16-byte store per lane.  Other chunks take the checked step by step path.
+constexpr int kTcDecWaves = 8;
+constexpr int kTcDecRing = 1024;            // ring words per wave
+constexpr int kTcDecFill = 256;             // words per refill (4 per lane)
+
+__global__ void __launch_bounds__(64 * kTcDecWaves)
 tc_decode_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offsets, int64_t d,
                  int8_t* __restrict__ codes, float* __restrict__ l1, int32_t* __restrict__ kmax,
                  int32_t* __restrict__ status) {
-    __shared__ uint8_t lut[kTcM];
+    __shared__ uint32_t tab[kTcM];
     __shared__ uint32_t sf[256], scum[257];
-    __shared__ uint16_t ring[2 * kTcRing];           // the chunk's words, two blocks at a time
-    const int lane = threadIdx.x;
+    __shared__ uint16_t ring[kTcDecWaves][kTcDecRing];
+    __shared__ __attribute__((aligned(16))) uint8_t ob[kTcDecWaves][kTcBlk * 64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t vec = blockIdx.y;
-    const int64_t c = blockIdx.x;
     const uint8_t* msg = msgs + offsets[vec];
     const uint64_t size = offsets[vec + 1] - offsets[vec];
     const uint32_t* h = reinterpret_cast<const uint32_t*>(msg);
     const int W = tc_lanes(d);
     const int64_t nch = tc_nchunks(d);
+    const int64_t c = (int64_t)blockIdx.x * kTcDecWaves + wv;
     bool ok = size >= 40 && h[0] == kTcMagic && (h[1] & 0xFFFFu) == 1u &&
               ((uint64_t)h[2] | ((uint64_t)h[3] << 32)) == (uint64_t)d && ((h[7] >> 16) & 0xFFu) == (uint32_t)kTcProbBits &&
               (int)(h[7] >> 24) == W && (int64_t)h[8] == nch && (uint64_t)h[9] == size;
     const int nsym = ok ? (int)(h[7] & 0xFFFFu) : 0;
     ok = ok && nsym <= 256 && (d == 0 || nsym >= 2) && tc_header_bytes(nsym, nch, W) <= size;
-    if (!ok) {
-        if (lane == 0 && c == 0) atomicOr(&status[vec], 1);
+    if (!ok) {                                                      // uniform over the workgroup
+        if (tid == 0 && blockIdx.x == 0) atomicOr(&status[vec], 1);
         return;
     }
     if (d == 0) {
-        if (lane == 0) {
+        if (tid == 0) {
             l1[vec] = __uint_as_float(h[6]);
             kmax[vec] = 0;
         }
         return;
     }
     const uint16_t* ft = reinterpret_cast<const uint16_t*>(msg + 40);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int s = lane + 64 * r;
-        sf[s] = s < nsym ? (uint32_t)ft[s] : 0u;
-    }
+    for (int q = tid; q < 256; q += 64 * kTcDecWaves) sf[q] = q < nsym ? (uint32_t)ft[q] : 0u;
     __syncthreads();
-    if (lane == 0) {
+    if (tid == 0) {
         uint32_t a = 0u;
-        for (int s = 0; s < 256; ++s) {
-            scum[s] = a;
-            a += sf[s];
+        for (int q = 0; q < 256; ++q) {
+            scum[q] = a;
+            a += sf[q];
         }
         scum[256] = a;
     }
     __syncthreads();
     if (scum[256] != kTcM) {
-        if (lane == 0) atomicOr(&status[vec], 2);
+        if (tid == 0 && blockIdx.x == 0) atomicOr(&status[vec], 2);
         return;
     }
-    // slot -> symbol: the s with cum[s] <= slot < cum[s+1] (binary search per slot)
-    for (uint32_t j = lane; j < kTcM; j += 64) {
+    // slot -> (code, f - 1, slot - cum[s]): the s with cum[s] <= slot < cum[s+1]
+    for (uint32_t j = tid; j < kTcM; j += 64 * kTcDecWaves) {
         int lo = 0, hi = 255;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if (scum[mid] <= j) lo = mid; else hi = mid - 1;
         }
-        lut[j] = (uint8_t)lo;
+        tab[j] = (uint32_t)(uint8_t)tc_code(lo) | ((sf[lo] - 1u) << 8) | ((j - scum[lo]) << 20);
     }
     __syncthreads();
+    if (c >= nch) return;                                           // no workgroup barriers below
     const uint64_t toff = tc_table_off(nsym);
     const uint32_t* wend = reinterpret_cast<const uint32_t*>(msg + toff);
     const uint32_t* st = wend + nch;
@@ -432,57 +572,83 @@ tc_decode_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ 
     bool bad = rend > wmax || r0 > rend;
     const uint32_t nw = bad ? 0u : rend - r0;        // the chunk's words: words[r0 .. rend)
     const uint16_t* cwp = words + r0;
-    // words stream through an LDS ring of two kTcRing-word blocks: block b sits in slot b & 1;
-    // while the decoder reads blocks cb and cb + 1, block cb + 2 is in flight in registers
-    auto fetch = [&](uint32_t blk, uint16_t (&v)[kTcRing / 64]) {
+    uint16_t* rg = ring[wv];
+    constexpr int kPF = kTcDecFill / 64;
+    uint16_t pf[kPF];
+    uint32_t fu = 0;                                 // words [fu - kTcDecRing, fu) are in the ring
+    auto fetch = [&]() {                             // pf = words [fu, fu + kTcDecFill)
 #pragma unroll
-        for (int j = 0; j < kTcRing / 64; ++j) {
-            const uint32_t u = blk * kTcRing + (uint32_t)(lane + 64 * j);
-            v[j] = u < nw ? cwp[u] : (uint16_t)0;
+        for (int j = 0; j < kPF; ++j) {
+            const uint32_t v = fu + (uint32_t)(lane + 64 * j);
+            pf[j] = v < nw ? cwp[v] : (uint16_t)0;
         }
     };
-    auto put = [&](uint32_t blk, const uint16_t (&v)[kTcRing / 64]) {
+    auto refill = [&]() {
+        tc_wave_sync();
 #pragma unroll
-        for (int j = 0; j < kTcRing / 64; ++j) ring[(blk & 1u) * kTcRing + lane + 64 * j] = v[j];
+        for (int j = 0; j < kPF; ++j) rg[(fu + (uint32_t)(lane + 64 * j)) & (kTcDecRing - 1)] = pf[j];
+        fu += kTcDecFill;
+        fetch();
+        tc_wave_sync();
     };
-    uint16_t pf[kTcRing / 64];
-    fetch(0, pf);
-    put(0, pf);
-    fetch(1, pf);
-    put(1, pf);
-    fetch(2, pf);
-    __syncthreads();
-    uint32_t u = 0, cb = 0;                          // words consumed; the block holding u
+    fetch();
+    refill();
+    uint32_t u = 0;                                  // words consumed
     uint32_t x = lane < W ? st[c * W + lane] : kTcL;
     int8_t* row = codes + vec * d + base;
-    const uint64_t below = (1ull << lane) - 1ull;
-    for (int64_t s0 = 0; s0 < steps && !bad; ++s0) {
-        const int64_t i = s0 * W + lane;
-        const bool act = lane < W && i < len;
+    // one step of a lane with a symbol; `chk`: test the word count (false on an overrun)
+    auto step = [&](int8_t& code, bool act, bool chk) -> bool {
         if (act) {
-            const uint32_t slot = x & (kTcM - 1u);
-            const int s = lut[slot];
-            x = sf[s] * (x >> kTcProbBits) + slot - scum[s];
-            row[i] = tc_code(s);
+            const uint32_t e = tab[x & (kTcM - 1u)];
+            x = (((e >> 8) & 0xFFFu) + 1u) * (x >> kTcProbBits) + (e >> 20);
+            code = (int8_t)(e & 0xFFu);
         }
         const bool need = act && x < kTcL;
         const uint64_t mk = __ballot(need);
         const uint32_t k = (uint32_t)__popcll(mk);
-        if (u + k > nw) {
-            bad = true;
-            break;
-        }
-        if (need) {
-            const uint32_t v = u + (uint32_t)__popcll(mk & below);
-            x = (x << 16) | (uint32_t)ring[((v / kTcRing) & 1u) * kTcRing + v % kTcRing];
-        }
+        if (chk && u + k > nw) return false;
+        const uint32_t v = u + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+        const uint32_t wd = rg[v & (kTcDecRing - 1)];
+        x = need ? ((x << 16) | wd) : x;
         u += k;
-        if (u / kTcRing != cb) {                     // entered block cb + 1: block cb + 2 into cb's slot
-            ++cb;
-            __syncthreads();                         // every lane is done with block cb - 1
-            put(cb + 1, pf);
-            fetch(cb + 2, pf);
-            __syncthreads();
+        return true;
+    };
+    if (W == 64 && len == csz) {
+        uint8_t* obw = ob[wv];
+        for (int b = 0; b < kTcSteps / kTcBlk && !bad; ++b) {
+#pragma unroll
+            for (int g = 0; g < kTcBlk / 4; ++g) {
+                if (fu < u + 2 * kTcDecFill) refill();               // uniform; keeps fu <= u + 768
+                if (fu < u + kTcDecFill) refill();
+                const bool chk = u + (uint32_t)kTcDecFill > nw;      // near the end: test each step
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    int8_t code = 0;
+                    if (!step(code, true, chk)) {
+                        bad = true;
+                        break;
+                    }
+                    obw[(4 * g + t) * 64 + lane] = (uint8_t)code;
+                }
+                if (bad) break;
+            }
+            if (bad) break;
+            tc_wave_sync();
+            reinterpret_cast<uint4*>(row + (int64_t)b * (kTcBlk * 64))[lane] = reinterpret_cast<const uint4*>(obw)[lane];
+            tc_wave_sync();
+        }
+    } else {
+        for (int64_t s0 = 0; s0 < steps && !bad; ++s0) {
+            if (fu < u + 2 * kTcDecFill) refill();
+            if (fu < u + kTcDecFill) refill();
+            const int64_t i = s0 * W + lane;
+            const bool act = lane < W && i < len;
+            int8_t code = 0;
+            if (!step(code, act, true)) {
+                bad = true;
+                break;
+            }
+            if (act) row[i] = code;
         }
     }
     const uint32_t r = r0 + u;

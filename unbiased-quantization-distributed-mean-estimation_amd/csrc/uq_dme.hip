@@ -2560,13 +2560,14 @@ int uq_tc_encode(const int8_t* codes, const float* l1, int64_t n, int64_t d, int
         const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
         if (d > 0) {
             hipLaunchKernelGGL(tc_hist_kernel, dim3((unsigned)((d + kTcHistSeg - 1) / kTcHistSeg), (unsigned)nj), dim3(256), 0,
-                               st, codes + j0 * d, d, exact, hist + j0 * 256);
+                               st, codes + j0 * d, d, hist + j0 * 256);
             if ((rc = hip_check(hipGetLastError(), "tc_hist_kernel launch"))) return rc;
         }
-        hipLaunchKernelGGL(tc_table_kernel, dim3((unsigned)nj), dim3(64), 0, st, hist + j0 * 256, d, tabs + j0);
+        hipLaunchKernelGGL(tc_table_kernel, dim3((unsigned)nj), dim3(64), 0, st, hist + j0 * 256, d, exact, tabs + j0);
         if ((rc = hip_check(hipGetLastError(), "tc_table_kernel launch"))) return rc;
         if (nch > 0) {
-            hipLaunchKernelGGL(tc_encode_kernel, dim3((unsigned)nch, (unsigned)nj), dim3(64), 0, st, codes + j0 * d, d, exact,
+            hipLaunchKernelGGL(tc_encode_kernel, dim3((unsigned)((nch + kTcEncWaves - 1) / kTcEncWaves), (unsigned)nj),
+                               dim3(64 * kTcEncWaves), 0, st, codes + j0 * d, d, exact,
                                tabs + j0, scratch + j0 * nch * ((int64_t)tc_lanes(d) * kTcSteps), cwords + j0 * nch,
                                states + j0 * nch * tc_lanes(d));
             if ((rc = hip_check(hipGetLastError(), "tc_encode_kernel launch"))) return rc;
@@ -2603,7 +2604,8 @@ int uq_tc_decode(const uint8_t* msgs, const uint64_t* offsets, int64_t n, int64_
     const int64_t nch = std::max<int64_t>(1, tc_nchunks(d));
     for (int64_t j0 = 0; j0 < n; j0 += kMaxGridY) {
         const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
-        hipLaunchKernelGGL(tc_decode_kernel, dim3((unsigned)nch, (unsigned)nj), dim3(64), 0, st, msgs, offsets + j0, d,
+        hipLaunchKernelGGL(tc_decode_kernel, dim3((unsigned)((nch + kTcDecWaves - 1) / kTcDecWaves), (unsigned)nj),
+                           dim3(64 * kTcDecWaves), 0, st, msgs, offsets + j0, d,
                            codes ? codes + j0 * d : codes, l1 + j0, kmax + j0, status + j0);
         if ((rc = hip_check(hipGetLastError(), "tc_decode_kernel launch"))) return rc;
     }
