@@ -3,17 +3,20 @@
 // header of include/uq_dme.h (uq_tc_*) and codes.py; oracle/uq_codec.c restates it on the CPU
 // byte for byte (tests compare whole messages).
 //
-//   KC1 tc_hist_kernel     symbol counts per client (LDS histogram per 64 Ki-symbol segment)
-//   KC2 tc_table_kernel    one wave per client: quantized frequencies (sum 2^12), cumulative
-//                          table, header size
-//   KC3 tc_encode_kernel   one wave per chunk (W interleaved rANS states x 1024 steps): steps
-//                          in reverse, renormalisation words pushed per step in lane order
-//                          (ballot + popcount), final states; words go to a scratch stack
+//   KC1 tc_hist_kernel     code counts per client (SWAR nibble counters for codes -4..3,
+//                          LDS atomics for the rest, per 64 Ki-code segment)
+//   KC2 tc_table_kernel    one wave per client: code -> symbol counts, quantized frequencies
+//                          (sum 2^12), cumulative table, header size
+//   KC3 tc_encode_kernel   one wave per chunk (W interleaved rANS states x 1024 steps), 8 per
+//                          workgroup: steps in reverse, renormalisation words pushed per step
+//                          in lane order (ballot + popcount), final states; words go to a
+//                          scratch stack
 //   KC4 tc_layout_kernel   one wave per client: cumulative words per chunk, message size
 //   KC5 tc_scan_kernel     message offsets (exclusive scan over clients)
 //   KC6 tc_pack_kernel     header, tables, states and words into the packed messages
-//   KC7 tc_decode_kernel   one wave per chunk: LDS slot->symbol table, forward steps, words
-//                          read per step in lane order; checks the chunk ends exactly
+//   KC7 tc_decode_kernel   one wave per chunk, 8 per workgroup: LDS slot table, forward
+//                          steps, words read per step in lane order; checks the chunk ends
+//                          exactly
 // Bytes: KC1 and KC3 read the codes (d per client each), KC3 writes <= 2 B per symbol of
 // scratch, KC6 copies the words; KC7 reads the message and writes d code bytes.
 constexpr int kTcProbBits = 12;
@@ -216,11 +219,10 @@ tc_table_kernel(const uint32_t* __restrict__ hist, int64_t d, int exact, TcTable
     }
 }
 
-// KC3: one wave per chunk.  scratch: [n][nch][csz] u16 (the chunk's words end at csz);
-// cwords [n][nch] u32, states [n][nch][W] u32.  Steps run in reverse in blocks of 16: each
-// lane loads its 16 code bytes of the next block while it encodes the current one.  x / f
-// is floor(x * RU(1/f)) in fp64: exact for x < 2^32 and f <= 2^12 (the product is >= x/f and
-// within 2^-20 of it, while a non-integer x/f is >= 2^-12 below the next integer).
+// KC3 layout: scratch [n][nch][csz] u16 (the chunk's words end at csz); cwords [n][nch] u32,
+// states [n][nch][W] u32.  Steps run in reverse in blocks of 16 (tc_load_blk prefetches a
+// lane's 16 code bytes of the next block in the generic path).  x / f uses the invariant
+// divisor form of tc_div (exact for every 32-bit x; tools/tc_div_check.c).
 constexpr int kTcBlk = 16;
 
 __device__ __forceinline__ void tc_load_blk(uint32_t (&b)[kTcBlk], const int8_t* row, int64_t blk, int W, int lane,
@@ -238,7 +240,7 @@ __device__ __forceinline__ void tc_wave_sync() {
 }
 
 // KC3: grid (ceil(nch / kTcEncWaves), n), one wave per chunk; the waves of a workgroup share
-// the per-symbol constants, one 16-byte LDS entry {x_max, f | cum << 16, RU(1/f)}.  Full
+// the per-symbol constants, one 16-byte LDS entry {x_max, f | cum << 16, divisor magic}.  Full
 // chunks (W = 64 lanes x 1024 steps: every chunk of d >= 65536 but a ragged last one) take a
 // branch-free path: each block of 16 steps arrives as one 16-byte load per lane (1 KB per
 // wave, loaded a block ahead) staged in LDS and read back one byte per step; words go to a
@@ -248,8 +250,16 @@ __device__ __forceinline__ void tc_wave_sync() {
 struct alignas(16) TcEnc {
     uint32_t xmax;      // renormalise while x > xmax: x >= f << 20 (f = 4096 never)
     uint32_t fc;        // f | cum << 16
-    double rcp;         // RU(1 / f)
+    uint32_t mg;        // x / f = (t + ((x - t) >> s1)) >> s2, t = mulhi(mg, x)
+    uint32_t sh;        // s1 | s2 << 8
 };
+// Division by the invariant f (Granlund & Montgomery 1994, fig. 4.1): exact for every
+// 32-bit x; l = ceil(log2 f), mg = floor(2^32 (2^l - f) / f) + 1, s1 = min(l, 1),
+// s2 = max(l - 1, 0).
+__device__ __forceinline__ uint32_t tc_div(uint32_t x, uint32_t mg, uint32_t sh) {
+    const uint32_t t = __umulhi(mg, x);
+    return (t + ((x - t) >> (sh & 0xFFu))) >> (sh >> 8);
+}
 constexpr int kTcEncWaves = 8;
 constexpr int kTcRingW = 1024;              // encoder word ring per wave (u16), power of two
 constexpr int kTcFlush = 256;               // words per ring flush (one 8-byte store per lane)
@@ -265,12 +275,13 @@ tc_encode_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, const T
     const TcTable* t = tabs + vec;
     for (int q = tid; q < 256; q += 64 * kTcEncWaves) {
         const uint32_t f = t->f[q];
-        double rc = f ? 1.0 / (double)f : 0.0;                    // RU(1/f): bump an RN result below 1/f
-        if (f && fma(rc, (double)f, -1.0) < 0.0) rc = __longlong_as_double(__double_as_longlong(rc) + 1);
+        int l = 0;
+        while (l < 31 && (1u << l) < f) ++l;                      // ceil(log2 f)
         TcEnc e;
         e.xmax = f >= 4096u ? 0xFFFFFFFFu : (f << 20) - 1u;
         e.fc = f | (t->cum[q] << 16);
-        e.rcp = rc;
+        e.mg = f ? (uint32_t)((((uint64_t)((1u << l) - f)) << 32) / f + 1u) : 0u;
+        e.sh = (uint32_t)(l < 1 ? l : 1) | ((uint32_t)(l > 1 ? l - 1 : 0) << 8);
         se[q] = e;
     }
     __syncthreads();
@@ -324,7 +335,7 @@ tc_encode_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, const T
                     x = need ? x >> 16 : x;
                     ptr -= k;
                     const uint32_t f = e.fc & 0xFFFFu;
-                    const uint32_t qd = (uint32_t)((double)x * e.rcp);   // floor(x / f), exact
+                    const uint32_t qd = tc_div(x, e.mg, e.sh);               // floor(x / f), exact
                     x = (qd << kTcProbBits) + (x - qd * f) + (e.fc >> 16);
                 }
                 if (fl - ptr >= kTcFlush) {                           // uniform; pending <= 256 + 7 + 256
@@ -370,7 +381,7 @@ tc_encode_kernel(const int8_t* __restrict__ codes, int64_t d, int exact, const T
             if (act) {
                 const TcEnc e = se[s];
                 const uint32_t f = e.fc & 0xFFFFu;
-                const uint32_t qd = (uint32_t)((double)x * e.rcp);  // floor(x / f), exact
+                const uint32_t qd = tc_div(x, e.mg, e.sh);          // floor(x / f), exact
                 x = (qd << kTcProbBits) + (x - qd * f) + (e.fc >> 16);
             }
         }
