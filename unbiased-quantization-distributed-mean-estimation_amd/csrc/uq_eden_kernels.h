@@ -371,17 +371,21 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
     constexpr int kLQ = kNormChunk / 256;             // float4 per loader thread
     float4 nx[kLQ];
     auto load = [&](int64_t ch) {
+        if (lvalid && (ch + 1) * kNormChunk <= nv) {         // wave-uniform: a whole chunk, no guards
+            // (per-element guards here kept the loads from overlapping: 1.11 vs 0.88 ms at
+            // 1024 x 2^20, tools/exp/norm_in_pipeline.py)
+#pragma unroll
+            for (int q = 0; q < kLQ; ++q)
+                nx[q] = *reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q));
+            return;
+        }
 #pragma unroll
         for (int q = 0; q < kLQ; ++q) {
             const int64_t i = ch * kNormChunk + 4 * (lj + 64 * q);
-            if (lvalid && i + 3 < nv) {
-                nx[q] = *reinterpret_cast<const float4*>(lp + i);
-            } else {
-                nx[q].x = (lvalid && i < nv) ? lp[i] : 0.f;
-                nx[q].y = (lvalid && i + 1 < nv) ? lp[i + 1] : 0.f;
-                nx[q].z = (lvalid && i + 2 < nv) ? lp[i + 2] : 0.f;
-                nx[q].w = (lvalid && i + 3 < nv) ? lp[i + 3] : 0.f;
-            }
+            nx[q].x = (lvalid && i < nv) ? lp[i] : 0.f;
+            nx[q].y = (lvalid && i + 1 < nv) ? lp[i + 1] : 0.f;
+            nx[q].z = (lvalid && i + 2 < nv) ? lp[i + 2] : 0.f;
+            nx[q].w = (lvalid && i + 3 < nv) ? lp[i + 3] : 0.f;
         }
     };
     auto store = [&](float* sb) {      // element e = 8 i + l of the chunk -> [k][l][i]
