@@ -204,3 +204,26 @@ def test_c4_size_2pow22_vs_oracle(uq):
             assert info[0] == D and bool(info[1] & 1) == A
             assert G.bits_equal(out, exp), (R, G.n_mismatch(out, exp))
     uq.check_status()
+
+
+def test_torch_ties_batch_multiworkgroup_levels(uq):
+    """A batch (n >= 32) at d = 2^20 takes KB7a: introselect's levels run over many workgroups
+    down to the 4096-pair LDS tails (~10 levels here), marking and tails in 256-thread
+    workgroups, then the join.  Tie-heavy integer rows (always ambiguous) and Gaussian rows,
+    every client bit-exact against the oracle's libstdc++ replay."""
+    rng = np.random.default_rng(77)
+    n, d = 40, 1 << 20
+    x = rng.standard_normal((n, d)).astype(f32)
+    x[::4] = rng.integers(-3, 4, (len(range(0, n, 4)), d)).astype(f32)
+    m = rate_to_m(1, d)
+    out, info = uq.biased_quantize(torch.as_tensor(x).cuda(), m=m, torch_threads=1, ties="torch", return_info=True)
+    out = out.cpu().numpy()
+    info = info.cpu().numpy()
+    amb = 0
+    for j in range(n):
+        exp, _, D, A = C.biased_quantize(x[j], m, 1, 0)
+        assert info[j, 0] == D and bool(info[j, 1] & 1) == A, j
+        assert G.bits_equal(out[j], exp), j
+        amb += int(A)
+    assert amb >= n // 4, amb
+    uq.check_status()

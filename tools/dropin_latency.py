@@ -16,17 +16,18 @@ def main():
     import uqdme
     res = {}
     for d in (172554, 1 << 20):
-        v = torch.randn(d, device="cuda")
+        vs = [torch.randn(d, device="cuda") for _ in range(16)]     # different vectors: some have
+        v = vs[0]                                                   # biased-quantizer threshold ties
         for name, f in (("Type_unbiased_quantize", uqdme.Type_unbiased_quantize),
                         ("Type_biased_quantize", uqdme.Type_biased_quantize),
                         ("EDEN_quantize_Hadamard", uqdme.EDEN_quantize_Hadamard)):
             for _ in range(3):
                 y = f(v, 1)
             torch.cuda.synchronize()
-            k = 50
+            k = 48
             t0 = time.perf_counter()
-            for _ in range(k):
-                y = f(v, 1)
+            for i in range(k):
+                y = f(vs[i % len(vs)], 1)
             torch.cuda.synchronize()
             res[f"{name}/d={d}"] = round((time.perf_counter() - t0) / k * 1e3, 4)
             del y

@@ -379,6 +379,7 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
 // scans), so rez_ties_kernel resumes from the saved (first, last, depth) with the same
 // queue it would have built itself.  Slot a serves list entry a (a < kTieSlots).
 constexpr int64_t kTieLevelMin = kTieLdsPairs;   // shorter ranges finish in rez_ties_kernel's LDS
+constexpr int64_t kTieLevelMinClients = 32;      // KB7a for batches of at least this many clients
 constexpr int kTieSegs = 256;               // segments per partition (one wave each)
 constexpr int kTieFillSegs = 64;            // workgroups per client for the queue fill
 

@@ -2187,7 +2187,11 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     uint32_t* list = (uint32_t*)(wsb + w.list_off);
     uint32_t* qbuf = (uint32_t*)(wsb + w.pairs_off);
     uint32_t* pos = (uint32_t*)(wsb + w.pos_off);
-    if (d <= kTieLevelMin) {
+    // KB7a pays ~85 short launches whether or not any client is listed (the host does not
+    // know): worth it for batches, where ~3 % of Gaussian clients are ambiguous at R = 1 and
+    // several replays would share one workgroup each; a few-client call (the per-vector
+    // drop-ins) replays in one kernel when it has to
+    if (d <= kTieLevelMin || n < kTieLevelMinClients) {
         hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
                            state, bits, qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)nullptr, 0);
         return hip_check(hipGetLastError(), "rez_ties_kernel launch");
