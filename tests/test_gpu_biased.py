@@ -227,3 +227,24 @@ def test_torch_ties_batch_multiworkgroup_levels(uq):
         amb += int(A)
     assert amb >= n // 4, amb
     uq.check_status()
+
+
+def test_torch_ties_many_listed_clients_stop_levels_early(uq):
+    """>= 128 listed clients: KB7a's levels stop at ranges of 65536 and the 1024-thread
+    replays resume those slots after the join (plus the list entries beyond the 256 slots).
+    Every client tie-heavy (ambiguous), bit-exact against the oracle."""
+    rng = np.random.default_rng(78)
+    n, d = 300, 1 << 17
+    x = rng.integers(-3, 4, (n, d)).astype(f32)
+    m = rate_to_m(1, d)
+    out, info = uq.biased_quantize(torch.as_tensor(x).cuda(), m=m, torch_threads=1, ties="torch", return_info=True)
+    out = out.cpu().numpy()
+    info = info.cpu().numpy()
+    amb = 0
+    for j in range(n):
+        exp, _, D, A = C.biased_quantize(x[j], m, 1, 0)
+        assert info[j, 0] == D and bool(info[j, 1] & 1) == A, j
+        assert G.bits_equal(out[j], exp), j
+        amb += int(A)
+    assert amb >= 128, amb
+    uq.check_status()

@@ -380,6 +380,8 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
 // queue it would have built itself.  Slot a serves list entry a (a < kTieSlots).
 constexpr int64_t kTieLevelMin = kTieLdsPairs;   // shorter ranges finish in rez_ties_kernel's LDS
 constexpr int64_t kTieLevelMinClients = 32;      // KB7a for batches of at least this many clients
+constexpr uint32_t kTieManyClients = 128;          // this many listed clients: levels only down to
+constexpr int64_t kTieLevelMinMany = 65536;        //   this range (tie-heavy batches)
 constexpr int kTieSegs = 256;               // segments per partition (one wave each)
 constexpr int kTieFillSegs = 64;            // workgroups per client for the queue fill
 
@@ -450,7 +452,10 @@ kt_pivot_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restri
     bool act = false;
     if (a < slots) {
         TieLevelState& t = tls[a];
-        act = a < (int)list[0] && t.filled && !t.err && t.depth > 0 && t.last - t.first > kTieLevelMin;
+        // with many listed clients the 1024-thread replays fill the GPU by themselves: the
+        // levels stop at kTieLevelMinMany and part 2 finishes those slots
+        const int64_t stop = list[0] >= kTieManyClients ? kTieLevelMinMany : kTieLevelMin;
+        act = a < (int)list[0] && t.filled && !t.err && t.depth > 0 && t.last - t.first > stop;
         t.active = act ? 1 : 0;
         if (act) {
             const int64_t dpad = (d + 3) & ~(int64_t)3;
@@ -794,7 +799,10 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         TT_T0();
         // resumed: KB7a filled this slot's queue and ran introselect's first levels
         const bool resumed = tls && li == blockIdx.x && tls[li].filled;
-        if ((part == 1 && !resumed) || (part == 2 && resumed)) continue;
+        // part 1: resumed slots whose range fits the LDS tail; part 2: everything else
+        // (resumed slots KB7a left longer resume from their saved state in 1024 threads)
+        const bool tail = resumed && (tls[li].err || tls[li].last - tls[li].first <= kTieLdsPairs);
+        if ((part == 1 && !tail) || (part == 2 && tail)) continue;
         // queue[j] = (value, j) (TopKImpl.h); 4 coordinates per lane and load
         const bool xv4 = ((uintptr_t)xv & 15u) == 0;
         for (int64_t i0 = 0; i0 < (resumed ? 0 : d); i0 += (int64_t)NT * 4 * kTieU) {
