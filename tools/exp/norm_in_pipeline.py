@@ -20,6 +20,8 @@ def main():
     L = ctypes.CDLL(os.path.join(HERE, "libexp_norm_pitch_pf.so"))
     L.exp_norm_pitch.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                  ctypes.c_int, ctypes.c_void_p]
+    L.exp_norm_nc.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                              ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     n, D = 1024, 1 << 20
     x = torch.randn(n, D, generator=torch.Generator(device="cuda").manual_seed(3), device="cuda")
     seeds = torch.randint(0, 100, (n,), generator=torch.Generator().manual_seed(5))
@@ -29,15 +31,17 @@ def main():
     vptr = ws.data_ptr() + 256                                 # EdenLayout.vec_off = kCtrlBytes
     nrm = torch.empty(n, device="cuda")
     sp = torch.cuda.current_stream().cuda_stream
-    for rep in range(4):
+    for rep in range(6):
         uqdme.eden_compress(x, 1, seeds=seeds)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        if L.exp_norm_pitch(vptr, n, D, D, nrm.data_ptr(), 0, sp) != 0:
-            raise RuntimeError("launch failed")
-        e1.record()
-        torch.cuda.synchronize()
-        print(json.dumps({"rep": rep, "exp_norm_on_pipeline_vectors_ms": round(e0.elapsed_time(e1), 4)}), flush=True)
+        for nc in (4, 44):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            if L.exp_norm_nc(vptr, n, D, D, nrm.data_ptr(), 0, nc, sp) != 0:
+                raise RuntimeError("launch failed")
+            e1.record()
+            torch.cuda.synchronize()
+            print(json.dumps({"rep": rep, "variant": "ahead2" if nc == 44 else "ahead1",
+                              "exp_norm_on_pipeline_vectors_ms": round(e0.elapsed_time(e1), 4)}), flush=True)
     # the same vectors copied to a fresh buffer
     v2 = torch.empty(n * D, device="cuda")
     v2.copy_(torch.from_blob if False else ws[256:256 + n * D * 4].view(torch.float32))

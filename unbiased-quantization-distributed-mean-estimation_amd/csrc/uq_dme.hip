@@ -2865,8 +2865,12 @@ int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, 
     a.tab = tab;
     rc = launch_fwht(a, n, false, vec, nullptr, st);                               // AS:123-141
     if (rc) return rc;
-    hipLaunchKernelGGL(eden_norm_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads), 0, st,
-                       vec, n, w.D, nrm);
+    if (w.D % kNormChunk == 0)
+        hipLaunchKernelGGL(eden_norm_whole_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads),
+                           0, st, vec, n, w.D, nrm);
+    else
+        hipLaunchKernelGGL(eden_norm_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads),
+                           0, st, vec, n, w.D, nrm);
     rc = hip_check(hipGetLastError(), "eden_norm_kernel launch");                  // AS:329 torch.norm
     if (rc) return rc;
     hipLaunchKernelGGL(eden_bins_kernel, dim3((unsigned)w.tiles, (unsigned)n), dim3(256), 0, st, vec, w.D, a.sqrtD,

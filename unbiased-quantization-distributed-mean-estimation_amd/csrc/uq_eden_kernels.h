@@ -356,6 +356,9 @@ constexpr int kNormRow = kNormChunk / 8 + 4;        // one torch lane's 128 step
 constexpr int kNormClientStride = 8 * kNormRow;
 constexpr int kNormBuf = kNormClients * kNormClientStride;
 constexpr int kNormThreads = 64 + 256;
+// Loads run two chunks ahead in two register sets (the loop is unrolled by two so the set is
+// static): chunk ch + 2's loads stay in flight across iteration ch + 1 (0.86 -> 0.77 ms at
+// 1024 x 2^20 in tools/exp/norm_nc.py).  Whole chunks load without per-element guards.
 __global__ void __launch_bounds__(kNormThreads)
 eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __restrict__ nrm) {
     __shared__ __attribute__((aligned(16))) float s[3][kNormBuf];
@@ -369,11 +372,10 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
     const bool lvalid = !chain && v0 + lk < n;
     const float* lp = v + (lvalid ? v0 + lk : 0) * D;
     constexpr int kLQ = kNormChunk / 256;             // float4 per loader thread
-    float4 nx[kLQ];
-    auto load = [&](int64_t ch) {
-        if (lvalid && (ch + 1) * kNormChunk <= nv) {         // wave-uniform: a whole chunk, no guards
-            // (per-element guards here kept the loads from overlapping: 1.11 vs 0.88 ms at
-            // 1024 x 2^20, tools/exp/norm_in_pipeline.py)
+    float4 na[kLQ], nb[kLQ];
+    auto load = [&](float4 (&nx)[kLQ], int64_t ch) {
+        if (ch >= nchunks) return;                       // uniform
+        if (lvalid && (ch + 1) * kNormChunk <= nv) {     // wave-uniform: a whole chunk, no guards
 #pragma unroll
             for (int q = 0; q < kLQ; ++q)
                 nx[q] = *reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q));
@@ -388,8 +390,7 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
             nx[q].w = (lvalid && i + 3 < nv) ? lp[i + 3] : 0.f;
         }
     };
-    auto store = [&](float* sb) {      // element e = 8 i + l of the chunk -> [k][l][i]
-        if (chain) return;
+    auto store = [&](const float4 (&nx)[kLQ], float* sb) {      // element e = 8 i + l -> [k][l][i]
 #pragma unroll
         for (int q = 0; q < kLQ; ++q) {
             const int e = 4 * (lj + 64 * q);
@@ -403,33 +404,45 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
     };
     const int ck = (tid >> 3) & (kNormClients - 1), cl = tid & 7;   // lanes >= 32 mirror 0..31
     float acc = 0.f;
-    if (nchunks > 0) {
-        if (!chain) load(0);
-        store(s[0]);
-        if (!chain && nchunks > 1) load(1);
+    auto chain_chunk = [&](int64_t ch) {
+        const int cnt = (int)(std::min<int64_t>(kNormChunk, nv - ch * kNormChunk) / 8);
+        const float* row = s[ch % 3] + ck * kNormClientStride + cl * kNormRow;
+        int i = 0;
+        for (; i + 16 <= cnt; i += 16) {
+            float4 t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const float4*>(row + i + 4 * u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                acc = fmaf(t[u].x, t[u].x, acc);
+                acc = fmaf(t[u].y, t[u].y, acc);
+                acc = fmaf(t[u].z, t[u].z, acc);
+                acc = fmaf(t[u].w, t[u].w, acc);
+            }
+        }
+        for (; i < cnt; ++i) acc = fmaf(row[i], row[i], acc);
+    };
+    if (nchunks > 0 && !chain) {
+        load(na, 0);
+        store(na, s[0]);
+        load(na, 1);                                   // chunk 1 -> na, chunk 2 -> nb
+        load(nb, 2);
     }
     __syncthreads();
-    for (int64_t ch = 0; ch < nchunks; ++ch) {
-        if (chain) {
-            const int cnt = (int)(std::min<int64_t>(kNormChunk, nv - ch * kNormChunk) / 8);
-            const float* row = s[ch % 3] + ck * kNormClientStride + cl * kNormRow;
-            int i = 0;
-            for (; i + 16 <= cnt; i += 16) {
-                float4 t[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const float4*>(row + i + 4 * u);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    acc = fmaf(t[u].x, t[u].x, acc);
-                    acc = fmaf(t[u].y, t[u].y, acc);
-                    acc = fmaf(t[u].z, t[u].z, acc);
-                    acc = fmaf(t[u].w, t[u].w, acc);
-                }
-            }
-            for (; i < cnt; ++i) acc = fmaf(row[i], row[i], acc);
-        } else if (ch + 1 < nchunks) {
-            store(s[(ch + 1) % 3]);
-            if (ch + 2 < nchunks) load(ch + 2);
+    for (int64_t ch = 0; ch < nchunks; ch += 2) {
+        // iteration ch: chain on chunk ch; chunk ch + 1 (na) into LDS, chunk ch + 3 -> na
+        if (chain) chain_chunk(ch);
+        else if (ch + 1 < nchunks) {
+            store(na, s[(ch + 1) % 3]);
+            load(na, ch + 3);
+        }
+        __syncthreads();
+        if (ch + 1 >= nchunks) break;
+        // iteration ch + 1: chain on chunk ch + 1; chunk ch + 2 (nb) into LDS, ch + 4 -> nb
+        if (chain) chain_chunk(ch + 1);
+        else if (ch + 2 < nchunks) {
+            store(nb, s[(ch + 2) % 3]);
+            load(nb, ch + 4);
         }
         __syncthreads();
     }
@@ -443,6 +456,88 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
             for (int64_t i = nv; i < D; ++i) tot = tot + p[i] * p[i];
             nrm[vec] = sqrtf(tot);
         }
+    }
+}
+
+// The same kernel when every chunk is whole (D a multiple of kNormChunk: D >= 1024), with
+// no guards anywhere: with the guarded loads and the general chunk count of the kernel
+// above the compiler's waits cost the two-ahead overlap (0.87-0.98 against 0.79 ms at
+// 1024 x 2^20, tools/exp/norm_in_pipeline.py).  Same adds in the same order.
+__global__ void __launch_bounds__(kNormThreads)
+eden_norm_whole_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __restrict__ nrm) {
+    __shared__ __attribute__((aligned(16))) float s[3][kNormBuf];
+    const int tid = threadIdx.x;
+    const int64_t v0 = (int64_t)blockIdx.x * kNormClients;
+    const int64_t nchunks = D / kNormChunk;
+    const bool chain = tid < kWave;
+    const int lt = tid - kWave, lk = lt >> 6, lj = lt & 63;
+    const bool lvalid = !chain && v0 + lk < n;
+    const float* lp = v + (lvalid ? v0 + lk : 0) * D;
+    constexpr int kLQ = kNormChunk / 256;
+    float4 na[kLQ], nb[kLQ];
+    auto load = [&](float4 (&nx)[kLQ], int64_t ch) {
+        if (!lvalid || ch >= nchunks) return;
+#pragma unroll
+        for (int q = 0; q < kLQ; ++q) nx[q] = *reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q));
+    };
+    auto store = [&](const float4 (&nx)[kLQ], float* sb) {
+        if (chain) return;
+#pragma unroll
+        for (int q = 0; q < kLQ; ++q) {
+            const int e = 4 * (lj + 64 * q);
+            const int i = e >> 3, l = e & 7;
+            float* base = sb + lk * kNormClientStride + i;
+            base[(l + 0) * kNormRow] = nx[q].x;
+            base[(l + 1) * kNormRow] = nx[q].y;
+            base[(l + 2) * kNormRow] = nx[q].z;
+            base[(l + 3) * kNormRow] = nx[q].w;
+        }
+    };
+    const int ck = (tid >> 3) & (kNormClients - 1), cl = tid & 7;
+    float acc = 0.f;
+    auto chainstep = [&](int64_t ch) {
+        const float* row = s[ch % 3] + ck * kNormClientStride + cl * kNormRow;
+        for (int i = 0; i < kNormChunk / 8; i += 16) {
+            float4 t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const float4*>(row + i + 4 * u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                acc = fmaf(t[u].x, t[u].x, acc);
+                acc = fmaf(t[u].y, t[u].y, acc);
+                acc = fmaf(t[u].z, t[u].z, acc);
+                acc = fmaf(t[u].w, t[u].w, acc);
+            }
+        }
+    };
+    if (!chain) {
+        load(na, 0);
+        store(na, s[0]);
+        load(na, 1);                    // chunk 1 -> na, chunk 2 -> nb
+        load(nb, 2);
+    }
+    __syncthreads();
+    for (int64_t ch = 0; ch < nchunks; ch += 2) {
+        if (chain) chainstep(ch);
+        else if (ch + 1 < nchunks) {
+            store(na, s[(ch + 1) % 3]);
+            load(na, ch + 3);
+        }
+        __syncthreads();
+        if (ch + 1 >= nchunks) break;
+        if (chain) chainstep(ch + 1);
+        else if (ch + 2 < nchunks) {
+            store(nb, s[(ch + 2) % 3]);
+            load(nb, ch + 4);
+        }
+        __syncthreads();
+    }
+    if (chain) {
+        const int base = tid & ~7;
+        float tot = __shfl(acc, base, kWave);
+        for (int j = 1; j < 8; ++j) tot = tot + __shfl(acc, base + j, kWave);
+        const int64_t vec = v0 + ck;
+        if (tid < 8 * kNormClients && cl == 0 && vec < n) nrm[vec] = sqrtf(tot);
     }
 }
 
