@@ -1830,7 +1830,10 @@ __device__ __forceinline__ void mean_add_bytes(float (&e)[kMeanCpt], const int8_
             if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[(j0 + jj) * d + i0 + k]];
 }
 
-template <bool VEC>
+// ALL: every thread's kMeanCpt columns lie inside d (d a multiple of 256 * kMeanCpt), so no
+// per-thread `full` test anywhere (a per-thread guard around the adds cost the loads'
+// overlap in other kernels here).
+template <bool VEC, bool ALL = false>
 __global__ void __launch_bounds__(256)
 codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, const int32_t* __restrict__ kmaxv,
                   int64_t n, int64_t d, float fm, float n_div, int accumulate, float* __restrict__ est) {
@@ -1839,7 +1842,7 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
     const int lane = tid & (kWave - 1);
     const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);
     const int64_t i0 = ((int64_t)blockIdx.x * 256 + tid) * kMeanCpt;
-    const bool full = VEC && i0 + kMeanCpt <= d;
+    const bool full = ALL || (VEC && i0 + kMeanCpt <= d);
     float e[kMeanCpt];
 #pragma unroll
     for (int k = 0; k < kMeanCpt; ++k) e[k] = (accumulate && i0 + k < d) ? est[i0 + k] : 0.0f;
@@ -2452,7 +2455,10 @@ int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax,
     const bool vec = (n == 0 || aligned16(codes)) && aligned16(est) && d % 16 == 0;
     const int64_t blocks = (d + 256 * kMeanCpt - 1) / (256 * kMeanCpt);
     if (blocks > 0x7FFFFFFF) return fail(UQ_E_INVALID, "d too large");
-    if (vec)
+    if (vec && d % (256 * kMeanCpt) == 0)
+        hipLaunchKernelGGL((codes_mean_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, kmax, n,
+                           d, (float)m, n_div, accumulate, est);
+    else if (vec)
         hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, kmax, n, d,
                            (float)m, n_div, accumulate, est);
     else
