@@ -66,8 +66,9 @@ def parse():
                     help="q: K2 writes the dequantized q, mean reads q (the reference's drop-in semantics); "
                          "codes: K2 writes q AND type codes, mean decodes codes; "
                          "encode: K2 writes codes only, the mean kernel dequantizes (DME wire pipeline)")
-    ap.add_argument("--probe-candidates", type=int, default=6,
-                    help="output-buffer sets probed once before warmup (pipeline.py); <= 1: no probe")
+    ap.add_argument("--probe-candidates", type=int, default=16,
+                    help="at most this many output-buffer sets probed once before warmup, until both "
+                         "speeds are seen (pipeline.py); <= 1: no probe")
     ap.add_argument("--side-pipelines", action="store_true", default=True,
                     help="also time the other pipelines (reported under 'pipelines')")
     ap.add_argument("--no-side-pipelines", dest="side_pipelines", action="store_false")

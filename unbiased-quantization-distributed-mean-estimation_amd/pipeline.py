@@ -11,9 +11,9 @@ and q + codes re-allocated ten times in one process K2 took 1.66-2.03 ms on the 
 q + codes fixed and x re-allocated ten times 1.67-1.73 ms (profiles/r02d_exp_placement_split.jsonl);
 the code layout does not matter (tile-major codes follow the same modes,
 profiles/r02c_exp_codes_layout.jsonl).  The pipeline's outputs are long-lived, so
-`probe_outputs` allocates a few candidate (q, codes) sets at once (each on its own pages),
-times K2 on each with the real batch, keeps the fastest and frees the rest: a one-time
-calibration like a workspace autotune.  Results do not depend on the buffers chosen.
+`probe_outputs` allocates candidate (q, codes) sets (each on its own pages, all held until
+the choice), times K2 on each with the real batch until it has seen both speeds, keeps the
+fastest and frees the rest: a one-time calibration like a workspace autotune.  Results do not depend on the buffers chosen.
 
 Every launch goes through the C-ABI (include/uq_dme.h); nothing here computes on the CPU."""
 from __future__ import annotations
@@ -95,14 +95,17 @@ class DMEPipeline:
             raise ValueError("X must hold one f32 draw per client on the device")
 
     # ---- output placement ------------------------------------------------------------
-    def probe_outputs(self, x, X, candidates: int = 4, reps: int = 3):
-        """Time K2 on `candidates` output sets (the current one included), keep the fastest.
-        Needs the batch's L1 (runs K1 first).  Returns the report (ms per candidate)."""
+    def probe_outputs(self, x, X, candidates: int = 16, reps: int = 3, batch: int = 4, spread: float = 1.10):
+        """Time K2 on output sets (the current one included), keep the fastest.  Sets are
+        added `batch` at a time, up to `candidates`, until the probe has seen both speeds
+        (slowest / fastest >= `spread`; the modes are ~17 % apart): with ~30-60 % of sets
+        fast, six fixed candidates left ~1 rank in 8 without a fast set.  Needs the batch's
+        L1 (runs K1 first).  Returns the report (ms per candidate)."""
         self._check(x, X)
         self.l1_norms(x)
-        sets = [(self.q, self.codes)] + [self._alloc_outputs() for _ in range(max(0, candidates - 1))]
-        times = []
-        for q, c in sets:
+        sets, times = [(self.q, self.codes)], []
+
+        def time_set(q, c):
             for _ in range(2):
                 self.quantize(x, X, q, c)
             torch.cuda.synchronize(self.dev)
@@ -112,7 +115,13 @@ class DMEPipeline:
                 self.quantize(x, X, q, c)
             e1.record()
             torch.cuda.synchronize(self.dev)
-            times.append(e0.elapsed_time(e1) / reps)
+            return e0.elapsed_time(e1) / reps
+
+        times.append(time_set(*sets[0]))
+        while len(sets) < candidates and max(times) < spread * min(times):
+            for _ in range(min(batch, candidates - len(sets))):
+                sets.append(self._alloc_outputs())
+                times.append(time_set(*sets[-1]))
         best = min(range(len(sets)), key=lambda i: times[i])
         self.q, self.codes = sets[best]
         del sets
