@@ -245,20 +245,23 @@ rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist, 
 }
 
 // KB4c: compact the keys of the chosen first-digit bucket (compact-mode clients).  Each
-// thread keeps its 64 keys in registers (16 float4 loads, coalesced, non-temporal), counts
-// the matches; one block scan + one atomic per workgroup reserves the output range.  The
-// matches are staged in LDS (branch-free: a non-match goes to the thread's junk slot) and
+// thread keeps its kCompactItems keys in registers (float4 loads, coalesced, non-temporal),
+// counts the matches; one block scan + one atomic per workgroup reserves the output range.
+// The matches are staged in LDS (branch-free: a non-match goes to the thread's junk slot) and
 // copied out coalesced; a workgroup with more than kCompactStage matches (tie-heavy data)
-// writes them straight from registers.
+// writes them straight from registers.  32 keys per thread (was 64: the VGPRs held three
+// workgroups per CU, 1.11 ms = 3.9 TB/s at 1024 x 2^20).
 constexpr int kCompactStage = 4096;
+constexpr int kCompactItems = 32;
+constexpr int kCompactSpan = 256 * kCompactItems;
 template <bool CHECK>
 __device__ __forceinline__ uint64_t compact_keys(const float* __restrict__ xv, int64_t d, int64_t b0, int tid,
                                                  const DivPlan& dp, float fm, bool up, uint32_t prefix,
-                                                 uint32_t (&key)[kHistItems]) {
+                                                 uint32_t (&key)[kCompactItems]) {
     typedef float f4v __attribute__((ext_vector_type(4)));
     uint64_t match = 0;
 #pragma unroll
-    for (int j = 0; j < kHistItems / 4; ++j) {
+    for (int j = 0; j < kCompactItems / 4; ++j) {
         const int64_t i = b0 + 4 * ((int64_t)j * 256 + tid);          // elements i .. i+3
         float v[4];
         if (!CHECK) {
@@ -292,12 +295,12 @@ rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restri
     const DivPlan dp = div_plan(l1[vec]);
     const float* xv = x + vec * d;
     const int tid = threadIdx.x;
-    const int64_t b0 = (int64_t)blockIdx.x * kHistSpan;
+    const int64_t b0 = (int64_t)blockIdx.x * kCompactSpan;
     __shared__ uint32_t lds[4];
     __shared__ uint32_t s_base;
     __shared__ uint32_t s_cand[kCompactStage + 256];             // staged matches + junk slots
-    uint32_t key[kHistItems];
-    const uint64_t match = (VEC4 && b0 + kHistSpan <= d)
+    uint32_t key[kCompactItems];
+    const uint64_t match = (VEC4 && b0 + kCompactSpan <= d)
                                ? compact_keys<false>(xv, d, b0, tid, dp, fm, up, prefix, key)
                                : compact_keys<true>(xv, d, b0, tid, dp, fm, up, prefix, key);
     uint32_t tot;
@@ -307,7 +310,7 @@ rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restri
     if (tot <= (uint32_t)kCompactStage) {                        // block-uniform
         const uint32_t junk = kCompactStage + tid;
 #pragma unroll
-        for (int e = 0; e < kHistItems; ++e) {
+        for (int e = 0; e < kCompactItems; ++e) {
             const uint32_t bit = (uint32_t)(match >> e) & 1u;
             s_cand[bit ? off : junk] = key[e];
             off += bit;
@@ -320,7 +323,7 @@ rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restri
         __syncthreads();
         off += s_base;
 #pragma unroll
-        for (int e = 0; e < kHistItems; ++e)
+        for (int e = 0; e < kCompactItems; ++e)
             if (((match >> e) & 1ull) && off < cap) cv[off++] = key[e];
     }
 }

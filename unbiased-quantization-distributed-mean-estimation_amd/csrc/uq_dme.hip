@@ -2682,10 +2682,11 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     const dim3 tgrid((unsigned)w.tiles, (unsigned)n);
     hipLaunchKernelGGL(rez_select_kernel<0>, dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.cap);
     // compact-mode clients: the chosen bucket's keys, then digits 2-3 on them
+    const dim3 cgrid((unsigned)((d + kCompactSpan - 1) / kCompactSpan), (unsigned)n);
     if (vec4)
-        hipLaunchKernelGGL(rez_compact_kernel<true>, hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
+        hipLaunchKernelGGL(rez_compact_kernel<true>, cgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
     else
-        hipLaunchKernelGGL(rez_compact_kernel<false>, hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
+        hipLaunchKernelGGL(rez_compact_kernel<false>, cgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
     hipLaunchKernelGGL(rez_cand_select_kernel, dim3((unsigned)n), dim3(256), 0, st, state, cand, cand_n, w.cap);
     // the others: full-vector histogram passes for digits 2-3
 #define UQ_RADIX(P)                                                                                          \
