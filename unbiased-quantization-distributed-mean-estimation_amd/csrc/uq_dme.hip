@@ -392,8 +392,11 @@ __device__ float lds_torch_sum(const float* a, int s, int lane) {
     return acc;
 }
 
-template <class Op>
-__global__ void __launch_bounds__(64 * kFinWaves)
+// WAVES = 1 when there is one torch chunk (T = 1 or d < 32768): the eight waves' staging
+// buffers (64 KB of LDS) held two workgroups per CU for one working wave (37 us at
+// 1024 x 2^20, T = 1).
+template <class Op, int WAVES = kFinWaves>
+__global__ void __launch_bounds__(64 * WAVES)
 l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
                    const float* __restrict__ part, float* __restrict__ l1_out,
                    const float* __restrict__ l1, float fm, uint32_t* __restrict__ hist_g,
@@ -406,17 +409,17 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
     }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const float* xv = x + vec * d;
-    __shared__ float fin_w[kFinWaves][32];
-    __shared__ __attribute__((aligned(16))) float s_stage_w[kFinWaves][kFinStage * 32];
-    __shared__ float s_tail_w[kFinWaves][64];
+    __shared__ float fin_w[WAVES][32];
+    __shared__ __attribute__((aligned(16))) float s_stage_w[WAVES][kFinStage * 32];
+    __shared__ float s_tail_w[WAVES][64];
     // the per-thread buffer of the two-pass reduction: plan.nbuf floats of dynamic LDS (a
     // static kMaxThreads buffer would halve the workgroups per CU for every T)
     extern __shared__ float s_chunk[];
     float* fin = fin_w[wv];
     float* s_stage = s_stage_w[wv];
     float* s_tail = s_tail_w[wv];
-    for (int t = plan.nchunks + (int)threadIdx.x; t < plan.nbuf; t += 64 * kFinWaves) s_chunk[t] = 0.0f;
-    for (int c = wv; c < plan.nchunks; c += kFinWaves) {
+    for (int t = plan.nchunks + (int)threadIdx.x; t < plan.nbuf; t += 64 * WAVES) s_chunk[t] = 0.0f;
+    for (int c = wv; c < plan.nchunks; c += WAVES) {
         const int64_t off = plan.off(c);
         const ChunkGeo& geo = plan.geo(c);
         const int64_t s = geo.size;
@@ -1953,6 +1956,11 @@ int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, flo
             hipLaunchKernelGGL((l1_partial_kernel<false, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn);
         int rc = hip_check(hipGetLastError(), "l1_partial_kernel launch");
         if (rc) return rc;
+    }
+    if (plan.nchunks == 1) {
+        hipLaunchKernelGGL((l1_finalize_kernel<Op, 1>), dim3((unsigned)n), dim3(64), (size_t)plan.nbuf * sizeof(float), st,
+                           x, d, plan, part, sum_out, l1, fm, hist, zn);
+        return hip_check(hipGetLastError(), "l1_finalize_kernel launch");
     }
     hipLaunchKernelGGL(l1_finalize_kernel<Op>, dim3((unsigned)n), dim3(64 * kFinWaves), (size_t)plan.nbuf * sizeof(float), st,
                        x, d, plan, part, sum_out, l1, fm, hist, zn);
