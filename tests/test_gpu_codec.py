@@ -84,3 +84,20 @@ def test_malformed_messages_are_reported(gpu_ready):
         uqdme.decode_messages(uqdme.TypeMessages.from_messages([bytes(b) for b in bad], 30000))
     ok = uqdme.decode_messages(uqdme.TypeMessages.from_messages(good, 30000))
     assert torch.equal(ok.codes, tc.codes)
+
+
+def test_empty_vectors_header_only(gpu_ready):
+    """d = 0: header-only messages (the d == 0 pack path), byte-identical to the CPU
+    restatement's, decoded back to L1 with no codes."""
+    import uqdme
+    n = 3
+    tc = uqdme.TypeCodes(codes=torch.zeros((n, 0), dtype=torch.int8, device="cuda"),
+                         l1=torch.tensor([0.0, 1.5, 2.25], device="cuda"), m=0,
+                         overflow=torch.zeros(n, dtype=torch.int32, device="cuda"))
+    msgs = uqdme.encode_messages(tc, exact_zero_signs=True)
+    gpu = msgs.messages()
+    for j in range(n):
+        assert gpu[j] == C.codec_encode(np.zeros(0, np.int8), 0, np.float32(tc.l1[j].item()), True), j
+    back = uqdme.decode_messages(msgs)
+    assert back.codes.shape == (n, 0)
+    assert torch.equal(back.l1, tc.l1)

@@ -2597,9 +2597,13 @@ int uq_tc_encode(const int8_t* codes, const float* l1, int64_t n, int64_t d, int
     if ((rc = hip_check(hipGetLastError(), "tc_scan_kernel launch"))) return rc;
     if (nch == 0) {
         // d == 0: header-only messages, written by one "chunk" each
-        hipLaunchKernelGGL(tc_pack_kernel, dim3(1, (unsigned)std::min<int64_t>(n, kMaxGridY)), dim3(256), 0, st, d, m, exact,
-                           l1, tabs, scratch, cwords, states, offsets, msgs);
-        return hip_check(hipGetLastError(), "tc_pack_kernel launch");
+        for (int64_t j0 = 0; j0 < n; j0 += kMaxGridY) {
+            const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
+            hipLaunchKernelGGL(tc_pack_kernel, dim3(1, (unsigned)nj), dim3(256), 0, st, d, m, exact, l1 + j0, tabs + j0,
+                               scratch, cwords, states, offsets + j0, msgs);
+            if ((rc = hip_check(hipGetLastError(), "tc_pack_kernel launch"))) return rc;
+        }
+        return UQ_OK;
     }
     for (int64_t j0 = 0; j0 < n; j0 += kMaxGridY) {
         const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
