@@ -1698,10 +1698,13 @@ tile_out_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __
 
 // =====================================================================================
 // K3: est[i] (+)= q[j][i] / n_div, j = 0..n-1 in order (ND:137-138).
-// Each thread owns 4 consecutive columns; loads for 8 clients are issued ahead.
+// Each thread owns 4 consecutive columns; loads for 8 clients are issued ahead.  1024-thread
+// workgroups (16 KB of a client row each): 0.85-0.88 -> 0.75-0.78 ms at 1024 x 2^20 against
+// 256 (tools/exp/exp_mean.hip, profiles/r03s_exp_mean_variants.jsonl).
 // =====================================================================================
+constexpr int kMeanThreads = 1024;
 template <bool VEC4>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kMeanThreads)
 client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, int64_t ld, float n_div, int accumulate,
                    float* __restrict__ est) {
     const int64_t col = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
@@ -1786,6 +1789,7 @@ codes_decode_kernel(const int8_t* __restrict__ codes, const float* __restrict__ 
 // kMeanUnroll clients, double-buffered: batch b+1 (crossing group boundaries) is in
 // flight while batch b is summed.
 constexpr int kMeanCpt = 8;
+constexpr int kCodesMeanThreads = 512;          // per workgroup: the tables serve 4 K columns
 constexpr int kMeanUnroll = 16;
 static_assert(kMeanClients == 2 * kMeanUnroll, "two code batches per table group");
 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
@@ -1814,7 +1818,7 @@ __device__ __forceinline__ void mean_add_batch(float (&e)[kMeanCpt], const uint2
 __device__ __forceinline__ void mean_build_tables(float (*tabn)[256], const float* __restrict__ l1,
                                                   const int32_t* __restrict__ kmaxv, int64_t j0, int nb, int wid,
                                                   int lane, float fm, float n_div) {
-    for (int jj = wid; jj < nb; jj += 256 / kWave) {
+    for (int jj = wid; jj < nb; jj += kCodesMeanThreads / kWave) {
         const float L = l1[j0 + jj];                // wave-uniform: scalar loads
         const int km = min(127, max(0, kmaxv[j0 + jj]));
         for (int k = lane; k <= km; k += kWave) {
@@ -1833,18 +1837,19 @@ __device__ __forceinline__ void mean_add_bytes(float (&e)[kMeanCpt], const int8_
             if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[(j0 + jj) * d + i0 + k]];
 }
 
-// ALL: every thread's kMeanCpt columns lie inside d (d a multiple of 256 * kMeanCpt), so no
+// ALL: every thread's kMeanCpt columns lie inside d (d a multiple of kCodesMeanThreads *
+// kMeanCpt), so no
 // per-thread `full` test anywhere (a per-thread guard around the adds cost the loads'
 // overlap in other kernels here).
 template <bool VEC, bool ALL = false>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kCodesMeanThreads)
 codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, const int32_t* __restrict__ kmaxv,
                   int64_t n, int64_t d, float fm, float n_div, int accumulate, float* __restrict__ est) {
     __shared__ float tabn[kMeanClients][256];     // indexed by the raw code byte, sign included
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);
-    const int64_t i0 = ((int64_t)blockIdx.x * 256 + tid) * kMeanCpt;
+    const int64_t i0 = ((int64_t)blockIdx.x * kCodesMeanThreads + tid) * kMeanCpt;
     const bool full = ALL || (VEC && i0 + kMeanCpt <= d);
     float e[kMeanCpt];
 #pragma unroll
@@ -2461,17 +2466,18 @@ int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax,
     if (!est || (n > 0 && (!codes || !l1 || !kmax))) return fail(UQ_E_INVALID, "null pointer");
     hipStream_t st = (hipStream_t)stream;
     const bool vec = (n == 0 || aligned16(codes)) && aligned16(est) && d % 16 == 0;
-    const int64_t blocks = (d + 256 * kMeanCpt - 1) / (256 * kMeanCpt);
+    const int64_t blocks = (d + kCodesMeanThreads * kMeanCpt - 1) / (kCodesMeanThreads * kMeanCpt);
     if (blocks > 0x7FFFFFFF) return fail(UQ_E_INVALID, "d too large");
-    if (vec && d % (256 * kMeanCpt) == 0)
-        hipLaunchKernelGGL((codes_mean_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, kmax, n,
-                           d, (float)m, n_div, accumulate, est);
+    const dim3 tb(kCodesMeanThreads);
+    if (vec && d % (kCodesMeanThreads * kMeanCpt) == 0)
+        hipLaunchKernelGGL((codes_mean_kernel<true, true>), dim3((unsigned)blocks), tb, 0, st, codes, l1, kmax, n, d,
+                           (float)m, n_div, accumulate, est);
     else if (vec)
-        hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, kmax, n, d,
-                           (float)m, n_div, accumulate, est);
+        hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), tb, 0, st, codes, l1, kmax, n, d, (float)m,
+                           n_div, accumulate, est);
     else
-        hipLaunchKernelGGL(codes_mean_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, codes, l1, kmax, n, d,
-                           (float)m, n_div, accumulate, est);
+        hipLaunchKernelGGL(codes_mean_kernel<false>, dim3((unsigned)blocks), tb, 0, st, codes, l1, kmax, n, d, (float)m,
+                           n_div, accumulate, est);
     return hip_check(hipGetLastError(), "codes_mean_kernel launch");
 }
 
@@ -2484,11 +2490,11 @@ int uq_client_mean_f32(const float* q, int64_t n, int64_t d, int64_t ld, float n
     hipStream_t st = (hipStream_t)stream;
     const bool vec4 = (n == 0 || aligned16(q)) && aligned16(est) && (d % 4 == 0) && (ld % 4 == 0);
     const int64_t threads = (d + 3) / 4;
-    dim3 grid((unsigned)((threads + 255) / 256));
+    dim3 grid((unsigned)((threads + kMeanThreads - 1) / kMeanThreads));
     if (vec4)
-        hipLaunchKernelGGL(client_mean_kernel<true>, grid, dim3(256), 0, st, q, n, d, ld, n_div, accumulate, est);
+        hipLaunchKernelGGL(client_mean_kernel<true>, grid, dim3(kMeanThreads), 0, st, q, n, d, ld, n_div, accumulate, est);
     else
-        hipLaunchKernelGGL(client_mean_kernel<false>, grid, dim3(256), 0, st, q, n, d, ld, n_div, accumulate, est);
+        hipLaunchKernelGGL(client_mean_kernel<false>, grid, dim3(kMeanThreads), 0, st, q, n, d, ld, n_div, accumulate, est);
     return hip_check(hipGetLastError(), "client_mean_kernel launch");
 }
 
