@@ -109,3 +109,42 @@ def test_eden_c4_size_2pow22_vs_oracle(uq):
             assert abs(sg - float(sc)) <= 2 * np.spacing(np.float32(abs(sc)))
             exp = E.eden_decompress(bins, np.float32(sg), nbits, 37, d)
             assert G.bits_equal(out.cpu().numpy()[0], exp), (d, nbits)
+
+
+def test_round_trip_fused_path_matches_compress_decompress(uq):
+    """uq_eden_f32 fuses the bins into the receiver's first pass when D > 4096: its bits
+    equal compress -> decompress, also for norms outside the fast division range
+    [2^-39, 2^40) (tiny, huge, zero vectors), and bins / scale match the oracle (a zero
+    vector's 0/0 coordinates go to the last bin, as torch.bucketize puts NaN)."""
+    rng = np.random.default_rng(11)
+    d = 20000                                                  # D = 32768: two passes
+    rows = [rng.standard_normal(d) * s for s in (1.0, 1e-13, 1e9, 1e-15, 1e15, 3e-30)]
+    rows.append(np.zeros(d))
+    x = np.stack(rows).astype(np.float32)
+    seeds = [3, 4, 5, 6, 7, 8, 9]
+    for nbits in (1, 2):
+        xt = torch.as_tensor(x).cuda()
+        msg = uq.eden_compress(xt, nbits, seeds=seeds)
+        sep = uq.eden_decompress(msg).cpu().numpy()
+        fused = uq.eden_quantize(xt, nbits, seeds=seeds).cpu().numpy()
+        assert G.bits_equal(sep, fused), nbits
+        for j in range(len(seeds)):
+            with np.errstate(invalid="ignore"):
+                bins, sc, _, _ = E.eden_compress(x[j], nbits, seeds[j])
+            assert np.array_equal(msg.bins.cpu().numpy()[j], bins), (nbits, j)   # NaN -> last bin
+            sg = float(msg.scale.cpu()[j])
+            if np.isnan(sc):
+                assert np.isnan(sg), (nbits, j)
+            else:
+                assert abs(sg - float(sc)) <= 2 * np.spacing(np.float32(abs(sc))), (nbits, j)
+        assert np.isnan(fused[-1]).all()                        # 0 / 0 norm, as the reference
+
+
+@pytest.mark.parametrize("d", [1 << 20, (1 << 22) - 5])
+def test_rht_forward_two_and_three_passes_vs_oracle(uq, d):
+    """The forward RHT writes its last pass straight into the output (two passes) or copies
+    from the workspace (three passes)."""
+    rng = np.random.default_rng(d % 1000)
+    x = rng.standard_normal(d).astype(np.float32)
+    fwd = uq.randomized_hadamard_transform(torch.as_tensor(x).cuda().view(1, -1), [21]).cpu().numpy()[0]
+    assert G.bits_equal(fwd, E.rht(x, 21))

@@ -152,6 +152,16 @@ __device__ __forceinline__ DivPlan div_plan(float L) {
     p.thr = 0x1p-59f / p.den;
     return p;
 }
+// z / nrm of EDEN's bins (AS:329): the Markstein sequence for a divisor in [2^-39, 2^40)
+// (tools/markstein_check.c checks every f32 numerator for divisors over that range)
+__device__ __forceinline__ DivPlan div_plan_norm(float nv) {
+    DivPlan p;
+    p.den = nv;
+    p.fast = nv >= 0x1p-39f && nv < 0x1p40f;
+    p.y = 1.0f / nv;
+    p.thr = 0x1p-59f / nv;
+    return p;
+}
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void div4(const float (&xs)[4], const DivPlan& dp, float (&vs)[4]) {
     if (dp.fast) {
@@ -2107,17 +2117,30 @@ void fwht_dispatch(dim3 grid, const FwhtArgs& b, int lo, int k, hipStream_t st) 
 }
 
 // Runs the FWHT passes of one transform.  MODE of the first pass: 1 sender, 2 receiver.
-int launch_fwht(FwhtArgs a, int64_t n, bool receiver, float* buf, float* out, hipStream_t st) {
+// Receiver: passes in place in `buf`, the last into `out`.  Sender: passes alternate
+// between `buf` and `out` (out == buf: in place; the forward RHT passes its output so
+// that a two-pass transform needs no copy); *result = the buffer holding the result.
+// lo0 > 0 (receiver): the passes below bit lo0 are done already, into `buf`.
+int launch_fwht(FwhtArgs a, int64_t n, bool receiver, float* buf, float* out, hipStream_t st,
+                float** result = nullptr, int lo0 = 0) {
     const int p = ilog2_pow2(a.D);
-    int lo = 0, k = std::min(p, kFwhtLowBits);
-    bool first = true;
+    int lo = lo0, k = std::min(p - lo0, lo0 ? kFwhtHighBits : kFwhtLowBits);
+    bool first = lo0 == 0;
+    float* cur = buf;                              // sender: the buffer the next pass writes
     for (;;) {
         const bool last = lo + k >= p;
         const int cols = lo == 0 ? 1 : kFwhtCols;
         const int64_t tiles = a.D / (((int64_t)1 << k) * cols);
         FwhtArgs b = a;
-        b.out = (last && receiver) ? out : buf;
-        if (!first) b.in = buf;
+        if (receiver) {
+            b.out = last ? out : buf;
+            if (!first) b.in = buf;
+        } else {
+            b.out = cur;
+            if (!first) b.in = cur == buf ? out : buf;
+            if (result) *result = cur;
+            cur = cur == buf ? out : buf;
+        }
         const dim3 grid((unsigned)tiles, (unsigned)n);
         if (first && !receiver) {
             if (last) fwht_dispatch<1, true, false>(grid, b, lo, k, st);
@@ -2829,8 +2852,9 @@ int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inver
     hipStream_t st = (hipStream_t)stream;
     float* buf = (float*)((char*)ws + w.vec_off);
     if (!inverse) {                                           // AS:123-141: pad, * diag, H
-        int rc = launch_fwht(a, n, false, buf, nullptr, st);
-        if (rc) return rc;
+        float* res = nullptr;
+        int rc = launch_fwht(a, n, false, buf, out, st, &res);
+        if (rc || res == out) return rc;
         return hip_check(hipMemcpyAsync(out, buf, (size_t)n * w.D * sizeof(float), hipMemcpyDeviceToDevice, st),
                          "copy rht");
     }
@@ -2865,6 +2889,31 @@ int uq_eden_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
     return UQ_OK;
 }
 
+// The sender up to the norms: RHT (AS:123-141) and torch.norm (AS:329); *rot = the rotated
+// vectors (one of the workspace's two vector buffers).
+int eden_front(const float* x, int64_t n, int64_t dim, const EdenTables& tab, const int8_t* signs,
+               const int32_t* sign_row, const EdenLayout& w, char* wsb, FwhtArgs& a, float** rot, hipStream_t st) {
+    float* nrm = (float*)(wsb + w.nrm_off);
+    a = FwhtArgs{};
+    a.in = x;
+    a.signs = signs;
+    a.sign_row = sign_row;
+    a.D = w.D;
+    a.dim = dim;
+    a.sqrtD = (float)std::sqrt((double)w.D);                 // np.sqrt(d) -> f32 operand
+    a.tab = tab;
+    float* vec = (float*)(wsb + w.vec_off);
+    int rc = launch_fwht(a, n, false, vec, vec, st, rot);
+    if (rc) return rc;
+    if (w.D % kNormChunk == 0)
+        hipLaunchKernelGGL(eden_norm_whole_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads),
+                           0, st, *rot, n, w.D, nrm);
+    else
+        hipLaunchKernelGGL(eden_norm_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads),
+                           0, st, *rot, n, w.D, nrm);
+    return hip_check(hipGetLastError(), "eden_norm_kernel launch");                 // AS:329 torch.norm
+}
+
 int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
                          const int32_t* sign_row, uint8_t* bins, float* scale, void* ws, size_t ws_bytes,
                          void* stream) {
@@ -2877,26 +2926,11 @@ int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, 
     if (!ws || ws_bytes < w.total) return fail(UQ_E_WORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
-    float* vec = (float*)(wsb + w.vec_off);
     float* nrm = (float*)(wsb + w.nrm_off);
     double* part = (double*)(wsb + w.part_off);
-    FwhtArgs a{};
-    a.in = x;
-    a.signs = signs;
-    a.sign_row = sign_row;
-    a.D = w.D;
-    a.dim = dim;
-    a.sqrtD = (float)std::sqrt((double)w.D);                 // np.sqrt(d) -> f32 operand
-    a.tab = tab;
-    rc = launch_fwht(a, n, false, vec, nullptr, st);                               // AS:123-141
-    if (rc) return rc;
-    if (w.D % kNormChunk == 0)
-        hipLaunchKernelGGL(eden_norm_whole_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads),
-                           0, st, vec, n, w.D, nrm);
-    else
-        hipLaunchKernelGGL(eden_norm_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads),
-                           0, st, vec, n, w.D, nrm);
-    rc = hip_check(hipGetLastError(), "eden_norm_kernel launch");                  // AS:329 torch.norm
+    FwhtArgs a;
+    float* vec = nullptr;
+    rc = eden_front(x, n, dim, tab, signs, sign_row, w, wsb, a, &vec, st);
     if (rc) return rc;
     hipLaunchKernelGGL(eden_bins_kernel, dim3((unsigned)w.tiles, (unsigned)n), dim3(256), 0, st, vec, w.D, a.sqrtD,
                        nrm, tab, bins, part, w.tiles);
@@ -2934,9 +2968,44 @@ int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbit
     const EdenLayout w = eden_layout(n < 0 ? 0 : n, dim < 0 ? 0 : dim);
     uint8_t* bins = (uint8_t*)((char*)ws + w.bins_off);
     float* scale = scale_out ? scale_out : (float*)((char*)ws + w.scale_off);
-    int rc = uq_eden_compress_f32(x, n, dim, nbits, signs, sign_row, bins, scale, ws, ws_bytes, stream);
+    if (w.D <= ((int64_t)1 << kFwhtLowBits) || n > 65535) {
+        // a single FWHT pass (or an invalid n, reported there): compress, then decompress
+        int rc = uq_eden_compress_f32(x, n, dim, nbits, signs, sign_row, bins, scale, ws, ws_bytes, stream);
+        if (rc) return rc;
+        return uq_eden_decompress_f32(bins, scale, n, dim, nbits, signs, sign_row, out, ws, ws_bytes, stream);
+    }
+    EdenTables tab;
+    int rc = eden_check(n, dim, nbits, signs, &tab);
     if (rc) return rc;
-    return uq_eden_decompress_f32(bins, scale, n, dim, nbits, signs, sign_row, out, ws, ws_bytes, stream);
+    if (n == 0 || dim == 0) return UQ_OK;
+    if (!x || !out) return fail(UQ_E_INVALID, "null pointer");
+    if (!ws || ws_bytes < w.total) return fail(UQ_E_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* wsb = (char*)ws;
+    float* nrm = (float*)(wsb + w.nrm_off);
+    double* part = (double*)(wsb + w.part_off);
+    FwhtArgs a;
+    float* rot = nullptr;
+    rc = eden_front(x, n, dim, tab, signs, sign_row, w, wsb, a, &rot, st);
+    if (rc) return rc;
+    // KE3 fused with the receiver's first pass (the bins stay in registers), in place: a
+    // workgroup reads its whole 4096-element tile before it writes it
+    float* buf = rot;
+    FwhtArgs b = a;
+    b.in = rot;
+    b.out = buf;
+    b.nrm = nrm;
+    b.part = part;
+    hipLaunchKernelGGL((fwht_low4096_kernel<3, false, false>), dim3((unsigned)w.tiles, (unsigned)n), dim3(256), 0, st, b);
+    rc = hip_check(hipGetLastError(), "fwht_low4096_kernel (bins) launch");        // AS:329-335, 383
+    if (rc) return rc;
+    hipLaunchKernelGGL(eden_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, w.tiles, nrm, n,
+                       scale);
+    rc = hip_check(hipGetLastError(), "eden_scale_kernel launch");
+    if (rc) return rc;
+    FwhtArgs r = a;                                                                  // AS:378-413
+    r.scale = scale;
+    return launch_fwht(r, n, true, buf, out, st, nullptr, kFwhtLowBits);
 }
 
 }  // extern "C"

@@ -18,7 +18,8 @@
 //                          lookup (receiver), the last pass / sqrt(D) (and * diag * scale,
 //                          truncation to dim on the receiver)
 //   KE2 eden_norm_kernel   torch.norm(v, 2) in torch CPU order: 8 lanes of fma, lanes in order
-//   KE3 eden_bins_kernel   bucketize -> u8 bins, fp64 partial dot per tile
+//   KE3 eden_bins_kernel   bucketize -> u8 bins, fp64 partial dot per tile (the round trip
+//                          fuses it into the receiver's first low pass, MODE 3)
 //   KE4 eden_scale_kernel  dot partials in tile order, scale = f32(nrm*nrm) / f32(dot)
 
 constexpr int kFwhtT = 256;            // threads per FWHT workgroup
@@ -84,12 +85,16 @@ rht_signs_kernel(const int32_t* __restrict__ seeds, int64_t D, int8_t* __restric
 // `dim`, zero-padded, times the diagonal.  MODE 2 (first receiver pass): in = u8 bins,
 // value = centroid.  LAST: divide by sqrt(D) as f32 (AS:114); RECV_LAST additionally
 // multiplies by the diagonal and the per-client scale and writes only [0, dim).
+// MODE 3 (fwht_low4096_kernel only, the round trip uq_eden_f32): in = rotated vectors;
+// KE3's bins and partial dots, then the receiver's first pass on the centroids.
 struct FwhtArgs {
     const void* in;
     float* out;
     const int8_t* signs;        // [rows][D] diagonal rows
     const int32_t* sign_row;    // [n] row of each client
     const float* scale;         // [n] (receiver last pass)
+    const float* nrm;           // [n] norms (MODE 3)
+    double* part;               // [n][tiles] partial dots (MODE 3)
     int64_t D, dim;
     float sqrtD;
     EdenTables tab;
@@ -187,10 +192,20 @@ __device__ __forceinline__ int pad17(int e) { return e + (e >> 4); }
 // Low pass over 4096 contiguous elements, index e = b0 + 16 b1 + 256 b2: round 1 thread
 // (b1, b2) holds b0 = 0..15 (bits 0-3), round 2 thread (b0, b2) holds b1 (bits 4-7),
 // round 3 thread (b0, b1) holds b2 (bits 8-11).
+// KE3's per-tile fp64 dot: butterfly sums inside each wave, the 4 wave sums in order
+// (one order for both kernels that compute it, so the same partials).
+__device__ __forceinline__ void dot_to_waves(double dot, int tid, double* red) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) dot += __shfl_xor(dot, o, kWave);
+    if ((tid & (kWave - 1)) == 0) red[tid / kWave] = dot;
+}
+__device__ __forceinline__ double dot_of_waves(const double* red) { return ((red[0] + red[1]) + red[2]) + red[3]; }
+
 template <int MODE, bool LAST, bool RECV_LAST>
 __global__ void __launch_bounds__(256)
 fwht_low4096_kernel(FwhtArgs a) {
     __shared__ float s[4096 + 256];
+    __shared__ double red[MODE == 3 ? 4 : 1];
     const int64_t vec = blockIdx.y;
     const int tid = threadIdx.x;
     const int64_t D = a.D;
@@ -221,6 +236,30 @@ fwht_low4096_kernel(FwhtArgs a) {
             const uint8_t* bb = reinterpret_cast<const uint8_t*>(&bv);
 #pragma unroll
             for (int i = 0; i < 16; ++i) v[i] = a.tab.c[bb[i]];                  // AS:383
+        } else if (MODE == 3) {
+            // round trip (uq_eden_f32): KE3 on the rotated vector, then the receiver's first
+            // pass on the centroids -- the bins never leave registers.  Same per-thread dot
+            // order and reduction as eden_bins_kernel, so the same partials.
+            const float* p = (const float*)a.in + vec * D + i0;
+            const DivPlan dp = div_plan_norm(a.nrm[vec]);
+            double dot = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
+                const float xs[4] = {t.x, t.y, t.z, t.w};
+                const float ys[4] = {xs[0] * a.sqrtD, xs[1] * a.sqrtD, xs[2] * a.sqrtD, xs[3] * a.sqrtD};
+                float zs[4];
+                div4(ys, dp, zs);                                               // AS:329 / norm
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float z = zs[c];
+                    int b = 0;
+                    for (int j = 0; j < a.tab.nb; ++j) b += !(a.tab.b[j] >= z) ? 1 : 0;   // NaN -> nb, as torch.bucketize
+                    v[4 * q + c] = a.tab.c[b];                                  // AS:383
+                    dot += (double)a.tab.c[b] * (double)xs[c];                  // AS:335
+                }
+            }
+            dot_to_waves(dot, tid, red);              // read back after round 1's barrier
         } else {
             const float* p = (const float*)a.in + vec * D + i0;
 #pragma unroll
@@ -235,6 +274,7 @@ fwht_low4096_kernel(FwhtArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[pad17(i + 16 * b1r1 + 256 * b2r1)] = v[i];
     __syncthreads();
+    if (MODE == 3 && tid == 0) a.part[vec * gridDim.x + blockIdx.x] = dot_of_waves(red);
     const int b0 = tid & 15, b2 = tid >> 4;                        // round 2: (b0, b2)
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = s[pad17(b0 + 16 * i + 256 * b2)];
@@ -246,6 +286,23 @@ fwht_low4096_kernel(FwhtArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = s[pad17(b0 + 16 * b1 + 256 * i)];
     stages16(v);                                                   // bits 8-11
+    if (!RECV_LAST) {
+        // back through LDS so that each lane stores 16 contiguous bytes (float4 stores
+        // of 1 KB per wave instead of 16 dword stores of 256 B)
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[pad17(b0 + 16 * b1 + 256 * i)] = LAST ? v[i] / a.sqrtD : v[i];   // AS:114
+        __syncthreads();
+        float* o = a.out + vec * D + base;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 4 * (tid + 256 * j);
+            const int pe = pad17(e);
+            const f32x4 t = {s[pe], s[pe + 1], s[pe + 2], s[pe + 3]};
+            __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(o + e));
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int64_t gi = base + b0 + 16 * b1 + 256 * i;          // lanes: consecutive b0 + 16 b1
@@ -560,11 +617,21 @@ eden_bins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const floa
             x[4 * q] = t.x; x[4 * q + 1] = t.y; x[4 * q + 2] = t.z; x[4 * q + 3] = t.w;
         }
         uint32_t w[4] = {0, 0, 0, 0};
+        const DivPlan dp = div_plan_norm(nv);
+        float zs[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float ys[4] = {x[4 * q] * sqrtD, x[4 * q + 1] * sqrtD, x[4 * q + 2] * sqrtD, x[4 * q + 3] * sqrtD};
+            float zq[4];
+            div4(ys, dp, zq);                                      // AS:329 vec * sqrt(D) / norm
+#pragma unroll
+            for (int c = 0; c < 4; ++c) zs[4 * q + c] = zq[c];
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const float z = (x[i] * sqrtD) / nv;                   // AS:329 vec * sqrt(D) / norm
+            const float z = zs[i];
             int b = 0;
-            for (int j = 0; j < tab.nb; ++j) b += (tab.b[j] < z) ? 1 : 0;   // bucketize, right=False
+            for (int j = 0; j < tab.nb; ++j) b += !(tab.b[j] >= z) ? 1 : 0;   // bucketize, right=False (NaN -> nb)
             w[i >> 2] |= (uint32_t)b << (8 * (i & 3));
             dot += (double)tab.c[b] * (double)x[i];                // AS:335 dot(centroids[bins], vec)
         }
@@ -574,19 +641,15 @@ eden_bins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const floa
             const float x = p[i];
             const float z = (x * sqrtD) / nv;
             int b = 0;
-            for (int j = 0; j < tab.nb; ++j) b += (tab.b[j] < z) ? 1 : 0;
+            for (int j = 0; j < tab.nb; ++j) b += !(tab.b[j] >= z) ? 1 : 0;
             bp[i] = (uint8_t)b;
             dot += (double)tab.c[b] * (double)x;
         }
     }
-    __shared__ double red[256];
-    red[tid] = dot;
+    __shared__ double red[4];
+    dot_to_waves(dot, tid, red);
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) red[tid] += red[tid + o];
-        __syncthreads();
-    }
-    if (tid == 0) part[vec * tiles + blockIdx.x] = red[0];
+    if (tid == 0) part[vec * tiles + blockIdx.x] = dot_of_waves(red);
 }
 
 // ---- KE4: scale per client ---------------------------------------------------------------
