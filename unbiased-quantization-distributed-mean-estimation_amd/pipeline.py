@@ -95,12 +95,14 @@ class DMEPipeline:
             raise ValueError("X must hold one f32 draw per client on the device")
 
     # ---- output placement ------------------------------------------------------------
-    def probe_outputs(self, x, X, candidates: int = 16, reps: int = 3, batch: int = 4, spread: float = 1.10):
+    def probe_outputs(self, x, X, candidates: int = 16, reps: int = 3, batch: int = 4, spread: float = 1.15):
         """Time K2 on output sets (the current one included), keep the fastest.  Sets are
         added `batch` at a time, up to `candidates`, until the probe has seen both speeds
-        (slowest / fastest >= `spread`; the modes are ~17 % apart): with ~30-60 % of sets
-        fast, six fixed candidates left ~1 rank in 8 without a fast set.  Needs the batch's
-        L1 (runs K1 first).  Returns the report (ms per candidate)."""
+        (slowest / fastest >= `spread`; the fast and slow modes are 15-20 % apart, and
+        spread 1.10 once stopped on an intermediate 1.74 ms set against 1.92-1.98 ms ones,
+        profiles/r04a_bench.json): with ~30-60 % of sets fast, six fixed candidates left
+        ~1 rank in 8 without a fast set.  Needs the batch's L1 (runs K1 first).  Returns
+        the report (ms per candidate)."""
         self._check(x, X)
         self.l1_norms(x)
         sets, times = [(self.q, self.codes)], []
