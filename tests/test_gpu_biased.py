@@ -248,3 +248,26 @@ def test_torch_ties_many_listed_clients_stop_levels_early(uq):
         amb += int(A)
     assert amb >= 128, amb
     uq.check_status()
+
+
+def test_tiny_vectors_several_selections(uq):
+    """d < 8 (a single scalar torch chunk, K1b's lane-0 path) with |Delta| >= 2: the first
+    radix digit's histogram must count each coordinate once.  Both tie rules, against the
+    oracle."""
+    rng = np.random.default_rng(5)
+    rows = []
+    while len(rows) < 24:
+        d = int(rng.integers(2, 8))
+        R = int(rng.choice([1, 2, 3, 4, 5, 6, 8]))
+        x = (rng.standard_normal(d) * rng.choice([1, 10, 0.1])).astype(f32)
+        _, _, D, _ = C.biased_quantize(x, rate_to_m(R, d), 1, 1)
+        if abs(D) >= 2:
+            rows.append((x, R))
+    for x, R in rows:
+        m = rate_to_m(R, x.shape[0])
+        for ties, rule in (("lowest", 1), ("torch", 0)):
+            exp, _, D, A = C.biased_quantize(x, m, 1, rule)
+            out, info = run(uq, x, R, 1, ties)
+            assert info[0] == D and bool(info[1] & 1) == A, (x, R, ties)
+            assert G.bits_equal(out, exp), (x, R, ties)
+    uq.check_status()

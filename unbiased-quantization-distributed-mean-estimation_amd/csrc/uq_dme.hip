@@ -435,11 +435,14 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
         const int64_t s = geo.size;
         float chunk_sum;
         if (s < 8) {
-            // ATen scalar row_sum (ILP 4, rows < step -> all rows land in acc0).
+            // ATen scalar row_sum (ILP 4, rows < step -> all rows land in acc0).  Lane 0
+            // only: the op may count each element (RezKHistOp's histogram)
             float p[4] = {0.f, 0.f, 0.f, 0.f};
-            if (s >= 4)
-                for (int k = 0; k < 4; ++k) p[k] = 0.f + op(xv[off + k]);
-            for (int64_t k = (s >= 4 ? 4 : 0); k < s; ++k) p[0] += op(xv[off + k]);
+            if (lane == 0) {
+                if (s >= 4)
+                    for (int k = 0; k < 4; ++k) p[k] = 0.f + op(xv[off + k]);
+                for (int64_t k = (s >= 4 ? 4 : 0); k < s; ++k) p[0] += op(xv[off + k]);
+            }
             chunk_sum = ((p[0] + p[1]) + p[2]) + p[3];
         } else {
             const int64_t vs = s / 8, rows = vs / 4;
