@@ -271,3 +271,31 @@ def test_tiny_vectors_several_selections(uq):
             assert info[0] == D and bool(info[1] & 1) == A, (x, R, ties)
             assert G.bits_equal(out, exp), (x, R, ties)
     uq.check_status()
+
+
+def test_fuzz_small_vectors_vs_oracle(uq):
+    """Seeded fuzz over d = 1..600: Gaussian, wide-range, tie-heavy integer and zero-heavy
+    rows at random rates, both tie rules, bit-exact against the oracle."""
+    rng = np.random.default_rng(2024)
+    rates = [0.5, 1, 1.5, 2, 3, 4, 6, 8]
+    for t in range(160):
+        d = int(rng.integers(1, 601))
+        kind = t % 4
+        if kind == 0:
+            x = rng.standard_normal(d)
+        elif kind == 1:
+            x = rng.standard_normal(d) * np.exp(rng.uniform(-20, 20, d))
+        elif kind == 2:
+            x = rng.integers(-3, 4, d)
+        else:
+            x = rng.standard_normal(d) * (rng.random(d) < 0.2)
+        x = x.astype(f32)
+        R = float(rng.choice(rates))
+        m = rate_to_m(R, d)
+        for ties, rule in (("lowest", 1), ("torch", 0)):
+            with np.errstate(all="ignore"):
+                exp, _, D, A = C.biased_quantize(x, m, 1, rule)
+            out, info = run(uq, x, R, 1, ties)
+            assert info[0] == D and bool(info[1] & 1) == A, (t, d, R, ties)
+            assert G.bits_equal(out, exp), (t, d, R, ties)
+    uq.check_status()
