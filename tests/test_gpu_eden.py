@@ -148,3 +148,26 @@ def test_rht_forward_two_and_three_passes_vs_oracle(uq, d):
     x = rng.standard_normal(d).astype(np.float32)
     fwd = uq.randomized_hadamard_transform(torch.as_tensor(x).cuda().view(1, -1), [21]).cpu().numpy()[0]
     assert G.bits_equal(fwd, E.rht(x, 21))
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 5, 16, 100, 4095, 4096, 4097, 5000, 8192, 12289])
+def test_eden_dims_across_pass_shapes_vs_oracle(uq, d):
+    """Dimensions around the pass shapes: a single generic pass (D < 4096), the low pass
+    alone (D = 4096, compress + decompress), two and three passes with the fused round
+    trip (D > 4096); bins / scale / outputs against the oracle, and the round trip equal to
+    compress -> decompress."""
+    rng = np.random.default_rng(d)
+    n = 3
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    seeds = [int(s) for s in rng.integers(0, 100, n)]
+    for nbits in (1, 2):
+        xt = torch.as_tensor(x).cuda()
+        out, scale = uq.eden_quantize(xt, nbits, seeds=seeds, return_scale=True)
+        msg = uq.eden_compress(xt, nbits, seeds=seeds)
+        assert G.bits_equal(uq.eden_decompress(msg).cpu().numpy(), out.cpu().numpy())
+        out, scale = out.cpu().numpy(), scale.cpu().numpy()
+        for j in range(n):
+            bins, sc, _, _ = E.eden_compress(x[j], nbits, seeds[j])
+            assert np.array_equal(msg.bins.cpu().numpy()[j], bins), (d, nbits, j)
+            assert abs(float(scale[j]) - float(sc)) <= 2 * np.spacing(np.float32(abs(sc))), (d, nbits, j)
+            assert G.bits_equal(out[j], E.eden_decompress(bins, scale[j], nbits, seeds[j], d)), (d, nbits, j)
