@@ -16,7 +16,9 @@ for stride in (4096,):
         for inplace in (1, 0):
             dst = a if inplace else b
             f = lambda: L.tile_bw(a.data_ptr(), dst.data_ptr(), n, D, stride, cols, sp)
-            assert f() == 0
+            rc = f()
+            if rc != 0:
+                raise RuntimeError(f"tile_bw returned {rc}")
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
