@@ -50,7 +50,10 @@ def run():
             qc = calls["q+codes"][0]
             calls["l1,q+codes"] = (lambda: h(x.data_ptr(), n, d, 1, l1o.data_ptr(), ws.data_ptr(), b.value, sp) or qc(), 13)
         for cname, (fn, bpe) in calls.items():
-            for _ in range(3): assert fn() == 0
+            for _ in range(3):
+                rc = fn()
+                if rc != 0:
+                    raise RuntimeError(f"{cname} returned {rc}")
             torch.cuda.synchronize()
             e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
             e0.record()

@@ -12,6 +12,12 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "unbiased-quantization-distributed-mean-estimation_amd")
 SO = os.path.join(PKG, "_build", "abl", "tieprof.so")
+def ok(rc):
+    """Raise on a non-zero C-ABI status (not an assert: calls must run under python -O)."""
+    if rc != 0:
+        raise RuntimeError(f"C-ABI call returned {rc}")
+
+
 PHASES = ["fill", "sweeps", "search", "swaps", "pivot", "lds", "mark", "levels(count)"]
 
 
@@ -35,7 +41,7 @@ def run(dist, n):
     info = torch.empty((n, 2), dtype=torch.int32, device="cuda")
     L = ctypes.CDLL(SO)
     b = ctypes.c_size_t()
-    assert L.uq_biased_workspace_bytes(ctypes.c_int64(n), ctypes.c_int64(d), 1, ctypes.byref(b)) == 0
+    ok(L.uq_biased_workspace_bytes(ctypes.c_int64(n), ctypes.c_int64(d), 1, ctypes.byref(b)))
     ws = torch.zeros(b.value, dtype=torch.uint8, device="cuda")
     prof = torch.zeros(8, dtype=torch.int64, device="cuda")
     L.uq_debug_set_tie_prof.argtypes = [ctypes.c_void_p]
@@ -45,12 +51,12 @@ def run(dist, n):
     sp = torch.cuda.current_stream().cuda_stream
     call = lambda: f(x.data_ptr(), out.data_ptr(), n, d, 224426, 1, 0, None, info.data_ptr(), ws.data_ptr(),  # noqa
                      b.value, sp)
-    assert call() == 0
+    ok(call())
     torch.cuda.synchronize()
-    assert L.uq_debug_set_tie_prof(ctypes.c_void_p(prof.data_ptr())) == 0
+    ok(L.uq_debug_set_tie_prof(ctypes.c_void_p(prof.data_ptr())))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    assert call() == 0
+    ok(call())
     e1.record()
     torch.cuda.synchronize()
     amb = int(((info[:, 1] & 8) != 0).sum())
