@@ -164,7 +164,27 @@ def main():
     sp = stream.cuda_stream
     P = lambda t: t.data_ptr()  # noqa: E731
 
+    # N > 1 over RCCL: the reduce of step k runs beside step k+1's kernels.  Two estimate
+    # buffers; step k+2 waits for reduce k before it overwrites that buffer (work.wait()
+    # orders the caller's stream after the collective, the host does not block).
+    overlap = dist is not None and BACKEND == "nccl" and args.mean_mode == "reduce"
+    est_bufs = [est, torch.empty_like(est)] if overlap else [est]
+    pending = [None] * len(est_bufs)
+    nstep = [0]
+
+    def drain():
+        for i, w in enumerate(pending):
+            if w is not None:
+                w.wait()
+                pending[i] = None
+
     def step(ev=None, pipeline=args.pipeline):
+        slot = nstep[0] % len(est_bufs)
+        nstep[0] += 1
+        est_s = est_bufs[slot]
+        if pending[slot] is not None:
+            pending[slot].wait()
+            pending[slot] = None
         if ev is not None:
             ev[0].record(stream)
         _lib.check(lib.uq_l1_torch_order_f32(P(x), n, d, T, P(l1), P(ws), nb, sp), "l1")
@@ -179,15 +199,16 @@ def main():
             ev[2].record(stream)
         if dist is None or args.mean_mode == "reduce":
             if pipeline == "q":
-                _lib.check(lib.uq_client_mean_f32(P(q), n, d, d, float(n_total), 0, P(est), sp), "mean")
+                _lib.check(lib.uq_client_mean_f32(P(q), n, d, d, float(n_total), 0, P(est_s), sp), "mean")
             else:
-                _lib.check(lib.uq_codes_mean_f32(P(codes), P(l1), P(ovf), n, d, m, float(n_total), 0, P(est), sp), "mean")
+                _lib.check(lib.uq_codes_mean_f32(P(codes), P(l1), P(ovf), n, d, m, float(n_total), 0, P(est_s), sp),
+                           "mean")
         if ev is not None:
             ev[3].record(stream)
         if dist is not None:
             if args.mean_mode == "reduce":
-                if BACKEND == "nccl":
-                    dist.reduce(est, dst=0, op=dist.ReduceOp.SUM)      # the one RCCL collective
+                if BACKEND == "nccl":                                  # the one RCCL collective
+                    pending[slot] = dist.reduce(est_s, dst=0, op=dist.ReduceOp.SUM, async_op=True)
                 else:
                     est_h = est.cpu()
                     dist.reduce(est_h, dst=0, op=dist.ReduceOp.SUM)
@@ -214,6 +235,7 @@ def main():
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
     for _ in range(args.warmup):                  # W untimed warmup steps
         step()
+    drain()
     torch.cuda.synchronize()
     _lib.check(lib.uq_check_status(P(ws), sp), "status after warmup")
     if dist is not None:
@@ -222,6 +244,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
+    drain()                                       # every reduce inside the timed region
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -281,7 +304,8 @@ def main():
                        "dist": args.dist,
                        "clients_per_gpu": n, "d": d, "bits_per_dimension": args.bits, "m": m,
                        "torch_threads_l1_order": T, "parallelism": f"client-sharded x{world}",
-                       "mean_mode": args.mean_mode if world > 1 else "single",
+                       "mean_mode": (args.mean_mode + (" (RCCL reduce of step k overlapped with step k+1)" if overlap else ""))
+                                    if world > 1 else "single",
                        **({"backend": BACKEND} if world > 1 and BACKEND != "nccl" else {}), "pipeline": args.pipeline},
             "kernel_ms": {"l1": round(float(seg_ms[0]), 4), "quantize": round(q_ms, 4),
                           "client_mean": round(float(seg_ms[2]), 4), "reduce": round(float(seg_ms[3]), 4)},
