@@ -1,0 +1,9 @@
+#!/bin/bash
+# GPU box: all GPU tests, smoke, bench, then the round profile (kernel-trace stats + PMC passes).
+set -e
+O=gpurun_out/r05a; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gputest.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
+bash tools/profile_round.sh $O codes
+echo r05a done
