@@ -69,6 +69,10 @@ def parse():
     ap.add_argument("--probe-candidates", type=int, default=16,
                     help="at most this many output-buffer sets probed once before warmup, until both "
                          "speeds are seen (pipeline.py); <= 1: no probe")
+    ap.add_argument("--probe-min", type=int, default=16,
+                    help="output sets the placement probe always times (16 x 5 GB at C2, freed after): the "
+                         "fastest of all 16 ran K2 1.69-1.71 ms in three processes, the spread-stop rule "
+                         "1.70-1.74 ms (profiles/r05b_exp_probe_all.jsonl)")
     ap.add_argument("--side-pipelines", action="store_true", default=True,
                     help="also time the other pipelines (reported under 'pipelines')")
     ap.add_argument("--no-side-pipelines", dest="side_pipelines", action="store_false")
@@ -157,7 +161,7 @@ def main():
     # resident buffers of the batched pipeline; the output placement is probed once (see
     # pipeline.py: K2's speed follows where q and the codes land in physical memory)
     pipe = uqdme.DMEPipeline(n, d, m=m, torch_threads=T)
-    probe = pipe.probe_outputs(x, X, candidates=args.probe_candidates) if args.probe_candidates > 1 else None
+    probe = pipe.probe_outputs(x, X, candidates=args.probe_candidates, min_candidates=args.probe_min) if args.probe_candidates > 1 else None
     q, codes, ovf, l1, est, ws, nb = pipe.q, pipe.codes, pipe.kmax, pipe.l1, pipe.est, pipe.ws, pipe.ws_bytes
     lib = _lib.load()
     stream = torch.cuda.current_stream(dev)

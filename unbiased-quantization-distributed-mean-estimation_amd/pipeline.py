@@ -95,7 +95,8 @@ class DMEPipeline:
             raise ValueError("X must hold one f32 draw per client on the device")
 
     # ---- output placement ------------------------------------------------------------
-    def probe_outputs(self, x, X, candidates: int = 16, reps: int = 3, batch: int = 4, spread: float = 1.15):
+    def probe_outputs(self, x, X, candidates: int = 16, reps: int = 3, batch: int = 4, spread: float = 1.15,
+                      min_candidates: int = 1):
         """Time K2 on output sets (the current one included), keep the fastest.  Sets are
         added `batch` at a time, up to `candidates`, until the probe has seen both speeds
         (slowest / fastest >= `spread`; the fast and slow modes are 15-20 % apart, and
@@ -120,7 +121,7 @@ class DMEPipeline:
             return e0.elapsed_time(e1) / reps
 
         times.append(time_set(*sets[0]))
-        while len(sets) < candidates and max(times) < spread * min(times):
+        while len(sets) < candidates and (len(sets) < min_candidates or max(times) < spread * min(times)):
             for _ in range(min(batch, candidates - len(sets))):
                 sets.append(self._alloc_outputs())
                 times.append(time_set(*sets[-1]))
