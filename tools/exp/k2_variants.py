@@ -21,6 +21,9 @@ VARIANTS = {
     "prio_mem": [(LOOP_ST, "        __builtin_amdgcn_s_setprio(2);\n" + LOOP_ST),
                  (LOOP_LD, LOOP_LD + "        __builtin_amdgcn_s_setprio(0);\n")],
     # ... only while it issues the loads of the next tile
+    # K1a: rows per unrolled group of the leaf loop (product: 4)
+    "k1_unroll4": [("        for (int r = 0; r < step; ++r) {", "#pragma unroll 4\n        for (int r = 0; r < step; ++r) {")],
+    "k1_unroll8": [("        for (int r = 0; r < step; ++r) {", "#pragma unroll 8\n        for (int r = 0; r < step; ++r) {")],
     "prio_ld": [(LOOP_LD, "        __builtin_amdgcn_s_setprio(2);\n" + LOOP_LD + "        __builtin_amdgcn_s_setprio(0);\n")],
 }
 
@@ -37,7 +40,8 @@ def build(names):
             shutil.copy(os.path.join(PKG, "csrc", f), d)
         src = os.path.join(d, "uq_dme.hip")
         s = open(src).read()
-        i = s.index("quantize_stream_kernel(const float* __restrict__ x")     # K2's body only
+        key = "l1_partial_kernel(" if name.startswith("k1_") else "quantize_stream_kernel(const float* __restrict__ x"
+        i = s.index(key)                                  # that kernel's body only
         j = s.index("__global__", i)
         body = s[i:j]
         for a, b in VARIANTS[name]:

@@ -220,6 +220,10 @@ struct AbsOp {            // AS:624  input_vector.abs().sum()
     uint32_t *h, *zn;
     __device__ static AbsOp make(const float*, float, int64_t) { return AbsOp{0.f, 0.f, nullptr, nullptr}; }
     __device__ float operator()(float v) const { return fabsf(v); }
+    __device__ void apply4(const float (&v)[4], float (&a)[4]) const {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] += fabsf(v[c]);
+    }
 };
 struct RezKOp {           // AS:648-649  k' = floor(m * p + 0.5), p = |x| / (L1 + 1e-12)
     DivPlan dp;
@@ -229,6 +233,15 @@ struct RezKOp {           // AS:648-649  k' = floor(m * p + 0.5), p = |x| / (L1 
         return RezKOp{div_plan(l1[vec]), fm, nullptr, nullptr};
     }
     __device__ float operator()(float v) const { return floorf(fm * div1(fabsf(v), dp) + 0.5f); }
+    // four elements per call (K1a): the quotients by div4 (one underflow test per four,
+    // the same bits as div1), then the per-element op; a[c] += op(v[c]) in the same order
+    __device__ void apply4(const float (&v)[4], float (&a)[4]) const {
+        const float ab[4] = {fabsf(v[0]), fabsf(v[1]), fabsf(v[2]), fabsf(v[3])};
+        float qs[4];
+        div4(ab, dp, qs);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] += floorf(fm * qs[c] + 0.5f);
+    }
 };
 // RezKOp that also counts the top 11 bits of the order key of +delta' = k' - m p into
 // h[2048] (the biased quantizer's first radix digit, KB4 pass 0), and delta' == 0 / NaN
@@ -242,8 +255,7 @@ struct RezKHistOp {
     __device__ static RezKHistOp make(const float* l1, float fm, int64_t vec) {
         return RezKHistOp{div_plan(l1[vec]), fm, nullptr, nullptr};
     }
-    __device__ float operator()(float v) const {
-        const float mp = fm * div1(fabsf(v), dp);
+    __device__ float count(float mp) const {
         const float kp = floorf(mp + 0.5f);
         float dp = (kp - mp) + 0.0f;
         uint32_t u = __float_as_uint(dp);
@@ -253,6 +265,14 @@ struct RezKHistOp {
         if (key == 0x80000000u) atomicAdd(&zn[0], 1u);
         else if (key == 0xFFC00000u) atomicAdd(&zn[1], 1u);
         return kp;
+    }
+    __device__ float operator()(float v) const { return count(fm * div1(fabsf(v), dp)); }
+    __device__ void apply4(const float (&v)[4], float (&a)[4]) const {     // as RezKOp::apply4
+        const float ab[4] = {fabsf(v[0]), fabsf(v[1]), fabsf(v[2]), fabsf(v[3])};
+        float qs[4];
+        div4(ab, dp, qs);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] += count(fm * qs[c]);
     }
 };
 
@@ -288,22 +308,21 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
         const int q = tid & 7;
         const int b = tid >> 3;
         const float* p = base + ((int64_t)b * step) * 32 + 4 * q;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
         for (int r = 0; r < step; ++r) {
-            float v0, v1, v2, v3;
+            float v[4];
             if (VEC4) {
                 typedef float k1x4 __attribute__((ext_vector_type(4)));
                 const k1x4 tv = __builtin_nontemporal_load(reinterpret_cast<const k1x4*>(p + (int64_t)r * 32));
-                const float4 t = make_float4(tv.x, tv.y, tv.z, tv.w);
-                v0 = t.x; v1 = t.y; v2 = t.z; v3 = t.w;
+                v[0] = tv.x; v[1] = tv.y; v[2] = tv.z; v[3] = tv.w;
             } else {
                 const float* pr = p + (int64_t)r * 32;
-                v0 = pr[0]; v1 = pr[1]; v2 = pr[2]; v3 = pr[3];
+                v[0] = pr[0]; v[1] = pr[1]; v[2] = pr[2]; v[3] = pr[3];
             }
-            a0 += op(v0); a1 += op(v1); a2 += op(v2); a3 += op(v3);
+            op.apply4(v, a);                  // a[c] += op(v[c]), streams 4q..4q+3 in row order
         }
         float* l = leaf + b * 32 + 4 * q;
-        l[0] = a0; l[1] = a1; l[2] = a2; l[3] = a3;
+        l[0] = a[0]; l[1] = a[1]; l[2] = a[2]; l[3] = a[3];
     }
     __syncthreads();
     if (tid < 32) {
