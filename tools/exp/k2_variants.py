@@ -24,6 +24,14 @@ VARIANTS = {
     # K1a: rows per unrolled group of the leaf loop (product: 4)
     "k1_unroll4": [("        for (int r = 0; r < step; ++r) {", "#pragma unroll 4\n        for (int r = 0; r < step; ++r) {")],
     "k1_unroll8": [("        for (int r = 0; r < step; ++r) {", "#pragma unroll 8\n        for (int r = 0; r < step; ++r) {")],
+    # K3 (client mean from q): non-temporal loads / the next 8 rows loaded before the adds
+    "k3_nt": [('            for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const float4*>(q + (j + u) * ld + col);', '            for (int u = 0; u < 8; ++u) {\n                typedef float m4 __attribute__((ext_vector_type(4)));\n                const m4 v = __builtin_nontemporal_load(reinterpret_cast<const m4*>(q + (j + u) * ld + col));\n                t[u] = make_float4(v.x, v.y, v.z, v.w);\n            }')],
+    "k3_db": [('        int64_t j = 0;\n        for (; j + 8 <= n; j += 8) {\n            float4 t[8];\n#pragma unroll\n            for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const float4*>(q + (j + u) * ld + col);\n#pragma unroll\n            for (int u = 0; u < 8; ++u) {', '        int64_t j = 0;\n        float4 nx[8];\n        if (n >= 8) {\n#pragma unroll\n            for (int u = 0; u < 8; ++u) nx[u] = *reinterpret_cast<const float4*>(q + u * ld + col);\n        }\n        for (; j + 8 <= n; j += 8) {\n            float4 t[8];\n#pragma unroll\n            for (int u = 0; u < 8; ++u) t[u] = nx[u];\n            if (j + 16 <= n) {\n#pragma unroll\n                for (int u = 0; u < 8; ++u) nx[u] = *reinterpret_cast<const float4*>(q + (j + 8 + u) * ld + col);\n            }\n#pragma unroll\n            for (int u = 0; u < 8; ++u) {')],
+    # EDEN norm loaders (KE2, both kernels): non-temporal loads of the rotated vectors
+    "eden_norm_nt": [("uq_eden_kernels.h",
+                      "nx[q] = *reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q));",
+                      "nx[q] = ld_stream(reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q)));",
+                      2)],
     "prio_ld": [(LOOP_LD, "        __builtin_amdgcn_s_setprio(2);\n" + LOOP_LD + "        __builtin_amdgcn_s_setprio(0);\n")],
 }
 
@@ -39,12 +47,21 @@ def build(names):
         for f in os.listdir(os.path.join(PKG, "csrc")):
             shutil.copy(os.path.join(PKG, "csrc", f), d)
         src = os.path.join(d, "uq_dme.hip")
+        header_subs = [v for v in VARIANTS[name] if len(v) == 4]      # (file, old, new, count)
+        for fn, a, b, cnt in header_subs:
+            hp = os.path.join(d, fn)
+            h = open(hp).read()
+            if h.count(a) != cnt:
+                raise SystemExit(f"{name}: {fn} pattern found {h.count(a)} times")
+            open(hp, "w").write(h.replace(a, b))
         s = open(src).read()
-        key = "l1_partial_kernel(" if name.startswith("k1_") else "quantize_stream_kernel(const float* __restrict__ x"
+        key = ("l1_partial_kernel(" if name.startswith("k1_") else
+               "client_mean_kernel(const float* __restrict__ q" if name.startswith("k3_") else
+               "quantize_stream_kernel(const float* __restrict__ x")
         i = s.index(key)                                  # that kernel's body only
         j = s.index("__global__", i)
         body = s[i:j]
-        for a, b in VARIANTS[name]:
+        for a, b in (v for v in VARIANTS[name] if len(v) == 2):
             if body.count(a) != 1:
                 raise SystemExit(f"{name}: pattern found {body.count(a)} times")
             body = body.replace(a, b)

@@ -1732,7 +1732,8 @@ tile_out_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __
 // K3: est[i] (+)= q[j][i] / n_div, j = 0..n-1 in order (ND:137-138).
 // Each thread owns 4 consecutive columns; loads for 8 clients are issued ahead.  1024-thread
 // workgroups (16 KB of a client row each): 0.85-0.88 -> 0.75-0.78 ms at 1024 x 2^20 against
-// 256 (tools/exp/exp_mean.hip, profiles/r03s_exp_mean_variants.jsonl).
+// 256 (tools/exp/exp_mean.hip, profiles/r03s_exp_mean_variants.jsonl); non-temporal loads (q
+// is read once): 0.740-0.754 -> 0.673-0.684 ms (profiles/r05k_exp_mean_q_variants.jsonl).
 // =====================================================================================
 constexpr int kMeanThreads = 1024;
 template <bool VEC4>
@@ -1747,7 +1748,7 @@ client_mean_kernel(const float* __restrict__ q, int64_t n, int64_t d, int64_t ld
         for (; j + 8 <= n; j += 8) {
             float4 t[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const float4*>(q + (j + u) * ld + col);
+            for (int u = 0; u < 8; ++u) t[u] = ld_stream(reinterpret_cast<const float4*>(q + (j + u) * ld + col));
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 e.x += t[u].x / n_div; e.y += t[u].y / n_div;

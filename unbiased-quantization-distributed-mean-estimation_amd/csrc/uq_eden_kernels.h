@@ -435,7 +435,7 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
         if (lvalid && (ch + 1) * kNormChunk <= nv) {     // wave-uniform: a whole chunk, no guards
 #pragma unroll
             for (int q = 0; q < kLQ; ++q)
-                nx[q] = *reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q));
+                nx[q] = ld_stream(reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q)));
             return;
         }
 #pragma unroll
@@ -535,7 +535,7 @@ eden_norm_whole_kernel(const float* __restrict__ v, int64_t n, int64_t D, float*
     auto load = [&](float4 (&nx)[kLQ], int64_t ch) {
         if (!lvalid || ch >= nchunks) return;
 #pragma unroll
-        for (int q = 0; q < kLQ; ++q) nx[q] = *reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q));
+        for (int q = 0; q < kLQ; ++q) nx[q] = ld_stream(reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q)));
     };
     auto store = [&](const float4 (&nx)[kLQ], float* sb) {
         if (chain) return;
