@@ -32,6 +32,11 @@ VARIANTS = {
                       "nx[q] = *reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q));",
                       "nx[q] = ld_stream(reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q)));",
                       2)],
+    # EDEN low pass (KE1 fwht_low4096_kernel): non-temporal loads of its input rows
+    "eden_low_nt": [("uq_eden_kernels.h", "const float4 t = *reinterpret_cast<const float4*>(x + i0 + 4 * q);",
+                     "const float4 t = ld_stream(reinterpret_cast<const float4*>(x + i0 + 4 * q));", 1),
+                    ("uq_eden_kernels.h", "const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);",
+                     "const float4 t = ld_stream(reinterpret_cast<const float4*>(p + 4 * q));", 2)],
     "prio_ld": [(LOOP_LD, "        __builtin_amdgcn_s_setprio(2);\n" + LOOP_LD + "        __builtin_amdgcn_s_setprio(0);\n")],
 }
 
