@@ -37,8 +37,17 @@ VARIANTS = {
                      "const float4 t = ld_stream(reinterpret_cast<const float4*>(x + i0 + 4 * q));", 1),
                     ("uq_eden_kernels.h", "const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);",
                      "const float4 t = ld_stream(reinterpret_cast<const float4*>(p + 4 * q));", 2)],
+    # K1a: the leaf loop loads a batch of rows before it adds them (all loads in flight)
+    "k1_batch8": [('        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        for (int r = 0; r < step; ++r) {\n            float v[4];', '        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        int r = 0;\n        if (VEC4) {\n            typedef float kbx4 __attribute__((ext_vector_type(4)));\n            for (; r + 8 <= step; r += 8) {\n                kbx4 tv[8];\n#pragma unroll\n                for (int u = 0; u < 8; ++u)\n                    tv[u] = __builtin_nontemporal_load(reinterpret_cast<const kbx4*>(p + (int64_t)(r + u) * 32));\n#pragma unroll\n                for (int u = 0; u < 8; ++u) {\n                    const float w[4] = {tv[u].x, tv[u].y, tv[u].z, tv[u].w};\n                    op.apply4(w, a);\n                }\n            }\n        }\n        for (; r < step; ++r) {\n            float v[4];')],
+    "k1_batch16": [('        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        for (int r = 0; r < step; ++r) {\n            float v[4];', '        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        int r = 0;\n        if (VEC4) {\n            typedef float kbx4 __attribute__((ext_vector_type(4)));\n            for (; r + 16 <= step; r += 16) {\n                kbx4 tv[16];\n#pragma unroll\n                for (int u = 0; u < 16; ++u)\n                    tv[u] = __builtin_nontemporal_load(reinterpret_cast<const kbx4*>(p + (int64_t)(r + u) * 32));\n#pragma unroll\n                for (int u = 0; u < 16; ++u) {\n                    const float w[4] = {tv[u].x, tv[u].y, tv[u].z, tv[u].w};\n                    op.apply4(w, a);\n                }\n            }\n        }\n        for (; r < step; ++r) {\n            float v[4];')],
+    "k1_batch32": [('        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        for (int r = 0; r < step; ++r) {\n            float v[4];', '        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        int r = 0;\n        if (VEC4) {\n            typedef float kbx4 __attribute__((ext_vector_type(4)));\n            for (; r + 32 <= step; r += 32) {\n                kbx4 tv[32];\n#pragma unroll\n                for (int u = 0; u < 32; ++u)\n                    tv[u] = __builtin_nontemporal_load(reinterpret_cast<const kbx4*>(p + (int64_t)(r + u) * 32));\n#pragma unroll\n                for (int u = 0; u < 32; ++u) {\n                    const float w[4] = {tv[u].x, tv[u].y, tv[u].z, tv[u].w};\n                    op.apply4(w, a);\n                }\n            }\n        }\n        for (; r < step; ++r) {\n            float v[4];')],
     "prio_ld": [(LOOP_LD, "        __builtin_amdgcn_s_setprio(2);\n" + LOOP_LD + "        __builtin_amdgcn_s_setprio(0);\n")],
 }
+
+# the batched loads for the plain L1 (AbsOp) only: the k' ops keep the row loop
+VARIANTS["k1_batch8_abs"] = [(VARIANTS["k1_batch8"][0][0],
+                              VARIANTS["k1_batch8"][0][1].replace("if (VEC4) {",
+                                                                  "if (VEC4 && std::is_same<Op, AbsOp>::value) {"))]
 
 
 def build(names):
