@@ -41,6 +41,13 @@ VARIANTS = {
     "k1_batch8": [('        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        for (int r = 0; r < step; ++r) {\n            float v[4];', '        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        int r = 0;\n        if (VEC4) {\n            typedef float kbx4 __attribute__((ext_vector_type(4)));\n            for (; r + 8 <= step; r += 8) {\n                kbx4 tv[8];\n#pragma unroll\n                for (int u = 0; u < 8; ++u)\n                    tv[u] = __builtin_nontemporal_load(reinterpret_cast<const kbx4*>(p + (int64_t)(r + u) * 32));\n#pragma unroll\n                for (int u = 0; u < 8; ++u) {\n                    const float w[4] = {tv[u].x, tv[u].y, tv[u].z, tv[u].w};\n                    op.apply4(w, a);\n                }\n            }\n        }\n        for (; r < step; ++r) {\n            float v[4];')],
     "k1_batch16": [('        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        for (int r = 0; r < step; ++r) {\n            float v[4];', '        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        int r = 0;\n        if (VEC4) {\n            typedef float kbx4 __attribute__((ext_vector_type(4)));\n            for (; r + 16 <= step; r += 16) {\n                kbx4 tv[16];\n#pragma unroll\n                for (int u = 0; u < 16; ++u)\n                    tv[u] = __builtin_nontemporal_load(reinterpret_cast<const kbx4*>(p + (int64_t)(r + u) * 32));\n#pragma unroll\n                for (int u = 0; u < 16; ++u) {\n                    const float w[4] = {tv[u].x, tv[u].y, tv[u].z, tv[u].w};\n                    op.apply4(w, a);\n                }\n            }\n        }\n        for (; r < step; ++r) {\n            float v[4];')],
     "k1_batch32": [('        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        for (int r = 0; r < step; ++r) {\n            float v[4];', '        float a[4] = {0.f, 0.f, 0.f, 0.f};\n        int r = 0;\n        if (VEC4) {\n            typedef float kbx4 __attribute__((ext_vector_type(4)));\n            for (; r + 32 <= step; r += 32) {\n                kbx4 tv[32];\n#pragma unroll\n                for (int u = 0; u < 32; ++u)\n                    tv[u] = __builtin_nontemporal_load(reinterpret_cast<const kbx4*>(p + (int64_t)(r + u) * 32));\n#pragma unroll\n                for (int u = 0; u < 32; ++u) {\n                    const float w[4] = {tv[u].x, tv[u].y, tv[u].z, tv[u].w};\n                    op.apply4(w, a);\n                }\n            }\n        }\n        for (; r < step; ++r) {\n            float v[4];')],
+    # UQR1 code histogram (KC1): non-temporal loads of the codes
+    "codec_hist_nt": [("uq_codec_kernels.h",
+                       "const uint4 w0 = *reinterpret_cast<const uint4*>(row + i);\n            const uint4 w1 = *reinterpret_cast<const uint4*>(row + i + 256 * 16);",
+                       "const uint4 w0 = ld_stream_u4(reinterpret_cast<const uint4*>(row + i));\n            const uint4 w1 = ld_stream_u4(reinterpret_cast<const uint4*>(row + i + 256 * 16));",
+                       1),
+                      ("uq_codec_kernels.h", "// Type-message codec",
+                       "__device__ __forceinline__ uint4 ld_stream_u4(const uint4* p) {\n    typedef uint32_t u4v __attribute__((ext_vector_type(4)));\n    const u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(p));\n    return make_uint4(v.x, v.y, v.z, v.w);\n}\n// Type-message codec", 1)],
     "prio_ld": [(LOOP_LD, "        __builtin_amdgcn_s_setprio(2);\n" + LOOP_LD + "        __builtin_amdgcn_s_setprio(0);\n")],
 }
 
