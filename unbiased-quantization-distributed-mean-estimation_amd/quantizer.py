@@ -277,14 +277,17 @@ def Type_unbiased_quantize(input_vector, bits_per_dimension=1):
     """Drop-in for NMSE_Results/Codes/All_Schemes.py:609 (same name: the Flower client
     derives directory names from `__name__`, FLM:177).
 
-    AS:611  always copies `input_vector` to a new f32 tensor on the device
+    AS:611  takes `input_vector` as f32 on the device (the input is only read; the result
+            is always a new tensor, as the reference's copy guarantees)
     AS:622  unknown `bits_per_dimension` -> KeyError (checked before any work)
     AS:634  consumes exactly one draw of torch's global CPU generator
     Returns a new f32 tensor of shape (d,) on the GPU."""
     dev = _device()
     l_rate = RATE_TABLE[bits_per_dimension]          # KeyError like the reference
     if torch.is_tensor(input_vector):
-        v = input_vector.detach().to(device=dev, dtype=torch.float32).clone()
+        # no device-side copy (AS:611 copies so as not to alias the input; here the kernels
+        # only read v and write a new output, and d == 0 returns a clone below)
+        v = input_vector.detach().to(device=dev, dtype=torch.float32)
     else:
         v = torch.tensor(np.asarray(input_vector), dtype=torch.float32, device=dev)
     if v.dim() != 1:
@@ -294,5 +297,5 @@ def Type_unbiased_quantize(input_vector, bits_per_dimension=1):
     m = int(l_rate * d)
     X = torch.rand(1)                                   # AS:634 (global CPU generator)
     if d == 0:
-        return v
+        return v.clone()
     return quantize_dequantize(v.view(1, d), X=X, m=m).view(d)
