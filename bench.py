@@ -136,7 +136,6 @@ def main():
     args = parse()
     dist, rank, world, local = dist_init(args)
     import uqdme
-    from uqdme_amd import _lib
 
     dev = torch.device("cuda", torch.cuda.current_device())
     n, d = args.clients, args.dim
@@ -158,106 +157,68 @@ def main():
         x = torch.rand(n, d, generator=g, device=dev, dtype=torch.float32) * 2.0 - 1.0
     X_cpu = torch.rand(n_total, generator=torch.Generator().manual_seed(args.seed))[rank * n:(rank + 1) * n]
     X = X_cpu.to(dev)
-    # resident buffers of the batched pipeline; the output placement is probed once (see
-    # pipeline.py: K2's speed follows where q and the codes land in physical memory)
-    pipe = uqdme.DMEPipeline(n, d, m=m, torch_threads=T)
-    probe = pipe.probe_outputs(x, X, candidates=args.probe_candidates, min_candidates=args.probe_min) if args.probe_candidates > 1 else None
-    q, codes, ovf, l1, est, ws, nb = pipe.q, pipe.codes, pipe.kmax, pipe.l1, pipe.est, pipe.ws, pipe.ws_bytes
-    lib = _lib.load()
+    # the library's multi-GPU product API (distributed.ShardedDME): a resident DMEPipeline
+    # (K1 -> K2 -> K3c) per rank, then ONE RCCL reduce of est to rank 0 (N > 1; with RCCL the
+    # reduce of step k runs beside step k+1's kernels, see ShardedDME).  The output placement
+    # is probed once (pipeline.py: K2's speed follows where q and the codes land).
+    sh = uqdme.ShardedDME(n, d, n_total, m=m, torch_threads=T, pipeline="codes", mode=args.mean_mode)
+    pipe = sh.pipe
+    probe = sh.probe_outputs(x, X, candidates=args.probe_candidates, min_candidates=args.probe_min) \
+        if args.probe_candidates > 1 else None
+    q, ovf = pipe.q, pipe.kmax
     stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
-    P = lambda t: t.data_ptr()  # noqa: E731
-
-    # N > 1 over RCCL: the reduce of step k runs beside step k+1's kernels.  Two estimate
-    # buffers; step k+2 waits for reduce k before it overwrites that buffer (work.wait()
-    # orders the caller's stream after the collective, the host does not block).
-    overlap = dist is not None and BACKEND == "nccl" and args.mean_mode == "reduce"
-    est_bufs = [est, torch.empty_like(est)] if overlap else [est]
-    pending = [None] * len(est_bufs)
-    nstep = [0]
-
-    def drain():
-        for i, w in enumerate(pending):
-            if w is not None:
-                w.wait()
-                pending[i] = None
-
-    def step(ev=None, pipeline=args.pipeline):
-        slot = nstep[0] % len(est_bufs)
-        nstep[0] += 1
-        est_s = est_bufs[slot]
-        if pending[slot] is not None:
-            pending[slot].wait()
-            pending[slot] = None
-        if ev is not None:
-            ev[0].record(stream)
-        _lib.check(lib.uq_l1_torch_order_f32(P(x), n, d, T, P(l1), P(ws), nb, sp), "l1")
-        if ev is not None:
-            ev[1].record(stream)
-        if pipeline == "q":
-            _lib.check(lib.uq_type_unbiased_f32(P(x), P(q), n, d, m, P(X), P(l1), None, T, P(ws), nb, sp), "quantize")
-        else:
-            _lib.check(lib.uq_type_unbiased_codes_f32(P(x), P(q) if pipeline == "codes" else None, P(codes), P(ovf),
-                                                      n, d, m, P(X), P(l1), None, T, P(ws), nb, sp), "quantize")
-        if ev is not None:
-            ev[2].record(stream)
-        if dist is None or args.mean_mode == "reduce":
-            if pipeline == "q":
-                _lib.check(lib.uq_client_mean_f32(P(q), n, d, d, float(n_total), 0, P(est_s), sp), "mean")
-            else:
-                _lib.check(lib.uq_codes_mean_f32(P(codes), P(l1), P(ovf), n, d, m, float(n_total), 0, P(est_s), sp),
-                           "mean")
-        if ev is not None:
-            ev[3].record(stream)
-        if dist is not None:
-            if args.mean_mode == "reduce":
-                if BACKEND == "nccl":                                  # the one RCCL collective
-                    pending[slot] = dist.reduce(est_s, dst=0, op=dist.ReduceOp.SUM, async_op=True)
-                else:
-                    est_h = est.cpu()
-                    dist.reduce(est_h, dst=0, op=dist.ReduceOp.SUM)
-                    est.copy_(est_h)
-            else:
-                if pipeline != "q":
-                    _lib.check(lib.uq_codes_decode_f32(P(codes), P(l1), n, d, m, P(q), sp), "decode")
-                uqdme.sharded_client_mean(q, float(n_total), mode="ordered", dst=0)
-        if ev is not None:
-            ev[4].record(stream)
+    overlap = sh.overlap
 
     def time_pipeline(pipeline, steps):
         for _ in range(2):
-            step(pipeline=pipeline)
+            sh.step(x, X, pipeline=pipeline)
+        sh.drain()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(steps):
-            step(pipeline=pipeline)
+            sh.step(x, X, pipeline=pipeline)
+        sh.drain()
         e1.record(stream)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / steps
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
     for _ in range(args.warmup):                  # W untimed warmup steps
-        step()
-    drain()
+        sh.step(x, X, pipeline=args.pipeline)
+    sh.drain()
     torch.cuda.synchronize()
-    _lib.check(lib.uq_check_status(P(ws), sp), "status after warmup")
+    pipe.check_status()                           # status after warmup
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
-    drain()                                       # every reduce inside the timed region
+        sh.step(x, X, events=evs[k], pipeline=args.pipeline)
+    sh.drain()                                    # every reduce inside the timed region
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    _lib.check(lib.uq_check_status(P(ws), sp), "status after timed steps")
+    pipe.check_status()                           # status after the timed steps
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if BACKEND == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    reduce_alone = None
+    if dist is not None and args.mean_mode == "reduce" and BACKEND == "nccl":
+        # the collective by itself (the timed steps overlap it, so their 'reduce' segment
+        # only covers its enqueue): events around reduce + wait on the caller's stream
+        ra = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            w = dist.reduce(pipe.est, dst=0, op=dist.ReduceOp.SUM, async_op=True)
+            w.wait()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ra.append(e0.elapsed_time(e1))
+        reduce_alone = round(float(np.median(ra)), 4)
 
     seg = np.array([[evs[k][i].elapsed_time(evs[k][i + 1]) for i in range(4)] for k in range(args.steps)])
     seg_ms = seg.mean(axis=0)  # l1, quantize, mean, reduce
@@ -284,7 +245,7 @@ def main():
                 ms = time_pipeline(pl, max(3, args.steps // 2))
                 side[pl] = {"ms_per_step": round(ms, 4), "value": round(n_total / ms / 1e3, 6),
                             "what": PIPELINE_WHAT[pl]}
-        _lib.check(lib.uq_check_status(P(ws), sp), "status after side pipelines")
+        pipe.check_status()                       # status after the side pipelines
         side["biased"] = time_biased(uqdme, x, args.bits, T, max(3, args.steps // 2))
         side["eden"] = time_eden(uqdme, x, q, max(3, args.steps // 2))
         side["codec"] = time_codec(uqdme, pipe, max(3, args.steps // 2))
@@ -312,7 +273,14 @@ def main():
                                     if world > 1 else "single",
                        **({"backend": BACKEND} if world > 1 and BACKEND != "nccl" else {}), "pipeline": args.pipeline},
             "kernel_ms": {"l1": round(float(seg_ms[0]), 4), "quantize": round(q_ms, 4),
-                          "client_mean": round(float(seg_ms[2]), 4), "reduce": round(float(seg_ms[3]), 4)},
+                          # the probe's median K2 time over all candidate output sets: what a
+                          # caller that allocates fresh outputs (no probe) gets on average
+                          "quantize_median_unprobed": probe["k2_ms_median_unprobed"] if probe else None,
+                          "client_mean": round(float(seg_ms[2]), 4),
+                          # overlapped RCCL reduce: the segment times its enqueue only;
+                          # reduce_alone = the collective timed by itself after the steps
+                          ("reduce_enqueue" if overlap else "reduce"): round(float(seg_ms[3]), 4),
+                          "reduce_alone": reduce_alone},
             "pipelines": side,
             "output_placement_probe": probe,
             "roofline": {"kernel": "quantize_stream_kernel (K2)", "bound": "hbm", "achieved": round(achieved, 2),

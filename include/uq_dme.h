@@ -66,6 +66,13 @@ int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64
                          const float* X, const float* l1, float* l1_out,
                          int32_t torch_threads, void* ws, size_t ws_bytes, void* stream);
 
+/* AS:609-641 for ONE vector per call, the form the reference's callers use (Normal_dist.py:137,
+ * Type_unbiased.py:160): out = Type_unbiased_quantize(x, ·) with the AS:634 draw X passed by
+ * value (no device copy of it), L1 computed here (torch order).  Same bits as
+ * uq_type_unbiased_f32 with n = 1. */
+int uq_type_unbiased_vec_f32(const float* x, float* out, int64_t d, int64_t m, float X, int32_t torch_threads,
+                             void* ws, size_t ws_bytes, void* stream);
+
 /* Normal_dist.py:137-138 — est[i] (+)= q[j][i] / n_div for j = 0..n-1 in client order
  * (f32 IEEE division, f32 add).  Row j starts at q + j*ld (ld >= d, so a column block
  * of a wider batch can be folded in).  accumulate=0 starts from zeros; accumulate=1
@@ -105,6 +112,15 @@ int uq_codes_decode_f32(const int8_t* codes, const float* l1, int64_t n, int64_t
  * kmax [n] as produced by the encoder (sizes the per-client decode tables). */
 int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax, int64_t n, int64_t d,
                       int64_t m, float n_div, int32_t accumulate, float* est, void* stream);
+
+/* As uq_codes_mean_f32, with the dequantized batch q (row j at q + j*ldq, ldq >= d) beside
+ * the codes: a client whose counts overflowed its codes (kmax[j] > 127, saturated) adds
+ * q[j][i] / n_div instead, so est is always bit-identical to uq_client_mean_f32(q).
+ * q == NULL is uq_codes_mean_f32 (overflowed clients then add their saturated codes).
+ * Clients without overflow read only their codes. */
+int uq_codes_q_mean_f32(const int8_t* codes, const float* q, int64_t ldq, const float* l1, const int32_t* kmax,
+                        int64_t n, int64_t d, int64_t m, float n_div, int32_t accumulate, float* est,
+                        void* stream);
 
 /* ---- type messages "UQR1": entropy-coded type codes ---------------
  * The reference has no wire format (parity unpinned); its client output is AS:640's

@@ -180,3 +180,10 @@ void uqo_client_mean(const float* q, int64_t n, int64_t d, float n_div, float* e
     for (int64_t j = 0; j < n; ++j)
         for (int64_t i = 0; i < d; ++i) est[i] += q[j * d + i] / n_div;
 }
+
+/* The same sum continued from est (clients fed in order over several calls: one call over
+ * all of them gives the same bits). */
+void uqo_client_mean_acc(const float* q, int64_t n, int64_t d, float n_div, float* est) {
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i < d; ++i) est[i] += q[j * d + i] / n_div;
+}

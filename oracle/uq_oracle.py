@@ -225,9 +225,13 @@ def client_mean(q_rows, n_div) -> np.ndarray:
 
 def script_nmse(est: np.ndarray, emp_mean: np.ndarray, vec_norm_squared: float,
                 num_users: int, num_trials: int = 50) -> float:
-    """ND:151-157: ||est - emp||^2 (f32 torch.norm) / (num_trials * sum||x||^2 * n)."""
+    """ND:151-157: torch.norm(est - emp).pow(2) / (num_trials * sum||x||^2 * n), all in f32
+    as torch CPU evaluates it: the norm in torch's order (8 interleaved lanes of fma
+    accumulation, lanes added in order, tail, f32 sqrt; oracle/uq_eden.py:torch_norm2),
+    pow(2) as one f32 multiply, the Python-float denominator rounded to f32."""
+    from .uq_eden import torch_norm2
     diff = (np.asarray(est, f32) - np.asarray(emp_mean, f32)).astype(f32)
-    nrm = f32(np.sqrt(np.sum(diff.astype(f64) ** 2)))
+    nrm = torch_norm2(diff)
     return float(f32(nrm * nrm) / f32(num_trials * vec_norm_squared * num_users))
 
 

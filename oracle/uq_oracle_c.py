@@ -35,6 +35,8 @@ def lib():
         L.uqo_quantize_batch_mt.argtypes = [p, p, i64, i64, i64, p, ctypes.c_int, p, ctypes.c_int]
         L.uqo_client_mean.restype = None
         L.uqo_client_mean.argtypes = [p, i64, i64, f, p]
+        L.uqo_client_mean_acc.restype = None
+        L.uqo_client_mean_acc.argtypes = [p, i64, i64, f, p]
         L.uqo_torch_sum.restype = f
         L.uqo_torch_sum.argtypes = [p, i64, ctypes.c_int]
         L.uqc_bound.restype = ctypes.c_uint64
@@ -94,6 +96,15 @@ def client_mean(q2d, n_div):
     n, d = q2d.shape
     est = np.empty(d, np.float32)
     lib().uqo_client_mean(_ptr(q2d), n, d, np.float32(n_div), _ptr(est))
+    return est
+
+
+def client_mean_acc(q2d, n_div, est):
+    """est += q2d[j] / n_div for rows in order, in place (continues a client-ordered mean)."""
+    q2d = np.ascontiguousarray(q2d, dtype=np.float32)
+    n, d = q2d.shape
+    assert est.dtype == np.float32 and est.flags.c_contiguous and est.shape == (d,)
+    lib().uqo_client_mean_acc(_ptr(q2d), n, d, np.float32(n_div), _ptr(est))
     return est
 
 

@@ -125,3 +125,20 @@ def test_codec_sizes_host_only(lib):
     assert w2.value > w1.value >= 4 * 2 * (1 << 20)         # the word scratch: 2 B per symbol
     assert lib.uq_tc_bound(-1, ctypes.byref(w1)) != 0
     assert lib.uq_tc_encode(None, None, 1, 10, 5, 2, None, 0, None, None, 0, None) != 0   # unknown flag
+
+
+def test_round3_entry_points_argument_errors(lib):
+    """uq_codes_q_mean_f32 / uq_type_unbiased_vec_f32: host-side checks (no kernel launched)."""
+    from uqdme_amd import _lib as L
+    for name in ("uq_codes_q_mean_f32", "uq_type_unbiased_vec_f32"):
+        res, args = L.SIGNATURES[name]
+        getattr(lib, name).restype = res
+        getattr(lib, name).argtypes = args
+    p = ctypes.c_void_p(16)
+    assert lib.uq_codes_q_mean_f32(p, p, 9, p, p, 4, 10, 5, 4.0, 0, p, None) == -1        # ldq < d
+    assert b"ldq" in lib.uq_last_error()
+    assert lib.uq_codes_q_mean_f32(None, None, 10, None, None, 4, 10, 5, 4.0, 0, p, None) == -1
+    assert lib.uq_codes_q_mean_f32(None, None, 10, None, None, 4, 0, 5, 4.0, 0, None, None) == 0   # d = 0
+    assert lib.uq_type_unbiased_vec_f32(None, None, 0, 0, 0.5, 1, None, 0, None) == 0      # d = 0: no-op
+    assert lib.uq_type_unbiased_vec_f32(p, None, 10, 2, 0.5, 1, p, 1 << 20, None) == -1    # null out
+    assert lib.uq_type_unbiased_vec_f32(p, p, 10, -2, 0.5, 1, p, 1 << 20, None) == -1      # m < 0

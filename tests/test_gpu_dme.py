@@ -27,7 +27,7 @@ def test_nd_harness_known_answers(uq):
                 for r in (1, 2):
                     got = float(res[r]["script"][ui, inst])
                     ref = row[f"nmse{r}"]
-                    assert abs(got - ref) <= 1e-6 * ref, (dist, n, inst, r, got, ref)   # north_star tolerance
+                    assert got == ref, (dist, n, inst, r, got, ref)   # bit for bit (north_star: 1e-6 rel)
                 k += 1
 
 
@@ -46,7 +46,7 @@ def test_other_distributions_vs_oracle(uq, dist):
 
 def test_sharded_mean_single_rank_nccl(uq):
     """The RCCL path of distributed.py with one rank: ordered and reduce modes equal the
-    single-call client mean bit-for-bit."""
+    single-call client mean bit-for-bit; ShardedDME's overlapped RCCL reduce likewise."""
     import os
     import socket
     import torch.distributed as dist
@@ -63,6 +63,28 @@ def test_sharded_mean_single_rank_nccl(uq):
             est = uq.sharded_client_mean(q, 33.0, mode=mode, block=1024)
             torch.cuda.synchronize()
             assert torch.equal(est, ref), mode
+        # ShardedDME (the bench's path) over RCCL with the async reduce overlapped with the
+        # next step: two estimate buffers alternate; every step's est equals the single-call
+        # mean of its own q once drained
+        n, d = 40, 8192
+        sh = uq.ShardedDME(n, d, n, 1, torch_threads=1, overlap=True)
+        assert sh.overlap and len(sh.est_bufs) == 2
+        X = torch.rand(n, generator=torch.Generator().manual_seed(9)).cuda()
+        outs = []
+        for k in range(3):
+            x = torch.randn(n, d, generator=torch.Generator(device="cuda").manual_seed(k), device="cuda")
+            est = sh.step(x, X)
+            q_ref = uq.quantize_dequantize(x, 1, X=X, torch_threads=1)
+            outs.append((est, uq.client_mean(q_ref, float(n))))
+            if k == 1:
+                sh.drain()
+                torch.cuda.synchronize()
+                assert torch.equal(outs[1][0], outs[1][1])
+        sh.drain()
+        torch.cuda.synchronize()
+        sh.check_status()
+        assert outs[2][0].data_ptr() == outs[0][0].data_ptr()
+        assert torch.equal(outs[2][0], outs[2][1])
     finally:
         dist.destroy_process_group()
 

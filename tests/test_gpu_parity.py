@@ -37,8 +37,9 @@ def test_c1_harness_bit_exact(uq):
     assert G.bits_equal(e2, z["est2"])
     n1 = O.script_nmse(e1, z["emp"], float(z["vec_norm_squared"]), 16)
     n2 = O.script_nmse(e2, z["emp"], float(z["vec_norm_squared"]), 16)
-    assert abs(n1 - float(z["nmse1"])) <= 1e-6 * float(z["nmse1"])   # north_star tolerance
-    assert abs(n2 - float(z["nmse2"])) <= 1e-6 * float(z["nmse2"])
+    # bit for bit (north_star allows 1e-6 relative): est is bit-exact and the oracle's
+    # script_nmse restates torch.norm's f32 order
+    assert n1 == float(z["nmse1"]) and n2 == float(z["nmse2"]), (n1, n2)
     ref_l1 = [O.l1_torch_order(z["x"][j], 1) for j in range(16)]
     assert G.bits_equal(l1.cpu().numpy(), np.array(ref_l1, f32))
 
@@ -110,6 +111,16 @@ def test_random_batches_vs_oracle(uq):
                 bad = G.n_mismatch(got, ref)
                 assert bad == 0, (d, gi, R, bad)
                 total += 1
+    # config C3's two distributions at its d = 2^20 (Laplace(1, 2), U(-1, 1))
+    for gi in (1, 5):
+        x = gens[gi]((5, 1 << 20)).astype(f32)
+        for R in (1, 2):
+            X = rng.random(5).astype(f32)
+            m = O.rate_to_m(R, 1 << 20)
+            got = uq.quantize_dequantize(dev(x), m=m, X=X, torch_threads=1).cpu().numpy()
+            ref, _ = C.quantize_batch(x, m, X, 1)
+            assert G.n_mismatch(got, ref) == 0, (gi, R)
+            total += 1
     assert total > 300
 
 

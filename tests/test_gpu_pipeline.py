@@ -30,3 +30,56 @@ def test_pipeline_step_matches_batched_apis(gpu_ready, n, d, bits):
         assert torch.equal(dec.view(torch.int32), q_ref.view(torch.int32)), probe
     with pytest.raises(ValueError):
         p.step(x[:, :-1].contiguous(), X)
+
+
+def test_pipelines_agree_and_overflowed_client_falls_back_to_q(gpu_ready):
+    """a client whose lattice counts overflow its int8 codes (one nonzero
+    coordinate: k = m there) -- the "codes" pipeline reads that client from q, so est is
+    still the client-ordered mean of q bit for bit (ND:137-138); "q" gives the same bits;
+    "encode" (no q to fall back to) raises from check_status."""
+    import uqdme
+    n, d, bits = 70, 8192, 1                       # 2 full 32-client groups + 6 in the tail
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(n, d, generator=g, device="cuda")
+    for j in (3, 40, 67):                          # one client in each group and in the tail
+        x[j].zero_()
+        x[j, 100 + j] = -2.5
+    X = torch.rand(n, generator=torch.Generator().manual_seed(4)).cuda()
+    q_ref = uqdme.quantize_dequantize(x, bits, X=X, torch_threads=1)
+    est_ref = uqdme.client_mean(q_ref, float(n))
+    for pl in ("codes", "q"):
+        p = uqdme.DMEPipeline(n, d, bits, torch_threads=1, pipeline=pl)
+        est = p.step(x, X)
+        p.check_status()
+        assert torch.equal(p.q.view(torch.int32), q_ref.view(torch.int32)), pl
+        assert torch.equal(est.view(torch.int32), est_ref.view(torch.int32)), pl
+        if pl == "codes":
+            assert p.overflowed() == 3
+            assert int(p.kmax[3]) == 128 and int(p.kmax[0]) <= 127
+    p = uqdme.DMEPipeline(n, d, bits, torch_threads=1, pipeline="encode")
+    p.step(x, X)
+    with pytest.raises(OverflowError):
+        p.check_status()
+    # accumulate continues the sum bit-for-bit from a previous est
+    p = uqdme.DMEPipeline(n, d, bits, torch_threads=1)
+    e1 = p.step(x, X, n_div=float(2 * n)).clone()
+    e2 = p.step(x, X, n_div=float(2 * n), accumulate=True, est=e1)
+    ref2 = uqdme.client_mean(torch.cat([q_ref, q_ref]), float(2 * n))
+    assert torch.equal(e2.view(torch.int32), ref2.view(torch.int32))
+
+
+@pytest.mark.parametrize("d", [1, 5, 4096, 172554, 1 << 20])
+def test_vector_entry_x_by_value_matches_batched(gpu_ready, d):
+    """uq_type_unbiased_vec_f32 (the per-call drop-in: X by value, no fill) gives the bits of
+    the batched entry with n = 1, over repeated calls on one workspace (the record counters
+    the tile-sum kernels now reset themselves)."""
+    import uqdme
+    gen = torch.Generator().manual_seed(d)
+    for rep in range(3):
+        v = torch.randn(d, generator=gen).cuda()
+        torch.manual_seed(100 + rep)
+        got = uqdme.Type_unbiased_quantize(v, 1)
+        torch.manual_seed(100 + rep)
+        X = torch.rand(1)
+        ref = uqdme.quantize_dequantize(v.view(1, d), X=X, m=uqdme.rate_to_m(1, d)).view(d)
+        assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), (d, rep)

@@ -25,9 +25,8 @@ def test_c1_harness_outputs_and_nmse():
     assert G.bits_equal(e2, z["est2"])
     n1 = O.script_nmse(e1, z["emp"], float(z["vec_norm_squared"]), 16)
     n2 = O.script_nmse(e2, z["emp"], float(z["vec_norm_squared"]), 16)
-    # north_star tolerance: NMSE within 1e-6 relative of the reference
-    assert abs(n1 - float(z["nmse1"])) <= 1e-6 * float(z["nmse1"])
-    assert abs(n2 - float(z["nmse2"])) <= 1e-6 * float(z["nmse2"])
+    # bit for bit: script_nmse restates torch.norm's f32 order (north_star allows 1e-6 relative)
+    assert n1 == float(z["nmse1"]) and n2 == float(z["nmse2"]), (n1, n2)
     # survey known answers
     assert float(z["nmse1"]) == 1.0085821486427449e-05
     assert float(z["nmse2"]) == 1.197929691443278e-06
@@ -103,7 +102,7 @@ def test_nd_harness_points():
                     norms.append(np.linalg.norm(v) ** 2)
                     vecs.append(v.astype(f32))
                 vns = sum(norms)
-                emp = (np.sum(np.stack(vecs).astype(f32), axis=0, dtype=f32) / f32(n)).astype(f32)
+                emp = (torch.stack([torch.from_numpy(v) for v in vecs]).sum(dim=0) / n).numpy()   # ND:95
                 q1, q2 = [], []
                 for v in vecs:
                     X1 = torch.rand(1, generator=gen).item()
@@ -114,10 +113,9 @@ def test_nd_harness_points():
                 n2 = O.script_nmse(O.client_mean(q2, n), emp, vns, n)
                 row = rows[k]
                 assert row["n"] == n and row["inst"] == inst
-                # emp uses a different f32 summation order than torch.stack().sum(0) for n>2,
-                # so compare at the north_star NMSE tolerance
-                assert abs(n1 - row["nmse1"]) <= 1e-6 * row["nmse1"], (dist, n, inst, n1, row)
-                assert abs(n2 - row["nmse2"]) <= 1e-6 * row["nmse2"], (dist, n, inst, n2, row)
+                # bit for bit (emp by the reference's own torch op; the norm in torch's order)
+                assert n1 == row["nmse1"], (dist, n, inst, n1, row)
+                assert n2 == row["nmse2"], (dist, n, inst, n2, row)
                 k += 1
 
 

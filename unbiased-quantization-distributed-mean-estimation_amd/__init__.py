@@ -18,7 +18,7 @@ from .eden import (EDEN_quantize_Hadamard, eden_quantize, eden_compress, eden_de
                    randomized_hadamard_transform, randomized_inverse_hadamard_transform)
 from .quicfl import QuicFLReceiver, quicfl_decompress
 from ._lib import UQError, load as load_library, library_path
-from .distributed import shard_range, sharded_client_mean, sharded_quantize_mean
+from .distributed import ShardedDME, shard_range, sharded_client_mean, sharded_quantize_mean
 from .dme import DISTRIBUTIONS, nmse_simulation
 from .pipeline import DMEPipeline
 from .fl_stats import compute_nmse_stats_auto, data_format, round_nmse
@@ -32,5 +32,5 @@ __all__ = [
     "TypeCodes", "Type_biased_quantize", "biased_quantize", "EDEN_quantize_Hadamard", "eden_quantize",
     "eden_compress", "eden_decompress", "EdenMessage", "rht_signs", "randomized_hadamard_transform",
     "randomized_inverse_hadamard_transform", "compute_nmse_stats_auto", "data_format", "round_nmse",
-    "DMEPipeline", "TypeMessages", "encode_messages", "decode_messages",
+    "DMEPipeline", "ShardedDME", "TypeMessages", "encode_messages", "decode_messages",
 ]

@@ -25,6 +25,7 @@ SIGNATURES = {
     "uq_workspace_bytes": (ctypes.c_int, [_i64, _i64, _i32, ctypes.POINTER(_sz)]),
     "uq_l1_torch_order_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _sz, _p]),
     "uq_type_unbiased_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _i32, _p, _sz, _p]),
+    "uq_type_unbiased_vec_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _f32, _i32, _p, _sz, _p]),
     "uq_client_mean_f32": (ctypes.c_int, [_p, _i64, _i64, _i64, _f32, _i32, _p, _p]),
     "uq_type_unbiased_mean_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _p, _p, _i32, _f32, _i32, _p,
                                                  _p, _sz, _p]),
@@ -32,6 +33,7 @@ SIGNATURES = {
     "uq_type_unbiased_codes_f32": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _i32, _p, _sz, _p]),
     "uq_codes_decode_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _p, _p]),
     "uq_codes_mean_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _f32, _i32, _p, _p]),
+    "uq_codes_q_mean_f32": (ctypes.c_int, [_p, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _i32, _p, _p]),
     "uq_biased_workspace_bytes": (ctypes.c_int, [_i64, _i64, _i32, ctypes.POINTER(_sz)]),
     "uq_type_biased_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _sz, _p]),
     "uq_rht_signs": (ctypes.c_int, [_p, _i64, _i64, _p, _p]),

@@ -1273,8 +1273,8 @@ template <bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock, 4)
 quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                        int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
-                       const float* __restrict__ Xs, const float* __restrict__ l1, int32_t seg_tiles, int32_t nseg,
-                       const uint64_t* __restrict__ pre) {
+                       const float* __restrict__ Xs, float Xval, const float* __restrict__ l1, int32_t seg_tiles,
+                       int32_t nseg, const uint64_t* __restrict__ pre) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image of tile t (then scratch)
     __shared__ __attribute__((aligned(16))) float s_o[kQTile];     // output image of tile t-1 / t
     __shared__ float s_tab[kTab];
@@ -1285,7 +1285,7 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     const int32_t te = min(tiles, tb + seg_tiles);
     const float L = l1[vec];
     const DivPlan dp = div_plan(L);
-    const float Xv = Xs[vec];
+    const float Xv = Xs ? Xs[vec] : Xval;            // one vector per call: X passed by value
     const uint32_t row_bytes = (uint32_t)(d * 4);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, row_bytes);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(WQ ? out + vec * d : x, row_bytes);
@@ -1331,6 +1331,10 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
 }
 
 // ---- small-batch forms (fewer clients than fill the GPU one workgroup per client) ----
+// (irregular-tile records, see TileRec below)
+constexpr int kRecEvents = 48;          // events per record
+constexpr int kRecPerClient = 32;       // records per client
+constexpr int kRecClients = 256;        // clients per launch chunk with records
 //   approximate tile sums A_t (agg_stream_kernel over segments, or tile_agg_kernel)
 //   tile_map_kernel      per tile: P'_t = the sums before it (approximate prefix), then in
 //                        the binade of P'_t the exact map (m0, m1), or an irregular tile's
@@ -1343,13 +1347,14 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
 // Approximate tile sums over a segment, streamed with the stream kernel's prefetch.
 __global__ void __launch_bounds__(kQBlock, 4)
 agg_stream_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
-                  int32_t seg_tiles, int32_t nseg, uint64_t* __restrict__ agg) {
+                  int32_t seg_tiles, int32_t nseg, uint64_t* __restrict__ agg, uint32_t* __restrict__ reccnt) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
     __shared__ ScanLds sl;
     const int tid = threadIdx.x;
     const int64_t vec = blockIdx.x / (uint32_t)nseg;
     const int32_t tb = (int32_t)(blockIdx.x % (uint32_t)nseg) * seg_tiles;
     const int32_t te = min(tiles, tb + seg_tiles);
+    if (tb == 0 && tid == 0 && vec < kRecClients) reccnt[vec] = 0u;   // tile_map_kernel's record counter
     const DivPlan dp = div_plan(l1[vec]);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, (uint32_t)(d * 4));
     const Binade B = binade_of(0.0);
@@ -1375,12 +1380,13 @@ agg_stream_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
 template <bool VEC4>
 __global__ void __launch_bounds__(kQBlock)
 tile_agg_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
-                uint64_t* __restrict__ agg) {
+                uint64_t* __restrict__ agg, uint32_t* __restrict__ reccnt) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
     __shared__ ScanLds sl;
     const int tid = threadIdx.x;
     const int32_t tile = blockIdx.x;
     const int64_t vec = blockIdx.y;
+    if (tile == 0 && tid == 0 && vec < kRecClients) reccnt[vec] = 0u;   // tile_map_kernel's record counter
     TileRegs r;
     load_tile<VEC4>(r, x, d, tiles, (uint32_t)(vec * tiles + tile), tid);
     stage_tile<VEC4>(r, s_x, tid);
@@ -1404,9 +1410,6 @@ tile_agg_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
 // run sum after the last event.  The fold walks a record in LDS instead of loading and
 // resolving the tile.  Tiles with more events, or beyond a client's record budget, or of
 // clients past kRecClients, are resolved from the data as before.
-constexpr int kRecEvents = 48;          // events per record
-constexpr int kRecPerClient = 32;       // records per client
-constexpr int kRecClients = 256;        // clients per launch chunk with records
 struct EvEntry {
     double run;                         // run sum between the previous event and this one
     double t0, t1;                      // clean tie
@@ -1514,6 +1517,7 @@ tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
 }
 
 constexpr int kFoldEvents = 256;   // record events prefetched into LDS (24 KB)
+constexpr int kFoldMaps = 1024;    // tile maps prefetched into LDS (16 KB): d <= 2^22 in one go
 
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
     const uint32_t lo = __shfl_up((uint32_t)v, o, kWave), hi = __shfl_up((uint32_t)(v >> 32), o, kWave);
@@ -1540,10 +1544,22 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
     __shared__ EvEntry s_ev[kFoldEvents];                  // the client's records, prefetched
     __shared__ uint32_t s_roff[kRecPerClient], s_rcnt[kRecPerClient];
     __shared__ double s_rlast[kRecPerClient];
+    __shared__ uint64_t s_m0[kFoldMaps], s_m1[kFoldMaps];
     const int tid = threadIdx.x;
     const int64_t vec = blockIdx.x;
     const int64_t base = vec * tiles;
     const DivPlan dp = div_plan(l1[vec]);
+    // every map in LDS when they fit: a run restarted after an irregular tile then reads its
+    // next 64 maps from LDS instead of waiting a global round trip (the fold at n = 1 is the
+    // serial floor of the per-call drop-in)
+    const bool mcache = tiles <= kFoldMaps;
+    if (mcache)
+        for (int i = tid; i < tiles; i += kQBlock) {
+            s_m0[i] = map0[base + i];
+            s_m1[i] = map1[base + i];
+        }
+    auto M0 = [&](int32_t t) -> uint64_t { return mcache ? s_m0[t] : map0[base + t]; };
+    auto M1 = [&](int32_t t) -> uint64_t { return mcache ? s_m1[t] : map1[base + t]; };
     // prefetch every record of this client that fits (two dependent round trips in all)
     const int nrec = vec < kRecClients ? (int)min(reccnt[vec], (uint32_t)kRecPerClient) : 0;
     if (tid < nrec) {
@@ -1580,10 +1596,10 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
         const int lane = tid & (kWave - 1);
         bool go = true;
         int32_t blk = tile;
-        uint64_t am = map0[base + min(blk + lane, tiles - 1)], bm = map1[base + min(blk + lane, tiles - 1)];
+        uint64_t am = M0(min(blk + lane, tiles - 1)), bm = M1(min(blk + lane, tiles - 1));
         while (go) {
             const int32_t nb = blk + kWave;
-            const uint64_t an = map0[base + min(nb + lane, tiles - 1)], bn = map1[base + min(nb + lane, tiles - 1)];
+            const uint64_t an = M0(min(nb + lane, tiles - 1)), bn = M1(min(nb + lane, tiles - 1));
             const uint64_t E0 = Pb >> 52;
             const bool valid = blk + lane < tiles && am != kIrrMap && (am >> 53) == E0;
             const uint64_t inv = __ballot(!valid);
@@ -1620,7 +1636,7 @@ exact_fold_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float f
         double P = __longlong_as_double((long long)Pb);
         const int64_t idx = base + tile;
         if (tid == 0) pre[idx] = Pb;
-        const uint32_t rid = map0[idx] == kIrrMap ? (uint32_t)map1[idx] : 0u;
+        const uint32_t rid = M0(tile) == kIrrMap ? (uint32_t)M1(tile) : 0u;
         if (rid != 0u && s_roff[rid - 1u] != ~0u) {            // recorded and prefetched: walk it
             if (tid == 0) {
                 const EvEntry* ev0 = s_ev + s_roff[rid - 1u];
@@ -1691,7 +1707,7 @@ template <bool VEC4, bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock)
 tile_out_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                 int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm, const float* __restrict__ Xs,
-                const float* __restrict__ l1, const uint64_t* __restrict__ pre) {
+                float Xval, const float* __restrict__ l1, const uint64_t* __restrict__ pre) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image, scratch, then output image
     __shared__ float s_tab[kTab];
     __shared__ ScanLds sl;
@@ -1719,7 +1735,7 @@ tile_out_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __
     const double base = resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);   // barrier-terminated if it used s_x
     uint32_t cw[4];
     float kmax = 0.0f;
-    tile_pass2<WQ, WC>(s_x, tv, s_tab, tid, base, L, fm, Xs[vec], cw, kmax);   // each thread rewrites its own row
+    tile_pass2<WQ, WC>(s_x, tv, s_tab, tid, base, L, fm, Xs ? Xs[vec] : Xval, cw, kmax);   // each thread rewrites its own row
     if (WC) {
         store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
         publish_kmax(kmax, L, overflow, vec, tid);
@@ -1847,13 +1863,16 @@ __device__ __forceinline__ void mean_add_batch(float (&e)[kMeanCpt], const uint2
     }
 }
 
-// Tables of clients j0 .. j0+nb-1 into tabn (callers bracket it with barriers).
+// Tables of clients j0 .. j0+nb-1 into tabn (callers bracket it with barriers).  With
+// `ovf` (LDS word, zero on entry), an overflowed client (kmax > 127) sets its bit there.
 __device__ __forceinline__ void mean_build_tables(float (*tabn)[256], const float* __restrict__ l1,
                                                   const int32_t* __restrict__ kmaxv, int64_t j0, int nb, int wid,
-                                                  int lane, float fm, float n_div) {
+                                                  int lane, float fm, float n_div, uint32_t* ovf = nullptr) {
     for (int jj = wid; jj < nb; jj += kCodesMeanThreads / kWave) {
         const float L = l1[j0 + jj];                // wave-uniform: scalar loads
-        const int km = min(127, max(0, kmaxv[j0 + jj]));
+        const int kr = kmaxv[j0 + jj];
+        const int km = min(127, max(0, kr));
+        if (ovf && kr > 127 && lane == 0) atomicOr(ovf, 1u << jj);
         for (int k = lane; k <= km; k += kWave) {
             const float v = ((L * (float)k) / fm) / n_div;
             tabn[jj][k] = v;                        // code k
@@ -1870,6 +1889,25 @@ __device__ __forceinline__ void mean_add_bytes(float (&e)[kMeanCpt], const int8_
             if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[(j0 + jj) * d + i0 + k]];
 }
 
+// A group holding an overflowed client, clients in order: an overflowed client adds
+// q[j][i] / n_div read from the dequantized batch (what K2 wrote correctly beside the
+// saturated codes; the same bits as its table entry would have had), the others their
+// table entries.  Any column alignment.
+__device__ __noinline__ void mean_add_mixed(float (&e)[kMeanCpt], const int8_t* __restrict__ codes,
+                                            const float* __restrict__ q, int64_t ldq, const float (*tabn)[256],
+                                            uint32_t ovf, int64_t j0, int nb, int64_t i0, int64_t d, float n_div) {
+    for (int jj = 0; jj < nb; ++jj) {
+        const int64_t j = j0 + jj;
+        if ((ovf >> jj) & 1u) {
+            for (int k = 0; k < kMeanCpt; ++k)
+                if (i0 + k < d) e[k] += q[j * ldq + i0 + k] / n_div;
+        } else {
+            for (int k = 0; k < kMeanCpt; ++k)
+                if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[j * d + i0 + k]];
+        }
+    }
+}
+
 // ALL: every thread's kMeanCpt columns lie inside d (d a multiple of kCodesMeanThreads *
 // kMeanCpt), so no
 // per-thread `full` test anywhere (a per-thread guard around the adds cost the loads'
@@ -1877,19 +1915,26 @@ __device__ __forceinline__ void mean_add_bytes(float (&e)[kMeanCpt], const int8_
 template <bool VEC, bool ALL = false>
 __global__ void __launch_bounds__(kCodesMeanThreads)
 codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, const int32_t* __restrict__ kmaxv,
-                  int64_t n, int64_t d, float fm, float n_div, int accumulate, float* __restrict__ est) {
+                  int64_t n, int64_t d, float fm, float n_div, int accumulate, float* __restrict__ est,
+                  const float* __restrict__ q, int64_t ldq) {
     __shared__ float tabn[kMeanClients][256];     // indexed by the raw code byte, sign included
+    // overflowed clients of group g as a bit mask in s_ovf[g & 1] (only with q): group g's
+    // table build sets bits in s_ovf[g & 1] and clears s_ovf[(g + 1) & 1], which every
+    // thread last read before group g's first barrier
+    __shared__ uint32_t s_ovf[2];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);
     const int64_t i0 = ((int64_t)blockIdx.x * kCodesMeanThreads + tid) * kMeanCpt;
     const bool full = ALL || (VEC && i0 + kMeanCpt <= d);
+    if (tid < 2) s_ovf[tid] = 0u;                   // ordered by the first group's barrier
     float e[kMeanCpt];
 #pragma unroll
     for (int k = 0; k < kMeanCpt; ++k) e[k] = (accumulate && i0 + k < d) ? est[i0 + k] : 0.0f;
     // full groups of kMeanClients: straight-line, unconditional loads (the prefetch of the
     // group after the last one is clamped to a valid row and never used), so the waits
-    // before each batch cover that batch only
+    // before each batch cover that batch only.  A group with an overflowed client (and q
+    // given) takes mean_add_mixed instead of the batch adds (wave-uniform branch).
     const int64_t groups = n / kMeanClients;
     const int8_t* cbase = codes + (full ? i0 : 0);
     uint2 wa[kMeanUnroll], wb[kMeanUnroll];
@@ -1897,24 +1942,31 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
     for (int64_t g = 0; g < groups; ++g) {
         const int64_t j0 = g * kMeanClients;
         __syncthreads();                            // previous group's tables no longer read
-        mean_build_tables(tabn, l1, kmaxv, j0, kMeanClients, wid, lane, fm, n_div);
+        if (q && tid == 0) s_ovf[(g + 1) & 1] = 0u;
+        mean_build_tables(tabn, l1, kmaxv, j0, kMeanClients, wid, lane, fm, n_div, q ? &s_ovf[g & 1] : nullptr);
         __syncthreads();
+        const uint32_t ovf = q ? s_ovf[g & 1] : 0u;
         if (VEC) {
             mean_load_batch(wb, cbase + (j0 + kMeanUnroll) * d, d);
-            if (full) mean_add_batch(e, wa, tabn, 0);
+            if (full && !ovf) mean_add_batch(e, wa, tabn, 0);
             const int64_t jn = (j0 + kMeanClients + kMeanUnroll <= n) ? j0 + kMeanClients : n - kMeanUnroll;
             mean_load_batch(wa, cbase + jn * d, d);
-            if (full) mean_add_batch(e, wb, tabn, kMeanUnroll);
+            if (full && !ovf) mean_add_batch(e, wb, tabn, kMeanUnroll);
         }
-        if (!full) mean_add_bytes(e, codes, tabn, j0, kMeanClients, i0, d);
+        if (ovf) mean_add_mixed(e, codes, q, ldq, tabn, ovf, j0, kMeanClients, i0, d, n_div);
+        else if (!full) mean_add_bytes(e, codes, tabn, j0, kMeanClients, i0, d);
     }
     const int64_t jr = groups * kMeanClients;
     const int nr = (int)(n - jr);
     if (nr > 0) {                                   // the last n % kMeanClients clients
         __syncthreads();
-        mean_build_tables(tabn, l1, kmaxv, jr, nr, wid, lane, fm, n_div);
+        if (q && tid == 0) s_ovf[(groups + 1) & 1] = 0u;
+        mean_build_tables(tabn, l1, kmaxv, jr, nr, wid, lane, fm, n_div, q ? &s_ovf[groups & 1] : nullptr);
         __syncthreads();
-        if (full) {
+        const uint32_t ovf = q ? s_ovf[groups & 1] : 0u;
+        if (ovf) {
+            mean_add_mixed(e, codes, q, ldq, tabn, ovf, jr, nr, i0, d, n_div);
+        } else if (full) {
             for (int jj = 0; jj < nr; ++jj) {
                 const uint2 w = *reinterpret_cast<const uint2*>(codes + (jr + jj) * d + i0);
 #pragma unroll
@@ -2343,16 +2395,21 @@ int uq_l1_torch_order_f32(const float* x, int64_t n, int64_t d, int32_t T, float
     return launch_l1(x, n, d, plan, part, l1_out, st);
 }
 
-int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_t* overflow, int64_t n, int64_t d,
-                               int64_t m, const float* X, const float* l1, float* l1_out, int32_t T, void* ws,
-                               size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+namespace {
+// AS:609-641 for a batch.  X: per-client draws (device), or nullptr with n == 1 and the one
+// draw passed by value in Xval (the per-call drop-in: no host-to-device copy of X).
+int unbiased_codes_impl(const float* x, float* out, int8_t* codes, int32_t* overflow, int64_t n, int64_t d,
+                        int64_t m, const float* X, float Xval, const float* l1, float* l1_out, int32_t T, void* ws,
+                        size_t ws_bytes, void* stream) {
     L1Plan plan;
     WsLayout w;
     int rc = check_common(x, n, d, T, ws, ws_bytes, &plan, &w);
     if (rc) return rc;
     if (m < 0) return fail(UQ_E_INVALID, "m must be >= 0");
     if (n == 0 || d == 0) return UQ_OK;
-    if (!X) return fail(UQ_E_INVALID, "null X");
+    if (!X && n != 1) return fail(UQ_E_INVALID, "null X");
     if (!out && !codes) return fail(UQ_E_INVALID, "nothing to write: out and codes are both NULL");
     if (codes && !overflow) return fail(UQ_E_INVALID, "codes need a kmax[n] array");
     hipStream_t st = (hipStream_t)stream;
@@ -2383,7 +2440,7 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
 #define UQ_STREAM(Q, C, CV)                                                                                 \
     case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
         hipLaunchKernelGGL((quantize_stream_kernel<Q, C, CV>), dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, \
-                           codes, overflow, d, w.tiles, fm, X, l1use, w.tiles, 1, nullptr);              \
+                           codes, overflow, d, w.tiles, fm, X, Xval, l1use, w.tiles, 1, nullptr);        \
         break;
         switch (sel & 7) {
             UQ_STREAM(1, 0, 1) UQ_STREAM(1, 1, 1) UQ_STREAM(1, 1, 0) UQ_STREAM(0, 1, 1) UQ_STREAM(0, 1, 0)
@@ -2400,16 +2457,13 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
         float* outj = out ? out + j0 * d : nullptr;
         int8_t* codesj = codes ? codes + j0 * d : nullptr;
         int32_t* ovj = codes ? overflow + j0 : nullptr;
-        const float* Xj = X + j0;
+        const float* Xj = X ? X + j0 : nullptr;
         const float* l1j = l1use + j0;
         uint64_t* agg = (uint64_t*)(wsb + w.agg_off) + j0 * w.tiles;
         uint64_t* pre = (uint64_t*)(wsb + w.incl_off) + j0 * w.tiles;
         uint64_t* map1 = (uint64_t*)(wsb + w.map1_off) + j0 * w.tiles;
         TileRec* recs = (TileRec*)(wsb + w.rec_off);
-        uint32_t* reccnt = (uint32_t*)(wsb + w.cnt_off);
-        rc = hip_check(hipMemsetAsync(reccnt, 0, std::min<int64_t>(nj, kRecClients) * sizeof(uint32_t), st),
-                       "memset record counters");
-        if (rc) return rc;
+        uint32_t* reccnt = (uint32_t*)(wsb + w.cnt_off);      // zeroed by the tile-sum kernels
         const int64_t total_tiles = nj * (int64_t)w.tiles;
         const bool seg = vec4 && d <= ((int64_t)1 << 29) && total_tiles >= kSegMinTiles;
         const dim3 tgrid((unsigned)w.tiles, (unsigned)nj);
@@ -2422,11 +2476,11 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
             R = (int32_t)std::max<int64_t>(1, (total_tiles + slots - 1) / slots);
             nseg = (w.tiles + R - 1) / R;
             hipLaunchKernelGGL(agg_stream_kernel, dim3((unsigned)(nj * nseg)), dim3(kQBlock), 0, st, xj, d, w.tiles, fm,
-                               l1j, R, nseg, agg);
+                               l1j, R, nseg, agg, reccnt);
         } else if (vec4) {
-            hipLaunchKernelGGL(tile_agg_kernel<true>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg);
+            hipLaunchKernelGGL(tile_agg_kernel<true>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg, reccnt);
         } else {
-            hipLaunchKernelGGL(tile_agg_kernel<false>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg);
+            hipLaunchKernelGGL(tile_agg_kernel<false>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg, reccnt);
         }
         rc = hip_check(hipGetLastError(), "tile sums launch");
         if (rc) return rc;
@@ -2452,7 +2506,7 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
 #define UQ_SEG(Q, C, CV)                                                                                    \
     case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
         hipLaunchKernelGGL((quantize_stream_kernel<Q, C, CV>), dim3((unsigned)(nj * nseg)), dim3(kQBlock), 0, st, xj, \
-                           outj, codesj, ovj, d, w.tiles, fm, Xj, l1j, R, nseg, pre);                      \
+                           outj, codesj, ovj, d, w.tiles, fm, Xj, Xval, l1j, R, nseg, pre);                \
         break;
             switch (sel & 7) {
                 UQ_SEG(1, 0, 1) UQ_SEG(1, 1, 1) UQ_SEG(1, 1, 0) UQ_SEG(0, 1, 1) UQ_SEG(0, 1, 0)
@@ -2466,7 +2520,7 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
 #define UQ_PHASED(V, Q, C, CV)                                                                                \
     case ((V) * 8 + (Q) * 4 + (C) * 2 + (CV)):                                                              \
         hipLaunchKernelGGL((tile_out_kernel<V, Q, C, CV>), tgrid, dim3(kQBlock), 0, st, xj, outj, codesj, ovj, d, \
-                           w.tiles, fm, Xj, l1j, pre);                                                        \
+                           w.tiles, fm, Xj, Xval, l1j, pre);                                                  \
         break;
         switch (sel) {
             UQ_PHASED(1, 1, 0, 1) UQ_PHASED(1, 1, 1, 1) UQ_PHASED(1, 1, 1, 0) UQ_PHASED(1, 0, 1, 1)
@@ -2479,6 +2533,24 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
         if (rc) return rc;
     }
     return UQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_t* overflow, int64_t n, int64_t d,
+                               int64_t m, const float* X, const float* l1, float* l1_out, int32_t T, void* ws,
+                               size_t ws_bytes, void* stream) {
+    if (n > 0 && d > 0 && !X) return fail(UQ_E_INVALID, "null X");
+    return unbiased_codes_impl(x, out, codes, overflow, n, d, m, X, 0.0f, l1, l1_out, T, ws, ws_bytes, stream);
+}
+
+int uq_type_unbiased_vec_f32(const float* x, float* out, int64_t d, int64_t m, float X, int32_t T, void* ws,
+                             size_t ws_bytes, void* stream) {
+    if (d > 0 && !out) return fail(UQ_E_INVALID, "null out");
+    return unbiased_codes_impl(x, out, nullptr, nullptr, 1, d, m, nullptr, X, nullptr, nullptr, T, ws, ws_bytes,
+                               stream);
 }
 
 int uq_type_unbiased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m, const float* X,
@@ -2505,11 +2577,12 @@ int uq_codes_decode_f32(const int8_t* codes, const float* l1, int64_t n, int64_t
     return hip_check(hipGetLastError(), "codes_decode_kernel launch");
 }
 
-int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax, int64_t n, int64_t d, int64_t m,
-                      float n_div, int32_t accumulate, float* est, void* stream) {
+int uq_codes_q_mean_f32(const int8_t* codes, const float* q, int64_t ldq, const float* l1, const int32_t* kmax,
+                        int64_t n, int64_t d, int64_t m, float n_div, int32_t accumulate, float* est, void* stream) {
     if (n < 0 || d < 0 || m < 0) return fail(UQ_E_INVALID, "n, d and m must be >= 0");
     if (d == 0) return UQ_OK;
     if (!est || (n > 0 && (!codes || !l1 || !kmax))) return fail(UQ_E_INVALID, "null pointer");
+    if (q && ldq < d) return fail(UQ_E_INVALID, "ldq must be >= d");
     hipStream_t st = (hipStream_t)stream;
     const bool vec = (n == 0 || aligned16(codes)) && aligned16(est) && d % 16 == 0;
     const int64_t blocks = (d + kCodesMeanThreads * kMeanCpt - 1) / (kCodesMeanThreads * kMeanCpt);
@@ -2517,14 +2590,19 @@ int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax,
     const dim3 tb(kCodesMeanThreads);
     if (vec && d % (kCodesMeanThreads * kMeanCpt) == 0)
         hipLaunchKernelGGL((codes_mean_kernel<true, true>), dim3((unsigned)blocks), tb, 0, st, codes, l1, kmax, n, d,
-                           (float)m, n_div, accumulate, est);
+                           (float)m, n_div, accumulate, est, q, ldq);
     else if (vec)
         hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), tb, 0, st, codes, l1, kmax, n, d, (float)m,
-                           n_div, accumulate, est);
+                           n_div, accumulate, est, q, ldq);
     else
         hipLaunchKernelGGL(codes_mean_kernel<false>, dim3((unsigned)blocks), tb, 0, st, codes, l1, kmax, n, d, (float)m,
-                           n_div, accumulate, est);
+                           n_div, accumulate, est, q, ldq);
     return hip_check(hipGetLastError(), "codes_mean_kernel launch");
+}
+
+int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax, int64_t n, int64_t d, int64_t m,
+                      float n_div, int32_t accumulate, float* est, void* stream) {
+    return uq_codes_q_mean_f32(codes, nullptr, d, l1, kmax, n, d, m, n_div, accumulate, est, stream);
 }
 
 int uq_client_mean_f32(const float* q, int64_t n, int64_t d, int64_t ld, float n_div, int32_t accumulate,

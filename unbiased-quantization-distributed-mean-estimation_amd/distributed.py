@@ -120,14 +120,104 @@ def sharded_client_mean(q_local: torch.Tensor, n_div: float, *, mode: str = "red
     return est if rank == dst else None
 
 
+class ShardedDME:
+    """One rank's share of the client-sharded DME step on a node (the path bench.py times).
+
+        sh = ShardedDME(n_local, d, n_total, bits_per_dimension=1, mode="reduce")
+        sh.probe_outputs(x_local, X_local)          # optional, once (pipeline.py)
+        est = sh.step(x_local, X_local)             # K1 -> K2 (q + codes) -> K3c -> reduce
+        sh.drain()                                  # every pending reduce done; est valid on dst
+
+    The rank quantizes its contiguous client block with a resident DMEPipeline (no data-path
+    collective) and folds it into a partial mean over n_total, then:
+      mode "reduce":  ONE reduce(SUM) of d floats to `dst` (RCCL over xGMI).  With RCCL and
+                      overlap=True (the default there) the reduce of step k is issued
+                      asynchronously and runs beside step k+1's kernels: two estimate buffers
+                      alternate, and step k+2 waits (stream-ordered, the host does not block)
+                      for reduce k before it overwrites that buffer.  est of step k is valid on
+                      `dst` after the next-but-one step or drain().
+      mode "ordered": the bit-exact chain of sharded_client_mean over q's column blocks
+                      (pipeline must write q).
+    With gloo (CPU tests, ranks sharing one GPU) the reduce is host-staged and synchronous."""
+
+    def __init__(self, n_local: int, d: int, n_total: int, bits_per_dimension=1, *, m: int | None = None,
+                 torch_threads: int = 1, pipeline: str = "codes", mode: str = "reduce", dst: int = 0, group=None,
+                 overlap: Optional[bool] = None, block: int = 1 << 18, device=None):
+        from .pipeline import DMEPipeline
+        if mode not in ("reduce", "ordered"):
+            raise ValueError("mode must be 'reduce' or 'ordered'")
+        if mode == "ordered" and pipeline == "encode":
+            raise ValueError("mode 'ordered' folds q: use pipeline 'codes' or 'q'")
+        self.pipe = DMEPipeline(n_local, d, bits_per_dimension, m=m, torch_threads=torch_threads, pipeline=pipeline,
+                                device=device)
+        self.n_total, self.mode, self.dst, self.group, self.block = int(n_total), mode, int(dst), group, int(block)
+        self.dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.dist_on else 1
+        self.rank = dist.get_rank(group) if self.dist_on else 0
+        rccl = self.dist_on and dist.get_backend(group) == "nccl"
+        self.overlap = bool(rccl and mode == "reduce" and self.world > 1 if overlap is None else overlap)
+        if self.overlap and not (rccl and mode == "reduce"):
+            raise ValueError("overlap needs the RCCL (nccl) backend and mode 'reduce'")
+        self.est_bufs = [self.pipe.est, torch.empty_like(self.pipe.est)] if self.overlap else [self.pipe.est]
+        self.pending = [None] * len(self.est_bufs)
+        self.nstep = 0
+
+    def probe_outputs(self, x_local, X_local, **kw):
+        return self.pipe.probe_outputs(x_local, X_local, **kw)
+
+    def step(self, x_local, X_local, *, events=None, pipeline: Optional[str] = None):
+        """Returns this step's est buffer (the global mean on `dst` once its reduce is done:
+        immediately unless overlap; None off `dst` in mode "ordered")."""
+        slot = self.nstep % len(self.est_bufs)
+        self.nstep += 1
+        est = self.est_bufs[slot]
+        if self.pending[slot] is not None:            # reduce of step k-2 still owns this buffer
+            self.pending[slot].wait()
+            self.pending[slot] = None
+        ev = list(events or (None,) * 5)
+        self.pipe.step(x_local, X_local, float(self.n_total), est=est, events=ev[:4], pipeline=pipeline)
+        if self.world > 1 or self.overlap:            # (overlap at world 1: RCCL's no-op reduce, tests)
+            if self.mode == "reduce":
+                if self.overlap:
+                    self.pending[slot] = dist.reduce(est, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group,
+                                                     async_op=True)
+                else:
+                    _reduce(est, self.dst, self.group)
+            else:
+                est = sharded_client_mean(self.pipe.q, float(self.n_total), mode="ordered", dst=self.dst,
+                                          block=self.block, group=self.group)
+        if ev[4] is not None:
+            ev[4].record()
+        return est if (self.rank == self.dst or self.mode == "reduce") else None
+
+    def drain(self):
+        """Wait (stream-ordered) for every pending reduce."""
+        for i, w in enumerate(self.pending):
+            if w is not None:
+                w.wait()
+                self.pending[i] = None
+
+    def check_status(self):
+        self.pipe.check_status()
+
+
 def sharded_quantize_mean(x_local: torch.Tensor, bits_per_dimension, X_local, n_total: int, *,
                           mode: str = "reduce", dst: int = 0, torch_threads: int = 1, group=None,
                           return_q: bool = False):
-    """Quantize this rank's clients (HIP) and form the global client mean.
+    """Quantize this rank's clients (HIP) and form the global client mean: one ShardedDME
+    step (K1 -> K2 writing q and type codes -> mean from the codes -> one reduce, or the
+    ordered chain), with buffers allocated for this call (no placement probe).
 
     x_local = the rank's contiguous client block (see shard_range); X_local = its
     slice of the per-client uniforms drawn once for all clients."""
-    from .quantizer import quantize_dequantize
-    q = quantize_dequantize(x_local, bits_per_dimension, X=X_local, torch_threads=torch_threads)
-    est = sharded_client_mean(q, float(n_total), mode=mode, dst=dst, group=group)
-    return (est, q) if return_q else est
+    from .quantizer import _as_device_f32_2d, _device
+    dev = _device()
+    x_local = _as_device_f32_2d(x_local, dev)
+    n_local, d = x_local.shape
+    X_local = torch.as_tensor(X_local, dtype=torch.float32).reshape(-1).to(dev)
+    sh = ShardedDME(n_local, d, n_total, bits_per_dimension, torch_threads=torch_threads, mode=mode, dst=dst,
+                    group=group, overlap=False, device=dev)
+    est = sh.step(x_local, X_local)
+    if est is not None and mode == "reduce" and sh.rank != dst:
+        est = None
+    return (est, sh.pipe.q) if return_q else est

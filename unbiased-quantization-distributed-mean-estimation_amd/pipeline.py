@@ -3,7 +3,15 @@
     p = DMEPipeline(n, d, bits_per_dimension=1, torch_threads=1)
     est = p.step(x, X, n_div)        # K1 L1 (AS:624) -> K2 quantize (AS:625-640, writes q and
                                      # type codes) -> K3c client-ordered mean (ND:137-138)
-    p.q, p.codes, p.l1               # the step's per-client outputs (overwritten by the next step)
+    p.q, p.codes, p.l1, p.kmax       # the step's per-client outputs (overwritten by the next step)
+
+Pipelines (what K2 writes and what the mean reads; est has the same bits in all three):
+    "codes"   q and the int8 type codes; the mean reads the codes (1 B per coordinate), and a
+              client whose counts overflowed its codes (kmax > 127) is read from q instead
+              (uq_codes_q_mean_f32), so est is always the client-ordered mean of q
+    "q"       q only; the mean reads q (4 B per coordinate) -- the drop-in's output form
+    "encode"  codes only (no q); the mean reads the codes.  An overflowed client cannot be
+              recovered without q: check_status() raises OverflowError for it.
 
 Output placement.  K2 writes q (4*d B per client) and the int8 codes (1*d) while reading x.
 On MI355X its time depends on where the OUTPUT buffers land in physical memory: with x fixed
@@ -12,20 +20,27 @@ q + codes fixed and x re-allocated ten times 1.67-1.73 ms (profiles/r02d_exp_pla
 the code layout does not matter (tile-major codes follow the same modes,
 profiles/r02c_exp_codes_layout.jsonl).  The pipeline's outputs are long-lived, so
 `probe_outputs` allocates candidate (q, codes) sets (each on its own pages, all held until
-the choice), times K2 on each with the real batch until it has seen both speeds, keeps the
-fastest and frees the rest: a one-time calibration like a workspace autotune.  Results do not depend on the buffers chosen.
+the choice: freeing a loser would hand its pages to the next candidate), times K2 on each
+with the real batch until it has seen both speeds, keeps the fastest and frees the rest: a
+one-time calibration like a workspace autotune.  Results do not depend on the buffers
+chosen.  Only callers that keep a pipeline resident get the probed speed; the one-shot
+batched APIs (quantize_dequantize, quantize_mean, ...) allocate per call and land in either
+mode (INTEGRATION.md).
 
 Every launch goes through the C-ABI (include/uq_dme.h); nothing here computes on the CPU."""
 from __future__ import annotations
 
 import ctypes
+import statistics
 
 import torch
 
 from . import _lib
 from .rates import rate_to_m
 
-__all__ = ["DMEPipeline"]
+__all__ = ["DMEPipeline", "PIPELINES"]
+
+PIPELINES = ("codes", "q", "encode")
 
 
 def _p(t) -> int:
@@ -34,14 +49,16 @@ def _p(t) -> int:
 
 class DMEPipeline:
     def __init__(self, n: int, d: int, bits_per_dimension=1, *, m: int | None = None, torch_threads: int = 1,
-                 write_q: bool = True, device=None):
+                 pipeline: str = "codes", device=None):
         if not torch.cuda.is_available():
             raise RuntimeError("uqdme requires a ROCm GPU (no CPU fallback by design)")
+        if pipeline not in PIPELINES:
+            raise ValueError(f"pipeline must be one of {PIPELINES}")
         self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.n, self.d = int(n), int(d)
         self.m = int(m) if m is not None else rate_to_m(bits_per_dimension, d)
         self.T = int(torch_threads)
-        self.write_q = bool(write_q)
+        self.pipeline = pipeline
         self.lib = _lib.load()
         b = ctypes.c_size_t()
         _lib.check(self.lib.uq_workspace_bytes(self.n, self.d, self.T, ctypes.byref(b)), "uq_workspace_bytes")
@@ -52,6 +69,11 @@ class DMEPipeline:
         self.est = torch.empty(self.d, dtype=torch.float32, device=self.dev)
         self.q, self.codes = self._alloc_outputs()
         self.probe_report = None
+        self._codes_valid = False       # the last K2 launch wrote codes (and kmax)
+
+    @property
+    def write_q(self) -> bool:
+        return self.pipeline != "encode"
 
     # ---- buffers ---------------------------------------------------------------------
     def _alloc_outputs(self):
@@ -67,26 +89,54 @@ class DMEPipeline:
         _lib.check(self.lib.uq_l1_torch_order_f32(_p(x), self.n, self.d, self.T, _p(self.l1), _p(self.ws),
                                                   self.ws_bytes, self._stream()), "uq_l1_torch_order_f32")
 
-    def quantize(self, x, X, q=None, codes=None):
-        q = self.q if q is None and self.write_q else q
-        codes = self.codes if codes is None else codes
-        _lib.check(self.lib.uq_type_unbiased_codes_f32(_p(x), _p(q), _p(codes), _p(self.kmax), self.n, self.d, self.m,
-                                                       _p(X), _p(self.l1), None, self.T, _p(self.ws), self.ws_bytes,
-                                                       self._stream()), "uq_type_unbiased_codes_f32")
+    def quantize(self, x, X, q=None, codes=None, pipeline: str | None = None):
+        """K2 with the batch's L1 (l1_norms first).  `pipeline` overrides what is written for
+        this launch ("q": q only, "encode": codes only, "codes": both)."""
+        pl = pipeline or self.pipeline
+        q = (self.q if q is None else q) if pl != "encode" else None
+        codes = (self.codes if codes is None else codes) if pl != "q" else None
+        if pl != "encode" and q is None:
+            raise ValueError("this pipeline holds no q buffer")
+        _lib.check(self.lib.uq_type_unbiased_codes_f32(_p(x), _p(q), _p(codes), _p(self.kmax if codes is not None else None),
+                                                       self.n, self.d, self.m, _p(X), _p(self.l1), None, self.T,
+                                                       _p(self.ws), self.ws_bytes, self._stream()),
+                   "uq_type_unbiased_codes_f32")
+        self._codes_valid = codes is not None
 
-    def mean(self, n_div: float, accumulate: bool = False):
-        _lib.check(self.lib.uq_codes_mean_f32(_p(self.codes), _p(self.l1), _p(self.kmax), self.n, self.d, self.m,
-                                              float(n_div), int(bool(accumulate)), _p(self.est), self._stream()),
-                   "uq_codes_mean_f32")
-        return self.est
+    def mean(self, n_div: float, accumulate: bool = False, est=None, pipeline: str | None = None):
+        """K3 (from q) or K3c (from the codes, overflowed clients from q when it was written)."""
+        pl = pipeline or self.pipeline
+        est = self.est if est is None else est
+        if pl == "q":
+            _lib.check(self.lib.uq_client_mean_f32(_p(self.q), self.n, self.d, self.d, float(n_div),
+                                                   int(bool(accumulate)), _p(est), self._stream()), "uq_client_mean_f32")
+        else:
+            q = self.q if pl == "codes" else None
+            _lib.check(self.lib.uq_codes_q_mean_f32(_p(self.codes), _p(q), self.d, _p(self.l1), _p(self.kmax), self.n,
+                                                    self.d, self.m, float(n_div), int(bool(accumulate)), _p(est),
+                                                    self._stream()), "uq_codes_q_mean_f32")
+        return est
 
-    def step(self, x, X, n_div=None, accumulate: bool = False):
+    def step(self, x, X, n_div=None, accumulate: bool = False, *, est=None, events=None,
+             pipeline: str | None = None):
         """One pass of the hot path over the resident batch x[n, d] (f32, contiguous, on the
-        device) with per-client uniforms X[n] (device f32).  Returns est (+)= sum_j q_j / n_div."""
+        device) with per-client uniforms X[n] (device f32).  Returns est (+)= sum_j q_j / n_div
+        (into `est` when given, else the pipeline's own buffer).  `events`: four HIP events
+        recorded on the stream before K1, after K1, after K2 and after the mean."""
         self._check(x, X)
+        ev = events or (None, None, None, None)
+        if ev[0] is not None:
+            ev[0].record()
         self.l1_norms(x)
-        self.quantize(x, X)
-        return self.mean(self.n if n_div is None else n_div, accumulate)
+        if ev[1] is not None:
+            ev[1].record()
+        self.quantize(x, X, pipeline=pipeline)
+        if ev[2] is not None:
+            ev[2].record()
+        out = self.mean(self.n if n_div is None else n_div, accumulate, est=est, pipeline=pipeline)
+        if ev[3] is not None:
+            ev[3].record()
+        return out
 
     def _check(self, x, X):
         if x.shape != (self.n, self.d) or x.dtype != torch.float32 or not x.is_contiguous() or x.device != self.dev:
@@ -96,17 +146,21 @@ class DMEPipeline:
 
     # ---- output placement ------------------------------------------------------------
     def probe_outputs(self, x, X, candidates: int = 16, reps: int = 3, batch: int = 4, spread: float = 1.15,
-                      min_candidates: int = 1):
+                      min_candidates: int = 1, reserve_frac: float = 0.25):
         """Time K2 on output sets (the current one included), keep the fastest.  Sets are
         added `batch` at a time, up to `candidates`, until the probe has seen both speeds
         (slowest / fastest >= `spread`; the fast and slow modes are 15-20 % apart, and
         spread 1.10 once stopped on an intermediate 1.74 ms set against 1.92-1.98 ms ones,
         profiles/r04a_bench.json): with ~30-60 % of sets fast, six fixed candidates left
-        ~1 rank in 8 without a fast set.  Needs the batch's L1 (runs K1 first).  Returns
-        the report (ms per candidate)."""
+        ~1 rank in 8 without a fast set.  No set is added once free device memory would
+        drop below `reserve_frac` of the device (the held sets are the probe's only cost:
+        ~5 GB each at 1024 x 2^20).  Needs the batch's L1 (runs K1 first).  Returns the
+        report: ms per candidate, the chosen one, and the median over all candidates (what a
+        caller allocating fresh outputs gets on average)."""
         self._check(x, X)
         self.l1_norms(x)
         sets, times = [(self.q, self.codes)], []
+        set_bytes = self.n * self.d * (5 if self.write_q else 1)
 
         def time_set(q, c):
             for _ in range(2):
@@ -120,17 +174,41 @@ class DMEPipeline:
             torch.cuda.synchronize(self.dev)
             return e0.elapsed_time(e1) / reps
 
+        def room() -> bool:
+            free, total = torch.cuda.mem_get_info(self.dev)
+            return free - set_bytes >= reserve_frac * total
+
         times.append(time_set(*sets[0]))
+        capped = False
         while len(sets) < candidates and (len(sets) < min_candidates or max(times) < spread * min(times)):
             for _ in range(min(batch, candidates - len(sets))):
+                if not room():
+                    capped = True
+                    break
                 sets.append(self._alloc_outputs())
                 times.append(time_set(*sets[-1]))
+            if capped:
+                break
         best = min(range(len(sets)), key=lambda i: times[i])
         self.q, self.codes = sets[best]
         del sets
         torch.cuda.empty_cache()
-        self.probe_report = {"candidates": len(times), "k2_ms": [round(t, 4) for t in times], "chosen": best}
+        self.probe_report = {"candidates": len(times), "k2_ms": [round(t, 4) for t in times], "chosen": best,
+                             "k2_ms_chosen": round(times[best], 4),
+                             "k2_ms_median_unprobed": round(statistics.median(times), 4),
+                             "memory_capped": capped}
         return self.probe_report
 
+    def overflowed(self) -> int:
+        """Clients of the last step whose counts overflowed their int8 codes (synchronises)."""
+        if not self._codes_valid:
+            return 0
+        return int(torch.count_nonzero(self.kmax > 127).item())
+
     def check_status(self):
+        """Synchronise; raise if an in-kernel wait timed out, or (pipeline "encode") if a
+        client's codes overflowed, since its est contribution is then wrong."""
         _lib.check(self.lib.uq_check_status(_p(self.ws), self._stream()), "uq_check_status")
+        if self.pipeline == "encode" and self.overflowed():
+            raise OverflowError("type codes overflowed (lattice counts > 127) in an encode-only step: "
+                                "est is wrong for those clients; use pipeline='codes' (falls back to q)")

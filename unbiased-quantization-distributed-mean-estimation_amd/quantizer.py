@@ -18,6 +18,7 @@ Every path calls the C-ABI in include/uq_dme.h; nothing here computes on the CPU
 from __future__ import annotations
 
 import ctypes
+import functools
 import os
 import threading
 
@@ -81,6 +82,7 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
         return ws
 
 
+@functools.lru_cache(maxsize=256)
 def _ws_bytes(n: int, d: int, T: int) -> int:
     out = ctypes.c_size_t(0)
     _lib.check(_lib.load().uq_workspace_bytes(n, d, T, ctypes.byref(out)), "uq_workspace_bytes")
@@ -298,4 +300,13 @@ def Type_unbiased_quantize(input_vector, bits_per_dimension=1):
     X = torch.rand(1)                                   # AS:634 (global CPU generator)
     if d == 0:
         return v.clone()
-    return quantize_dequantize(v.view(1, d), X=X, m=m).view(d)
+    if not v.is_contiguous():
+        v = v.contiguous()
+    # one vector per call: X goes to the kernels by value (uq_type_unbiased_vec_f32), so the
+    # call is the kernel chain alone -- no host-to-device copy of X, no workspace fill
+    T = get_torch_threads()
+    out = torch.empty_like(v)
+    ws = _workspace(dev, _ws_bytes(1, d, T))
+    _lib.check(_lib.load().uq_type_unbiased_vec_f32(_ptr(v), _ptr(out), d, m, float(X[0]), T, _ptr(ws),
+                                                    ws.numel(), _stream_ptr(dev)), "uq_type_unbiased_vec_f32")
+    return out
