@@ -1,7 +1,8 @@
 """Known NMSE answers for the multi-scheme DME loop, made by running the REFERENCE's own
 functions in the driver's call order (build container only):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_nmse_schemes.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_nmse_schemes.py            # d = 2048
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_nmse_schemes.py --dim 4194304  # C4's d = 2^22
 
 ND = NMSE_Results/Codes/Normal_dist.py.  Per client, in order: EDEN_quantize_Hadamard(v, 1),
 (v, 2) (ND:135-136), Type_unbiased_quantize(v, 1), (v, 2) (ND:137-138),
@@ -11,6 +12,7 @@ schemes of the shipped loop are left out (QUIC-FL crashes: its sender tables are
 """
 from __future__ import annotations
 
+import argparse
 import json
 import os
 import sys
@@ -25,11 +27,14 @@ sys.dont_write_bytecode = True
 sys.path.insert(0, "/root/reference/NMSE_Results/Codes")
 import All_Schemes as AS  # noqa: E402  (the reference module)
 
-DIM = 2048
 SCHEMES = [("eden", 1), ("eden", 2), ("unbiased", 1), ("unbiased", 2), ("biased", 1), ("biased", 2)]
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dim", type=int, default=2048)
+    a = ap.parse_args()
+    DIM = a.dim
     torch.set_num_threads(1)
     fns = {"eden": AS.EDEN_quantize_Hadamard, "unbiased": AS.Type_unbiased_quantize,
            "biased": AS.Type_biased_quantize}
@@ -58,7 +63,8 @@ def main():
                 rows.append(row)
                 print(dist, row, flush=True)
         res[dist] = rows
-    with open(os.path.join(HERE, "nd_nmse_schemes.json"), "w") as f:
+    name = "nd_nmse_schemes.json" if DIM == 2048 else f"nd_nmse_schemes_d{DIM}.json"
+    with open(os.path.join(HERE, name), "w") as f:
         json.dump({"dim": DIM, "rows": res}, f, indent=1)
 
 

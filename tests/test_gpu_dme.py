@@ -89,14 +89,20 @@ def test_sharded_mean_single_rank_nccl(uq):
         dist.destroy_process_group()
 
 
-def test_multi_scheme_nmse_known_answers(gpu_ready):
+@pytest.mark.parametrize("fixture", ["nd_nmse_schemes.json", "nd_nmse_schemes_d4194304.json"])
+def test_multi_scheme_nmse_known_answers(gpu_ready, fixture):
     """EDEN 1/2, unbiased 1/2 and biased 1/2 in the driver's call order against the
-    reference's own loop (tests/golden/nd_nmse_schemes.json): within 1e-6 relative."""
+    reference's own loop (tests/golden/nd_nmse_schemes*.json, made by
+    make_golden_nmse_schemes.py): d = 2048, and config C4's d = 2^22 (normal + laplace,
+    n in {1, 6}, two instances each).  Unbiased and biased within 1e-6 relative (north_star).
+    EDEN within 1e-6 at d = 2048 and 1e-5 at d = 2^22: its scale (AS:335) is an MKL sdot,
+    2^22 f32 products accumulated in MKL's CPU-dependent order, whose own rounding is ~1e-6
+    relative at that size (the GPU accumulates in fp64; observed 1.3e-6 on normal n=1)."""
     import json
     import os
     import uqdme
     from tests.golden_data import GOLDEN
-    ref = json.load(open(os.path.join(GOLDEN, "nd_nmse_schemes.json")))
+    ref = json.load(open(os.path.join(GOLDEN, fixture)))
     for dist, rows in ref["rows"].items():
         res = uqdme.nmse_simulation(dist, dim=ref["dim"], users=(1, 6), num_instances=2,
                                     schemes=("eden", "unbiased", "biased"), torch_threads=1)
@@ -106,4 +112,5 @@ def test_multi_scheme_nmse_known_answers(gpu_ready):
                 for r in (1, 2):
                     got = float(res[(sc, r)]["script"][ui, row["inst"]])
                     exp = row[f"{sc}{r}"]
-                    assert abs(got - exp) <= 1e-6 * exp, (dist, row["n"], row["inst"], sc, r, got, exp)
+                    tol = 1e-5 if sc == "eden" and ref["dim"] > 2048 else 1e-6
+                    assert abs(got - exp) <= tol * exp, (dist, row["n"], row["inst"], sc, r, got, exp)

@@ -1863,16 +1863,13 @@ __device__ __forceinline__ void mean_add_batch(float (&e)[kMeanCpt], const uint2
     }
 }
 
-// Tables of clients j0 .. j0+nb-1 into tabn (callers bracket it with barriers).  With
-// `ovf` (LDS word, zero on entry), an overflowed client (kmax > 127) sets its bit there.
+// Tables of clients j0 .. j0+nb-1 into tabn (callers bracket it with barriers).
 __device__ __forceinline__ void mean_build_tables(float (*tabn)[256], const float* __restrict__ l1,
                                                   const int32_t* __restrict__ kmaxv, int64_t j0, int nb, int wid,
-                                                  int lane, float fm, float n_div, uint32_t* ovf = nullptr) {
+                                                  int lane, float fm, float n_div) {
     for (int jj = wid; jj < nb; jj += kCodesMeanThreads / kWave) {
         const float L = l1[j0 + jj];                // wave-uniform: scalar loads
-        const int kr = kmaxv[j0 + jj];
-        const int km = min(127, max(0, kr));
-        if (ovf && kr > 127 && lane == 0) atomicOr(ovf, 1u << jj);
+        const int km = min(127, max(0, kmaxv[j0 + jj]));
         for (int k = lane; k <= km; k += kWave) {
             const float v = ((L * (float)k) / fm) / n_div;
             tabn[jj][k] = v;                        // code k
@@ -1889,11 +1886,18 @@ __device__ __forceinline__ void mean_add_bytes(float (&e)[kMeanCpt], const int8_
             if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[(j0 + jj) * d + i0 + k]];
 }
 
-// A group holding an overflowed client, clients in order: an overflowed client adds
+// Overflowed clients (kmax > 127: a count saturated its int8 code) among j0 .. j0+nb-1.
+__device__ __forceinline__ uint32_t mean_ovf_mask(const int32_t* __restrict__ kmaxv, int64_t j0, int nb) {
+    uint32_t mk = 0;
+    for (int jj = 0; jj < nb; ++jj) mk |= (kmaxv[j0 + jj] > 127 ? 1u : 0u) << jj;
+    return mk;
+}
+
+// Clients j0 .. j0+nb-1 in order when some client overflowed: an overflowed client adds
 // q[j][i] / n_div read from the dequantized batch (what K2 wrote correctly beside the
 // saturated codes; the same bits as its table entry would have had), the others their
 // table entries.  Any column alignment.
-__device__ __noinline__ void mean_add_mixed(float (&e)[kMeanCpt], const int8_t* __restrict__ codes,
+__device__ __forceinline__ void mean_add_mixed(float (&e)[kMeanCpt], const int8_t* __restrict__ codes,
                                             const float* __restrict__ q, int64_t ldq, const float (*tabn)[256],
                                             uint32_t ovf, int64_t j0, int nb, int64_t i0, int64_t d, float n_div) {
     for (int jj = 0; jj < nb; ++jj) {
@@ -1918,55 +1922,66 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
                   int64_t n, int64_t d, float fm, float n_div, int accumulate, float* __restrict__ est,
                   const float* __restrict__ q, int64_t ldq) {
     __shared__ float tabn[kMeanClients][256];     // indexed by the raw code byte, sign included
-    // overflowed clients of group g as a bit mask in s_ovf[g & 1] (only with q): group g's
-    // table build sets bits in s_ovf[g & 1] and clears s_ovf[(g + 1) & 1], which every
-    // thread last read before group g's first barrier
-    __shared__ uint32_t s_ovf[2];
+    __shared__ uint32_t s_ovf;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);
     const int64_t i0 = ((int64_t)blockIdx.x * kCodesMeanThreads + tid) * kMeanCpt;
     const bool full = ALL || (VEC && i0 + kMeanCpt <= d);
-    if (tid < 2) s_ovf[tid] = 0u;                   // ordered by the first group's barrier
     float e[kMeanCpt];
 #pragma unroll
     for (int k = 0; k < kMeanCpt; ++k) e[k] = (accumulate && i0 + k < d) ? est[i0 + k] : 0.0f;
+    // With q: does any client overflow its codes?  (n kmax words per workgroup, L2-served.)
+    // Then the whole launch takes the mixed loop below, which reads those clients from q;
+    // the common case keeps the straight-line loop untouched (no per-group test in it).
+    bool any = false;
+    if (q) {
+        if (tid == 0) s_ovf = 0u;
+        __syncthreads();
+        bool a = false;
+        for (int64_t j = tid; j < n; j += kCodesMeanThreads) a = a || kmaxv[j] > 127;
+        if (a) s_ovf = 1u;
+        __syncthreads();
+        any = s_ovf != 0u;
+    }
+    const int64_t groups = n / kMeanClients;
+    if (any) {
+        for (int64_t j0 = 0; j0 < n; j0 += kMeanClients) {
+            const int nb = (int)min((int64_t)kMeanClients, n - j0);
+            const uint32_t ovf = mean_ovf_mask(kmaxv, j0, nb);
+            __syncthreads();
+            mean_build_tables(tabn, l1, kmaxv, j0, nb, wid, lane, fm, n_div);
+            __syncthreads();
+            mean_add_mixed(e, codes, q, ldq, tabn, ovf, j0, nb, i0, d, n_div);
+        }
+    } else {
     // full groups of kMeanClients: straight-line, unconditional loads (the prefetch of the
     // group after the last one is clamped to a valid row and never used), so the waits
-    // before each batch cover that batch only.  A group with an overflowed client (and q
-    // given) takes mean_add_mixed instead of the batch adds (wave-uniform branch).
-    const int64_t groups = n / kMeanClients;
+    // before each batch cover that batch only
     const int8_t* cbase = codes + (full ? i0 : 0);
     uint2 wa[kMeanUnroll], wb[kMeanUnroll];
     if (VEC && groups > 0) mean_load_batch(wa, cbase, d);
     for (int64_t g = 0; g < groups; ++g) {
         const int64_t j0 = g * kMeanClients;
         __syncthreads();                            // previous group's tables no longer read
-        if (q && tid == 0) s_ovf[(g + 1) & 1] = 0u;
-        mean_build_tables(tabn, l1, kmaxv, j0, kMeanClients, wid, lane, fm, n_div, q ? &s_ovf[g & 1] : nullptr);
+        mean_build_tables(tabn, l1, kmaxv, j0, kMeanClients, wid, lane, fm, n_div);
         __syncthreads();
-        const uint32_t ovf = q ? s_ovf[g & 1] : 0u;
         if (VEC) {
             mean_load_batch(wb, cbase + (j0 + kMeanUnroll) * d, d);
-            if (full && !ovf) mean_add_batch(e, wa, tabn, 0);
+            if (full) mean_add_batch(e, wa, tabn, 0);
             const int64_t jn = (j0 + kMeanClients + kMeanUnroll <= n) ? j0 + kMeanClients : n - kMeanUnroll;
             mean_load_batch(wa, cbase + jn * d, d);
-            if (full && !ovf) mean_add_batch(e, wb, tabn, kMeanUnroll);
+            if (full) mean_add_batch(e, wb, tabn, kMeanUnroll);
         }
-        if (ovf) mean_add_mixed(e, codes, q, ldq, tabn, ovf, j0, kMeanClients, i0, d, n_div);
-        else if (!full) mean_add_bytes(e, codes, tabn, j0, kMeanClients, i0, d);
+        if (!full) mean_add_bytes(e, codes, tabn, j0, kMeanClients, i0, d);
     }
     const int64_t jr = groups * kMeanClients;
     const int nr = (int)(n - jr);
     if (nr > 0) {                                   // the last n % kMeanClients clients
         __syncthreads();
-        if (q && tid == 0) s_ovf[(groups + 1) & 1] = 0u;
-        mean_build_tables(tabn, l1, kmaxv, jr, nr, wid, lane, fm, n_div, q ? &s_ovf[groups & 1] : nullptr);
+        mean_build_tables(tabn, l1, kmaxv, jr, nr, wid, lane, fm, n_div);
         __syncthreads();
-        const uint32_t ovf = q ? s_ovf[groups & 1] : 0u;
-        if (ovf) {
-            mean_add_mixed(e, codes, q, ldq, tabn, ovf, jr, nr, i0, d, n_div);
-        } else if (full) {
+        if (full) {
             for (int jj = 0; jj < nr; ++jj) {
                 const uint2 w = *reinterpret_cast<const uint2*>(codes + (jr + jj) * d + i0);
 #pragma unroll
@@ -1977,6 +1992,7 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
         } else {
             mean_add_bytes(e, codes, tabn, jr, nr, i0, d);
         }
+    }
     }
     if (full) {
         *reinterpret_cast<float4*>(est + i0) = make_float4(e[0], e[1], e[2], e[3]);

@@ -62,12 +62,12 @@ def draw_vectors(dist: str, n: int, dim: int, rs=np.random):
 
 def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_instances: int = 50,
                     num_trials: int = 50, rates=(1, 2), seed: int = 42, torch_threads: int = 1,
-                    device=None, schemes=("unbiased",)):
+                    device=None, schemes=("unbiased",), progress=None):
     """NMSE curves of the selected schemes with the reference's normalisation.
 
     Returns {rate: {...}} for the default unbiased-only run, else {(scheme, rate): {...}};
     each value holds "script" ([len(users), num_instances]), "avg", "max", "standard_avg",
-    "standard_max"."""
+    "standard_max".  `progress(n, inst)` is called after each instance (long runs)."""
     device = device or torch.device("cuda", torch.cuda.current_device())
     schemes = tuple(schemes)
     for sc in schemes:
@@ -102,6 +102,8 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                     q = eden_quantize(xd, r, seeds=draws[(sc, r)])
                 est = client_mean(q, n).cpu()
                 script[(sc, r)][ui, inst] = float(torch.norm(est - emp).pow(2) / (num_trials * vns * n))   # ND:155
+            if progress is not None:
+                progress(n, inst)
     out = {}
     for k in keys:
         sv = script[k].astype(np.float32)             # the reference stores NMSE in f32 tensors
