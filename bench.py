@@ -366,7 +366,8 @@ def time_codec(uqdme, pipe, steps):
     P = lambda t: t.data_ptr()  # noqa: E731
     enc = lambda: _lib.check(lib.uq_tc_encode(P(pipe.codes), P(pipe.l1), n, d, pipe.m, 0, P(data), data.numel(),  # noqa: E731
                                               P(off), P(ws), ws.numel(), sp), "encode")
-    dec = lambda: _lib.check(lib.uq_tc_decode(P(data), P(off), n, d, P(codes), P(l1), P(km), P(status), sp),  # noqa: E731
+    dec = lambda: _lib.check(lib.uq_tc_decode(P(data), data.numel(), P(off), n, d, pipe.m, P(codes), P(l1), P(km),  # noqa: E731
+                                              P(status), sp),
                              "decode")
     res = {}
     for name, f in (("encode", enc), ("decode", dec)):

@@ -137,16 +137,18 @@ int uq_codes_q_mean_f32(const int8_t* codes, const float* q, int64_t ldq, const 
  * uq_tc_encode: codes [n][d] int8, l1 [n] f32 (device) -> messages packed back to back in
  *   msgs (device, msgs_bytes >= n * bound), offsets [n+1] u64 (device): client j's message is
  *   msgs[offsets[j] .. offsets[j+1]).  Workspace: uq_tc_workspace_bytes (no zero-fill needed).
- * uq_tc_decode: messages (device, offsets [n+1]) -> codes [n][d], l1 [n], kmax [n]; status [n]
- *   int32 (device) is 0 for a well-formed message, else bit 0 bad header / d mismatch, bit 1
- *   bad frequency table, bit 2 word stream overrun or underrun, bit 3 wrong final state. */
+ * uq_tc_decode: messages (device buffer of msgs_bytes, offsets [n+1]) -> codes [n][d], l1 [n],
+ *   kmax [n]; status [n] int32 (device) is 0 for a well-formed message, else bit 0 bad header,
+ *   d mismatch or offsets outside [0, msgs_bytes] / not increasing / unaligned (nothing is read
+ *   outside the buffer), bit 1 bad frequency table, bit 2 word stream overrun or underrun,
+ *   bit 3 wrong final state, bit 4 the header's m differs from `m` (m < 0: any m). */
 #define UQ_TC_EXACT_ZERO_SIGNS 1
 int uq_tc_bound(int64_t d, size_t* bytes_out);
 int uq_tc_workspace_bytes(int64_t n, int64_t d, size_t* bytes_out);
 int uq_tc_encode(const int8_t* codes, const float* l1, int64_t n, int64_t d, int64_t m, int32_t flags,
                  uint8_t* msgs, size_t msgs_bytes, uint64_t* offsets, void* ws, size_t ws_bytes, void* stream);
-int uq_tc_decode(const uint8_t* msgs, const uint64_t* offsets, int64_t n, int64_t d, int8_t* codes, float* l1,
-                 int32_t* kmax, int32_t* status, void* stream);
+int uq_tc_decode(const uint8_t* msgs, size_t msgs_bytes, const uint64_t* offsets, int64_t n, int64_t d, int64_t m,
+                 int8_t* codes, float* l1, int32_t* kmax, int32_t* status, void* stream);
 
 /* ---- biased type quantizer (Reznik rounding) ------------------------------------------
  * NMSE_Results/Codes/All_Schemes.py:669-687 Type_biased_quantize and :644-666 Reznik for

@@ -101,3 +101,64 @@ def test_empty_vectors_header_only(gpu_ready):
     back = uqdme.decode_messages(msgs)
     assert back.codes.shape == (n, 0)
     assert torch.equal(back.l1, tc.l1)
+
+
+def test_offsets_bounds_and_m_checked_on_device(gpu_ready):
+    """uq_tc_decode reads nothing outside [msgs, msgs + msgs_bytes) -- offsets past
+    the buffer, decreasing or unaligned are status bit 0 -- and a header whose m differs
+    from the batch's expected m is status bit 4; the well-formed messages beside them still
+    decode.  TypeMessages.from_messages refuses a batch mixing m values on the host."""
+    import uqdme
+    from uqdme_amd import _lib
+    lib = _lib.load()
+    n, d = 4, 30000
+    x, X = _batch(n, d, "normal", 6)
+    tc = uqdme.quantize_encode(torch.from_numpy(x).cuda(), 1, X=X, torch_threads=1)
+    msgs = uqdme.encode_messages(tc)
+    off = msgs.offsets.clone()
+    sp = torch.cuda.current_stream().cuda_stream
+
+    def dec(data, offs, m):
+        codes = torch.zeros((n, d), dtype=torch.int8, device="cuda")
+        l1 = torch.zeros(n, device="cuda")
+        km = torch.zeros(n, dtype=torch.int32, device="cuda")
+        st = torch.zeros(n, dtype=torch.int32, device="cuda")
+        _lib.check(lib.uq_tc_decode(data.data_ptr(), data.numel(), offs.data_ptr(), n, d, m, codes.data_ptr(),
+                                    l1.data_ptr(), km.data_ptr(), st.data_ptr(), sp), "decode")
+        torch.cuda.synchronize()
+        return codes, st.cpu().tolist()
+
+    want = torch.where(tc.codes == -1, torch.zeros_like(tc.codes), tc.codes)   # value mode: no zero signs
+    codes, st = dec(msgs.data, off, tc.m)
+    assert st == [0] * n and torch.equal(codes, want)
+    codes, st = dec(msgs.data[:int(off[2])], off, tc.m)             # buffer ends inside message 2
+    assert st[:2] == [0, 0] and st[2] & 1 and st[3] & 1 and torch.equal(codes[:2], want[:2])
+    o2 = off.clone()
+    o2[3] = 1 << 40                                                  # far outside, and decreasing after it
+    codes, st = dec(msgs.data, o2, tc.m)
+    assert st[0] == st[1] == 0 and st[2] & 1 and st[3] & 1
+    o3 = off.clone()
+    o3[1] += 2                                                       # unaligned start
+    _, st = dec(msgs.data, o3, tc.m)
+    assert st[1] & 1
+    _, st = dec(msgs.data, off, tc.m + 1)                            # another m than the batch's
+    assert all(s & 16 for s in st)
+    other = uqdme.encode_messages(uqdme.quantize_encode(torch.from_numpy(x).cuda(), 2, X=X, torch_threads=1))
+    with pytest.raises(ValueError):
+        uqdme.TypeMessages.from_messages(msgs.messages()[:2] + other.messages()[2:], d)
+
+
+def test_chunked_encode_matches_one_shot(gpu_ready):
+    """encode_messages through a small staging buffer (client chunks) returns exactly the
+    one-shot messages, in a buffer of exactly their size."""
+    import uqdme
+    n, d = 7, 20000
+    x, X = _batch(n, d, "laplace", 8)
+    tc = uqdme.quantize_encode(torch.from_numpy(x).cuda(), 1, X=X, torch_threads=1)
+    one = uqdme.encode_messages(tc)
+    bound = one.data.numel() // n
+    chunked = uqdme.encode_messages(tc, staging_bytes=3 * bound)          # chunks of 3, 3, 1 clients
+    assert chunked.messages() == one.messages()
+    assert chunked.data.numel() == chunked.total_bytes() == one.total_bytes()
+    back = uqdme.decode_messages(chunked)
+    assert torch.equal(back.codes, torch.where(tc.codes == -1, torch.zeros_like(tc.codes), tc.codes))

@@ -42,7 +42,7 @@ def main():
     P = lambda t: t.data_ptr()  # noqa: E731
     enc = lambda: _lib.check(lib.uq_tc_encode(P(tc.codes), P(tc.l1), n, d, tc.m, 0, P(data), data.numel(), P(off),  # noqa: E731
                                               P(ws), ws.numel(), sp), "encode")
-    dec = lambda: _lib.check(lib.uq_tc_decode(P(data), P(off), n, d, P(codes), P(l1), P(km), P(status), sp), "decode")  # noqa: E731
+    dec = lambda: _lib.check(lib.uq_tc_decode(P(data), data.numel(), P(off), n, d, tc.m, P(codes), P(l1), P(km), P(status), sp), "decode")  # noqa: E731
     res = {"clients": n, "d": d, "bits": a.bits}
     for name, f in (("encode", enc), ("decode", dec)):
         f()

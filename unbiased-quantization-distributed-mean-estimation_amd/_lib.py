@@ -46,7 +46,7 @@ SIGNATURES = {
     "uq_tc_bound": (ctypes.c_int, [_i64, ctypes.POINTER(_sz)]),
     "uq_tc_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
     "uq_tc_encode": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _i32, _p, _sz, _p, _p, _sz, _p]),
-    "uq_tc_decode": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _p, _p, _p, _p]),
+    "uq_tc_decode": (ctypes.c_int, [_p, _sz, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p]),
 }
 
 

@@ -117,14 +117,26 @@ class TypeMessages:
 
     @classmethod
     def from_messages(cls, msgs, d: int, device=None) -> "TypeMessages":
-        """Pack host messages (bytes) of one batch for decode_messages; m and the flags are
-        read from the first header (every message is checked by the decoder)."""
-        sizes = np.array([len(b) for b in msgs], np.int64)
+        """Pack host messages (bytes) of one batch for decode_messages.  Every header must
+        carry the same m and flags (one batch is decoded and averaged with one m; ValueError
+        otherwise); the decoder then checks each message in full, and flags (status bit 4) any
+        whose m differs from the batch's."""
+        for j, b in enumerate(msgs):
+            if len(b) < 40 or b[:4] != b"UQR1":
+                raise ValueError(f"message {j} is not a UQR1 message")
+        ms = {struct.unpack_from("<Q", b, 16)[0] for b in msgs}
+        fl = {struct.unpack_from("<H", b, 6)[0] & 1 for b in msgs}
+        if len(ms) > 1 or len(fl) > 1:
+            raise ValueError(f"messages of one batch must share m and flags (m: {sorted(ms)[:4]}, flags: {sorted(fl)})")
+        # each message starts 4-byte aligned (the decoder reads 32-bit words); sizes are
+        # multiples of 4 by construction (tc_align4), others are padded here
+        sizes = np.array([(len(b) + 3) & ~3 for b in msgs], np.int64)
         off = np.zeros(len(msgs) + 1, np.int64)
         np.cumsum(sizes, out=off[1:])
-        buf = np.frombuffer(b"".join(msgs), np.uint8) if msgs else np.zeros(0, np.uint8)
-        m = struct.unpack_from("<Q", msgs[0], 16)[0] if msgs else 0
-        exact = bool(struct.unpack_from("<H", msgs[0], 6)[0] & 1) if msgs else False
+        buf = (np.frombuffer(b"".join(b + bytes(-len(b) % 4) for b in msgs), np.uint8) if msgs
+               else np.zeros(0, np.uint8))
+        m = ms.pop() if msgs else 0
+        exact = bool(fl.pop()) if msgs else False
         dev = device or "cuda"
         return cls(data=torch.from_numpy(buf.copy()).to(dev), offsets=torch.from_numpy(off).to(dev), n=len(msgs),
                    d=int(d), m=int(m), exact_zero_signs=exact)
@@ -140,8 +152,19 @@ def _tc_sizes(lib, n, d):
     return int(b.value), int(w.value)
 
 
-def encode_messages(tc: "TypeCodes", exact_zero_signs: bool = False) -> TypeMessages:
-    """Entropy-code a batch of type codes on the GPU (one UQR1 message per client)."""
+STAGING_BYTES = 256 << 20     # encode_messages: worst-case message bytes staged per client chunk
+
+
+def encode_messages(tc: "TypeCodes", exact_zero_signs: bool = False,
+                    staging_bytes: int = STAGING_BYTES) -> TypeMessages:
+    """Entropy-code a batch of type codes on the GPU (one UQR1 message per client).
+
+    The encoder writes into a buffer sized for the worst case (uq_tc_bound: ~2 B per
+    coordinate) with ~2 B per coordinate of workspace scratch, against ~R/8 B per coordinate
+    of actual message.  A batch whose worst case exceeds `staging_bytes` is encoded in client
+    chunks through one staging buffer and workspace of that size, each chunk's exact bytes
+    kept (one synchronisation per chunk): at 1024 x 2^20 the transient is ~0.5 GB instead of
+    ~4.3 GB, and the returned buffer holds exactly the messages."""
     from . import _lib
     from .quantizer import _device, _ptr, _stream_ptr
     dev = _device()
@@ -150,13 +173,35 @@ def encode_messages(tc: "TypeCodes", exact_zero_signs: bool = False) -> TypeMess
     l1 = tc.l1.to(device=dev, dtype=torch.float32).contiguous()
     n, d = codes.shape
     tc.check()
-    bound, wsb = _tc_sizes(lib, n, d)
-    data = torch.empty(max(1, n * bound), dtype=torch.uint8, device=dev)
-    offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    flags = 1 if exact_zero_signs else 0
+    bound, _ = _tc_sizes(lib, n, d)
+    chunk = n if n * bound <= staging_bytes else max(1, staging_bytes // max(1, bound))
+
+    def encode(j0, nj, data, offsets, ws):
+        _lib.check(lib.uq_tc_encode(_ptr(codes[j0:j0 + nj]), _ptr(l1[j0:j0 + nj]), nj, d, int(tc.m), flags,
+                                    _ptr(data), data.numel(), _ptr(offsets), _ptr(ws), ws.numel(), _stream_ptr(dev)),
+                   "uq_tc_encode")
+
+    if chunk >= n:
+        _, wsb = _tc_sizes(lib, n, d)
+        data = torch.empty(max(1, n * bound), dtype=torch.uint8, device=dev)
+        offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        encode(0, n, data, offsets, torch.empty(max(1, wsb), dtype=torch.uint8, device=dev))
+        return TypeMessages(data=data, offsets=offsets, n=n, d=d, m=int(tc.m), exact_zero_signs=bool(exact_zero_signs))
+    _, wsb = _tc_sizes(lib, chunk, d)
+    stage = torch.empty(chunk * bound, dtype=torch.uint8, device=dev)
+    soff = torch.empty(chunk + 1, dtype=torch.int64, device=dev)
     ws = torch.empty(max(1, wsb), dtype=torch.uint8, device=dev)
-    _lib.check(lib.uq_tc_encode(_ptr(codes), _ptr(l1), n, d, int(tc.m), 1 if exact_zero_signs else 0, _ptr(data),
-                                data.numel(), _ptr(offsets), _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_tc_encode")
-    return TypeMessages(data=data, offsets=offsets, n=n, d=d, m=int(tc.m), exact_zero_signs=bool(exact_zero_signs))
+    parts, offs, base = [], [torch.zeros(1, dtype=torch.int64, device=dev)], 0
+    for j0 in range(0, n, chunk):
+        nj = min(chunk, n - j0)
+        encode(j0, nj, stage, soff[:nj + 1], ws)
+        tot = int(soff[nj].item())
+        parts.append(stage[:tot].clone())
+        offs.append(soff[1:nj + 1] + base)
+        base += tot
+    return TypeMessages(data=torch.cat(parts), offsets=torch.cat(offs), n=n, d=d, m=int(tc.m),
+                        exact_zero_signs=bool(exact_zero_signs))
 
 
 def decode_messages(msgs: TypeMessages) -> "TypeCodes":
@@ -172,8 +217,8 @@ def decode_messages(msgs: TypeMessages) -> "TypeCodes":
     status = torch.empty(max(1, n), dtype=torch.int32, device=dev)
     data = msgs.data.to(dev)
     offsets = msgs.offsets.to(dev)
-    _lib.check(lib.uq_tc_decode(_ptr(data), _ptr(offsets), n, d, _ptr(codes), _ptr(l1), _ptr(kmax), _ptr(status),
-                                _stream_ptr(dev)), "uq_tc_decode")
+    _lib.check(lib.uq_tc_decode(_ptr(data), data.numel(), _ptr(offsets), n, d, int(msgs.m), _ptr(codes), _ptr(l1),
+                                _ptr(kmax), _ptr(status), _stream_ptr(dev)), "uq_tc_decode")
     bad = int(torch.count_nonzero(status[:n]).item()) if n else 0
     if bad:
         raise ValueError(f"{bad} malformed UQR1 message(s) (status {status[:n].cpu().numpy().tolist()[:8]})")

@@ -768,6 +768,28 @@ rez_tie_list_kernel(const RezState* __restrict__ st, int64_t n, uint32_t* __rest
     if (tid == 0) list[0] = base;
 }
 
+// Defined fallback of a replay that failed its consistency checks (internal error,
+// reported through the status word): the client keeps kRezAmbiguous without kRezTorchTies,
+// so KB6 ranks its threshold ties in index order (the UQ_TIES_LOWEST_INDEX choice) from
+// per-tile tie counts -- which rez_tiecount_kernel skips for listed clients, so the
+// workgroup counts them here (a wave per 4096-tile).
+template <int NT>
+__device__ void tt_fallback_tilecounts(const float* __restrict__ xv, int64_t d, const DivPlan& dp, float fm, bool up,
+                                       uint32_t tau, uint32_t* __restrict__ trow, int32_t tiles) {
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    for (int32_t t = w; t < tiles; t += NT / kWave) {
+        const int64_t b = (int64_t)t * kSelTile, e = min(d, b + (int64_t)kSelTile);
+        uint32_t c = 0;
+        for (int64_t i = b + lane; i < e; i += kWave) {
+            float kp;
+            c += rez_elem(xv[i], dp, fm, up, kp) == tau ? 1u : 0u;
+        }
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, kWave);
+        if (lane == 0) trow[t] = c;
+    }
+}
+
 // NT threads per workgroup.  part 0: every listed client (slots walk the list).  With
 // KB7a's level state `tls`: part 1 finishes the clients KB7a resumed (slot a = list entry a,
 // LDS tails: NT = kTieThreadsLds), part 2 every other listed client.
@@ -776,8 +798,11 @@ __global__ void __launch_bounds__(NT)
 rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
                 RezState* __restrict__ st, uint32_t* __restrict__ tie_bits, uint32_t* __restrict__ qbuf,
                 uint32_t* __restrict__ pos, const uint32_t* __restrict__ list, uint32_t* __restrict__ ctrl,
-                const TieLevelState* __restrict__ tls, int part) {
+                const TieLevelState* __restrict__ tls, int part, uint32_t* __restrict__ tilecnt, int32_t tiles) {
     TT_DECL();
+    // ctrl[3] != 0 (tests only: the workspace's control block) forces every replay down the
+    // failure path below, so its fallback can be checked against the lowest-index rule
+    const bool force_fail = ctrl[3] != 0u;
     const int64_t dpad = (d + 3) & ~(int64_t)3;              // 16-byte aligned K and I rows
     const Queue A{qbuf + (size_t)blockIdx.x * 2 * dpad, qbuf + (size_t)blockIdx.x * 2 * dpad + dpad};
     uint32_t* Lpos = pos + (size_t)blockIdx.x * 2 * d;
@@ -855,6 +880,7 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
                                                   tls[li].depth);
             else ok = tt_introselect<NT>(A, Lpos, Rpos, d, k - 1, sh, lK, lI, lL, lR, 0, d, 2 * floor_log2_i64(d));
         }
+        ok = ok && !force_fail;
         uint32_t* bits = tie_bits + vec * ((d + 31) / 32);
         TT_T0();
         if (ok) {
@@ -882,13 +908,15 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         }
         __syncthreads();
         TT_ACC(6);
+        const bool good = __syncthreads_count(!(ok && sh.marked == s.need)) == 0;
         if (tid == 0) {
-            if (ok && sh.marked == s.need) {
+            if (good) {
                 st[vec].flags = s.flags | kRezTorchTies;
             } else {
                 __hip_atomic_store(ctrl + 2, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+        if (!good) tt_fallback_tilecounts<NT>(xv, d, dp, fm, up, s.prefix, tilecnt + vec * tiles, tiles);
         __syncthreads();
     }
 }

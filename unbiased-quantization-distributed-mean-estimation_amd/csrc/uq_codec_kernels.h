@@ -511,22 +511,34 @@ constexpr int kTcDecRing = 1024;            // ring words per wave
 constexpr int kTcDecFill = 256;             // words per refill (4 per lane)
 
 __global__ void __launch_bounds__(64 * kTcDecWaves)
-tc_decode_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offsets, int64_t d,
-                 int8_t* __restrict__ codes, float* __restrict__ l1, int32_t* __restrict__ kmax,
-                 int32_t* __restrict__ status) {
+tc_decode_kernel(const uint8_t* __restrict__ msgs, uint64_t msgs_bytes, const uint64_t* __restrict__ offsets,
+                 int64_t d, int64_t m_expect, int8_t* __restrict__ codes, float* __restrict__ l1,
+                 int32_t* __restrict__ kmax, int32_t* __restrict__ status) {
     __shared__ uint32_t tab[kTcM];
     __shared__ uint32_t sf[256], scum[257];
     __shared__ uint16_t ring[kTcDecWaves][kTcDecRing];
     __shared__ __attribute__((aligned(16))) uint8_t ob[kTcDecWaves][kTcBlk * 64];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t vec = blockIdx.y;
-    const uint8_t* msg = msgs + offsets[vec];
-    const uint64_t size = offsets[vec + 1] - offsets[vec];
+    // offsets come from the peer: nothing is read unless [o0, o1) lies inside the buffer
+    const uint64_t o0 = offsets[vec], o1 = offsets[vec + 1];
+    if (!(o0 <= o1 && o1 <= msgs_bytes && o1 - o0 >= 40 && (o0 & 3u) == 0u)) {
+        if (tid == 0 && blockIdx.x == 0) atomicOr(&status[vec], 1);
+        return;
+    }
+    const uint8_t* msg = msgs + o0;
+    const uint64_t size = o1 - o0;
     const uint32_t* h = reinterpret_cast<const uint32_t*>(msg);
+    // every header carries m (h[4..5]); a batch is decoded for one m (codes_mean / decode
+    // apply it), so a message of another m is flagged (bit 4) instead of mis-scaled
+    if (m_expect >= 0 && ((uint64_t)h[4] | ((uint64_t)h[5] << 32)) != (uint64_t)m_expect) {
+        if (tid == 0 && blockIdx.x == 0) atomicOr(&status[vec], 16);
+        return;
+    }
     const int W = tc_lanes(d);
     const int64_t nch = tc_nchunks(d);
     const int64_t c = (int64_t)blockIdx.x * kTcDecWaves + wv;
-    bool ok = size >= 40 && h[0] == kTcMagic && (h[1] & 0xFFFFu) == 1u &&
+    bool ok = h[0] == kTcMagic && (h[1] & 0xFFFFu) == 1u &&
               ((uint64_t)h[2] | ((uint64_t)h[3] << 32)) == (uint64_t)d && ((h[7] >> 16) & 0xFFu) == (uint32_t)kTcProbBits &&
               (int)(h[7] >> 24) == W && (int64_t)h[8] == nch && (uint64_t)h[9] == size;
     const int nsym = ok ? (int)(h[7] & 0xFFFFu) : 0;

@@ -2323,7 +2323,8 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     // drop-ins) replays in one kernel when it has to
     if (d <= kTieLevelMin || n < kTieLevelMinClients) {
         hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
-                           state, bits, qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)nullptr, 0);
+                           state, bits, qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)nullptr, 0,
+                           (uint32_t*)(wsb + w.tcnt_off), w.tiles);
         return hip_check(hipGetLastError(), "rez_ties_kernel launch");
     }
     // KB7a: introselect's levels over (segments x slots) workgroups, level by level, down to
@@ -2350,7 +2351,8 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     hipLaunchKernelGGL(kt_mark_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, d, qbuf, list, state, tls, bits);
     if ((rc = hip_check(hipGetLastError(), "kt_mark_kernel launch"))) return rc;
     hipLaunchKernelGGL(rez_ties_kernel<kTieThreadsLds>, dim3(S), dim3(kTieThreadsLds), 0, st, x, d, l1, fm, state, bits,
-                       qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)tls, 1);
+                       qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)tls, 1, (uint32_t*)(wsb + w.tcnt_off),
+                       w.tiles);
     *tls_out = tls;
     return hip_check(hipGetLastError(), "rez_ties_kernel launch");
 }
@@ -2359,7 +2361,8 @@ int launch_torch_ties_rest(const float* x, int64_t d, const float* l1, float fm,
                            char* wsb, const BiasedLayout& w, const TieLevelState* tls, hipStream_t st) {
     hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
                        state, bits, (uint32_t*)(wsb + w.pairs_off), (uint32_t*)(wsb + w.pos_off),
-                       (const uint32_t*)(wsb + w.list_off), (uint32_t*)wsb, tls, 2);
+                       (const uint32_t*)(wsb + w.list_off), (uint32_t*)wsb, tls, 2, (uint32_t*)(wsb + w.tcnt_off),
+                       w.tiles);
     return hip_check(hipGetLastError(), "rez_ties_kernel launch");
 }
 
@@ -2761,8 +2764,8 @@ int uq_tc_encode(const int8_t* codes, const float* l1, int64_t n, int64_t d, int
     return UQ_OK;
 }
 
-int uq_tc_decode(const uint8_t* msgs, const uint64_t* offsets, int64_t n, int64_t d, int8_t* codes, float* l1,
-                 int32_t* kmax, int32_t* status, void* stream) {
+int uq_tc_decode(const uint8_t* msgs, size_t msgs_bytes, const uint64_t* offsets, int64_t n, int64_t d, int64_t m,
+                 int8_t* codes, float* l1, int32_t* kmax, int32_t* status, void* stream) {
     if (n < 0 || d < 0 || d > ((int64_t)1 << 31)) return fail(UQ_E_INVALID, "bad n / d");
     if (n == 0) return UQ_OK;
     if (!msgs || !offsets || !l1 || !kmax || !status || (d > 0 && !codes)) return fail(UQ_E_INVALID, "null pointer");
@@ -2773,7 +2776,7 @@ int uq_tc_decode(const uint8_t* msgs, const uint64_t* offsets, int64_t n, int64_
     for (int64_t j0 = 0; j0 < n; j0 += kMaxGridY) {
         const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
         hipLaunchKernelGGL(tc_decode_kernel, dim3((unsigned)((nch + kTcDecWaves - 1) / kTcDecWaves), (unsigned)nj),
-                           dim3(64 * kTcDecWaves), 0, st, msgs, offsets + j0, d,
+                           dim3(64 * kTcDecWaves), 0, st, msgs, (uint64_t)msgs_bytes, offsets + j0, d, m,
                            codes ? codes + j0 * d : codes, l1 + j0, kmax + j0, status + j0);
         if ((rc = hip_check(hipGetLastError(), "tc_decode_kernel launch"))) return rc;
     }
