@@ -34,33 +34,40 @@ def test_pipeline_step_matches_batched_apis(gpu_ready, n, d, bits):
 
 def test_pipelines_agree_and_overflowed_client_falls_back_to_q(gpu_ready):
     """a client whose lattice counts overflow its int8 codes (one nonzero
-    coordinate: k = m there) -- the "codes" pipeline reads that client from q, so est is
-    still the client-ordered mean of q bit for bit (ND:137-138); "q" gives the same bits;
-    "encode" (no q to fall back to) raises from check_status."""
+    coordinate: k = m there; or, in a second batch, a NaN / inf coordinate, whose L1 is not
+    finite) -- the "codes" pipeline reads that client from q, so est is still the
+    client-ordered mean of q bit for bit (ND:137-138); "q" gives the same bits; "encode" (no
+    q to fall back to) raises from check_status."""
     import uqdme
     n, d, bits = 70, 8192, 1                       # 2 full 32-client groups + 6 in the tail
     g = torch.Generator(device="cuda").manual_seed(11)
-    x = torch.randn(n, d, generator=g, device="cuda")
+    x0 = torch.randn(n, d, generator=g, device="cuda")
     for j in (3, 40, 67):                          # one client in each group and in the tail
-        x[j].zero_()
-        x[j, 100 + j] = -2.5
+        x0[j].zero_()
+        x0[j, 100 + j] = -2.5
+    x1 = x0.clone()
+    x1[20, 7] = float("nan")
+    x1[50, 9] = float("inf")
     X = torch.rand(n, generator=torch.Generator().manual_seed(4)).cuda()
-    q_ref = uqdme.quantize_dequantize(x, bits, X=X, torch_threads=1)
-    est_ref = uqdme.client_mean(q_ref, float(n))
-    for pl in ("codes", "q"):
-        p = uqdme.DMEPipeline(n, d, bits, torch_threads=1, pipeline=pl)
-        est = p.step(x, X)
-        p.check_status()
-        assert torch.equal(p.q.view(torch.int32), q_ref.view(torch.int32)), pl
-        assert torch.equal(est.view(torch.int32), est_ref.view(torch.int32)), pl
-        if pl == "codes":
-            assert p.overflowed() == 3
-            assert int(p.kmax[3]) == 128 and int(p.kmax[0]) <= 127
-    p = uqdme.DMEPipeline(n, d, bits, torch_threads=1, pipeline="encode")
-    p.step(x, X)
-    with pytest.raises(OverflowError):
-        p.check_status()
+    for x, novf in ((x0, 3), (x1, 5)):
+        q_ref = uqdme.quantize_dequantize(x, bits, X=X, torch_threads=1)
+        est_ref = uqdme.client_mean(q_ref, float(n))
+        for pl in ("codes", "q"):
+            p = uqdme.DMEPipeline(n, d, bits, torch_threads=1, pipeline=pl)
+            est = p.step(x, X)
+            p.check_status()
+            assert torch.equal(p.q.view(torch.int32), q_ref.view(torch.int32)), pl
+            assert torch.equal(est.view(torch.int32), est_ref.view(torch.int32)), pl
+            if pl == "codes":
+                assert p.overflowed() == novf
+                assert int(p.kmax[3]) == 128 and int(p.kmax[0]) <= 127
+        p = uqdme.DMEPipeline(n, d, bits, torch_threads=1, pipeline="encode")
+        p.step(x, X)
+        with pytest.raises(OverflowError):
+            p.check_status()
     # accumulate continues the sum bit-for-bit from a previous est
+    x = x0
+    q_ref = uqdme.quantize_dequantize(x, bits, X=X, torch_threads=1)
     p = uqdme.DMEPipeline(n, d, bits, torch_threads=1)
     e1 = p.step(x, X, n_div=float(2 * n)).clone()
     e2 = p.step(x, X, n_div=float(2 * n), accumulate=True, est=e1)

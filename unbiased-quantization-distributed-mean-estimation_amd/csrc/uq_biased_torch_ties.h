@@ -379,6 +379,11 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
 // scans), so rez_ties_kernel resumes from the saved (first, last, depth) with the same
 // queue it would have built itself.  Slot a serves list entry a (a < kTieSlots).
 constexpr int64_t kTieLevelMin = kTieLdsPairs;   // shorter ranges finish in rez_ties_kernel's LDS
+// KB7a's levels stop at ranges of this length; the 256-thread replays beside KB6 (part 1)
+// take it from there (global-memory levels, then the LDS tail): 3 fewer levels of five
+// dependent launches each at d = 2^20, 5.28-5.34 -> 5.16-5.24 ms per torch-tie batch (two
+// boxes, bit-identical; stopping at 65536 gained nothing: profiles/r3f_exp_biased_levels.jsonl)
+constexpr int64_t kTieLevelStop = 16384;
 constexpr int64_t kTieLevelMinClients = 32;      // KB7a for batches of at least this many clients
 constexpr uint32_t kTieManyClients = 128;          // this many listed clients: levels only down to
 constexpr int64_t kTieLevelMinMany = 65536;        //   this range (tie-heavy batches)
@@ -454,7 +459,7 @@ kt_pivot_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restri
         TieLevelState& t = tls[a];
         // with many listed clients the 1024-thread replays fill the GPU by themselves: the
         // levels stop at kTieLevelMinMany and part 2 finishes those slots
-        const int64_t stop = list[0] >= kTieManyClients ? kTieLevelMinMany : kTieLevelMin;
+        const int64_t stop = list[0] >= kTieManyClients ? kTieLevelMinMany : kTieLevelStop;
         act = a < (int)list[0] && t.filled && !t.err && t.depth > 0 && t.last - t.first > stop;
         t.active = act ? 1 : 0;
         if (act) {
@@ -826,7 +831,7 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         const bool resumed = tls && li == blockIdx.x && tls[li].filled;
         // part 1: resumed slots whose range fits the LDS tail; part 2: everything else
         // (resumed slots KB7a left longer resume from their saved state in 1024 threads)
-        const bool tail = resumed && (tls[li].err || tls[li].last - tls[li].first <= kTieLdsPairs);
+        const bool tail = resumed && (tls[li].err || tls[li].last - tls[li].first <= kTieLevelStop);
         if ((part == 1 && !tail) || (part == 2 && tail)) continue;
         // queue[j] = (value, j) (TopKImpl.h); 4 coordinates per lane and load
         const bool xv4 = ((uintptr_t)xv & 15u) == 0;

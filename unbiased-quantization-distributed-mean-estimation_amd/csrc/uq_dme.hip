@@ -2338,7 +2338,7 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     // after ~8 levels from 2^20), so enough levels for 0.6 per level, plus two; an idle level
     // costs five ~5 us launches, and a range still longer goes global in rez_ties_kernel
     int levels = 2;
-    for (double r = (double)d; r > (double)kTieLevelMin; r *= 0.6) ++levels;
+    for (double r = (double)d; r > (double)kTieLevelStop; r *= 0.6) ++levels;
     uint32_t* alist = (uint32_t*)(wsb + w.alist_off);
     for (int lv = 0; lv < levels; ++lv) {
         hipLaunchKernelGGL(kt_pivot_kernel, dim3(1), dim3(kTieSlots), 0, st, d, qbuf, list, tls, (int)S, alist);
