@@ -85,3 +85,66 @@ def test_reduce_mean_matches_within_f32_rounding():
     got = run(2, n_total, d, "reduce")
     ref = reference(n_total, d)
     np.testing.assert_allclose(got, ref, rtol=0, atol=8 * np.finfo(np.float32).eps * np.abs(ref).max())
+
+
+class CpuPipe:
+    """torch-CPU stand-in for DMEPipeline (test infrastructure): q = a fixed function of x
+    (the quantizer is not what these tests check), est (+)= q[j] / n_div in client order."""
+
+    def __init__(self, n, d):
+        self.q = torch.zeros(n, d)
+        self.est = torch.zeros(d)
+        self.fold = cpu_fold
+
+    def step(self, x, X, n_div, accumulate=False, *, est=None, events=None, pipeline=None):
+        self.q.copy_(torch.round(x * 4) / 4 + X[:, None])
+        out = self.est if est is None else est
+        out.copy_(cpu_fold(self.q, n_div, None))
+        return out
+
+    def probe_outputs(self, *a, **k):
+        return None
+
+    def check_status(self):
+        pass
+
+
+def _sharded_dme_worker(rank, world, port, n_total, d, mode, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from uqdme_amd.distributed import ShardedDME
+        lo, hi = shard_range(n_total, world, rank)
+        sh = ShardedDME(hi - lo, d, n_total, mode=mode, pipe=CpuPipe(hi - lo, d), block=64)
+        assert not sh.overlap and sh.world == world
+        for k in range(3):                                   # three rounds, new clients each
+            g = torch.Generator().manual_seed(100 + k)
+            x = torch.randn(n_total, d, generator=g)
+            X = torch.rand(n_total, generator=g)
+            est = sh.step(x[lo:hi].contiguous(), X[lo:hi].contiguous())
+            sh.drain()
+            if rank == 0:
+                np.save(os.path.join(outdir, f"est_{k}.npy"), est.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mode", [(2, "reduce"), (2, "ordered"), (3, "ordered")])
+def test_sharded_dme_protocol_multi_rank(world, mode):
+    """ShardedDME (the object bench.py --gpus N drives) at world 2-3 over gloo on CPU: each
+    rank folds its contiguous client block, then one reduce (f32 re-association only) or the
+    ordered chain (bit-identical to the sequential client-ordered mean), over three steps."""
+    n_total, d = 11, 300
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_sharded_dme_worker, args=(world, free_port(), n_total, d, mode, td), nprocs=world, join=True)
+        for k in range(3):
+            got = np.load(os.path.join(td, f"est_{k}.npy"))
+            g = torch.Generator().manual_seed(100 + k)
+            x = torch.randn(n_total, d, generator=g)
+            X = torch.rand(n_total, generator=g)
+            ref = cpu_fold(torch.round(x * 4) / 4 + X[:, None], float(n_total), None).numpy()
+            if mode == "ordered":
+                assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+            else:
+                np.testing.assert_allclose(got, ref, rtol=0, atol=8 * np.finfo(np.float32).eps * np.abs(ref).max())

@@ -138,18 +138,23 @@ class ShardedDME:
                       `dst` after the next-but-one step or drain().
       mode "ordered": the bit-exact chain of sharded_client_mean over q's column blocks
                       (pipeline must write q).
-    With gloo (CPU tests, ranks sharing one GPU) the reduce is host-staged and synchronous."""
+    With gloo (CPU tests, ranks sharing one GPU) the reduce is host-staged and synchronous.
+    `pipe` replaces the HIP pipeline by any object with its interface (est, q, step(x, X,
+    n_div, est=, events=, pipeline=), probe_outputs, check_status): the CPU multi-process
+    tests run this protocol with a torch-CPU stand-in."""
 
     def __init__(self, n_local: int, d: int, n_total: int, bits_per_dimension=1, *, m: int | None = None,
                  torch_threads: int = 1, pipeline: str = "codes", mode: str = "reduce", dst: int = 0, group=None,
-                 overlap: Optional[bool] = None, block: int = 1 << 18, device=None):
-        from .pipeline import DMEPipeline
+                 overlap: Optional[bool] = None, block: int = 1 << 18, device=None, pipe=None):
         if mode not in ("reduce", "ordered"):
             raise ValueError("mode must be 'reduce' or 'ordered'")
         if mode == "ordered" and pipeline == "encode":
             raise ValueError("mode 'ordered' folds q: use pipeline 'codes' or 'q'")
-        self.pipe = DMEPipeline(n_local, d, bits_per_dimension, m=m, torch_threads=torch_threads, pipeline=pipeline,
-                                device=device)
+        if pipe is None:
+            from .pipeline import DMEPipeline
+            pipe = DMEPipeline(n_local, d, bits_per_dimension, m=m, torch_threads=torch_threads, pipeline=pipeline,
+                               device=device)
+        self.pipe = pipe
         self.n_total, self.mode, self.dst, self.group, self.block = int(n_total), mode, int(dst), group, int(block)
         self.dist_on = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if self.dist_on else 1
@@ -159,6 +164,7 @@ class ShardedDME:
         if self.overlap and not (rccl and mode == "reduce"):
             raise ValueError("overlap needs the RCCL (nccl) backend and mode 'reduce'")
         self.est_bufs = [self.pipe.est, torch.empty_like(self.pipe.est)] if self.overlap else [self.pipe.est]
+        self.fold = getattr(pipe, "fold", None)          # ordered chain's per-rank fold (default: HIP)
         self.pending = [None] * len(self.est_bufs)
         self.nstep = 0
 
@@ -185,7 +191,7 @@ class ShardedDME:
                     _reduce(est, self.dst, self.group)
             else:
                 est = sharded_client_mean(self.pipe.q, float(self.n_total), mode="ordered", dst=self.dst,
-                                          block=self.block, group=self.group)
+                                          block=self.block, group=self.group, fold=self.fold)
         if ev[4] is not None:
             ev[4].record()
         return est if (self.rank == self.dst or self.mode == "reduce") else None
