@@ -1240,6 +1240,23 @@ __device__ __forceinline__ void publish_kmax(float kmaxf, float L, int32_t* kmax
     for (int o = kWave / 2; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o, kWave));
     if ((tid & (kWave - 1)) == 0) atomicMax(&kmaxv[vec], kmax);
 }
+// The whole client in this workgroup (the stream form with nseg == 1): the block's max is
+// the client's, stored plainly -- kmax needs no zero-fill before the launch (one memset per
+// call less: ~5 us of the bench step).  s_red: kQBlock / kWave ints of LDS.
+__device__ __forceinline__ void store_kmax_block(float kmaxf, float L, int32_t* kmaxv, int64_t vec, int tid,
+                                                 int* s_red) {
+    int kmax = (kmaxf <= 127.0f && isfinite(L)) ? (int)kmaxf : 128;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o, kWave));
+    if ((tid & (kWave - 1)) == 0) s_red[tid / kWave] = kmax;
+    __syncthreads();
+    if (tid == 0) {
+        int m = s_red[0];
+#pragma unroll
+        for (int w = 1; w < kQBlock / kWave; ++w) m = max(m, s_red[w]);
+        kmaxv[vec] = m;
+    }
+}
 
 template <bool VEC4>
 __device__ __forceinline__ void store_tile(const float* s_data, float* __restrict__ ot, int len, int tid) {
@@ -1326,7 +1343,10 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);
     if (WC) {
         store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
-        publish_kmax(kmax, L, overflow, vec, tid);
+        if (nseg == 1)
+            store_kmax_block(kmax, L, overflow, vec, tid, reinterpret_cast<int*>(sl.wave));
+        else
+            publish_kmax(kmax, L, overflow, vec, tid);
     }
 }
 
@@ -2444,17 +2464,18 @@ int unbiased_codes_impl(const float* x, float* out, int8_t* codes, int32_t* over
         rc = hip_check(hipMemcpyAsync(l1_out, l1use, n * sizeof(float), hipMemcpyDeviceToDevice, st), "copy l1");
         if (rc) return rc;
     }
-    if (codes) {
+    // rows are 16-byte aligned when d % 4 == 0, or when there is only one row
+    const bool vec4 = aligned16(x) && (!out || aligned16(out)) && (d % 4 == 0 || n == 1);
+    const bool stream_form = n >= kStreamMinClients && vec4 && d <= ((int64_t)1 << 29);
+    if (codes && !stream_form) {          // the stream form stores each client's kmax itself
         rc = hip_check(hipMemsetAsync(overflow, 0, n * sizeof(int32_t), st), "memset kmax");
         if (rc) return rc;
     }
     const float fm = (float)m;   // torch casts the Python int to f32 for `m * p` and `/ m`
-    // rows are 16-byte aligned when d % 4 == 0, or when there is only one row
-    const bool vec4 = aligned16(x) && (!out || aligned16(out)) && (d % 4 == 0 || n == 1);
     const bool cvec = !codes || (aligned16(codes) && d % 16 == 0);
     const int wq = out ? 1 : 0, wc = codes ? 1 : 0;
     const int sel = (vec4 ? 8 : 0) | (wq ? 4 : 0) | (wc ? 2 : 0) | (cvec ? 1 : 0);
-    if (n >= kStreamMinClients && vec4 && d <= ((int64_t)1 << 29)) {
+    if (stream_form) {
         // enough clients to fill the GPU: one workgroup per client vector
 #define UQ_STREAM(Q, C, CV)                                                                                 \
     case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
