@@ -70,6 +70,7 @@ class DMEPipeline:
         self.q, self.codes = self._alloc_outputs()
         self.probe_report = None
         self._codes_valid = False       # the last K2 launch wrote codes (and kmax)
+        self._mean_without_q = False    # the last mean read codes with no q to fall back to
 
     @property
     def write_q(self) -> bool:
@@ -108,10 +109,12 @@ class DMEPipeline:
         pl = pipeline or self.pipeline
         est = self.est if est is None else est
         if pl == "q":
+            self._mean_without_q = False
             _lib.check(self.lib.uq_client_mean_f32(_p(self.q), self.n, self.d, self.d, float(n_div),
                                                    int(bool(accumulate)), _p(est), self._stream()), "uq_client_mean_f32")
         else:
             q = self.q if pl == "codes" else None
+            self._mean_without_q = q is None
             _lib.check(self.lib.uq_codes_q_mean_f32(_p(self.codes), _p(q), self.d, _p(self.l1), _p(self.kmax), self.n,
                                                     self.d, self.m, float(n_div), int(bool(accumulate)), _p(est),
                                                     self._stream()), "uq_codes_q_mean_f32")
@@ -206,9 +209,10 @@ class DMEPipeline:
         return int(torch.count_nonzero(self.kmax > 127).item())
 
     def check_status(self):
-        """Synchronise; raise if an in-kernel wait timed out, or (pipeline "encode") if a
-        client's codes overflowed, since its est contribution is then wrong."""
+        """Synchronise; raise if an in-kernel wait timed out, or if the last mean was taken
+        from codes alone (pipeline "encode", or a step overridden to it) while a client's
+        codes overflowed, since its est contribution is then wrong."""
         _lib.check(self.lib.uq_check_status(_p(self.ws), self._stream()), "uq_check_status")
-        if self.pipeline == "encode" and self.overflowed():
+        if self._mean_without_q and self.overflowed():
             raise OverflowError("type codes overflowed (lattice counts > 127) in an encode-only step: "
                                 "est is wrong for those clients; use pipeline='codes' (falls back to q)")
