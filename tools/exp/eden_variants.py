@@ -33,7 +33,7 @@ first = next(iter(libs.values()))[0]
 if first.uq_rht_signs(seeds.data_ptr(), 1, d, signs.data_ptr(), sp) != 0:
     raise RuntimeError("rht signs failed")
 ref = None
-for rep in range(3):
+for rep in range(int(os.environ.get("REPS", 3))):
     for name, (L, ws, nb) in libs.items():
         fn = lambda: L.uq_eden_f32(x.data_ptr(), out.data_ptr(), n, d, 1, signs.data_ptr(), rows.data_ptr(),  # noqa: E731
                                    scale.data_ptr(), ws.data_ptr(), nb, sp)

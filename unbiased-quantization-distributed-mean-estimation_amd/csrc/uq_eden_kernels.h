@@ -408,7 +408,7 @@ fwht_high256_kernel(FwhtArgs a, int lo) {
 // triple-buffered LDS image laid out [client][l][i], so a chain lane reads 4 consecutive
 // steps with one ds_read_b128.
 constexpr int kNormClients = 4;
-constexpr int kNormChunk = 1024;                    // floats per client per chunk
+constexpr int kNormChunk = 2048;                    // floats per client per chunk (1024: EDEN batch +0.05 ms, 512: +0.4 ms; profiles/r3j_exp_eden_norm_chunk.jsonl)
 constexpr int kNormRow = kNormChunk / 8 + 4;        // one torch lane's 128 steps (+4 pad)
 constexpr int kNormClientStride = 8 * kNormRow;
 constexpr int kNormBuf = kNormClients * kNormClientStride;
