@@ -130,12 +130,14 @@ def _sharded_dme_worker(rank, world, port, n_total, d, mode, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "reduce"), (2, "ordered"), (3, "ordered")])
-def test_sharded_dme_protocol_multi_rank(world, mode):
+@pytest.mark.parametrize("world,mode,n_total", [(2, "reduce", 11), (2, "ordered", 11), (3, "ordered", 11),
+                                                (3, "reduce", 2), (3, "ordered", 2)])
+def test_sharded_dme_protocol_multi_rank(world, mode, n_total):
     """ShardedDME (the object bench.py --gpus N drives) at world 2-3 over gloo on CPU: each
     rank folds its contiguous client block, then one reduce (f32 re-association only) or the
-    ordered chain (bit-identical to the sequential client-ordered mean), over three steps."""
-    n_total, d = 11, 300
+    ordered chain (bit-identical to the sequential client-ordered mean), over three steps;
+    with fewer clients than ranks a rank holds none."""
+    d = 300
     with tempfile.TemporaryDirectory() as td:
         mp.spawn(_sharded_dme_worker, args=(world, free_port(), n_total, d, mode, td), nprocs=world, join=True)
         for k in range(3):

@@ -90,3 +90,17 @@ def test_vector_entry_x_by_value_matches_batched(gpu_ready, d):
         X = torch.rand(1)
         ref = uqdme.quantize_dequantize(v.view(1, d), X=X, m=uqdme.rate_to_m(1, d)).view(d)
         assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), (d, rep)
+
+
+def test_empty_batch_pipeline(gpu_ready):
+    """A rank with no clients (more ranks than clients): every launch is a no-op and the
+    mean is zeros, so its reduce contributes nothing."""
+    import uqdme
+    p = uqdme.DMEPipeline(0, 4096, 1, torch_threads=1)
+    x = torch.empty((0, 4096), device="cuda")
+    X = torch.empty(0, device="cuda")
+    for pl in ("codes", "q", "encode"):
+        est = p.step(x, X, n_div=5.0, pipeline=pl)
+        torch.cuda.synchronize()
+        p.check_status()
+        assert torch.count_nonzero(est) == 0, pl
