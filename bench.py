@@ -358,13 +358,14 @@ def time_codec(uqdme, pipe, steps):
     data = torch.empty(n * b.value, dtype=torch.uint8, device="cuda")
     off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     ws = torch.empty(w.value, dtype=torch.uint8, device="cuda")
-    codes = torch.empty_like(pipe.codes)
+    src = pipe.codes.contiguous()      # the pipeline's rows are pitched; the codec takes dense [n, d]
+    codes = torch.empty_like(src)
     l1 = torch.empty_like(pipe.l1)
     km = torch.empty_like(pipe.kmax)
     status = torch.empty(n, dtype=torch.int32, device="cuda")
     sp = torch.cuda.current_stream().cuda_stream
     P = lambda t: t.data_ptr()  # noqa: E731
-    enc = lambda: _lib.check(lib.uq_tc_encode(P(pipe.codes), P(pipe.l1), n, d, pipe.m, 0, P(data), data.numel(),  # noqa: E731
+    enc = lambda: _lib.check(lib.uq_tc_encode(P(src), P(pipe.l1), n, d, pipe.m, 0, P(data), data.numel(),  # noqa: E731
                                               P(off), P(ws), ws.numel(), sp), "encode")
     dec = lambda: _lib.check(lib.uq_tc_decode(P(data), data.numel(), P(off), n, d, pipe.m, P(codes), P(l1), P(km),  # noqa: E731
                                               P(status), sp),
@@ -381,7 +382,7 @@ def time_codec(uqdme, pipe, steps):
         torch.cuda.synchronize()
         res[f"{name}_ms"] = round(e0.elapsed_time(e1) / steps, 4)
     total = int(off[n].item())
-    ok = bool(torch.equal(codes, torch.where(pipe.codes == -1, torch.zeros_like(pipe.codes), pipe.codes))
+    ok = bool(torch.equal(codes, torch.where(src == -1, torch.zeros_like(src), src))
               and int(torch.count_nonzero(status).item()) == 0)
     res.update({"bits_per_dim": round(8.0 * total / (n * d), 4), "bytes_per_client": round(total / n, 1),
                 "roundtrip_ok": ok, "what": "UQR1 rANS type messages (value mode) of the bench batch's codes, "

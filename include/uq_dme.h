@@ -103,6 +103,14 @@ int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_
                                float* l1_out, int32_t torch_threads, void* ws, size_t ws_bytes,
                                void* stream);
 
+/* As uq_type_unbiased_codes_f32 with row pitches: q row j at out + j*ldq (floats, ldq >= d),
+ * codes row j at codes + j*ldc (bytes, ldc >= d), e.g. rows of wider caller buffers.  Same
+ * bits as the dense call; nothing is written between rows. */
+int uq_type_unbiased_codes_ld_f32(const float* x, float* out, int64_t ldq, int8_t* codes, int64_t ldc,
+                                  int32_t* kmax, int64_t n, int64_t d, int64_t m, const float* X,
+                                  const float* l1, float* l1_out, int32_t torch_threads, void* ws,
+                                  size_t ws_bytes, void* stream);
+
 /* q[j][i] = decode(codes[j][i]; l1[j], m). */
 int uq_codes_decode_f32(const int8_t* codes, const float* l1, int64_t n, int64_t d, int64_t m,
                         float* out, void* stream);
@@ -121,6 +129,11 @@ int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax,
 int uq_codes_q_mean_f32(const int8_t* codes, const float* q, int64_t ldq, const float* l1, const int32_t* kmax,
                         int64_t n, int64_t d, int64_t m, float n_div, int32_t accumulate, float* est,
                         void* stream);
+
+/* As uq_codes_q_mean_f32 with the codes' row pitch: codes row j at codes + j*ldc (ldc >= d). */
+int uq_codes_q_mean_ld_f32(const int8_t* codes, int64_t ldc, const float* q, int64_t ldq, const float* l1,
+                           const int32_t* kmax, int64_t n, int64_t d, int64_t m, float n_div,
+                           int32_t accumulate, float* est, void* stream);
 
 /* ---- type messages "UQR1": entropy-coded type codes ---------------
  * The reference has no wire format (parity unpinned); its client output is AS:640's

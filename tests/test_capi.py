@@ -142,3 +142,23 @@ def test_round3_entry_points_argument_errors(lib):
     assert lib.uq_type_unbiased_vec_f32(None, None, 0, 0, 0.5, 1, None, 0, None) == 0      # d = 0: no-op
     assert lib.uq_type_unbiased_vec_f32(p, None, 10, 2, 0.5, 1, p, 1 << 20, None) == -1    # null out
     assert lib.uq_type_unbiased_vec_f32(p, p, 10, -2, 0.5, 1, p, 1 << 20, None) == -1      # m < 0
+
+
+def test_pitched_entry_points_argument_errors(lib):
+    """uq_type_unbiased_codes_ld_f32 / uq_codes_q_mean_ld_f32: row pitches below d are rejected
+    before anything is launched (n = 0 for the quantize call, so even a missing check would
+    launch nothing)."""
+    from uqdme_amd import _lib as L
+    for name in ("uq_type_unbiased_codes_ld_f32", "uq_codes_q_mean_ld_f32"):
+        res, args = L.SIGNATURES[name]
+        getattr(lib, name).restype = res
+        getattr(lib, name).argtypes = args
+    p = ctypes.c_void_p(16)
+    ws = ctypes.create_string_buffer(1 << 16)
+    wsp = ctypes.cast(ws, ctypes.c_void_p)
+    assert lib.uq_type_unbiased_codes_ld_f32(p, p, 9, p, 10, p, 0, 10, 5, p, None, None, 1, wsp, 1 << 16, None) == -1
+    assert b"pitch" in lib.uq_last_error()
+    assert lib.uq_type_unbiased_codes_ld_f32(p, p, 10, p, 9, p, 0, 10, 5, p, None, None, 1, wsp, 1 << 16, None) == -1
+    assert lib.uq_type_unbiased_codes_ld_f32(p, p, 10, p, 10, p, 0, 10, 5, p, None, None, 1, wsp, 1 << 16, None) == 0
+    assert lib.uq_codes_q_mean_ld_f32(p, 9, p, 10, p, p, 4, 10, 5, 4.0, 0, p, None) == -1       # ldc < d
+    assert b"ldc" in lib.uq_last_error()

@@ -1291,7 +1291,7 @@ __global__ void __launch_bounds__(kQBlock, 4)
 quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                        int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
                        const float* __restrict__ Xs, float Xval, const float* __restrict__ l1, int32_t seg_tiles,
-                       int32_t nseg, const uint64_t* __restrict__ pre) {
+                       int32_t nseg, const uint64_t* __restrict__ pre, int64_t ldo, int64_t ldc) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image of tile t (then scratch)
     __shared__ __attribute__((aligned(16))) float s_o[kQTile];     // output image of tile t-1 / t
     __shared__ float s_tab[kTab];
@@ -1305,8 +1305,8 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     const float Xv = Xs ? Xs[vec] : Xval;            // one vector per call: X passed by value
     const uint32_t row_bytes = (uint32_t)(d * 4);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, row_bytes);
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(WQ ? out + vec * d : x, row_bytes);
-    const __amdgpu_buffer_rsrc_t rc = make_rsrc(WC ? (const void*)(codes + vec * d) : (const void*)x, row_bytes / 4u);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(WQ ? out + vec * ldo : x, row_bytes);
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(WC ? (const void*)(codes + vec * ldc) : (const void*)x, row_bytes / 4u);
     TileRegs pre_x;
     load_tile_buf(pre_x, rx, (uint32_t)tb * (uint32_t)(kQTile * 4), tid);
     build_table(s_tab, tid, L, fm);
@@ -1319,7 +1319,7 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         if (tile > tb) {
             const uint32_t tp = (uint32_t)(tile - 1) * (uint32_t)kQTile;
             if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);      // beyond d: dropped by the range check
-            if (WC) store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
+            if (WC) store_codes_buf<CVEC>(rc, codes + vec * ldc, cw, tp, d, tid);
         }
         if (tile + 1 < te) load_tile_buf(pre_x, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
         const int64_t t0 = (int64_t)tile * kQTile;
@@ -1342,7 +1342,7 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     const uint32_t tp = (uint32_t)(te - 1) * (uint32_t)kQTile;
     if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);
     if (WC) {
-        store_codes_buf<CVEC>(rc, codes + vec * d, cw, tp, d, tid);
+        store_codes_buf<CVEC>(rc, codes + vec * ldc, cw, tp, d, tid);
         if (nseg == 1)
             store_kmax_block(kmax, L, overflow, vec, tid, reinterpret_cast<int*>(sl.wave));
         else
@@ -1727,7 +1727,7 @@ template <bool VEC4, bool WQ, bool WC, bool CVEC>
 __global__ void __launch_bounds__(kQBlock)
 tile_out_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                 int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm, const float* __restrict__ Xs,
-                float Xval, const float* __restrict__ l1, const uint64_t* __restrict__ pre) {
+                float Xval, const float* __restrict__ l1, const uint64_t* __restrict__ pre, int64_t ldo, int64_t ldc) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image, scratch, then output image
     __shared__ float s_tab[kTab];
     __shared__ ScanLds sl;
@@ -1757,11 +1757,11 @@ tile_out_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __
     float kmax = 0.0f;
     tile_pass2<WQ, WC>(s_x, tv, s_tab, tid, base, L, fm, Xs ? Xs[vec] : Xval, cw, kmax);   // each thread rewrites its own row
     if (WC) {
-        store_codes<CVEC>(codes + vec * d + t0, cw, len, tid);
+        store_codes<CVEC>(codes + vec * ldc + t0, cw, len, tid);
         publish_kmax(kmax, L, overflow, vec, tid);
     }
     __syncthreads();
-    if (WQ) store_tile<VEC4>(s_x, out + vec * d + t0, len, tid);
+    if (WQ) store_tile<VEC4>(s_x, out + vec * ldo + t0, len, tid);
 }
 
 // =====================================================================================
@@ -1863,10 +1863,10 @@ constexpr int kMeanUnroll = 16;
 static_assert(kMeanClients == 2 * kMeanUnroll, "two code batches per table group");
 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ void mean_load_batch(uint2 (&w)[kMeanUnroll], const int8_t* cp, int64_t d) {
+__device__ __forceinline__ void mean_load_batch(uint2 (&w)[kMeanUnroll], const int8_t* cp, int64_t ldc) {
 #pragma unroll
     for (int u = 0; u < kMeanUnroll; ++u) {
-        const u32x2v t = __builtin_nontemporal_load(reinterpret_cast<const u32x2v*>(cp + (int64_t)u * d));
+        const u32x2v t = __builtin_nontemporal_load(reinterpret_cast<const u32x2v*>(cp + (int64_t)u * ldc));
         w[u] = make_uint2(t.x, t.y);
     }
 }
@@ -1899,11 +1899,11 @@ __device__ __forceinline__ void mean_build_tables(float (*tabn)[256], const floa
 }
 
 // ragged / unaligned columns: bytewise, clients j0 .. j0+nb-1 in order
-__device__ __forceinline__ void mean_add_bytes(float (&e)[kMeanCpt], const int8_t* __restrict__ codes,
+__device__ __forceinline__ void mean_add_bytes(float (&e)[kMeanCpt], const int8_t* __restrict__ codes, int64_t ldc,
                                                const float (*tabn)[256], int64_t j0, int nb, int64_t i0, int64_t d) {
     for (int jj = 0; jj < nb; ++jj)
         for (int k = 0; k < kMeanCpt; ++k)
-            if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[(j0 + jj) * d + i0 + k]];
+            if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[(j0 + jj) * ldc + i0 + k]];
 }
 
 // Overflowed clients (kmax > 127: a count saturated its int8 code) among j0 .. j0+nb-1.
@@ -1917,7 +1917,7 @@ __device__ __forceinline__ uint32_t mean_ovf_mask(const int32_t* __restrict__ km
 // q[j][i] / n_div read from the dequantized batch (what K2 wrote correctly beside the
 // saturated codes; the same bits as its table entry would have had), the others their
 // table entries.  Any column alignment.
-__device__ __forceinline__ void mean_add_mixed(float (&e)[kMeanCpt], const int8_t* __restrict__ codes,
+__device__ __forceinline__ void mean_add_mixed(float (&e)[kMeanCpt], const int8_t* __restrict__ codes, int64_t ldc,
                                             const float* __restrict__ q, int64_t ldq, const float (*tabn)[256],
                                             uint32_t ovf, int64_t j0, int nb, int64_t i0, int64_t d, float n_div) {
     for (int jj = 0; jj < nb; ++jj) {
@@ -1927,7 +1927,7 @@ __device__ __forceinline__ void mean_add_mixed(float (&e)[kMeanCpt], const int8_
                 if (i0 + k < d) e[k] += q[j * ldq + i0 + k] / n_div;
         } else {
             for (int k = 0; k < kMeanCpt; ++k)
-                if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[j * d + i0 + k]];
+                if (i0 + k < d) e[k] += tabn[jj][(uint8_t)codes[j * ldc + i0 + k]];
         }
     }
 }
@@ -1938,9 +1938,9 @@ __device__ __forceinline__ void mean_add_mixed(float (&e)[kMeanCpt], const int8_
 // overlap in other kernels here).
 template <bool VEC, bool ALL = false>
 __global__ void __launch_bounds__(kCodesMeanThreads)
-codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1, const int32_t* __restrict__ kmaxv,
-                  int64_t n, int64_t d, float fm, float n_div, int accumulate, float* __restrict__ est,
-                  const float* __restrict__ q, int64_t ldq) {
+codes_mean_kernel(const int8_t* __restrict__ codes, int64_t ldc, const float* __restrict__ l1,
+                  const int32_t* __restrict__ kmaxv, int64_t n, int64_t d, float fm, float n_div, int accumulate,
+                  float* __restrict__ est, const float* __restrict__ q, int64_t ldq) {
     __shared__ float tabn[kMeanClients][256];     // indexed by the raw code byte, sign included
     __shared__ uint32_t s_ovf;
     const int tid = threadIdx.x;
@@ -1972,7 +1972,7 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
             __syncthreads();
             mean_build_tables(tabn, l1, kmaxv, j0, nb, wid, lane, fm, n_div);
             __syncthreads();
-            mean_add_mixed(e, codes, q, ldq, tabn, ovf, j0, nb, i0, d, n_div);
+            mean_add_mixed(e, codes, ldc, q, ldq, tabn, ovf, j0, nb, i0, d, n_div);
         }
     } else {
     // full groups of kMeanClients: straight-line, unconditional loads (the prefetch of the
@@ -1980,20 +1980,20 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
     // before each batch cover that batch only
     const int8_t* cbase = codes + (full ? i0 : 0);
     uint2 wa[kMeanUnroll], wb[kMeanUnroll];
-    if (VEC && groups > 0) mean_load_batch(wa, cbase, d);
+    if (VEC && groups > 0) mean_load_batch(wa, cbase, ldc);
     for (int64_t g = 0; g < groups; ++g) {
         const int64_t j0 = g * kMeanClients;
         __syncthreads();                            // previous group's tables no longer read
         mean_build_tables(tabn, l1, kmaxv, j0, kMeanClients, wid, lane, fm, n_div);
         __syncthreads();
         if (VEC) {
-            mean_load_batch(wb, cbase + (j0 + kMeanUnroll) * d, d);
+            mean_load_batch(wb, cbase + (j0 + kMeanUnroll) * ldc, ldc);
             if (full) mean_add_batch(e, wa, tabn, 0);
             const int64_t jn = (j0 + kMeanClients + kMeanUnroll <= n) ? j0 + kMeanClients : n - kMeanUnroll;
-            mean_load_batch(wa, cbase + jn * d, d);
+            mean_load_batch(wa, cbase + jn * ldc, ldc);
             if (full) mean_add_batch(e, wb, tabn, kMeanUnroll);
         }
-        if (!full) mean_add_bytes(e, codes, tabn, j0, kMeanClients, i0, d);
+        if (!full) mean_add_bytes(e, codes, ldc, tabn, j0, kMeanClients, i0, d);
     }
     const int64_t jr = groups * kMeanClients;
     const int nr = (int)(n - jr);
@@ -2003,14 +2003,14 @@ codes_mean_kernel(const int8_t* __restrict__ codes, const float* __restrict__ l1
         __syncthreads();
         if (full) {
             for (int jj = 0; jj < nr; ++jj) {
-                const uint2 w = *reinterpret_cast<const uint2*>(codes + (jr + jj) * d + i0);
+                const uint2 w = *reinterpret_cast<const uint2*>(codes + (jr + jj) * ldc + i0);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) e[k] += tabn[jj][(w.x >> (8 * k)) & 0xFF];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) e[4 + k] += tabn[jj][(w.y >> (8 * k)) & 0xFF];
             }
         } else {
-            mean_add_bytes(e, codes, tabn, jr, nr, i0, d);
+            mean_add_bytes(e, codes, ldc, tabn, jr, nr, i0, d);
         }
     }
     }
@@ -2439,14 +2439,17 @@ int uq_l1_torch_order_f32(const float* x, int64_t n, int64_t d, int32_t T, float
 namespace {
 // AS:609-641 for a batch.  X: per-client draws (device), or nullptr with n == 1 and the one
 // draw passed by value in Xval (the per-call drop-in: no host-to-device copy of X).
-int unbiased_codes_impl(const float* x, float* out, int8_t* codes, int32_t* overflow, int64_t n, int64_t d,
-                        int64_t m, const float* X, float Xval, const float* l1, float* l1_out, int32_t T, void* ws,
-                        size_t ws_bytes, void* stream) {
+// Row j of q at out + j*ldo, of the codes at codes + j*ldc (ldo, ldc >= d: row pitches let the
+// caller stagger the rows' physical placement, see DMEPipeline).
+int unbiased_codes_impl(const float* x, float* out, int64_t ldo, int8_t* codes, int64_t ldc, int32_t* overflow,
+                        int64_t n, int64_t d, int64_t m, const float* X, float Xval, const float* l1, float* l1_out,
+                        int32_t T, void* ws, size_t ws_bytes, void* stream) {
     L1Plan plan;
     WsLayout w;
     int rc = check_common(x, n, d, T, ws, ws_bytes, &plan, &w);
     if (rc) return rc;
     if (m < 0) return fail(UQ_E_INVALID, "m must be >= 0");
+    if ((out && ldo < d) || (codes && ldc < d)) return fail(UQ_E_INVALID, "row pitches must be >= d");
     if (n == 0 || d == 0) return UQ_OK;
     if (!X && n != 1) return fail(UQ_E_INVALID, "null X");
     if (!out && !codes) return fail(UQ_E_INVALID, "nothing to write: out and codes are both NULL");
@@ -2465,14 +2468,14 @@ int unbiased_codes_impl(const float* x, float* out, int8_t* codes, int32_t* over
         if (rc) return rc;
     }
     // rows are 16-byte aligned when d % 4 == 0, or when there is only one row
-    const bool vec4 = aligned16(x) && (!out || aligned16(out)) && (d % 4 == 0 || n == 1);
+    const bool vec4 = aligned16(x) && (!out || aligned16(out)) && ((d % 4 == 0 && ldo % 4 == 0) || n == 1);
     const bool stream_form = n >= kStreamMinClients && vec4 && d <= ((int64_t)1 << 29);
     if (codes && !stream_form) {          // the stream form stores each client's kmax itself
         rc = hip_check(hipMemsetAsync(overflow, 0, n * sizeof(int32_t), st), "memset kmax");
         if (rc) return rc;
     }
     const float fm = (float)m;   // torch casts the Python int to f32 for `m * p` and `/ m`
-    const bool cvec = !codes || (aligned16(codes) && d % 16 == 0);
+    const bool cvec = !codes || (aligned16(codes) && d % 16 == 0 && (ldc % 16 == 0 || n == 1));
     const int wq = out ? 1 : 0, wc = codes ? 1 : 0;
     const int sel = (vec4 ? 8 : 0) | (wq ? 4 : 0) | (wc ? 2 : 0) | (cvec ? 1 : 0);
     if (stream_form) {
@@ -2480,7 +2483,7 @@ int unbiased_codes_impl(const float* x, float* out, int8_t* codes, int32_t* over
 #define UQ_STREAM(Q, C, CV)                                                                                 \
     case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
         hipLaunchKernelGGL((quantize_stream_kernel<Q, C, CV>), dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, \
-                           codes, overflow, d, w.tiles, fm, X, Xval, l1use, w.tiles, 1, nullptr);        \
+                           codes, overflow, d, w.tiles, fm, X, Xval, l1use, w.tiles, 1, nullptr, ldo, ldc); \
         break;
         switch (sel & 7) {
             UQ_STREAM(1, 0, 1) UQ_STREAM(1, 1, 1) UQ_STREAM(1, 1, 0) UQ_STREAM(0, 1, 1) UQ_STREAM(0, 1, 0)
@@ -2494,8 +2497,8 @@ int unbiased_codes_impl(const float* x, float* out, int8_t* codes, int32_t* over
     for (int64_t j0 = 0; j0 < n; j0 += kMaxGridY) {
         const int64_t nj = std::min<int64_t>(kMaxGridY, n - j0);
         const float* xj = x + j0 * d;
-        float* outj = out ? out + j0 * d : nullptr;
-        int8_t* codesj = codes ? codes + j0 * d : nullptr;
+        float* outj = out ? out + j0 * ldo : nullptr;
+        int8_t* codesj = codes ? codes + j0 * ldc : nullptr;
         int32_t* ovj = codes ? overflow + j0 : nullptr;
         const float* Xj = X ? X + j0 : nullptr;
         const float* l1j = l1use + j0;
@@ -2546,7 +2549,7 @@ int unbiased_codes_impl(const float* x, float* out, int8_t* codes, int32_t* over
 #define UQ_SEG(Q, C, CV)                                                                                    \
     case ((Q) * 4 + (C) * 2 + (CV)):                                                                      \
         hipLaunchKernelGGL((quantize_stream_kernel<Q, C, CV>), dim3((unsigned)(nj * nseg)), dim3(kQBlock), 0, st, xj, \
-                           outj, codesj, ovj, d, w.tiles, fm, Xj, Xval, l1j, R, nseg, pre);                \
+                           outj, codesj, ovj, d, w.tiles, fm, Xj, Xval, l1j, R, nseg, pre, ldo, ldc);      \
         break;
             switch (sel & 7) {
                 UQ_SEG(1, 0, 1) UQ_SEG(1, 1, 1) UQ_SEG(1, 1, 0) UQ_SEG(0, 1, 1) UQ_SEG(0, 1, 0)
@@ -2560,7 +2563,7 @@ int unbiased_codes_impl(const float* x, float* out, int8_t* codes, int32_t* over
 #define UQ_PHASED(V, Q, C, CV)                                                                                \
     case ((V) * 8 + (Q) * 4 + (C) * 2 + (CV)):                                                              \
         hipLaunchKernelGGL((tile_out_kernel<V, Q, C, CV>), tgrid, dim3(kQBlock), 0, st, xj, outj, codesj, ovj, d, \
-                           w.tiles, fm, Xj, Xval, l1j, pre);                                                  \
+                           w.tiles, fm, Xj, Xval, l1j, pre, ldo, ldc);                                        \
         break;
         switch (sel) {
             UQ_PHASED(1, 1, 0, 1) UQ_PHASED(1, 1, 1, 1) UQ_PHASED(1, 1, 1, 0) UQ_PHASED(1, 0, 1, 1)
@@ -2579,17 +2582,25 @@ int unbiased_codes_impl(const float* x, float* out, int8_t* codes, int32_t* over
 
 extern "C" {
 
+int uq_type_unbiased_codes_ld_f32(const float* x, float* out, int64_t ldq, int8_t* codes, int64_t ldc,
+                                  int32_t* overflow, int64_t n, int64_t d, int64_t m, const float* X, const float* l1,
+                                  float* l1_out, int32_t T, void* ws, size_t ws_bytes, void* stream) {
+    if (n > 0 && d > 0 && !X) return fail(UQ_E_INVALID, "null X");
+    return unbiased_codes_impl(x, out, ldq, codes, ldc, overflow, n, d, m, X, 0.0f, l1, l1_out, T, ws, ws_bytes,
+                               stream);
+}
+
 int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_t* overflow, int64_t n, int64_t d,
                                int64_t m, const float* X, const float* l1, float* l1_out, int32_t T, void* ws,
                                size_t ws_bytes, void* stream) {
-    if (n > 0 && d > 0 && !X) return fail(UQ_E_INVALID, "null X");
-    return unbiased_codes_impl(x, out, codes, overflow, n, d, m, X, 0.0f, l1, l1_out, T, ws, ws_bytes, stream);
+    return uq_type_unbiased_codes_ld_f32(x, out, d, codes, d, overflow, n, d, m, X, l1, l1_out, T, ws, ws_bytes,
+                                         stream);
 }
 
 int uq_type_unbiased_vec_f32(const float* x, float* out, int64_t d, int64_t m, float X, int32_t T, void* ws,
                              size_t ws_bytes, void* stream) {
     if (d > 0 && !out) return fail(UQ_E_INVALID, "null out");
-    return unbiased_codes_impl(x, out, nullptr, nullptr, 1, d, m, nullptr, X, nullptr, nullptr, T, ws, ws_bytes,
+    return unbiased_codes_impl(x, out, d, nullptr, d, nullptr, 1, d, m, nullptr, X, nullptr, nullptr, T, ws, ws_bytes,
                                stream);
 }
 
@@ -2617,27 +2628,34 @@ int uq_codes_decode_f32(const int8_t* codes, const float* l1, int64_t n, int64_t
     return hip_check(hipGetLastError(), "codes_decode_kernel launch");
 }
 
-int uq_codes_q_mean_f32(const int8_t* codes, const float* q, int64_t ldq, const float* l1, const int32_t* kmax,
-                        int64_t n, int64_t d, int64_t m, float n_div, int32_t accumulate, float* est, void* stream) {
+int uq_codes_q_mean_ld_f32(const int8_t* codes, int64_t ldc, const float* q, int64_t ldq, const float* l1,
+                           const int32_t* kmax, int64_t n, int64_t d, int64_t m, float n_div, int32_t accumulate,
+                           float* est, void* stream) {
     if (n < 0 || d < 0 || m < 0) return fail(UQ_E_INVALID, "n, d and m must be >= 0");
     if (d == 0) return UQ_OK;
     if (!est || (n > 0 && (!codes || !l1 || !kmax))) return fail(UQ_E_INVALID, "null pointer");
     if (q && ldq < d) return fail(UQ_E_INVALID, "ldq must be >= d");
+    if (ldc < d) return fail(UQ_E_INVALID, "ldc must be >= d");
     hipStream_t st = (hipStream_t)stream;
-    const bool vec = (n == 0 || aligned16(codes)) && aligned16(est) && d % 16 == 0;
+    const bool vec = (n == 0 || aligned16(codes)) && aligned16(est) && d % 16 == 0 && ldc % 16 == 0;
     const int64_t blocks = (d + kCodesMeanThreads * kMeanCpt - 1) / (kCodesMeanThreads * kMeanCpt);
     if (blocks > 0x7FFFFFFF) return fail(UQ_E_INVALID, "d too large");
     const dim3 tb(kCodesMeanThreads);
     if (vec && d % (kCodesMeanThreads * kMeanCpt) == 0)
-        hipLaunchKernelGGL((codes_mean_kernel<true, true>), dim3((unsigned)blocks), tb, 0, st, codes, l1, kmax, n, d,
-                           (float)m, n_div, accumulate, est, q, ldq);
+        hipLaunchKernelGGL((codes_mean_kernel<true, true>), dim3((unsigned)blocks), tb, 0, st, codes, ldc, l1, kmax, n,
+                           d, (float)m, n_div, accumulate, est, q, ldq);
     else if (vec)
-        hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), tb, 0, st, codes, l1, kmax, n, d, (float)m,
-                           n_div, accumulate, est, q, ldq);
+        hipLaunchKernelGGL(codes_mean_kernel<true>, dim3((unsigned)blocks), tb, 0, st, codes, ldc, l1, kmax, n, d,
+                           (float)m, n_div, accumulate, est, q, ldq);
     else
-        hipLaunchKernelGGL(codes_mean_kernel<false>, dim3((unsigned)blocks), tb, 0, st, codes, l1, kmax, n, d, (float)m,
-                           n_div, accumulate, est, q, ldq);
+        hipLaunchKernelGGL(codes_mean_kernel<false>, dim3((unsigned)blocks), tb, 0, st, codes, ldc, l1, kmax, n, d,
+                           (float)m, n_div, accumulate, est, q, ldq);
     return hip_check(hipGetLastError(), "codes_mean_kernel launch");
+}
+
+int uq_codes_q_mean_f32(const int8_t* codes, const float* q, int64_t ldq, const float* l1, const int32_t* kmax,
+                        int64_t n, int64_t d, int64_t m, float n_div, int32_t accumulate, float* est, void* stream) {
+    return uq_codes_q_mean_ld_f32(codes, d, q, ldq, l1, kmax, n, d, m, n_div, accumulate, est, stream);
 }
 
 int uq_codes_mean_f32(const int8_t* codes, const float* l1, const int32_t* kmax, int64_t n, int64_t d, int64_t m,

@@ -82,6 +82,11 @@ class DMEPipeline:
         c = torch.empty((self.n, self.d), dtype=torch.int8, device=self.dev)
         return q, c
 
+    @staticmethod
+    def _ld(t) -> int:
+        """Row pitch of an output buffer (the launches take pitched rows, e.g. a caller's views)."""
+        return int(t.stride(0)) if t is not None and t.dim() == 2 and t.shape[0] > 1 else (0 if t is None else t.shape[-1])
+
     def _stream(self):
         return torch.cuda.current_stream(self.dev).cuda_stream
 
@@ -98,10 +103,12 @@ class DMEPipeline:
         codes = (self.codes if codes is None else codes) if pl != "q" else None
         if pl != "encode" and q is None:
             raise ValueError("this pipeline holds no q buffer")
-        _lib.check(self.lib.uq_type_unbiased_codes_f32(_p(x), _p(q), _p(codes), _p(self.kmax if codes is not None else None),
-                                                       self.n, self.d, self.m, _p(X), _p(self.l1), None, self.T,
-                                                       _p(self.ws), self.ws_bytes, self._stream()),
-                   "uq_type_unbiased_codes_f32")
+        _lib.check(self.lib.uq_type_unbiased_codes_ld_f32(_p(x), _p(q), max(self._ld(q), self.d), _p(codes),
+                                                          max(self._ld(codes), self.d),
+                                                          _p(self.kmax if codes is not None else None), self.n, self.d,
+                                                          self.m, _p(X), _p(self.l1), None, self.T, _p(self.ws),
+                                                          self.ws_bytes, self._stream()),
+                   "uq_type_unbiased_codes_ld_f32")
         self._codes_valid = codes is not None
 
     def mean(self, n_div: float, accumulate: bool = False, est=None, pipeline: str | None = None):
@@ -110,14 +117,16 @@ class DMEPipeline:
         est = self.est if est is None else est
         if pl == "q":
             self._mean_without_q = False
-            _lib.check(self.lib.uq_client_mean_f32(_p(self.q), self.n, self.d, self.d, float(n_div),
-                                                   int(bool(accumulate)), _p(est), self._stream()), "uq_client_mean_f32")
+            _lib.check(self.lib.uq_client_mean_f32(_p(self.q), self.n, self.d, max(self._ld(self.q), self.d),
+                                                   float(n_div), int(bool(accumulate)), _p(est), self._stream()),
+                       "uq_client_mean_f32")
         else:
             q = self.q if pl == "codes" else None
             self._mean_without_q = q is None
-            _lib.check(self.lib.uq_codes_q_mean_f32(_p(self.codes), _p(q), self.d, _p(self.l1), _p(self.kmax), self.n,
-                                                    self.d, self.m, float(n_div), int(bool(accumulate)), _p(est),
-                                                    self._stream()), "uq_codes_q_mean_f32")
+            _lib.check(self.lib.uq_codes_q_mean_ld_f32(_p(self.codes), max(self._ld(self.codes), self.d), _p(q),
+                                                       max(self._ld(q), self.d), _p(self.l1), _p(self.kmax), self.n,
+                                                       self.d, self.m, float(n_div), int(bool(accumulate)), _p(est),
+                                                       self._stream()), "uq_codes_q_mean_ld_f32")
         return est
 
     def step(self, x, X, n_div=None, accumulate: bool = False, *, est=None, events=None,
