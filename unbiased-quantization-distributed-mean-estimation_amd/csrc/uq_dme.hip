@@ -281,8 +281,10 @@ struct RezKHistOp {
 // One workgroup = one level-1 group = step leaves x step rows x 32 streams.
 // Thread (leaf b, quad q) sums rows [b*step, (b+1)*step) of streams 4q..4q+3
 // sequentially (ATen level 0); then 32 threads add the step leaves in order (level 1).
+// BIG: cascade steps 64-256 (one chunk of more than 2^28 elements, e.g. T = 1 beyond
+// d = 2^28): 256 threads, each taking leaves b, b + 32, ...; 32 KB of leaf sums.
 // =====================================================================================
-template <bool VEC4, class Op>
+template <bool VEC4, class Op, bool BIG = false>
 __global__ void __launch_bounds__(256)
 l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __restrict__ part,
                   const float* __restrict__ l1, float fm, uint32_t* __restrict__ hist_g, uint32_t* __restrict__ zn_g) {
@@ -302,11 +304,10 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
     const int step = 1 << lp;
     const int tid = threadIdx.x;
     const int nthreads = 8 * step;            // 8 quads x step leaves
-    __shared__ float leaf[256 * 4];           // [leaf][32] (step <= 32 -> <= 1024 floats)
+    __shared__ float leaf[(BIG ? 256 : 32) * 32];   // [leaf][32]
     const float* base = x + vec * d + plan.off(c) + (int64_t)g * step * step * 32;
-    if (tid < nthreads) {
+    for (int b = tid >> 3; BIG ? b < step : tid < nthreads; b += 32) {
         const int q = tid & 7;
-        const int b = tid >> 3;
         const float* p = base + ((int64_t)b * step) * 32 + 4 * q;
         float a[4] = {0.f, 0.f, 0.f, 0.f};
         for (int r = 0; r < step; ++r) {
@@ -323,6 +324,7 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
         }
         float* l = leaf + b * 32 + 4 * q;
         l[0] = a[0]; l[1] = a[1]; l[2] = a[2]; l[3] = a[3];
+        if (!BIG) break;
     }
     __syncthreads();
     if (tid < 32) {
@@ -2073,13 +2075,21 @@ int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, flo
         vec4 = vec4 && (plan.nchunks == 1 || plan.cs % 4 == 0);
         int maxstep = std::max(16, 1 << plan.last.lp);
         if (plan.nchunks > 1) maxstep = std::max(maxstep, 1 << plan.full.lp);
-        if (maxstep > 32) return fail(UQ_E_INVALID, "L1 cascade step > 32 unsupported (d too large)");
         dim3 grid(plan.total_groups, (unsigned)n);
-        dim3 block(8 * maxstep);
-        if (vec4)
-            hipLaunchKernelGGL((l1_partial_kernel<true, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn);
-        else
-            hipLaunchKernelGGL((l1_partial_kernel<false, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn);
+        if (maxstep > 32) {              // steps 64..256 (chunk_geo stops at 256)
+            if (vec4)
+                hipLaunchKernelGGL((l1_partial_kernel<true, Op, true>), grid, dim3(256), 0, st, x, d, plan, part, l1, fm,
+                                   hist, zn);
+            else
+                hipLaunchKernelGGL((l1_partial_kernel<false, Op, true>), grid, dim3(256), 0, st, x, d, plan, part, l1, fm,
+                                   hist, zn);
+        } else {
+            dim3 block(8 * maxstep);
+            if (vec4)
+                hipLaunchKernelGGL((l1_partial_kernel<true, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn);
+            else
+                hipLaunchKernelGGL((l1_partial_kernel<false, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn);
+        }
         int rc = hip_check(hipGetLastError(), "l1_partial_kernel launch");
         if (rc) return rc;
     }
