@@ -74,3 +74,18 @@ def test_max_size_vectors_bit_exact(uq, n, d, T, entry):
         # counts sum to ~0.29 m.  The oracle and the GPU agree on this bit for bit.)
         k = np.rint(np.abs(got[j].astype(np.float64)) * m / np.float64(l1[j]))
         assert int(k.sum()) <= m + 1
+
+
+def test_max_size_biased_bit_exact(uq):
+    """Type_biased_quantize (AS:644-687) on one vector of 2^28 + 64 floats: the k' cascade
+    with torch's step 64 (K1a's large-step variant), the radix select over 2^28 keys and --
+    when the threshold is tied -- the torch topk replay at that size, bit-exact against the
+    C++ oracle with torch's tie choice."""
+    d = (1 << 28) + 64
+    x = np.random.default_rng(9).standard_normal(d, dtype=f32)
+    m = O.rate_to_m(1, d)
+    got = uq.biased_quantize(torch.from_numpy(x[None]).cuda(), m=m, torch_threads=1, ties="torch")
+    uq.check_status()
+    got = got.cpu().numpy()[0]
+    ref, L, D, amb = C.biased_quantize(x, m, 1, 0)
+    assert G.n_mismatch(got, ref) == 0, (D, amb)
