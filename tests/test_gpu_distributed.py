@@ -1,7 +1,7 @@
 """GPU, several processes: the client-sharded product path (distributed.py)
 with the HIP quantizer and the HIP client-ordered fold in every rank.
 
-Two ranks share cuda:0 over gloo (tests/dist_worker.py; RCCL refuses two ranks on one
+2, 4 or 8 ranks share cuda:0 over gloo (tests/dist_worker.py; RCCL refuses two ranks on one
 device, and the driver's 8-GPU bench covers RCCL).  Against the single-process path on the
 same clients (quantize_dequantize + client_mean, ND:133-138):
   * every rank's q block is bit-identical to the single-process rows;
@@ -49,11 +49,13 @@ def _launch(case, world, out):
     assert rcs == [0] * world, rcs
 
 
-@pytest.mark.parametrize("case", ["c1", "laplace"])
-def test_two_ranks_share_gpu_product_path(gpu_ready, tmp_path, case):
+# (case, world): world 4 splits C1's 16 clients 4 ways; world 8 rehearses the 8-GPU node's
+# sharding with 6 Laplace clients, so two ranks hold no client (their partial mean is zeros
+# and the ordered chain passes their blocks through unchanged)
+@pytest.mark.parametrize("case,world", [("c1", 2), ("laplace", 2), ("c1", 4), ("laplace", 8)])
+def test_ranks_share_gpu_product_path(gpu_ready, tmp_path, case, world):
     import uqdme
     from uqdme_amd.distributed import shard_range
-    world = 2
     _launch(case, world, str(tmp_path))
     x, Xs = case_inputs(case)
     n = x.shape[0]
