@@ -232,6 +232,17 @@ int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, i
                            void* stream);
 int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
                 const int32_t* sign_row, float* scale_out, void* ws, size_t ws_bytes, void* stream);
+/* torch.norm(v[j], 2) of each row of v [n][D] f32 in torch's CPU order (AS:329: 8 lanes of
+ * fma chains, lanes added in order, sqrt), the norm the EDEN entry points use:
+ *   mode 1: the sequential chains (one chain per torch lane; what batches above 256 rows use)
+ *   mode 2: the segmented chains (1 <= n <= 256, D a power of two >= 16384; workspace
+ *           uq_eden_norm_workspace_bytes): the same bits, the chains cut into segments that
+ *           are resolved in parallel (include/../DESIGN.md §4, EDEN)
+ *   mode 0: mode 2 where it applies, else mode 1 (the choice the EDEN entry points make).
+ * nrm [n] f32. */
+int uq_eden_norm_workspace_bytes(int64_t n, int64_t D, size_t* bytes_out);
+int uq_eden_norm_f32(const float* v, int64_t n, int64_t D, int32_t mode, float* nrm, void* ws, size_t ws_bytes,
+                     void* stream);
 
 /* After the stream has been synchronised: UQ_OK, or UQ_E_TIMEOUT if any
  * inter-workgroup wait in a previous call on this workspace gave up. Clears it. */

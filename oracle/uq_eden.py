@@ -127,6 +127,12 @@ def torch_norm2(v: np.ndarray) -> f32:
     s = accf[0]
     for j in range(1, 8):
         s = f32(s + accf[j])
+    # below one 8-wide vector torch takes other paths (measured, torch 2.10): |x| for one
+    # element, fma for two, mul + add for four
+    if v.shape[0] == 1:
+        return f32(abs(v[0]))
+    if v.shape[0] == 2:
+        return f32(np.sqrt(f32(np.float64(f32(np.float64(v[0]) * v[0])) + np.float64(v[1]) * v[1])))
     for t in v[n:]:
         s = f32(s + f32(t * t))
     return f32(np.sqrt(s))

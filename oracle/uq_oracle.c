@@ -187,3 +187,26 @@ void uqo_client_mean_acc(const float* q, int64_t n, int64_t d, float n_div, floa
     for (int64_t j = 0; j < n; ++j)
         for (int64_t i = 0; i < d; ++i) est[i] += q[j * d + i] / n_div;
 }
+
+/* torch.norm(v, 2) on CPU f32, the EDEN sender's norm (NMSE_Results/Codes/All_Schemes.py:329):
+ * 8 lanes of fma chains over the first d - d % 8 elements, lanes added in order, the tail
+ * as f32 v*v adds, sqrt.  The C form of oracle/uq_eden.py:torch_norm2 (pinned there against
+ * torch; tests/test_oracle_golden.py checks both against torch.norm). */
+float uqo_torch_norm2(const float* v, int64_t d) {
+    float acc[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    const int64_t nv = d - d % 8;
+    for (int64_t i = 0; i < nv; i += 8)
+        for (int l = 0; l < 8; ++l) acc[l] = fmaf(v[i + l], v[i + l], acc[l]);
+    float s = acc[0];
+    for (int l = 1; l < 8; ++l) s = s + acc[l];
+    /* below one 8-wide vector torch takes other paths (measured, torch 2.10): |x| for one
+     * element, fma for two, mul + add for four; ragged tails after whole vectors are not
+     * pinned (EDEN's D is a power of two) */
+    if (d == 1) return fabsf(v[0]);
+    if (d == 2) return sqrtf(fmaf(v[1], v[1], fmaf(v[0], v[0], 0.0f)));
+    for (int64_t i = nv; i < d; ++i) {
+        const float p = v[i] * v[i];
+        s = s + p;
+    }
+    return sqrtf(s);
+}

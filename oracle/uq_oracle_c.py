@@ -39,6 +39,8 @@ def lib():
         L.uqo_client_mean_acc.argtypes = [p, i64, i64, f, p]
         L.uqo_torch_sum.restype = f
         L.uqo_torch_sum.argtypes = [p, i64, ctypes.c_int]
+        L.uqo_torch_norm2.restype = f
+        L.uqo_torch_norm2.argtypes = [p, i64]
         L.uqc_bound.restype = ctypes.c_uint64
         L.uqc_bound.argtypes = [i64]
         L.uqc_encode.restype = ctypes.c_uint64
@@ -106,6 +108,12 @@ def client_mean_acc(q2d, n_div, est):
     assert est.dtype == np.float32 and est.flags.c_contiguous and est.shape == (d,)
     lib().uqo_client_mean_acc(_ptr(q2d), n, d, np.float32(n_div), _ptr(est))
     return est
+
+
+def torch_norm2(v) -> np.float32:
+    """torch.norm(v, 2) in torch's CPU f32 order (8 fma lanes; oracle/uq_eden.py:torch_norm2)."""
+    v = np.ascontiguousarray(v, dtype=np.float32).reshape(-1)
+    return np.float32(lib().uqo_torch_norm2(_ptr(v), v.shape[0]))
 
 
 def torch_sum(v, torch_threads: int = 1):

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     import uqdme
     res = {}
-    for d in (172554, 1 << 20):
+    for d in (172554, 1 << 20, 1 << 22):
         vs = [torch.randn(d, device="cuda") for _ in range(16)]     # different vectors: some have
         v = vs[0]                                                   # biased-quantizer threshold ties
         for name, f in (("Type_unbiased_quantize", uqdme.Type_unbiased_quantize),

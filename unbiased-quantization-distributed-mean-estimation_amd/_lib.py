@@ -46,6 +46,8 @@ SIGNATURES = {
     "uq_eden_compress_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _sz, _p]),
     "uq_eden_decompress_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "uq_eden_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
+    "uq_eden_norm_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
+    "uq_eden_norm_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _sz, _p]),
     "uq_tc_bound": (ctypes.c_int, [_i64, ctypes.POINTER(_sz)]),
     "uq_tc_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
     "uq_tc_encode": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _i32, _p, _sz, _p, _p, _sz, _p]),

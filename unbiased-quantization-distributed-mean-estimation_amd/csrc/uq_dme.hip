@@ -2204,10 +2204,67 @@ int ilog2_pow2(int64_t D) {
     return p;
 }
 
+// torch.norm of few clients: the segmented chains (KE2a-KE2d) instead of KE2's sequential
+// ones.  KE2 keeps batches above kSegNormMaxN: it hides its chains behind the reads there,
+// while KE2s reads the vectors twice.
+constexpr int64_t kSegNormMaxN = 256;
+
+bool segnorm_applies(int64_t n, int64_t D) {
+    return n >= 1 && n <= kSegNormMaxN && D >= kSegMinD && (D & (D - 1)) == 0;
+}
+
+struct SegNormLayout {
+    size_t segsum, g, e, kind, cnt, tseg, tab, total;      // offsets from the region start
+};
+SegNormLayout segnorm_layout(int64_t n, int64_t D) {
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t nk = (size_t)n * 8 * (size_t)(D / kSegBlock);
+    SegNormLayout L{};
+    L.segsum = 0;
+    L.g = up(nk * sizeof(double));
+    L.e = up(L.g + nk * sizeof(float));
+    L.kind = up(L.e + nk * sizeof(float));
+    L.cnt = up(L.kind + nk * sizeof(int32_t));
+    L.tseg = up(L.cnt + (size_t)n * sizeof(int32_t));
+    L.tab = up(L.tseg + (size_t)n * kSegTabCap * sizeof(int32_t));
+    L.total = up(L.tab + (size_t)n * kSegTabCap * kSegTab * sizeof(float));
+    return L;
+}
+
+int launch_segnorm(const float* v, int64_t n, int64_t D, char* region, float* nrm, hipStream_t st) {
+    const SegNormLayout L = segnorm_layout(n, D);
+    double* segsum = (double*)(region + L.segsum);
+    float* g = (float*)(region + L.g);
+    float* e = (float*)(region + L.e);
+    int32_t* kind = (int32_t*)(region + L.kind);
+    int32_t* cnt = (int32_t*)(region + L.cnt);
+    int32_t* tseg = (int32_t*)(region + L.tseg);
+    float* tab = (float*)(region + L.tab);
+    const int64_t K = D / kSegBlock;
+    const dim3 grid((unsigned)(K / kSegPerWG), (unsigned)n);
+    hipLaunchKernelGGL(eden_segsum_kernel, grid, dim3(256), 0, st, v, D, segsum);
+    hipLaunchKernelGGL(eden_segscan_kernel, dim3(8u, (unsigned)n), dim3(256), 0, st, segsum, K, g, cnt);
+    hipLaunchKernelGGL(eden_segchain_kernel, grid, dim3(256), 0, st, v, D, g, e, kind, cnt, tseg);
+    hipLaunchKernelGGL(eden_segtab_kernel, dim3((unsigned)kSegTabCap, (unsigned)n), dim3(256), 0, st, v, D, g, cnt, tseg,
+                       tab);
+    hipLaunchKernelGGL(eden_segwalk_kernel, dim3((unsigned)n), dim3(512), 0, st, v, D, g, e, kind, tab, nrm);
+    return hip_check(hipGetLastError(), "eden segmented norm launch");
+}
+
+int launch_chainnorm(const float* v, int64_t n, int64_t D, float* nrm, hipStream_t st) {
+    const dim3 grid((unsigned)((n + kNormClients - 1) / kNormClients));
+    if (D % kNormChunk == 0)
+        hipLaunchKernelGGL(eden_norm_whole_kernel, grid, dim3(kNormThreads), 0, st, v, n, D, nrm);
+    else
+        hipLaunchKernelGGL(eden_norm_kernel, grid, dim3(kNormThreads), 0, st, v, n, D, nrm);
+    return hip_check(hipGetLastError(), "eden_norm_kernel launch");
+}
+
 struct EdenLayout {
-    size_t vec_off, nrm_off, part_off, bins_off, scale_off, total;
+    size_t vec_off, nrm_off, part_off, bins_off, scale_off, seg_off, total;
     int64_t D;
     int32_t tiles;
+    bool seg;                 // the segmented norm (its region at seg_off)
 };
 
 EdenLayout eden_layout(int64_t n, int64_t dim) {
@@ -2220,7 +2277,9 @@ EdenLayout eden_layout(int64_t n, int64_t dim) {
     w.part_off = up(w.nrm_off + (size_t)n * sizeof(float));
     w.bins_off = up(w.part_off + (size_t)n * w.tiles * sizeof(double));
     w.scale_off = up(w.bins_off + (size_t)n * w.D);
-    w.total = up(w.scale_off + (size_t)n * sizeof(float));
+    w.seg_off = up(w.scale_off + (size_t)n * sizeof(float));
+    w.seg = segnorm_applies(n, w.D);
+    w.total = w.seg_off + (w.seg ? segnorm_layout(n, w.D).total : 0);
     return w;
 }
 
@@ -3074,13 +3133,31 @@ int eden_front(const float* x, int64_t n, int64_t dim, const EdenTables& tab, co
     float* vec = (float*)(wsb + w.vec_off);
     int rc = launch_fwht(a, n, false, vec, vec, st, rot);
     if (rc) return rc;
-    if (w.D % kNormChunk == 0)
-        hipLaunchKernelGGL(eden_norm_whole_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads),
-                           0, st, *rot, n, w.D, nrm);
-    else
-        hipLaunchKernelGGL(eden_norm_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)), dim3(kNormThreads),
-                           0, st, *rot, n, w.D, nrm);
-    return hip_check(hipGetLastError(), "eden_norm_kernel launch");                 // AS:329 torch.norm
+    if (w.seg) return launch_segnorm(*rot, n, w.D, wsb + w.seg_off, nrm, st);       // AS:329 torch.norm
+    return launch_chainnorm(*rot, n, w.D, nrm, st);
+}
+
+int uq_eden_norm_workspace_bytes(int64_t n, int64_t D, size_t* bytes_out) {
+    if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
+    if (n < 0 || D < 0) return fail(UQ_E_INVALID, "n and D must be >= 0");
+    *bytes_out = segnorm_applies(n, D) ? segnorm_layout(n, D).total : 0;
+    return UQ_OK;
+}
+
+int uq_eden_norm_f32(const float* v, int64_t n, int64_t D, int32_t mode, float* nrm, void* ws, size_t ws_bytes,
+                     void* stream) {
+    if (n < 0 || D < 0) return fail(UQ_E_INVALID, "n and D must be >= 0");
+    if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 clients per call");
+    if (mode < 0 || mode > 2) return fail(UQ_E_INVALID, "mode must be 0 (auto), 1 (chains) or 2 (segmented)");
+    if (n == 0) return UQ_OK;
+    if (!v || !nrm) return fail(UQ_E_INVALID, "null pointer");
+    const bool seg = mode == 2 || (mode == 0 && segnorm_applies(n, D));
+    if (seg && !segnorm_applies(n, D))
+        return fail(UQ_E_INVALID, "segmented norm: 1 <= n <= 256 and D a power of two >= 16384");
+    if (D == 0) return hip_check(hipMemsetAsync(nrm, 0, (size_t)n * sizeof(float), (hipStream_t)stream), "norm fill");
+    if (!seg) return launch_chainnorm(v, n, D, nrm, (hipStream_t)stream);
+    if (!ws || ws_bytes < segnorm_layout(n, D).total) return fail(UQ_E_WORKSPACE, "workspace too small");
+    return launch_segnorm(v, n, D, (char*)ws, nrm, (hipStream_t)stream);
 }
 
 int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,

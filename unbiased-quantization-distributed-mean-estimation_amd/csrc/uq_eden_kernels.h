@@ -510,8 +510,11 @@ eden_norm_kernel(const float* __restrict__ v, int64_t n, int64_t D, float* __res
         const int64_t vec = v0 + ck;
         if (tid < 8 * kNormClients && cl == 0 && vec < n) {
             const float* p = v + vec * D;
-            for (int64_t i = nv; i < D; ++i) tot = tot + p[i] * p[i];
-            nrm[vec] = sqrtf(tot);
+            // torch's CPU norm below one 8-wide vector (EDEN's D = 1, 2, 4): |x| for one
+            // element, fma for two, mul + add for four (measured on torch 2.10)
+            if (D == 2) tot = fmaf(p[1], p[1], fmaf(p[0], p[0], 0.0f));
+            else for (int64_t i = nv; i < D; ++i) tot = tot + p[i] * p[i];
+            nrm[vec] = D == 1 ? fabsf(p[0]) : sqrtf(tot);
         }
     }
 }
@@ -598,6 +601,283 @@ eden_norm_whole_kernel(const float* __restrict__ v, int64_t n, int64_t D, float*
     }
 }
 
+// ---- KE2s: the same norm for small batches, its chains cut into segments -----------------
+// KE2 runs each client's 8 chains of D/8 dependent fmas end to end: with few clients the
+// chain IS the kernel (0.64 ms at n = 1, D = 2^20: 80 % of the per-call EDEN drop-in).  The
+// segmented form gives the same bits with the chains cut into segments of kSegSteps steps:
+//   KE2a  fp64 sum of v^2 per (lane, segment)                                  (approximate)
+//   KE2b  guess g = f32(fp64 exclusive prefix of those sums) per segment        (approximate)
+//   KE2c  e = the segment's f32 fma chain run from g.  Inside one binade the f32 grid is
+//         uniform, so RN(a + p) = RN(b + p) + (a - b) for grid points a, b when a + p and
+//         b + p stay in that binade and are not midpoints (a - b shifts a midpoint onto a
+//         midpoint, so the two chains meet ties at the same steps).  Hence any start A in
+//         g's binade ends at A + (e - g) exactly, if the guess chain met no tie and stayed in
+//         the binade and A + (e - g) is still in it.  Segments whose guess chain crosses a
+//         binade edge, meets a tie (or cannot rule one out), or starts / ends within
+//         kSegTab/2 grid steps of an edge are listed for a table:
+//   KE2t  the chain run from each of the kSegTab f32 starts whose bit patterns surround g's.
+//   KE2d  one wave per torch lane walks its segments in order from A = 0: a wave prefix sum
+//         of e - g resolves every segment up to the first one that does not translate
+//         (exact: one binade range, checked), that one is resolved by its table or, when A
+//         is outside the table, by running its kSegSteps steps.  The lanes are then added
+//         in order as in KE2.  Every end value is the sequential chain's, bit for bit.
+constexpr int kSegSteps = 64;                          // chain steps per segment
+constexpr int kSegBlock = 8 * kSegSteps;               // floats of one segment (all 8 lanes)
+constexpr int kSegPerWG = 32;                          // segments per KE2a / KE2c workgroup
+constexpr int kSegPad = kSegBlock + 8;                 // LDS row of a segment (8 floats apart: banks)
+constexpr int kSegTab = 1024;                          // table starts per listed segment
+constexpr int kSegTabCap = 256;                        // tables per client (beyond: KE2d runs the steps)
+constexpr int64_t kSegMinD = (int64_t)kSegBlock * kSegPerWG;
+
+__device__ __forceinline__ uint32_t fbits(float x) { return __float_as_uint(x); }
+__device__ __forceinline__ int fexp(float x) { return (int)((__float_as_uint(x) >> 23) & 0xFFu); }
+
+// kSegPerWG segments of one client from v into LDS rows [segment][8 * step + lane]
+__device__ __forceinline__ void seg_stage(const float* __restrict__ v, int64_t D, int64_t client, int64_t seg0,
+                                          float* s, int tid) {
+    const float4* src = reinterpret_cast<const float4*>(v + client * D + seg0 * kSegBlock);
+#pragma unroll
+    for (int j = 0; j < kSegBlock * kSegPerWG / 4 / 256; ++j) {
+        const int q = tid + 256 * j;
+        const int e = 4 * q;
+        *reinterpret_cast<float4*>(s + (e / kSegBlock) * kSegPad + (e % kSegBlock)) = src[q];
+    }
+}
+
+__global__ void __launch_bounds__(256)
+eden_segsum_kernel(const float* __restrict__ v, int64_t D, double* __restrict__ segsum) {
+    __shared__ __attribute__((aligned(16))) float s[kSegPerWG * kSegPad];
+    const int tid = threadIdx.x;
+    const int64_t client = blockIdx.y;
+    const int64_t K = D / kSegBlock;
+    const int64_t seg0 = (int64_t)blockIdx.x * kSegPerWG;
+    seg_stage(v, D, client, seg0, s, tid);
+    __syncthreads();
+    const int sl = tid >> 3, l = tid & 7;
+    const float* row = s + sl * kSegPad + l;
+    double acc = 0.0;
+    for (int i = 0; i < kSegSteps; ++i) {
+        const double x = row[8 * i];
+        acc += x * x;
+    }
+    segsum[(client * 8 + l) * K + seg0 + sl] = acc;
+}
+
+// one workgroup per (lane, client): the exclusive prefix of the lane's K segment sums, in
+// rounds of 1024 (4 per thread, coalesced); lane 0's workgroup zeroes the table count
+__global__ void __launch_bounds__(256)
+eden_segscan_kernel(const double* __restrict__ segsum, int64_t K, float* __restrict__ g, int32_t* __restrict__ tabcnt) {
+    __shared__ double wsum[256 / kWave];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+    const int l = blockIdx.x;
+    const int64_t client = blockIdx.y;
+    if (tid == 0 && l == 0) tabcnt[client] = 0;
+    const double* src = segsum + (client * 8 + l) * K;
+    float* dst = g + (client * 8 + l) * K;
+    double carry = 0.0;
+    for (int64_t r0 = 0; r0 < K; r0 += 1024) {
+        double x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = r0 + 4 * tid + k;
+            x[k] = i < K ? src[i] : 0.0;
+        }
+        const double t = (x[0] + x[1]) + (x[2] + x[3]);
+        const double incl = wave_incl_scan(t, lane);
+        if (lane == kWave - 1) wsum[wid] = incl;
+        __syncthreads();
+        double run = carry + wave_prev(incl), tot = carry;
+#pragma unroll
+        for (int w = 0; w < 256 / kWave; ++w) {
+            if (w < wid) run += wsum[w];
+            tot += wsum[w];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = r0 + 4 * tid + k;
+            if (i < K) dst[i] = (float)run;
+            run += x[k];
+        }
+        carry = tot;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+eden_segchain_kernel(const float* __restrict__ v, int64_t D, const float* __restrict__ g, float* __restrict__ e,
+                     int32_t* __restrict__ kind, int32_t* __restrict__ tabcnt, int32_t* __restrict__ tabseg) {
+    __shared__ __attribute__((aligned(16))) float s[kSegPerWG * kSegPad];
+    const int tid = threadIdx.x;
+    const int64_t client = blockIdx.y;
+    const int64_t K = D / kSegBlock;
+    const int64_t seg0 = (int64_t)blockIdx.x * kSegPerWG;
+    seg_stage(v, D, client, seg0, s, tid);
+    __syncthreads();
+    const int sl = tid >> 3, l = tid & 7;
+    const int64_t idx = (client * 8 + l) * K + seg0 + sl;
+    const float* row = s + sl * kSegPad + l;
+    const float g0 = g[idx];
+    float b = g0;
+    bool tie = false;
+    for (int i = 0; i < kSegSteps; ++i) {
+        const float x = row[8 * i];
+        const float r = fmaf(x, x, b);
+        // (b + x*x) - r exactly (fp64: b - r is exact when their exponents are within 28, and
+        // the fma returns the residual exactly whenever it is one of the values tested): a
+        // midpoint is half a grid step, u/2, or u/4 just below a power of two
+        const int er = fexp(r);
+        const double u = __longlong_as_double((long long)((uint64_t)(std::max(er, 1) - 150 + 1023) << 52));
+        const double res = fabs(fma((double)x, (double)x, (double)b - (double)r));
+        tie = tie || res == 0.5 * u || res == 0.25 * u || (b != 0.0f && er - fexp(b) > 28);
+        b = r;
+    }
+    const int eg = fexp(g0);
+    const bool finite = eg < 255 && fexp(b) < 255;
+    const bool cross = fexp(b) != eg;
+    const bool near_bottom = eg > 0 && (fbits(g0) & 0x7FFFFFu) < (uint32_t)(kSegTab / 2);
+    const bool near_top = !cross && (((uint32_t)(eg + 1) << 23) - fbits(b)) <= (uint32_t)(kSegTab / 2);
+    int32_t k = 0;
+    if (!finite || cross || tie || near_bottom || near_top) {
+        const int slot = atomicAdd(&tabcnt[client], 1);
+        if (slot < kSegTabCap) {
+            k = slot + 1;
+            tabseg[client * kSegTabCap + slot] = (int32_t)((seg0 + sl) * 8 + l);
+        } else {
+            k = -1;                                    // no table: KE2d runs its steps
+        }
+    }
+    e[idx] = b;
+    kind[idx] = k;
+}
+
+__global__ void __launch_bounds__(256)
+eden_segtab_kernel(const float* __restrict__ v, int64_t D, const float* __restrict__ g, const int32_t* __restrict__ tabcnt,
+                   const int32_t* __restrict__ tabseg, float* __restrict__ tab) {
+    __shared__ float xs[kSegSteps];
+    const int64_t client = blockIdx.y;
+    const int slot = blockIdx.x;
+    if (slot >= std::min(tabcnt[client], kSegTabCap)) return;            // uniform
+    const int tid = threadIdx.x;
+    const int32_t code = tabseg[client * kSegTabCap + slot];
+    const int64_t seg = code >> 3;
+    const int l = code & 7;
+    const int64_t K = D / kSegBlock;
+    if (tid < kSegSteps) xs[tid] = v[client * D + 8 * (seg * kSegSteps + tid) + l];
+    __syncthreads();
+    const int64_t gb = fbits(g[(client * 8 + l) * K + seg]);
+    constexpr int kPer = kSegTab / 256;
+    float a[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int64_t sb = gb + tid + 256 * k - kSegTab / 2;
+        a[k] = sb < 0 ? __uint_as_float(0x7FC00000u) : __uint_as_float((uint32_t)sb);   // (never looked up)
+    }
+    for (int i = 0; i < kSegSteps; ++i) {
+        const float x = xs[i];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) a[k] = fmaf(x, x, a[k]);
+    }
+    float* out = tab + ((int64_t)client * kSegTabCap + slot) * kSegTab;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) out[tid + 256 * k] = a[k];
+}
+
+// one workgroup per client, wave l walks torch lane l's chain.  A wave holds kWalkChunks
+// chunks of 64 segments in registers (lane j: segment 64 q + j of chunk q) and loads the next
+// tile of chunks while it walks this one.
+constexpr int kWalkChunks = 8;
+__global__ void __launch_bounds__(512)
+eden_segwalk_kernel(const float* __restrict__ v, int64_t D, const float* __restrict__ g, const float* __restrict__ e,
+                    const int32_t* __restrict__ kind, const float* __restrict__ tab, float* __restrict__ nrm) {
+    __shared__ float accs[8];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), l = tid / kWave;
+    const int64_t client = blockIdx.x;
+    const int64_t K = D / kSegBlock;
+    const int64_t base = (client * 8 + l) * K;
+    float cg[kWalkChunks], ce[kWalkChunks], ng[kWalkChunks] = {}, ne[kWalkChunks] = {};
+    int32_t ck[kWalkChunks], nk[kWalkChunks] = {};
+    auto fetch = [&](int64_t tile, float (&fg)[kWalkChunks], float (&fe)[kWalkChunks], int32_t (&fk)[kWalkChunks]) {
+#pragma unroll
+        for (int q = 0; q < kWalkChunks; ++q) {
+            const int64_t s = (tile * kWalkChunks + q) * kWave + lane;
+            fg[q] = s < K ? g[base + s] : 0.0f;
+            fe[q] = s < K ? e[base + s] : 0.0f;
+            fk[q] = s < K ? kind[base + s] : 0;
+        }
+    };
+    float A = 0.0f;                                    // wave-uniform
+    int64_t s0 = 0;
+    // resolve segment s0 of chunk c (registers: this lane's segment of the chunk) and, when
+    // it translates, every following one of the chunk that does
+    auto step = [&](int64_t c, float sg, float se, int32_t sk) {
+        const int o = (int)(s0 - c * kWave);
+        const bool inb = lane >= o && c * kWave + lane < K;
+        const bool fin = fexp(sg) < 255 && fexp(se) < 255;
+        const double tau = (inb && fin) ? (double)se - (double)sg : 0.0;   // >= 0: chains never decrease
+        const double Aj = (double)A + wave_prev(wave_incl_scan(tau, lane));
+        // the partial sums are exact while they stay below 2^28 times A's binade (multiples of
+        // its grid step, 51 bits); A = 0 (or not finite) resolves one segment at a time
+        const bool span = A > 0.0f && fexp(A) < 255;
+        const double lim = __longlong_as_double((long long)((uint64_t)(std::max(fexp(A), 1) - 127 + 28 + 1023) << 52));
+        const float af = (float)Aj;
+        const float r = af + (float)tau;
+        const bool valid = inb && fin && (lane == o || (span && Aj + tau < lim)) && (double)af == Aj &&
+                           (af == sg || (sk == 0 && fexp(af) == fexp(sg) && fexp(r) == fexp(sg)));
+        const uint64_t bad = __ballot(inb && !valid);
+        const uint64_t inm = __ballot(inb);
+        const int first = bad ? __builtin_ctzll(bad) : 64 - __builtin_clzll(inm);
+        if (first > o) {                               // segments o .. first - 1 resolved
+            const float res = af == sg ? se : r;
+            A = __shfl(res, first - 1, kWave);
+            s0 = c * kWave + first;
+            return;
+        }
+        // segment s0 does not translate: its table, or its steps
+        const int32_t kk = __shfl(sk, o, kWave);
+        const float gg = __shfl(sg, o, kWave);
+        bool done = false;
+        if (kk > 0) {
+            const int64_t d = (int64_t)fbits(A) - (int64_t)fbits(gg) + kSegTab / 2;
+            if (d >= 0 && d < kSegTab) {
+                A = tab[((int64_t)client * kSegTabCap + (kk - 1)) * kSegTab + d];
+                done = true;
+            }
+        }
+        if (!done) {
+            const float x = v[client * D + 8 * (s0 * kSegSteps + lane) + l];
+            for (int i = 0; i < kSegSteps; ++i) {
+                const float xi = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)fbits(x), i));
+                A = fmaf(xi, xi, A);
+            }
+        }
+        s0 += 1;
+    };
+    fetch(0, cg, ce, ck);
+    const int64_t tiles = (K + kWalkChunks * kWave - 1) / (kWalkChunks * kWave);
+    for (int64_t t = 0; t < tiles; ++t) {
+        if (t + 1 < tiles) fetch(t + 1, ng, ne, nk);
+#pragma unroll
+        for (int q = 0; q < kWalkChunks; ++q) {
+            const int64_t c = t * kWalkChunks + q;
+            const int64_t cend = std::min<int64_t>(K, (c + 1) * kWave);
+            while (s0 < cend) step(c, cg[q], ce[q], ck[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < kWalkChunks; ++q) {
+            cg[q] = ng[q];
+            ce[q] = ne[q];
+            ck[q] = nk[q];
+        }
+    }
+    if (lane == 0) accs[l] = A;
+    __syncthreads();
+    if (tid == 0) {
+        float tot = accs[0];
+        for (int j = 1; j < 8; ++j) tot = tot + accs[j];
+        nrm[client] = sqrtf(tot);
+    }
+}
+
 // ---- KE3: bins and partial dots ---------------------------------------------------------
 __global__ void __launch_bounds__(256)
 eden_bins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm,
@@ -659,7 +939,16 @@ eden_scale_kernel(const double* __restrict__ part, int32_t tiles, const float* _
     const int64_t vec = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (vec >= n) return;
     double dot = 0.0;
-    for (int t = 0; t < tiles; ++t) dot += part[vec * tiles + t];
+    const double* pp = part + vec * tiles;
+    int t = 0;
+    for (; t + 16 <= tiles; t += 16) {                   // 16 loads in flight, adds in tile order
+        double q[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) q[k] = pp[t + k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) dot += q[k];
+    }
+    for (; t < tiles; ++t) dot += pp[t];
     const float nv = nrm[vec];
     scale[vec] = (nv * nv) / (float)dot;                    // AS:335 norm ** 2 / dot
 }
