@@ -327,3 +327,25 @@ def test_failed_replay_falls_back_to_index_order(uq, n, d):
     out_l = uq.biased_quantize(x, m=m, torch_threads=1, ties="lowest")
     assert torch.equal(out_t.view(torch.int32), out_l.view(torch.int32))
     uq.check_status()
+
+
+@pytest.mark.parametrize("d", [(1 << 17) + 5, 1 << 20])
+def test_candidate_digits_few_and_many_clients_agree(uq, d):
+    """Batches of <= 16 clients run the candidate digits (KB4d) over many workgroups per
+    client, larger ones one workgroup per client: the same rows give the same bits either
+    way (torch ties and lowest index), and both match the oracle."""
+    rng = np.random.default_rng(d % 977)
+    x = rng.standard_normal((17, d)).astype(f32)
+    x[3] = np.round(x[3] * 4) / 4                      # tie-heavy rows
+    x[9] = rng.integers(-3, 4, d)
+    xt = torch.as_tensor(x).cuda()
+    m = rate_to_m(1, d)
+    for ties, code in (("torch", 0), ("lowest", 1)):
+        few = uq.biased_quantize(xt[:16], m=m, torch_threads=1, ties=ties).cpu().numpy()
+        many = uq.biased_quantize(xt, m=m, torch_threads=1, ties=ties).cpu().numpy()
+        assert G.bits_equal(few, many[:16]), ties
+        one = uq.biased_quantize(xt[9:10], m=m, torch_threads=1, ties=ties).cpu().numpy()
+        assert G.bits_equal(one[0], many[9]), ties
+        for j in (0, 3, 9):
+            exp, *_ = C.biased_quantize(x[j], m, 1, code)
+            assert G.bits_equal(many[j], exp), (ties, j)

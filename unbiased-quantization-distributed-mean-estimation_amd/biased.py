@@ -80,14 +80,15 @@ def biased_quantize(x, bits_per_dimension=1, *, m: int | None = None, torch_thre
 
 def Type_biased_quantize(input_vector, bits_per_dimension=1):
     """Drop-in for NMSE_Results/Codes/All_Schemes.py:669 (same name for FLM:177's
-    directory naming).  Copies the input (AS:671), KeyError for an unknown rate
-    (AS:684), bit-identical to the reference on torch CPU with the same intra-op
-    thread count, ties included.  The reference raises when m' is not finite (AS:656);
-    so does this."""
+    directory naming).  KeyError for an unknown rate (AS:684), bit-identical to the
+    reference on torch CPU with the same intra-op thread count, ties included.  The
+    reference raises when m' is not finite (AS:656); so does this.  AS:671 copies the input
+    so as not to alias it; here the kernels only read it and the result is always a new
+    tensor (d == 0 returns a clone), so no device-side copy is made."""
     dev = _device()
     l_rate = RATE_TABLE[bits_per_dimension]
     if torch.is_tensor(input_vector):
-        v = input_vector.detach().to(device=dev, dtype=torch.float32).clone()
+        v = input_vector.detach().to(device=dev, dtype=torch.float32)
     else:
         v = torch.tensor(np.asarray(input_vector), dtype=torch.float32, device=dev)
     if v.dim() != 1:
@@ -95,7 +96,9 @@ def Type_biased_quantize(input_vector, bits_per_dimension=1):
     d = v.numel()
     m = int(l_rate * d)
     if d == 0:
-        return v
+        return v.clone()
+    if not v.is_contiguous():
+        v = v.contiguous()
     out, info = biased_quantize(v.view(1, d), m=m, ties="torch", return_info=True)
     flags = int(info[0, 1].item())
     check_status()

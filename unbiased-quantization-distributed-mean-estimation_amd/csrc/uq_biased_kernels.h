@@ -329,6 +329,45 @@ rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restri
 }
 
 // KB4d: digits 2 and 3 on the candidates (one workgroup per compact-mode client).
+// cand_pick: the digit of candidate pass `pass` (1: bits 10-20, 2: bits 0-9) holding the
+// kleft-th largest key, from the pass's histogram h (nb bins); updates s in every thread.
+__device__ __forceinline__ void cand_pick(const uint32_t* h, int pass, RezState& s, uint32_t* lds) {
+    const int tid = threadIdx.x;
+    const int shift = pass == 1 ? 10 : 0;
+    const int nb = pass == 1 ? 2048 : 1024;
+    const int per = nb / 256;
+    const int hi = nb - tid * per;
+    uint32_t c[8], sum = 0;
+    for (int k = 0; k < per; ++k) {
+        c[k] = h[hi - 1 - k];
+        sum += c[k];
+    }
+    __shared__ uint32_t s_digit, s_above, s_eq;
+    if (tid == 0) { s_digit = 0u; s_above = 0u; s_eq = 0u; }
+    uint32_t total;
+    uint32_t above = block_excl_scan_u32(sum, lds, &total);
+    if (above < s.kleft && above + sum >= s.kleft) {
+        for (int k = 0; k < per; ++k) {
+            if (above + c[k] >= s.kleft) {
+                s_digit = (uint32_t)(hi - 1 - k);
+                s_above = above;
+                s_eq = c[k];
+                break;
+            }
+            above += c[k];
+        }
+    }
+    __syncthreads();
+    s.prefix |= s_digit << shift;
+    s.kleft -= s_above;
+    if (pass == 2) {
+        s.eq = s_eq;
+        s.need = s.kleft;
+        if (s.eq > s.need) s.flags |= kRezAmbiguous;
+    }
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(256)
 rez_cand_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ cand,
                        const uint32_t* __restrict__ cand_n, uint32_t cap) {
@@ -344,7 +383,6 @@ rez_cand_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ c
         const int shift = pass == 1 ? 10 : 0;
         const uint32_t dmask = pass == 1 ? 0x7FFu : 0x3FFu;
         const uint32_t hmask = pass == 1 ? 0xFFE00000u : 0xFFFFFC00u;
-        const int nb = (int)dmask + 1;
         for (int b = tid; b < kRadixBins; b += 256) h[b] = 0u;
         __syncthreads();
         // 8 independent candidate loads in flight per thread, then their LDS atomics
@@ -362,38 +400,63 @@ rez_cand_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ c
             if ((key & hmask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
         }
         __syncthreads();
-        const int per = nb / 256;
-        const int hi = nb - tid * per;
-        uint32_t c[8], sum = 0;
-        for (int k = 0; k < per; ++k) {
-            c[k] = h[hi - 1 - k];
-            sum += c[k];
-        }
-        __shared__ uint32_t s_digit, s_above, s_eq;
-        if (tid == 0) { s_digit = 0u; s_above = 0u; s_eq = 0u; }
-        uint32_t total;
-        uint32_t above = block_excl_scan_u32(sum, lds, &total);
-        if (above < s.kleft && above + sum >= s.kleft) {
-            for (int k = 0; k < per; ++k) {
-                if (above + c[k] >= s.kleft) {
-                    s_digit = (uint32_t)(hi - 1 - k);
-                    s_above = above;
-                    s_eq = c[k];
-                    break;
-                }
-                above += c[k];
-            }
-        }
-        __syncthreads();
-        s.prefix |= s_digit << shift;
-        s.kleft -= s_above;
-        if (pass == 2) {
-            s.eq = s_eq;
-            s.need = s.kleft;
-            if (s.eq > s.need) s.flags |= kRezAmbiguous;
-        }
-        __syncthreads();
+        cand_pick(h, pass, s, lds);
     }
+    if (tid == 0) st[vec] = s;
+}
+
+// The same two passes for a few clients with long candidate lists (the per-call drop-in):
+// KB4d1 histograms kCandSpan candidates per workgroup into the client's pass histogram
+// (hist[vec][pass], zero until then: the full-vector passes skip compact-mode clients),
+// KB4d2 picks the digit from it with cand_pick (same bits as rez_cand_select_kernel).
+constexpr int kCandSpan = 256 * 32;
+template <int PASS>
+__global__ void __launch_bounds__(256)
+rez_cand_hist_kernel(const RezState* __restrict__ st, const uint32_t* __restrict__ cand,
+                     const uint32_t* __restrict__ cand_n, uint32_t cap, uint32_t* __restrict__ hist) {
+    const int64_t vec = blockIdx.y;
+    if (st[vec].kleft == 0 || !(st[vec].flags & kRezCompact)) return;
+    const uint32_t nc = std::min(cand_n[vec], cap);
+    const uint32_t b0 = blockIdx.x * (uint32_t)kCandSpan;
+    if (b0 >= nc) return;
+    constexpr int shift = PASS == 1 ? 10 : 0;
+    constexpr uint32_t dmask = PASS == 1 ? 0x7FFu : 0x3FFu;
+    constexpr uint32_t hmask = PASS == 1 ? 0xFFE00000u : 0xFFFFFC00u;
+    constexpr int nb = (int)dmask + 1;
+    __shared__ uint32_t h[nb];
+    const int tid = threadIdx.x;
+    for (int b = tid; b < nb; b += 256) h[b] = 0u;
+    __syncthreads();
+    const uint32_t prefix = st[vec].prefix;
+    const uint32_t* cv = cand + (size_t)vec * cap;
+    uint32_t kk[kCandSpan / 256];
+#pragma unroll
+    for (int u = 0; u < kCandSpan / 256; ++u) {
+        const uint32_t i = b0 + tid + 256u * u;
+        kk[u] = i < nc ? cv[i] : ~prefix;                     // ~prefix never matches
+    }
+#pragma unroll
+    for (int u = 0; u < kCandSpan / 256; ++u)
+        if ((kk[u] & hmask) == prefix) atomicAdd(&h[(kk[u] >> shift) & dmask], 1u);
+    __syncthreads();
+    uint32_t* g = hist + ((size_t)vec * 3 + PASS) * kRadixBins;
+    for (int b = tid; b < nb; b += 256)
+        if (h[b]) atomicAdd(&g[b], h[b]);
+}
+
+template <int PASS>
+__global__ void __launch_bounds__(256)
+rez_cand_pick_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist) {
+    const int64_t vec = blockIdx.x;
+    if (st[vec].kleft == 0 || !(st[vec].flags & kRezCompact)) return;
+    __shared__ uint32_t h[kRadixBins];
+    __shared__ uint32_t lds[4];
+    const int tid = threadIdx.x;
+    const uint32_t* g = hist + ((size_t)vec * 3 + PASS) * kRadixBins;
+    for (int b = tid; b < kRadixBins; b += 256) h[b] = g[b];
+    __syncthreads();
+    RezState s = st[vec];
+    cand_pick(h, PASS, s, lds);
     if (tid == 0) st[vec] = s;
 }
 

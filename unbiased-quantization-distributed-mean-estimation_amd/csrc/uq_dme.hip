@@ -2208,6 +2208,9 @@ int ilog2_pow2(int64_t D) {
 // ones.  KE2 keeps batches above kSegNormMaxN: it hides its chains behind the reads there,
 // while KE2s reads the vectors twice.
 constexpr int64_t kSegNormMaxN = 256;
+// biased quantizer: batches of at most this many clients run the candidate digits (KB4d) over
+// many workgroups per client (one workgroup per client walks up to d/8 keys twice)
+constexpr int64_t kCandMultiMaxN = 16;
 
 bool segnorm_applies(int64_t n, int64_t D) {
     return n >= 1 && n <= kSegNormMaxN && D >= kSegMinD && (D & (D - 1)) == 0;
@@ -2956,7 +2959,17 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         hipLaunchKernelGGL(rez_compact_kernel<true>, cgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
     else
         hipLaunchKernelGGL(rez_compact_kernel<false>, cgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
-    hipLaunchKernelGGL(rez_cand_select_kernel, dim3((unsigned)n), dim3(256), 0, st, state, cand, cand_n, w.cap);
+    const unsigned cspans = (unsigned)((w.cap + kCandSpan - 1) / kCandSpan);
+    if (n <= kCandMultiMaxN && cspans > 1) {         // few clients: digits 2-3 over many workgroups
+        hipLaunchKernelGGL(rez_cand_hist_kernel<1>, dim3(cspans, (unsigned)n), dim3(256), 0, st, state, cand, cand_n,
+                           w.cap, hist);
+        hipLaunchKernelGGL(rez_cand_pick_kernel<1>, dim3((unsigned)n), dim3(256), 0, st, state, hist);
+        hipLaunchKernelGGL(rez_cand_hist_kernel<2>, dim3(cspans, (unsigned)n), dim3(256), 0, st, state, cand, cand_n,
+                           w.cap, hist);
+        hipLaunchKernelGGL(rez_cand_pick_kernel<2>, dim3((unsigned)n), dim3(256), 0, st, state, hist);
+    } else {
+        hipLaunchKernelGGL(rez_cand_select_kernel, dim3((unsigned)n), dim3(256), 0, st, state, cand, cand_n, w.cap);
+    }
     // the others: full-vector histogram passes for digits 2-3
 #define UQ_RADIX(P)                                                                                          \
     if (vec4)                                                                                                \
