@@ -91,3 +91,36 @@ def test_drop_in_uses_segmented_norm_and_matches_batch(lib):
     for j in (0, 511, 1023):
         one = uqdme.eden_quantize(xt[j:j + 1], 1, seeds=[seeds[j]])
         assert torch.equal(one[0].view(torch.int32), batch[j].view(torch.int32)), j
+
+
+def test_segmented_norm_fuzz_vs_oracle(lib):
+    """256 random rows (the largest segmented batch) at D = 2^15 from many distributions and
+    scales, few-bit values among them (ties), each against the C oracle."""
+    D, n = 1 << 15, 256
+    rng = np.random.default_rng(2025)
+    rows = []
+    for j in range(n):
+        kind = j % 8
+        if kind == 0:
+            r = rng.standard_normal(D) * 10.0 ** rng.uniform(-20, 18)
+        elif kind == 1:
+            r = rng.uniform(-1, 1, D) * 10.0 ** rng.uniform(-5, 5)
+        elif kind == 2:
+            r = rng.laplace(1, 2, D)
+        elif kind == 3:
+            r = rng.lognormal(1, 2, D)
+        elif kind == 4:
+            r = rng.integers(-(1 << rng.integers(1, 12)), 1 << rng.integers(1, 12), D) * 2.0 ** rng.integers(-30, 10)
+        elif kind == 5:
+            r = np.where(rng.random(D) < rng.uniform(0.001, 0.2), rng.standard_normal(D), 0.0)
+        elif kind == 6:
+            r = rng.standard_normal(D) * np.exp(np.linspace(-rng.uniform(0, 30), rng.uniform(0, 30), D))
+        else:
+            r = rng.choice([-1.5, -0.75, 0.25, 1.0, 3.0], D) * 2.0 ** rng.integers(-12, 12)
+        rows.append(r)
+    with np.errstate(all="ignore"):
+        X = np.stack(rows).astype(np.float32)
+        ref = np.array([C.torch_norm2(v) for v in X])
+    got = _norm(lib, torch.from_numpy(X).cuda(), 2)
+    bad = [j for j in range(n) if not same_bits(got[j], ref[j])]
+    assert not bad, [(j, got[j], ref[j]) for j in bad[:5]]

@@ -628,6 +628,7 @@ constexpr int kSegPad = kSegBlock + 8;                 // LDS row of a segment (
 constexpr int kSegTab = 1024;                          // table starts per listed segment
 constexpr int kSegTabCap = 256;                        // tables per client (beyond: KE2d runs the steps)
 constexpr int64_t kSegMinD = (int64_t)kSegBlock * kSegPerWG;
+static_assert(kSegSteps == 64, "KE2d's step path loads one segment as one value per lane of a wave");
 
 __device__ __forceinline__ uint32_t fbits(float x) { return __float_as_uint(x); }
 __device__ __forceinline__ int fexp(float x) { return (int)((__float_as_uint(x) >> 23) & 0xFFu); }
