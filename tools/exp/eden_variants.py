@@ -1,5 +1,5 @@
 """Time the EDEN 1-bit round trip (uq_eden_f32) of every library in _build/abl/ on one
-resident 1024 x 2^20 N(0,1) batch, alternating libraries three times; outputs are compared
+resident N(0,1) batch (EDEN_N x EDEN_D, default 1024 x 2^20), alternating libraries three times; outputs are compared
 with the first library's (bit-identical expected)."""
 import ctypes
 import json
@@ -10,13 +10,14 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 OUT = os.path.join(ROOT, "unbiased-quantization-distributed-mean-estimation_amd", "_build", "abl")
 P, I64, I32, SZ = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_size_t
-n, d = 1024, 1 << 20
+n, d = int(os.environ.get("EDEN_N", 1024)), int(os.environ.get("EDEN_D", 1 << 20))
 g = torch.Generator(device="cuda").manual_seed(3)
 x = torch.randn(n, d, generator=g, device="cuda")
 out = torch.empty_like(x)
 scale = torch.empty(n, device="cuda")
 seeds = torch.tensor([123], dtype=torch.int32, device="cuda")           # one rotation for all clients (AS:802)
-signs = torch.empty((1, d), dtype=torch.int8, device="cuda")
+D = 1 << (d - 1).bit_length()                       # padded length (AS:128)
+signs = torch.empty((1, D), dtype=torch.int8, device="cuda")
 rows = torch.zeros(n, dtype=torch.int32, device="cuda")
 sp = torch.cuda.current_stream().cuda_stream
 libs = {}
@@ -30,7 +31,7 @@ for f in sorted(os.listdir(OUT)):
             raise RuntimeError("workspace query failed")
         libs[f[:-3]] = (L, torch.zeros(b.value, dtype=torch.uint8, device="cuda"), b.value)
 first = next(iter(libs.values()))[0]
-if first.uq_rht_signs(seeds.data_ptr(), 1, d, signs.data_ptr(), sp) != 0:
+if first.uq_rht_signs(seeds.data_ptr(), 1, D, signs.data_ptr(), sp) != 0:
     raise RuntimeError("rht signs failed")
 ref = None
 for rep in range(int(os.environ.get("REPS", 3))):

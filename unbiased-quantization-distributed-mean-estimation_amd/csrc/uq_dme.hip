@@ -2295,7 +2295,17 @@ void fwht_dispatch(dim3 grid, const FwhtArgs& b, int lo, int k, hipStream_t st) 
     else if (lo > 0 && k == kFwhtHighBits && M == 0 && ((int64_t)1 << lo) % kHighCols == 0)
         hipLaunchKernelGGL((fwht_high256_kernel<L, R>), dim3(grid.x * kFwhtCols / kHighCols, grid.y), dim3(kHighT), 0, st,
                            b, lo);
-    else
+    else if (lo > 0 && k <= 6 && M == 0) {
+        const dim3 g2((unsigned)(((b.D >> k) + 255) / 256), grid.y);
+        switch (k) {
+            case 1: hipLaunchKernelGGL((fwht_small_kernel<1, L, R>), g2, dim3(256), 0, st, b, lo); break;
+            case 2: hipLaunchKernelGGL((fwht_small_kernel<2, L, R>), g2, dim3(256), 0, st, b, lo); break;
+            case 3: hipLaunchKernelGGL((fwht_small_kernel<3, L, R>), g2, dim3(256), 0, st, b, lo); break;
+            case 4: hipLaunchKernelGGL((fwht_small_kernel<4, L, R>), g2, dim3(256), 0, st, b, lo); break;
+            case 5: hipLaunchKernelGGL((fwht_small_kernel<5, L, R>), g2, dim3(256), 0, st, b, lo); break;
+            default: hipLaunchKernelGGL((fwht_small_kernel<6, L, R>), g2, dim3(256), 0, st, b, lo); break;
+        }
+    } else
         hipLaunchKernelGGL((fwht_pass_kernel<M, L, R>), grid, dim3(kFwhtT), 0, st, b, lo, k);
 }
 

@@ -400,6 +400,44 @@ fwht_high256_kernel(FwhtArgs a, int lo) {
         }
 }
 
+// ---- KE1'': a pass of at most 6 bits after the first (D = 2^13..2^18: 12 + 1..6; 2^21, 2^22: 12 + 8 + 1..2)
+// fwht_pass_kernel would stage 2^K x 32 elements per 256-thread workgroup; here a thread owns
+// one column j below 2^lo and keeps its 2^K rows (stride 2^lo) in registers: coalesced rows,
+// the same stages in the same order (so the same bits), the same epilogue.
+template <int K, bool LAST, bool RECV_LAST>
+__global__ void __launch_bounds__(256)
+fwht_small_kernel(FwhtArgs a, int lo) {
+    const int64_t vec = blockIdx.y;
+    const int64_t D = a.D;
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= (D >> K)) return;
+    const int64_t base = ((q >> lo) << (lo + K)) + (q & (((int64_t)1 << lo) - 1));
+    const float* in = (const float*)a.in + vec * D;
+    float v[1 << K];
+#pragma unroll
+    for (int r = 0; r < (1 << K); ++r) v[r] = in[base + ((int64_t)r << lo)];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+        for (int r = 0; r < (1 << K); ++r)
+            if (!(r & (1 << j))) bfly(v[r], v[r | (1 << j)]);         // AS:107-112
+    const int8_t* sg = a.signs + (int64_t)(a.sign_row ? a.sign_row[vec] : 0) * D;
+#pragma unroll
+    for (int r = 0; r < (1 << K); ++r) {
+        const int64_t i = base + ((int64_t)r << lo);
+        float x = v[r];
+        if (LAST) x = x / a.sqrtD;                                  // AS:114 vec /= sqrt(d)
+        if (RECV_LAST) {
+            if (i < a.dim) {
+                x = x * (float)sg[i];                               // AS:152 * diag
+                a.out[vec * a.dim + i] = a.scale ? a.scale[vec] * x : x;   // AS:413 scale * vec, [:dim]
+            }
+        } else {
+            a.out[vec * D + i] = x;
+        }
+    }
+}
+
 // ---- KE2: torch.norm(v, 2) -------------------------------------------------------------
 // torch CPU order: 8 interleaved lanes, acc_l = fma(v[8i + l], v[8i + l], acc_l) in i order,
 // then acc_0 + acc_1 + ... + acc_7, the scalar tail, sqrt (f32).  One workgroup serves 4
