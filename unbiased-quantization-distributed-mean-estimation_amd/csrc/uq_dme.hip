@@ -2306,7 +2306,9 @@ void fwht_dispatch(dim3 grid, const FwhtArgs& b, int lo, int k, hipStream_t st) 
     else if (lo > 0 && k == kFwhtHighBits && M == 0 && ((int64_t)1 << lo) % kHighCols == 0)
         hipLaunchKernelGGL((fwht_high256_kernel<L, R>), dim3(grid.x * kFwhtCols / kHighCols, grid.y), dim3(kHighT), 0, st,
                            b, lo);
-    else if (lo > 0 && k <= 6 && M == 0) {
+    else if (lo > 0 && k <= 6 && M == 0 && (int64_t)grid.y * ((b.D >> k) / 256) >= 1024) {
+        // (a thread per column: with fewer than 1024 workgroups, e.g. one client of 2^18,
+        // the generic kernel's 2^k x 32 tiles spread the pass over more of the GPU)
         const dim3 g2((unsigned)(((b.D >> k) + 255) / 256), grid.y);
         switch (k) {
             case 1: hipLaunchKernelGGL((fwht_small_kernel<1, L, R>), g2, dim3(256), 0, st, b, lo); break;
