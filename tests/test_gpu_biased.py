@@ -349,3 +349,22 @@ def test_candidate_digits_few_and_many_clients_agree(uq, d):
         for j in (0, 3, 9):
             exp, *_ = C.biased_quantize(x[j], m, 1, code)
             assert G.bits_equal(many[j], exp), (ties, j)
+
+
+def test_few_clients_2pow22_take_level_replay(uq):
+    """A few clients at d >= 2^21 replay torch's tie choice through KB7a's levels (one
+    workgroup walking 2^22 keys took milliseconds): Gaussian and tie-heavy rows, bit-exact
+    against the oracle, at least one row replayed."""
+    rng = np.random.default_rng(622)
+    d, n = 1 << 22, 4
+    x = rng.standard_normal((n, d)).astype(f32)
+    x[1] = np.round(x[1] * 4) / 4
+    x[3] = np.round(x[3] * 8) / 8
+    m = rate_to_m(1, d)
+    out, info = uq.biased_quantize(torch.as_tensor(x).cuda(), m=m, torch_threads=1, ties="torch", return_info=True)
+    out, info = out.cpu().numpy(), info.cpu().numpy()
+    assert (info[:, 1] & 8).any(), info
+    for j in range(n):
+        exp, *_ = C.biased_quantize(x[j], m, 1, 0)
+        assert G.bits_equal(out[j], exp), (j, G.n_mismatch(out[j], exp))
+    uq.check_status()

@@ -385,6 +385,9 @@ constexpr int64_t kTieLevelMin = kTieLdsPairs;   // shorter ranges finish in rez
 // boxes, bit-identical; stopping at 65536 gained nothing: profiles/r3f_exp_biased_levels.jsonl)
 constexpr int64_t kTieLevelStop = 16384;
 constexpr int64_t kTieLevelMinClients = 32;      // KB7a for batches of at least this many clients
+// ... and for any batch of vectors this long: one replay workgroup walking 2^22 keys took
+// ~9 ms (a 6-client batch at d = 2^22 with one ambiguous client), KB7a's idle launches 0.35 ms
+constexpr int64_t kTieLevelBigD = (int64_t)1 << 21;
 constexpr uint32_t kTieManyClients = 128;          // this many listed clients: levels only down to
 constexpr int64_t kTieLevelMinMany = 65536;        //   this range (tie-heavy batches)
 constexpr int kTieSegs = 256;               // segments per partition (one wave each)

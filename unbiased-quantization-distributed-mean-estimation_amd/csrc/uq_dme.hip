@@ -2434,9 +2434,10 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     uint32_t* pos = (uint32_t*)(wsb + w.pos_off);
     // KB7a pays ~85 short launches whether or not any client is listed (the host does not
     // know): worth it for batches, where ~3 % of Gaussian clients are ambiguous at R = 1 and
-    // several replays would share one workgroup each; a few-client call (the per-vector
+    // several replays would share one workgroup each, and for vectors of 2^21 and more, whose
+    // one-workgroup replay takes milliseconds; a few-client call at smaller d (the per-vector
     // drop-ins) replays in one kernel when it has to
-    if (d <= kTieLevelMin || n < kTieLevelMinClients) {
+    if (d <= kTieLevelMin || (n < kTieLevelMinClients && d < kTieLevelBigD)) {
         hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
                            state, bits, qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)nullptr, 0,
                            (uint32_t*)(wsb + w.tcnt_off), w.tiles);
