@@ -136,17 +136,25 @@ def quantize_dequantize(x, bits_per_dimension=1, X=None, *, m: int | None = None
     T = get_torch_threads() if torch_threads is None else int(torch_threads)
     if X is None:
         X = draw_uniforms(n, generator)
-    X = torch.as_tensor(X, dtype=torch.float32).reshape(-1).to(dev)
+    X = torch.as_tensor(X, dtype=torch.float32).reshape(-1)
     if X.numel() != n:
         raise ValueError("X must have one draw per row")
-    if l1 is not None:
-        l1 = torch.as_tensor(l1, dtype=torch.float32).reshape(-1).to(dev).contiguous()
-        if l1.numel() != n:
-            raise ValueError("l1 must have one value per row")
     if out is None:
         out = torch.empty_like(x)
     elif out.shape != x.shape or out.dtype != torch.float32 or out.device != x.device or not out.is_contiguous():
         raise ValueError("out must be a contiguous f32 tensor like x")
+    if n == 1 and d > 0 and l1 is None and not return_l1 and X.device.type == "cpu":
+        # one vector with its draw on the host: the drop-in's entry (X by value, no copy of
+        # X to the device, no workspace fill; same kernels, same bits): 0.20 -> 0.15 ms at 2^22
+        ws = _workspace(dev, _ws_bytes(1, d, T))
+        _lib.check(_lib.load().uq_type_unbiased_vec_f32(_ptr(x), _ptr(out), d, mm, float(X[0]), T, _ptr(ws),
+                                                        ws.numel(), _stream_ptr(dev)), "uq_type_unbiased_vec_f32")
+        return out
+    X = X.to(dev)
+    if l1 is not None:
+        l1 = torch.as_tensor(l1, dtype=torch.float32).reshape(-1).to(dev).contiguous()
+        if l1.numel() != n:
+            raise ValueError("l1 must have one value per row")
     l1_out = torch.empty(n, dtype=torch.float32, device=dev) if return_l1 else None
     nb = _ws_bytes(n, d, T)
     ws = _workspace(dev, nb)
