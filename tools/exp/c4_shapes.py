@@ -3,7 +3,7 @@ harness's client counts {1, 6, 11, 51, 101} and 256), to find shapes that fall o
 batch kernels' per-client rate.  One JSON line per (scheme, n): ms per batch (HIP events,
 5 calls after one warm call) and us per client.
 
-    python tools/exp/c4_shapes.py [d]"""
+    python tools/exp/c4_shapes.py [d] [schemes, comma-separated]"""
 import json
 import os
 import sys
@@ -28,6 +28,7 @@ def timed(f, reps=5):
 
 def main():
     d = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 22
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     g = torch.Generator(device="cuda").manual_seed(4)
     for n in (1, 6, 11, 51, 101, 256):
         x = torch.randn(n, d, generator=g, device="cuda")
@@ -37,6 +38,8 @@ def main():
         for name, f in (("unbiased", lambda: uqdme.quantize_dequantize(x, 1, X=X, torch_threads=1)),
                         ("biased", lambda: uqdme.biased_quantize(x, m=m, torch_threads=1, ties="torch")),
                         ("eden", lambda: uqdme.eden_quantize(x, 1, seeds=seeds))):
+            if only and name not in only:
+                continue
             ms = timed(f)
             print(json.dumps({"scheme": name, "d": d, "n": n, "ms": round(ms, 4), "us_per_client": round(ms * 1e3 / n, 2)}),
                   flush=True)

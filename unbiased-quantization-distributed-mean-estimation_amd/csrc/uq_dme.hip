@@ -498,7 +498,7 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
                         const float v = s_stage[kk * 32 + lane];
                         if (k < n3) {
                             b2 += v;
-                            if ((k + 1) % step == 0) {
+                            if (((k + 1) & (step - 1)) == 0) {         // step = 2^lp (no 64-bit modulo)
                                 acc3 += b2;
                                 b2 = 0.f;
                             }
