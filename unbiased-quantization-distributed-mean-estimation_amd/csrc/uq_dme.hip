@@ -2301,7 +2301,9 @@ EdenLayout eden_layout(int64_t n, int64_t dim) {
 // 256 x 64 high pass, the generic LDS kernel otherwise (same stages, same bits).
 template <int M, bool L, bool R>
 void fwht_dispatch(dim3 grid, const FwhtArgs& b, int lo, int k, hipStream_t st) {
-    if (lo == 0 && k == kFwhtLowBits && (M != 2 || (b.D % 16) == 0))
+    if (lo == 0 && k == kFwhtLow16Bits && (M == 1 || M == 2) && !L)
+        hipLaunchKernelGGL((fwht_low16k_kernel<M>), dim3((unsigned)(b.D >> kFwhtLow16Bits), grid.y), dim3(1024), 0, st, b);
+    else if (lo == 0 && k == kFwhtLowBits && (M != 2 || (b.D % 16) == 0))
         hipLaunchKernelGGL((fwht_low4096_kernel<M, L, R>), grid, dim3(256), 0, st, b);
     else if (lo > 0 && k == kFwhtHighBits && M == 0 && ((int64_t)1 << lo) % kHighCols == 0)
         hipLaunchKernelGGL((fwht_high256_kernel<L, R>), dim3(grid.x * kFwhtCols / kHighCols, grid.y), dim3(kHighT), 0, st,
@@ -2330,7 +2332,9 @@ void fwht_dispatch(dim3 grid, const FwhtArgs& b, int lo, int k, hipStream_t st) 
 int launch_fwht(FwhtArgs a, int64_t n, bool receiver, float* buf, float* out, hipStream_t st,
                 float** result = nullptr, int lo0 = 0) {
     const int p = ilog2_pow2(a.D);
-    int lo = lo0, k = std::min(p - lo0, lo0 ? kFwhtHighBits : kFwhtLowBits);
+    // D = 2^22 (config C4): a 14-bit first pass, then 8 (one pass fewer than 12 + 8 + 2)
+    int lo = lo0, k = std::min(p - lo0, lo0 ? kFwhtHighBits : (p == kFwhtLow16Bits + kFwhtHighBits ? kFwhtLow16Bits
+                                                                                                    : kFwhtLowBits));
     bool first = lo0 == 0;
     float* cur = buf;                              // sender: the buffer the next pass writes
     for (;;) {
@@ -3251,8 +3255,10 @@ int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbit
     const EdenLayout w = eden_layout(n < 0 ? 0 : n, dim < 0 ? 0 : dim);
     uint8_t* bins = (uint8_t*)((char*)ws + w.bins_off);
     float* scale = scale_out ? scale_out : (float*)((char*)ws + w.scale_off);
-    if (w.D <= ((int64_t)1 << kFwhtLowBits) || n > 65535) {
-        // a single FWHT pass (or an invalid n, reported there): compress, then decompress
+    if (w.D <= ((int64_t)1 << kFwhtLowBits) || n > 65535 || w.D == ((int64_t)1 << (kFwhtLow16Bits + kFwhtHighBits))) {
+        // a single FWHT pass (or an invalid n, reported there), or D = 2^22 whose 14 + 8
+        // passes (two each way, without the fused bins of the 12-bit pass) move fewer bytes
+        // than the fused 12 + 8 + 2: compress, then decompress
         int rc = uq_eden_compress_f32(x, n, dim, nbits, signs, sign_row, bins, scale, ws, ws_bytes, stream);
         if (rc) return rc;
         return uq_eden_decompress_f32(bins, scale, n, dim, nbits, signs, sign_row, out, ws, ws_bytes, stream);

@@ -24,6 +24,7 @@
 
 constexpr int kFwhtT = 256;            // threads per FWHT workgroup
 constexpr int kFwhtLowBits = 12;       // first pass: contiguous tiles of 4096
+constexpr int kFwhtLow16Bits = 14;     // ... of 16384 when D = 2^22 (14 + 8)
 constexpr int kFwhtHighBits = 8;       // later passes: 2^8 rows x 32 columns
 constexpr int kFwhtCols = 32;
 constexpr int kEdenTile = 4096;        // KE3 tile (256 threads x 16)
@@ -316,6 +317,91 @@ fwht_low4096_kernel(FwhtArgs a) {
         } else {
             a.out[vec * D + gi] = r;
         }
+    }
+}
+
+// First pass over 16384 contiguous elements (bits 0-13), for D = 2^22: 14 + 8 bits instead of
+// 12 + 8 + 2, one pass fewer each way.  1024 threads; index e = b0 + 16 b1 + 256 b2 + 4096 b3
+// (b3: 2 bits).  Rounds as fwht_low4096_kernel (b0, b1, b2 in registers in turn, padded LDS
+// transposes), then bits 12-13: a thread takes four columns p = b0 + 16 b1 + 256 b2 and their
+// four b3 values.  The same stages in the same order, so the same bits as 12 + 8 + 2.
+// MODE 1: sender (pad, * diag), 2: receiver (centroids of the bins); never the last pass.
+template <int MODE>
+__global__ void __launch_bounds__(1024)
+fwht_low16k_kernel(FwhtArgs a) {
+    __shared__ float s[16384 + 1024];
+    const int64_t vec = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int64_t D = a.D;
+    const int64_t base = (int64_t)blockIdx.x * 16384;
+    float v[16];
+    {   // round-1 layout: 16 contiguous elements
+        const int64_t i0 = base + (int64_t)tid * 16;
+        if (MODE == 1) {
+            const int8_t* sg = a.signs + (int64_t)(a.sign_row ? a.sign_row[vec] : 0) * D;
+            const float* x = (const float*)a.in + vec * a.dim;
+            const bool full = i0 + 16 <= a.dim && (((uintptr_t)(x + i0)) & 15) == 0;
+            if (full) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 t = *reinterpret_cast<const float4*>(x + i0 + 4 * q);
+                    v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = (i0 + i < a.dim) ? x[i0 + i] : 0.f;
+            }
+            const int4 sgv = *reinterpret_cast<const int4*>(sg + i0);       // 16 signs
+            const int8_t* sb = reinterpret_cast<const int8_t*>(&sgv);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = v[i] * (float)sb[i];            // AS:132/137 * diag
+        } else {
+            const int4 bv = *reinterpret_cast<const int4*>((const uint8_t*)a.in + vec * D + i0);
+            const uint8_t* bb = reinterpret_cast<const uint8_t*>(&bv);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = a.tab.c[bb[i]];                  // AS:383
+        }
+    }
+    const int b3 = tid >> 8, o3 = 4096 * b3;
+    stages16(v);                                                   // bits 0-3
+    {
+        const int b1 = tid & 15, b2 = (tid >> 4) & 15;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[pad17(i + 16 * b1 + 256 * b2 + o3)] = v[i];
+    }
+    __syncthreads();
+    const int b0 = tid & 15;
+    {
+        const int b2 = (tid >> 4) & 15;                            // round 2: (b0, b2, b3)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = s[pad17(b0 + 16 * i + 256 * b2 + o3)];
+        stages16(v);                                               // bits 4-7
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[pad17(b0 + 16 * i + 256 * b2 + o3)] = v[i];
+    }
+    __syncthreads();
+    {
+        const int b1 = (tid >> 4) & 15;                            // round 3: (b0, b1, b3)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = s[pad17(b0 + 16 * b1 + 256 * i + o3)];
+        stages16(v);                                               // bits 8-11
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[pad17(b0 + 16 * b1 + 256 * i + o3)] = v[i];
+    }
+    __syncthreads();
+    float* o = a.out + vec * D + base;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {                                  // round 4: bits 12-13
+        const int p = tid + 1024 * j;
+        float w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = s[pad17(p + 4096 * k)];
+        bfly(w[0], w[1]);                                          // bit 12
+        bfly(w[2], w[3]);
+        bfly(w[0], w[2]);                                          // bit 13
+        bfly(w[1], w[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(w[k], o + p + 4096 * k);
     }
 }
 
