@@ -780,12 +780,13 @@ eden_segsum_kernel(const float* __restrict__ v, int64_t D, double* __restrict__ 
     __syncthreads();
     const int sl = tid >> 3, l = tid & 7;
     const float* row = s + sl * kSegPad + l;
-    double acc = 0.0;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};              // an approximation: any order will do
+#pragma unroll 16
     for (int i = 0; i < kSegSteps; ++i) {
         const double x = row[8 * i];
-        acc += x * x;
+        acc[i & 3] += x * x;
     }
-    segsum[(client * 8 + l) * K + seg0 + sl] = acc;
+    segsum[(client * 8 + l) * K + seg0 + sl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
 // one workgroup per (lane, client): the exclusive prefix of the lane's K segment sums, in
@@ -844,7 +845,8 @@ eden_segchain_kernel(const float* __restrict__ v, int64_t D, const float* __rest
     const float g0 = g[idx];
     float b = g0;
     bool tie = false;
-    for (int i = 0; i < kSegSteps; ++i) {
+#pragma unroll 16
+    for (int i = 0; i < kSegSteps; ++i) {                 // (unrolled: LDS reads ahead of the chain)
         const float x = row[8 * i];
         const float r = fmaf(x, x, b);
         // (b + x*x) - r exactly (fp64: b - r is exact when their exponents are within 28, and
