@@ -218,11 +218,48 @@ int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inver
  * word % h_len).  X [n][D] int32 in [0, table_rows); recv_table [table_rows][h_len] f32
  * (<= 1024 entries: the reference tables <b>_X_<s>_h_256_q_recv_table.pt); exact_mask u8 [n][D] and
  * exact_vals f32 [n][D] (dense) or both NULL; scale [n] f32.  The inverse RHT is uq_rht_f32
- * (inverse = 1).  The sender (AS:429-505) is not provided: its tables are not in the
- * reference. */
+ * (inverse = 1). */
 int uq_quicfl_prepare_f32(const int32_t* X, int64_t n, int64_t D, const float* recv_table, int32_t table_rows,
                           int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask, const float* exact_vals,
                           const float* scale, float* out, void* stream);
+
+/* ---- QUIC-FL sender (baseline) --------------------------------------
+ * QuicFLSender.compress (NMSE_Results/Codes/All_Schemes.py:455-503) for a batch of n messages,
+ * bit-identical to the reference's CPU run (tests/golden/quicfl_sender_vectors.*):
+ *   rotation: the sender RHT of uq_rht_f32 (diagonal row sign_row[j] of signs [rows][D]);
+ *   scale[j] = f32(1 / torch.norm(rot)) * f32(sqrt(D))       (AS:466/470, Tensor.__rtruediv__)
+ *   v = rot * scale; exact = |v| > f32(norm.ppf(1 - 2^-9));   (AS:472-478)
+ *   q = v / delta (0 where exact); p = q - floor(q);           (AS:480-483)
+ *   h = randint(0, h_len, (D,)) and bernoulli(p) from MT19937 seeded with prng_seeds[j]
+ *       (= xxh64(str(seed)) % 2^16, uq_xxh64), the D randint words first;
+ *   idx = ((floor(q) + b) * h_len + h) + half_table in f32, truncated (torch.take wraps
+ *       negatives), half_table = ((table_numel / h_len) - 1) * h_len / 2   (AS:443, AS:486);
+ *   X = table[idx].X + bernoulli(table[idx].p) from a second generator, truncated (AS:489-490).
+ * table_xp: device f32 [table_numel][2] = (sender_table_X, sender_table_p) pairs.
+ * The second generator (the reference's global torch generator): px_state [n][626] u32 =
+ *   (left, next, state[624]) of ATen's mt19937 per message (next = 625 - left unless left = 1),
+ *   or px_state = NULL and px_seeds [n] (fresh generators, manual_seed(px_seeds[j]));
+ *   px_state_out [n][626] (or NULL) receives the state after the message's D draws.
+ * Outputs: X [n][D] int64 (x_kind 0, the reference's X.long()) or uint8 (x_kind 1; values
+ *   outside 0..255 flag UQ_QFL_X_RANGE); exact_mask [n][D] u8; exact_vals [n][D] f32 with
+ *   message j's exact values compacted in index order in its first exact_count[j] entries;
+ *   scale [n] f32; info [n] int32 flags: UQ_QFL_BAD_P (some p outside [0, 1]: the reference's
+ *   bernoulli raises RuntimeError, e.g. an all-zero vector), UQ_QFL_BAD_INDEX (an index outside
+ *   [-numel, numel): torch.take raises IndexError), UQ_QFL_BAD_PX (a table p outside [0, 1]),
+ *   UQ_QFL_X_RANGE.  h_len must be 1..256; workspace: uq_quicfl_workspace_bytes. */
+#define UQ_QFL_BAD_P 1
+#define UQ_QFL_BAD_INDEX 2
+#define UQ_QFL_BAD_PX 4
+#define UQ_QFL_X_RANGE 8
+#define UQ_QFL_STATE_WORDS 626
+int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out);
+int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
+                           const float* table_xp, int64_t table_numel, int32_t h_len, float delta,
+                           const int32_t* prng_seeds, const uint32_t* px_state, const int32_t* px_seeds,
+                           uint32_t* px_state_out, void* X, int32_t x_kind, uint8_t* exact_mask, float* exact_vals,
+                           int32_t* exact_count, float* scale, int32_t* info, void* ws, size_t ws_bytes, void* stream);
+/* xxHash64 of `len` bytes (AS:457 hashes str(seed) with seed 0); host-only, no GPU. */
+uint64_t uq_xxh64(const void* data, size_t len, uint64_t seed);
 int uq_eden_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out);
 int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
                          const int32_t* sign_row, uint8_t* bins, float* scale, void* ws, size_t ws_bytes,

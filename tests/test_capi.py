@@ -162,3 +162,32 @@ def test_pitched_entry_points_argument_errors(lib):
     assert lib.uq_type_unbiased_codes_ld_f32(p, p, 10, p, 10, p, 0, 10, 5, p, None, None, 1, wsp, 1 << 16, None) == 0
     assert lib.uq_codes_q_mean_ld_f32(p, 9, p, 10, p, p, 4, 10, 5, 4.0, 0, p, None) == -1       # ldc < d
     assert b"ldc" in lib.uq_last_error()
+
+
+def test_xxh64_and_quicfl_argument_checks(lib):
+    """uq_xxh64 (AS:457's hash, host-only) against the oracle's restatement; the sender's
+    host-side argument checks (no kernel launched)."""
+    from oracle import uq_quicfl as Q
+    for s in (0, 1, 42, 99, 123, -3, 10 ** 12):
+        b = str(s).encode()
+        assert lib.uq_xxh64(b, len(b), 0) == Q.xxh64(b)
+    for n in range(0, 70, 3):
+        b = bytes((i * 7 + 3) & 255 for i in range(n))
+        assert lib.uq_xxh64(b, len(b), 0) == Q.xxh64(b)
+    sz = ctypes.c_size_t()
+    assert lib.uq_quicfl_workspace_bytes(4, 1000, ctypes.byref(sz)) == 0 and sz.value >= 4 * 1024 * 5
+    args = [None, 1, 1000, None, None, None, 64 * 3, 64, 0.5, None, None, None, None, None, 0, None, None, None,
+            None, None, None, 0, None]
+    bad = list(args)
+    bad[7] = 300                                   # h_len > 256
+    assert lib.uq_quicfl_compress_f32(*bad) == -1
+    bad = list(args)
+    bad[6] = 100                                   # numel not a multiple of h_len
+    assert lib.uq_quicfl_compress_f32(*bad) == -1
+    bad = list(args)
+    bad[14] = 2                                    # x_kind
+    assert lib.uq_quicfl_compress_f32(*bad) == -1
+    assert lib.uq_quicfl_compress_f32(*args) == -1  # null pointers
+    empty = list(args)
+    empty[1] = 0
+    assert lib.uq_quicfl_compress_f32(*empty) == 0  # an empty batch is a no-op

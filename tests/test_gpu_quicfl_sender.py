@@ -1,0 +1,205 @@
+"""GPU: the QUIC-FL sender (AS:429-503) and the QUICFL_quantize drop-in (AS:814-832) through the
+C ABI (uq_quicfl_compress_f32), bit for bit against the reference's own outputs on synthetic
+sender tables (tests/golden/make_golden_quicfl_sender.py) and against the oracle
+(oracle/uq_quicfl.py) on batches; sender -> GPU receiver round trips."""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import uq_eden as E
+from oracle import uq_quicfl as Q
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+sys.path.insert(0, HERE)
+from quicfl_tables import DATA, SR_BITS, data_txt, sender_tables  # noqa: E402
+
+
+def gen(kind, seed, dim):
+    rs = np.random.RandomState(seed)
+    if kind == "normal":
+        v = rs.normal(0, 1, dim)
+    elif kind == "laplace":
+        v = rs.laplace(1, 2, dim)
+    elif kind == "zeros":
+        v = np.zeros(dim)
+    elif kind == "spike":
+        v = rs.normal(0, 1, dim)
+        v[dim // 3] = 3000.0
+    return v.astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def fx(gpu_ready):
+    meta = json.load(open(os.path.join(HERE, "quicfl_sender_vectors.json")))
+    z = np.load(os.path.join(HERE, "quicfl_sender_vectors.npz"))
+    rmeta = json.load(open(os.path.join(HERE, "quicfl_recv_vectors.json")))
+    rz = np.load(os.path.join(HERE, "quicfl_recv_vectors.npz"))
+    return meta, z, rmeta, rz
+
+
+def senders(meta):
+    import uqdme
+    out = {}
+    for tag in ("pub", "small", "oor"):
+        tabs = {}
+        for b in (1, 2, 3, 4):
+            dd = dict(DATA[b])
+            x_len = None
+            if tag != "pub":
+                x_len = meta[tag]["x_len"]
+                dd.update(x_len=x_len, delta=meta[tag]["delta"])
+            X, p = sender_tables(b, x_len=x_len)
+            tabs[b] = (X, p, dd)
+        out[tag] = uqdme.QuicFLSender(tables=tabs)
+    return out
+
+
+def set_global(gseed, pre):
+    torch.manual_seed(gseed)
+    if pre:
+        torch.rand(pre)
+
+
+def state_words():
+    import uqdme_amd.quicfl as q
+    return q.generator_words(torch.default_generator)[1]
+
+
+def test_sender_matches_reference(fx):
+    import uqdme
+    meta, z, rmeta, rz = fx
+    snd = senders(meta)
+    rx = uqdme.QuicFLReceiver(tables={b: rz[f"recv{b}"] for b in (1, 2, 3, 4)})
+    checked = 0
+    for c in meta["cases"]:
+        k = c["idx"]
+        x = z[f"x{k}"] if c.get("x_stored") else gen(c["kind"], c["vseed"], c["dim"])
+        set_global(c["gseed"], c["pre"])
+        before = state_words()
+        data = {"vec": torch.from_numpy(x), "seed": c["seed"], "nbits": c["nbits"], "rotation_seed": c["rotation_seed"]}
+        if "error" in c:
+            exc = {"RuntimeError": RuntimeError, "IndexError": IndexError}[c["error"]]
+            with pytest.raises(exc):
+                snd[c["tables"]].compress(data)
+            assert np.array_equal(state_words(), before), k          # nothing drawn: the reference raised first
+            continue
+        msg = snd[c["tables"]].compress(data)
+        assert msg["prng_seed"] == c["prng_seed"] and msg["dim"] == c["dim"] and msg["h_len"] == c["h_len"]
+        assert msg["X"].dtype == torch.int64 and msg["X"].is_cuda
+        assert np.array_equal(msg["X"].cpu().numpy(), z[f"X{k}"].astype(np.int64)), k
+        assert msg["exact_indeces"].dtype == torch.bool
+        assert np.array_equal(np.flatnonzero(msg["exact_indeces"].cpu().numpy()), z[f"ei{k}"]), k
+        assert msg["exact_values"].cpu().numpy().view(np.uint32).tolist() == z[f"ev{k}"].view(np.uint32).tolist(), k
+        assert msg["scale"].dim() == 0 and int(msg["scale"].cpu().numpy().view(np.uint32)) == c["scale_bits"], k
+        after = state_words()
+        assert (after[0], after[1]) == (c["left1"], c["next1"]) and np.array_equal(after[2:], z[f"st1_{k}"]), k
+        if c["tables"] == "pub":                                    # sender -> GPU receiver
+            out = rx.decompress(msg).cpu().numpy()
+            if f"rx{k}" in z.files:
+                assert out.view(np.uint32).tolist() == z[f"rx{k}"].view(np.uint32).tolist(), k
+            else:
+                assert hashlib.sha256(out.tobytes()).hexdigest() == c["rx_sha"], k
+                assert np.array_equal(out[z[f"rxpos{k}"]].view(np.uint32), z[f"rxs{k}"].view(np.uint32))
+        checked += 1
+    assert checked == 27
+
+
+def test_dropin_matches_reference(fx, tmp_path):
+    """QUICFL_quantize twice in a row from manual_seed(g), the tables under a prefix as the
+    reference reads them (sender tables synthetic, receiver tables the reference's)."""
+    import uqdme
+    meta, z, rmeta, rz = fx
+    for b in (1, 2, 3, 4):
+        fn = str(tmp_path / f"{b}_X_{SR_BITS[b]}_h_256_q_")
+        X, p = sender_tables(b)
+        torch.save(torch.from_numpy(X), fn + "sender_table_X.pt")
+        torch.save(torch.from_numpy(p), fn + "sender_table_p.pt")
+        torch.save(torch.from_numpy(rz[f"recv{b}"]), fn + "recv_table.pt")
+        open(fn + "data.txt", "w").write(data_txt(b))
+    uqdme.set_tables_prefix(str(tmp_path))
+    try:
+        for c in meta["dropin"]:
+            j = c["idx"]
+            torch.manual_seed(c["gseed"])
+            for t in range(2):
+                out = uqdme.QUICFL_quantize(z[f"dx{j}"], c["nbits"])
+                assert isinstance(out, np.ndarray) and out.dtype == np.float32 and out.shape == (c["dim"],)
+                assert out.view(np.uint32).tolist() == z[f"dout{j}_{t}"].view(np.uint32).tolist(), (j, t)
+            w = state_words()
+            assert (w[0], w[1]) == (c["left1"], c["next1"]) and np.array_equal(w[2:], z[f"dst1_{j}"])
+    finally:
+        uqdme.set_tables_prefix(None)
+
+
+def test_missing_tables_raise_like_the_reference(tmp_path):
+    import uqdme
+    with pytest.raises(FileNotFoundError):
+        uqdme.QuicFLSender(prefix=str(tmp_path) + "/")
+
+
+def _oracle_row(x, nbits, seed, rot, tX, tp, dd, gstate):
+    return Q.compress(x, nbits, seed, rot, tX, tp, dd["delta"], dd["h_len"], gstate)
+
+
+@pytest.mark.parametrize("nbits,n,dim", [(1, 6, 3000), (2, 3, 1 << 14), (4, 5, 4096), (3, 2, 70000)])
+def test_batch_matches_oracle(fx, nbits, n, dim):
+    """quicfl_compress over n rows (seeded generators per row for the bernoulli(p_X) draws),
+    uint8 X; and the batch receiver on its messages vs the receiver oracle."""
+    import uqdme
+    meta, z, rmeta, rz = fx
+    snd = senders(meta)["pub"]
+    rng = np.random.default_rng(nbits * 100 + n)
+    x = (rng.standard_normal((n, dim)) * rng.uniform(0.5, 3, (n, 1))).astype(np.float32)
+    seeds = [int(s) for s in rng.integers(0, 100, n)]
+    rots = [int(s) for s in rng.integers(0, 200, n)]
+    pxs = [int(s) for s in rng.integers(0, 2 ** 31, n)]
+    msg = uqdme.quicfl_compress(torch.from_numpy(x), nbits, seeds, rots, sender=snd, px_seeds=pxs)
+    assert msg.X.dtype == torch.uint8
+    tX, tp = sender_tables(nbits)
+    out = uqdme.quicfl_decompress_messages(msg, rz[f"recv{nbits}"]).cpu().numpy()
+    for j in range(n):
+        exp, _ = _oracle_row(x[j], nbits, seeds[j], rots[j], tX, tp, DATA[nbits], Q.seeded_state(pxs[j]))
+        assert np.array_equal(msg.X[j].cpu().numpy().astype(np.int64), exp["X"]), j
+        assert np.array_equal(msg.exact_mask[j].cpu().numpy(), exp["exact_indeces"]), j
+        cnt = int(msg.exact_count[j])
+        assert msg.exact_vals[j, :cnt].cpu().numpy().view(np.uint32).tolist() == exp["exact_values"].view(np.uint32).tolist()
+        assert np.float32(msg.scale[j].item()).view(np.uint32) == np.float32(exp["scale"]).view(np.uint32)
+        rec = E.quicfl_decompress(exp["X"], rz[f"recv{nbits}"], rmeta["tables"][str(nbits)]["h_len"], exp["prng_seed"],
+                                  exp["exact_indeces"], exp["exact_values"], exp["scale"], rots[j], dim)
+        assert out[j].view(np.uint32).tolist() == rec.view(np.uint32).tolist(), j
+
+
+def test_batch_states_and_many_messages(fx):
+    """px_states from generators at arbitrary positions (left/next off the block edge), and a
+    batch above 256 messages (the sequential-chain norm instead of the segmented one)."""
+    import uqdme
+    import uqdme_amd.quicfl as q
+    meta, z, rmeta, rz = fx
+    snd = senders(meta)["pub"]
+    n, dim, nbits = 300, 16384, 2
+    rng = np.random.default_rng(7)
+    x = rng.laplace(1, 2, (n, dim)).astype(np.float32)
+    seeds = [int(s) for s in rng.integers(0, 10 ** 6, n)]
+    states = np.empty((n, 626), np.uint32)
+    g = torch.Generator()
+    for j in range(n):
+        g.manual_seed(int(j * 7919 + 1))
+        pre = int(rng.integers(0, 2000))
+        if pre:
+            torch.rand(pre, generator=g)
+        states[j] = q.generator_words(g)[1]
+    msg, new = q.quicfl_compress(torch.from_numpy(x), nbits, seeds, [123] * n, sender=snd, px_states=states,
+                                 _state_out=True)
+    tX, tp = sender_tables(nbits)
+    for j in list(range(0, n, 37)) + [n - 1]:
+        st = (int(states[j, 0]), int(states[j, 1]), states[j, 2:])
+        exp, gst = _oracle_row(x[j], nbits, seeds[j], 123, tX, tp, DATA[nbits], st)
+        assert np.array_equal(msg.X[j].cpu().numpy().astype(np.int64), exp["X"]), j
+        assert np.float32(msg.scale[j].item()).view(np.uint32) == np.float32(exp["scale"]).view(np.uint32), j
+        assert (new[j, 0], new[j, 1]) == (gst[0], gst[1]) and np.array_equal(new[j, 2:], gst[2]), j

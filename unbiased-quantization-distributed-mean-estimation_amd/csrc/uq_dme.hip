@@ -2039,6 +2039,7 @@ codes_mean_kernel(const int8_t* __restrict__ codes, int64_t ldc, const float* __
 #include "uq_biased_kernels.h"
 #include "uq_biased_torch_ties.h"
 #include "uq_eden_kernels.h"
+#include "uq_quicfl_kernels.h"
 #include "uq_codec_kernels.h"
 
 // ---- host-side helpers ---------------------------------------------------------------
@@ -3295,6 +3296,111 @@ int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbit
     FwhtArgs r = a;                                                                  // AS:378-413
     r.scale = scale;
     return launch_fwht(r, n, true, buf, out, st, nullptr, kFwhtLowBits);
+}
+
+// ---- QUIC-FL sender ----------------------------------------------------------------------
+// Workspace: the EDEN layout (rotated vectors, norms, segmented-norm region) + h [n][D] u8.
+static size_t quicfl_h_off(int64_t n, int64_t dim) {
+    return (eden_layout(n, dim).total + 255) & ~(size_t)255;
+}
+
+int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
+    if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
+    if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
+    *bytes_out = quicfl_h_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D;
+    return UQ_OK;
+}
+
+int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
+                           const float* table_xp, int64_t table_numel, int32_t h_len, float delta,
+                           const int32_t* prng_seeds, const uint32_t* px_state, const int32_t* px_seeds,
+                           uint32_t* px_state_out, void* X, int32_t x_kind, uint8_t* exact_mask, float* exact_vals,
+                           int32_t* exact_count, float* scale, int32_t* info, void* ws, size_t ws_bytes,
+                           void* stream) {
+    if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
+    if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 messages per call");
+    if (dim > ((int64_t)1 << 28)) return fail(UQ_E_INVALID, "dim must be <= 2^28");
+    if (h_len < 1 || h_len > 256) return fail(UQ_E_INVALID, "h_len must be 1..256");
+    if (table_numel < h_len || table_numel % h_len) return fail(UQ_E_INVALID, "table_numel must be a multiple of h_len");
+    if (x_kind != 0 && x_kind != 1) return fail(UQ_E_INVALID, "x_kind must be 0 (int64) or 1 (uint8)");
+    if (n == 0 || dim == 0) return UQ_OK;
+    if (!x || !signs || !table_xp || !prng_seeds || !X || !exact_mask || !exact_vals || !exact_count || !scale || !info)
+        return fail(UQ_E_INVALID, "null pointer");
+    if (!px_state && !px_seeds) return fail(UQ_E_INVALID, "px_state or px_seeds is required");
+    const EdenLayout w = eden_layout(n, dim);
+    const size_t hoff = quicfl_h_off(n, dim);
+    if (!ws || ws_bytes < hoff + (size_t)n * (size_t)w.D) return fail(UQ_E_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* wsb = (char*)ws;
+    FwhtArgs a;
+    float* rot = nullptr;
+    int rc = eden_front(x, n, dim, EdenTables{}, signs, sign_row, w, wsb, a, &rot, st);     // AS:460-470
+    if (rc) return rc;
+    QflSendArgs q{};
+    q.rot = rot;
+    q.nrm = (const float*)(wsb + w.nrm_off);
+    q.tab = (const float2*)table_xp;
+    q.numel = table_numel;
+    q.half = ((table_numel / h_len) - 1) * h_len / 2;                                        // AS:443
+    q.h_len = h_len;
+    q.delta = delta;
+    q.sqrtD = (float)std::sqrt((double)w.D);                                                  // np.sqrt(D) -> f32
+    q.prng_seeds = prng_seeds;
+    q.px_state = px_state;
+    q.px_seeds = px_seeds;
+    q.px_state_out = px_state_out;
+    q.hbuf = (uint8_t*)(wsb + hoff);
+    q.X = X;
+    q.x_kind = x_kind;
+    q.mask = exact_mask;
+    q.ev = exact_vals;
+    q.ecount = exact_count;
+    q.scale = scale;
+    q.info = info;
+    q.D = w.D;
+    hipLaunchKernelGGL(quicfl_send_kernel, dim3((unsigned)n), dim3(kQfT), 0, st, q);
+    return hip_check(hipGetLastError(), "quicfl_send_kernel launch");
+}
+
+// xxHash64 (the public XXH64 algorithm), for AS:457's prng seed
+static inline uint64_t xxh_rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static inline uint64_t xxh_read64(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
+static inline uint32_t xxh_read32(const uint8_t* p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
+
+uint64_t uq_xxh64(const void* data, size_t len, uint64_t seed) {
+    const uint64_t P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165667B19E3779F9ull,
+                   P4 = 0x85EBCA77C2B2AE63ull, P5 = 0x27D4EB2F165667C5ull;
+    auto round = [&](uint64_t acc, uint64_t lane) { return xxh_rotl(acc + lane * P2, 31) * P1; };
+    const uint8_t* p = (const uint8_t*)data;
+    const uint8_t* end = p + len;
+    uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        while (p + 32 <= end) {
+            v1 = round(v1, xxh_read64(p));
+            v2 = round(v2, xxh_read64(p + 8));
+            v3 = round(v3, xxh_read64(p + 16));
+            v4 = round(v4, xxh_read64(p + 24));
+            p += 32;
+        }
+        h = xxh_rotl(v1, 1) + xxh_rotl(v2, 7) + xxh_rotl(v3, 12) + xxh_rotl(v4, 18);
+        for (uint64_t v : {v1, v2, v3, v4}) h = (h ^ round(0, v)) * P1 + P4;
+    } else {
+        h = seed + P5;
+    }
+    h += (uint64_t)len;
+    for (; p + 8 <= end; p += 8) h = xxh_rotl(h ^ round(0, xxh_read64(p)), 27) * P1 + P4;
+    if (p + 4 <= end) {
+        h = xxh_rotl(h ^ ((uint64_t)xxh_read32(p) * P1), 23) * P2 + P3;
+        p += 4;
+    }
+    for (; p < end; ++p) h = xxh_rotl(h ^ ((uint64_t)*p * P5), 11) * P1;
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    h ^= h >> 32;
+    return h;
 }
 
 }  // extern "C"

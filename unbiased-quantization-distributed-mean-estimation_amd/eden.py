@@ -63,6 +63,17 @@ def _sign_rows(seeds: torch.Tensor, D: int, dev):
                 _sign_cache[key] = tab
         return tab, seeds_cpu.to(torch.int32).to(dev)
     uniq, inv = torch.unique(seeds_cpu, return_inverse=True)
+    if uniq.numel() <= 4:                 # a few other seeds (e.g. QUIC-FL's fixed 123, AS:822): cached too
+        key = (dev.index, D, tuple(uniq.tolist()))
+        with _cache_lock:
+            tab = _sign_cache.get(key)
+            if tab is None:
+                if len(_sign_cache) > 64:
+                    for k in [k for k in _sign_cache if len(k) == 3][:32]:
+                        del _sign_cache[k]
+                tab = rht_signs(uniq, D, dev)
+                _sign_cache[key] = tab
+        return tab, inv.to(torch.int32).to(dev)
     return rht_signs(uniq, D, dev), inv.to(torch.int32).to(dev)
 
 

@@ -1,33 +1,268 @@
-"""QUIC-FL receiver on the GPU — SURVEY §8(f) row 2 (baseline), the half the reference pins.
+"""QUIC-FL on the GPU — SURVEY §8(f) row 2 (baseline): sender, receiver and the drop-in.
 
-    QuicFLReceiver(device=..., bits=[1, 2, 3, 4], sr_bits=[6, 5, 4, 4], prefix=.../tables/)
-        mirrors NMSE_Results/Codes/All_Schemes.py:507-535: receiver tables loaded from the
-        reference's tables/ directory (torch.load(weights_only=True)), decompress(data) takes
-        the sender's message dict and returns vec[:dim].
+    QuicFLSender(device=..., bits=[1, 2, 3, 4], sr_bits=[6, 5, 4, 4], prefix=.../tables/)
+        mirrors NMSE_Results/Codes/All_Schemes.py:429-503: per bit width the sender tables
+        `<b>_X_<s>_h_256_q_sender_table_X.pt` / `..._p.pt` (torch.load(weights_only=True)) and
+        `data.txt` (ast.literal_eval, not eval); compress(data) returns the reference's message
+        dict and draws its bernoulli(p_X) words from torch's global CPU generator, which it
+        leaves where the reference would.
+    QuicFLReceiver(...)    AS:507-535, decompress(data) -> vec[:dim] on the GPU.
+    QUICFL_quantize(input_vector, bits_per_dimension=1)
+        AS:814-832: one torch.randint(0, 100) draw of the global CPU generator, compress,
+        decompress, NumPy f32 result.  Tables come from `set_tables_prefix()` /
+        $UQDME_QUICFL_TABLES (the reference reads its own tables/ directory).
+    quicfl_compress(x[n, d], nbits, seeds, rotation_seeds, sender=...)  -> QuicFLMessages
     quicfl_decompress(X[n, D], nbits, prng_seeds, rotation_seeds, scale[n], dim, recv_table)
-        the same for a batch: (exact ? exact value : recv_table[X * h_len + h]) / scale, inverse
-        RHT, [:dim], with h = torch.randint(0, h_len, (D,)) of a CPU generator seeded with
-        prng_seed (MT19937 word % h_len).
 
-Bit-identical to the reference's QuicFLReceiver.decompress (tests/golden/quicfl_recv_vectors.*).
-The sender (QuicFLSender, AS:429-505) is not provided: its tables
-(tables/*_sender_table_X.pt, *_sender_table_p.pt) are missing from the reference, whose drivers
-crash at their first QUIC-FL call (Normal_dist.py:141), so no sender output can be pinned.
+Bit-identical to the reference's QuicFLSender.compress (X, exact_indeces, exact_values, scale,
+the global generator's state after the call) on synthetic sender tables
+(tests/golden/quicfl_sender_vectors.*), and to its QuicFLReceiver.decompress on its own
+receiver tables (tests/golden/quicfl_recv_vectors.*).  The published sender tables are not in
+the reference, so outputs on them remain unpinned.
 """
 from __future__ import annotations
 
 import ast
+import ctypes
 import os
+import struct
+import threading
+from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from . import _lib
-from .eden import padded_dim, randomized_inverse_hadamard_transform
-from .quantizer import _device, _ptr, _stream_ptr
+from .eden import _sign_rows, padded_dim, randomized_inverse_hadamard_transform
+from .quantizer import _as_device_f32_2d, _device, _ptr, _stream_ptr, _workspace
 
-__all__ = ["QuicFLReceiver", "quicfl_decompress"]
+__all__ = ["QuicFLReceiver", "QuicFLSender", "QuicFLMessages", "QUICFL_quantize", "quicfl_compress",
+           "quicfl_decompress", "quicfl_decompress_messages", "prng_seed", "set_tables_prefix"]
+
+STATE_WORDS = 626                  # UQ_QFL_STATE_WORDS: (left, next, 624 words)
+_FLAG_P, _FLAG_INDEX, _FLAG_PX, _FLAG_X = 1, 2, 4, 8
+_tables_prefix = None
+_dropin_lock = threading.Lock()
+_dropin: dict = {}
 
 
+def set_tables_prefix(prefix) -> None:
+    """Directory (with trailing separator or not) holding the QUIC-FL tables the drop-in
+    QUICFL_quantize loads, as the reference's `str(path) + '/tables/'` (AS:431, AS:509)."""
+    global _tables_prefix
+    _tables_prefix = None if prefix is None else os.path.join(str(prefix), "")
+
+
+def default_tables_prefix() -> str:
+    if _tables_prefix is not None:
+        return _tables_prefix
+    env = os.environ.get("UQDME_QUICFL_TABLES")
+    if env:
+        return os.path.join(env, "")
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "tables", "")
+
+
+def prng_seed(seed) -> int:
+    """AS:457: xxh64(str(seed)).intdigest() % 2^16 (xxHash64 in the C library)."""
+    b = str(seed).encode()
+    return int(_lib.load().uq_xxh64(b, len(b), 0)) % (1 << 16)
+
+
+# ---- torch CPU generator state <-> (left, next, 624 words) --------------------------------------
+def generator_words(gen: torch.Generator):
+    """(get_state() bytes, uint32 [626] = left, next, state words) of a CPU generator."""
+    st = gen.get_state().numpy().copy()
+    _, left, _, nxt = struct.unpack_from("<QiiQ", st.tobytes(), 0)
+    out = np.empty(STATE_WORDS, np.uint32)
+    out[0], out[1] = left, nxt
+    out[2:] = np.frombuffer(st[24:24 + 624 * 8].tobytes(), dtype=np.uint64).astype(np.uint32)
+    return st, out
+
+
+def set_generator_words(gen: torch.Generator, st: np.ndarray, words: np.ndarray) -> None:
+    b = bytearray(st.tobytes())
+    struct.pack_into("<i", b, 8, int(words[0]))
+    struct.pack_into("<Q", b, 16, int(words[1]))
+    b[24:24 + 624 * 8] = np.asarray(words[2:], np.uint32).astype(np.uint64).tobytes()
+    gen.set_state(torch.frombuffer(bytearray(b), dtype=torch.uint8).clone())
+
+
+def _check_state(words: np.ndarray) -> None:
+    left, nxt = int(words[0]), int(words[1])
+    if not 1 <= left <= 624 or (left > 1 and nxt != 625 - left):
+        raise ValueError("generator state with left/next outside ATen mt19937's invariant")
+
+
+# ---- sender ------------------------------------------------------------------------------------------
+class QuicFLSender:
+    """AS:429-503 with the same constructor arguments and compress(data) contract."""
+
+    def __init__(self, device=None, bits=(1, 2, 3, 4), sr_bits=(6, 5, 4, 4), prefix=None, tables=None):
+        self.device = device if device is not None else _device()
+        self.sender_table_X, self.sender_table_p, self.data, self.half_table_size = {}, {}, {}, {}
+        self._xp = {}
+        if tables is not None:                      # {nbits: (table_X, table_p, data dict)}
+            for b, (tx, tp, dd) in tables.items():
+                self._add(int(b), torch.as_tensor(tx, dtype=torch.float32), torch.as_tensor(tp, dtype=torch.float32),
+                          dict(dd))
+        else:
+            prefix = default_tables_prefix() if prefix is None else prefix
+            for b, s in zip(bits, sr_bits):
+                fn = f"{prefix}{b}_X_{s}_h_256_q_"
+                self._add(b, *self.sender_table(fn, self.device))
+
+    def _add(self, b, tx, tp, dd):
+        if tx.numel() != tp.numel():
+            raise ValueError("sender_table_X and sender_table_p differ in size")
+        self.sender_table_X[b], self.sender_table_p[b], self.data[b] = tx, tp, dd
+        h = int(dd["h_len"])
+        self.half_table_size[b] = ((tx.numel() // h) - 1) * h // 2                      # AS:443
+
+    @staticmethod
+    def sender_table(prefix, device=None):
+        """AS:447-451 with safe loaders: torch.load(weights_only=True), ast.literal_eval."""
+        tx = torch.load(prefix + "sender_table_X.pt", weights_only=True).to(torch.float32)
+        tp = torch.load(prefix + "sender_table_p.pt", weights_only=True).to(torch.float32)
+        with open(prefix + "data.txt") as f:
+            dd = ast.literal_eval(f.read())
+        return tx, tp, dd
+
+    def table_xp(self, nbits: int, dev) -> torch.Tensor:
+        """(X, p) pairs [numel, 2] f32 on the device (one 8-byte gather per coordinate)."""
+        key = (nbits, dev.index)
+        t = self._xp.get(key)
+        if t is None:
+            t = torch.stack([self.sender_table_X[nbits].reshape(-1), self.sender_table_p[nbits].reshape(-1)], 1)
+            t = t.to(dev).contiguous()
+            self._xp[key] = t
+        return t
+
+    def compress(self, data, generator: torch.Generator | None = None):
+        """AS:455-503.  The bernoulli(p_X) words come from `generator` (default: torch's
+        global CPU generator, as the reference on CPU) and advance it by D words."""
+        nbits = data["nbits"]
+        dd = self.data[nbits]                                          # KeyError like AS:465
+        vec = data["vec"]
+        v = vec.detach() if torch.is_tensor(vec) else torch.as_tensor(np.asarray(vec))
+        v = v.reshape(1, -1)
+        if v.shape[1] == 0:
+            raise ValueError("empty vector (the reference's RHT and norm of an empty vector are degenerate)")
+        gen = generator if generator is not None else torch.default_generator
+        st, words = generator_words(gen)
+        msg, new = quicfl_compress(v, nbits, [data["seed"]], [data["rotation_seed"]], sender=self,
+                                   px_states=words[None, :], x_dtype=torch.int64, _state_out=True)
+        set_generator_words(gen, st, new[0])
+        cnt = int(msg.exact_count[0])
+        return {
+            "X": msg.X[0],
+            "exact_values": msg.exact_vals[0, :cnt],
+            "exact_indeces": msg.exact_mask[0],
+            "seed": data["seed"],
+            "prng_seed": int(msg.prng_seeds[0]),
+            "rotation_seed": data["rotation_seed"],
+            "dim": int(v.shape[1]),
+            "scale": msg.scale[0],
+            "nbits": nbits,
+            "h_len": dd["h_len"],
+        }
+
+
+@dataclass
+class QuicFLMessages:
+    X: torch.Tensor             # [n, D] uint8 or int64
+    exact_mask: torch.Tensor    # [n, D] bool (exact_indeces)
+    exact_vals: torch.Tensor    # [n, D] f32, row j's exact values in its first exact_count[j] entries
+    exact_count: torch.Tensor   # [n] int32 (host)
+    scale: torch.Tensor         # [n] f32
+    prng_seeds: torch.Tensor    # [n] int64 (host)
+    rotation_seeds: torch.Tensor
+    dim: int
+    nbits: int
+    h_len: int
+
+    def exact_dense(self) -> torch.Tensor:
+        """[n, D] f32: each message's exact values at their coordinates, 0 elsewhere."""
+        n, D = self.exact_mask.shape
+        dense = torch.zeros((n, D), dtype=torch.float32, device=self.exact_vals.device)
+        keep = torch.arange(D, device=self.exact_vals.device)[None, :] < self.exact_count.to(self.exact_vals.device)[:, None]
+        dense[self.exact_mask] = self.exact_vals[keep]
+        return dense
+
+
+def _ws(n, d, dev):
+    b = ctypes.c_size_t(0)
+    _lib.check(_lib.load().uq_quicfl_workspace_bytes(n, d, ctypes.byref(b)), "uq_quicfl_workspace_bytes")
+    return _workspace(dev, int(b.value))
+
+
+def quicfl_compress(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSender, px_seeds=None, px_states=None,
+                    x_dtype=torch.uint8, _state_out: bool = False):
+    """QuicFLSender.compress (AS:455-503) for every row of x [n, d].  seeds: the messages'
+    `seed` (hashed to the local generator's seed, AS:457); rotation_seeds: the RHT seeds.
+    The bernoulli(p_X) draws (AS:489) of message j come from a fresh generator seeded with
+    px_seeds[j], or from px_states[j] ([626] = left, next, state words of a torch CPU
+    generator, see generator_words).  X is returned as uint8 (x_dtype=torch.uint8, values
+    outside 0..255 raise) or int64 (the reference's X.long())."""
+    dev = _device()
+    dd = sender.data[nbits]
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    D = padded_dim(d)
+    s = [int(v) for v in torch.as_tensor(seeds).reshape(-1).tolist()] if not isinstance(seeds, (list, tuple)) else list(seeds)
+    rs = torch.as_tensor(rotation_seeds, dtype=torch.int64).reshape(-1)
+    if len(s) != n or rs.numel() != n:
+        raise ValueError("one seed and one rotation seed per message")
+    ps = torch.tensor([prng_seed(v) for v in s], dtype=torch.int64)
+    if x_dtype not in (torch.uint8, torch.int64):
+        raise ValueError("x_dtype must be torch.uint8 or torch.int64")
+    X = torch.empty((n, D), dtype=x_dtype, device=dev)
+    mask = torch.empty((n, D), dtype=torch.bool, device=dev)
+    ev = torch.empty((n, D), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    scale = torch.empty(n, dtype=torch.float32, device=dev)
+    info = torch.zeros(n, dtype=torch.int32, device=dev)
+    st_in = st_out = pxs = None
+    if px_states is not None:
+        w = np.asarray(px_states, np.uint32).reshape(n, STATE_WORDS)
+        for r in w:
+            _check_state(r)
+        st_in = torch.from_numpy(w.view(np.int32).copy()).to(dev)
+        st_out = torch.empty_like(st_in)
+    else:
+        if px_seeds is None:
+            raise ValueError("px_seeds or px_states is required")
+        pxs = torch.as_tensor(px_seeds, dtype=torch.int64).reshape(-1)
+        if pxs.numel() != n:
+            raise ValueError("one px seed per message")
+        pxs = (pxs & 0xFFFFFFFF).to(torch.int64)
+        pxs = torch.where(pxs >= 1 << 31, pxs - (1 << 32), pxs).to(torch.int32).to(dev)
+    if n and d:
+        tab, rows = _sign_rows(rs, D, dev)
+        xp = sender.table_xp(nbits, dev)
+        ws = _ws(n, d, dev)
+        _lib.check(_lib.load().uq_quicfl_compress_f32(
+            _ptr(x), n, d, _ptr(tab), _ptr(rows), _ptr(xp), xp.shape[0], int(dd["h_len"]),
+            float(np.float32(dd["delta"])), _ptr(ps.to(torch.int32).to(dev)), _ptr(st_in), _ptr(pxs), _ptr(st_out),
+            _ptr(X), 0 if x_dtype == torch.int64 else 1, _ptr(mask), _ptr(ev), _ptr(cnt), _ptr(scale), _ptr(info),
+            _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_quicfl_compress_f32")
+        flags = int(np.bitwise_or.reduce(info.cpu().numpy()))
+        if flags & _FLAG_P:
+            raise RuntimeError("Expected p_in >= 0 && p_in <= 1 to be true, but got false.")   # AS:484 bernoulli
+        if flags & _FLAG_INDEX:
+            raise IndexError("out of range: a sender-table index outside the table (AS:486 torch.take)")
+        if flags & _FLAG_PX:
+            raise RuntimeError("Expected p_in >= 0 && p_in <= 1 to be true, but got false.")   # AS:489 bernoulli
+        if flags & _FLAG_X:
+            raise OverflowError("X outside 0..255: use x_dtype=torch.int64")
+    msg = QuicFLMessages(X=X, exact_mask=mask, exact_vals=ev, exact_count=cnt.cpu(), scale=scale, prng_seeds=ps,
+                         rotation_seeds=rs, dim=d, nbits=nbits, h_len=int(dd["h_len"]))
+    if _state_out:
+        new = st_out.cpu().numpy().view(np.uint32) if st_out is not None else None
+        return msg, new
+    return msg
+
+
+# ---- receiver ----------------------------------------------------------------------------------------
 def quicfl_decompress(X, nbits: int, prng_seeds, rotation_seeds, scale, dim: int, recv_table, h_len: int | None = None,
                       exact_mask=None, exact_vals=None) -> torch.Tensor:
     """Batched QuicFLReceiver.decompress (AS:526-535).  X [n, D] integers in [0, rows) with D a
@@ -71,6 +306,12 @@ def quicfl_decompress(X, nbits: int, prng_seeds, rotation_seeds, scale, dim: int
     return randomized_inverse_hadamard_transform(pre, rs)[:, :dim]
 
 
+def quicfl_decompress_messages(msg: QuicFLMessages, recv_table) -> torch.Tensor:
+    """The receiver (AS:526-535) on every message of a quicfl_compress batch -> [n, dim]."""
+    return quicfl_decompress(msg.X, msg.nbits, msg.prng_seeds, msg.rotation_seeds, msg.scale, msg.dim, recv_table,
+                             msg.h_len, msg.exact_mask, msg.exact_dense())
+
+
 class QuicFLReceiver:
     """AS:507-535 with the same constructor arguments and decompress(data) contract."""
 
@@ -81,10 +322,9 @@ class QuicFLReceiver:
             for b, t in tables.items():
                 self.recv_table[int(b)] = torch.as_tensor(t, dtype=torch.float32)
         else:
-            if prefix is None:
-                raise ValueError("prefix: the reference's tables/ directory (AS:509)")
+            prefix = default_tables_prefix() if prefix is None else prefix
             for b, s in zip(bits, sr_bits):
-                fn = os.path.join(prefix, f"{b}_X_{s}_h_256_q_")
+                fn = f"{prefix}{b}_X_{s}_h_256_q_"
                 self.recv_table[b] = self.receiver_table(fn, self.device)
 
     @staticmethod
@@ -105,10 +345,42 @@ class QuicFLReceiver:
         mask = vals = None
         ei = data.get("exact_indeces")
         if ei is not None and bool(torch.as_tensor(ei).any()):
-            mask = torch.as_tensor(ei).reshape(1, D).to(torch.bool)
-            vals = torch.zeros((1, D), dtype=torch.float32)
-            vals[mask] = torch.as_tensor(data["exact_values"], dtype=torch.float32).reshape(-1).cpu()
+            dev = _device()
+            mask = torch.as_tensor(ei).reshape(1, D).to(device=dev, dtype=torch.bool)
+            vals = torch.zeros((1, D), dtype=torch.float32, device=dev)
+            vals[mask] = torch.as_tensor(data["exact_values"], dtype=torch.float32).reshape(-1).to(dev)
         out = quicfl_decompress(X, data["nbits"], [int(data["prng_seed"])], [int(data["rotation_seed"])],
                                 [float(torch.as_tensor(data["scale"]))], int(data["dim"]),
                                 self.recv_table[int(data["nbits"])], int(data["h_len"]), mask, vals)
         return out.view(-1)
+
+
+def _dropin_pair():
+    prefix = default_tables_prefix()
+    dev = _device()
+    key = (prefix, dev.index)
+    with _dropin_lock:
+        pair = _dropin.get(key)
+        if pair is None:
+            pair = (QuicFLSender(device=dev, prefix=prefix), QuicFLReceiver(device=dev, prefix=prefix))
+            _dropin[key] = pair
+    return pair
+
+
+def QUICFL_quantize(input_vector, bits_per_dimension=1):
+    """Drop-in for AS:814-832 (same name for the drivers' result keys): one torch.randint(0, 100)
+    draw of the global CPU generator (the message seed), compress (bernoulli(p_X) from the same
+    generator), decompress; returns a NumPy f32 array of length d."""
+    dev = _device()
+    if torch.is_tensor(input_vector):
+        v = input_vector.detach().to(device=dev, dtype=torch.float32).reshape(-1)
+    else:
+        v = torch.tensor(np.asarray(input_vector), dtype=torch.float32, device=dev).reshape(-1)
+    sender, receiver = _dropin_pair()
+    data = {"vec": v, "seed": int(torch.randint(0, 100, (1,)).item()), "nbits": bits_per_dimension,
+            "rotation_seed": 123, "nlevels": 2 ** bits_per_dimension}
+    data = sender.compress(data)
+    out = receiver.decompress(data)
+    host = torch.empty(out.numel(), dtype=torch.float32, pin_memory=True)
+    host.copy_(out)
+    return host.numpy()
