@@ -91,13 +91,18 @@ class CpuPipe:
     """torch-CPU stand-in for DMEPipeline (test infrastructure): q = a fixed function of x
     (the quantizer is not what these tests check), est (+)= q[j] / n_div in client order."""
 
-    def __init__(self, n, d):
+    def __init__(self, n, d, pipeline="codes"):
         self.q = torch.zeros(n, d)
         self.est = torch.zeros(d)
         self.fold = cpu_fold
+        self.pipeline = pipeline
+        self.means = 0
 
-    def step(self, x, X, n_div, accumulate=False, *, est=None, events=None, pipeline=None):
+    def step(self, x, X, n_div, accumulate=False, *, est=None, events=None, pipeline=None, mean=True):
         self.q.copy_(torch.round(x * 4) / 4 + X[:, None])
+        if not mean:
+            return None
+        self.means += 1
         out = self.est if est is None else est
         out.copy_(cpu_fold(self.q, n_div, None))
         return out
@@ -126,6 +131,10 @@ def _sharded_dme_worker(rank, world, port, n_total, d, mode, outdir):
             sh.drain()
             if rank == 0:
                 np.save(os.path.join(outdir, f"est_{k}.npy"), est.numpy())
+        if mode == "ordered":
+            assert sh.pipe.means == 0                         # the chain folds q; no wasted mean kernel
+            with pytest.raises(ValueError):                  # an encode step writes no q to fold
+                sh.step(x[lo:hi].contiguous(), X[lo:hi].contiguous(), pipeline="encode")
     finally:
         dist.destroy_process_group()
 
@@ -150,3 +159,52 @@ def test_sharded_dme_protocol_multi_rank(world, mode, n_total):
                 assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
             else:
                 np.testing.assert_allclose(got, ref, rtol=0, atol=8 * np.finfo(np.float32).eps * np.abs(ref).max())
+
+
+def _overlap_worker(rank, world, port, n_total, d, steps, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from uqdme_amd.distributed import ShardedDME
+        lo, hi = shard_range(n_total, world, rank)
+        got = {}
+        sh = ShardedDME(hi - lo, d, n_total, mode="reduce", pipe=CpuPipe(hi - lo, d), overlap=True,
+                        on_complete=lambda k, est: got.__setitem__(k, est.clone()))
+        ref = ShardedDME(hi - lo, d, n_total, mode="reduce", pipe=CpuPipe(hi - lo, d), overlap=False)
+        assert sh.overlap and len(sh.est_bufs) == 2 and not ref.overlap
+        sync = []
+        bufs = []
+        for k in range(steps):                              # step k >= 2 reuses step k-2's buffer
+            g = torch.Generator().manual_seed(300 + k)
+            x = torch.randn(n_total, d, generator=g)
+            X = torch.rand(n_total, generator=g)
+            est = sh.step(x[lo:hi].contiguous(), X[lo:hi].contiguous())
+            bufs.append(est.data_ptr())
+            if k >= 2:
+                assert k - 2 in got                         # reduce k-2 completed before its buffer was reused
+            sync.append(ref.step(x[lo:hi].contiguous(), X[lo:hi].contiguous()).clone())
+        sh.drain()
+        assert sorted(got) == list(range(steps)) and all(s is None for s in sh.pending)
+        assert bufs[0] == bufs[2] and bufs[1] == bufs[3] and bufs[0] != bufs[1]
+        if rank == 0:
+            for k in range(steps):
+                np.save(os.path.join(outdir, f"ov_{k}.npy"), got[k].numpy())
+                np.save(os.path.join(outdir, f"sy_{k}.npy"), sync[k].numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 9), (3, 10)])
+def test_sharded_dme_overlapped_reduce_multi_rank(world, n_total):
+    """The two-buffer asynchronous reduce ShardedDME uses over RCCL (bench --gpus N), run with
+    gloo's async reduce on host tensors at world 2-3 over five steps: every step's est on dst
+    (taken by on_complete when its reduce is waited for, before step k+2 reuses the buffer)
+    equals the synchronous path's bit for bit (Normal_dist.py:137-138 per round)."""
+    d, steps = 257, 5
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_overlap_worker, args=(world, free_port(), n_total, d, steps, td), nprocs=world, join=True)
+        for k in range(steps):
+            ov = np.load(os.path.join(td, f"ov_{k}.npy"))
+            sy = np.load(os.path.join(td, f"sy_{k}.npy"))
+            assert np.array_equal(ov.view(np.uint32), sy.view(np.uint32)), k

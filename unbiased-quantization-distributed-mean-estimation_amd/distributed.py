@@ -135,17 +135,23 @@ class ShardedDME:
                       asynchronously and runs beside step k+1's kernels: two estimate buffers
                       alternate, and step k+2 waits (stream-ordered, the host does not block)
                       for reduce k before it overwrites that buffer.  est of step k is valid on
-                      `dst` after the next-but-one step or drain().
+                      `dst` once reduce k is waited for: at step k+2, or drain().  on_complete(k,
+                      est) is called right then (before the buffer is reused), so a caller can
+                      take every step's estimate (copies enqueued there are stream-ordered after
+                      the reduce).
       mode "ordered": the bit-exact chain of sharded_client_mean over q's column blocks
-                      (pipeline must write q).
-    With gloo (CPU tests, ranks sharing one GPU) the reduce is host-staged and synchronous.
+                      (the pipeline must write q; its own mean kernel is skipped).
+    With gloo and device tensors (ranks sharing one GPU) the reduce is host-staged and
+    synchronous; with gloo and host tensors (the CPU tests' stand-in pipeline) overlap=True runs
+    the same two-buffer protocol with gloo's async reduce.
     `pipe` replaces the HIP pipeline by any object with its interface (est, q, step(x, X,
     n_div, est=, events=, pipeline=), probe_outputs, check_status): the CPU multi-process
     tests run this protocol with a torch-CPU stand-in."""
 
     def __init__(self, n_local: int, d: int, n_total: int, bits_per_dimension=1, *, m: int | None = None,
                  torch_threads: int = 1, pipeline: str = "codes", mode: str = "reduce", dst: int = 0, group=None,
-                 overlap: Optional[bool] = None, block: int = 1 << 18, device=None, pipe=None):
+                 overlap: Optional[bool] = None, block: int = 1 << 18, device=None, pipe=None,
+                 on_complete: Optional[Callable[[int, torch.Tensor], None]] = None):
         if mode not in ("reduce", "ordered"):
             raise ValueError("mode must be 'reduce' or 'ordered'")
         if mode == "ordered" and pipeline == "encode":
@@ -160,13 +166,23 @@ class ShardedDME:
         self.world = dist.get_world_size(group) if self.dist_on else 1
         self.rank = dist.get_rank(group) if self.dist_on else 0
         rccl = self.dist_on and dist.get_backend(group) == "nccl"
+        host_gloo = self.dist_on and not rccl and not self.pipe.est.is_cuda      # async gloo on host tensors
         self.overlap = bool(rccl and mode == "reduce" and self.world > 1 if overlap is None else overlap)
-        if self.overlap and not (rccl and mode == "reduce"):
-            raise ValueError("overlap needs the RCCL (nccl) backend and mode 'reduce'")
+        if self.overlap and not ((rccl or host_gloo) and mode == "reduce"):
+            raise ValueError("overlap needs mode 'reduce' and RCCL (or gloo with host tensors)")
         self.est_bufs = [self.pipe.est, torch.empty_like(self.pipe.est)] if self.overlap else [self.pipe.est]
         self.fold = getattr(pipe, "fold", None)          # ordered chain's per-rank fold (default: HIP)
         self.pending = [None] * len(self.est_bufs)
+        self.pending_step = [None] * len(self.est_bufs)
+        self.on_complete = on_complete
         self.nstep = 0
+
+    def _complete(self, slot):
+        self.pending[slot].wait()
+        self.pending[slot] = None
+        k, self.pending_step[slot] = self.pending_step[slot], None
+        if self.on_complete is not None:
+            self.on_complete(k, self.est_bufs[slot])
 
     def probe_outputs(self, x_local, X_local, **kw):
         return self.pipe.probe_outputs(x_local, X_local, **kw)
@@ -174,19 +190,25 @@ class ShardedDME:
     def step(self, x_local, X_local, *, events=None, pipeline: Optional[str] = None):
         """Returns this step's est buffer (the global mean on `dst` once its reduce is done:
         immediately unless overlap; None off `dst` in mode "ordered")."""
+        pl = pipeline or getattr(self.pipe, "pipeline", None)
+        if self.mode == "ordered" and pl == "encode":
+            raise ValueError("mode 'ordered' folds q: an 'encode' step writes no q")
         slot = self.nstep % len(self.est_bufs)
+        k = self.nstep
         self.nstep += 1
         est = self.est_bufs[slot]
         if self.pending[slot] is not None:            # reduce of step k-2 still owns this buffer
-            self.pending[slot].wait()
-            self.pending[slot] = None
+            self._complete(slot)
         ev = list(events or (None,) * 5)
-        self.pipe.step(x_local, X_local, float(self.n_total), est=est, events=ev[:4], pipeline=pipeline)
+        ordered = self.mode == "ordered" and self.world > 1
+        self.pipe.step(x_local, X_local, float(self.n_total), est=est, events=ev[:4], pipeline=pipeline,
+                       mean=not ordered)
         if self.world > 1 or self.overlap:            # (overlap at world 1: RCCL's no-op reduce, tests)
             if self.mode == "reduce":
                 if self.overlap:
                     self.pending[slot] = dist.reduce(est, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group,
                                                      async_op=True)
+                    self.pending_step[slot] = k
                 else:
                     _reduce(est, self.dst, self.group)
             else:
@@ -198,10 +220,9 @@ class ShardedDME:
 
     def drain(self):
         """Wait (stream-ordered) for every pending reduce."""
-        for i, w in enumerate(self.pending):
-            if w is not None:
-                w.wait()
-                self.pending[i] = None
+        order = sorted((k, i) for i, k in enumerate(self.pending_step) if k is not None)
+        for _, i in order:                            # oldest first, so on_complete sees steps in order
+            self._complete(i)
 
     def check_status(self):
         self.pipe.check_status()
@@ -211,8 +232,9 @@ def sharded_quantize_mean(x_local: torch.Tensor, bits_per_dimension, X_local, n_
                           mode: str = "reduce", dst: int = 0, torch_threads: int = 1, group=None,
                           return_q: bool = False):
     """Quantize this rank's clients (HIP) and form the global client mean: one ShardedDME
-    step (K1 -> K2 writing q and type codes -> mean from the codes -> one reduce, or the
-    ordered chain), with buffers allocated for this call (no placement probe).
+    step (K1 -> K2 writing q -> client mean of q -> one reduce, or the ordered chain), with
+    buffers allocated for this call (no placement probe; the same est bits as the codes
+    pipeline, without writing codes a one-shot caller never reads).
 
     x_local = the rank's contiguous client block (see shard_range); X_local = its
     slice of the per-client uniforms drawn once for all clients."""
@@ -221,8 +243,8 @@ def sharded_quantize_mean(x_local: torch.Tensor, bits_per_dimension, X_local, n_
     x_local = _as_device_f32_2d(x_local, dev)
     n_local, d = x_local.shape
     X_local = torch.as_tensor(X_local, dtype=torch.float32).reshape(-1).to(dev)
-    sh = ShardedDME(n_local, d, n_total, bits_per_dimension, torch_threads=torch_threads, mode=mode, dst=dst,
-                    group=group, overlap=False, device=dev)
+    sh = ShardedDME(n_local, d, n_total, bits_per_dimension, torch_threads=torch_threads, pipeline="q", mode=mode,
+                    dst=dst, group=group, overlap=False, device=dev)
     est = sh.step(x_local, X_local)
     if est is not None and mode == "reduce" and sh.rank != dst:
         est = None

@@ -79,7 +79,7 @@ class DMEPipeline:
     # ---- buffers ---------------------------------------------------------------------
     def _alloc_outputs(self):
         q = torch.empty((self.n, self.d), dtype=torch.float32, device=self.dev) if self.write_q else None
-        c = torch.empty((self.n, self.d), dtype=torch.int8, device=self.dev)
+        c = torch.empty((self.n, self.d), dtype=torch.int8, device=self.dev) if self.pipeline != "q" else None
         return q, c
 
     @staticmethod
@@ -103,6 +103,8 @@ class DMEPipeline:
         codes = (self.codes if codes is None else codes) if pl != "q" else None
         if pl != "encode" and q is None:
             raise ValueError("this pipeline holds no q buffer")
+        if pl != "q" and codes is None:
+            raise ValueError("this pipeline holds no codes buffer (pipeline 'q')")
         _lib.check(self.lib.uq_type_unbiased_codes_ld_f32(_p(x), _p(q), max(self._ld(q), self.d), _p(codes),
                                                           max(self._ld(codes), self.d),
                                                           _p(self.kmax if codes is not None else None), self.n, self.d,
@@ -130,11 +132,12 @@ class DMEPipeline:
         return est
 
     def step(self, x, X, n_div=None, accumulate: bool = False, *, est=None, events=None,
-             pipeline: str | None = None):
+             pipeline: str | None = None, mean: bool = True):
         """One pass of the hot path over the resident batch x[n, d] (f32, contiguous, on the
         device) with per-client uniforms X[n] (device f32).  Returns est (+)= sum_j q_j / n_div
         (into `est` when given, else the pipeline's own buffer).  `events`: four HIP events
-        recorded on the stream before K1, after K1, after K2 and after the mean."""
+        recorded on the stream before K1, after K1, after K2 and after the mean.  mean=False
+        stops after K2 (a caller folding q itself, e.g. ShardedDME's ordered chain)."""
         self._check(x, X)
         ev = events or (None, None, None, None)
         if ev[0] is not None:
@@ -145,7 +148,7 @@ class DMEPipeline:
         self.quantize(x, X, pipeline=pipeline)
         if ev[2] is not None:
             ev[2].record()
-        out = self.mean(self.n if n_div is None else n_div, accumulate, est=est, pipeline=pipeline)
+        out = self.mean(self.n if n_div is None else n_div, accumulate, est=est, pipeline=pipeline) if mean else None
         if ev[3] is not None:
             ev[3].record()
         return out
@@ -172,7 +175,7 @@ class DMEPipeline:
         self._check(x, X)
         self.l1_norms(x)
         sets, times = [(self.q, self.codes)], []
-        set_bytes = self.n * self.d * (5 if self.write_q else 1)
+        set_bytes = self.n * self.d * ((4 if self.write_q else 0) + (1 if self.pipeline != "q" else 0))
 
         def time_set(q, c):
             for _ in range(2):
