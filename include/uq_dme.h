@@ -39,6 +39,8 @@ extern "C" {
 
 /* Library ABI version (major*100 + minor). */
 int uq_version(void);
+/* SHA-256 (hex) of the sources and flags the library was built from (build_ext.build_id()). */
+const char* uq_build_id(void);
 
 /* Thread-local description of the last error returned on this thread. */
 const char* uq_last_error(void);
@@ -181,7 +183,9 @@ int uq_tc_decode(const uint8_t* msgs, size_t msgs_bytes, const uint64_t* offsets
  * bit2 = |Delta| > d (the reference's topk raises), bit3 = torch tie choice replayed,
  * bit4 = threshold digits 2-3 found on the compacted first-digit bucket (informational).
  * Workspace: uq_biased_workspace_bytes; zero-filled once before first use (it holds the
- * status word of uq_check_status, which reports an inconsistent tie replay). */
+ * status word of uq_check_status, which reports an inconsistent tie replay).  Its bytes
+ * 12..15 are reserved and must stay zero (the library never writes them; a nonzero value
+ * forces every tie replay onto its index-order fallback, which the tests use to exercise it). */
 #define UQ_TIES_TORCH 0
 #define UQ_TIES_LOWEST_INDEX 1
 int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t torch_threads, size_t* bytes_out);
@@ -209,7 +213,9 @@ int uq_rht_signs(const int32_t* seeds, int64_t rows, int64_t D, int8_t* signs, v
  *   inverse = 0: out [n][D] = H(pad(x[j], D) * diag) (HadamardSender.randomized_hadamard_transform,
  *                AS:123-141); x rows have length dim
  *   inverse = 1: out [n][D] = H(x[j]) * diag (HadamardReceiver, AS:146-153); dim must be D
- * bit-identical to the reference (f32 butterflies a + b, (a + b) - 2b; / f32(sqrt(D))). */
+ * bit-identical to the reference (f32 butterflies a + b, (a + b) - 2b; / f32(sqrt(D))).
+ * (It uses only the vector part of that workspace, not the norm's tables, so a smaller
+ * buffer passes the size check; uq_eden_workspace_bytes is always enough.) */
 int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inverse, const int8_t* signs,
                const int32_t* sign_row, void* ws, size_t ws_bytes, void* stream);
 /* uq_quicfl_prepare_f32: QuicFLReceiver.decompress (AS:526-532) up to its inverse RHT, for a

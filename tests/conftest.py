@@ -20,3 +20,15 @@ def gpu_ready():
     import uqdme
     uqdme.load_library()   # fails loudly if the extension is missing
     return True
+
+
+def pytest_report_header(config):
+    """The HIP library's build id (a SHA-256 of its sources and flags) in every test log."""
+    try:
+        import uqdme
+        from uqdme_amd import build_ext
+        lib = uqdme.load_library()
+        got = lib.uq_build_id().decode()
+        return [f"uqdme library build id: {got} ({'matches' if got == build_ext.build_id() else 'STALE vs'} sources)"]
+    except Exception as e:  # noqa: BLE001  (the header must never break collection)
+        return [f"uqdme library: not loaded ({e})"]

@@ -191,3 +191,11 @@ def test_xxh64_and_quicfl_argument_checks(lib):
     empty = list(args)
     empty[1] = 0
     assert lib.uq_quicfl_compress_f32(*empty) == 0  # an empty batch is a no-op
+
+
+def test_build_id_matches_sources(lib):
+    """The loaded binary was built from the current sources and flags (content hash, not
+    file times: build_ext.needs_build rebuilds on any mismatch)."""
+    from uqdme_amd import build_ext
+    assert lib.uq_build_id().decode() == build_ext.build_id()
+    assert not build_ext.needs_build()

@@ -7,6 +7,7 @@ Output: unbiased-quantization-distributed-mean-estimation_amd/_build/libuq_dme.s
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -34,25 +35,45 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+HEADER = os.path.join(PKG_DIR, "..", "include", "uq_dme.h")
+ID_FILE = SO + ".build_id"
+
+
+def build_id() -> str:
+    """SHA-256 over the library's sources (csrc/*, include/uq_dme.h) and the compile flags:
+    the identity of the binary they produce.  The library reports the id it was built from
+    (uq_build_id), so a stale binary is detected by content, not by file times."""
+    h = hashlib.sha256()
+    csrc = os.path.join(PKG_DIR, "csrc")
+    for f in sorted(os.listdir(csrc)) + [None]:
+        path = HEADER if f is None else os.path.join(csrc, f)
+        h.update((os.path.basename(path) + "\0").encode())
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    h.update("\0".join(HIPCC_FLAGS).encode())
+    return h.hexdigest()
+
+
 def needs_build() -> bool:
-    if not os.path.exists(SO):
+    if not os.path.exists(SO) or not os.path.exists(ID_FILE):
         return True
-    deps = [os.path.join(PKG_DIR, "csrc", f) for f in os.listdir(os.path.join(PKG_DIR, "csrc"))]
-    deps.append(os.path.join(PKG_DIR, "..", "include", "uq_dme.h"))
-    src_m = max(os.path.getmtime(f) for f in deps)
-    return os.path.getmtime(SO) < src_m
+    with open(ID_FILE) as f:
+        return f.read().strip() != build_id()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return SO
     os.makedirs(OUT_DIR, exist_ok=True)
+    bid = build_id()
     tmp = SO + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-o", tmp, SRC]
+    cmd = [hipcc(), *HIPCC_FLAGS, f'-DUQ_BUILD_ID="{bid}"', "-o", tmp, SRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, SO)
+    with open(ID_FILE, "w") as f:
+        f.write(bid + "\n")
     return SO
 
 

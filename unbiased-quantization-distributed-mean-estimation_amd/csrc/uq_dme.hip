@@ -2491,7 +2491,12 @@ int launch_torch_ties_rest(const float* x, int64_t d, const float* l1, float fm,
 
 extern "C" {
 
-int uq_version(void) { return 101; }
+int uq_version(void) { return 102; }
+
+#ifndef UQ_BUILD_ID
+#define UQ_BUILD_ID "unknown"
+#endif
+const char* uq_build_id(void) { return UQ_BUILD_ID; }
 
 const char* uq_last_error(void) { return g_err.c_str(); }
 
@@ -3110,7 +3115,9 @@ int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inver
     if (!x || !out || !signs) return fail(UQ_E_INVALID, "null pointer");
     const EdenLayout w = eden_layout(n, dim);
     if (inverse && dim != w.D) return fail(UQ_E_INVALID, "inverse RHT input length must be a power of two");
-    if (!ws || ws_bytes < w.total) return fail(UQ_E_WORKSPACE, "workspace too small");
+    // the transform uses the vector region only (no norm: the segmented-norm tables past
+    // seg_off are not needed here)
+    if (!ws || ws_bytes < w.seg_off) return fail(UQ_E_WORKSPACE, "workspace too small");
     FwhtArgs a{};
     a.in = x;
     a.signs = signs;
