@@ -9,6 +9,11 @@ ND = NMSE_Results/Codes/Normal_dist.py.  Per client, in order: EDEN_quantize_Had
 Type_biased_quantize(v, 1), (v, 2) (ND:139-140), all drawing from the global torch RNG seeded
 42, vectors from np.random seeded 42 (ND:14-15, 88-91), NMSE as ND:151-157.  The other
 schemes of the shipped loop are left out (QUIC-FL crashes: its sender tables are missing).
+Every EDEN call's rotation seed and scale (EdenSender.compress's output, AS:348: an MKL sdot,
+whose summation order is CPU-dependent) are recorded too, so the GPU test can check the rest of
+the EDEN path bit for bit with the reference's scale substituted, and the scale itself apart.
+Gamma, Bernoulli and Lognormal are the other drivers' generators (Gamma_dist.py:86,
+Bernoulli_dist.py:90, Lognormal_dist.py:90).
 """
 from __future__ import annotations
 
@@ -33,13 +38,27 @@ SCHEMES = [("eden", 1), ("eden", 2), ("unbiased", 1), ("unbiased", 2), ("biased"
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dim", type=int, default=2048)
+    ap.add_argument("--dists", default="normal,laplace,gamma,bernoulli,lognormal")
     a = ap.parse_args()
     DIM = a.dim
     torch.set_num_threads(1)
     fns = {"eden": AS.EDEN_quantize_Hadamard, "unbiased": AS.Type_unbiased_quantize,
            "biased": AS.Type_biased_quantize}
-    res = {}
-    for dist in ("normal", "laplace"):
+    gens = {"normal": lambda: np.random.normal(0, 1, DIM),
+            "laplace": lambda: np.random.laplace(loc=1, scale=2, size=DIM),
+            "gamma": lambda: np.random.gamma(shape=2, scale=2, size=DIM),
+            "bernoulli": lambda: np.random.choice(np.arange(2), size=DIM, p=[0.3, 0.7]),
+            "lognormal": lambda: np.random.lognormal(mean=1, sigma=2, size=DIM)}
+    seen = []                                       # every EdenSender.compress output, in call order
+    orig = AS.EdenSender.compress
+
+    def recording_compress(self, data):
+        out = orig(self, data)
+        seen.append((int(out["seed"]), int(np.float32(out["scale"].item()).view(np.uint32))))
+        return out
+    AS.EdenSender.compress = recording_compress
+    res, scales = {}, {}
+    for dist in a.dists.split(","):
         np.random.seed(42)
         torch.manual_seed(42)
         rows = []
@@ -47,16 +66,19 @@ def main():
             for inst in range(2):
                 vecs, norms = [], []
                 for _ in range(n):
-                    v = (np.random.normal(0, 1, DIM) if dist == "normal"
-                         else np.random.laplace(loc=1, scale=2, size=DIM))
+                    v = np.asarray(gens[dist](), dtype=np.float64)
                     norms.append(np.linalg.norm(v) ** 2)
                     vecs.append(torch.as_tensor(v, dtype=torch.float32))
                 vns = sum(norms)
                 emp = torch.stack(vecs).sum(dim=0) / n
                 est = {k: torch.zeros(DIM) for k in SCHEMES}
-                for v in vecs:
+                for j, v in enumerate(vecs):
                     for k in SCHEMES:
+                        del seen[:]
                         est[k] += torch.as_tensor(fns[k[0]](v, k[1])) / n
+                        if k[0] == "eden":
+                            assert len(seen) == 1
+                            scales.setdefault(dist, []).append([n, inst, j, k[1], seen[0][0], seen[0][1]])
                 row = {"n": n, "inst": inst}
                 for k in SCHEMES:
                     row[f"{k[0]}{k[1]}"] = float(torch.norm(est[k] - emp).pow(2) / (50 * vns * n))
@@ -65,7 +87,8 @@ def main():
         res[dist] = rows
     name = "nd_nmse_schemes.json" if DIM == 2048 else f"nd_nmse_schemes_d{DIM}.json"
     with open(os.path.join(HERE, name), "w") as f:
-        json.dump({"dim": DIM, "rows": res}, f, indent=1)
+        json.dump({"dim": DIM, "rows": res, "eden_scales_fields": ["n", "inst", "client", "bits", "seed", "scale_bits"],
+                   "eden_scales": scales}, f, indent=1)
 
 
 if __name__ == "__main__":

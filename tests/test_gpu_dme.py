@@ -104,8 +104,9 @@ def test_multi_scheme_nmse_known_answers(gpu_ready, fixture):
     from tests.golden_data import GOLDEN
     ref = json.load(open(os.path.join(GOLDEN, fixture)))
     for dist, rows in ref["rows"].items():
+        mine = {}
         res = uqdme.nmse_simulation(dist, dim=ref["dim"], users=(1, 6), num_instances=2,
-                                    schemes=("eden", "unbiased", "biased"), torch_threads=1)
+                                    schemes=("eden", "unbiased", "biased"), torch_threads=1, eden_scales_out=mine)
         for row in rows:
             ui = (1, 6).index(row["n"])
             for sc in ("eden", "unbiased", "biased"):
@@ -114,3 +115,24 @@ def test_multi_scheme_nmse_known_answers(gpu_ready, fixture):
                     exp = row[f"{sc}{r}"]
                     tol = 1e-5 if sc == "eden" and ref["dim"] > 2048 else 1e-6
                     assert abs(got - exp) <= tol * exp, (dist, row["n"], row["inst"], sc, r, got, exp)
+        if "eden_scales" not in ref:
+            continue
+        # EDEN with the reference's own scales (EdenSender.compress outputs): every other step
+        # is bit-exact, so the NMSE must be too; the scales themselves (an MKL sdot on the
+        # reference's side, fp64 here) agree within 2e-6 relative
+        theirs = {}
+        for n, inst, client, bits, seed, sbits in ref["eden_scales"][dist]:
+            theirs.setdefault((n, inst, bits), []).append(np.uint32(sbits).view(np.float32))
+        worst = 0.0
+        for key, sc_ref in theirs.items():
+            sc_ref = np.asarray(sc_ref, np.float32)
+            rel = np.abs(mine[key].astype(np.float64) - sc_ref) / np.abs(sc_ref)
+            worst = max(worst, float(rel.max()))
+        assert worst <= 2e-6, (dist, worst)
+        sub = uqdme.nmse_simulation(dist, dim=ref["dim"], users=(1, 6), num_instances=2, schemes=("eden",),
+                                    torch_threads=1, eden_scales=theirs)
+        for row in rows:
+            ui = (1, 6).index(row["n"])
+            for r in (1, 2):
+                got = np.float32(sub[("eden", r)]["script"][ui, row["inst"]])
+                assert got == np.float32(row[f"eden{r}"]), (dist, row["n"], row["inst"], r, got, row[f"eden{r}"])

@@ -1,7 +1,10 @@
 """Per-call latency of the drop-ins (one client per call, as the reference's callers use
-them): Type_unbiased_quantize, Type_biased_quantize, EDEN_quantize_Hadamard.
+them): Type_unbiased_quantize, Type_biased_quantize, EDEN_quantize_Hadamard.  "ms_per_call":
+48 calls back to back (host work overlapping the GPU), "ms_synced": each call waited for.
+Sizes: the reference harness's own (d = 1024 in C1, 2048 in Normal_dist.py:40), 4096, the
+largest single-launch size (32767) and GRAIN (32768), the FL model (172 554), 2^20, 2^22.
 
-    python tools/dropin_latency.py"""
+    python tools/dropin_latency.py [--dims 1024,2048]"""
 import json
 import os
 import sys
@@ -13,9 +16,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dims", default="1024,2048,4096,32767,32768,172554,1048576,4194304")
+    a = ap.parse_args()
     import uqdme
-    res = {}
-    for d in (172554, 1 << 20, 1 << 22):
+    res, synced = {}, {}
+    for d in [int(v) for v in a.dims.split(",")]:
         vs = [torch.randn(d, device="cuda") for _ in range(16)]     # different vectors: some have
         v = vs[0]                                                   # biased-quantizer threshold ties
         for name, f in (("Type_unbiased_quantize", uqdme.Type_unbiased_quantize),
@@ -30,8 +37,13 @@ def main():
                 y = f(vs[i % len(vs)], 1)
             torch.cuda.synchronize()
             res[f"{name}/d={d}"] = round((time.perf_counter() - t0) / k * 1e3, 4)
+            t0 = time.perf_counter()
+            for i in range(k):
+                y = f(vs[i % len(vs)], 1)
+                torch.cuda.synchronize()
+            synced[f"{name}/d={d}"] = round((time.perf_counter() - t0) / k * 1e3, 4)
             del y
-    print(json.dumps({"tool": "dropin_latency", "ms_per_call": res}))
+    print(json.dumps({"tool": "dropin_latency", "ms_per_call": res, "ms_synced": synced}))
 
 
 if __name__ == "__main__":

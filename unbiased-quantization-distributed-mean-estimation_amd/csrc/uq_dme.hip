@@ -1299,23 +1299,15 @@ __device__ __forceinline__ void store_tile(const float* s_data, float* __restric
 // Segments: workgroup b takes client b / nseg, tiles [s*seg_tiles, (s+1)*seg_tiles) with
 // s = b % nseg, starting from the exact P = pre[first tile] (the per-client fold of the
 // small-batch form) -- or from P = 0 over the whole vector when nseg == 1 (pre == nullptr).
+// The tile loop of one workgroup (tiles [tb, te) of client `vec` from the exact start P).
 template <bool WQ, bool WC, bool CVEC>
-__global__ void __launch_bounds__(kQBlock, 4)
-quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
-                       int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
-                       const float* __restrict__ Xs, float Xval, const float* __restrict__ l1, int32_t seg_tiles,
-                       int32_t nseg, const uint64_t* __restrict__ pre, int64_t ldo, int64_t ldc) {
-    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image of tile t (then scratch)
-    __shared__ __attribute__((aligned(16))) float s_o[kQTile];     // output image of tile t-1 / t
-    __shared__ float s_tab[kTab];
-    __shared__ ScanLds sl;
+__device__ __forceinline__ void stream_tiles(const float* __restrict__ x, float* __restrict__ out,
+                                             int8_t* __restrict__ codes, int32_t* __restrict__ overflow, int64_t d,
+                                             int32_t tb, int32_t te, float fm, float Xv, float L, int32_t nseg,
+                                             double P, int64_t ldo, int64_t ldc, int64_t vec, float* s_x, float* s_o,
+                                             float* s_tab, ScanLds& sl) {
     const int tid = threadIdx.x;
-    const int64_t vec = blockIdx.x / (uint32_t)nseg;
-    const int32_t tb = (int32_t)(blockIdx.x % (uint32_t)nseg) * seg_tiles;
-    const int32_t te = min(tiles, tb + seg_tiles);
-    const float L = l1[vec];
     const DivPlan dp = div_plan(L);
-    const float Xv = Xs ? Xs[vec] : Xval;            // one vector per call: X passed by value
     const uint32_t row_bytes = (uint32_t)(d * 4);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, row_bytes);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(WQ ? out + vec * ldo : x, row_bytes);
@@ -1323,7 +1315,6 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     TileRegs pre_x;
     load_tile_buf(pre_x, rx, (uint32_t)tb * (uint32_t)(kQTile * 4), tid);
     build_table(s_tab, tid, L, fm);
-    double P = pre ? __longlong_as_double((long long)pre[vec * tiles + tb]) : 0.0;
     uint32_t cw[4] = {0u, 0u, 0u, 0u};
     float kmax = 0.0f;
     for (int32_t tile = tb; tile < te; ++tile) {
@@ -1361,6 +1352,111 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
         else
             publish_kmax(kmax, L, overflow, vec, tid);
     }
+}
+
+template <bool WQ, bool WC, bool CVEC>
+__global__ void __launch_bounds__(kQBlock, 4)
+quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
+                       int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
+                       const float* __restrict__ Xs, float Xval, const float* __restrict__ l1, int32_t seg_tiles,
+                       int32_t nseg, const uint64_t* __restrict__ pre, int64_t ldo, int64_t ldc) {
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];     // input image of tile t (then scratch)
+    __shared__ __attribute__((aligned(16))) float s_o[kQTile];     // output image of tile t-1 / t
+    __shared__ float s_tab[kTab];
+    __shared__ ScanLds sl;
+    const int64_t vec = blockIdx.x / (uint32_t)nseg;
+    const int32_t tb = (int32_t)(blockIdx.x % (uint32_t)nseg) * seg_tiles;
+    const int32_t te = min(tiles, tb + seg_tiles);
+    const float Xv = Xs ? Xs[vec] : Xval;            // one vector per call: X passed by value
+    const double P = pre ? __longlong_as_double((long long)pre[vec * tiles + tb]) : 0.0;
+    stream_tiles<WQ, WC, CVEC>(x, out, codes, overflow, d, tb, te, fm, Xv, l1[vec], nseg, P, ldo, ldc, vec, s_x, s_o,
+                               s_tab, sl);
+}
+
+// torch CPU `x.abs().sum()` of one vector shorter than GRAIN (one cascade, the same for every
+// torch thread count; K1a + K1b's arithmetic with step 16) by one 256-thread workgroup, into
+// every thread.  scr: >= 64 * 32 + 64 floats of LDS.
+constexpr int64_t kSmallL1Max = kGrain - 1;
+__device__ float block_torch_l1(const float* __restrict__ xv, int64_t s, float* scr) {
+    const int tid = threadIdx.x;
+    float* leaf = scr;                               // [64 leaves][32 streams]
+    float* col = scr + 64 * 32;                      // [32] stream results, then [0] the sum
+    if (s < 8) {                                     // ATen scalar row_sum
+        if (tid == 0) {
+            float p[4] = {0.f, 0.f, 0.f, 0.f};
+            if (s >= 4)
+                for (int k = 0; k < 4; ++k) p[k] = 0.f + fabsf(xv[k]);
+            for (int64_t k = (s >= 4 ? 4 : 0); k < s; ++k) p[0] += fabsf(xv[k]);
+            col[0] = 0.0f + (((p[0] + p[1]) + p[2]) + p[3]);
+        }
+        __syncthreads();
+        const float r = col[0];
+        __syncthreads();
+        return r;
+    }
+    const int64_t vs = s / 8, rows = vs / 4;         // rows of 32 floats (8 lanes x 4 ILP)
+    const int nleaf = (int)(rows / 16);              // cascade step 16: rows < 1024
+    for (int b = tid >> 3; b < nleaf; b += kQBlock / 8) {     // level 0: leaf b, streams 4q..4q+3
+        const int q = tid & 7;
+        const float* p = xv + (int64_t)b * 16 * 32 + 4 * q;
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < 16; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) a[c] += fabsf(p[r * 32 + c]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) leaf[b * 32 + 4 * q + c] = a[c];
+    }
+    __syncthreads();
+    if (tid < 32) {                                  // levels 1-2 (a3 never fills below 4096 rows), open rows
+        float a1 = 0.f, a2 = 0.f, a0 = 0.f;
+        for (int b = 0; b < nleaf; ++b) {
+            a1 += leaf[b * 32 + tid];
+            if (((b + 1) & 15) == 0) {
+                a2 += a1;
+                a1 = 0.f;
+            }
+        }
+        for (int64_t r = (int64_t)nleaf * 16; r < rows; ++r) a0 += fabsf(xv[r * 32 + tid]);
+        col[tid] = ((a0 + a1) + a2) + 0.f;
+    }
+    __syncthreads();
+    if (tid == 0) {                                  // ILP vectors, leftover 8-vectors, tail (ATen order)
+        float p0[8];
+        for (int l = 0; l < 8; ++l) p0[l] = col[l];
+        for (int64_t v = rows * 4; v < vs; ++v)
+            for (int l = 0; l < 8; ++l) p0[l] += fabsf(xv[v * 8 + l]);
+        for (int k = 1; k < 4; ++k)
+            for (int l = 0; l < 8; ++l) p0[l] += col[k * 8 + l];
+        float acc = 0.f;
+        for (int64_t k = vs * 8; k < s; ++k) acc += fabsf(xv[k]);
+        for (int l = 0; l < 8; ++l) acc += p0[l];
+        col[0] = 0.0f + acc;                         // the two-pass reduction's 0 + chunk
+    }
+    __syncthreads();
+    const float r = col[0];
+    __syncthreads();
+    return r;
+}
+
+// The whole AS:609-641 for vectors shorter than GRAIN in ONE launch (the reference's own
+// harness sizes: d = 1024 in C1, 2048 in Normal_dist.py:40): one workgroup per client computes
+// L1 in torch order (or takes l1in), then streams its tiles exactly as quantize_stream_kernel.
+template <bool WQ, bool WC, bool CVEC>
+__global__ void __launch_bounds__(kQBlock, 4)
+quantize_small_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
+                      int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
+                      const float* __restrict__ Xs, float Xval, const float* __restrict__ l1in,
+                      float* __restrict__ l1out, int64_t ldo, int64_t ldc) {
+    __shared__ __attribute__((aligned(16))) float s_x[kQTile];
+    __shared__ __attribute__((aligned(16))) float s_o[kQTile];
+    __shared__ float s_tab[kTab];
+    __shared__ ScanLds sl;
+    const int64_t vec = blockIdx.x;
+    const float L = l1in ? l1in[vec] : block_torch_l1(x + vec * d, d, s_x);     // AS:624
+    if (l1out && threadIdx.x == 0) l1out[vec] = L;
+    const float Xv = Xs ? Xs[vec] : Xval;
+    stream_tiles<WQ, WC, CVEC>(x, out, codes, overflow, d, 0, tiles, fm, Xv, L, 1, 0.0, ldo, ldc, vec, s_x, s_o, s_tab,
+                               sl);
 }
 
 // ---- small-batch forms (fewer clients than fill the GPU one workgroup per client) ----
@@ -2430,6 +2526,61 @@ int torch_ties_prepare(int64_t n, int64_t d, RezState* state, uint32_t* bits, ch
     return hip_check(hipGetLastError(), "rez_tie_list_kernel launch");
 }
 
+// Captured KB7a level chains, per thread (streams and workspaces are per thread in practice):
+// keyed by (device, every pointer the chain's kernels take, d, slots, levels).  *exec =
+// nullptr when capture is unavailable (then the caller launches the chain directly).
+struct LevelPtrs {
+    const void *qbuf, *list, *tls, *cnt, *pos, *alist;
+    bool operator==(const LevelPtrs& o) const {
+        return qbuf == o.qbuf && list == o.list && tls == o.tls && cnt == o.cnt && pos == o.pos && alist == o.alist;
+    }
+};
+template <class F>
+int level_graph(const LevelPtrs& wsb, int64_t d, unsigned S, int levels, hipStream_t st, F&& launch,
+                hipGraphExec_t* exec) {
+    struct Entry {
+        int dev;
+        LevelPtrs wsb;
+        int64_t d;
+        unsigned S;
+        int levels;
+        hipGraphExec_t exec;
+    };
+    static thread_local Entry cache[8] = {};
+    static thread_local int next = 0;
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc) return rc;
+    for (const Entry& e : cache)
+        if (e.exec && e.dev == dev && e.wsb == wsb && e.d == d && e.S == S && e.levels == levels) {
+            *exec = e.exec;
+            return UQ_OK;
+        }
+    *exec = nullptr;
+    if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        return UQ_OK;                                   // not capturable here: launch directly
+    }
+    const int lrc = launch(st);
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(st, &g);
+    if (lrc) {
+        if (g) (void)hipGraphDestroy(g);
+        return lrc;
+    }
+    if ((rc = hip_check(ec, "end KB7a capture"))) return rc;
+    hipGraphExec_t ex = nullptr;
+    rc = hip_check(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0), "instantiate KB7a graph");
+    (void)hipGraphDestroy(g);
+    if (rc) return rc;
+    Entry& slot = cache[next];
+    next = (next + 1) % 8;
+    if (slot.exec) (void)hipGraphExecDestroy(slot.exec);
+    slot = Entry{dev, wsb, d, S, levels, ex};
+    *exec = ex;
+    return UQ_OK;
+}
+
 int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, float fm, RezState* state,
                       uint32_t* bits, char* wsb, const BiasedLayout& w, hipStream_t st, const TieLevelState** tls_out) {
     *tls_out = nullptr;
@@ -2461,13 +2612,30 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     int levels = 2;
     for (double r = (double)d; r > (double)kTieLevelStop; r *= 0.6) ++levels;
     uint32_t* alist = (uint32_t*)(wsb + w.alist_off);
-    for (int lv = 0; lv < levels; ++lv) {
-        hipLaunchKernelGGL(kt_pivot_kernel, dim3(1), dim3(kTieSlots), 0, st, d, qbuf, list, tls, (int)S, alist);
-        hipLaunchKernelGGL(kt_count_kernel, dim3(kTieGrid), dim3(256), 0, st, d, qbuf, tls, cnt, alist);
-        hipLaunchKernelGGL(kt_list_kernel, dim3(kTieGrid), dim3(256), 0, st, d, qbuf, pos, tls, cnt, alist);
-        hipLaunchKernelGGL(kt_jcut_kernel, dim3(S), dim3(kJcutThreads), 0, st, d, pos, tls, cnt, alist);
-        hipLaunchKernelGGL(kt_swap_kernel, dim3(kTieGrid), dim3(256), 0, st, d, qbuf, pos, tls, alist);
-        if ((rc = hip_check(hipGetLastError(), "KB7a level launch"))) return rc;
+    // the per-level launches take (active slot, segment) items, one per wave: S slots need at
+    // most S * kTieSegs / 4 workgroups (a one-client call launched 2048, 1984 of them idle)
+    const unsigned lgrid = (unsigned)std::min<int64_t>(kTieGrid, (int64_t)S * kTieSegs / 4);
+    auto levels_on = [&](hipStream_t ls) {
+        for (int lv = 0; lv < levels; ++lv) {
+            hipLaunchKernelGGL(kt_pivot_kernel, dim3(1), dim3(kTieSlots), 0, ls, d, qbuf, list, tls, (int)S, alist);
+            hipLaunchKernelGGL(kt_count_kernel, dim3(lgrid), dim3(256), 0, ls, d, qbuf, tls, cnt, alist);
+            hipLaunchKernelGGL(kt_list_kernel, dim3(lgrid), dim3(256), 0, ls, d, qbuf, pos, tls, cnt, alist);
+            hipLaunchKernelGGL(kt_jcut_kernel, dim3(S), dim3(kJcutThreads), 0, ls, d, pos, tls, cnt, alist);
+            hipLaunchKernelGGL(kt_swap_kernel, dim3(lgrid), dim3(256), 0, ls, d, qbuf, pos, tls, alist);
+        }
+        return hip_check(hipGetLastError(), "KB7a level launch");
+    };
+    // The level chain (~13 levels x 5 dependent launches, whether or not a client is listed)
+    // is replayed as a captured HIP graph: its arguments are workspace pointers, d and S
+    // only, so one capture serves every call on the same workspace (per-call host cost was
+    // ~65 launches, more than the chain's GPU time for a few-client call).
+    hipGraphExec_t exec = nullptr;
+    rc = level_graph(LevelPtrs{qbuf, list, tls, cnt, pos, alist}, d, S, levels, st, levels_on, &exec);
+    if (rc) return rc;
+    if (exec) {
+        if ((rc = hip_check(hipGraphLaunch(exec, st), "KB7a level graph launch"))) return rc;
+    } else if ((rc = levels_on(st))) {
+        return rc;
     }
     hipLaunchKernelGGL(kt_mark_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, d, qbuf, list, state, tls, bits);
     if ((rc = hip_check(hipGetLastError(), "kt_mark_kernel launch"))) return rc;
@@ -2564,6 +2732,25 @@ int unbiased_codes_impl(const float* x, float* out, int64_t ldo, int8_t* codes, 
     char* wsb = (char*)ws;
     float* l1buf = (float*)(wsb + w.l1_off);
     const float* l1use = l1;
+    const bool vec4s = aligned16(x) && (!out || aligned16(out)) && ((d % 4 == 0 && ldo % 4 == 0) || n == 1);
+    if (d <= kSmallL1Max && vec4s && n <= 0x7FFFFFFF) {
+        // shorter than GRAIN: L1 (one torch cascade for any thread count) and the exact scan
+        // in one workgroup per client, one launch
+        const float fm = (float)m;
+        const bool cv = !codes || (aligned16(codes) && d % 16 == 0 && (ldc % 16 == 0 || n == 1));
+        const int sl = (out ? 4 : 0) | (codes ? 2 : 0) | (cv ? 1 : 0);
+#define UQ_SMALL(Q, C, CV)                                                                                      \
+    case ((Q) * 4 + (C) * 2 + (CV)):                                                                          \
+        hipLaunchKernelGGL((quantize_small_kernel<Q, C, CV>), dim3((unsigned)n), dim3(kQBlock), 0, st, x, out, codes, \
+                           overflow, d, w.tiles, fm, X, Xval, l1, l1_out, ldo, ldc);                            \
+        break;
+        switch (sl) {
+            UQ_SMALL(1, 0, 1) UQ_SMALL(1, 1, 1) UQ_SMALL(1, 1, 0) UQ_SMALL(0, 1, 1) UQ_SMALL(0, 1, 0)
+            default: return fail(UQ_E_INVALID, "internal: bad kernel selector");
+        }
+#undef UQ_SMALL
+        return hip_check(hipGetLastError(), "quantize_small_kernel launch");      // (l1_out written there)
+    }
     if (!l1use) {
         rc = launch_l1(x, n, d, plan, (float*)(wsb + w.part_off), l1buf, st);
         if (rc) return rc;
@@ -3102,9 +3289,10 @@ int uq_quicfl_prepare_f32(const int32_t* X, int64_t n, int64_t D, const float* r
     if ((exact_mask == nullptr) != (exact_vals == nullptr)) return fail(UQ_E_INVALID, "exact_mask and exact_vals go together");
     if (h_len < 1 || table_rows < 1 || (int64_t)h_len * table_rows > kQflTab)
         return fail(UQ_E_INVALID, "receiver table must hold 1..1024 entries");
-    hipLaunchKernelGGL(quicfl_prepare_kernel, dim3((unsigned)n), dim3(640), 0, (hipStream_t)stream, X, D, recv_table,
-                       table_rows * h_len, h_len, prng_seeds, exact_mask, exact_vals, scale, out);
-    return hip_check(hipGetLastError(), "quicfl_prepare_kernel launch");
+    hipLaunchKernelGGL(quicfl_recv_wave_kernel, dim3((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)),
+                       dim3(64 * kQfWavesPerWG), 0, (hipStream_t)stream, X, n, D, recv_table, table_rows * h_len, h_len,
+                       prng_seeds, exact_mask, exact_vals, scale, out);
+    return hip_check(hipGetLastError(), "quicfl_recv_wave_kernel launch");
 }
 
 int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inverse, const int8_t* signs,
@@ -3365,8 +3553,10 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.scale = scale;
     q.info = info;
     q.D = w.D;
-    hipLaunchKernelGGL(quicfl_send_kernel, dim3((unsigned)n), dim3(kQfT), 0, st, q);
-    return hip_check(hipGetLastError(), "quicfl_send_kernel launch");
+    q.n = n;
+    hipLaunchKernelGGL(quicfl_send_wave_kernel, dim3((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)),
+                       dim3(64 * kQfWavesPerWG), 0, st, q);
+    return hip_check(hipGetLastError(), "quicfl_send_wave_kernel launch");
 }
 
 // xxHash64 (the public XXH64 algorithm), for AS:457's prng seed

@@ -1079,60 +1079,3 @@ eden_scale_kernel(const double* __restrict__ part, int32_t tiles, const float* _
     const float nv = nrm[vec];
     scale[vec] = (nv * nv) / (float)dot;                    // AS:335 norm ** 2 / dot
 }
-
-// ---- QUIC-FL receiver (AS:507-535), the half of QUIC-FL the reference's tables pin ------
-// QuicFLReceiver.decompress before its inverse RHT: h = torch.randint(0, h_len, (D,)) from a
-// CPU generator seeded with prng_seed (MT19937 word % h_len, verified against torch), then
-// v = recv_table[X * h_len + h] (torch.take), exact coordinates overwritten, v / scale (f32).
-// One workgroup per client runs the client's MT19937 stream (as rht_signs_kernel) and
-// emits 624 coordinates per twist; the table (<= 16 x 64 floats) sits in LDS.
-constexpr int kQflTab = 1024;
-__global__ void __launch_bounds__(640)
-quicfl_prepare_kernel(const int32_t* __restrict__ X, int64_t D, const float* __restrict__ table, int32_t tab_n,
-                      int32_t h_len, const int32_t* __restrict__ prng_seeds, const uint8_t* __restrict__ exact_mask,
-                      const float* __restrict__ exact_vals, const float* __restrict__ scale, float* __restrict__ out) {
-    __shared__ uint32_t mt[624];
-    __shared__ float tab[kQflTab];
-    const int tid = threadIdx.x;
-    const int64_t row = (int64_t)blockIdx.x * D;
-    for (int i = tid; i < tab_n; i += 640) tab[i] = table[i];
-    if (tid == 0) {
-        mt[0] = (uint32_t)prng_seeds[blockIdx.x];
-        for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
-    }
-    const float sc = scale[blockIdx.x];
-    __syncthreads();
-    auto twist_word = [&](int i) -> uint32_t {
-        const uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7FFFFFFFu);
-        return mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908B0DFu : 0u);
-    };
-    for (int64_t base = 0; base < D; base += 624) {
-        uint32_t nv = 0;
-        if (tid < 227) nv = twist_word(tid);
-        __syncthreads();
-        if (tid < 227) mt[tid] = nv;
-        __syncthreads();
-        if (tid >= 227 && tid < 454) nv = twist_word(tid);
-        __syncthreads();
-        if (tid >= 227 && tid < 454) mt[tid] = nv;
-        __syncthreads();
-        if (tid >= 454 && tid < 624) nv = twist_word(tid);
-        __syncthreads();
-        if (tid >= 454 && tid < 624) mt[tid] = nv;
-        __syncthreads();
-        const int64_t i = base + tid;
-        if (tid < 624 && i < D) {
-            uint32_t y = mt[tid];
-            y ^= y >> 11;
-            y ^= (y << 7) & 0x9D2C5680u;
-            y ^= (y << 15) & 0xEFC60000u;
-            y ^= y >> 18;
-            const uint32_t h = y % (uint32_t)h_len;                        // AS:528 randint
-            int64_t idx = (int64_t)X[row + i] * h_len + h;                 // AS:530 take
-            idx = idx < 0 ? 0 : (idx >= tab_n ? tab_n - 1 : idx);          // validated by the host
-            float v = tab[idx];
-            if (exact_mask && exact_mask[row + i]) v = exact_vals[row + i]; // AS:531
-            out[row + i] = v / sc;                                         // AS:532
-        }
-    }
-}

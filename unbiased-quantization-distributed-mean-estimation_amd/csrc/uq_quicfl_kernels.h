@@ -1,5 +1,6 @@
-// uq_quicfl_kernels.h — QUIC-FL sender.  Included by uq_dme.hip inside
-// its anonymous namespace, after uq_eden_kernels.h (the sender's RHT and norm are EDEN's).
+// uq_quicfl_kernels.h — QUIC-FL sender and receiver streams.  Included by
+// uq_dme.hip inside its anonymous namespace, after uq_eden_kernels.h (the RHT and the norm are
+// EDEN's).
 //
 // Reference (AS = NMSE_Results/Codes/All_Schemes.py), QuicFLSender.compress AS:455-503:
 //   AS:457      prng_seed = xxh64(str(seed)) % 2^16; local generator seeded with it
@@ -11,33 +12,33 @@
 //               after the D randint words, one word per element, 1 iff low24(w) * 2^-24 < p
 //   AS:486-490  idx = ((iq * h_len) + h) + half in f32, .long(); X = table_X[idx] +
 //               bernoulli(table_p[idx]) from the GLOBAL generator (one word per element), .long()
-// Kernel:
-//   KQ1 quicfl_send_kernel  one 640-thread workgroup per message.  Both generators run as
-//       MT19937 in LDS (double-buffered 624-word blocks: block b in buf[b & 1], so the words
-//       of blocks b - 1 and b are readable while b + 1 is twisted into the other buffer).
-//       Pass A: the local stream's first D words -> h (u8 scratch).  Pass B: 624 elements per
-//       round; the local stream (words D..2D-1) and the global stream twist together (three
-//       dependency phases each, one shared set of barriers), then each thread runs its
-//       element through AS:472-490; the (X, p) table gather is one 8-byte load.  The exact
-//       values are compacted in index order (wave ballots, per-wave counts written to LDS and
-//       consumed after the next barrier).  Barriers fence LDS only, so the next round's
-//       vector loads stay in flight across them.
-//   The global generator starts from ATen's mt19937 state (left, next, 624 words): the first
-//   left - 1 words are state[next ..], then twisted blocks; the state after the D draws is
-//   written back for the host to restore into torch's generator.
+// QuicFLReceiver.decompress AS:526-532 (before its inverse RHT): h from the same local stream,
+//   v = recv_table[X * h_len + h], exact overrides, v / scale.
+//
+// Both are serial in their MT19937 streams (ATen's mt19937: 624-word blocks, each twisted
+// from the previous), so the unit of parallelism is the message: ONE WAVE per message, no
+// workgroup barriers.  A wave twists a block in place in its LDS slice: word i needs
+// s[i], s[i+1] (old) and s[(i+397) % 624], which is old for i < 227 and new (written 227
+// words earlier) otherwise.  With 64 words per group, each group's operands lie >= 3 groups
+// back, so the wave reads every a/b operand up front and the c operands in three rounds
+// (groups 0-3, 4-6, 7-9); the wave's LDS operations stay in program order, so no barrier is
+// needed.  A 624-element round takes the words of its elements from the current block (slots
+// before the twist) and the next one (after it).
+//   KQ1 quicfl_send_wave_kernel     pass A: h = word % h_len (u8 scratch); pass B: the local
+//       stream (words D..2D-1) and the global stream side by side, each lane 10 elements of
+//       the round; the (X, p) table gather of round c is issued before round c-1 is finished
+//       (its X, exact flag and value stored then), so the gather latency overlaps a round of
+//       twisting.  Exact values are compacted in index order by wave ballots.
+//   KQ2 quicfl_recv_wave_kernel     the receiver's h stream and table lookup (LDS table).
+//   The global generator starts from ATen's state (left, next, 624 words): the first left - 1
+//   words are state[next ..], then twisted blocks; the state after the D draws is written back
+//   for the host to restore into torch's generator.
 
-constexpr int kQfT = 640;              // threads per sender workgroup (10 waves)
 constexpr int kMtN = 624;              // MT19937 state words
-constexpr int kQfWaves = kQfT / 64;
+constexpr int kMtGroups = 10;          // 64-word groups per block (the last one 48 words)
+constexpr int kQfWavesPerWG = 4;       // messages per workgroup (one wave each)
 constexpr float kQflExactT = 2.8856349124267573f;   // f32(norm.ppf(1 - 2^-9)) (AS:475-478)
 constexpr int kQfStateWords = 2 + kMtN;             // (left, next, words) per generator state
-
-// LDS-only barrier: orders LDS traffic between the waves without waiting for vector memory
-__device__ __forceinline__ void lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= y >> 11;
@@ -53,45 +54,71 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
     return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908B0DFu : 0u);
 }
 
+// torch's uniform in bernoulli: (w & 0xFFFFFF) * 2^-24 (computed in double, then compared with
+// the f32 p): both sides are exact f32 values, so the f32 comparison is the same test
+__device__ __forceinline__ float u24(uint32_t w) { return (float)(w & 0xFFFFFFu) * 0x1p-24f; }
+
 __device__ __forceinline__ void mt_seed(uint32_t* mt, uint32_t seed) {     // init_genrand, one lane
     mt[0] = seed;
     for (int i = 1; i < kMtN; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
 }
 
-// Twist block b of up to two streams (buf[b & 1] -> buf[(b + 1) & 1]).  Every thread calls
-// it with the same flags.  The buffer written must be free (a barrier since its last
-// readers); the call ends with a barrier, after which both blocks are readable.
-__device__ __forceinline__ void mt_twist2(uint32_t (*s0)[kMtN], int64_t b0, bool do0, uint32_t (*s1)[kMtN],
-                                          int64_t b1, bool do1, int tid) {
-    const uint32_t* o0 = s0[b0 & 1];
-    uint32_t* n0 = s0[(b0 + 1) & 1];
-    const uint32_t* o1 = s1[b1 & 1];
-    uint32_t* n1 = s1[(b1 + 1) & 1];
-    uint32_t a0 = 0, c0 = 0, d0 = 0, a1 = 0, c1 = 0, d1 = 0;
-    if (tid < kMtN) {
-        if (do0) { a0 = o0[tid]; c0 = tid + 1 < kMtN ? o0[tid + 1] : 0u; d0 = tid < 227 ? o0[tid + 397] : 0u; }
-        if (do1) { a1 = o1[tid]; c1 = tid + 1 < kMtN ? o1[tid + 1] : 0u; d1 = tid < 227 ? o1[tid + 397] : 0u; }
-    }
-    if (tid < 227) {                                            // from old words only
-        if (do0) n0[tid] = mt_mix(a0, c0, d0);
-        if (do1) n1[tid] = mt_mix(a1, c1, d1);
-    }
-    lds_sync();
-    if (tid >= 227 && tid < 454) {                              // reads new[tid - 227]
-        if (do0) n0[tid] = mt_mix(a0, c0, n0[tid - 227]);
-        if (do1) n1[tid] = mt_mix(a1, c1, n1[tid - 227]);
-    }
-    lds_sync();
-    if (tid >= 454 && tid < kMtN) {
-        if (tid < kMtN - 1) {
-            if (do0) n0[tid] = mt_mix(a0, c0, n0[tid - 227]);
-            if (do1) n1[tid] = mt_mix(a1, c1, n1[tid - 227]);
-        } else {                                                // the last word wraps to new[0]
-            if (do0) n0[tid] = mt_mix(a0, n0[0], n0[396]);
-            if (do1) n1[tid] = mt_mix(a1, n1[0], n1[396]);
+// Orders one wave's LDS accesses across lanes: the compiler sees single-lane addresses only
+// (s[i] and s[i + 1] never alias for ONE lane) and could otherwise move a read past another
+// lane's write; the wave's LDS operations themselves execute in program order.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One wave twists the block in s[624] in place (the sequential next_state's result).
+__device__ __forceinline__ void mt_twist_wave(uint32_t* s, int lane) {
+    uint32_t a[kMtGroups], b[kMtGroups], c[kMtGroups];
+#pragma unroll
+    for (int g = 0; g < kMtGroups; ++g) {                      // old a, b of every word
+        const int i = 64 * g + lane;
+        if (i < kMtN) {
+            a[g] = s[i];
+            b[g] = s[i + 1 < kMtN ? i + 1 : 0];                 // (i = 623 re-reads new s[0] below)
         }
     }
-    lds_sync();
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {                              // words 0..226: c = old s[i + 397]
+        const int i = 64 * g + lane;
+        if (i < 227) c[g] = s[i + 397];
+    }
+    wave_lds_fence();                                          // every old operand read before any write
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int i = 64 * g + lane;
+        if (i < 227) s[i] = mt_mix(a[g], b[g], c[g]);
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int g = 3; g < 7; ++g) {                              // words 227..447: c = new s[i - 227] (0..220)
+        const int i = 64 * g + lane;
+        if (i >= 227) c[g] = s[i - 227];
+    }
+#pragma unroll
+    for (int g = 3; g < 7; ++g) {
+        const int i = 64 * g + lane;
+        if (i >= 227) s[i] = mt_mix(a[g], b[g], c[g]);        // (writes 227..447, reads were 0..220)
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int g = 7; g < kMtGroups; ++g) {                      // words 448..623: c = new s[i - 227] (221..396)
+        const int i = 64 * g + lane;
+        if (i < kMtN) {
+            c[g] = s[i - 227];
+            if (i == kMtN - 1) b[g] = s[0];                    // the last word twists with the new s[0]
+        }
+    }
+#pragma unroll
+    for (int g = 7; g < kMtGroups; ++g) {
+        const int i = 64 * g + lane;
+        if (i < kMtN) s[i] = mt_mix(a[g], b[g], c[g]);        // (writes 448..623, reads were 0, 221..396)
+    }
+    wave_lds_fence();
 }
 
 struct QflSendArgs {
@@ -116,17 +143,26 @@ struct QflSendArgs {
     float* scale;               // [n]
     int32_t* info;              // [n] UQ_QFL_* flags
     int64_t D;
+    int64_t n;
 };
 
-__global__ void __launch_bounds__(kQfT)
-quicfl_send_kernel(QflSendArgs a) {
-    __shared__ uint32_t Ls[2][kMtN];      // local generator blocks
-    __shared__ uint32_t Gs[2][kMtN];      // global generator blocks
-    __shared__ int32_t wcnt[2][kQfWaves];
-    __shared__ int32_t sflags;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wv = tid >> 6;
-    const int64_t j = blockIdx.x;
+// Round state carried from stage 1 (words, flags, gather issued) to stage 2 (X, stores).
+struct QflRound {
+    float2 t[kMtGroups];
+    uint32_t wg[kMtGroups];
+    float v[kMtGroups];
+    uint32_t ex;                // bit k: element k of this lane is exact
+};
+
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_send_wave_kernel(QflSendArgs a) {
+    __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];      // local generator block per wave
+    __shared__ uint32_t Gsh[kQfWavesPerWG][kMtN];      // global generator block per wave
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    if (j >= a.n) return;                                       // whole wave: no barrier below
+    uint32_t* Ls = Lsh[wv];
+    uint32_t* Gs = Gsh[wv];
     const int64_t D = a.D;
     const int64_t row = j * D;
     int32_t gleft = 1, gnext = 0;
@@ -134,174 +170,265 @@ quicfl_send_kernel(QflSendArgs a) {
         const uint32_t* st = a.px_state + j * kQfStateWords;
         gleft = (int32_t)st[0];
         gnext = (int32_t)st[1];
-        for (int i = tid; i < kMtN; i += kQfT) Gs[0][i] = st[2 + i];
-    } else if (tid == 64) {
-        mt_seed(Gs[0], (uint32_t)a.px_seeds[j]);
+        for (int i = lane; i < kMtN; i += 64) Gs[i] = st[2 + i];
+    } else if (lane == 1) {
+        mt_seed(Gs, (uint32_t)a.px_seeds[j]);
     }
-    if (tid == 0) {
-        mt_seed(Ls[0], (uint32_t)a.prng_seeds[j]);
-        sflags = 0;
-    }
-    const float nv = a.nrm[j];
-    const float sc = (1.0f / nv) * a.sqrtD;                      // AS:466/470 (IEEE 1/x, then f32 mul)
-    lds_sync();
+    if (lane == 0) mt_seed(Ls, (uint32_t)a.prng_seeds[j]);
+    wave_lds_fence();
+    const float sc = (1.0f / a.nrm[j]) * a.sqrtD;              // AS:466/470 (IEEE 1/x, then f32 mul)
     const int64_t nch = (D + kMtN - 1) / kMtN;
-    const int h_len = a.h_len;
+    const uint32_t h_len = (uint32_t)a.h_len;
     uint8_t* hb = a.hbuf + row;
 
-    // ---- pass A: h = randint(0, h_len, (D,), local) (AS:465/469): word i is block c + 1, slot tid
-    int64_t haveL = 0;
-    // (no barrier before a twist here: the buffer it writes held block c - 1, whose last
-    // readers, round c - 2's lanes and round c - 1's twist, are behind that twist's barriers)
+    // ---- pass A: h = randint(0, h_len, (D,), local) (AS:465/469): word i is block c + 1, slot e
     for (int64_t c = 0; c < nch; ++c) {
-        mt_twist2(Ls, haveL, true, Gs, 0, false, tid);
-        ++haveL;
-        const int64_t i = c * kMtN + tid;
-        if (tid < kMtN && i < D) hb[i] = (uint8_t)(mt_temper(Ls[haveL & 1][tid]) % (uint32_t)h_len);
+        mt_twist_wave(Ls, lane);
+        const int64_t i0 = c * kMtN;
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            const int e = 64 * k + lane;
+            if (e < kMtN && i0 + e < D) hb[i0 + e] = (uint8_t)(mt_temper(Ls[e]) % h_len);
+        }
     }
+    int64_t haveL = nch;                                        // block in Ls
 
     // ---- pass B: local words D + i (virtual position 624 + D + i), global words i
     const int64_t vL = (int64_t)kMtN + D;
-    const int64_t qL = vL / kMtN, rL = vL % kMtN;
+    const int64_t qL = vL / kMtN;
+    const int rL = (int)(vL % kMtN);
     const int64_t vG = gleft > 1 ? (int64_t)gnext : (int64_t)kMtN;     // the first left - 1 words are state[next ..]
-    const int64_t qG = vG / kMtN, rG = vG % kMtN;
+    const int64_t qG = vG / kMtN;
+    const int rG = (int)(vG % kMtN);
     int64_t haveG = 0;
     const float thr = kQflExactT;
     const float fdelta = a.delta;
-    const float fh = (float)h_len;
+    const float fh = (float)a.h_len;
     const float fhalf = (float)a.half;
     const int64_t numel = a.numel;
     int32_t flags = 0;
-    int64_t etot = 0;                                            // exact values written so far
-    bool pend = false;                                           // an exact value of the previous round
-    float pend_v = 0.f;
-    int pend_rank = 0;
-    // loads of round c + 1 are issued before round c's twists
-    float r_cur = 0.f, r_nxt = 0.f;
-    uint32_t h_cur = 0, h_nxt = 0;
-    if (tid < kMtN && tid < D) {
-        r_cur = __builtin_nontemporal_load(a.rot + row + tid);
-        h_cur = hb[tid];
+    int64_t etot = 0;                                           // exact values written so far
+    QflRound pr;                                                // the previous round (stage 2 pending)
+    bool have_prev = false;
+    int64_t prev_i0 = 0;
+    float r_cur[kMtGroups], r_nxt[kMtGroups];
+    uint32_t h_cur[kMtGroups], h_nxt[kMtGroups];
+    // (every global load below is unconditional with a clamped index: a load under a per-element
+    // branch is waited for before the next one, which serialises a lane's ten loads)
+    const int64_t last = D - 1;
+#pragma unroll
+    for (int k = 0; k < kMtGroups; ++k) {
+        const int64_t e = 64 * k + lane < last ? 64 * k + lane : last;
+        r_cur[k] = __builtin_nontemporal_load(a.rot + row + e);
+        h_cur[k] = hb[e];
     }
+
+    auto finish = [&](const QflRound& r, int64_t i0) {          // stage 2 of a round (AS:489-490, 494-495)
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            const int e = 64 * k + lane;
+            const int64_t i = i0 + e;
+            const bool active = e < kMtN && i < D;
+            const bool ex = (r.ex >> k) & 1u;
+            if (active) {
+                const float2 t = r.t[k];
+                if (!(t.y >= 0.f && t.y <= 1.f)) flags |= UQ_QFL_BAD_PX;
+                const float bx = (u24(r.wg[k]) < t.y) ? 1.f : 0.f;
+                const float xf = t.x + bx;                           // AS:489
+                if (a.x_kind == 0) {
+                    int64_t xv = 0;
+                    if (xf > -9.2e18f && xf < 9.2e18f) xv = (int64_t)xf;  // AS:490 .long()
+                    else flags |= UQ_QFL_X_RANGE;
+                    __builtin_nontemporal_store(xv, (int64_t*)a.X + row + i);
+                } else {
+                    int32_t xv = 0;
+                    if (xf > -1.0f && xf < 256.0f) xv = (int32_t)xf;
+                    else flags |= UQ_QFL_X_RANGE;
+                    ((uint8_t*)a.X)[row + i] = (uint8_t)xv;
+                }
+                a.mask[row + i] = ex ? 1 : 0;
+            }
+            const uint64_t bal = __ballot(active && ex);        // index order: group k, then lane
+            if (active && ex) a.ev[row + etot + __popcll(bal & ((1ull << lane) - 1ull))] = r.v[k];
+            etot += __popcll(bal);
+        }
+    };
+
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t i0 = c * kMtN;
-        const int64_t i = i0 + tid;
-        const bool active = tid < kMtN && i < D;
-        const int64_t in = i + kMtN;
-        if (tid < kMtN && in < D) {
-            r_nxt = __builtin_nontemporal_load(a.rot + row + in);
-            h_nxt = hb[in];
+        const int lastE = (int)((D - 1 - i0) < (kMtN - 1) ? (D - 1 - i0) : (kMtN - 1));
+        // next round's loads first
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            const int64_t in = i0 + kMtN + 64 * k + lane;
+            const int64_t ic = in < last ? in : last;
+            r_nxt[k] = __builtin_nontemporal_load(a.rot + row + ic);
+            h_nxt[k] = hb[ic];
         }
-        lds_sync();                                              // round c-1's readers are done
-        if (pend) {                                              // round c-1's exact values, in index order
-            int64_t base = etot;
-            for (int w = 0; w < wv; ++w) base += wcnt[(c - 1) & 1][w];
-            a.ev[row + base + pend_rank] = pend_v;
+        // the words of this round: slots rX + e of blocks qX + c (before) and qX + c + 1 (after)
+        while (haveL < qL + c) { mt_twist_wave(Ls, lane); ++haveL; }
+        while (haveG < qG + c) { mt_twist_wave(Gs, lane); ++haveG; }
+        uint32_t wl[kMtGroups], wg[kMtGroups];
+        // (slot p = rX + e: p < 624 before the twist, p - 624 after; reads unconditional)
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            const int e = 64 * k + lane;
+            wl[k] = Ls[rL + e < kMtN ? rL + e : 0];
+            wg[k] = Gs[rG + e < kMtN ? rG + e : 0];
         }
-        if (c) {
-            for (int w = 0; w < kQfWaves; ++w) etot += wcnt[(c - 1) & 1][w];
+        if (rL + lastE >= kMtN) {
+            mt_twist_wave(Ls, lane);
+            ++haveL;
+#pragma unroll
+            for (int k = 0; k < kMtGroups; ++k) {
+                const int p = rL + 64 * k + lane;
+                const uint32_t w = Ls[p >= kMtN && p < 2 * kMtN ? p - kMtN : 0];
+                if (p >= kMtN) wl[k] = w;
+            }
         }
-        pend = false;
-        const int64_t lastT = (D - 1 - i0) < (kMtN - 1) ? (D - 1 - i0) : (kMtN - 1);    // last slot used
-        const int64_t needL = qL + c + ((rL + lastT) >= kMtN ? 1 : 0);
-        const int64_t needG = qG + c + ((rG + lastT) >= kMtN ? 1 : 0);
-        while (haveL < needL || haveG < needG) {
-            const bool dl = haveL < needL, dg = haveG < needG;
-            mt_twist2(Ls, haveL, dl, Gs, haveG, dg, tid);
-            haveL += dl;
-            haveG += dg;
+        if (rG + lastE >= kMtN) {
+            mt_twist_wave(Gs, lane);
+            ++haveG;
+#pragma unroll
+            for (int k = 0; k < kMtGroups; ++k) {
+                const int p = rG + 64 * k + lane;
+                const uint32_t w = Gs[p >= kMtN && p < 2 * kMtN ? p - kMtN : 0];
+                if (p >= kMtN) wg[k] = w;
+            }
         }
-        bool ex = false;
-        float v = 0.f;
-        if (active) {
-            const int64_t pL = rL + tid, pG = rG + tid;
-            const int64_t bL = qL + c + (pL >= kMtN), bG = qG + c + (pG >= kMtN);
-            const uint32_t wl = mt_temper(Ls[bL & 1][pL >= kMtN ? pL - kMtN : pL]);
-            const uint32_t wg = mt_temper(Gs[bG & 1][pG >= kMtN ? pG - kMtN : pG]);
-            v = r_cur * sc;                                          // AS:472
-            ex = (v > thr) || (v < -thr);                            // AS:478
-            const float q = ex ? 0.f : v / fdelta;                   // AS:480-481
-            const float fl = floorf(q);
-            const float p = q - fl;                                  // AS:483
-            if (!(p >= 0.f && p <= 1.f)) flags |= UQ_QFL_BAD_P;
-            const float bern = ((double)(wl & 0xFFFFFFu) * 0x1p-24 < (double)p) ? 1.f : 0.f;
-            const float iq = fl + bern;                              // AS:484
-            const float t1 = iq * fh;                                // AS:486 in f32 (no fma: -ffp-contract=off)
-            const float t2 = t1 + (float)h_cur;
-            const float idxf = t2 + fhalf;
+        // stage 1 of round c: AS:472-487, the gather issued
+        QflRound cr;
+        cr.ex = 0;
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            const int e = 64 * k + lane;
+            const bool active = e < kMtN && i0 + e < D;
+            cr.wg[k] = mt_temper(wg[k]);
+            cr.v[k] = 0.f;
             int64_t idx = 0;
-            if (!(idxf > -9.0e18f && idxf < 9.0e18f)) {
-                flags |= UQ_QFL_BAD_INDEX;
-            } else {
-                idx = (int64_t)idxf;                                 // .long(): truncation
-                if (idx < -numel || idx >= numel) flags |= UQ_QFL_BAD_INDEX;
-                else if (idx < 0) idx += numel;                      // torch.take wraps negatives
+            if (active) {
+                const float v = r_cur[k] * sc;                        // AS:472
+                const bool ex = (v > thr) || (v < -thr);              // AS:478
+                const float q = ex ? 0.f : v / fdelta;                // AS:480-481
+                const float fl = floorf(q);
+                const float p = q - fl;                               // AS:483
+                if (!(p >= 0.f && p <= 1.f)) flags |= UQ_QFL_BAD_P;
+                const uint32_t w = mt_temper(wl[k]);
+                const float bern = (u24(w) < p) ? 1.f : 0.f;
+                const float iq = fl + bern;                           // AS:484
+                const float t1 = iq * fh;                             // AS:486 in f32 (no fma: -ffp-contract=off)
+                const float t2 = t1 + (float)h_cur[k];
+                const float idxf = t2 + fhalf;
+                if (!(idxf > -9.0e18f && idxf < 9.0e18f)) {
+                    flags |= UQ_QFL_BAD_INDEX;
+                } else {
+                    idx = (int64_t)idxf;                              // .long(): truncation
+                    if (idx < -numel || idx >= numel) flags |= UQ_QFL_BAD_INDEX;
+                    else if (idx < 0) idx += numel;                   // torch.take wraps negatives
+                }
+                idx = idx < 0 ? 0 : (idx >= numel ? numel - 1 : idx);  // (flagged above; stay in bounds)
+                cr.v[k] = v;
+                cr.ex |= (ex ? 1u : 0u) << k;
             }
-            idx = idx < 0 ? 0 : (idx >= numel ? numel - 1 : idx);    // (flagged above; stay in bounds)
-            const float2 t = a.tab[idx];                             // AS:486-487
-            if (!(t.y >= 0.f && t.y <= 1.f)) flags |= UQ_QFL_BAD_PX;
-            const float bx = ((double)(wg & 0xFFFFFFu) * 0x1p-24 < (double)t.y) ? 1.f : 0.f;
-            const float xf = t.x + bx;                               // AS:489
-            if (a.x_kind == 0) {
-                int64_t xv = 0;
-                if (xf > -9.2e18f && xf < 9.2e18f) xv = (int64_t)xf;  // AS:490 .long()
-                else flags |= UQ_QFL_X_RANGE;
-                __builtin_nontemporal_store(xv, (int64_t*)a.X + row + i);
-            } else {
-                int32_t xv = 0;
-                if (xf > -1.0f && xf < 256.0f) xv = (int32_t)xf;
-                else flags |= UQ_QFL_X_RANGE;
-                ((uint8_t*)a.X)[row + i] = (uint8_t)xv;
-            }
-            a.mask[row + i] = ex ? 1 : 0;
+            cr.t[k] = a.tab[idx];                                     // AS:486-487 (idx 0 when inactive)
         }
-        // exact values: rank within the wave now, wave offsets after the next barrier
-        const uint64_t bal = __ballot(ex);
-        if (lane == 0) wcnt[c & 1][wv] = (int32_t)__popcll(bal);
-        if (ex) {
-            pend = true;
-            pend_v = v;
-            pend_rank = (int)__popcll(bal & ((1ull << lane) - 1ull));
+        if (have_prev) finish(pr, prev_i0);                         // round c-1 while round c's gathers fly
+        pr = cr;
+        have_prev = true;
+        prev_i0 = i0;
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            r_cur[k] = r_nxt[k];
+            h_cur[k] = h_nxt[k];
         }
-        r_cur = r_nxt;
-        h_cur = h_nxt;
     }
-    lds_sync();
-    if (pend) {
-        int64_t base = etot;
-        for (int w = 0; w < wv; ++w) base += wcnt[(nch - 1) & 1][w];
-        a.ev[row + base + pend_rank] = pend_v;
-    }
-    if (nch) {
-        for (int w = 0; w < kQfWaves; ++w) etot += wcnt[(nch - 1) & 1][w];
-    }
-    if (flags) atomicOr(&sflags, flags);
-    // the global generator after its D draws
+    if (have_prev) finish(pr, prev_i0);
+
+    // flags: OR over the wave
+    for (int s = 32; s >= 1; s >>= 1) flags |= __shfl_xor(flags, s);
+    // the global generator after its D draws: the block holding word D - 1
     if (a.px_state_out) {
         uint32_t* so = a.px_state_out + j * kQfStateWords;
-        const uint32_t* src;
         uint32_t left1, next1;
         if (D <= (int64_t)gleft - 1) {                           // every draw from the current block
-            src = Gs[0];
             left1 = (uint32_t)(gleft - D);
             next1 = (uint32_t)(gnext + D);
         } else {
-            const int64_t vlast = vG + D - 1;
-            const int64_t bl = vlast / kMtN, pos = vlast % kMtN;
-            src = Gs[bl & 1];
+            const int64_t pos = (vG + D - 1) % kMtN;
             next1 = (uint32_t)(pos + 1);
             left1 = (uint32_t)(kMtN - pos);
         }
-        for (int i = tid; i < kMtN; i += kQfT) so[2 + i] = src[i];
-        if (tid == 0) {
+        for (int i = lane; i < kMtN; i += 64) so[2 + i] = Gs[i];
+        if (lane == 0) {
             so[0] = left1;
             so[1] = next1;
         }
     }
-    lds_sync();
-    if (tid == 0) {
+    if (lane == 0) {
         a.ecount[j] = (int32_t)etot;
         a.scale[j] = sc;
-        a.info[j] = sflags;
+        a.info[j] = flags;
+    }
+}
+
+// ---- receiver: QuicFLReceiver.decompress before its inverse RHT (AS:526-532) -----------------
+// h = torch.randint(0, h_len, (D,)) of a generator seeded with prng_seed (word % h_len), then
+// v = recv_table[X * h_len + h], exact coordinates overwritten, v / scale (f32).  One wave per
+// message; the table (<= 1024 floats) sits in LDS, shared by the workgroup's waves.
+constexpr int kQflTab = 1024;
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_recv_wave_kernel(const int32_t* __restrict__ X, int64_t n, int64_t D, const float* __restrict__ table,
+                        int32_t tab_n, int32_t h_len, const int32_t* __restrict__ prng_seeds,
+                        const uint8_t* __restrict__ exact_mask, const float* __restrict__ exact_vals,
+                        const float* __restrict__ scale, float* __restrict__ out) {
+    __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];
+    __shared__ float tab[kQflTab];
+    for (int i = threadIdx.x; i < tab_n; i += 64 * kQfWavesPerWG) tab[i] = table[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    if (j >= n) return;
+    uint32_t* Ls = Lsh[wv];
+    if (lane == 0) mt_seed(Ls, (uint32_t)prng_seeds[j]);
+    wave_lds_fence();
+    const int64_t row = j * D;
+    const float sc = scale[j];
+    const int64_t nch = (D + kMtN - 1) / kMtN;
+    // loads unconditional with clamped indices (see the sender), the next round's first
+    const int64_t last = D - 1;
+    int32_t xr[kMtGroups];
+    uint8_t mr[kMtGroups];
+    float vr[kMtGroups];
+    auto load_round = [&](int64_t i0, int32_t* xo, uint8_t* mo, float* vo) {
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            const int64_t i = i0 + 64 * k + lane;
+            const int64_t ic = i < last ? i : last;
+            xo[k] = X[row + ic];
+            mo[k] = exact_mask ? exact_mask[row + ic] : (uint8_t)0;
+            vo[k] = exact_mask ? exact_vals[row + ic] : 0.f;
+        }
+    };
+    load_round(0, xr, mr, vr);
+    for (int64_t c = 0; c < nch; ++c) {
+        const int64_t i0 = c * kMtN;
+        int32_t xn[kMtGroups];
+        uint8_t mn[kMtGroups];
+        float vn[kMtGroups];
+        load_round(i0 + kMtN, xn, mn, vn);
+        mt_twist_wave(Ls, lane);
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            const int e = 64 * k + lane;
+            const int64_t i = i0 + e;
+            const uint32_t h = mt_temper(Ls[e < kMtN ? e : 0]) % (uint32_t)h_len;     // AS:528 randint
+            int64_t idx = (int64_t)xr[k] * h_len + h;                                   // AS:530 take
+            idx = idx < 0 ? 0 : (idx >= tab_n ? tab_n - 1 : idx);                       // validated by the host
+            const float v = mr[k] ? vr[k] : tab[idx];                                   // AS:531
+            if (e < kMtN && i < D) out[row + i] = v / sc;                              // AS:532
+            xr[k] = xn[k];
+            mr[k] = mn[k];
+            vr[k] = vn[k];
+        }
     }
 }

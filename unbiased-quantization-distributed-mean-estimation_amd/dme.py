@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from .biased import biased_quantize
-from .eden import eden_quantize
+from .eden import eden_compress, eden_decompress, eden_quantize
 from .quantizer import client_mean, quantize_dequantize
 
 SCHEME_ORDER = ("eden", "unbiased", "biased")     # ND:135-140 call order
@@ -62,12 +62,15 @@ def draw_vectors(dist: str, n: int, dim: int, rs=np.random):
 
 def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_instances: int = 50,
                     num_trials: int = 50, rates=(1, 2), seed: int = 42, torch_threads: int = 1,
-                    device=None, schemes=("unbiased",), progress=None):
+                    device=None, schemes=("unbiased",), progress=None, eden_scales=None, eden_scales_out=None):
     """NMSE curves of the selected schemes with the reference's normalisation.
 
     Returns {rate: {...}} for the default unbiased-only run, else {(scheme, rate): {...}};
     each value holds "script" ([len(users), num_instances]), "avg", "max", "standard_avg",
-    "standard_max".  `progress(n, inst)` is called after each instance (long runs)."""
+    "standard_max".  `progress(n, inst)` is called after each instance (long runs).
+    eden_scales {(n, inst, rate): [scale per client]} replaces EDEN's scale (AS:348) by the
+    given values (the receiver then runs on them); eden_scales_out, a dict, receives the
+    scales computed here under the same keys."""
     device = device or torch.device("cuda", torch.cuda.current_device())
     schemes = tuple(schemes)
     for sc in schemes:
@@ -98,8 +101,15 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                                             torch_threads=torch_threads)
                 elif sc == "biased":
                     q = biased_quantize(xd, r, torch_threads=torch_threads)
-                else:
+                elif eden_scales is None and eden_scales_out is None:
                     q = eden_quantize(xd, r, seeds=draws[(sc, r)])
+                else:                                 # compress, (record / replace the scale), decompress
+                    msg = eden_compress(xd, r, seeds=draws[(sc, r)])
+                    if eden_scales_out is not None:
+                        eden_scales_out[(n, inst, r)] = msg.scale.cpu().numpy().copy()
+                    if eden_scales is not None:
+                        msg.scale = torch.as_tensor(np.asarray(eden_scales[(n, inst, r)], np.float32)).to(device)
+                    q = eden_decompress(msg)
                 est = client_mean(q, n).cpu()
                 script[(sc, r)][ui, inst] = float(torch.norm(est - emp).pow(2) / (num_trials * vns * n))   # ND:155
             if progress is not None:
