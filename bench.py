@@ -161,6 +161,8 @@ def main():
     # (K1 -> K2 -> K3c) per rank, then ONE RCCL reduce of est to rank 0 (N > 1; with RCCL the
     # reduce of step k runs beside step k+1's kernels, see ShardedDME).  The output placement
     # is probed once (pipeline.py: K2's speed follows where q and the codes land).
+    if args.mean_mode == "ordered" and args.pipeline == "encode" and world > 1:
+        raise SystemExit("--mean-mode ordered folds q across ranks: use --pipeline codes or q")
     sh = uqdme.ShardedDME(n, d, n_total, m=m, torch_threads=T, pipeline="codes", mode=args.mean_mode)
     pipe = sh.pipe
     probe = sh.probe_outputs(x, X, candidates=args.probe_candidates, min_candidates=args.probe_min) \
@@ -249,6 +251,7 @@ def main():
         side["biased"] = time_biased(uqdme, x, args.bits, T, max(3, args.steps // 2))
         side["eden"] = time_eden(uqdme, x, q, max(3, args.steps // 2))
         side["codec"] = time_codec(uqdme, pipe, max(3, args.steps // 2))
+        side["quicfl"] = time_quicfl(uqdme, x, max(2, args.steps // 4))
         if int(torch.count_nonzero(ovf > 127)):
             raise RuntimeError("type-code overflow in the bench workload")
 
@@ -343,6 +346,42 @@ def time_eden(uqdme, x, q, steps):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     return {"ms_per_step": round(ms, 4), "value": round(n / ms / 1e3, 6), "what": "EDEN 1-bit batch (RHT, bins, scale, inverse RHT), no mean"}
+
+
+def time_quicfl(uqdme, x, steps):
+    """Side line: the QUIC-FL baseline (AS:429-535, 1 bit) on the same resident batch: the
+    sender (RHT, norm, KQ1: h stream, SR rounding, table X / p, bernoulli(p_X)) and the receiver
+    (KQ2 + inverse RHT) per step.  Sender tables: the synthetic ones the parity fixtures use
+    (tests/golden/quicfl_tables.py; the published tables are not in the reference), with the
+    reference's data.txt parameters; receiver tables: the reference's."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from quicfl_tables import DATA, sender_tables
+    n, d = x.shape
+    X, p = sender_tables(1)
+    snd = uqdme.QuicFLSender(tables={1: (X, p, DATA[1])})
+    rt = np.load(os.path.join(ROOT, "tests", "golden", "quicfl_recv_vectors.npz"))["recv1"]
+    seeds, rots, pxs = list(range(n)), [123] * n, list(range(7, 7 + n))
+    held = {}
+
+    def timed(f):
+        f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        return round(e0.elapsed_time(e1) / steps, 4)
+
+    res = {"compress_ms": timed(lambda: held.update(
+        m=uqdme.quicfl_compress(x, 1, seeds, rots, sender=snd, px_seeds=pxs)))}
+    res["decompress_ms"] = timed(lambda: uqdme.quicfl_decompress_messages(held["m"], rt))
+    ms = res["compress_ms"] + res["decompress_ms"]
+    res.update({"ms_per_step": round(ms, 4), "value": round(n / ms / 1e3, 6),
+                "what": "QUIC-FL 1-bit batch (sender + receiver), synthetic sender tables, no mean"})
+    return res
 
 
 def time_codec(uqdme, pipe, steps):

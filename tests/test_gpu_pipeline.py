@@ -104,3 +104,47 @@ def test_empty_batch_pipeline(gpu_ready):
         torch.cuda.synchronize()
         p.check_status()
         assert torch.count_nonzero(est) == 0, pl
+
+
+def test_output_pool_never_hands_out_a_held_result(gpu_ready):
+    """The one-shot APIs' output pool (outpool.py): results the caller still holds -- whole
+    tensors, views, NumPy aliases -- are never handed out again; released sets are reused
+    (same storage) and every result has the same bits as a plain allocation's."""
+    import uqdme
+    from uqdme_amd.outpool import POOL
+    n, d = 8, 4096
+    x = torch.randn(n, d, device="cuda")
+    X = torch.rand(n)
+    ref = uqdme.quantize_dequantize(x, 1, X=X, torch_threads=1).clone()
+    old = POOL.min_bytes
+    POOL.min_bytes = 0
+    POOL.clear()
+    try:
+        held = [uqdme.quantize_dequantize(x, 1, X=X, torch_threads=1) for _ in range(4)]
+        ptrs = {h.data_ptr() for h in held}
+        assert len(ptrs) == 4                                    # each held result has its own storage
+        for h in held:
+            assert torch.equal(h, ref)
+        view = held[0][3]
+        keep = held[1].cpu()                                     # a host copy: not an alias
+        del held
+        torch.cuda.synchronize()
+        again = [uqdme.quantize_dequantize(x, 1, X=X, torch_threads=1) for _ in range(6)]
+        assert all(a.data_ptr() != view.data_ptr() - 3 * d * 4 for a in again)   # held via a view
+        assert all(torch.equal(a, ref) for a in again)
+        assert torch.equal(keep, ref.cpu())
+        del again
+        torch.cuda.synchronize()
+        loop_ptrs = set()
+        for _ in range(12):                                      # the caller's loop: q = f(x)
+            q = uqdme.quantize_dequantize(x, 1, X=X, torch_threads=1)
+            loop_ptrs.add(q.data_ptr())
+            assert torch.equal(q, ref)
+        torch.cuda.synchronize()
+        assert len(loop_ptrs) <= POOL.explore + POOL.keep        # sets are reused, not allocated per call
+        tc, q2 = uqdme.quantize_encode(x, 1, X=X, torch_threads=1, return_q=True)
+        assert torch.equal(q2, ref) and torch.equal(uqdme.decode(tc), ref)
+        assert torch.equal(view, ref[3])
+    finally:
+        POOL.min_bytes = old
+        POOL.clear()

@@ -191,7 +191,7 @@ class ShardedDME:
         """Returns this step's est buffer (the global mean on `dst` once its reduce is done:
         immediately unless overlap; None off `dst` in mode "ordered")."""
         pl = pipeline or getattr(self.pipe, "pipeline", None)
-        if self.mode == "ordered" and pl == "encode":
+        if self.mode == "ordered" and self.world > 1 and pl == "encode":
             raise ValueError("mode 'ordered' folds q: an 'encode' step writes no q")
         slot = self.nstep % len(self.est_bufs)
         k = self.nstep

@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .outpool import POOL
 from .rates import RATE_TABLE, rate_to_m
 
 __all__ = [
@@ -139,8 +140,9 @@ def quantize_dequantize(x, bits_per_dimension=1, X=None, *, m: int | None = None
     X = torch.as_tensor(X, dtype=torch.float32).reshape(-1)
     if X.numel() != n:
         raise ValueError("X must have one draw per row")
+    token = None
     if out is None:
-        out = torch.empty_like(x)
+        (out,), token = POOL.acquire(dev, [((n, d), torch.float32)])     # probed placement for big batches
     elif out.shape != x.shape or out.dtype != torch.float32 or out.device != x.device or not out.is_contiguous():
         raise ValueError("out must be a contiguous f32 tensor like x")
     if n == 1 and d > 0 and l1 is None and not return_l1 and X.device.type == "cpu":
@@ -158,9 +160,9 @@ def quantize_dequantize(x, bits_per_dimension=1, X=None, *, m: int | None = None
     l1_out = torch.empty(n, dtype=torch.float32, device=dev) if return_l1 else None
     nb = _ws_bytes(n, d, T)
     ws = _workspace(dev, nb)
-    _lib.check(_lib.load().uq_type_unbiased_f32(_ptr(x), _ptr(out), n, d, mm, _ptr(X), _ptr(l1), _ptr(l1_out),
-                                                T, _ptr(ws), ws.numel(), _stream_ptr(dev)),
-               "uq_type_unbiased_f32")
+    POOL.timed(token, lambda: _lib.check(_lib.load().uq_type_unbiased_f32(
+        _ptr(x), _ptr(out), n, d, mm, _ptr(X), _ptr(l1), _ptr(l1_out), T, _ptr(ws), ws.numel(), _stream_ptr(dev)),
+        "uq_type_unbiased_f32"))
     return (out, l1_out) if return_l1 else out
 
 
@@ -182,15 +184,17 @@ def quantize_encode(x, bits_per_dimension=1, X=None, *, m: int | None = None, to
         raise ValueError("X must have one draw per row")
     if l1 is not None:
         l1 = torch.as_tensor(l1, dtype=torch.float32).reshape(-1).to(dev).contiguous()
-    codes = torch.empty((n, d), dtype=torch.int8, device=dev)
+    specs = [((n, d), torch.int8)] + ([((n, d), torch.float32)] if return_q else [])
+    bufs, token = POOL.acquire(dev, specs)                      # probed placement for big batches
+    codes = bufs[0]
+    q = bufs[1] if return_q else None
     overflow = torch.zeros(n, dtype=torch.int32, device=dev)     # per-client kmax (128 = overflow)
     l1_out = torch.empty(n, dtype=torch.float32, device=dev)
-    q = torch.empty_like(x) if return_q else None
     nb = _ws_bytes(n, d, T)
     ws = _workspace(dev, nb)
-    _lib.check(_lib.load().uq_type_unbiased_codes_f32(_ptr(x), _ptr(q), _ptr(codes), _ptr(overflow), n, d, mm,
-                                                      _ptr(X), _ptr(l1), _ptr(l1_out), T, _ptr(ws), ws.numel(),
-                                                      _stream_ptr(dev)), "uq_type_unbiased_codes_f32")
+    POOL.timed(token, lambda: _lib.check(_lib.load().uq_type_unbiased_codes_f32(
+        _ptr(x), _ptr(q), _ptr(codes), _ptr(overflow), n, d, mm, _ptr(X), _ptr(l1), _ptr(l1_out), T, _ptr(ws),
+        ws.numel(), _stream_ptr(dev)), "uq_type_unbiased_codes_f32"))
     tc = TypeCodes(codes=codes, l1=l1_out, m=mm, overflow=overflow)
     return (tc, q) if return_q else tc
 
@@ -264,14 +268,14 @@ def quantize_mean(x, bits_per_dimension=1, X=None, n_div=None, *, m: int | None 
     if est is None:
         est = torch.empty(d, dtype=torch.float32, device=dev)
         accumulate = False
+    token = None
     if out is None:
-        out = torch.empty_like(x)
+        (out,), token = POOL.acquire(dev, [((n, d), torch.float32)])     # scratch q: probed placement
     nb = _ws_bytes(n, d, T)
     ws = _workspace(dev, nb)
-    _lib.check(_lib.load().uq_type_unbiased_mean_f32(_ptr(x), _ptr(out), n, d, mm, _ptr(X), _ptr(None), T,
-                                                     float(n_div), int(bool(accumulate)), _ptr(est),
-                                                     _ptr(ws), ws.numel(), _stream_ptr(dev)),
-               "uq_type_unbiased_mean_f32")
+    POOL.timed(token, lambda: _lib.check(_lib.load().uq_type_unbiased_mean_f32(
+        _ptr(x), _ptr(out), n, d, mm, _ptr(X), _ptr(None), T, float(n_div), int(bool(accumulate)), _ptr(est),
+        _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_type_unbiased_mean_f32"))
     return est
 
 
