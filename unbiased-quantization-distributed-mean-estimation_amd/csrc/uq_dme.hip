@@ -2337,8 +2337,9 @@ SegNormLayout segnorm_layout(int64_t n, int64_t D) {
     L.kind = up(L.e + nk * sizeof(float));
     L.cnt = up(L.kind + nk * sizeof(int32_t));
     L.tseg = up(L.cnt + (size_t)n * sizeof(int32_t));
-    L.tab = up(L.tseg + (size_t)n * kSegTabCap * sizeof(int32_t));
-    L.total = up(L.tab + (size_t)n * kSegTabCap * kSegTab * sizeof(float));
+    const size_t cap = (size_t)seg_tab_cap(D);
+    L.tab = up(L.tseg + (size_t)n * cap * sizeof(int32_t));
+    L.total = up(L.tab + (size_t)n * cap * kSegTab * sizeof(float));
     return L;
 }
 
@@ -2355,10 +2356,10 @@ int launch_segnorm(const float* v, int64_t n, int64_t D, char* region, float* nr
     const dim3 grid((unsigned)(K / kSegPerWG), (unsigned)n);
     hipLaunchKernelGGL(eden_segsum_kernel, grid, dim3(256), 0, st, v, D, segsum);
     hipLaunchKernelGGL(eden_segscan_kernel, dim3(8u, (unsigned)n), dim3(256), 0, st, segsum, K, g, cnt);
-    hipLaunchKernelGGL(eden_segchain_kernel, grid, dim3(256), 0, st, v, D, g, e, kind, cnt, tseg);
-    hipLaunchKernelGGL(eden_segtab_kernel, dim3((unsigned)kSegTabCap, (unsigned)n), dim3(256), 0, st, v, D, g, cnt, tseg,
-                       tab);
-    hipLaunchKernelGGL(eden_segwalk_kernel, dim3((unsigned)n), dim3(512), 0, st, v, D, g, e, kind, tab, nrm);
+    const int cap = seg_tab_cap(D);
+    hipLaunchKernelGGL(eden_segchain_kernel, grid, dim3(256), 0, st, v, D, g, e, kind, cnt, tseg, cap);
+    hipLaunchKernelGGL(eden_segtab_kernel, dim3((unsigned)cap, (unsigned)n), dim3(256), 0, st, v, D, g, cnt, tseg, tab, cap);
+    hipLaunchKernelGGL(eden_segwalk_kernel, dim3((unsigned)n), dim3(512), 0, st, v, D, g, e, kind, tab, nrm, cap);
     return hip_check(hipGetLastError(), "eden segmented norm launch");
 }
 
@@ -3517,6 +3518,7 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     if (dim > ((int64_t)1 << 28)) return fail(UQ_E_INVALID, "dim must be <= 2^28");
     if (h_len < 1 || h_len > 256) return fail(UQ_E_INVALID, "h_len must be 1..256");
     if (table_numel < h_len || table_numel % h_len) return fail(UQ_E_INVALID, "table_numel must be a multiple of h_len");
+    if (table_numel >= ((int64_t)1 << 24)) return fail(UQ_E_INVALID, "table_numel must be below 2^24");
     if (x_kind != 0 && x_kind != 1) return fail(UQ_E_INVALID, "x_kind must be 0 (int64) or 1 (uint8)");
     if (n == 0 || dim == 0) return UQ_OK;
     if (!x || !signs || !table_xp || !prng_seeds || !X || !exact_mask || !exact_vals || !exact_count || !scale || !info)
@@ -3554,8 +3556,11 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.info = info;
     q.D = w.D;
     q.n = n;
-    hipLaunchKernelGGL(quicfl_send_wave_kernel, dim3((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)),
-                       dim3(64 * kQfWavesPerWG), 0, st, q);
+    const dim3 grid((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG));
+    if (x_kind == 0)
+        hipLaunchKernelGGL(quicfl_send_wave_kernel<0>, grid, dim3(64 * kQfWavesPerWG), 0, st, q);
+    else
+        hipLaunchKernelGGL(quicfl_send_wave_kernel<1>, grid, dim3(64 * kQfWavesPerWG), 0, st, q);
     return hip_check(hipGetLastError(), "quicfl_send_wave_kernel launch");
 }
 

@@ -750,7 +750,13 @@ constexpr int kSegBlock = 8 * kSegSteps;               // floats of one segment 
 constexpr int kSegPerWG = 32;                          // segments per KE2a / KE2c workgroup
 constexpr int kSegPad = kSegBlock + 8;                 // LDS row of a segment (8 floats apart: banks)
 constexpr int kSegTab = 1024;                          // table starts per listed segment
-constexpr int kSegTabCap = 256;                        // tables per client (beyond: KE2d runs the steps)
+constexpr int kSegTabCap = 256;                        // tables per client at most (beyond: KE2d runs the steps)
+// tables per client for a vector of D: the table region is cap * 4 KB per client, so short
+// vectors get fewer (a 2^14 vector is 64 KB; beyond the cap a segment's 64 steps run in KE2d)
+__host__ __device__ inline int seg_tab_cap(int64_t D) {
+    const int64_t c = D / 512;
+    return (int)(c < 32 ? 32 : (c > kSegTabCap ? kSegTabCap : c));
+}
 constexpr int64_t kSegMinD = (int64_t)kSegBlock * kSegPerWG;
 static_assert(kSegSteps == 64, "KE2d's step path loads one segment as one value per lane of a wave");
 
@@ -831,7 +837,7 @@ eden_segscan_kernel(const double* __restrict__ segsum, int64_t K, float* __restr
 
 __global__ void __launch_bounds__(256)
 eden_segchain_kernel(const float* __restrict__ v, int64_t D, const float* __restrict__ g, float* __restrict__ e,
-                     int32_t* __restrict__ kind, int32_t* __restrict__ tabcnt, int32_t* __restrict__ tabseg) {
+                     int32_t* __restrict__ kind, int32_t* __restrict__ tabcnt, int32_t* __restrict__ tabseg, int cap) {
     __shared__ __attribute__((aligned(16))) float s[kSegPerWG * kSegPad];
     const int tid = threadIdx.x;
     const int64_t client = blockIdx.y;
@@ -866,9 +872,9 @@ eden_segchain_kernel(const float* __restrict__ v, int64_t D, const float* __rest
     int32_t k = 0;
     if (!finite || cross || tie || near_bottom || near_top) {
         const int slot = atomicAdd(&tabcnt[client], 1);
-        if (slot < kSegTabCap) {
+        if (slot < cap) {
             k = slot + 1;
-            tabseg[client * kSegTabCap + slot] = (int32_t)((seg0 + sl) * 8 + l);
+            tabseg[client * cap + slot] = (int32_t)((seg0 + sl) * 8 + l);
         } else {
             k = -1;                                    // no table: KE2d runs its steps
         }
@@ -879,13 +885,13 @@ eden_segchain_kernel(const float* __restrict__ v, int64_t D, const float* __rest
 
 __global__ void __launch_bounds__(256)
 eden_segtab_kernel(const float* __restrict__ v, int64_t D, const float* __restrict__ g, const int32_t* __restrict__ tabcnt,
-                   const int32_t* __restrict__ tabseg, float* __restrict__ tab) {
+                   const int32_t* __restrict__ tabseg, float* __restrict__ tab, int cap) {
     __shared__ float xs[kSegSteps];
     const int64_t client = blockIdx.y;
     const int slot = blockIdx.x;
-    if (slot >= std::min(tabcnt[client], kSegTabCap)) return;            // uniform
+    if (slot >= std::min(tabcnt[client], cap)) return;                   // uniform
     const int tid = threadIdx.x;
-    const int32_t code = tabseg[client * kSegTabCap + slot];
+    const int32_t code = tabseg[client * cap + slot];
     const int64_t seg = code >> 3;
     const int l = code & 7;
     const int64_t K = D / kSegBlock;
@@ -904,7 +910,7 @@ eden_segtab_kernel(const float* __restrict__ v, int64_t D, const float* __restri
 #pragma unroll
         for (int k = 0; k < kPer; ++k) a[k] = fmaf(x, x, a[k]);
     }
-    float* out = tab + ((int64_t)client * kSegTabCap + slot) * kSegTab;
+    float* out = tab + ((int64_t)client * cap + slot) * kSegTab;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) out[tid + 256 * k] = a[k];
 }
@@ -915,7 +921,7 @@ eden_segtab_kernel(const float* __restrict__ v, int64_t D, const float* __restri
 constexpr int kWalkChunks = 8;
 __global__ void __launch_bounds__(512)
 eden_segwalk_kernel(const float* __restrict__ v, int64_t D, const float* __restrict__ g, const float* __restrict__ e,
-                    const int32_t* __restrict__ kind, const float* __restrict__ tab, float* __restrict__ nrm) {
+                    const int32_t* __restrict__ kind, const float* __restrict__ tab, float* __restrict__ nrm, int cap) {
     __shared__ float accs[8];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), l = tid / kWave;
     const int64_t client = blockIdx.x;
@@ -966,7 +972,7 @@ eden_segwalk_kernel(const float* __restrict__ v, int64_t D, const float* __restr
         if (kk > 0) {
             const int64_t d = (int64_t)fbits(A) - (int64_t)fbits(gg) + kSegTab / 2;
             if (d >= 0 && d < kSegTab) {
-                A = tab[((int64_t)client * kSegTabCap + (kk - 1)) * kSegTab + d];
+                A = tab[((int64_t)client * cap + (kk - 1)) * kSegTab + d];
                 done = true;
             }
         }

@@ -148,12 +148,21 @@ struct QflSendArgs {
 
 // Round state carried from stage 1 (words, flags, gather issued) to stage 2 (X, stores).
 struct QflRound {
-    float2 t[kMtGroups];
-    uint32_t wg[kMtGroups];
+    uint32_t t[kMtGroups][2];   // gathered (table_X, table_p) bits
+    uint32_t wg[kMtGroups];     // tempered global words
     float v[kMtGroups];
     uint32_t ex;                // bit k: element k of this lane is exact
+    uint32_t act;               // bit k: element k of this lane exists
 };
 
+__device__ __forceinline__ uint32_t qf_off(bool ok, uint32_t off) { return ok ? off : 0xFFFFFFFFu; }  // dropped
+
+// Every per-element global access goes through a buffer descriptor (32-bit offsets,
+// out-of-range loads return 0 and out-of-range stores are dropped): no per-element branches,
+// and a lane's ten loads of a round are all in flight at once (a load under a per-element
+// branch is waited for before the next one).  XK: 0 = int64 X (the drop-in's X.long()),
+// 1 = uint8 X (batches).
+template <int XK>
 __global__ void __launch_bounds__(64 * kQfWavesPerWG)
 quicfl_send_wave_kernel(QflSendArgs a) {
     __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];      // local generator block per wave
@@ -164,6 +173,7 @@ quicfl_send_wave_kernel(QflSendArgs a) {
     uint32_t* Ls = Lsh[wv];
     uint32_t* Gs = Gsh[wv];
     const int64_t D = a.D;
+    const uint32_t Du = (uint32_t)D;
     const int64_t row = j * D;
     int32_t gleft = 1, gnext = 0;
     if (a.px_state) {
@@ -179,16 +189,24 @@ quicfl_send_wave_kernel(QflSendArgs a) {
     const float sc = (1.0f / a.nrm[j]) * a.sqrtD;              // AS:466/470 (IEEE 1/x, then f32 mul)
     const int64_t nch = (D + kMtN - 1) / kMtN;
     const uint32_t h_len = (uint32_t)a.h_len;
-    uint8_t* hb = a.hbuf + row;
+    const bool hpow2 = (h_len & (h_len - 1)) == 0;
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.rot + row, Du * 4u);
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.hbuf + row, Du);
+    const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.mask + row, Du);
+    const __amdgpu_buffer_rsrc_t rX = make_rsrc(XK == 0 ? (void*)((int64_t*)a.X + row) : (void*)((uint8_t*)a.X + row),
+                                                XK == 0 ? Du * 8u : Du);
+    const __amdgpu_buffer_rsrc_t rt = make_rsrc(a.tab, (uint32_t)a.numel * 8u);
 
     // ---- pass A: h = randint(0, h_len, (D,), local) (AS:465/469): word i is block c + 1, slot e
     for (int64_t c = 0; c < nch; ++c) {
         mt_twist_wave(Ls, lane);
-        const int64_t i0 = c * kMtN;
+        const uint32_t i0 = (uint32_t)(c * kMtN);
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
-            if (e < kMtN && i0 + e < D) hb[i0 + e] = (uint8_t)(mt_temper(Ls[e]) % h_len);
+            const uint32_t w = mt_temper(Ls[e < kMtN ? e : 0]);
+            const uint32_t h = hpow2 ? (w & (h_len - 1u)) : (w % h_len);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)h, rh, qf_off(e < kMtN, i0 + (uint32_t)e), 0, 0);
         }
     }
     int64_t haveL = nch;                                        // block in Ls
@@ -202,74 +220,70 @@ quicfl_send_wave_kernel(QflSendArgs a) {
     const int rG = (int)(vG % kMtN);
     int64_t haveG = 0;
     const float thr = kQflExactT;
-    const float fdelta = a.delta;
+    const DivPlan dp = div_plan_norm(a.delta);                  // q = v / delta: reciprocal + Markstein (exact)
     const float fh = (float)a.h_len;
     const float fhalf = (float)a.half;
-    const int64_t numel = a.numel;
+    const float fnumel = (float)a.numel;                        // exact: numel < 2^24 (host check)
+    const int32_t numel = (int32_t)a.numel;
     int32_t flags = 0;
     int64_t etot = 0;                                           // exact values written so far
     QflRound pr;                                                // the previous round (stage 2 pending)
     bool have_prev = false;
-    int64_t prev_i0 = 0;
+    uint32_t prev_i0 = 0;
     float r_cur[kMtGroups], r_nxt[kMtGroups];
     uint32_t h_cur[kMtGroups], h_nxt[kMtGroups];
-    // (every global load below is unconditional with a clamped index: a load under a per-element
-    // branch is waited for before the next one, which serialises a lane's ten loads)
-    const int64_t last = D - 1;
 #pragma unroll
     for (int k = 0; k < kMtGroups; ++k) {
-        const int64_t e = 64 * k + lane < last ? 64 * k + lane : last;
-        r_cur[k] = __builtin_nontemporal_load(a.rot + row + e);
-        h_cur[k] = hb[e];
+        const uint32_t e = 64u * k + lane;
+        r_cur[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, e * 4u, 0, kAuxNT));
+        h_cur[k] = __builtin_amdgcn_raw_buffer_load_b8(rh, e, 0, 0);
     }
 
-    auto finish = [&](const QflRound& r, int64_t i0) {          // stage 2 of a round (AS:489-490, 494-495)
+    auto finish = [&](const QflRound& r, uint32_t i0) {          // stage 2 of a round (AS:489-490, 494-495)
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
-            const int e = 64 * k + lane;
-            const int64_t i = i0 + e;
-            const bool active = e < kMtN && i < D;
+            const uint32_t i = i0 + 64u * k + lane;
+            const bool active = (r.act >> k) & 1u;
             const bool ex = (r.ex >> k) & 1u;
-            if (active) {
-                const float2 t = r.t[k];
-                if (!(t.y >= 0.f && t.y <= 1.f)) flags |= UQ_QFL_BAD_PX;
-                const float bx = (u24(r.wg[k]) < t.y) ? 1.f : 0.f;
-                const float xf = t.x + bx;                           // AS:489
-                if (a.x_kind == 0) {
-                    int64_t xv = 0;
-                    if (xf > -9.2e18f && xf < 9.2e18f) xv = (int64_t)xf;  // AS:490 .long()
-                    else flags |= UQ_QFL_X_RANGE;
-                    __builtin_nontemporal_store(xv, (int64_t*)a.X + row + i);
-                } else {
-                    int32_t xv = 0;
-                    if (xf > -1.0f && xf < 256.0f) xv = (int32_t)xf;
-                    else flags |= UQ_QFL_X_RANGE;
-                    ((uint8_t*)a.X)[row + i] = (uint8_t)xv;
-                }
-                a.mask[row + i] = ex ? 1 : 0;
+            const float tx = __uint_as_float(r.t[k][0]), tp = __uint_as_float(r.t[k][1]);
+            flags |= (active && !(tp >= 0.f && tp <= 1.f)) ? UQ_QFL_BAD_PX : 0;
+            const float bx = (u24(r.wg[k]) < tp) ? 1.f : 0.f;
+            const float xf = tx + bx;                                // AS:489
+            if (XK == 0) {
+                const bool ok = xf > -9.2e18f && xf < 9.2e18f;
+                flags |= (active && !ok) ? UQ_QFL_X_RANGE : 0;
+                const int64_t xv = ok ? (int64_t)xf : 0;             // AS:490 .long()
+                const uint32_t lo = (uint32_t)xv, hi = (uint32_t)((uint64_t)xv >> 32);
+                typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+                const u32x2v w = {lo, hi};
+                __builtin_amdgcn_raw_buffer_store_b64(w, rX, qf_off(active, i * 8u), 0, kAuxNT);
+            } else {
+                const bool ok = xf > -1.0f && xf < 256.0f;
+                flags |= (active && !ok) ? UQ_QFL_X_RANGE : 0;
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ok ? (int32_t)xf : 0), rX, qf_off(active, i), 0, 0);
             }
-            const uint64_t bal = __ballot(active && ex);        // index order: group k, then lane
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ex ? 1 : 0), rm, qf_off(active, i), 0, 0);
+            const uint64_t bal = __ballot(active && ex);            // index order: group k, then lane
             if (active && ex) a.ev[row + etot + __popcll(bal & ((1ull << lane) - 1ull))] = r.v[k];
             etot += __popcll(bal);
         }
     };
 
     for (int64_t c = 0; c < nch; ++c) {
-        const int64_t i0 = c * kMtN;
-        const int lastE = (int)((D - 1 - i0) < (kMtN - 1) ? (D - 1 - i0) : (kMtN - 1));
-        // next round's loads first
+        const uint32_t i0 = (uint32_t)(c * kMtN);
+        const int lastE = (int)((D - 1 - (int64_t)i0) < (kMtN - 1) ? (D - 1 - (int64_t)i0) : (kMtN - 1));
+        // next round's loads first (beyond D: the descriptor returns 0)
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
-            const int64_t in = i0 + kMtN + 64 * k + lane;
-            const int64_t ic = in < last ? in : last;
-            r_nxt[k] = __builtin_nontemporal_load(a.rot + row + ic);
-            h_nxt[k] = hb[ic];
+            const uint32_t in = i0 + (uint32_t)kMtN + 64u * k + lane;
+            r_nxt[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, in * 4u, 0, kAuxNT));
+            h_nxt[k] = __builtin_amdgcn_raw_buffer_load_b8(rh, in, 0, 0);
         }
         // the words of this round: slots rX + e of blocks qX + c (before) and qX + c + 1 (after)
         while (haveL < qL + c) { mt_twist_wave(Ls, lane); ++haveL; }
         while (haveG < qG + c) { mt_twist_wave(Gs, lane); ++haveG; }
-        uint32_t wl[kMtGroups], wg[kMtGroups];
         // (slot p = rX + e: p < 624 before the twist, p - 624 after; reads unconditional)
+        uint32_t wl[kMtGroups], wg[kMtGroups];
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
@@ -296,41 +310,37 @@ quicfl_send_wave_kernel(QflSendArgs a) {
                 if (p >= kMtN) wg[k] = w;
             }
         }
-        // stage 1 of round c: AS:472-487, the gather issued
+        // stage 1 of round c: AS:472-487, the gather issued (branch-free: inactive elements
+        // compute on zeros, raise no flags and store nothing)
         QflRound cr;
         cr.ex = 0;
+        cr.act = 0;
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
-            const bool active = e < kMtN && i0 + e < D;
+            const bool active = e < kMtN && (int64_t)i0 + e < D;
             cr.wg[k] = mt_temper(wg[k]);
-            cr.v[k] = 0.f;
-            int64_t idx = 0;
-            if (active) {
-                const float v = r_cur[k] * sc;                        // AS:472
-                const bool ex = (v > thr) || (v < -thr);              // AS:478
-                const float q = ex ? 0.f : v / fdelta;                // AS:480-481
-                const float fl = floorf(q);
-                const float p = q - fl;                               // AS:483
-                if (!(p >= 0.f && p <= 1.f)) flags |= UQ_QFL_BAD_P;
-                const uint32_t w = mt_temper(wl[k]);
-                const float bern = (u24(w) < p) ? 1.f : 0.f;
-                const float iq = fl + bern;                           // AS:484
-                const float t1 = iq * fh;                             // AS:486 in f32 (no fma: -ffp-contract=off)
-                const float t2 = t1 + (float)h_cur[k];
-                const float idxf = t2 + fhalf;
-                if (!(idxf > -9.0e18f && idxf < 9.0e18f)) {
-                    flags |= UQ_QFL_BAD_INDEX;
-                } else {
-                    idx = (int64_t)idxf;                              // .long(): truncation
-                    if (idx < -numel || idx >= numel) flags |= UQ_QFL_BAD_INDEX;
-                    else if (idx < 0) idx += numel;                   // torch.take wraps negatives
-                }
-                idx = idx < 0 ? 0 : (idx >= numel ? numel - 1 : idx);  // (flagged above; stay in bounds)
-                cr.v[k] = v;
-                cr.ex |= (ex ? 1u : 0u) << k;
-            }
-            cr.t[k] = a.tab[idx];                                     // AS:486-487 (idx 0 when inactive)
+            const float v = r_cur[k] * sc;                            // AS:472
+            const bool ex = (v > thr) || (v < -thr);                  // AS:478
+            const float q = ex ? 0.f : div1(v, dp);                   // AS:480-481 (= v / delta)
+            const float fl = floorf(q);
+            const float p = q - fl;                                   // AS:483
+            flags |= (active && !(p >= 0.f && p <= 1.f)) ? UQ_QFL_BAD_P : 0;
+            const float bern = (u24(mt_temper(wl[k])) < p) ? 1.f : 0.f;
+            const float iq = fl + bern;                               // AS:484
+            const float t1 = iq * fh;                                 // AS:486 in f32 (no fma: -ffp-contract=off)
+            const float t2 = t1 + (float)h_cur[k];
+            const float it = truncf(t2 + fhalf);                      // .long() truncates
+            const bool inr = it >= -fnumel && it < fnumel;            // torch.take's range (NaN: out)
+            flags |= (active && !inr) ? UQ_QFL_BAD_INDEX : 0;
+            int32_t idx = inr ? (int32_t)it : 0;
+            idx = idx < 0 ? idx + numel : idx;                        // torch.take wraps negatives
+            const auto t = __builtin_amdgcn_raw_buffer_load_b64(rt, (uint32_t)idx * 8u, 0, 0);   // AS:486-487
+            cr.t[k][0] = t[0];
+            cr.t[k][1] = t[1];
+            cr.v[k] = v;
+            cr.ex |= (active && ex ? 1u : 0u) << k;
+            cr.act |= (active ? 1u : 0u) << k;
         }
         if (have_prev) finish(pr, prev_i0);                         // round c-1 while round c's gathers fly
         pr = cr;
