@@ -18,6 +18,8 @@
  *   gcc -O2 -mfma -fopenmp -ffp-contract=off tools/markstein_check.c -o /tmp/mk -lm
  *   /tmp/mk [n_divisors=14]        # ~13 s per divisor on 8 cores
  *   /tmp/mk 13 m                   # the biased dequantize divisors m (div_plan_m)
+ *   /tmp/mk 6 q                    # QUIC-FL's q = v / delta (quicfl_send_wave_kernel, div_plan_norm):
+ *                                  # the deltas of the reference's four data.txt (AS:480) and the tests' 0.06, 0.05
  * Round-1 run: 14 divisors, 59,894,661,120 quotients, 0 mismatches.  An earlier variant
  * without the guard showed the failures it removes: |x| <= 2^-87 (residual underflow).
  */
@@ -48,6 +50,9 @@ static const float kM[] = {219.f, 652.f, 224426.f, 668488.f, 897706.f, 2673952.f
 
 int main(int argc, char** argv) {
     const int mmode = argc > 2 && strcmp(argv[2], "m") == 0;
+    const int qmode = argc > 2 && strcmp(argv[2], "q") == 0;
+    static const double kDelta[] = {0.0006194538156387708, 0.0006194538156392149, 0.0006194538156414353, 0.06, 0.05,
+                                    0.0006194538156414353 * 4096};
     const int nb = argc > 1 ? atoi(argv[1]) : 14;
     uint64_t s = 12345;
     long long bad = 0, total = 0;
@@ -61,6 +66,10 @@ int main(int argc, char** argv) {
         if (mmode) {
             if (ib >= (int)(sizeof kM / sizeof kM[0])) break;
             den = kM[ib];
+        }
+        if (qmode) {
+            if (ib >= (int)(sizeof kDelta / sizeof kDelta[0])) break;
+            den = (float)kDelta[ib];
         }
         const float y = 1.0f / den, thr = 0x1p-59f / den;
         long long lb = 0;
