@@ -402,40 +402,48 @@ quicfl_recv_wave_kernel(const int32_t* __restrict__ X, int64_t n, int64_t D, con
     if (lane == 0) mt_seed(Ls, (uint32_t)prng_seeds[j]);
     wave_lds_fence();
     const int64_t row = j * D;
-    const float sc = scale[j];
+    const uint32_t Du = (uint32_t)D;
+    const DivPlan dp = div_plan_norm(scale[j]);                 // v / scale (AS:532): exact quotient
+    const uint32_t hl = (uint32_t)h_len;
+    const bool hpow2 = (hl & (hl - 1)) == 0;
     const int64_t nch = (D + kMtN - 1) / kMtN;
-    // loads unconditional with clamped indices (see the sender), the next round's first
-    const int64_t last = D - 1;
+    // buffer descriptors: branch-free loads (0 beyond D) and stores (dropped beyond D)
+    const __amdgpu_buffer_rsrc_t rXs = make_rsrc(X + row, Du * 4u);
+    const __amdgpu_buffer_rsrc_t rmk = make_rsrc(exact_mask ? (const void*)(exact_mask + row) : (const void*)X,
+                                                 exact_mask ? Du : 0u);
+    const __amdgpu_buffer_rsrc_t rvl = make_rsrc(exact_vals ? (const void*)(exact_vals + row) : (const void*)X,
+                                                 exact_vals ? Du * 4u : 0u);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(out + row, Du * 4u);
     int32_t xr[kMtGroups];
-    uint8_t mr[kMtGroups];
+    uint32_t mr[kMtGroups];
     float vr[kMtGroups];
-    auto load_round = [&](int64_t i0, int32_t* xo, uint8_t* mo, float* vo) {
+    auto load_round = [&](uint32_t i0, int32_t* xo, uint32_t* mo, float* vo) {
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
-            const int64_t i = i0 + 64 * k + lane;
-            const int64_t ic = i < last ? i : last;
-            xo[k] = X[row + ic];
-            mo[k] = exact_mask ? exact_mask[row + ic] : (uint8_t)0;
-            vo[k] = exact_mask ? exact_vals[row + ic] : 0.f;
+            const uint32_t i = i0 + 64u * k + lane;
+            xo[k] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rXs, i * 4u, 0, kAuxNT);
+            mo[k] = __builtin_amdgcn_raw_buffer_load_b8(rmk, i, 0, 0);
+            vo[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rvl, i * 4u, 0, 0));
         }
     };
     load_round(0, xr, mr, vr);
     for (int64_t c = 0; c < nch; ++c) {
-        const int64_t i0 = c * kMtN;
+        const uint32_t i0 = (uint32_t)(c * kMtN);
         int32_t xn[kMtGroups];
-        uint8_t mn[kMtGroups];
+        uint32_t mn[kMtGroups];
         float vn[kMtGroups];
         load_round(i0 + kMtN, xn, mn, vn);
         mt_twist_wave(Ls, lane);
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
-            const int64_t i = i0 + e;
-            const uint32_t h = mt_temper(Ls[e < kMtN ? e : 0]) % (uint32_t)h_len;     // AS:528 randint
-            int64_t idx = (int64_t)xr[k] * h_len + h;                                   // AS:530 take
+            const uint32_t w = mt_temper(Ls[e < kMtN ? e : 0]);
+            const uint32_t h = hpow2 ? (w & (hl - 1u)) : (w % hl);                     // AS:528 randint
+            int32_t idx = xr[k] * h_len + (int32_t)h;                                   // AS:530 take
             idx = idx < 0 ? 0 : (idx >= tab_n ? tab_n - 1 : idx);                       // validated by the host
             const float v = mr[k] ? vr[k] : tab[idx];                                   // AS:531
-            if (e < kMtN && i < D) out[row + i] = v / sc;                              // AS:532
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(div1(v, dp)), ro,     // AS:532
+                                                  qf_off(e < kMtN, (i0 + (uint32_t)e) * 4u), 0, kAuxNT);
             xr[k] = xn[k];
             mr[k] = mn[k];
             vr[k] = vn[k];
