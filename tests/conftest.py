@@ -32,3 +32,13 @@ def pytest_report_header(config):
         return [f"uqdme library build id: {got} ({'matches' if got == build_ext.build_id() else 'STALE vs'} sources)"]
     except Exception as e:  # noqa: BLE001  (the header must never break collection)
         return [f"uqdme library: not loaded ({e})"]
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _release_output_pool():
+    """The one-shot APIs keep output sets of large batches (outpool.py); release them after
+    each test module so a later module's large allocations do not compete with them."""
+    yield
+    mod = sys.modules.get("uqdme_amd.outpool")
+    if mod is not None:
+        mod.POOL.clear()

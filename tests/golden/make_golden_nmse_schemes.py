@@ -33,17 +33,27 @@ sys.path.insert(0, "/root/reference/NMSE_Results/Codes")
 import All_Schemes as AS  # noqa: E402  (the reference module)
 
 SCHEMES = [("eden", 1), ("eden", 2), ("unbiased", 1), ("unbiased", 2), ("biased", 1), ("biased", 2)]
+QUICFL = [("quicfl", 1), ("quicfl", 2)]          # ND:141-142, after the biased quantizer
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--dists", default="normal,laplace,gamma,bernoulli,lognormal")
+    ap.add_argument("--quicfl", action="store_true",
+                    help="also QUICFL_quantize (ND:141-142) on the synthetic sender tables of quicfl_tables.py")
     a = ap.parse_args()
     DIM = a.dim
     torch.set_num_threads(1)
     fns = {"eden": AS.EDEN_quantize_Hadamard, "unbiased": AS.Type_unbiased_quantize,
-           "biased": AS.Type_biased_quantize}
+           "biased": AS.Type_biased_quantize, "quicfl": AS.QUICFL_quantize}
+    schemes = SCHEMES + (QUICFL if a.quicfl else [])
+    if a.quicfl:                                    # the sender reads its tables from a prefix (AS:431)
+        import tempfile
+        sys.path.insert(0, HERE)
+        from make_golden_quicfl_sender import write_prefix
+        pre = write_prefix(os.path.join(tempfile.mkdtemp(prefix="qfl_nd_"), "pub"))
+        AS.QuicFLSender.__init__.__defaults__ = ("cpu", [1, 2, 3, 4], [6, 5, 4, 4], pre)
     gens = {"normal": lambda: np.random.normal(0, 1, DIM),
             "laplace": lambda: np.random.laplace(loc=1, scale=2, size=DIM),
             "gamma": lambda: np.random.gamma(shape=2, scale=2, size=DIM),
@@ -71,21 +81,23 @@ def main():
                     vecs.append(torch.as_tensor(v, dtype=torch.float32))
                 vns = sum(norms)
                 emp = torch.stack(vecs).sum(dim=0) / n
-                est = {k: torch.zeros(DIM) for k in SCHEMES}
+                est = {k: torch.zeros(DIM) for k in schemes}
                 for j, v in enumerate(vecs):
-                    for k in SCHEMES:
+                    for k in schemes:
                         del seen[:]
                         est[k] += torch.as_tensor(fns[k[0]](v, k[1])) / n
                         if k[0] == "eden":
                             assert len(seen) == 1
                             scales.setdefault(dist, []).append([n, inst, j, k[1], seen[0][0], seen[0][1]])
                 row = {"n": n, "inst": inst}
-                for k in SCHEMES:
+                for k in schemes:
                     row[f"{k[0]}{k[1]}"] = float(torch.norm(est[k] - emp).pow(2) / (50 * vns * n))
                 rows.append(row)
                 print(dist, row, flush=True)
         res[dist] = rows
     name = "nd_nmse_schemes.json" if DIM == 2048 else f"nd_nmse_schemes_d{DIM}.json"
+    if a.quicfl:
+        name = name.replace(".json", "_quicfl.json")
     with open(os.path.join(HERE, name), "w") as f:
         json.dump({"dim": DIM, "rows": res, "eden_scales_fields": ["n", "inst", "client", "bits", "seed", "scale_bits"],
                    "eden_scales": scales}, f, indent=1)

@@ -136,3 +136,37 @@ def test_multi_scheme_nmse_known_answers(gpu_ready, fixture):
             for r in (1, 2):
                 got = np.float32(sub[("eden", r)]["script"][ui, row["inst"]])
                 assert got == np.float32(row[f"eden{r}"]), (dist, row["n"], row["inst"], r, got, row[f"eden{r}"])
+
+
+def test_nd_loop_with_quicfl_known_answers(gpu_ready):
+    """The driver loop with QUICFL_quantize in its place (ND:141-142, after the biased
+    quantizer) against the reference's own loop on synthetic sender tables
+    (tests/golden/nd_nmse_schemes_quicfl.json, make_golden_nmse_schemes.py --quicfl): the
+    QUIC-FL draws (a message seed, then D bernoulli(p_X) words of the global generator per
+    call) interleave with EDEN's and the unbiased quantizer's, so every scheme's NMSE is
+    checked; unbiased, biased and QUIC-FL within 1e-6 relative (QUIC-FL bit for bit in
+    practice), EDEN as in test_multi_scheme_nmse_known_answers."""
+    import json
+    import os
+    import sys
+    import uqdme
+    from tests.golden_data import GOLDEN
+    sys.path.insert(0, GOLDEN)
+    from quicfl_tables import DATA, sender_tables
+    ref = json.load(open(os.path.join(GOLDEN, "nd_nmse_schemes_quicfl.json")))
+    rz = np.load(os.path.join(GOLDEN, "quicfl_recv_vectors.npz"))
+    tx = uqdme.QuicFLSender(tables={b: (*sender_tables(b), DATA[b]) for b in (1, 2, 3, 4)})
+    rx = uqdme.QuicFLReceiver(tables={b: rz[f"recv{b}"] for b in (1, 2, 3, 4)})
+    for dist, rows in ref["rows"].items():
+        res = uqdme.nmse_simulation(dist, dim=ref["dim"], users=(1, 6), num_instances=2,
+                                    schemes=("eden", "unbiased", "biased", "quicfl"), torch_threads=1, quicfl=(tx, rx))
+        for row in rows:
+            ui = (1, 6).index(row["n"])
+            for sc in ("eden", "unbiased", "biased", "quicfl"):
+                for r in (1, 2):
+                    got = float(res[(sc, r)]["script"][ui, row["inst"]])
+                    exp = row[f"{sc}{r}"]
+                    assert abs(got - exp) <= 1e-6 * exp, (dist, row["n"], row["inst"], sc, r, got, exp)
+            for r in (1, 2):
+                got = np.float32(res[("quicfl", r)]["script"][ui, row["inst"]])
+                assert got == np.float32(row[f"quicfl{r}"]), (dist, row, r)

@@ -16,9 +16,12 @@ The reference also calls other schemes in the same loop (ND:133-147), consuming 
 global torch RNG in client-major, scheme-minor order.  `schemes` selects which of the
 implemented ones run, in the reference's call order: EDEN_quantize_Hadamard (ND:135-136,
 one randint(0, 100) per call), Type_unbiased_quantize (ND:137-138, one rand(1) per call),
-Type_biased_quantize (ND:139-140, no draws).  DRIVE / QUIC-FL / Kashin / Scalar are not
-built (the shipped drivers crash at QUIC-FL, ND:141, whose sender tables are missing), so
-the draw stream equals that of a driver calling only the selected schemes.
+Type_biased_quantize (ND:139-140, no draws), QUICFL_quantize (ND:141-142: one randint(0, 100)
+for the message seed, then D words of the same generator for bernoulli(p_X), AS:489 -- the host
+advances a copy of the CPU generator past those words and hands each message its generator
+state, so the batched sender draws exactly the reference's words; tables from `quicfl=(sender,
+receiver)` or the drop-in's prefix).  DRIVE / Kashin / Scalar are not built, so the draw stream
+equals that of a driver calling only the selected schemes.
 """
 from __future__ import annotations
 
@@ -28,8 +31,9 @@ import torch
 from .biased import biased_quantize
 from .eden import eden_compress, eden_decompress, eden_quantize
 from .quantizer import client_mean, quantize_dequantize
+from .quicfl import quicfl_compress, quicfl_decompress_messages
 
-SCHEME_ORDER = ("eden", "unbiased", "biased")     # ND:135-140 call order
+SCHEME_ORDER = ("eden", "unbiased", "biased", "quicfl")     # ND:135-142 call order
 
 __all__ = ["DISTRIBUTIONS", "draw_vectors", "nmse_simulation", "USERS_ND"]
 
@@ -62,7 +66,8 @@ def draw_vectors(dist: str, n: int, dim: int, rs=np.random):
 
 def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_instances: int = 50,
                     num_trials: int = 50, rates=(1, 2), seed: int = 42, torch_threads: int = 1,
-                    device=None, schemes=("unbiased",), progress=None, eden_scales=None, eden_scales_out=None):
+                    device=None, schemes=("unbiased",), progress=None, eden_scales=None, eden_scales_out=None,
+                    quicfl=None):
     """NMSE curves of the selected schemes with the reference's normalisation.
 
     Returns {rate: {...}} for the default unbiased-only run, else {(scheme, rate): {...}};
@@ -77,6 +82,11 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
         if sc not in SCHEME_ORDER:
             raise ValueError(f"unknown scheme {sc!r}")
     order = [sc for sc in SCHEME_ORDER if sc in schemes]
+    if "quicfl" in order:
+        from .eden import padded_dim
+        from .quicfl import _dropin_pair, generator_words
+        qsend, qrecv = quicfl if quicfl is not None else _dropin_pair()
+        qD = padded_dim(dim)
     rs = np.random.RandomState(seed)                 # legacy stream == np.random.seed(seed)
     gen = torch.Generator().manual_seed(seed)        # == torch.manual_seed(seed) CPU stream
     keys = [(sc, r) for sc in order for r in rates]
@@ -94,6 +104,10 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                             draws[(sc, r)].append(int(torch.randint(0, 100, (1,), generator=gen)))   # AS:797
                         elif sc == "unbiased":
                             draws[(sc, r)].append(float(torch.rand(1, generator=gen)))               # AS:634
+                        elif sc == "quicfl":
+                            seed = int(torch.randint(0, 100, (1,), generator=gen))                    # AS:820
+                            draws[(sc, r)].append((seed, generator_words(gen)[1]))
+                            torch.rand(qD, generator=gen)          # the D bernoulli(p_X) words (AS:489)
             xd = xs.to(device)
             for sc, r in keys:
                 if sc == "unbiased":
@@ -101,6 +115,11 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                                             torch_threads=torch_threads)
                 elif sc == "biased":
                     q = biased_quantize(xd, r, torch_threads=torch_threads)
+                elif sc == "quicfl":
+                    seeds = [s_ for s_, _ in draws[(sc, r)]]
+                    states = np.stack([w for _, w in draws[(sc, r)]])
+                    msg = quicfl_compress(xd, r, seeds, [123] * n, sender=qsend, px_states=states)   # AS:822
+                    q = quicfl_decompress_messages(msg, qrecv.recv_table[r])
                 elif eden_scales is None and eden_scales_out is None:
                     q = eden_quantize(xd, r, seeds=draws[(sc, r)])
                 else:                                 # compress, (record / replace the scale), decompress

@@ -14,7 +14,9 @@ time.  For large batches the one-shot APIs therefore take their outputs from thi
     used the slowest free ones are released, so the loop settles on the fastest placements
     (at least two, since a caller typically holds the previous result while asking for the
     next);
-  * small batches (< `min_bytes`) bypass the pool: their placement does not matter.
+  * small batches (< `min_bytes`) bypass the pool: their placement does not matter; the pool
+    holds at most `max_frac` of device memory (then a call gets a plain allocation), and
+    `POOL.clear()` releases everything it holds.
 
 Results are the same bits whichever set is used; only the time differs.
 """
@@ -61,8 +63,12 @@ class _Set:
 
 
 class OutputPool:
-    def __init__(self, explore: int = 6, keep: int = 2, min_bytes: int = 1 << 28, reserve_frac: float = 0.25):
+    def __init__(self, explore: int = 6, keep: int = 2, min_bytes: int = 1 << 28, reserve_frac: float = 0.25,
+                 max_frac: float = 0.125):
+        # max_frac: the pool never holds more than this share of device memory (36 GB of an
+        # MI355X's 288 GB); beyond it a call gets a plain allocation
         self.explore, self.keep, self.min_bytes, self.reserve_frac = explore, keep, min_bytes, reserve_frac
+        self.max_frac = max_frac
         self._lock = threading.Lock()
         self._sets: dict = {}
         self.enabled = True
@@ -96,7 +102,9 @@ class OutputPool:
                 # exploring: a new placement; explored but every kept set is held: one more
                 if len(sets) < self.explore + self.keep:
                     fm, tot = torch.cuda.mem_get_info(dev)
-                    if fm - nbytes >= self.reserve_frac * tot:
+                    pooled = sum(sum(b.numel() * b.element_size() for b in st.bufs)
+                                 for e in self._sets.values() for st in e["sets"] if e is not None)
+                    if fm - nbytes >= self.reserve_frac * tot and pooled + nbytes <= self.max_frac * tot:
                         chosen = self._alloc(dev, specs)
                         sets.append(chosen)
             if chosen is None and free:
