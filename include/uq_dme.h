@@ -257,6 +257,7 @@ int uq_quicfl_prepare_f32(const int32_t* X, int64_t n, int64_t D, const float* r
 #define UQ_QFL_BAD_INDEX 2
 #define UQ_QFL_BAD_PX 4
 #define UQ_QFL_X_RANGE 8
+#define UQ_QFL_TIMEOUT 16   /* internal: a wait of the few-message kernel ran out (never expected) */
 #define UQ_QFL_STATE_WORDS 626
 int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out);
 int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,

@@ -196,6 +196,17 @@ def test_batch_states_and_many_messages(fx):
         states[j] = q.generator_words(g)[1]
     msg, new = q.quicfl_compress(torch.from_numpy(x), nbits, seeds, [123] * n, sender=snd, px_states=states,
                                  _state_out=True)
+    # the first 20 messages again as a few-message call (one workgroup per message: scout
+    # waves hand each run its generator blocks): the same bits and end states as the batch's
+    # one-wave-per-message kernel
+    few, fnew = q.quicfl_compress(torch.from_numpy(x[:20]), nbits, seeds[:20], [123] * 20, sender=snd,
+                                  px_states=states[:20], _state_out=True)
+    assert torch.equal(few.X, msg.X[:20]) and torch.equal(few.exact_mask, msg.exact_mask[:20])
+    assert torch.equal(few.scale, msg.scale[:20]) and torch.equal(few.exact_count, msg.exact_count[:20])
+    for j in range(20):
+        cnt = int(few.exact_count[j])
+        assert torch.equal(few.exact_vals[j, :cnt], msg.exact_vals[j, :cnt]), j
+    assert np.array_equal(fnew, new[:20])
     tX, tp = sender_tables(nbits)
     for j in list(range(0, n, 37)) + [n - 1]:
         st = (int(states[j, 0]), int(states[j, 1]), states[j, 2:])

@@ -3556,6 +3556,15 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.info = info;
     q.D = w.D;
     q.n = n;
+    // few messages: a workgroup per message (scouts + runs: the streams' length is the critical
+    // path, not the per-coordinate work); batches: a wave per message
+    if (n <= kQfTeamMaxN && w.D >= (int64_t)kMtN * kQfRuns) {
+        if (x_kind == 0)
+            hipLaunchKernelGGL(quicfl_send_team_kernel<0>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
+        else
+            hipLaunchKernelGGL(quicfl_send_team_kernel<1>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
+        return hip_check(hipGetLastError(), "quicfl_send_team_kernel launch");
+    }
     const dim3 grid((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG));
     if (x_kind == 0)
         hipLaunchKernelGGL(quicfl_send_wave_kernel<0>, grid, dim3(64 * kQfWavesPerWG), 0, st, q);

@@ -157,76 +157,75 @@ struct QflRound {
 
 __device__ __forceinline__ uint32_t qf_off(bool ok, uint32_t off) { return ok ? off : 0xFFFFFFFFu; }  // dropped
 
-// Every per-element global access goes through a buffer descriptor (32-bit offsets,
-// out-of-range loads return 0 and out-of-range stores are dropped): no per-element branches,
-// and a lane's ten loads of a round are all in flight at once (a load under a per-element
-// branch is waited for before the next one).  XK: 0 = int64 X (the drop-in's X.long()),
-// 1 = uint8 X (batches).
-template <int XK>
-__global__ void __launch_bounds__(64 * kQfWavesPerWG)
-quicfl_send_wave_kernel(QflSendArgs a) {
-    __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];      // local generator block per wave
-    __shared__ uint32_t Gsh[kQfWavesPerWG][kMtN];      // global generator block per wave
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
-    if (j >= a.n) return;                                       // whole wave: no barrier below
-    uint32_t* Ls = Lsh[wv];
-    uint32_t* Gs = Gsh[wv];
-    const int64_t D = a.D;
-    const uint32_t Du = (uint32_t)D;
-    const int64_t row = j * D;
-    int32_t gleft = 1, gnext = 0;
-    if (a.px_state) {
-        const uint32_t* st = a.px_state + j * kQfStateWords;
-        gleft = (int32_t)st[0];
-        gnext = (int32_t)st[1];
-        for (int i = lane; i < kMtN; i += 64) Gs[i] = st[2 + i];
-    } else if (lane == 1) {
-        mt_seed(Gs, (uint32_t)a.px_seeds[j]);
-    }
-    if (lane == 0) mt_seed(Ls, (uint32_t)a.prng_seeds[j]);
-    wave_lds_fence();
-    const float sc = (1.0f / a.nrm[j]) * a.sqrtD;              // AS:466/470 (IEEE 1/x, then f32 mul)
-    const int64_t nch = (D + kMtN - 1) / kMtN;
-    const uint32_t h_len = (uint32_t)a.h_len;
-    const bool hpow2 = (h_len & (h_len - 1)) == 0;
-    const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.rot + row, Du * 4u);
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.hbuf + row, Du);
-    const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.mask + row, Du);
-    const __amdgpu_buffer_rsrc_t rX = make_rsrc(XK == 0 ? (void*)((int64_t*)a.X + row) : (void*)((uint8_t*)a.X + row),
-                                                XK == 0 ? Du * 8u : Du);
-    const __amdgpu_buffer_rsrc_t rt = make_rsrc(a.tab, (uint32_t)a.numel * 8u);
+// Per-message constants of the sender's passes (wave-uniform).
+struct QflCtx {
+    int64_t row, D;
+    int64_t qL, qG;             // block of the first pass-B word of round 0 (local, global)
+    int rL, rG;                 // its slot
+    __amdgpu_buffer_rsrc_t rr, rh, rm, rX, rt;
+    float sc, fh, fhalf, fnumel;
+    DivPlan dp;
+    int32_t numel;
+    uint32_t h_len;
+    bool hpow2;
+};
 
-    // ---- pass A: h = randint(0, h_len, (D,), local) (AS:465/469): word i is block c + 1, slot e
-    for (int64_t c = 0; c < nch; ++c) {
+template <int XK>
+__device__ __forceinline__ QflCtx qfl_ctx(const QflSendArgs& a, int64_t j, int32_t gleft, int32_t gnext) {
+    QflCtx c;
+    c.D = a.D;
+    c.row = j * a.D;
+    const uint32_t Du = (uint32_t)a.D;
+    const int64_t vL = (int64_t)kMtN + a.D;                         // pass-B local words D + i
+    c.qL = vL / kMtN;
+    c.rL = (int)(vL % kMtN);
+    const int64_t vG = gleft > 1 ? (int64_t)gnext : (int64_t)kMtN;  // the first left - 1 words are state[next ..]
+    c.qG = vG / kMtN;
+    c.rG = (int)(vG % kMtN);
+    c.rr = make_rsrc(a.rot + c.row, Du * 4u);
+    c.rh = make_rsrc(a.hbuf + c.row, Du);
+    c.rm = make_rsrc(a.mask + c.row, Du);
+    c.rX = make_rsrc(XK == 0 ? (void*)((int64_t*)a.X + c.row) : (void*)((uint8_t*)a.X + c.row), XK == 0 ? Du * 8u : Du);
+    c.rt = make_rsrc(a.tab, (uint32_t)a.numel * 8u);
+    c.sc = (1.0f / a.nrm[j]) * a.sqrtD;                             // AS:466/470 (IEEE 1/x, then f32 mul)
+    c.dp = div_plan_norm(a.delta);                                  // q = v / delta: reciprocal + Markstein (exact)
+    c.fh = (float)a.h_len;
+    c.fhalf = (float)a.half;
+    c.fnumel = (float)a.numel;                                      // exact: numel < 2^24 (host check)
+    c.numel = (int32_t)a.numel;
+    c.h_len = (uint32_t)a.h_len;
+    c.hpow2 = (c.h_len & (c.h_len - 1)) == 0;
+    return c;
+}
+
+// Pass A over rounds [c0, c1): Ls holds block c0 of the local stream on entry (block c + 1 holds
+// the words of round c), block c1 on exit.  h = randint(0, h_len, (D,), local) (AS:465/469).
+__device__ __forceinline__ void qfl_pass_a(const QflCtx& c, uint32_t* Ls, int64_t c0, int64_t c1, int lane) {
+    for (int64_t r = c0; r < c1; ++r) {
         mt_twist_wave(Ls, lane);
-        const uint32_t i0 = (uint32_t)(c * kMtN);
+        const uint32_t i0 = (uint32_t)(r * kMtN);
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
             const uint32_t w = mt_temper(Ls[e < kMtN ? e : 0]);
-            const uint32_t h = hpow2 ? (w & (h_len - 1u)) : (w % h_len);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)h, rh, qf_off(e < kMtN, i0 + (uint32_t)e), 0, 0);
+            const uint32_t h = c.hpow2 ? (w & (c.h_len - 1u)) : (w % c.h_len);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)h, c.rh, qf_off(e < kMtN, i0 + (uint32_t)e), 0, 0);
         }
     }
-    int64_t haveL = nch;                                        // block in Ls
+}
 
-    // ---- pass B: local words D + i (virtual position 624 + D + i), global words i
-    const int64_t vL = (int64_t)kMtN + D;
-    const int64_t qL = vL / kMtN;
-    const int rL = (int)(vL % kMtN);
-    const int64_t vG = gleft > 1 ? (int64_t)gnext : (int64_t)kMtN;     // the first left - 1 words are state[next ..]
-    const int64_t qG = vG / kMtN;
-    const int rG = (int)(vG % kMtN);
-    int64_t haveG = 0;
+// Pass B over rounds [c0, c1) (AS:472-490): Ls holds local block haveL <= qL + c0, Gs global
+// block haveG <= qG + c0.  Exact values go to ev[row + ev_base + count] in index order; returns
+// the count, ORs UQ_QFL_* into flags.  Every per-element global access goes through a buffer
+// descriptor (out-of-range loads return 0, stores are dropped): no per-element branch, and a
+// lane's ten loads of a round are in flight together.
+template <int XK>
+__device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict__ ev, uint32_t* Ls, int64_t& haveL,
+                                              uint32_t* Gs, int64_t& haveG, int64_t c0, int64_t c1, int64_t ev_base,
+                                              int32_t& flags, int lane) {
+    const int64_t D = c.D;
     const float thr = kQflExactT;
-    const DivPlan dp = div_plan_norm(a.delta);                  // q = v / delta: reciprocal + Markstein (exact)
-    const float fh = (float)a.h_len;
-    const float fhalf = (float)a.half;
-    const float fnumel = (float)a.numel;                        // exact: numel < 2^24 (host check)
-    const int32_t numel = (int32_t)a.numel;
-    int32_t flags = 0;
-    int64_t etot = 0;                                           // exact values written so far
+    int64_t etot = 0;
     QflRound pr;                                                // the previous round (stage 2 pending)
     bool have_prev = false;
     uint32_t prev_i0 = 0;
@@ -234,9 +233,9 @@ quicfl_send_wave_kernel(QflSendArgs a) {
     uint32_t h_cur[kMtGroups], h_nxt[kMtGroups];
 #pragma unroll
     for (int k = 0; k < kMtGroups; ++k) {
-        const uint32_t e = 64u * k + lane;
-        r_cur[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, e * 4u, 0, kAuxNT));
-        h_cur[k] = __builtin_amdgcn_raw_buffer_load_b8(rh, e, 0, 0);
+        const uint32_t e = (uint32_t)(c0 * kMtN) + 64u * k + lane;
+        r_cur[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.rr, e * 4u, 0, kAuxNT));
+        h_cur[k] = __builtin_amdgcn_raw_buffer_load_b8(c.rh, e, 0, 0);
     }
 
     auto finish = [&](const QflRound& r, uint32_t i0) {          // stage 2 of a round (AS:489-490, 494-495)
@@ -253,64 +252,62 @@ quicfl_send_wave_kernel(QflSendArgs a) {
                 const bool ok = xf > -9.2e18f && xf < 9.2e18f;
                 flags |= (active && !ok) ? UQ_QFL_X_RANGE : 0;
                 const int64_t xv = ok ? (int64_t)xf : 0;             // AS:490 .long()
-                const uint32_t lo = (uint32_t)xv, hi = (uint32_t)((uint64_t)xv >> 32);
                 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-                const u32x2v w = {lo, hi};
-                __builtin_amdgcn_raw_buffer_store_b64(w, rX, qf_off(active, i * 8u), 0, kAuxNT);
+                const u32x2v w = {(uint32_t)xv, (uint32_t)((uint64_t)xv >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(w, c.rX, qf_off(active, i * 8u), 0, kAuxNT);
             } else {
                 const bool ok = xf > -1.0f && xf < 256.0f;
                 flags |= (active && !ok) ? UQ_QFL_X_RANGE : 0;
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ok ? (int32_t)xf : 0), rX, qf_off(active, i), 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ok ? (int32_t)xf : 0), c.rX, qf_off(active, i), 0, 0);
             }
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ex ? 1 : 0), rm, qf_off(active, i), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ex ? 1 : 0), c.rm, qf_off(active, i), 0, 0);
             const uint64_t bal = __ballot(active && ex);            // index order: group k, then lane
-            if (active && ex) a.ev[row + etot + __popcll(bal & ((1ull << lane) - 1ull))] = r.v[k];
+            if (active && ex) ev[c.row + ev_base + etot + __popcll(bal & ((1ull << lane) - 1ull))] = r.v[k];
             etot += __popcll(bal);
         }
     };
 
-    for (int64_t c = 0; c < nch; ++c) {
-        const uint32_t i0 = (uint32_t)(c * kMtN);
+    for (int64_t rd = c0; rd < c1; ++rd) {
+        const uint32_t i0 = (uint32_t)(rd * kMtN);
         const int lastE = (int)((D - 1 - (int64_t)i0) < (kMtN - 1) ? (D - 1 - (int64_t)i0) : (kMtN - 1));
         // next round's loads first (beyond D: the descriptor returns 0)
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const uint32_t in = i0 + (uint32_t)kMtN + 64u * k + lane;
-            r_nxt[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, in * 4u, 0, kAuxNT));
-            h_nxt[k] = __builtin_amdgcn_raw_buffer_load_b8(rh, in, 0, 0);
+            r_nxt[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.rr, in * 4u, 0, kAuxNT));
+            h_nxt[k] = __builtin_amdgcn_raw_buffer_load_b8(c.rh, in, 0, 0);
         }
-        // the words of this round: slots rX + e of blocks qX + c (before) and qX + c + 1 (after)
-        while (haveL < qL + c) { mt_twist_wave(Ls, lane); ++haveL; }
-        while (haveG < qG + c) { mt_twist_wave(Gs, lane); ++haveG; }
-        // (slot p = rX + e: p < 624 before the twist, p - 624 after; reads unconditional)
+        // the words of this round: slots rX + e of blocks qX + rd (before) and qX + rd + 1 (after)
+        while (haveL < c.qL + rd) { mt_twist_wave(Ls, lane); ++haveL; }
+        while (haveG < c.qG + rd) { mt_twist_wave(Gs, lane); ++haveG; }
         uint32_t wl[kMtGroups], wg[kMtGroups];
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
-            wl[k] = Ls[rL + e < kMtN ? rL + e : 0];
-            wg[k] = Gs[rG + e < kMtN ? rG + e : 0];
+            wl[k] = Ls[c.rL + e < kMtN ? c.rL + e : 0];
+            wg[k] = Gs[c.rG + e < kMtN ? c.rG + e : 0];
         }
-        if (rL + lastE >= kMtN) {
+        if (c.rL + lastE >= kMtN) {
             mt_twist_wave(Ls, lane);
             ++haveL;
 #pragma unroll
             for (int k = 0; k < kMtGroups; ++k) {
-                const int p = rL + 64 * k + lane;
+                const int p = c.rL + 64 * k + lane;
                 const uint32_t w = Ls[p >= kMtN && p < 2 * kMtN ? p - kMtN : 0];
                 if (p >= kMtN) wl[k] = w;
             }
         }
-        if (rG + lastE >= kMtN) {
+        if (c.rG + lastE >= kMtN) {
             mt_twist_wave(Gs, lane);
             ++haveG;
 #pragma unroll
             for (int k = 0; k < kMtGroups; ++k) {
-                const int p = rG + 64 * k + lane;
+                const int p = c.rG + 64 * k + lane;
                 const uint32_t w = Gs[p >= kMtN && p < 2 * kMtN ? p - kMtN : 0];
                 if (p >= kMtN) wg[k] = w;
             }
         }
-        // stage 1 of round c: AS:472-487, the gather issued (branch-free: inactive elements
+        // stage 1 of round rd: AS:472-487, the gather issued (branch-free: inactive elements
         // compute on zeros, raise no flags and store nothing)
         QflRound cr;
         cr.ex = 0;
@@ -320,29 +317,29 @@ quicfl_send_wave_kernel(QflSendArgs a) {
             const int e = 64 * k + lane;
             const bool active = e < kMtN && (int64_t)i0 + e < D;
             cr.wg[k] = mt_temper(wg[k]);
-            const float v = r_cur[k] * sc;                            // AS:472
+            const float v = r_cur[k] * c.sc;                          // AS:472
             const bool ex = (v > thr) || (v < -thr);                  // AS:478
-            const float q = ex ? 0.f : div1(v, dp);                   // AS:480-481 (= v / delta)
+            const float q = ex ? 0.f : div1(v, c.dp);                 // AS:480-481 (= v / delta)
             const float fl = floorf(q);
             const float p = q - fl;                                   // AS:483
             flags |= (active && !(p >= 0.f && p <= 1.f)) ? UQ_QFL_BAD_P : 0;
             const float bern = (u24(mt_temper(wl[k])) < p) ? 1.f : 0.f;
             const float iq = fl + bern;                               // AS:484
-            const float t1 = iq * fh;                                 // AS:486 in f32 (no fma: -ffp-contract=off)
+            const float t1 = iq * c.fh;                               // AS:486 in f32 (no fma: -ffp-contract=off)
             const float t2 = t1 + (float)h_cur[k];
-            const float it = truncf(t2 + fhalf);                      // .long() truncates
-            const bool inr = it >= -fnumel && it < fnumel;            // torch.take's range (NaN: out)
+            const float it = truncf(t2 + c.fhalf);                    // .long() truncates
+            const bool inr = it >= -c.fnumel && it < c.fnumel;        // torch.take's range (NaN: out)
             flags |= (active && !inr) ? UQ_QFL_BAD_INDEX : 0;
             int32_t idx = inr ? (int32_t)it : 0;
-            idx = idx < 0 ? idx + numel : idx;                        // torch.take wraps negatives
-            const auto t = __builtin_amdgcn_raw_buffer_load_b64(rt, (uint32_t)idx * 8u, 0, 0);   // AS:486-487
+            idx = idx < 0 ? idx + c.numel : idx;                      // torch.take wraps negatives
+            const auto t = __builtin_amdgcn_raw_buffer_load_b64(c.rt, (uint32_t)idx * 8u, 0, 0);   // AS:486-487
             cr.t[k][0] = t[0];
             cr.t[k][1] = t[1];
             cr.v[k] = v;
             cr.ex |= (active && ex ? 1u : 0u) << k;
             cr.act |= (active ? 1u : 0u) << k;
         }
-        if (have_prev) finish(pr, prev_i0);                         // round c-1 while round c's gathers fly
+        if (have_prev) finish(pr, prev_i0);                         // round rd-1 while round rd's gathers fly
         pr = cr;
         have_prev = true;
         prev_i0 = i0;
@@ -353,31 +350,182 @@ quicfl_send_wave_kernel(QflSendArgs a) {
         }
     }
     if (have_prev) finish(pr, prev_i0);
+    return etot;
+}
 
-    // flags: OR over the wave
-    for (int s = 32; s >= 1; s >>= 1) flags |= __shfl_xor(flags, s);
-    // the global generator after its D draws: the block holding word D - 1
-    if (a.px_state_out) {
-        uint32_t* so = a.px_state_out + j * kQfStateWords;
-        uint32_t left1, next1;
-        if (D <= (int64_t)gleft - 1) {                           // every draw from the current block
-            left1 = (uint32_t)(gleft - D);
-            next1 = (uint32_t)(gnext + D);
-        } else {
-            const int64_t pos = (vG + D - 1) % kMtN;
-            next1 = (uint32_t)(pos + 1);
-            left1 = (uint32_t)(kMtN - pos);
-        }
-        for (int i = lane; i < kMtN; i += 64) so[2 + i] = Gs[i];
-        if (lane == 0) {
-            so[0] = left1;
-            so[1] = next1;
-        }
+// The global generator's state after the message's D draws (the block holding word D - 1,
+// which Gs holds after the last round).
+__device__ __forceinline__ void qfl_state_out(uint32_t* so, const uint32_t* Gs, int64_t D, int32_t gleft, int32_t gnext,
+                                              int64_t vG, int lane) {
+    uint32_t left1, next1;
+    if (D <= (int64_t)gleft - 1) {                               // every draw from the current block
+        left1 = (uint32_t)(gleft - D);
+        next1 = (uint32_t)(gnext + D);
+    } else {
+        const int64_t pos = (vG + D - 1) % kMtN;
+        next1 = (uint32_t)(pos + 1);
+        left1 = (uint32_t)(kMtN - pos);
     }
+    for (int i = lane; i < kMtN; i += 64) so[2 + i] = Gs[i];
+    if (lane == 0) {
+        so[0] = left1;
+        so[1] = next1;
+    }
+}
+
+__device__ __forceinline__ void qfl_gen_init(const QflSendArgs& a, int64_t j, uint32_t* Gs, int32_t& gleft,
+                                             int32_t& gnext, int lane) {
+    gleft = 1;
+    gnext = 0;
+    if (a.px_state) {
+        const uint32_t* st = a.px_state + j * kQfStateWords;
+        gleft = (int32_t)st[0];
+        gnext = (int32_t)st[1];
+        for (int i = lane; i < kMtN; i += 64) Gs[i] = st[2 + i];
+    } else if (lane == 1) {
+        mt_seed(Gs, (uint32_t)a.px_seeds[j]);
+    }
+}
+
+// KQ1 for batches: one wave per message.  XK: 0 = int64 X (the drop-in's X.long()), 1 = uint8 X.
+template <int XK>
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_send_wave_kernel(QflSendArgs a) {
+    __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];      // local generator block per wave
+    __shared__ uint32_t Gsh[kQfWavesPerWG][kMtN];      // global generator block per wave
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    if (j >= a.n) return;                                       // whole wave: no barrier below
+    uint32_t* Ls = Lsh[wv];
+    uint32_t* Gs = Gsh[wv];
+    int32_t gleft, gnext;
+    qfl_gen_init(a, j, Gs, gleft, gnext, lane);
+    if (lane == 0) mt_seed(Ls, (uint32_t)a.prng_seeds[j]);
+    wave_lds_fence();
+    const QflCtx c = qfl_ctx<XK>(a, j, gleft, gnext);
+    const int64_t nch = (a.D + kMtN - 1) / kMtN;
+    qfl_pass_a(c, Ls, 0, nch, lane);
+    int64_t haveL = nch, haveG = 0;
+    int32_t flags = 0;
+    const int64_t etot = qfl_pass_b<XK>(c, a.ev, Ls, haveL, Gs, haveG, 0, nch, 0, flags, lane);
+    for (int s = 32; s >= 1; s >>= 1) flags |= __shfl_xor(flags, s);
+    if (a.px_state_out)
+        qfl_state_out(a.px_state_out + j * kQfStateWords, Gs, a.D, gleft, gnext, c.qG * kMtN + c.rG, lane);
     if (lane == 0) {
         a.ecount[j] = (int32_t)etot;
-        a.scale[j] = sc;
+        a.scale[j] = c.sc;
         a.info[j] = flags;
+    }
+}
+
+// KQ1 for a few messages (the per-call drop-in): one 512-thread workgroup per message.  Wave
+// 0 ("scout") runs the local stream from its seed through all 2D words, wave 1 the global stream
+// through D words; neither does per-coordinate work.  The other 6 waves take contiguous runs of
+// rounds: when a scout's stream reaches the block a run starts from, the scout copies the block
+// into that wave's LDS slice and raises its flag, so each run generates only its own words.
+// The critical path is the scout's 2D / 624 twists, not the coordinates' arithmetic.  Exact
+// values are written per run and compacted into index order at the end.  Flags are waited for
+// with a bounded spin (UQ_QFL_TIMEOUT if it ever ran out: the scouts never wait on anyone).
+constexpr int kQfTeamWaves = 8;                    // 2 scouts + 6 runs (<= 256 VGPRs per lane)
+constexpr int kQfRuns = kQfTeamWaves - 2;
+constexpr int64_t kQfTeamMaxN = 64;                 // messages per call up to which the team kernel runs
+__device__ __forceinline__ bool qfl_wait_flag(int* f) {
+    for (int it = 0; it < (1 << 24); ++it) {
+        if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+__device__ __forceinline__ void qfl_give(uint32_t* dst, const uint32_t* src, int* f, int lane) {
+    for (int i = lane; i < kMtN; i += 64) dst[i] = src[i];
+    wave_lds_fence();
+    if (lane == 0) __hip_atomic_store(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int XK>
+__global__ void __launch_bounds__(64 * kQfTeamWaves)
+quicfl_send_team_kernel(QflSendArgs a) {
+    __shared__ uint32_t LA[kQfRuns][kMtN], LB[kQfRuns][kMtN], GB[kQfRuns][kMtN];
+    __shared__ uint32_t SL[kMtN], SG[kMtN];             // the scouts' blocks
+    __shared__ int rdy[kQfRuns][3];
+    __shared__ int64_t cnt[kQfRuns];
+    __shared__ int32_t sflags;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = blockIdx.x;
+    const int64_t D = a.D;
+    const int64_t nch = (D + kMtN - 1) / kMtN;
+    const int64_t per = (nch + kQfRuns - 1) / kQfRuns;   // rounds per run
+    for (int i = threadIdx.x; i < kQfRuns * 3; i += 64 * kQfTeamWaves) (&rdy[0][0])[i] = 0;
+    if (threadIdx.x < kQfRuns) cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) sflags = 0;
+    int32_t gleft, gnext;
+    if (wv == 1) qfl_gen_init(a, j, SG, gleft, gnext, lane);     // every wave needs gleft/gnext below
+    else {
+        gleft = a.px_state ? (int32_t)a.px_state[j * kQfStateWords] : 1;
+        gnext = a.px_state ? (int32_t)a.px_state[j * kQfStateWords + 1] : 0;
+    }
+    if (wv == 0 && lane == 0) mt_seed(SL, (uint32_t)a.prng_seeds[j]);
+    __syncthreads();
+    const QflCtx c = qfl_ctx<XK>(a, j, gleft, gnext);
+    int32_t flags = 0;
+    if (wv == 0) {                                       // local scout: blocks 0 .. qL + start of the last run
+        __builtin_amdgcn_s_setprio(3);
+        int64_t last = 0;
+        for (int s = 0; s < kQfRuns; ++s)
+            if (s * per < nch) last = c.qL + s * per;
+        for (int64_t k = 0; k <= last; ++k) {
+            if (k) mt_twist_wave(SL, lane);
+            if (k < nch && k % per == 0) qfl_give(LA[k / per], SL, &rdy[k / per][0], lane);
+            const int64_t kb = k - c.qL;
+            if (kb >= 0 && kb < nch && kb % per == 0) qfl_give(LB[kb / per], SL, &rdy[kb / per][1], lane);
+        }
+    } else if (wv == 1) {                                // global scout
+        __builtin_amdgcn_s_setprio(3);
+        int64_t last = 0;
+        for (int s = 0; s < kQfRuns; ++s)
+            if (s * per < nch) last = c.qG + s * per;
+        for (int64_t k = 0; k <= last; ++k) {
+            if (k) mt_twist_wave(SG, lane);
+            const int64_t kg = k - c.qG;
+            if (kg >= 0 && kg < nch && kg % per == 0) qfl_give(GB[kg / per], SG, &rdy[kg / per][2], lane);
+        }
+    } else {                                             // run s: rounds [c0, c1)
+        const int s = wv - 2;
+        const int64_t c0 = s * per, c1 = min(nch, c0 + per);
+        if (c0 < c1) {
+            bool ok = qfl_wait_flag(&rdy[s][0]);
+            if (ok) qfl_pass_a(c, LA[s], c0, c1, lane);
+            ok = ok && qfl_wait_flag(&rdy[s][1]) && qfl_wait_flag(&rdy[s][2]);
+            if (ok) {
+                int64_t haveL = c.qL + c0, haveG = c.qG + c0;
+                const int64_t e = qfl_pass_b<XK>(c, a.ev, LB[s], haveL, GB[s], haveG, c0, c1, c0 * kMtN, flags, lane);
+                if (lane == 0) cnt[s] = e;
+                if (c1 == nch && a.px_state_out)
+                    qfl_state_out(a.px_state_out + j * kQfStateWords, GB[s], D, gleft, gnext, c.qG * kMtN + c.rG, lane);
+            } else {
+                flags |= UQ_QFL_TIMEOUT;
+            }
+        }
+        for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
+        if (lane == 0 && flags) atomicOr(&sflags, flags);
+    }
+    __syncthreads();
+    if (wv == 0) {                                       // exact values of run s: [c0*624, +cnt) -> index order
+        int64_t base = 0;
+        for (int s = 0; s < kQfRuns; ++s) {
+            const int64_t src = s * per * kMtN, n_s = cnt[s];
+            for (int64_t i0 = 0; i0 < n_s; i0 += 64) {   // (base <= src: a downward move, chunk by chunk)
+                const int64_t i = i0 + lane;
+                const float v = i < n_s ? a.ev[c.row + src + i] : 0.f;
+                if (i < n_s) a.ev[c.row + base + i] = v;
+            }
+            base += n_s;
+        }
+        if (lane == 0) {
+            a.ecount[j] = (int32_t)base;
+            a.scale[j] = c.sc;
+            a.info[j] = sflags;
+        }
     }
 }
 

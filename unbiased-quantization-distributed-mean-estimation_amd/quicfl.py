@@ -40,7 +40,7 @@ __all__ = ["QuicFLReceiver", "QuicFLSender", "QuicFLMessages", "QUICFL_quantize"
            "quicfl_decompress", "quicfl_decompress_messages", "prng_seed", "set_tables_prefix"]
 
 STATE_WORDS = 626                  # UQ_QFL_STATE_WORDS: (left, next, 624 words)
-_FLAG_P, _FLAG_INDEX, _FLAG_PX, _FLAG_X = 1, 2, 4, 8
+_FLAG_P, _FLAG_INDEX, _FLAG_PX, _FLAG_X, _FLAG_TIMEOUT = 1, 2, 4, 8, 16
 _tables_prefix = None
 _dropin_lock = threading.Lock()
 _dropin: dict = {}
@@ -254,6 +254,8 @@ def quicfl_compress(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSende
             raise RuntimeError("Expected p_in >= 0 && p_in <= 1 to be true, but got false.")   # AS:489 bernoulli
         if flags & _FLAG_X:
             raise OverflowError("X outside 0..255: use x_dtype=torch.int64")
+        if flags & _FLAG_TIMEOUT:
+            raise RuntimeError("uq_quicfl_compress_f32: internal wait ran out (results invalid)")
     msg = QuicFLMessages(X=X, exact_mask=mask, exact_vals=ev, exact_count=cnt.cpu(), scale=scale, prng_seeds=ps,
                          rotation_seeds=rs, dim=d, nbits=nbits, h_len=int(dd["h_len"]))
     if _state_out:
