@@ -41,6 +41,11 @@ extern "C" {
 int uq_version(void);
 /* SHA-256 (hex) of the sources and flags the library was built from (build_ext.build_id()). */
 const char* uq_build_id(void);
+/* Test hook, process-wide: on != 0 makes every later torch-tie replay (biased quantizer,
+ * UQ_TIES_TORCH) take its failure path, so the defined fallback (lowest-index order plus the
+ * internal-error status) can be tested.  Returns the previous setting.  Never set by the
+ * library; production callers leave it at 0. */
+int uq_test_force_replay_failure(int on);
 
 /* Thread-local description of the last error returned on this thread. */
 const char* uq_last_error(void);
@@ -183,9 +188,9 @@ int uq_tc_decode(const uint8_t* msgs, size_t msgs_bytes, const uint64_t* offsets
  * bit2 = |Delta| > d (the reference's topk raises), bit3 = torch tie choice replayed,
  * bit4 = threshold digits 2-3 found on the compacted first-digit bucket (informational).
  * Workspace: uq_biased_workspace_bytes; zero-filled once before first use (it holds the
- * status word of uq_check_status, which reports an inconsistent tie replay).  Its bytes
- * 12..15 are reserved and must stay zero (the library never writes them; a nonzero value
- * forces every tie replay onto its index-order fallback, which the tests use to exercise it). */
+ * status word of uq_check_status, which reports an inconsistent tie replay).  The tests
+ * exercise the replay's index-order fallback through uq_test_force_replay_failure, not
+ * through the workspace: no workspace content changes which path a replay takes. */
 #define UQ_TIES_TORCH 0
 #define UQ_TIES_LOWEST_INDEX 1
 int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t torch_threads, size_t* bytes_out);

@@ -304,25 +304,23 @@ def test_fuzz_small_vectors_vs_oracle(uq):
 @pytest.mark.parametrize("n,d", [(3, 1 << 16), (40, 1 << 20)])
 def test_failed_replay_falls_back_to_index_order(uq, n, d):
     """a torch-tie replay that fails its consistency checks (forced here through
-    the workspace's test word, control word 3) reports the internal error through
+    the library's test hook uq_test_force_replay_failure) reports the internal error through
     check_status and leaves a DEFINED output: the client's threshold ties ranked in index
     order, i.e. exactly the UQ_TIES_LOWEST_INDEX result (the replay kernel counts the tile
     ties that rez_tiecount_kernel skipped for listed clients).  Both replay forms: one kernel
     (few clients) and KB7a's levels (n >= 32)."""
-    from uqdme_amd.biased import _biased_ws_bytes
-    from uqdme_amd.quantizer import _workspace
+    from uqdme_amd._lib import load
     rng = np.random.default_rng(n)
     x = torch.as_tensor(rng.integers(-3, 4, (n, d)).astype(f32)).cuda()
     m = rate_to_m(1, d)
-    ws = _workspace(torch.device("cuda", 0), _biased_ws_bytes(n, d, 1))
-    ws[12:16] = torch.tensor([1, 0, 0, 0], dtype=torch.uint8, device="cuda")
+    assert load().uq_test_force_replay_failure(1) == 0
     try:
         out_t, info = uq.biased_quantize(x, m=m, torch_threads=1, ties="torch", return_info=True)
         torch.cuda.synchronize()
         with pytest.raises(uq.UQError):
             uq.check_status()
     finally:
-        ws[12:16] = 0
+        assert load().uq_test_force_replay_failure(0) == 1
     assert int((info[:, 1] & 1).sum()) >= n // 2 and int((info[:, 1] & 8).sum()) == 0   # ambiguous, none replayed
     out_l = uq.biased_quantize(x, m=m, torch_threads=1, ties="lowest")
     assert torch.equal(out_t.view(torch.int32), out_l.view(torch.int32))

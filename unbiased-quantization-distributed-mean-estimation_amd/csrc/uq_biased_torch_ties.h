@@ -806,11 +806,12 @@ __global__ void __launch_bounds__(NT)
 rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
                 RezState* __restrict__ st, uint32_t* __restrict__ tie_bits, uint32_t* __restrict__ qbuf,
                 uint32_t* __restrict__ pos, const uint32_t* __restrict__ list, uint32_t* __restrict__ ctrl,
-                const TieLevelState* __restrict__ tls, int part, uint32_t* __restrict__ tilecnt, int32_t tiles) {
+                const TieLevelState* __restrict__ tls, int part, uint32_t* __restrict__ tilecnt, int32_t tiles,
+                int force_fail) {
     TT_DECL();
-    // ctrl[3] != 0 (tests only: the workspace's control block) forces every replay down the
-    // failure path below, so its fallback can be checked against the lowest-index rule
-    const bool force_fail = ctrl[3] != 0u;
+    // force_fail != 0 (test hook uq_test_force_replay_failure, never set by the library itself)
+    // sends every replay down the failure path below, so its fallback can be checked against
+    // the lowest-index rule
     const int64_t dpad = (d + 3) & ~(int64_t)3;              // 16-byte aligned K and I rows
     const Queue A{qbuf + (size_t)blockIdx.x * 2 * dpad, qbuf + (size_t)blockIdx.x * 2 * dpad + dpad};
     uint32_t* Lpos = pos + (size_t)blockIdx.x * 2 * d;

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -2140,6 +2141,8 @@ codes_mean_kernel(const int8_t* __restrict__ codes, int64_t ldc, const float* __
 
 // ---- host-side helpers ---------------------------------------------------------------
 thread_local std::string g_err;
+// test hook (uq_test_force_replay_failure): every torch-tie replay takes its failure path
+std::atomic<int> g_force_replay_failure{0};
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -2597,7 +2600,7 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     if (d <= kTieLevelMin || (n < kTieLevelMinClients && d < kTieLevelBigD)) {
         hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
                            state, bits, qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)nullptr, 0,
-                           (uint32_t*)(wsb + w.tcnt_off), w.tiles);
+                           (uint32_t*)(wsb + w.tcnt_off), w.tiles, g_force_replay_failure.load());
         return hip_check(hipGetLastError(), "rez_ties_kernel launch");
     }
     // KB7a: introselect's levels over (segments x slots) workgroups, level by level, down to
@@ -2642,7 +2645,7 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     if ((rc = hip_check(hipGetLastError(), "kt_mark_kernel launch"))) return rc;
     hipLaunchKernelGGL(rez_ties_kernel<kTieThreadsLds>, dim3(S), dim3(kTieThreadsLds), 0, st, x, d, l1, fm, state, bits,
                        qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)tls, 1, (uint32_t*)(wsb + w.tcnt_off),
-                       w.tiles);
+                       w.tiles, g_force_replay_failure.load());
     *tls_out = tls;
     return hip_check(hipGetLastError(), "rez_ties_kernel launch");
 }
@@ -2652,7 +2655,7 @@ int launch_torch_ties_rest(const float* x, int64_t d, const float* l1, float fm,
     hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
                        state, bits, (uint32_t*)(wsb + w.pairs_off), (uint32_t*)(wsb + w.pos_off),
                        (const uint32_t*)(wsb + w.list_off), (uint32_t*)wsb, tls, 2, (uint32_t*)(wsb + w.tcnt_off),
-                       w.tiles);
+                       w.tiles, g_force_replay_failure.load());
     return hip_check(hipGetLastError(), "rez_ties_kernel launch");
 }
 
@@ -2666,6 +2669,8 @@ int uq_version(void) { return 102; }
 #define UQ_BUILD_ID "unknown"
 #endif
 const char* uq_build_id(void) { return UQ_BUILD_ID; }
+
+int uq_test_force_replay_failure(int on) { return g_force_replay_failure.exchange(on ? 1 : 0); }
 
 const char* uq_last_error(void) { return g_err.c_str(); }
 
