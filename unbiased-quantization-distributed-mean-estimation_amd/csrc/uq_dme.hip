@@ -3563,7 +3563,7 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.n = n;
     // few messages: a workgroup per message (scouts + runs: the streams' length is the critical
     // path, not the per-coordinate work); batches: a wave per message
-    if (n <= kQfTeamMaxN && w.D >= (int64_t)kMtN * kQfRuns) {
+    if (n <= kQfTeamMaxN && w.D >= (int64_t)kMtN * kQfRuns && w.D <= kQfTeamMaxD) {
         if (x_kind == 0)
             hipLaunchKernelGGL(quicfl_send_team_kernel<0>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
         else

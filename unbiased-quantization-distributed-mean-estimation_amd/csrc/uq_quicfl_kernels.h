@@ -429,6 +429,10 @@ quicfl_send_wave_kernel(QflSendArgs a) {
 constexpr int kQfTeamWaves = 8;                    // 2 scouts + 6 runs (<= 256 VGPRs per lane)
 constexpr int kQfRuns = kQfTeamWaves - 2;
 constexpr int64_t kQfTeamMaxN = 64;                 // messages per call up to which the team kernel runs
+// padded dims up to which it runs: the last run waits for the scouts' 2D/624 twists (about
+// 30 ms at 2^23), far inside qfl_wait_flag's bound of 2^24 sleeps; longer vectors take the
+// one-wave-per-message kernel, which never waits
+constexpr int64_t kQfTeamMaxD = (int64_t)1 << 23;
 __device__ __forceinline__ bool qfl_wait_flag(int* f) {
     for (int it = 0; it < (1 << 24); ++it) {
         if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) return true;
