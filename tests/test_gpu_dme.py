@@ -97,7 +97,8 @@ def test_multi_scheme_nmse_known_answers(gpu_ready, fixture):
     n in {1, 6}, two instances each).  Unbiased and biased within 1e-6 relative (north_star).
     EDEN within 1e-6 at d = 2048 and 1e-5 at d = 2^22: its scale (AS:335) is an MKL sdot,
     2^22 f32 products accumulated in MKL's CPU-dependent order, whose own rounding is ~1e-6
-    relative at that size (the GPU accumulates in fp64; observed 1.3e-6 on normal n=1)."""
+    relative at that size (the GPU accumulates in fp64; observed 1.3e-6 on normal n=1).  With
+    the reference's own scales substituted, EDEN's NMSE is checked bit for bit."""
     import json
     import os
     import uqdme
@@ -129,8 +130,9 @@ def test_multi_scheme_nmse_known_answers(gpu_ready, fixture):
             rel = np.abs(mine[key].astype(np.float64) - sc_ref) / np.abs(sc_ref)
             worst = max(worst, float(rel.max()))
         assert worst <= 2e-6, (dist, worst)
-        sub = uqdme.nmse_simulation(dist, dim=ref["dim"], users=(1, 6), num_instances=2, schemes=("eden",),
-                                    torch_threads=1, eden_scales=theirs)
+        # (all three schemes again: their draws interleave on the global generator, ND:133-147)
+        sub = uqdme.nmse_simulation(dist, dim=ref["dim"], users=(1, 6), num_instances=2,
+                                    schemes=("eden", "unbiased", "biased"), torch_threads=1, eden_scales=theirs)
         for row in rows:
             ui = (1, 6).index(row["n"])
             for r in (1, 2):
