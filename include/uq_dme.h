@@ -193,6 +193,11 @@ int uq_tc_decode(const uint8_t* msgs, size_t msgs_bytes, const uint64_t* offsets
  * through the workspace: no workspace content changes which path a replay takes. */
 #define UQ_TIES_TORCH 0
 #define UQ_TIES_LOWEST_INDEX 1
+/* OR'd into UQ_TIES_TORCH: the call may wait once on an internal stream (never on `stream`)
+ * for the number of clients whose tie choice needs the replay, and skips the replay's kernels
+ * when it is zero -- for synchronous few-client callers (the per-vector drop-in); results are
+ * the same bits either way. */
+#define UQ_TIES_HOST_CHECK 4
 int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t torch_threads, size_t* bytes_out);
 int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m,
                        int32_t torch_threads, int32_t tie_policy, float* l1_out, int32_t* info,
@@ -233,6 +238,22 @@ int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inver
 int uq_quicfl_prepare_f32(const int32_t* X, int64_t n, int64_t D, const float* recv_table, int32_t table_rows,
                           int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask, const float* exact_vals,
                           const float* scale, float* out, void* stream);
+/* uq_quicfl_receive_f32: the same for messages as they come (uq_quicfl_compress_f32's or the
+ * reference's dict): X [n][D] int64 (x_kind 0), uint8 (1) or int32 (2), read in place; the
+ * index X * h_len + h is taken like torch.take (AS:530): -numel <= index < numel, negatives
+ * wrap, any other index sets UQ_QFL_BAD_INDEX in info[j] (that coordinate's output is 0; the
+ * reference raises IndexError).  exact_mask u8/bool [n][D] or NULL; exact_vals f32 [n][D]
+ * dense (exact_layout 0: the value at its coordinate) or compact (exact_layout 1: row j's
+ * exact values in index order in its first entries, as uq_quicfl_compress_f32 writes them;
+ * exact_vals rows are still D entries long).  exact_count [n] or NULL (compact only): a row
+ * whose mask does not hold exactly exact_count[j] coordinates gets UQ_QFL_BAD_EXACT (the
+ * reference's `vec[exact_indeces] = exact_values` raises).  info [n] int32 or NULL.
+ * D <= 2^28.  uq_quicfl_prepare_f32 = x_kind 2, dense, no info. */
+#define UQ_QFL_BAD_EXACT 32
+int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, const float* recv_table,
+                          int32_t table_rows, int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask,
+                          const float* exact_vals, int32_t exact_layout, const int32_t* exact_count, const float* scale,
+                          float* out, int32_t* info, void* stream);
 
 /* ---- QUIC-FL sender (baseline) --------------------------------------
  * QuicFLSender.compress (NMSE_Results/Codes/All_Schemes.py:455-503) for a batch of n messages,

@@ -366,3 +366,24 @@ def test_few_clients_2pow22_take_level_replay(uq):
         exp, *_ = C.biased_quantize(x[j], m, 1, 0)
         assert G.bits_equal(out[j], exp), (j, G.n_mismatch(out[j], exp))
     uq.check_status()
+
+
+@pytest.mark.parametrize("d", [(1 << 21) + 3, 1 << 22])
+def test_host_check_skips_replay_with_same_bits(uq, d):
+    """UQ_TIES_HOST_CHECK (the per-vector drop-in's policy): when no row needs the torch-tie
+    replay its kernels are skipped; when some do, they run.  Same bits as the plain call either
+    way, for tie-free and tie-heavy rows, one row and a few."""
+    rng = np.random.default_rng(d % 1013)
+    smooth = rng.standard_normal((3, d)).astype(f32)
+    ties = rng.integers(-3, 4, (3, d)).astype(f32)
+    m = rate_to_m(1, d)
+    for x in (smooth, ties, np.stack([smooth[0], ties[1]])):
+        xt = torch.as_tensor(x).cuda()
+        for rows in (xt[:1], xt):
+            a, ia = uq.biased_quantize(rows, m=m, torch_threads=1, ties="torch", return_info=True)
+            b, ib = uq.biased_quantize(rows, m=m, torch_threads=1, ties="torch", return_info=True, host_check=True)
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32)) and torch.equal(ia, ib)
+    out = uq.Type_biased_quantize(torch.as_tensor(ties[2]).cuda(), 1)
+    ref = uq.biased_quantize(torch.as_tensor(ties[2:3]).cuda(), m=rate_to_m(1, d), ties="torch")
+    assert torch.equal(out.view(torch.int32), ref.view(d).view(torch.int32))
+    uq.check_status()

@@ -1,6 +1,6 @@
 """GPU: the QUIC-FL receiver (AS:507-535) against the reference's QuicFLReceiver.decompress
 outputs (tests/golden/make_golden_quicfl.py) and the oracle, bit for bit, through the C ABI
-(uq_quicfl_prepare_f32 + uq_rht_f32)."""
+(uq_quicfl_receive_f32 + uq_rht_f32)."""
 import json
 import os
 
@@ -57,3 +57,53 @@ def test_batched_receiver_matches_oracle(fx):
         assert out[j].view(np.uint32).tolist() == exp.view(np.uint32).tolist(), j
     with pytest.raises(IndexError):
         uqdme.quicfl_decompress(torch.full((1, D), 1 << nbits), nbits, [1], [1], [1.0], dim, tab)
+
+
+def test_receiver_x_kinds_layouts_and_errors(fx):
+    """uq_quicfl_receive_f32: X read in place as int64 / uint8 / int32; exact values dense or
+    compact (index order, quicfl_compress's layout); the take index -numel <= i < numel with
+    negatives wrapping (AS:530) -- all bit-equal to the oracle; a compact row whose count
+    disagrees with its mask raises like AS:531, an index past the table raises IndexError."""
+    import uqdme
+    meta, z = fx
+    rng = np.random.default_rng(11)
+    nbits, n, dim, D = 3, 5, 5000, 8192
+    tab = z[f"recv{nbits}"]
+    rows = tab.shape[0]
+    X = rng.integers(0, rows, size=(n, D))
+    X[1, :50] = -1                                   # -h_len + h: wraps to the last row (take semantics)
+    X[2, 7] = -rows                                  # the lowest index take accepts
+    mask = rng.random((n, D)) < 0.004
+    mask[3] = False                                  # a row without exact coordinates
+    dense = np.where(mask, rng.standard_normal((n, D)) * 5, 0).astype(np.float32)
+    compact = np.zeros((n, D), np.float32)
+    cnt = mask.sum(1)
+    for j in range(n):
+        compact[j, :cnt[j]] = dense[j][mask[j]]
+    ps = rng.integers(0, 1 << 16, size=n)
+    rs = rng.integers(0, 100, size=n)
+    sc = (rng.random(n) * 3 + 0.5).astype(np.float32)
+    exp = [E.quicfl_decompress(X[j], tab, tab.shape[1], int(ps[j]), mask[j], dense[j][mask[j]], sc[j], int(rs[j]), dim)
+           for j in range(n)]
+    md = torch.from_numpy(mask).cuda()
+    for dt in (torch.int64, torch.int32):
+        Xd = torch.from_numpy(X).to(dt).cuda()
+        for vals, c in ((dense, None), (compact, cnt)):
+            out = uqdme.quicfl_decompress(Xd, nbits, ps, rs, sc, dim, tab, tab.shape[1], md, torch.from_numpy(vals).cuda(),
+                                          c).cpu().numpy()
+            for j in range(n):
+                assert out[j].view(np.uint32).tolist() == exp[j].view(np.uint32).tolist(), (dt, c is None, j)
+    Xu = np.where(X < 0, 0, X)                        # uint8 rows: the non-negative part
+    exp_u = E.quicfl_decompress(Xu[0], tab, tab.shape[1], int(ps[0]), mask[0], dense[0][mask[0]], sc[0], int(rs[0]), dim)
+    out = uqdme.quicfl_decompress(torch.from_numpy(Xu[:1]).to(torch.uint8).cuda(), nbits, ps[:1], rs[:1], sc[:1], dim, tab,
+                                  None, md[:1], torch.from_numpy(compact[:1]).cuda(), cnt[:1]).cpu().numpy()
+    assert out[0].view(np.uint32).tolist() == exp_u.view(np.uint32).tolist()
+    bad = cnt.copy()
+    bad[4] += 1
+    with pytest.raises(RuntimeError):
+        uqdme.quicfl_decompress(torch.from_numpy(X).cuda(), nbits, ps, rs, sc, dim, tab, None, md,
+                                torch.from_numpy(compact).cuda(), bad)
+    Xb = X.copy()
+    Xb[0, 3] = -rows - 1                             # below -numel for every h
+    with pytest.raises(IndexError):
+        uqdme.quicfl_decompress(torch.from_numpy(Xb).cuda(), nbits, ps, rs, sc, dim, tab)

@@ -44,6 +44,7 @@ SIGNATURES = {
     "uq_rht_signs": (ctypes.c_int, [_p, _i64, _i64, _p, _p]),
     "uq_rht_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _sz, _p]),
     "uq_quicfl_prepare_f32": (ctypes.c_int, [_p, _i64, _i64, _p, _i32, _i32, _p, _p, _p, _p, _p, _p]),
+    "uq_quicfl_receive_f32": (ctypes.c_int, [_p, _i32, _i64, _i64, _p, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p, _p, _p]),
     "uq_quicfl_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
     "uq_quicfl_compress_f32": (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _i64, _i32, _f32, _p, _p, _p, _p, _p, _i32,
                                               _p, _p, _p, _p, _p, _p, _sz, _p]),

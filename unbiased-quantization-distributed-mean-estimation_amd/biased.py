@@ -32,6 +32,7 @@ __all__ = ["Type_biased_quantize", "biased_quantize", "TIES_TORCH", "TIES_LOWEST
 
 TIES_TORCH = 0            # UQ_TIES_TORCH
 TIES_LOWEST_INDEX = 1     # UQ_TIES_LOWEST_INDEX
+_HOST_CHECK = 4           # UQ_TIES_HOST_CHECK
 FLAG_AMBIGUOUS = 1
 FLAG_NONFINITE = 2
 FLAG_RANGE = 4
@@ -48,11 +49,15 @@ def _biased_ws_bytes(n: int, d: int, T: int) -> int:
 
 
 def biased_quantize(x, bits_per_dimension=1, *, m: int | None = None, torch_threads: int | None = None,
-                    ties="torch", out=None, return_l1: bool = False, return_info: bool = False):
+                    ties="torch", out=None, return_l1: bool = False, return_info: bool = False,
+                    host_check: bool = False):
     """Batched Type_biased_quantize over the rows of x [n, d].
 
     return_info adds an int32 [n, 2] tensor {Delta, flags} per row (flags: 1 a tie
-    straddled the threshold, 2 m' not finite, 4 |Delta| > d, 8 torch tie choice replayed)."""
+    straddled the threshold, 2 m' not finite, 4 |Delta| > d, 8 torch tie choice replayed).
+    host_check (torch ties): the call may wait once for the number of rows whose tie choice
+    needs the replay and skips the replay's kernels when there are none (UQ_TIES_HOST_CHECK:
+    for synchronous few-row callers; the same bits either way)."""
     dev = _device()
     x = _as_device_f32_2d(x, dev)
     n, d = x.shape
@@ -67,7 +72,8 @@ def biased_quantize(x, bits_per_dimension=1, *, m: int | None = None, torch_thre
     l1_out = torch.empty(n, dtype=torch.float32, device=dev) if return_l1 else None
     info = torch.empty((n, 2), dtype=torch.int32, device=dev) if return_info else None
     ws = _workspace(dev, _biased_ws_bytes(n, d, T))
-    _lib.check(_lib.load().uq_type_biased_f32(_ptr(x), _ptr(out), n, d, mm, T, _TIES[ties], _ptr(l1_out),
+    policy = _TIES[ties] | (_HOST_CHECK if host_check and _TIES[ties] == TIES_TORCH else 0)
+    _lib.check(_lib.load().uq_type_biased_f32(_ptr(x), _ptr(out), n, d, mm, T, policy, _ptr(l1_out),
                                               _ptr(info), _ptr(ws), ws.numel(), _stream_ptr(dev)),
                "uq_type_biased_f32")
     res = [out]
@@ -99,7 +105,7 @@ def Type_biased_quantize(input_vector, bits_per_dimension=1):
         return v.clone()
     if not v.is_contiguous():
         v = v.contiguous()
-    out, info = biased_quantize(v.view(1, d), m=m, ties="torch", return_info=True)
+    out, info = biased_quantize(v.view(1, d), m=m, ties="torch", return_info=True, host_check=True)
     flags = int(info[0, 1].item())
     check_status()
     if flags & FLAG_NONFINITE:

@@ -2490,6 +2490,7 @@ int eden_check(int64_t n, int64_t dim, int32_t nbits, const int8_t* signs, EdenT
 struct SideStream {
     hipStream_t s;
     hipEvent_t fork, join;
+    uint32_t* count;            // pinned host word (UQ_TIES_HOST_CHECK reads the tie list's length)
 };
 
 int side_stream(SideStream** out) {
@@ -2510,6 +2511,8 @@ int side_stream(SideStream** out) {
         rc = hip_check(hipEventCreateWithFlags(&cache[dev].fork, hipEventDisableTiming), "create event");
         if (rc) return rc;
         rc = hip_check(hipEventCreateWithFlags(&cache[dev].join, hipEventDisableTiming), "create event");
+        if (rc) return rc;
+        rc = hip_check(hipHostMalloc((void**)&cache[dev].count, sizeof(uint32_t), hipHostMallocDefault), "pinned word");
         if (rc) return rc;
         made[dev] = true;
     }
@@ -3138,6 +3141,8 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     if (d >= ((int64_t)1 << 31)) return fail(UQ_E_INVALID, "d must be < 2^31");
     if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 clients per call");
     if (T < 1) return fail(UQ_E_INVALID, "torch_threads must be >= 1");
+    const bool host_check = (tie_policy & UQ_TIES_HOST_CHECK) != 0;
+    tie_policy &= ~UQ_TIES_HOST_CHECK;
     if (tie_policy != UQ_TIES_LOWEST_INDEX && tie_policy != UQ_TIES_TORCH)
         return fail(UQ_E_INVALID, "unknown tie_policy");
     L1Plan plan;
@@ -3247,7 +3252,18 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         rc = tiecount(sb->s, (const uint32_t*)(wsb + w.list_off));
         if (rc) return rc;
         const TieLevelState* tls = nullptr;
-        rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls);
+        // UQ_TIES_HOST_CHECK: wait for the side stream (KB6 keeps the GPU busy meanwhile) and
+        // skip the replay chain -- KB7a's ~65 level launches -- when no client is listed
+        bool replay = true;
+        if (host_check) {
+            rc = hip_check(hipMemcpyAsync(sb->count, wsb + w.list_off, sizeof(uint32_t), hipMemcpyDeviceToHost, sb->s),
+                           "copy tie list length");
+            if (rc) return rc;
+            rc = hip_check(hipStreamSynchronize(sb->s), "sync side stream");
+            if (rc) return rc;
+            replay = *sb->count != 0u;
+        }
+        if (replay) rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls);
         if (rc) return rc;
         rc = hip_check(hipEventRecord(sb->join, sb->s), "record join");
         if (rc) return rc;
@@ -3285,20 +3301,40 @@ int uq_rht_signs(const int32_t* seeds, int64_t rows, int64_t D, int8_t* signs, v
     return hip_check(hipGetLastError(), "rht_signs_kernel launch");
 }
 
-int uq_quicfl_prepare_f32(const int32_t* X, int64_t n, int64_t D, const float* recv_table, int32_t table_rows,
-                          int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask, const float* exact_vals,
-                          const float* scale, float* out, void* stream) {
+int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, const float* recv_table,
+                          int32_t table_rows, int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask,
+                          const float* exact_vals, int32_t exact_layout, const int32_t* exact_count, const float* scale,
+                          float* out, int32_t* info, void* stream) {
     if (n < 0 || D < 0) return fail(UQ_E_INVALID, "n and D must be >= 0");
     if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 clients per call");
+    if (D > ((int64_t)1 << 28)) return fail(UQ_E_INVALID, "at most 2^28 coordinates per message");
+    if (x_kind < 0 || x_kind > 2) return fail(UQ_E_INVALID, "x_kind must be 0 (int64), 1 (uint8) or 2 (int32)");
+    if (exact_layout != 0 && exact_layout != 1) return fail(UQ_E_INVALID, "exact_layout must be 0 (dense) or 1 (compact)");
     if (n == 0 || D == 0) return UQ_OK;
     if (!X || !recv_table || !prng_seeds || !scale || !out) return fail(UQ_E_INVALID, "null pointer");
     if ((exact_mask == nullptr) != (exact_vals == nullptr)) return fail(UQ_E_INVALID, "exact_mask and exact_vals go together");
     if (h_len < 1 || table_rows < 1 || (int64_t)h_len * table_rows > kQflTab)
         return fail(UQ_E_INVALID, "receiver table must hold 1..1024 entries");
-    hipLaunchKernelGGL(quicfl_recv_wave_kernel, dim3((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)),
-                       dim3(64 * kQfWavesPerWG), 0, (hipStream_t)stream, X, n, D, recv_table, table_rows * h_len, h_len,
-                       prng_seeds, exact_mask, exact_vals, scale, out);
+    const dim3 grid((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)), block(64 * kQfWavesPerWG);
+    hipStream_t st = (hipStream_t)stream;
+    const int tn = table_rows * h_len;
+    if (x_kind == 0)
+        hipLaunchKernelGGL(quicfl_recv_wave_kernel<0>, grid, block, 0, st, X, n, D, recv_table, tn, h_len, prng_seeds,
+                           exact_mask, exact_vals, exact_layout, exact_count, scale, out, info);
+    else if (x_kind == 1)
+        hipLaunchKernelGGL(quicfl_recv_wave_kernel<1>, grid, block, 0, st, X, n, D, recv_table, tn, h_len, prng_seeds,
+                           exact_mask, exact_vals, exact_layout, exact_count, scale, out, info);
+    else
+        hipLaunchKernelGGL(quicfl_recv_wave_kernel<2>, grid, block, 0, st, X, n, D, recv_table, tn, h_len, prng_seeds,
+                           exact_mask, exact_vals, exact_layout, exact_count, scale, out, info);
     return hip_check(hipGetLastError(), "quicfl_recv_wave_kernel launch");
+}
+
+int uq_quicfl_prepare_f32(const int32_t* X, int64_t n, int64_t D, const float* recv_table, int32_t table_rows,
+                          int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask, const float* exact_vals,
+                          const float* scale, float* out, void* stream) {
+    return uq_quicfl_receive_f32(X, 2, n, D, recv_table, table_rows, h_len, prng_seeds, exact_mask, exact_vals, 0, nullptr,
+                                 scale, out, nullptr, stream);
 }
 
 int uq_rht_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t inverse, const int8_t* signs,

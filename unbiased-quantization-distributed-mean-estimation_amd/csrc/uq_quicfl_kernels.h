@@ -535,14 +535,23 @@ quicfl_send_team_kernel(QflSendArgs a) {
 
 // ---- receiver: QuicFLReceiver.decompress before its inverse RHT (AS:526-532) -----------------
 // h = torch.randint(0, h_len, (D,)) of a generator seeded with prng_seed (word % h_len), then
-// v = recv_table[X * h_len + h], exact coordinates overwritten, v / scale (f32).  One wave per
-// message; the table (<= 1024 floats) sits in LDS, shared by the workgroup's waves.
+// v = recv_table.take(X * h_len + h) (AS:530: -numel <= index < numel, negatives wrap, anything
+// else raises -> UQ_QFL_BAD_INDEX), exact coordinates overwritten (AS:531), v / scale (f32).
+// One wave per message; the table (<= 1024 floats) sits in LDS, shared by the workgroup's waves.
+// XK: X as int64 (0, the reference's X.long()), uint8 (1, the batch sender's) or int32 (2).
+// Exact values dense (at their coordinate) or compact (the message's exact values in index
+// order, as the sender writes them): a compact value's slot is the number of exact coordinates
+// before it, from wave ballots over the round's mask and a running count.  Loads run ahead:
+// X one round, the mask two rounds (its ballots give the next round's value slots, whose loads
+// are then one round ahead too).
 constexpr int kQflTab = 1024;
+template <int XK>
 __global__ void __launch_bounds__(64 * kQfWavesPerWG)
-quicfl_recv_wave_kernel(const int32_t* __restrict__ X, int64_t n, int64_t D, const float* __restrict__ table,
+quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const float* __restrict__ table,
                         int32_t tab_n, int32_t h_len, const int32_t* __restrict__ prng_seeds,
-                        const uint8_t* __restrict__ exact_mask, const float* __restrict__ exact_vals,
-                        const float* __restrict__ scale, float* __restrict__ out) {
+                        const uint8_t* __restrict__ exact_mask, const float* __restrict__ exact_vals, int compact,
+                        const int32_t* __restrict__ exact_count, const float* __restrict__ scale,
+                        float* __restrict__ out, int32_t* __restrict__ info) {
     __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];
     __shared__ float tab[kQflTab];
     for (int i = threadIdx.x; i < tab_n; i += 64 * kQfWavesPerWG) tab[i] = table[i];
@@ -559,46 +568,84 @@ quicfl_recv_wave_kernel(const int32_t* __restrict__ X, int64_t n, int64_t D, con
     const uint32_t hl = (uint32_t)h_len;
     const bool hpow2 = (hl & (hl - 1)) == 0;
     const int64_t nch = (D + kMtN - 1) / kMtN;
+    constexpr uint32_t xb = XK == 0 ? 8u : (XK == 1 ? 1u : 4u);  // bytes per X
     // buffer descriptors: branch-free loads (0 beyond D) and stores (dropped beyond D)
-    const __amdgpu_buffer_rsrc_t rXs = make_rsrc(X + row, Du * 4u);
-    const __amdgpu_buffer_rsrc_t rmk = make_rsrc(exact_mask ? (const void*)(exact_mask + row) : (const void*)X,
+    const __amdgpu_buffer_rsrc_t rXs = make_rsrc((const char*)X + row * xb, Du * xb);
+    const __amdgpu_buffer_rsrc_t rmk = make_rsrc(exact_mask ? (const void*)(exact_mask + row) : X,
                                                  exact_mask ? Du : 0u);
-    const __amdgpu_buffer_rsrc_t rvl = make_rsrc(exact_vals ? (const void*)(exact_vals + row) : (const void*)X,
+    const __amdgpu_buffer_rsrc_t rvl = make_rsrc(exact_vals ? (const void*)(exact_vals + row) : X,
                                                  exact_vals ? Du * 4u : 0u);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(out + row, Du * 4u);
-    int32_t xr[kMtGroups];
-    uint32_t mr[kMtGroups];
-    float vr[kMtGroups];
-    auto load_round = [&](uint32_t i0, int32_t* xo, uint32_t* mo, float* vo) {
+    const uint64_t below = (1ull << lane) - 1ull;
+    int64_t xr[kMtGroups], xn[kMtGroups];
+    uint32_t mr[kMtGroups], mn[kMtGroups];
+    float vr[kMtGroups], vn[kMtGroups];
+    uint32_t ebase = 0;                                          // exact coordinates before the round being slotted
+    auto load_x = [&](uint32_t i0, int64_t* xo) {
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const uint32_t i = i0 + 64u * k + lane;
-            xo[k] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rXs, i * 4u, 0, kAuxNT);
-            mo[k] = __builtin_amdgcn_raw_buffer_load_b8(rmk, i, 0, 0);
-            vo[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rvl, i * 4u, 0, 0));
+            if (XK == 0) {
+                const auto w = __builtin_amdgcn_raw_buffer_load_b64(rXs, i * 8u, 0, kAuxNT);
+                xo[k] = (int64_t)(((uint64_t)w[1] << 32) | w[0]);
+            } else if (XK == 1) {
+                xo[k] = __builtin_amdgcn_raw_buffer_load_b8(rXs, i, 0, kAuxNT);
+            } else {
+                xo[k] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rXs, i * 4u, 0, kAuxNT);
+            }
         }
     };
-    load_round(0, xr, mr, vr);
+    auto load_m = [&](uint32_t i0, uint32_t* mo) {
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) mo[k] = __builtin_amdgcn_raw_buffer_load_b8(rmk, i0 + 64u * k + lane, 0, 0);
+    };
+    auto load_v = [&](uint32_t i0, const uint32_t* mo, float* vo) {   // the round's exact values (0 elsewhere)
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            const int e = 64 * k + lane;
+            const bool m = mo[k] != 0u && e < kMtN;
+            uint32_t slot = i0 + (uint32_t)e;
+            if (compact) {
+                const uint64_t bal = __ballot(m);
+                slot = ebase + (uint32_t)__popcll(bal & below);
+                ebase += (uint32_t)__popcll(bal);
+            }
+            vo[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rvl, qf_off(m, slot * 4u), 0, 0));
+        }
+    };
+    int32_t flags = 0;
+    load_x(0, xr);
+    load_m(0, mr);
+    load_m(kMtN, mn);
+    load_v(0, mr, vr);
     for (int64_t c = 0; c < nch; ++c) {
         const uint32_t i0 = (uint32_t)(c * kMtN);
-        int32_t xn[kMtGroups];
-        uint32_t mn[kMtGroups];
-        float vn[kMtGroups];
-        load_round(i0 + kMtN, xn, mn, vn);
+        uint32_t m2[kMtGroups];
+        load_x(i0 + kMtN, xn);
+        load_m(i0 + 2u * kMtN, m2);
+        load_v(i0 + kMtN, mn, vn);
         mt_twist_wave(Ls, lane);
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
+            const bool act = e < kMtN && (int64_t)i0 + e < D;
             const uint32_t w = mt_temper(Ls[e < kMtN ? e : 0]);
             const uint32_t h = hpow2 ? (w & (hl - 1u)) : (w % hl);                     // AS:528 randint
-            int32_t idx = xr[k] * h_len + (int32_t)h;                                   // AS:530 take
-            idx = idx < 0 ? 0 : (idx >= tab_n ? tab_n - 1 : idx);                       // validated by the host
-            const float v = mr[k] ? vr[k] : tab[idx];                                   // AS:531
+            const int64_t it = (int64_t)((uint64_t)xr[k] * (uint64_t)hl + h);          // AS:530 (int64 arithmetic)
+            const bool inr = it >= -(int64_t)tab_n && it < (int64_t)tab_n;
+            flags |= (act && !inr) ? UQ_QFL_BAD_INDEX : 0;
+            const int32_t idx = inr ? (int32_t)(it < 0 ? it + tab_n : it) : 0;        // take wraps negatives
+            const float v = mr[k] ? vr[k] : (inr ? tab[idx] : 0.f);                   // AS:531
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(div1(v, dp)), ro,     // AS:532
                                                   qf_off(e < kMtN, (i0 + (uint32_t)e) * 4u), 0, kAuxNT);
             xr[k] = xn[k];
             mr[k] = mn[k];
+            mn[k] = m2[k];
             vr[k] = vn[k];
         }
     }
+    for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
+    // AS:531 vec[exact_indeces] = exact_values raises unless the counts agree
+    if (compact && exact_count && (int64_t)ebase != (int64_t)exact_count[j]) flags |= UQ_QFL_BAD_EXACT;
+    if (info && lane == 0) info[j] = flags;
 }

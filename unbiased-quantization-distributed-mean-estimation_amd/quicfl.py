@@ -40,7 +40,7 @@ __all__ = ["QuicFLReceiver", "QuicFLSender", "QuicFLMessages", "QUICFL_quantize"
            "quicfl_decompress", "quicfl_decompress_messages", "prng_seed", "set_tables_prefix"]
 
 STATE_WORDS = 626                  # UQ_QFL_STATE_WORDS: (left, next, 624 words)
-_FLAG_P, _FLAG_INDEX, _FLAG_PX, _FLAG_X, _FLAG_TIMEOUT = 1, 2, 4, 8, 16
+_FLAG_P, _FLAG_INDEX, _FLAG_PX, _FLAG_X, _FLAG_TIMEOUT, _FLAG_EXACT = 1, 2, 4, 8, 16, 32   # UQ_QFL_*
 _tables_prefix = None
 _dropin_lock = threading.Lock()
 _dropin: dict = {}
@@ -265,11 +265,18 @@ def quicfl_compress(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSende
 
 
 # ---- receiver ----------------------------------------------------------------------------------------
+_X_KIND = {torch.int64: 0, torch.uint8: 1, torch.int32: 2}
+
+
 def quicfl_decompress(X, nbits: int, prng_seeds, rotation_seeds, scale, dim: int, recv_table, h_len: int | None = None,
-                      exact_mask=None, exact_vals=None) -> torch.Tensor:
-    """Batched QuicFLReceiver.decompress (AS:526-535).  X [n, D] integers in [0, rows) with D a
-    power of two; recv_table [rows, h_len]; exact_mask bool [n, D] with exact_vals f32 [n, D]
-    (dense: the value where the mask is set) or both None; scale [n]; returns [n, dim] f32."""
+                      exact_mask=None, exact_vals=None, exact_count=None) -> torch.Tensor:
+    """Batched QuicFLReceiver.decompress (AS:526-535).  X [n, D] integers (int64, uint8 or int32
+    are read in place on the device) with D a power of two; recv_table [rows, h_len];
+    exact_mask bool [n, D] with exact_vals f32 [n, D], or both None.  exact_vals is dense (the
+    value at its coordinate) when exact_count is None, else compact: row j's exact values in
+    index order in its first exact_count[j] entries (quicfl_compress's layout).  scale [n];
+    returns [n, dim] f32.  Raises IndexError where torch.take would (AS:530) and RuntimeError
+    when a compact row's count does not match its mask (AS:531)."""
     dev = _device()
     X = torch.as_tensor(X)
     if X.dim() == 1:
@@ -283,9 +290,9 @@ def quicfl_decompress(X, nbits: int, prng_seeds, rotation_seeds, scale, dim: int
     rows, hl = (tab.shape[0], tab.shape[1]) if tab.dim() == 2 else (1, tab.numel())
     if h_len is not None and int(h_len) != hl:
         raise ValueError("h_len does not match the receiver table")
-    if X.numel() and (int(X.min()) < 0 or int(X.max()) >= rows):
-        raise IndexError("X outside the receiver table (torch.take raises, AS:530)")
-    Xd = X.to(device=dev, dtype=torch.int32).contiguous()
+    if X.dtype not in _X_KIND:
+        X = X.to(torch.int64)
+    Xd = X.to(dev).contiguous()
     ps = torch.as_tensor(prng_seeds, dtype=torch.int64).reshape(-1)
     rs = torch.as_tensor(rotation_seeds, dtype=torch.int64).reshape(-1)
     sc = torch.as_tensor(scale, dtype=torch.float32).reshape(-1).to(dev)
@@ -293,25 +300,36 @@ def quicfl_decompress(X, nbits: int, prng_seeds, rotation_seeds, scale, dim: int
         raise ValueError("one prng seed, rotation seed and scale per message")
     if (exact_mask is None) != (exact_vals is None):
         raise ValueError("exact_mask and exact_vals go together")
-    m = v = None
+    m = v = cnt = None
     if exact_mask is not None:
-        m = torch.as_tensor(exact_mask).to(device=dev, dtype=torch.uint8).reshape(n, D).contiguous()
+        m = torch.as_tensor(exact_mask).to(device=dev).reshape(n, D)
+        m = (m if m.dtype in (torch.bool, torch.uint8) else m != 0).contiguous()
         v = torch.as_tensor(exact_vals, dtype=torch.float32).to(dev).reshape(n, D).contiguous()
+        if exact_count is not None:
+            cnt = torch.as_tensor(exact_count, dtype=torch.int32).reshape(-1).to(dev)
+            if cnt.numel() != n:
+                raise ValueError("one exact count per message")
     pre = torch.empty((n, D), dtype=torch.float32, device=dev)
     if n:
         seeds32 = (ps & 0xFFFFFFFF).to(torch.int64)
         seeds32 = torch.where(seeds32 >= 1 << 31, seeds32 - (1 << 32), seeds32).to(torch.int32).to(dev)
-        _lib.check(_lib.load().uq_quicfl_prepare_f32(_ptr(Xd), n, D, _ptr(tab), rows, hl, _ptr(seeds32),
-                                                      _ptr(m) if m is not None else None,
-                                                      _ptr(v) if v is not None else None, _ptr(sc), _ptr(pre),
-                                                      _stream_ptr(dev)), "uq_quicfl_prepare_f32")
+        info = torch.zeros(n, dtype=torch.int32, device=dev)
+        _lib.check(_lib.load().uq_quicfl_receive_f32(
+            _ptr(Xd), _X_KIND[Xd.dtype], n, D, _ptr(tab), rows, hl, _ptr(seeds32), _ptr(m), _ptr(v),
+            0 if cnt is None else 1, _ptr(cnt), _ptr(sc), _ptr(pre), _ptr(info), _stream_ptr(dev)), "uq_quicfl_receive_f32")
+        flags = int(np.bitwise_or.reduce(info.cpu().numpy()))
+        if flags & _FLAG_INDEX:
+            raise IndexError("index out of range in self (AS:530 recv_table.take)")
+        if flags & _FLAG_EXACT:
+            raise RuntimeError("shape mismatch: exact_values do not match exact_indeces (AS:531)")
     return randomized_inverse_hadamard_transform(pre, rs)[:, :dim]
 
 
 def quicfl_decompress_messages(msg: QuicFLMessages, recv_table) -> torch.Tensor:
-    """The receiver (AS:526-535) on every message of a quicfl_compress batch -> [n, dim]."""
+    """The receiver (AS:526-535) on every message of a quicfl_compress batch -> [n, dim]
+    (X, mask and the compact exact values read in place)."""
     return quicfl_decompress(msg.X, msg.nbits, msg.prng_seeds, msg.rotation_seeds, msg.scale, msg.dim, recv_table,
-                             msg.h_len, msg.exact_mask, msg.exact_dense())
+                             msg.h_len, msg.exact_mask, msg.exact_vals, msg.exact_count)
 
 
 class QuicFLReceiver:
@@ -344,16 +362,20 @@ class QuicFLReceiver:
         """AS:526-535: the message dict of QuicFLSender.compress -> vec[:dim] (on the GPU)."""
         X = torch.as_tensor(data["X"]).reshape(1, -1)
         D = X.shape[1]
-        mask = vals = None
+        mask = vals = cnt = None
         ei = data.get("exact_indeces")
-        if ei is not None and bool(torch.as_tensor(ei).any()):
+        if ei is not None:
             dev = _device()
-            mask = torch.as_tensor(ei).reshape(1, D).to(device=dev, dtype=torch.bool)
-            vals = torch.zeros((1, D), dtype=torch.float32, device=dev)
-            vals[mask] = torch.as_tensor(data["exact_values"], dtype=torch.float32).reshape(-1).to(dev)
+            mask = torch.as_tensor(ei).reshape(1, D).to(dev)
+            ev = torch.as_tensor(data["exact_values"], dtype=torch.float32).reshape(-1)
+            if ev.numel() > D:
+                raise RuntimeError("shape mismatch: more exact_values than coordinates (AS:531)")
+            vals = torch.zeros((1, D), dtype=torch.float32, device=dev)   # compact: the values, then room to D
+            vals[0, :ev.numel()] = ev.to(dev)
+            cnt = [ev.numel()]
         out = quicfl_decompress(X, data["nbits"], [int(data["prng_seed"])], [int(data["rotation_seed"])],
-                                [float(torch.as_tensor(data["scale"]))], int(data["dim"]),
-                                self.recv_table[int(data["nbits"])], int(data["h_len"]), mask, vals)
+                                data["scale"], int(data["dim"]), self.recv_table[int(data["nbits"])],
+                                int(data["h_len"]), mask, vals, cnt)
         return out.view(-1)
 
 
