@@ -193,10 +193,10 @@ int uq_tc_decode(const uint8_t* msgs, size_t msgs_bytes, const uint64_t* offsets
  * through the workspace: no workspace content changes which path a replay takes. */
 #define UQ_TIES_TORCH 0
 #define UQ_TIES_LOWEST_INDEX 1
-/* OR'd into UQ_TIES_TORCH: the call may wait once on an internal stream (never on `stream`)
- * for the number of clients whose tie choice needs the replay, and skips the replay's kernels
- * when it is zero -- for synchronous few-client callers (the per-vector drop-in); results are
- * the same bits either way. */
+/* OR'd into UQ_TIES_TORCH: the call synchronises `stream` once, to read the number of clients
+ * whose tie choice needs the replay, and skips the replay's kernels when it is zero -- for
+ * synchronous few-client callers (the per-vector drop-in); results are the same bits either
+ * way. */
 #define UQ_TIES_HOST_CHECK 4
 int uq_biased_workspace_bytes(int64_t n, int64_t d, int32_t torch_threads, size_t* bytes_out);
 int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t m,

@@ -18,6 +18,7 @@ indices instead (identical whenever info flag 1 is clear; see include/uq_dme.h).
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -33,6 +34,7 @@ __all__ = ["Type_biased_quantize", "biased_quantize", "TIES_TORCH", "TIES_LOWEST
 TIES_TORCH = 0            # UQ_TIES_TORCH
 TIES_LOWEST_INDEX = 1     # UQ_TIES_LOWEST_INDEX
 _HOST_CHECK = 4           # UQ_TIES_HOST_CHECK
+_tls = threading.local()
 FLAG_AMBIGUOUS = 1
 FLAG_NONFINITE = 2
 FLAG_RANGE = 4
@@ -106,8 +108,18 @@ def Type_biased_quantize(input_vector, bits_per_dimension=1):
     if not v.is_contiguous():
         v = v.contiguous()
     out, info = biased_quantize(v.view(1, d), m=m, ties="torch", return_info=True, host_check=True)
-    flags = int(info[0, 1].item())
-    check_status()
+    # one synchronisation for the flags and this workspace's status word (uq_check_status's
+    # word at byte 8; check_status() would read every cached workspace of the stream)
+    ws = _workspace(dev, _biased_ws_bytes(1, d, get_torch_threads()))
+    hw = getattr(_tls, "pinned", None)
+    if hw is None:
+        hw = _tls.pinned = torch.empty(2, dtype=torch.int32, pin_memory=True)
+    hw[0:1].copy_(info[0, 1:2], non_blocking=True)
+    hw[1:2].copy_(ws[8:12].view(torch.int32), non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    flags, status = int(hw[0]), int(hw[1])
+    if status:
+        check_status()                            # raises with the library's message, clears the word
     if flags & FLAG_NONFINITE:
         raise ValueError("cannot convert float NaN to integer (m' is not finite, AS:656)")
     if flags & FLAG_RANGE:

@@ -3232,7 +3232,31 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
                                list);
         return hip_check(hipGetLastError(), "rez_tiecount_kernel launch");
     };
-    if (tie_policy == UQ_TIES_TORCH) {
+    if (tie_policy == UQ_TIES_TORCH && host_check) {
+        // UQ_TIES_HOST_CHECK (synchronous few-client callers): one stream; after the tie list
+        // is built, wait for it and skip the replay chain -- KB7a's ~65 level launches --
+        // when no client is listed; then every client's output in one launch
+        rc = torch_ties_prepare(n, d, state, bits, wsb, w, st);
+        if (rc) return rc;
+        SideStream* sb = nullptr;
+        rc = side_stream(&sb);                            // (its pinned word)
+        if (rc) return rc;
+        rc = hip_check(hipMemcpyAsync(sb->count, wsb + w.list_off, sizeof(uint32_t), hipMemcpyDeviceToHost, st),
+                       "copy tie list length");
+        if (rc) return rc;
+        rc = tiecount(st, (const uint32_t*)(wsb + w.list_off));
+        if (rc) return rc;
+        rc = hip_check(hipStreamSynchronize(st), "sync");
+        if (rc) return rc;
+        if (*sb->count != 0u) {
+            const TieLevelState* tls = nullptr;
+            rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, st, &tls);
+            if (rc) return rc;
+            if (tls && (rc = launch_torch_ties_rest(x, d, l1buf, fm, state, bits, wsb, w, tls, st))) return rc;
+        }
+        rc = output(st, 0);
+        if (rc) return rc;
+    } else if (tie_policy == UQ_TIES_TORCH) {
         // fork: KB7 (few workgroups, latency-bound) on the side stream while KB6 writes the
         // clients without a threshold tie on the caller's stream; join, then the rest
         SideStream* sb = nullptr;
@@ -3252,18 +3276,7 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         rc = tiecount(sb->s, (const uint32_t*)(wsb + w.list_off));
         if (rc) return rc;
         const TieLevelState* tls = nullptr;
-        // UQ_TIES_HOST_CHECK: wait for the side stream (KB6 keeps the GPU busy meanwhile) and
-        // skip the replay chain -- KB7a's ~65 level launches -- when no client is listed
-        bool replay = true;
-        if (host_check) {
-            rc = hip_check(hipMemcpyAsync(sb->count, wsb + w.list_off, sizeof(uint32_t), hipMemcpyDeviceToHost, sb->s),
-                           "copy tie list length");
-            if (rc) return rc;
-            rc = hip_check(hipStreamSynchronize(sb->s), "sync side stream");
-            if (rc) return rc;
-            replay = *sb->count != 0u;
-        }
-        if (replay) rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls);
+        rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls);
         if (rc) return rc;
         rc = hip_check(hipEventRecord(sb->join, sb->s), "record join");
         if (rc) return rc;
