@@ -3232,7 +3232,10 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
                                list);
         return hip_check(hipGetLastError(), "rez_tiecount_kernel launch");
     };
-    if (tie_policy == UQ_TIES_TORCH && host_check) {
+    // (the check pays only where the replay would be KB7a's level chain; a one-kernel replay
+    // costs less than the synchronisation)
+    const bool kb7a = !(d <= kTieLevelMin || (n < kTieLevelMinClients && d < kTieLevelBigD));
+    if (tie_policy == UQ_TIES_TORCH && host_check && kb7a) {
         // UQ_TIES_HOST_CHECK (synchronous few-client callers): one stream; after the tie list
         // is built, wait for it and skip the replay chain -- KB7a's ~65 level launches --
         // when no client is listed; then every client's output in one launch
