@@ -16,14 +16,12 @@
 //   v = recv_table[X * h_len + h], exact overrides, v / scale.
 //
 // Both are serial in their MT19937 streams (ATen's mt19937: 624-word blocks, each twisted
-// from the previous), so the unit of parallelism is the message: ONE WAVE per message, no
-// workgroup barriers.  A wave twists a block in place in its LDS slice: word i needs
-// s[i], s[i+1] (old) and s[(i+397) % 624], which is old for i < 227 and new (written 227
-// words earlier) otherwise.  With 64 words per group, each group's operands lie >= 3 groups
-// back, so the wave reads every a/b operand up front and the c operands in three rounds
-// (groups 0-3, 4-6, 7-9); the wave's LDS operations stay in program order, so no barrier is
-// needed.  A 624-element round takes the words of its elements from the current block (slots
-// before the twist) and the next one (after it).
+// from the previous), so the unit of parallelism is the message: ONE WAVE per message (or, for
+// a few messages, a team of waves: KQ1t), no workgroup barriers.  A wave keeps a block in
+// registers (word 64 g + lane in VGPR g) and twists it with lane moves (mt_twist_reg).  A
+// 624-element round takes the words of its elements from the current block and the next one:
+// pass A and the receiver read word e of the round's own block (no lane move); pass B's words
+// start at an offset, read from a two-block LDS ring.
 //   KQ1 quicfl_send_wave_kernel     pass A: h = word % h_len (u8 scratch); pass B: the local
 //       stream (words D..2D-1) and the global stream side by side, each lane 10 elements of
 //       the round; the (X, p) table gather of round c is issued before round c-1 is finished
@@ -71,54 +69,60 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// One wave twists the block in s[624] in place (the sequential next_state's result).
-__device__ __forceinline__ void mt_twist_wave(uint32_t* s, int lane) {
-    uint32_t a[kMtGroups], b[kMtGroups], c[kMtGroups];
+// A block in registers: word 64 g + lane in s[g] (g = 9: lanes < 48).  One wave twists it into
+// the next block (ATen's next_state): word i takes s[i], s[i + 1] (old) and s[(i + 397) % 624],
+// which is old for i < 227 and new (227 words back) otherwise.  Operands move between lanes by
+// a DPP wave shift (the +1 neighbour) and ds_bpermute (the +13 / +29 lane rotations of the c
+// operand); the groups' dependencies (group g >= 4 needs new groups g-4 and g-3) leave four
+// levels.  tools/exp/mt_twist_bench.hip: 0.59 us per twist (+ temper) against 1.39 us for the
+// LDS in-place form with its wave fences, bit-identical to a host MT19937.
+__device__ __forceinline__ uint32_t mt_perm(uint32_t v, int src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+__device__ __forceinline__ void mt_twist_reg(uint32_t (&s)[kMtGroups], int lane) {
+    const int r13 = (lane + 13) & 63, r29 = (lane + 29) & 63;
+    uint32_t b[kMtGroups], N[kMtGroups];
 #pragma unroll
-    for (int g = 0; g < kMtGroups; ++g) {                      // old a, b of every word
-        const int i = 64 * g + lane;
-        if (i < kMtN) {
-            a[g] = s[i];
-            b[g] = s[i + 1 < kMtN ? i + 1 : 0];                 // (i = 623 re-reads new s[0] below)
+    for (int g = 0; g < kMtGroups; ++g) {                       // b = old word i + 1
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s[g], 0x130, 0xF, 0xF, false);  // wave_shl:1
+        const uint32_t first = g + 1 < kMtGroups ? (uint32_t)__builtin_amdgcn_readlane((int)s[g + 1], 0) : 0u;
+        b[g] = lane == 63 ? first : nx;
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {                               // i < 192: c = old word i + 397
+        const uint32_t t1 = mt_perm(s[g + 6], r13), t2 = mt_perm(s[g + 7], r13);
+        N[g] = mt_mix(s[g], b[g], lane < 51 ? t1 : t2);
+    }
+    {                                                           // i = 192..255: old s[9] below 227, new N[0] above
+        const uint32_t t1 = mt_perm(s[9], r13), t2 = mt_perm(N[0], r29);
+        N[3] = mt_mix(s[3], b[3], lane < 35 ? t1 : t2);
+    }
+#pragma unroll
+    for (int g = 4; g < kMtGroups; ++g) {                       // c = new word i - 227
+        const uint32_t t1 = mt_perm(N[g - 4], r29), t2 = mt_perm(N[g - 3], r29);
+        uint32_t bb = b[g];
+        if (g == kMtGroups - 1) {                               // word 623 twists with the new word 0
+            const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)N[0], 0);
+            bb = lane == 47 ? n0 : bb;
         }
+        N[g] = mt_mix(s[g], bb, lane < 35 ? t1 : t2);
     }
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {                              // words 0..226: c = old s[i + 397]
-        const int i = 64 * g + lane;
-        if (i < 227) c[g] = s[i + 397];
-    }
-    wave_lds_fence();                                          // every old operand read before any write
+    for (int g = 0; g < kMtGroups; ++g) s[g] = N[g];
+}
+__device__ __forceinline__ void mt_load(uint32_t (&s)[kMtGroups], const uint32_t* src, int lane) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < kMtGroups; ++g) {
         const int i = 64 * g + lane;
-        if (i < 227) s[i] = mt_mix(a[g], b[g], c[g]);
+        s[g] = src[i < kMtN ? i : 0];
     }
-    wave_lds_fence();
+}
+__device__ __forceinline__ void mt_store(const uint32_t (&s)[kMtGroups], uint32_t* dst, int lane) {
 #pragma unroll
-    for (int g = 3; g < 7; ++g) {                              // words 227..447: c = new s[i - 227] (0..220)
+    for (int g = 0; g < kMtGroups; ++g) {
         const int i = 64 * g + lane;
-        if (i >= 227) c[g] = s[i - 227];
+        if (i < kMtN) dst[i] = s[g];
     }
-#pragma unroll
-    for (int g = 3; g < 7; ++g) {
-        const int i = 64 * g + lane;
-        if (i >= 227) s[i] = mt_mix(a[g], b[g], c[g]);        // (writes 227..447, reads were 0..220)
-    }
-    wave_lds_fence();
-#pragma unroll
-    for (int g = 7; g < kMtGroups; ++g) {                      // words 448..623: c = new s[i - 227] (221..396)
-        const int i = 64 * g + lane;
-        if (i < kMtN) {
-            c[g] = s[i - 227];
-            if (i == kMtN - 1) b[g] = s[0];                    // the last word twists with the new s[0]
-        }
-    }
-#pragma unroll
-    for (int g = 7; g < kMtGroups; ++g) {
-        const int i = 64 * g + lane;
-        if (i < kMtN) s[i] = mt_mix(a[g], b[g], c[g]);        // (writes 448..623, reads were 0, 221..396)
-    }
-    wave_lds_fence();
 }
 
 struct QflSendArgs {
@@ -198,31 +202,47 @@ __device__ __forceinline__ QflCtx qfl_ctx(const QflSendArgs& a, int64_t j, int32
     return c;
 }
 
-// Pass A over rounds [c0, c1): Ls holds block c0 of the local stream on entry (block c + 1 holds
-// the words of round c), block c1 on exit.  h = randint(0, h_len, (D,), local) (AS:465/469).
-__device__ __forceinline__ void qfl_pass_a(const QflCtx& c, uint32_t* Ls, int64_t c0, int64_t c1, int lane) {
+// Pass A over rounds [c0, c1): s holds block c0 of the local stream on entry (block c + 1 holds
+// the words of round c), block c1 on exit.  h = randint(0, h_len, (D,), local) (AS:465/469):
+// element e of a round is word e of its block, i.e. register group e / 64 of its own lane.
+__device__ __forceinline__ void qfl_pass_a(const QflCtx& c, uint32_t (&s)[kMtGroups], int64_t c0, int64_t c1,
+                                           int lane) {
     for (int64_t r = c0; r < c1; ++r) {
-        mt_twist_wave(Ls, lane);
+        mt_twist_reg(s, lane);
         const uint32_t i0 = (uint32_t)(r * kMtN);
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
-            const uint32_t w = mt_temper(Ls[e < kMtN ? e : 0]);
+            const uint32_t w = mt_temper(s[k]);
             const uint32_t h = c.hpow2 ? (w & (c.h_len - 1u)) : (w % c.h_len);
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)h, c.rh, qf_off(e < kMtN, i0 + (uint32_t)e), 0, 0);
         }
     }
 }
 
-// Pass B over rounds [c0, c1) (AS:472-490): Ls holds local block haveL <= qL + c0, Gs global
-// block haveG <= qG + c0.  Exact values go to ev[row + ev_base + count] in index order; returns
-// the count, ORs UQ_QFL_* into flags.  Every per-element global access goes through a buffer
-// descriptor (out-of-range loads return 0, stores are dropped): no per-element branch, and a
-// lane's ten loads of a round are in flight together.
+// A stream read at an offset (pass B's words start at slot rL / rG of a block): the block in
+// registers (`have` twists) and a two-block LDS ring W holding blocks have - 1 and have at
+// (block & 1) * 624, so a round's 624 words are one ring read each, wherever they start.
+__device__ __forceinline__ void qfl_window_to(uint32_t (&s)[kMtGroups], uint32_t* W, int64_t& have, int64_t need,
+                                              int lane) {
+    while (have < need) {
+        mt_twist_reg(s, lane);
+        ++have;
+        mt_store(s, W + (have & 1) * kMtN, lane);
+    }
+}
+
+// Pass B over rounds [c0, c1) (AS:472-490): sL / sG hold local block haveL <= qL + c0 and
+// global block haveG <= qG + c0, each also stored in its ring (WL, WG) on entry.  Exact values
+// go to ev[row + ev_base + count] in index order; returns the count, ORs UQ_QFL_* into flags.
+// Every per-element global access goes through a buffer descriptor (out-of-range loads return
+// 0, stores are dropped): no per-element branch, and a lane's ten loads of a round are in flight
+// together.
 template <int XK>
-__device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict__ ev, uint32_t* Ls, int64_t& haveL,
-                                              uint32_t* Gs, int64_t& haveG, int64_t c0, int64_t c1, int64_t ev_base,
-                                              int32_t& flags, int lane) {
+__device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict__ ev, uint32_t (&sL)[kMtGroups],
+                                              uint32_t* WL, int64_t& haveL, uint32_t (&sG)[kMtGroups], uint32_t* WG,
+                                              int64_t& haveG, int64_t c0, int64_t c1, int64_t ev_base, int32_t& flags,
+                                              int lane) {
     const int64_t D = c.D;
     const float thr = kQflExactT;
     int64_t etot = 0;
@@ -277,35 +297,20 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             r_nxt[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.rr, in * 4u, 0, kAuxNT));
             h_nxt[k] = __builtin_amdgcn_raw_buffer_load_b8(c.rh, in, 0, 0);
         }
-        // the words of this round: slots rX + e of blocks qX + rd (before) and qX + rd + 1 (after)
-        while (haveL < c.qL + rd) { mt_twist_wave(Ls, lane); ++haveL; }
-        while (haveG < c.qG + rd) { mt_twist_wave(Gs, lane); ++haveG; }
+        // the words of this round: slots rX .. rX + lastE of block qX + rd and, past 623, of
+        // block qX + rd + 1 (twisted only when the round reaches it, so the global stream ends
+        // on the block holding its last word)
+        qfl_window_to(sL, WL, haveL, c.qL + rd + (c.rL + lastE >= kMtN ? 1 : 0), lane);
+        qfl_window_to(sG, WG, haveG, c.qG + rd + (c.rG + lastE >= kMtN ? 1 : 0), lane);
+        wave_lds_fence();
+        const int bL = (int)(((c.qL + rd) & 1) * kMtN) + c.rL, bG = (int)(((c.qG + rd) & 1) * kMtN) + c.rG;
         uint32_t wl[kMtGroups], wg[kMtGroups];
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
-            const int e = 64 * k + lane;
-            wl[k] = Ls[c.rL + e < kMtN ? c.rL + e : 0];
-            wg[k] = Gs[c.rG + e < kMtN ? c.rG + e : 0];
-        }
-        if (c.rL + lastE >= kMtN) {
-            mt_twist_wave(Ls, lane);
-            ++haveL;
-#pragma unroll
-            for (int k = 0; k < kMtGroups; ++k) {
-                const int p = c.rL + 64 * k + lane;
-                const uint32_t w = Ls[p >= kMtN && p < 2 * kMtN ? p - kMtN : 0];
-                if (p >= kMtN) wl[k] = w;
-            }
-        }
-        if (c.rG + lastE >= kMtN) {
-            mt_twist_wave(Gs, lane);
-            ++haveG;
-#pragma unroll
-            for (int k = 0; k < kMtGroups; ++k) {
-                const int p = c.rG + 64 * k + lane;
-                const uint32_t w = Gs[p >= kMtN && p < 2 * kMtN ? p - kMtN : 0];
-                if (p >= kMtN) wg[k] = w;
-            }
+            const int e = 64 * k + lane < kMtN ? 64 * k + lane : 0;
+            const int pl = bL + e, pg = bG + e;
+            wl[k] = WL[pl >= 2 * kMtN ? pl - 2 * kMtN : pl];
+            wg[k] = WG[pg >= 2 * kMtN ? pg - 2 * kMtN : pg];
         }
         // stage 1 of round rd: AS:472-487, the gather issued (branch-free: inactive elements
         // compute on zeros, raise no flags and store nothing)
@@ -353,10 +358,10 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
     return etot;
 }
 
-// The global generator's state after the message's D draws (the block holding word D - 1,
-// which Gs holds after the last round).
-__device__ __forceinline__ void qfl_state_out(uint32_t* so, const uint32_t* Gs, int64_t D, int32_t gleft, int32_t gnext,
-                                              int64_t vG, int lane) {
+// The global generator's state after the message's D draws: the block holding word D - 1
+// (sG after the last round) and ATen's (left, next) for it.
+__device__ __forceinline__ void qfl_state_out(uint32_t* so, const uint32_t (&sG)[kMtGroups], int64_t D, int32_t gleft,
+                                              int32_t gnext, int64_t vG, int lane) {
     uint32_t left1, next1;
     if (D <= (int64_t)gleft - 1) {                               // every draw from the current block
         left1 = (uint32_t)(gleft - D);
@@ -366,24 +371,28 @@ __device__ __forceinline__ void qfl_state_out(uint32_t* so, const uint32_t* Gs, 
         next1 = (uint32_t)(pos + 1);
         left1 = (uint32_t)(kMtN - pos);
     }
-    for (int i = lane; i < kMtN; i += 64) so[2 + i] = Gs[i];
+    mt_store(sG, so + 2, lane);
     if (lane == 0) {
         so[0] = left1;
         so[1] = next1;
     }
 }
 
-__device__ __forceinline__ void qfl_gen_init(const QflSendArgs& a, int64_t j, uint32_t* Gs, int32_t& gleft,
-                                             int32_t& gnext, int lane) {
+// The global generator of message j into registers: ATen's state (left, next, words) or a
+// fresh generator seeded with px_seeds[j] (init_genrand by one lane in `scratch`).
+__device__ __forceinline__ void qfl_gen_init(const QflSendArgs& a, int64_t j, uint32_t (&sG)[kMtGroups],
+                                             uint32_t* scratch, int32_t& gleft, int32_t& gnext, int lane) {
     gleft = 1;
     gnext = 0;
     if (a.px_state) {
         const uint32_t* st = a.px_state + j * kQfStateWords;
         gleft = (int32_t)st[0];
         gnext = (int32_t)st[1];
-        for (int i = lane; i < kMtN; i += 64) Gs[i] = st[2 + i];
-    } else if (lane == 1) {
-        mt_seed(Gs, (uint32_t)a.px_seeds[j]);
+        mt_load(sG, st + 2, lane);
+    } else {
+        if (lane == 0) mt_seed(scratch, (uint32_t)a.px_seeds[j]);
+        wave_lds_fence();
+        mt_load(sG, scratch, lane);
     }
 }
 
@@ -391,26 +400,31 @@ __device__ __forceinline__ void qfl_gen_init(const QflSendArgs& a, int64_t j, ui
 template <int XK>
 __global__ void __launch_bounds__(64 * kQfWavesPerWG)
 quicfl_send_wave_kernel(QflSendArgs a) {
-    __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];      // local generator block per wave
-    __shared__ uint32_t Gsh[kQfWavesPerWG][kMtN];      // global generator block per wave
+    __shared__ uint32_t WLsh[kQfWavesPerWG][2 * kMtN];    // local stream ring per wave (first: the seed scratch)
+    __shared__ uint32_t WGsh[kQfWavesPerWG][2 * kMtN];    // global stream ring per wave
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
     if (j >= a.n) return;                                       // whole wave: no barrier below
-    uint32_t* Ls = Lsh[wv];
-    uint32_t* Gs = Gsh[wv];
+    uint32_t* WL = WLsh[wv];
+    uint32_t* WG = WGsh[wv];
+    uint32_t sL[kMtGroups], sG[kMtGroups];
     int32_t gleft, gnext;
-    qfl_gen_init(a, j, Gs, gleft, gnext, lane);
-    if (lane == 0) mt_seed(Ls, (uint32_t)a.prng_seeds[j]);
+    qfl_gen_init(a, j, sG, WG, gleft, gnext, lane);
+    if (lane == 0) mt_seed(WL, (uint32_t)a.prng_seeds[j]);
+    wave_lds_fence();
+    mt_load(sL, WL, lane);
     wave_lds_fence();
     const QflCtx c = qfl_ctx<XK>(a, j, gleft, gnext);
     const int64_t nch = (a.D + kMtN - 1) / kMtN;
-    qfl_pass_a(c, Ls, 0, nch, lane);
+    qfl_pass_a(c, sL, 0, nch, lane);
     int64_t haveL = nch, haveG = 0;
+    mt_store(sL, WL + (haveL & 1) * kMtN, lane);
+    mt_store(sG, WG, lane);
     int32_t flags = 0;
-    const int64_t etot = qfl_pass_b<XK>(c, a.ev, Ls, haveL, Gs, haveG, 0, nch, 0, flags, lane);
+    const int64_t etot = qfl_pass_b<XK>(c, a.ev, sL, WL, haveL, sG, WG, haveG, 0, nch, 0, flags, lane);
     for (int s = 32; s >= 1; s >>= 1) flags |= __shfl_xor(flags, s);
     if (a.px_state_out)
-        qfl_state_out(a.px_state_out + j * kQfStateWords, Gs, a.D, gleft, gnext, c.qG * kMtN + c.rG, lane);
+        qfl_state_out(a.px_state_out + j * kQfStateWords, sG, a.D, gleft, gnext, c.qG * kMtN + c.rG, lane);
     if (lane == 0) {
         a.ecount[j] = (int32_t)etot;
         a.scale[j] = c.sc;
@@ -421,16 +435,17 @@ quicfl_send_wave_kernel(QflSendArgs a) {
 // KQ1 for a few messages (the per-call drop-in): one 512-thread workgroup per message.  Wave
 // 0 ("scout") runs the local stream from its seed through all 2D words, wave 1 the global stream
 // through D words; neither does per-coordinate work.  The other 6 waves take contiguous runs of
-// rounds: when a scout's stream reaches the block a run starts from, the scout copies the block
-// into that wave's LDS slice and raises its flag, so each run generates only its own words.
-// The critical path is the scout's 2D / 624 twists, not the coordinates' arithmetic.  Exact
-// values are written per run and compacted into index order at the end.  Flags are waited for
-// with a bounded spin (UQ_QFL_TIMEOUT if it ever ran out: the scouts never wait on anyone).
-constexpr int kQfTeamWaves = 8;                    // 2 scouts + 6 runs (<= 256 VGPRs per lane)
+// rounds: when a scout's stream reaches the block a run starts from, the scout stores that block
+// into the run's LDS slice (pass A) or ring (pass B) and raises its flag, so each run generates
+// only its own words.  The critical path is the scouts' 2D / 624 twists, not the coordinates'
+// arithmetic.  Exact values are written per run and compacted into index order at the end.
+// Flags are waited for with a bounded spin (UQ_QFL_TIMEOUT if it ever ran out: the scouts never
+// wait on anyone).
+constexpr int kQfTeamWaves = 8;                    // 2 scouts + 6 runs
 constexpr int kQfRuns = kQfTeamWaves - 2;
 constexpr int64_t kQfTeamMaxN = 64;                 // messages per call up to which the team kernel runs
 // padded dims up to which it runs: the last run waits for the scouts' 2D/624 twists (about
-// 30 ms at 2^23), far inside qfl_wait_flag's bound of 2^24 sleeps; longer vectors take the
+// 15 ms at 2^23), far inside qfl_wait_flag's bound of 2^24 sleeps; longer vectors take the
 // one-wave-per-message kernel, which never waits
 constexpr int64_t kQfTeamMaxD = (int64_t)1 << 23;
 __device__ __forceinline__ bool qfl_wait_flag(int* f) {
@@ -440,8 +455,8 @@ __device__ __forceinline__ bool qfl_wait_flag(int* f) {
     }
     return false;
 }
-__device__ __forceinline__ void qfl_give(uint32_t* dst, const uint32_t* src, int* f, int lane) {
-    for (int i = lane; i < kMtN; i += 64) dst[i] = src[i];
+__device__ __forceinline__ void qfl_give(uint32_t* dst, const uint32_t (&s)[kMtGroups], int* f, int lane) {
+    mt_store(s, dst, lane);
     wave_lds_fence();
     if (lane == 0) __hip_atomic_store(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -449,8 +464,9 @@ __device__ __forceinline__ void qfl_give(uint32_t* dst, const uint32_t* src, int
 template <int XK>
 __global__ void __launch_bounds__(64 * kQfTeamWaves)
 quicfl_send_team_kernel(QflSendArgs a) {
-    __shared__ uint32_t LA[kQfRuns][kMtN], LB[kQfRuns][kMtN], GB[kQfRuns][kMtN];
-    __shared__ uint32_t SL[kMtN], SG[kMtN];             // the scouts' blocks
+    __shared__ uint32_t LA[kQfRuns][kMtN];               // pass-A start block per run
+    __shared__ uint32_t WL[kQfRuns][2 * kMtN], WG[kQfRuns][2 * kMtN];   // pass-B rings per run
+    __shared__ uint32_t seed_scratch[2][kMtN];
     __shared__ int rdy[kQfRuns][3];
     __shared__ int64_t cnt[kQfRuns];
     __shared__ int32_t sflags;
@@ -462,50 +478,60 @@ quicfl_send_team_kernel(QflSendArgs a) {
     for (int i = threadIdx.x; i < kQfRuns * 3; i += 64 * kQfTeamWaves) (&rdy[0][0])[i] = 0;
     if (threadIdx.x < kQfRuns) cnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) sflags = 0;
-    int32_t gleft, gnext;
-    if (wv == 1) qfl_gen_init(a, j, SG, gleft, gnext, lane);     // every wave needs gleft/gnext below
-    else {
-        gleft = a.px_state ? (int32_t)a.px_state[j * kQfStateWords] : 1;
-        gnext = a.px_state ? (int32_t)a.px_state[j * kQfStateWords + 1] : 0;
+    uint32_t s[kMtGroups];                               // the scouts' stream block
+    int32_t gleft = a.px_state ? (int32_t)a.px_state[j * kQfStateWords] : 1;
+    int32_t gnext = a.px_state ? (int32_t)a.px_state[j * kQfStateWords + 1] : 0;
+    if (wv == 1) qfl_gen_init(a, j, s, seed_scratch[1], gleft, gnext, lane);
+    if (wv == 0) {
+        if (lane == 0) mt_seed(seed_scratch[0], (uint32_t)a.prng_seeds[j]);
+        wave_lds_fence();
+        mt_load(s, seed_scratch[0], lane);
     }
-    if (wv == 0 && lane == 0) mt_seed(SL, (uint32_t)a.prng_seeds[j]);
     __syncthreads();
     const QflCtx c = qfl_ctx<XK>(a, j, gleft, gnext);
     int32_t flags = 0;
     if (wv == 0) {                                       // local scout: blocks 0 .. qL + start of the last run
         __builtin_amdgcn_s_setprio(3);
         int64_t last = 0;
-        for (int s = 0; s < kQfRuns; ++s)
-            if (s * per < nch) last = c.qL + s * per;
+        for (int r = 0; r < kQfRuns; ++r)
+            if (r * per < nch) last = c.qL + r * per;
         for (int64_t k = 0; k <= last; ++k) {
-            if (k) mt_twist_wave(SL, lane);
-            if (k < nch && k % per == 0) qfl_give(LA[k / per], SL, &rdy[k / per][0], lane);
+            if (k) mt_twist_reg(s, lane);
+            if (k < nch && k % per == 0) qfl_give(LA[k / per], s, &rdy[k / per][0], lane);
             const int64_t kb = k - c.qL;
-            if (kb >= 0 && kb < nch && kb % per == 0) qfl_give(LB[kb / per], SL, &rdy[kb / per][1], lane);
+            if (kb >= 0 && kb < nch && kb % per == 0) qfl_give(WL[kb / per] + (k & 1) * kMtN, s, &rdy[kb / per][1], lane);
         }
     } else if (wv == 1) {                                // global scout
         __builtin_amdgcn_s_setprio(3);
         int64_t last = 0;
-        for (int s = 0; s < kQfRuns; ++s)
-            if (s * per < nch) last = c.qG + s * per;
+        for (int r = 0; r < kQfRuns; ++r)
+            if (r * per < nch) last = c.qG + r * per;
         for (int64_t k = 0; k <= last; ++k) {
-            if (k) mt_twist_wave(SG, lane);
+            if (k) mt_twist_reg(s, lane);
             const int64_t kg = k - c.qG;
-            if (kg >= 0 && kg < nch && kg % per == 0) qfl_give(GB[kg / per], SG, &rdy[kg / per][2], lane);
+            if (kg >= 0 && kg < nch && kg % per == 0) qfl_give(WG[kg / per] + (k & 1) * kMtN, s, &rdy[kg / per][2], lane);
         }
-    } else {                                             // run s: rounds [c0, c1)
-        const int s = wv - 2;
-        const int64_t c0 = s * per, c1 = min(nch, c0 + per);
+    } else {                                             // run r: rounds [c0, c1)
+        const int r = wv - 2;
+        const int64_t c0 = r * per, c1 = min(nch, c0 + per);
         if (c0 < c1) {
-            bool ok = qfl_wait_flag(&rdy[s][0]);
-            if (ok) qfl_pass_a(c, LA[s], c0, c1, lane);
-            ok = ok && qfl_wait_flag(&rdy[s][1]) && qfl_wait_flag(&rdy[s][2]);
+            bool ok = qfl_wait_flag(&rdy[r][0]);
+            if (ok) {
+                uint32_t sa[kMtGroups];
+                mt_load(sa, LA[r], lane);
+                qfl_pass_a(c, sa, c0, c1, lane);
+            }
+            ok = ok && qfl_wait_flag(&rdy[r][1]) && qfl_wait_flag(&rdy[r][2]);
             if (ok) {
                 int64_t haveL = c.qL + c0, haveG = c.qG + c0;
-                const int64_t e = qfl_pass_b<XK>(c, a.ev, LB[s], haveL, GB[s], haveG, c0, c1, c0 * kMtN, flags, lane);
-                if (lane == 0) cnt[s] = e;
+                uint32_t sL[kMtGroups], sG[kMtGroups];
+                mt_load(sL, WL[r] + (haveL & 1) * kMtN, lane);
+                mt_load(sG, WG[r] + (haveG & 1) * kMtN, lane);
+                const int64_t e = qfl_pass_b<XK>(c, a.ev, sL, WL[r], haveL, sG, WG[r], haveG, c0, c1, c0 * kMtN, flags,
+                                                 lane);
+                if (lane == 0) cnt[r] = e;
                 if (c1 == nch && a.px_state_out)
-                    qfl_state_out(a.px_state_out + j * kQfStateWords, GB[s], D, gleft, gnext, c.qG * kMtN + c.rG, lane);
+                    qfl_state_out(a.px_state_out + j * kQfStateWords, sG, D, gleft, gnext, c.qG * kMtN + c.rG, lane);
             } else {
                 flags |= UQ_QFL_TIMEOUT;
             }
@@ -514,16 +540,16 @@ quicfl_send_team_kernel(QflSendArgs a) {
         if (lane == 0 && flags) atomicOr(&sflags, flags);
     }
     __syncthreads();
-    if (wv == 0) {                                       // exact values of run s: [c0*624, +cnt) -> index order
+    if (wv == 0) {                                       // exact values of run r: [c0*624, +cnt) -> index order
         int64_t base = 0;
-        for (int s = 0; s < kQfRuns; ++s) {
-            const int64_t src = s * per * kMtN, n_s = cnt[s];
-            for (int64_t i0 = 0; i0 < n_s; i0 += 64) {   // (base <= src: a downward move, chunk by chunk)
+        for (int r = 0; r < kQfRuns; ++r) {
+            const int64_t src = r * per * kMtN, n_r = cnt[r];
+            for (int64_t i0 = 0; i0 < n_r; i0 += 64) {   // (base <= src: a downward move, chunk by chunk)
                 const int64_t i = i0 + lane;
-                const float v = i < n_s ? a.ev[c.row + src + i] : 0.f;
-                if (i < n_s) a.ev[c.row + base + i] = v;
+                const float v = i < n_r ? a.ev[c.row + src + i] : 0.f;
+                if (i < n_r) a.ev[c.row + base + i] = v;
             }
-            base += n_s;
+            base += n_r;
         }
         if (lane == 0) {
             a.ecount[j] = (int32_t)base;
@@ -552,7 +578,7 @@ quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const 
                         const uint8_t* __restrict__ exact_mask, const float* __restrict__ exact_vals, int compact,
                         const int32_t* __restrict__ exact_count, const float* __restrict__ scale,
                         float* __restrict__ out, int32_t* __restrict__ info) {
-    __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];
+    __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];                // seed scratch per wave
     __shared__ float tab[kQflTab];
     for (int i = threadIdx.x; i < tab_n; i += 64 * kQfWavesPerWG) tab[i] = table[i];
     __syncthreads();
@@ -562,6 +588,8 @@ quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const 
     uint32_t* Ls = Lsh[wv];
     if (lane == 0) mt_seed(Ls, (uint32_t)prng_seeds[j]);
     wave_lds_fence();
+    uint32_t sL[kMtGroups];                                      // the h stream's block in registers
+    mt_load(sL, Ls, lane);
     const int64_t row = j * D;
     const uint32_t Du = (uint32_t)D;
     const DivPlan dp = div_plan_norm(scale[j]);                 // v / scale (AS:532): exact quotient
@@ -624,12 +652,12 @@ quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const 
         load_x(i0 + kMtN, xn);
         load_m(i0 + 2u * kMtN, m2);
         load_v(i0 + kMtN, mn, vn);
-        mt_twist_wave(Ls, lane);
+        mt_twist_reg(sL, lane);
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
             const bool act = e < kMtN && (int64_t)i0 + e < D;
-            const uint32_t w = mt_temper(Ls[e < kMtN ? e : 0]);
+            const uint32_t w = mt_temper(sL[k]);
             const uint32_t h = hpow2 ? (w & (hl - 1u)) : (w % hl);                     // AS:528 randint
             const int64_t it = (int64_t)((uint64_t)xr[k] * (uint64_t)hl + h);          // AS:530 (int64 arithmetic)
             const bool inr = it >= -(int64_t)tab_n && it < (int64_t)tab_n;
