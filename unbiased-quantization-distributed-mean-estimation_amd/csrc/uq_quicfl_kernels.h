@@ -246,17 +246,25 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
     const int64_t D = c.D;
     const float thr = kQflExactT;
     int64_t etot = 0;
-    QflRound pr;                                                // the previous round (stage 2 pending)
-    bool have_prev = false;
-    uint32_t prev_i0 = 0;
-    float r_cur[kMtGroups], r_nxt[kMtGroups];
-    uint32_t h_cur[kMtGroups], h_nxt[kMtGroups];
+    // Two register sets for a round's inputs and for its pending stage 2, used alternately by
+    // the loop unrolled by two: a set whose loads are in flight is never copied, so the next
+    // round's loads and this round's gathers stay in flight across the round (with one set,
+    // the end-of-round copies waited for every load).
+    struct In {
+        float r[kMtGroups];
+        uint32_t h[kMtGroups];
+    };
+    In I0, I1;
+    QflRound R0, R1;
+    auto load_in = [&](uint32_t i0, In& o) {
 #pragma unroll
-    for (int k = 0; k < kMtGroups; ++k) {
-        const uint32_t e = (uint32_t)(c0 * kMtN) + 64u * k + lane;
-        r_cur[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.rr, e * 4u, 0, kAuxNT));
-        h_cur[k] = __builtin_amdgcn_raw_buffer_load_b8(c.rh, e, 0, 0);
-    }
+        for (int k = 0; k < kMtGroups; ++k) {
+            const uint32_t e = i0 + 64u * k + lane;
+            o.r[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.rr, e * 4u, 0, kAuxNT));
+            o.h[k] = __builtin_amdgcn_raw_buffer_load_b8(c.rh, e, 0, 0);
+        }
+    };
+    load_in((uint32_t)(c0 * kMtN), I0);
 
     auto finish = [&](const QflRound& r, uint32_t i0) {          // stage 2 of a round (AS:489-490, 494-495)
 #pragma unroll
@@ -287,16 +295,12 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
         }
     };
 
-    for (int64_t rd = c0; rd < c1; ++rd) {
+    // one round: loads for round rd + 1 into `nxt`, stage 1 of round rd from `cur` into `cr`
+    // (its gathers issued), then stage 2 of round rd - 1 (`pr`) while those gathers fly
+    auto round = [&](int64_t rd, const In& cur, In& nxt, QflRound& cr, const QflRound& pr, bool fin) {
         const uint32_t i0 = (uint32_t)(rd * kMtN);
         const int lastE = (int)((D - 1 - (int64_t)i0) < (kMtN - 1) ? (D - 1 - (int64_t)i0) : (kMtN - 1));
-        // next round's loads first (beyond D: the descriptor returns 0)
-#pragma unroll
-        for (int k = 0; k < kMtGroups; ++k) {
-            const uint32_t in = i0 + (uint32_t)kMtN + 64u * k + lane;
-            r_nxt[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.rr, in * 4u, 0, kAuxNT));
-            h_nxt[k] = __builtin_amdgcn_raw_buffer_load_b8(c.rh, in, 0, 0);
-        }
+        load_in(i0 + (uint32_t)kMtN, nxt);                           // (beyond D: the descriptor returns 0)
         // the words of this round: slots rX .. rX + lastE of block qX + rd and, past 623, of
         // block qX + rd + 1 (twisted only when the round reaches it, so the global stream ends
         // on the block holding its last word)
@@ -304,34 +308,29 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
         qfl_window_to(sG, WG, haveG, c.qG + rd + (c.rG + lastE >= kMtN ? 1 : 0), lane);
         wave_lds_fence();
         const int bL = (int)(((c.qL + rd) & 1) * kMtN) + c.rL, bG = (int)(((c.qG + rd) & 1) * kMtN) + c.rG;
-        uint32_t wl[kMtGroups], wg[kMtGroups];
-#pragma unroll
-        for (int k = 0; k < kMtGroups; ++k) {
-            const int e = 64 * k + lane < kMtN ? 64 * k + lane : 0;
-            const int pl = bL + e, pg = bG + e;
-            wl[k] = WL[pl >= 2 * kMtN ? pl - 2 * kMtN : pl];
-            wg[k] = WG[pg >= 2 * kMtN ? pg - 2 * kMtN : pg];
-        }
-        // stage 1 of round rd: AS:472-487, the gather issued (branch-free: inactive elements
-        // compute on zeros, raise no flags and store nothing)
-        QflRound cr;
         cr.ex = 0;
         cr.act = 0;
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
+            const int es = e < kMtN ? e : 0;
+            const int pl = bL + es, pg = bG + es;
+            const uint32_t wl = WL[pl >= 2 * kMtN ? pl - 2 * kMtN : pl];
+            const uint32_t wg = WG[pg >= 2 * kMtN ? pg - 2 * kMtN : pg];
+            // stage 1 (AS:472-487), branch-free: inactive elements compute on zeros, raise no
+            // flags and store nothing
             const bool active = e < kMtN && (int64_t)i0 + e < D;
-            cr.wg[k] = mt_temper(wg[k]);
-            const float v = r_cur[k] * c.sc;                          // AS:472
+            cr.wg[k] = mt_temper(wg);
+            const float v = cur.r[k] * c.sc;                          // AS:472
             const bool ex = (v > thr) || (v < -thr);                  // AS:478
             const float q = ex ? 0.f : div1(v, c.dp);                 // AS:480-481 (= v / delta)
             const float fl = floorf(q);
             const float p = q - fl;                                   // AS:483
             flags |= (active && !(p >= 0.f && p <= 1.f)) ? UQ_QFL_BAD_P : 0;
-            const float bern = (u24(mt_temper(wl[k])) < p) ? 1.f : 0.f;
+            const float bern = (u24(mt_temper(wl)) < p) ? 1.f : 0.f;
             const float iq = fl + bern;                               // AS:484
             const float t1 = iq * c.fh;                               // AS:486 in f32 (no fma: -ffp-contract=off)
-            const float t2 = t1 + (float)h_cur[k];
+            const float t2 = t1 + (float)cur.h[k];
             const float it = truncf(t2 + c.fhalf);                    // .long() truncates
             const bool inr = it >= -c.fnumel && it < c.fnumel;        // torch.take's range (NaN: out)
             flags |= (active && !inr) ? UQ_QFL_BAD_INDEX : 0;
@@ -344,17 +343,13 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             cr.ex |= (active && ex ? 1u : 0u) << k;
             cr.act |= (active ? 1u : 0u) << k;
         }
-        if (have_prev) finish(pr, prev_i0);                         // round rd-1 while round rd's gathers fly
-        pr = cr;
-        have_prev = true;
-        prev_i0 = i0;
-#pragma unroll
-        for (int k = 0; k < kMtGroups; ++k) {
-            r_cur[k] = r_nxt[k];
-            h_cur[k] = h_nxt[k];
-        }
+        if (fin) finish(pr, i0 - (uint32_t)kMtN);
+    };
+    for (int64_t rd = c0; rd < c1; rd += 2) {
+        round(rd, I0, I1, R0, R1, rd > c0);
+        if (rd + 1 < c1) round(rd + 1, I1, I0, R1, R0, true);
     }
-    if (have_prev) finish(pr, prev_i0);
+    if (c1 > c0) finish(((c1 - 1 - c0) & 1) ? R1 : R0, (uint32_t)((c1 - 1) * kMtN));
     return etot;
 }
 
@@ -605,53 +600,55 @@ quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const 
                                                  exact_vals ? Du * 4u : 0u);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(out + row, Du * 4u);
     const uint64_t below = (1ull << lane) - 1ull;
-    int64_t xr[kMtGroups], xn[kMtGroups];
-    uint32_t mr[kMtGroups], mn[kMtGroups];
-    float vr[kMtGroups], vn[kMtGroups];
+    // Three register sets (X, mask, exact values of a round) used in rotation by the loop
+    // unrolled by three, so no set is copied while its loads are in flight
+    struct Set {
+        int64_t x[kMtGroups];
+        uint32_t m[kMtGroups];
+        float v[kMtGroups];
+    };
+    Set S0, S1, S2;
     uint32_t ebase = 0;                                          // exact coordinates before the round being slotted
-    auto load_x = [&](uint32_t i0, int64_t* xo) {
+    auto load_x = [&](uint32_t i0, Set& o) {
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const uint32_t i = i0 + 64u * k + lane;
             if (XK == 0) {
                 const auto w = __builtin_amdgcn_raw_buffer_load_b64(rXs, i * 8u, 0, kAuxNT);
-                xo[k] = (int64_t)(((uint64_t)w[1] << 32) | w[0]);
+                o.x[k] = (int64_t)(((uint64_t)w[1] << 32) | w[0]);
             } else if (XK == 1) {
-                xo[k] = __builtin_amdgcn_raw_buffer_load_b8(rXs, i, 0, kAuxNT);
+                o.x[k] = __builtin_amdgcn_raw_buffer_load_b8(rXs, i, 0, kAuxNT);
             } else {
-                xo[k] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rXs, i * 4u, 0, kAuxNT);
+                o.x[k] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rXs, i * 4u, 0, kAuxNT);
             }
         }
     };
-    auto load_m = [&](uint32_t i0, uint32_t* mo) {
+    auto load_m = [&](uint32_t i0, Set& o) {
 #pragma unroll
-        for (int k = 0; k < kMtGroups; ++k) mo[k] = __builtin_amdgcn_raw_buffer_load_b8(rmk, i0 + 64u * k + lane, 0, 0);
+        for (int k = 0; k < kMtGroups; ++k) o.m[k] = __builtin_amdgcn_raw_buffer_load_b8(rmk, i0 + 64u * k + lane, 0, 0);
     };
-    auto load_v = [&](uint32_t i0, const uint32_t* mo, float* vo) {   // the round's exact values (0 elsewhere)
+    auto load_v = [&](uint32_t i0, Set& o) {                     // the round's exact values (0 elsewhere)
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
-            const bool m = mo[k] != 0u && e < kMtN;
+            const bool m = o.m[k] != 0u && e < kMtN;
             uint32_t slot = i0 + (uint32_t)e;
             if (compact) {
                 const uint64_t bal = __ballot(m);
                 slot = ebase + (uint32_t)__popcll(bal & below);
                 ebase += (uint32_t)__popcll(bal);
             }
-            vo[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rvl, qf_off(m, slot * 4u), 0, 0));
+            o.v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rvl, qf_off(m, slot * 4u), 0, 0));
         }
     };
     int32_t flags = 0;
-    load_x(0, xr);
-    load_m(0, mr);
-    load_m(kMtN, mn);
-    load_v(0, mr, vr);
-    for (int64_t c = 0; c < nch; ++c) {
+    // round c: X of c + 1 and the mask of c + 2 loaded, the values of c + 1 slotted from its mask
+    // (loaded a round earlier); then the h stream's block and the outputs of round c
+    auto round = [&](int64_t c, const Set& cur, Set& nx, Set& nx2) {
         const uint32_t i0 = (uint32_t)(c * kMtN);
-        uint32_t m2[kMtGroups];
-        load_x(i0 + kMtN, xn);
-        load_m(i0 + 2u * kMtN, m2);
-        load_v(i0 + kMtN, mn, vn);
+        load_x(i0 + kMtN, nx);
+        load_m(i0 + 2u * kMtN, nx2);
+        load_v(i0 + kMtN, nx);
         mt_twist_reg(sL, lane);
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
@@ -659,18 +656,23 @@ quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const 
             const bool act = e < kMtN && (int64_t)i0 + e < D;
             const uint32_t w = mt_temper(sL[k]);
             const uint32_t h = hpow2 ? (w & (hl - 1u)) : (w % hl);                     // AS:528 randint
-            const int64_t it = (int64_t)((uint64_t)xr[k] * (uint64_t)hl + h);          // AS:530 (int64 arithmetic)
+            const int64_t it = (int64_t)((uint64_t)cur.x[k] * (uint64_t)hl + h);       // AS:530 (int64 arithmetic)
             const bool inr = it >= -(int64_t)tab_n && it < (int64_t)tab_n;
             flags |= (act && !inr) ? UQ_QFL_BAD_INDEX : 0;
             const int32_t idx = inr ? (int32_t)(it < 0 ? it + tab_n : it) : 0;        // take wraps negatives
-            const float v = mr[k] ? vr[k] : (inr ? tab[idx] : 0.f);                   // AS:531
+            const float v = cur.m[k] ? cur.v[k] : (inr ? tab[idx] : 0.f);             // AS:531
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(div1(v, dp)), ro,     // AS:532
                                                   qf_off(e < kMtN, (i0 + (uint32_t)e) * 4u), 0, kAuxNT);
-            xr[k] = xn[k];
-            mr[k] = mn[k];
-            mn[k] = m2[k];
-            vr[k] = vn[k];
         }
+    };
+    load_x(0, S0);
+    load_m(0, S0);
+    load_m(kMtN, S1);
+    load_v(0, S0);
+    for (int64_t c = 0; c < nch; c += 3) {
+        round(c, S0, S1, S2);
+        if (c + 1 < nch) round(c + 1, S1, S2, S0);
+        if (c + 2 < nch) round(c + 2, S2, S0, S1);
     }
     for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
     // AS:531 vec[exact_indeces] = exact_values raises unless the counts agree
