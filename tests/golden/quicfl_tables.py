@@ -45,3 +45,22 @@ def data_txt(b: int, **override) -> str:
     d = dict(DATA[b])
     d.update(override)
     return repr(d)
+
+
+def write_tables(root: str) -> str:
+    """A complete table prefix as QuicFLSender / QuicFLReceiver read it: the synthetic sender
+    tables above, data.txt, and the reference's receiver tables from the committed fixture
+    (quicfl_recv_vectors.npz).  Returns the prefix (root + '/')."""
+    import os
+    import torch
+    os.makedirs(root, exist_ok=True)
+    rz = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "quicfl_recv_vectors.npz"))
+    for b in (1, 2, 3, 4):
+        fn = os.path.join(root, f"{b}_X_{SR_BITS[b]}_h_256_q_")
+        X, p = sender_tables(b)
+        torch.save(torch.from_numpy(X), fn + "sender_table_X.pt")
+        torch.save(torch.from_numpy(p), fn + "sender_table_p.pt")
+        torch.save(torch.from_numpy(rz[f"recv{b}"]), fn + "recv_table.pt")
+        with open(fn + "data.txt", "w") as f:
+            f.write(data_txt(b))
+    return root + "/"

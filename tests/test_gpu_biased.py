@@ -387,3 +387,27 @@ def test_host_check_skips_replay_with_same_bits(uq, d):
     ref = uq.biased_quantize(torch.as_tensor(ties[2:3]).cuda(), m=rate_to_m(1, d), ties="torch")
     assert torch.equal(out.view(torch.int32), ref.view(d).view(torch.int32))
     uq.check_status()
+
+
+@pytest.mark.parametrize("d", [1, 5, 8, 100, 1023, 1024, 2048, 4097, 32767])
+def test_small_vector_single_launch(uq, d):
+    """KB-small (d < GRAIN, one launch): the lowest-index rule for any batch, and torch ties
+    under the host check (the drop-in's policy; an ambiguous row reruns the multi-kernel
+    path), bit-exact with the oracle on smooth, tie-heavy and zero-heavy rows, info pairs
+    included; R = 1 and 4."""
+    rng = np.random.default_rng(d)
+    rows = [rng.standard_normal(d), rng.integers(-3, 4, d), np.where(rng.random(d) < 0.7, 0, rng.standard_normal(d)),
+            rng.laplace(1, 2, d)]
+    x = np.stack(rows).astype(f32)
+    xt = torch.as_tensor(x).cuda()
+    for R in (1, 4):
+        m = rate_to_m(R, d)
+        lo, ilo = uq.biased_quantize(xt, m=m, torch_threads=1, ties="lowest", return_info=True)
+        to, ito = uq.biased_quantize(xt, m=m, torch_threads=1, ties="torch", return_info=True, host_check=True)
+        for j in range(x.shape[0]):
+            for rule, got, info in ((1, lo, ilo), (0, to, ito)):
+                with np.errstate(all="ignore"):
+                    exp, _, D, A = C.biased_quantize(x[j], m, 1, rule)
+                assert int(info[j, 0]) == D and bool(int(info[j, 1]) & 1) == A, (d, R, j, rule)
+                assert G.bits_equal(got[j].cpu().numpy(), exp), (d, R, j, rule)
+    uq.check_status()

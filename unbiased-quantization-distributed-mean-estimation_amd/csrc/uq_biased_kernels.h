@@ -652,3 +652,124 @@ rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t 
             if (e0 + j < d) ov[e0 + j] = q[j];
     }
 }
+
+// KB-small: the whole AS:644-687 for vectors shorter than GRAIN in ONE launch (the reference
+// harness's d = 1024 / 2048 per-vector calls): one 256-thread workgroup per client computes
+// L1 and m' in torch's cascade order (block_torch_sum), Delta, the |Delta|-th largest key by
+// three radix passes over the client's keys held in LDS (dynamic, 4 d bytes), and the outputs.
+// Threshold ties are resolved by the lowest-index rule (index-order ranks: one block scan
+// over contiguous per-thread segments); with UQ_TIES_TORCH an ambiguous client is only flagged
+// (kRezAmbiguous without kRezTorchTies) and the host reruns the multi-kernel path for it.
+// Writes l1buf[vec], st[vec] (delta, flags: the info pair) and out.
+constexpr int64_t kSmallBiasedMax = kGrain - 1;
+__global__ void __launch_bounds__(256)
+biased_small_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, float fm,
+                    const float* __restrict__ l1in, float* __restrict__ l1buf, RezState* __restrict__ st) {
+    extern __shared__ uint32_t keys[];                // [d] keys of the client
+    __shared__ float scr[64 * 32 + 64];
+    __shared__ uint32_t h[kRadixBins];
+    __shared__ uint32_t lds[4];
+    __shared__ uint32_t sel_digit, sel_above, sel_cnt;
+    const int tid = threadIdx.x;
+    const int64_t vec = blockIdx.x;
+    const float* xv = x + vec * d;
+    float* ov = out + vec * d;
+    const float L = l1in ? l1in[vec] : block_torch_sum(xv, d, scr, [](float v) { return fabsf(v); });   // AS:680
+    const DivPlan dp = div_plan(L);
+    const float mprime = block_torch_sum(xv, d, scr, [&](float v) {                                 // AS:648-649
+        return floorf(fm * div1(fabsf(v), dp) + 0.5f);
+    });
+    RezState s{};                                     // KB3 (AS:651-656)
+    s.mprime = mprime;
+    if (!(mprime == fm)) {
+        if (!isfinite(mprime)) {
+            s.flags |= kRezNonFinite;
+        } else {
+            const float df = mprime - fm;
+            const long long D = (long long)df;
+            const long long K = D > 0 ? D : -D;
+            if (K > d) s.flags |= kRezRange;
+            else {
+                s.delta = (int32_t)D;
+                s.kleft = (uint32_t)K;
+            }
+        }
+    }
+    const bool up = s.delta > 0;
+    const bool on = s.kleft != 0;
+    if (on) {                                         // KB4: keys, then the 3 radix digits from the top
+        for (int64_t i = tid; i < d; i += 256) {
+            float kp;
+            keys[i] = rez_elem(xv[i], dp, fm, up, kp);
+        }
+        uint32_t prefix = 0, kleft = s.kleft, eq = 0;
+        auto pass = [&](int shift, uint32_t dmask, uint32_t hmask) {
+            const int nb = (int)dmask + 1;
+            for (int b = tid; b < kRadixBins; b += 256) h[b] = 0u;
+            __syncthreads();
+            for (int64_t i = tid; i < d; i += 256) {
+                const uint32_t k = keys[i];
+                if ((k & hmask) == prefix) atomicAdd(&h[(k >> shift) & dmask], 1u);
+            }
+            __syncthreads();
+            const int per = nb / 256;
+            const int hi = nb - tid * per;            // thread 0 the highest digits
+            uint32_t sum = 0;
+            for (int k = 0; k < per; ++k) sum += h[hi - 1 - k];
+            uint32_t total;
+            uint32_t above = block_excl_scan_u32(sum, lds, &total);
+            if (above < kleft && above + sum >= kleft) {
+                for (int k = 0; k < per; ++k) {
+                    const uint32_t c = h[hi - 1 - k];
+                    if (above + c >= kleft) {
+                        sel_digit = (uint32_t)(hi - 1 - k);
+                        sel_above = above;
+                        sel_cnt = c;
+                        break;
+                    }
+                    above += c;
+                }
+            }
+            __syncthreads();
+            prefix |= sel_digit << shift;
+            kleft -= sel_above;
+            eq = sel_cnt;
+            __syncthreads();
+        };
+        pass(RadixPass<0>::shift, RadixPass<0>::dmask, RadixPass<0>::hmask);
+        pass(RadixPass<1>::shift, RadixPass<1>::dmask, RadixPass<1>::hmask);
+        pass(RadixPass<2>::shift, RadixPass<2>::dmask, RadixPass<2>::hmask);
+        s.prefix = prefix;
+        s.kleft = kleft;
+        s.eq = eq;
+        s.need = kleft;
+        if (eq > kleft) s.flags |= kRezAmbiguous;
+    }
+    const bool amb = on && (s.flags & kRezAmbiguous);
+    const uint32_t tau = s.prefix;
+    const DivPlan dpm = div_plan_m(fm);
+    const float adj = up ? -1.f : 1.f;
+    auto emit = [&](int64_t i, bool sel) {            // KB6 (AS:661/665/687)
+        float kp;
+        (void)rez_elem(xv[i], dp, fm, up, kp);
+        const float k2 = sel ? kp + adj : kp;          // k''
+        ov[i] = (L * torch_signf(xv[i])) * div1(k2, dpm);
+    };
+    if (!amb) {
+        for (int64_t i = tid; i < d; i += 256) emit(i, on && keys[i] >= tau);
+    } else {                                          // lowest indices among the ties
+        const int64_t seg = (d + 255) / 256, b0 = tid * seg, b1 = b0 + seg < d ? b0 + seg : d;
+        uint32_t cnt = 0;
+        for (int64_t i = b0; i < b1; ++i) cnt += keys[i] == tau;
+        uint32_t total;
+        uint32_t rank = block_excl_scan_u32(cnt, lds, &total);
+        for (int64_t i = b0; i < b1; ++i) {
+            const uint32_t k = keys[i];
+            emit(i, k > tau || (k == tau && rank++ < s.need));
+        }
+    }
+    if (tid == 0) {
+        l1buf[vec] = L;
+        st[vec] = s;
+    }
+}

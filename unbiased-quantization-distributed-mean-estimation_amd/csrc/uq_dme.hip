@@ -1374,11 +1374,13 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
                                s_tab, sl);
 }
 
-// torch CPU `x.abs().sum()` of one vector shorter than GRAIN (one cascade, the same for every
+// torch CPU `f(x).sum()` of one vector shorter than GRAIN (one cascade, the same for every
 // torch thread count; K1a + K1b's arithmetic with step 16) by one 256-thread workgroup, into
-// every thread.  scr: >= 64 * 32 + 64 floats of LDS.
+// every thread: f = abs for L1 (AS:624), k' for the biased quantizer's m' (AS:648-649).
+// scr: >= 64 * 32 + 64 floats of LDS.
 constexpr int64_t kSmallL1Max = kGrain - 1;
-__device__ float block_torch_l1(const float* __restrict__ xv, int64_t s, float* scr) {
+template <class F>
+__device__ float block_torch_sum(const float* __restrict__ xv, int64_t s, float* scr, F f) {
     const int tid = threadIdx.x;
     float* leaf = scr;                               // [64 leaves][32 streams]
     float* col = scr + 64 * 32;                      // [32] stream results, then [0] the sum
@@ -1386,8 +1388,8 @@ __device__ float block_torch_l1(const float* __restrict__ xv, int64_t s, float* 
         if (tid == 0) {
             float p[4] = {0.f, 0.f, 0.f, 0.f};
             if (s >= 4)
-                for (int k = 0; k < 4; ++k) p[k] = 0.f + fabsf(xv[k]);
-            for (int64_t k = (s >= 4 ? 4 : 0); k < s; ++k) p[0] += fabsf(xv[k]);
+                for (int k = 0; k < 4; ++k) p[k] = 0.f + f(xv[k]);
+            for (int64_t k = (s >= 4 ? 4 : 0); k < s; ++k) p[0] += f(xv[k]);
             col[0] = 0.0f + (((p[0] + p[1]) + p[2]) + p[3]);
         }
         __syncthreads();
@@ -1403,7 +1405,7 @@ __device__ float block_torch_l1(const float* __restrict__ xv, int64_t s, float* 
         float a[4] = {0.f, 0.f, 0.f, 0.f};
         for (int r = 0; r < 16; ++r)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) a[c] += fabsf(p[r * 32 + c]);
+            for (int c = 0; c < 4; ++c) a[c] += f(p[r * 32 + c]);
 #pragma unroll
         for (int c = 0; c < 4; ++c) leaf[b * 32 + 4 * q + c] = a[c];
     }
@@ -1417,7 +1419,7 @@ __device__ float block_torch_l1(const float* __restrict__ xv, int64_t s, float* 
                 a1 = 0.f;
             }
         }
-        for (int64_t r = (int64_t)nleaf * 16; r < rows; ++r) a0 += fabsf(xv[r * 32 + tid]);
+        for (int64_t r = (int64_t)nleaf * 16; r < rows; ++r) a0 += f(xv[r * 32 + tid]);
         col[tid] = ((a0 + a1) + a2) + 0.f;
     }
     __syncthreads();
@@ -1425,11 +1427,11 @@ __device__ float block_torch_l1(const float* __restrict__ xv, int64_t s, float* 
         float p0[8];
         for (int l = 0; l < 8; ++l) p0[l] = col[l];
         for (int64_t v = rows * 4; v < vs; ++v)
-            for (int l = 0; l < 8; ++l) p0[l] += fabsf(xv[v * 8 + l]);
+            for (int l = 0; l < 8; ++l) p0[l] += f(xv[v * 8 + l]);
         for (int k = 1; k < 4; ++k)
             for (int l = 0; l < 8; ++l) p0[l] += col[k * 8 + l];
         float acc = 0.f;
-        for (int64_t k = vs * 8; k < s; ++k) acc += fabsf(xv[k]);
+        for (int64_t k = vs * 8; k < s; ++k) acc += f(xv[k]);
         for (int l = 0; l < 8; ++l) acc += p0[l];
         col[0] = 0.0f + acc;                         // the two-pass reduction's 0 + chunk
     }
@@ -1437,6 +1439,9 @@ __device__ float block_torch_l1(const float* __restrict__ xv, int64_t s, float* 
     const float r = col[0];
     __syncthreads();
     return r;
+}
+__device__ __forceinline__ float block_torch_l1(const float* __restrict__ xv, int64_t s, float* scr) {
+    return block_torch_sum(xv, s, scr, [](float v) { return fabsf(v); });
 }
 
 // The whole AS:609-641 for vectors shorter than GRAIN in ONE launch (the reference's own
@@ -2491,7 +2496,9 @@ struct SideStream {
     hipStream_t s;
     hipEvent_t fork, join;
     uint32_t* count;            // pinned host word (UQ_TIES_HOST_CHECK reads the tie list's length)
+    void* states;               // pinned host RezStates (the small-vector path's flags), kSmallCheckMaxN
 };
+constexpr int64_t kSmallCheckMaxN = 64;    // clients per host-checked small-vector biased call
 
 int side_stream(SideStream** out) {
     int dev = 0;
@@ -2513,6 +2520,8 @@ int side_stream(SideStream** out) {
         rc = hip_check(hipEventCreateWithFlags(&cache[dev].join, hipEventDisableTiming), "create event");
         if (rc) return rc;
         rc = hip_check(hipHostMalloc((void**)&cache[dev].count, sizeof(uint32_t), hipHostMallocDefault), "pinned word");
+        if (rc) return rc;
+        rc = hip_check(hipHostMalloc(&cache[dev].states, kSmallCheckMaxN * 32, hipHostMallocDefault), "pinned states");
         if (rc) return rc;
         made[dev] = true;
     }
@@ -3164,6 +3173,40 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     float* l1buf = (float*)(wsb + w.l1_off);
     float* msum = (float*)(wsb + w.msum_off);
     RezState* state = (RezState*)(wsb + w.st_off);
+    auto finish = [&]() {                     // l1_out and the info pairs
+        int frc = UQ_OK;
+        if (l1_out) frc = hip_check(hipMemcpyAsync(l1_out, l1buf, n * sizeof(float), hipMemcpyDeviceToDevice, st), "copy l1");
+        if (!frc && info)
+            frc = hip_check(hipMemcpy2DAsync(info, 2 * sizeof(int32_t), state, sizeof(RezState), 2 * sizeof(int32_t), n,
+                                             hipMemcpyDeviceToDevice, st), "copy info");
+        return frc;
+    };
+    // vectors shorter than GRAIN: one launch (KB-small) with the lowest-index rule; with torch
+    // ties only under UQ_TIES_HOST_CHECK, which reads the clients' flags back and runs the
+    // multi-kernel path below when a threshold tie needs torch's choice
+    if (d <= kSmallBiasedMax &&
+        (tie_policy == UQ_TIES_LOWEST_INDEX || (host_check && n <= kSmallCheckMaxN))) {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)biased_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)(kSmallBiasedMax * sizeof(uint32_t)));
+            attr = true;
+        }
+        hipLaunchKernelGGL(biased_small_kernel, dim3((unsigned)n), dim3(256), (size_t)d * sizeof(uint32_t), st, x, out, d,
+                           (float)m, (const float*)nullptr, l1buf, state);
+        int rc = hip_check(hipGetLastError(), "biased_small_kernel launch");
+        if (rc) return rc;
+        if (tie_policy == UQ_TIES_LOWEST_INDEX) return finish();
+        SideStream* sb = nullptr;
+        if ((rc = side_stream(&sb))) return rc;
+        rc = hip_check(hipMemcpyAsync(sb->states, state, (size_t)n * sizeof(RezState), hipMemcpyDeviceToHost, st),
+                       "copy states");
+        if (rc) return rc;
+        if ((rc = hip_check(hipStreamSynchronize(st), "sync"))) return rc;
+        bool tie = false;
+        for (int64_t i = 0; i < n; ++i) tie |= (((const RezState*)sb->states)[i].flags & kRezAmbiguous) != 0;
+        if (!tie) return finish();
+    }
     uint32_t* hist = (uint32_t*)(wsb + w.hist_off);
     uint32_t* tcnt = (uint32_t*)(wsb + w.tcnt_off);
     uint32_t* bits = (uint32_t*)(wsb + w.bits_off);
@@ -3297,14 +3340,7 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         rc = output(st, 0);
         if (rc) return rc;
     }
-    if (l1_out) {
-        rc = hip_check(hipMemcpyAsync(l1_out, l1buf, n * sizeof(float), hipMemcpyDeviceToDevice, st), "copy l1");
-        if (rc) return rc;
-    }
-    if (info)
-        rc = hip_check(hipMemcpy2DAsync(info, 2 * sizeof(int32_t), state, sizeof(RezState), 2 * sizeof(int32_t), n,
-                                        hipMemcpyDeviceToDevice, st), "copy info");
-    return rc;
+    return finish();
 }
 
 // ---- EDEN + RHT ------------------------------------------------------------------------
