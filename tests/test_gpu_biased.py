@@ -406,8 +406,12 @@ def test_small_vector_single_launch(uq, d):
         to, ito = uq.biased_quantize(xt, m=m, torch_threads=1, ties="torch", return_info=True, host_check=True)
         for j in range(x.shape[0]):
             for rule, got, info in ((1, lo, ilo), (0, to, ito)):
-                with np.errstate(all="ignore"):
-                    exp, _, D, A = C.biased_quantize(x[j], m, 1, rule)
+                try:
+                    with np.errstate(all="ignore"):
+                        exp, _, D, A = C.biased_quantize(x[j], m, 1, rule)
+                except (RuntimeError, ValueError):         # the reference raises (AS:656 / AS:660)
+                    assert int(info[j, 1]) & 6, (d, R, j, rule)
+                    continue
                 assert int(info[j, 0]) == D and bool(int(info[j, 1]) & 1) == A, (d, R, j, rule)
                 assert G.bits_equal(got[j].cpu().numpy(), exp), (d, R, j, rule)
     uq.check_status()

@@ -107,3 +107,35 @@ def test_receiver_x_kinds_layouts_and_errors(fx):
     Xb[0, 3] = -rows - 1                             # below -numel for every h
     with pytest.raises(IndexError):
         uqdme.quicfl_decompress(torch.from_numpy(Xb).cuda(), nbits, ps, rs, sc, dim, tab)
+
+
+def test_receiver_team_equals_wave(fx):
+    """A few messages (one workgroup each: the h stream's scout hands the runs their first
+    blocks; compact slots start after the earlier runs' exact coordinates) give the bits the
+    batch kernel (one wave per message) gives, for every X kind and both exact layouts."""
+    import uqdme
+    meta, z = fx
+    rng = np.random.default_rng(21)
+    nbits, n, D = 2, 70, 1 << 15
+    tab = z[f"recv{nbits}"]
+    X = rng.integers(0, tab.shape[0], size=(n, D))
+    mask = rng.random((n, D)) < 0.004
+    dense = np.where(mask, rng.standard_normal((n, D)), 0).astype(np.float32)
+    compact = np.zeros((n, D), np.float32)
+    cnt = mask.sum(1)
+    for j in range(n):
+        compact[j, :cnt[j]] = dense[j][mask[j]]
+    ps = rng.integers(0, 1 << 16, size=n)
+    rs = rng.integers(0, 100, size=n)
+    sc = (rng.random(n) * 3 + 0.5).astype(np.float32)
+    md = torch.from_numpy(mask).cuda()
+    for dt in (torch.uint8, torch.int32, torch.int64):
+        Xd = torch.from_numpy(X).to(dt).cuda()
+        for vals, c in ((dense, None), (compact, cnt)):
+            vd = torch.from_numpy(vals).cuda()
+            full = uqdme.quicfl_decompress(Xd, nbits, ps, rs, sc, D, tab, None, md, vd, c)
+            few = uqdme.quicfl_decompress(Xd[:5], nbits, ps[:5], rs[:5], sc[:5], D, tab, None, md[:5], vd[:5],
+                                          None if c is None else c[:5])
+            assert torch.equal(full[:5].view(torch.int32), few.view(torch.int32)), (dt, c is None)
+    exp = E.quicfl_decompress(X[3], tab, tab.shape[1], int(ps[3]), mask[3], dense[3][mask[3]], sc[3], int(rs[3]), D)
+    assert few[3].cpu().numpy().view(np.uint32).tolist() == exp.view(np.uint32).tolist()

@@ -3367,18 +3367,34 @@ int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, c
     if ((exact_mask == nullptr) != (exact_vals == nullptr)) return fail(UQ_E_INVALID, "exact_mask and exact_vals go together");
     if (h_len < 1 || table_rows < 1 || (int64_t)h_len * table_rows > kQflTab)
         return fail(UQ_E_INVALID, "receiver table must hold 1..1024 entries");
-    const dim3 grid((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)), block(64 * kQfWavesPerWG);
     hipStream_t st = (hipStream_t)stream;
-    const int tn = table_rows * h_len;
-    if (x_kind == 0)
-        hipLaunchKernelGGL(quicfl_recv_wave_kernel<0>, grid, block, 0, st, X, n, D, recv_table, tn, h_len, prng_seeds,
-                           exact_mask, exact_vals, exact_layout, exact_count, scale, out, info);
-    else if (x_kind == 1)
-        hipLaunchKernelGGL(quicfl_recv_wave_kernel<1>, grid, block, 0, st, X, n, D, recv_table, tn, h_len, prng_seeds,
-                           exact_mask, exact_vals, exact_layout, exact_count, scale, out, info);
-    else
-        hipLaunchKernelGGL(quicfl_recv_wave_kernel<2>, grid, block, 0, st, X, n, D, recv_table, tn, h_len, prng_seeds,
-                           exact_mask, exact_vals, exact_layout, exact_count, scale, out, info);
+    QflRecvArgs r{};
+    r.X = X;
+    r.n = n;
+    r.D = D;
+    r.table = recv_table;
+    r.tab_n = table_rows * h_len;
+    r.h_len = h_len;
+    r.prng_seeds = prng_seeds;
+    r.exact_mask = exact_mask;
+    r.exact_vals = exact_vals;
+    r.compact = exact_layout;
+    r.exact_count = exact_count;
+    r.scale = scale;
+    r.out = out;
+    r.info = info;
+    // few messages: a workgroup per message (the h stream's scout + 7 runs); batches: a wave each
+    if (n <= kQfTeamMaxN && D >= (int64_t)kMtN * kQrRuns && D <= kQfTeamMaxD) {
+        const dim3 grid((unsigned)n), block(64 * kQfTeamWaves);
+        if (x_kind == 0) hipLaunchKernelGGL(quicfl_recv_team_kernel<0>, grid, block, 0, st, r);
+        else if (x_kind == 1) hipLaunchKernelGGL(quicfl_recv_team_kernel<1>, grid, block, 0, st, r);
+        else hipLaunchKernelGGL(quicfl_recv_team_kernel<2>, grid, block, 0, st, r);
+        return hip_check(hipGetLastError(), "quicfl_recv_team_kernel launch");
+    }
+    const dim3 grid((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)), block(64 * kQfWavesPerWG);
+    if (x_kind == 0) hipLaunchKernelGGL(quicfl_recv_wave_kernel<0>, grid, block, 0, st, r);
+    else if (x_kind == 1) hipLaunchKernelGGL(quicfl_recv_wave_kernel<1>, grid, block, 0, st, r);
+    else hipLaunchKernelGGL(quicfl_recv_wave_kernel<2>, grid, block, 0, st, r);
     return hip_check(hipGetLastError(), "quicfl_recv_wave_kernel launch");
 }
 

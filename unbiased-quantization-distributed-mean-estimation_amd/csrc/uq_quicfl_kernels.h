@@ -566,39 +566,44 @@ quicfl_send_team_kernel(QflSendArgs a) {
 // X one round, the mask two rounds (its ballots give the next round's value slots, whose loads
 // are then one round ahead too).
 constexpr int kQflTab = 1024;
+struct QflRecvArgs {
+    const void* X;                  // [n][D] int64 / uint8 / int32 (XK)
+    int64_t n, D;
+    const float* table;             // [tab_n] receiver table
+    int32_t tab_n, h_len;
+    const int32_t* prng_seeds;
+    const uint8_t* exact_mask;      // [n][D] or null
+    const float* exact_vals;        // [n][D] dense or compact, or null
+    int compact;
+    const int32_t* exact_count;     // [n] or null (compact: checked against the mask)
+    const float* scale;             // [n]
+    float* out;                     // [n][D]
+    int32_t* info;                  // [n] or null
+};
+
+// Rounds [c0, c1) of message j's receiver (AS:526-532): s holds the h stream's block c0 on
+// entry; ebase = the message's exact coordinates before round c0 (compact layout).  Returns
+// UQ_QFL_* flags; *eend = the exact count through the rounds slotted.
 template <int XK>
-__global__ void __launch_bounds__(64 * kQfWavesPerWG)
-quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const float* __restrict__ table,
-                        int32_t tab_n, int32_t h_len, const int32_t* __restrict__ prng_seeds,
-                        const uint8_t* __restrict__ exact_mask, const float* __restrict__ exact_vals, int compact,
-                        const int32_t* __restrict__ exact_count, const float* __restrict__ scale,
-                        float* __restrict__ out, int32_t* __restrict__ info) {
-    __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];                // seed scratch per wave
-    __shared__ float tab[kQflTab];
-    for (int i = threadIdx.x; i < tab_n; i += 64 * kQfWavesPerWG) tab[i] = table[i];
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
-    if (j >= n) return;
-    uint32_t* Ls = Lsh[wv];
-    if (lane == 0) mt_seed(Ls, (uint32_t)prng_seeds[j]);
-    wave_lds_fence();
-    uint32_t sL[kMtGroups];                                      // the h stream's block in registers
-    mt_load(sL, Ls, lane);
+__device__ __forceinline__ int32_t qfl_recv_rounds(const QflRecvArgs& a, const float* tab, int64_t j,
+                                                   uint32_t (&sL)[kMtGroups], int64_t c0, int64_t c1, uint32_t ebase,
+                                                   uint32_t* eend, int lane) {
+    const int64_t D = a.D;
     const int64_t row = j * D;
     const uint32_t Du = (uint32_t)D;
-    const DivPlan dp = div_plan_norm(scale[j]);                 // v / scale (AS:532): exact quotient
-    const uint32_t hl = (uint32_t)h_len;
+    const DivPlan dp = div_plan_norm(a.scale[j]);               // v / scale (AS:532): exact quotient
+    const uint32_t hl = (uint32_t)a.h_len;
+    const int32_t tab_n = a.tab_n;
     const bool hpow2 = (hl & (hl - 1)) == 0;
-    const int64_t nch = (D + kMtN - 1) / kMtN;
+    const bool compact = a.compact != 0;
     constexpr uint32_t xb = XK == 0 ? 8u : (XK == 1 ? 1u : 4u);  // bytes per X
     // buffer descriptors: branch-free loads (0 beyond D) and stores (dropped beyond D)
-    const __amdgpu_buffer_rsrc_t rXs = make_rsrc((const char*)X + row * xb, Du * xb);
-    const __amdgpu_buffer_rsrc_t rmk = make_rsrc(exact_mask ? (const void*)(exact_mask + row) : X,
-                                                 exact_mask ? Du : 0u);
-    const __amdgpu_buffer_rsrc_t rvl = make_rsrc(exact_vals ? (const void*)(exact_vals + row) : X,
-                                                 exact_vals ? Du * 4u : 0u);
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(out + row, Du * 4u);
+    const __amdgpu_buffer_rsrc_t rXs = make_rsrc((const char*)a.X + row * xb, Du * xb);
+    const __amdgpu_buffer_rsrc_t rmk = make_rsrc(a.exact_mask ? (const void*)(a.exact_mask + row) : a.X,
+                                                 a.exact_mask ? Du : 0u);
+    const __amdgpu_buffer_rsrc_t rvl = make_rsrc(a.exact_vals ? (const void*)(a.exact_vals + row) : a.X,
+                                                 a.exact_vals ? Du * 4u : 0u);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + row, Du * 4u);
     const uint64_t below = (1ull << lane) - 1ull;
     // Three register sets (X, mask, exact values of a round) used in rotation by the loop
     // unrolled by three, so no set is copied while its loads are in flight
@@ -608,7 +613,6 @@ quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const 
         float v[kMtGroups];
     };
     Set S0, S1, S2;
-    uint32_t ebase = 0;                                          // exact coordinates before the round being slotted
     auto load_x = [&](uint32_t i0, Set& o) {
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
@@ -648,7 +652,7 @@ quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const 
         const uint32_t i0 = (uint32_t)(c * kMtN);
         load_x(i0 + kMtN, nx);
         load_m(i0 + 2u * kMtN, nx2);
-        load_v(i0 + kMtN, nx);
+        if (c + 1 < c1) load_v(i0 + kMtN, nx);
         mt_twist_reg(sL, lane);
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
@@ -665,17 +669,120 @@ quicfl_recv_wave_kernel(const void* __restrict__ X, int64_t n, int64_t D, const 
                                                   qf_off(e < kMtN, (i0 + (uint32_t)e) * 4u), 0, kAuxNT);
         }
     };
-    load_x(0, S0);
-    load_m(0, S0);
-    load_m(kMtN, S1);
-    load_v(0, S0);
-    for (int64_t c = 0; c < nch; c += 3) {
+    const uint32_t b0 = (uint32_t)(c0 * kMtN);
+    load_x(b0, S0);
+    load_m(b0, S0);
+    load_m(b0 + kMtN, S1);
+    load_v(b0, S0);
+    for (int64_t c = c0; c < c1; c += 3) {
         round(c, S0, S1, S2);
-        if (c + 1 < nch) round(c + 1, S1, S2, S0);
-        if (c + 2 < nch) round(c + 2, S2, S0, S1);
+        if (c + 1 < c1) round(c + 1, S1, S2, S0);
+        if (c + 2 < c1) round(c + 2, S2, S0, S1);
     }
+    *eend = ebase;
+    return flags;
+}
+
+// KQ2 for batches: one wave per message, the table (<= 1024 floats) in LDS for the
+// workgroup's waves.
+template <int XK>
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_recv_wave_kernel(QflRecvArgs a) {
+    __shared__ uint32_t Lsh[kQfWavesPerWG][kMtN];                // seed scratch per wave
+    __shared__ float tab[kQflTab];
+    for (int i = threadIdx.x; i < a.tab_n; i += 64 * kQfWavesPerWG) tab[i] = a.table[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    if (j >= a.n) return;
+    uint32_t* Ls = Lsh[wv];
+    if (lane == 0) mt_seed(Ls, (uint32_t)a.prng_seeds[j]);
+    wave_lds_fence();
+    uint32_t sL[kMtGroups];                                      // the h stream's block in registers
+    mt_load(sL, Ls, lane);
+    uint32_t etot = 0;
+    int32_t flags = qfl_recv_rounds<XK>(a, tab, j, sL, 0, (a.D + kMtN - 1) / kMtN, 0u, &etot, lane);
     for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
     // AS:531 vec[exact_indeces] = exact_values raises unless the counts agree
-    if (compact && exact_count && (int64_t)ebase != (int64_t)exact_count[j]) flags |= UQ_QFL_BAD_EXACT;
-    if (info && lane == 0) info[j] = flags;
+    if (a.compact && a.exact_count && (int64_t)etot != (int64_t)a.exact_count[j]) flags |= UQ_QFL_BAD_EXACT;
+    if (a.info && lane == 0) a.info[j] = flags;
+}
+
+// KQ2t for a few messages (the drop-in): one 512-thread workgroup per message.  The runs
+// first count the exact coordinates of their rounds (their compact slots start after the
+// earlier runs'), then wave 0 twists the h stream from its seed and hands each of the 7 runs
+// its first block (as the sender's scouts do); the runs twist onward from there.
+constexpr int kQrRuns = kQfTeamWaves - 1;
+template <int XK>
+__global__ void __launch_bounds__(64 * kQfTeamWaves)
+quicfl_recv_team_kernel(QflRecvArgs a) {
+    __shared__ float tab[kQflTab];
+    __shared__ uint32_t SA[kQrRuns][kMtN];
+    __shared__ uint32_t seed[kMtN];
+    __shared__ uint32_t ecnt[kQrRuns];
+    __shared__ int rdy[kQrRuns];
+    __shared__ int32_t sflags;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = blockIdx.x;
+    const int64_t nch = (a.D + kMtN - 1) / kMtN;
+    const int64_t per = (nch + kQrRuns - 1) / kQrRuns;
+    for (int i = threadIdx.x; i < a.tab_n; i += 64 * kQfTeamWaves) tab[i] = a.table[i];
+    if (threadIdx.x < kQrRuns) rdy[threadIdx.x] = 0;
+    if (threadIdx.x == 0) sflags = 0;
+    if (wv == 0) {
+        if (lane == 0) mt_seed(seed, (uint32_t)a.prng_seeds[j]);
+    } else {                                             // run r's exact coordinates (compact slots)
+        const int r = wv - 1;
+        const int64_t c0 = r * per, c1 = min(nch, c0 + per);
+        uint32_t cnt = 0;
+        if (a.compact && a.exact_mask) {
+            const uint8_t* mk = a.exact_mask + j * a.D;
+            const int64_t e1 = min(a.D, c1 * kMtN);
+            for (int64_t i = c0 * kMtN + lane; i < e1; i += 64) cnt += mk[i] != 0;
+            for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+        }
+        if (lane == 0) ecnt[r] = cnt;
+    }
+    __syncthreads();
+    int32_t flags = 0;
+    if (wv == 0) {                                       // the scout: blocks 0 .. start of the last run
+        __builtin_amdgcn_s_setprio(3);
+        uint32_t s[kMtGroups];
+        mt_load(s, seed, lane);
+        int64_t last = 0;
+        for (int r = 0; r < kQrRuns; ++r)
+            if (r * per < nch) last = r * per;
+        for (int64_t k = 0; k <= last; ++k) {
+            if (k) mt_twist_reg(s, lane);
+            if (k % per == 0) {
+                mt_store(s, SA[k / per], lane);
+                wave_lds_fence();
+                if (lane == 0) __hip_atomic_store(&rdy[k / per], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    } else {
+        const int r = wv - 1;
+        const int64_t c0 = r * per, c1 = min(nch, c0 + per);
+        if (c0 < c1) {
+            if (qfl_wait_flag(&rdy[r])) {
+                uint32_t s[kMtGroups];
+                mt_load(s, SA[r], lane);
+                uint32_t base = 0, eend = 0;
+                for (int q = 0; q < r; ++q) base += ecnt[q];
+                flags = qfl_recv_rounds<XK>(a, tab, j, s, c0, c1, base, &eend, lane);
+            } else {
+                flags = UQ_QFL_TIMEOUT;
+            }
+        }
+        for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
+        if (lane == 0 && flags) atomicOr(&sflags, flags);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && a.info) {
+        int32_t f = sflags;
+        uint32_t tot = 0;
+        for (int q = 0; q < kQrRuns; ++q) tot += ecnt[q];
+        if (a.compact && a.exact_count && (int64_t)tot != (int64_t)a.exact_count[j]) f |= UQ_QFL_BAD_EXACT;
+        a.info[j] = f;
+    }
 }
