@@ -201,6 +201,39 @@ __device__ __forceinline__ float div1(float x, const DivPlan& dp) {
     if (__builtin_expect(!(fabsf(q) >= dp.thr) && x != 0.0f, 0)) q = x / dp.den;
     return q;
 }
+// N quotients with div1's bits and no per-element branch: the Markstein steps on pairs
+// (packed fma), one guard test over the lane's N elements and a wave-uniform branch into the
+// IEEE division for the rare lane that needs it.  Elements whose bit is set in `skip` are
+// left out of the guard (their quotient is discarded by the caller).
+template <int N>
+__device__ __forceinline__ void div_n(const float (&xs)[N], const DivPlan& dp, float (&vs)[N], uint32_t skip = 0u) {
+    static_assert(N % 2 == 0, "pairs");
+    if (dp.fast) {
+        const f32x2 Y = {dp.y, dp.y}, B = {-dp.den, -dp.den};
+#pragma unroll
+        for (int h = 0; h < N / 2; ++h) {
+            const f32x2 a = {xs[2 * h], xs[2 * h + 1]};
+            f32x2 q = a * Y;
+            f32x2 r = __builtin_elementwise_fma(B, q, a);
+            q = __builtin_elementwise_fma(r, Y, q);
+            r = __builtin_elementwise_fma(B, q, a);
+            q = __builtin_elementwise_fma(r, Y, q);
+            vs[2 * h] = q.x;
+            vs[2 * h + 1] = q.y;
+        }
+        bool bad = false;
+#pragma unroll
+        for (int c = 0; c < N; ++c) bad |= !(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f && !((skip >> c) & 1u);
+        if (__builtin_expect(__ballot(bad) != 0ull, 0)) {
+#pragma unroll
+            for (int c = 0; c < N; ++c)
+                if (!(fabsf(vs[c]) >= dp.thr) && xs[c] != 0.0f) vs[c] = xs[c] / dp.den;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < N; ++c) vs[c] = xs[c] / dp.den;
+    }
+}
 // RN(k / m) for the dequantize step (m >= 1 is exact in f32 up to 2^24 and below 2^40
 // always): the same Markstein sequence with den = m itself (no 1e-12 term).
 __device__ __forceinline__ DivPlan div_plan_m(float fm) {

@@ -310,6 +310,16 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
         const int bL = (int)(((c.qL + rd) & 1) * kMtN) + c.rL, bG = (int)(((c.qG + rd) & 1) * kMtN) + c.rG;
         cr.ex = 0;
         cr.act = 0;
+        // AS:472-481: v, the exact mask, q = v / delta for the lane's ten elements at once
+        // (exact elements' quotients are discarded, so they stay out of the division's guard)
+        float vv[kMtGroups], qq[kMtGroups];
+        uint32_t exm = 0;
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            vv[k] = cur.r[k] * c.sc;                                  // AS:472
+            exm |= ((vv[k] > thr) || (vv[k] < -thr) ? 1u : 0u) << k;  // AS:478
+        }
+        div_n(vv, c.dp, qq, exm);
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
@@ -321,9 +331,9 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             // flags and store nothing
             const bool active = e < kMtN && (int64_t)i0 + e < D;
             cr.wg[k] = mt_temper(wg);
-            const float v = cur.r[k] * c.sc;                          // AS:472
-            const bool ex = (v > thr) || (v < -thr);                  // AS:478
-            const float q = ex ? 0.f : div1(v, c.dp);                 // AS:480-481 (= v / delta)
+            const float v = vv[k];
+            const bool ex = (exm >> k) & 1u;
+            const float q = ex ? 0.f : qq[k];                         // AS:480-481 (= v / delta), q[exact] = 0
             const float fl = floorf(q);
             const float p = q - fl;                                   // AS:483
             flags |= (active && !(p >= 0.f && p <= 1.f)) ? UQ_QFL_BAD_P : 0;
@@ -654,6 +664,7 @@ __device__ __forceinline__ int32_t qfl_recv_rounds(const QflRecvArgs& a, const f
         load_m(i0 + 2u * kMtN, nx2);
         if (c + 1 < c1) load_v(i0 + kMtN, nx);
         mt_twist_reg(sL, lane);
+        float vv[kMtGroups], qq[kMtGroups];
 #pragma unroll
         for (int k = 0; k < kMtGroups; ++k) {
             const int e = 64 * k + lane;
@@ -664,9 +675,14 @@ __device__ __forceinline__ int32_t qfl_recv_rounds(const QflRecvArgs& a, const f
             const bool inr = it >= -(int64_t)tab_n && it < (int64_t)tab_n;
             flags |= (act && !inr) ? UQ_QFL_BAD_INDEX : 0;
             const int32_t idx = inr ? (int32_t)(it < 0 ? it + tab_n : it) : 0;        // take wraps negatives
-            const float v = cur.m[k] ? cur.v[k] : (inr ? tab[idx] : 0.f);             // AS:531
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(div1(v, dp)), ro,     // AS:532
-                                                  qf_off(e < kMtN, (i0 + (uint32_t)e) * 4u), 0, kAuxNT);
+            vv[k] = cur.m[k] ? cur.v[k] : (inr ? tab[idx] : 0.f);                      // AS:531
+        }
+        div_n(vv, dp, qq);                                                              // AS:532 v / scale
+#pragma unroll
+        for (int k = 0; k < kMtGroups; ++k) {
+            const int e = 64 * k + lane;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(qq[k]), ro, qf_off(e < kMtN, (i0 + (uint32_t)e) * 4u), 0,
+                                                  kAuxNT);
         }
     };
     const uint32_t b0 = (uint32_t)(c0 * kMtN);
