@@ -2181,8 +2181,6 @@ codes_mean_kernel(const int8_t* __restrict__ codes, int64_t ldc, const float* __
 thread_local std::string g_err;
 // test hook (uq_test_force_replay_failure): every torch-tie replay takes its failure path
 std::atomic<int> g_force_replay_failure{0};
-// test hook (uq_test_quicfl_one_wave): batches take the one-wave-per-message sender
-std::atomic<int> g_qfl_one_wave{0};
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -2718,8 +2716,6 @@ int uq_version(void) { return 102; }
 const char* uq_build_id(void) { return UQ_BUILD_ID; }
 
 int uq_test_force_replay_failure(int on) { return g_force_replay_failure.exchange(on ? 1 : 0); }
-
-int uq_test_quicfl_one_wave(int on) { return g_qfl_one_wave.exchange(on ? 1 : 0); }
 
 const char* uq_last_error(void) { return g_err.c_str(); }
 
@@ -3710,18 +3706,6 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
         else
             hipLaunchKernelGGL(quicfl_send_team_kernel<1>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
         return hip_check(hipGetLastError(), "quicfl_send_team_kernel launch");
-    }
-    // batches: three waves per message (a stream each) while the L stream's lead-in (D words of
-    // twisting before its first block) stays far inside the rings' bounded waits; a wave per
-    // message beyond that
-    if (w.D <= kTriMaxD && !g_qfl_one_wave.load()) {
-        const dim3 tgrid((unsigned)((n + kTriMsgs - 1) / kTriMsgs));
-        if (x_kind == 0) hipLaunchKernelGGL(quicfl_send_tri_kernel<0>, tgrid, dim3(64 * 3 * kTriMsgs), 0, st, q);
-        else hipLaunchKernelGGL(quicfl_send_tri_kernel<1>, tgrid, dim3(64 * 3 * kTriMsgs), 0, st, q);
-        if ((rc = hip_check(hipGetLastError(), "quicfl_send_tri_kernel launch"))) return rc;
-        hipLaunchKernelGGL(quicfl_exact_compact_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, exact_mask,
-                           exact_vals, exact_count, n, w.D);
-        return hip_check(hipGetLastError(), "quicfl_exact_compact_kernel launch");
     }
     const dim3 grid((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG));
     if (x_kind == 0)

@@ -802,292 +802,3 @@ quicfl_recv_team_kernel(QflRecvArgs a) {
         a.info[j] = f;
     }
 }
-
-// ---- KQ1x: the sender for batches, three waves per message -------------------------------
-// One wave per message leaves the SIMD idle more than half the time (VALU busy 42 %,
-// profiles/r4j_quicfl_sq_counters.json): the message's work is the per-coordinate arithmetic
-// behind three serial streams.  Here each of a message's three waves twists ONE stream -- H
-// (the local generator's first D words: h, AS:465/469), L (its next D words: bernoulli(p),
-// AS:484; the wave first twists through the H half) or G (the global generator, AS:489) --
-// and publishes its tempered blocks into an LDS ring; all three then take a third of every
-// round's coordinates (register groups g = w, w + 3, w + 6, w + 9) with the words of all three
-// rings.  Published and consumed counters per stream / wave order the rings (bounded waits:
-// UQ_QFL_TIMEOUT, and the wave stops, if one ever ran out).  No h scratch in HBM; exact values
-// go to their coordinate and quicfl_exact_compact_kernel moves them into index order.
-constexpr int kTriMsgs = 2;                 // messages per workgroup (6 waves)
-constexpr int kTriK = 4;                    // ring blocks per stream
-constexpr int kTriG = 4;                    // register groups per wave (10 over 3 waves: 4, 3, 3)
-constexpr int64_t kTriMaxD = (int64_t)1 << 24;  // the L stream's lead-in: 2^24 / 624 twists, ~16 ms
-__device__ __forceinline__ bool tri_wait_ge(int* f, int v) {
-    for (int it = 0; it < (1 << 22); ++it) {
-        if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) return true;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-
-template <int XK>
-__global__ void __launch_bounds__(64 * 3 * kTriMsgs) __attribute__((amdgpu_waves_per_eu(3)))   // 2 workgroups per CU
-quicfl_send_tri_kernel(QflSendArgs a) {
-    __shared__ uint32_t ring[kTriMsgs][3][kTriK * kMtN];       // tempered words of H, L, G
-    __shared__ int pub[kTriMsgs][3];                            // H: rounds available; L, G: blocks published (+1)
-    __shared__ int done[kTriMsgs][3];                           // rounds whose words wave w has read
-    __shared__ int32_t sflags[kTriMsgs];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int mi = wv / 3, role = wv % 3;
-    const int64_t j = (int64_t)blockIdx.x * kTriMsgs + mi;
-    if (threadIdx.x < kTriMsgs * 3) {
-        (&pub[0][0])[threadIdx.x] = 0;
-        (&done[0][0])[threadIdx.x] = 0;
-    }
-    if (threadIdx.x < kTriMsgs) sflags[threadIdx.x] = 0;
-    __syncthreads();
-    const bool live = j < a.n;
-    int32_t flags = 0;
-    if (live) {
-        uint32_t* R = ring[mi][role];
-        int* pubm = pub[mi];
-        int* donem = done[mi];
-        int32_t gleft = a.px_state ? (int32_t)a.px_state[j * kQfStateWords] : 1;
-        int32_t gnext = a.px_state ? (int32_t)a.px_state[j * kQfStateWords + 1] : 0;
-        uint32_t s[kMtGroups];                                  // this wave's stream
-        if (role == 2) {
-            qfl_gen_init(a, j, s, R, gleft, gnext, lane);       // (R as the seed scratch)
-        } else {
-            if (lane == 0) mt_seed(R, (uint32_t)a.prng_seeds[j]);
-            wave_lds_fence();
-            mt_load(s, R, lane);
-        }
-        wave_lds_fence();
-        const QflCtx c = qfl_ctx<XK>(a, j, gleft, gnext);
-        const int64_t D = c.D;
-        const int64_t nch = (D + kMtN - 1) / kMtN;
-        const int lastE_end = (int)((D - 1) - (nch - 1) * kMtN);          // last element of the last round
-        // blocks of a stream: H block t + 1 serves round t; L / G blocks qX + t (+ 1 when the
-        // round crosses the block end) serve round t
-        const int64_t qX = role == 1 ? c.qL : c.qG;
-        const int rX = role == 1 ? c.rL : c.rG;
-        int64_t have = 0;                                       // blocks twisted (this wave's stream)
-        int64_t npub = 0;                                       // next block index to publish
-        int64_t last_blk;                                       // last block the stream publishes
-        if (role == 0) {
-            have = 0;
-            npub = 1;
-            last_blk = nch;
-        } else {
-            npub = qX;
-            last_blk = qX + nch - 1 + (rX + lastE_end >= kMtN ? 1 : 0);
-            if (role == 1)                                      // twist through the H half first
-                while (have < qX) { mt_twist_reg(s, lane); ++have; }
-        }
-        bool ok = true;
-        // publish the blocks rounds <= tmax need
-        auto produce = [&](int64_t tmax) {
-            int64_t target = role == 0 ? tmax + 1 : qX + tmax + 1;     // (+1 for a crossing round)
-            if (target > last_blk) target = last_blk;
-            while (ok && npub <= target) {
-                // the slot's previous block (npub - K) must be read by every wave: H's by round
-                // npub - K - 1, L / G's by round npub - K - qX (the later of its two rounds)
-                const int64_t need_done = role == 0 ? npub - kTriK : npub - kTriK - qX + 1;
-                if (need_done > 0)
-                    for (int w = 0; w < 3 && ok; ++w) ok = tri_wait_ge(&donem[w], (int)need_done);
-                if (!ok) break;
-                while (have < npub) { mt_twist_reg(s, lane); ++have; }
-                uint32_t* dst = R + (int)(npub % kTriK) * kMtN;
-#pragma unroll
-                for (int g = 0; g < kMtGroups; ++g) {
-                    const int i = 64 * g + lane;
-                    if (i < kMtN) dst[i] = mt_temper(s[g]);
-                }
-                wave_lds_fence();
-                ++npub;
-                if (lane == 0)
-                    __hip_atomic_store(&pubm[role], (int)npub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        };
-        // this wave's groups
-        int ng = 0;
-        int grp[kTriG];
-#pragma unroll
-        for (int q = 0; q < kTriG; ++q) {
-            const int g = role + 3 * q;
-            grp[q] = g < kMtGroups ? g : -1;
-            ng += g < kMtGroups ? 1 : 0;
-        }
-        const float thr = kQflExactT;
-        struct In {
-            float r[kTriG];
-        };
-        struct Rd {
-            uint32_t t[kTriG][2];
-            uint32_t wg[kTriG];
-            float v[kTriG];
-            uint32_t ex, act;
-        };
-        In I0, I1;
-        Rd R0, R1;
-        auto load_in = [&](uint32_t i0, In& o) {
-#pragma unroll
-            for (int q = 0; q < kTriG; ++q) {
-                const uint32_t e = i0 + 64u * (uint32_t)(grp[q] < 0 ? 0 : grp[q]) + lane;
-                o.r[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.rr, qf_off(grp[q] >= 0, e * 4u), 0,
-                                                                              kAuxNT));
-            }
-        };
-        auto finish = [&](const Rd& r, uint32_t i0) {           // AS:489-490, 494-495
-#pragma unroll
-            for (int q = 0; q < kTriG; ++q) {
-                const uint32_t i = i0 + 64u * (uint32_t)(grp[q] < 0 ? 0 : grp[q]) + lane;
-                const bool active = (r.act >> q) & 1u;
-                const bool ex = (r.ex >> q) & 1u;
-                const float tx = __uint_as_float(r.t[q][0]), tp = __uint_as_float(r.t[q][1]);
-                flags |= (active && !(tp >= 0.f && tp <= 1.f)) ? UQ_QFL_BAD_PX : 0;
-                const float bx = (u24(r.wg[q]) < tp) ? 1.f : 0.f;
-                const float xf = tx + bx;                                // AS:489
-                if (XK == 0) {
-                    const bool okx = xf > -9.2e18f && xf < 9.2e18f;
-                    flags |= (active && !okx) ? UQ_QFL_X_RANGE : 0;
-                    const int64_t xv = okx ? (int64_t)xf : 0;            // AS:490 .long()
-                    typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-                    const u32x2v w = {(uint32_t)xv, (uint32_t)((uint64_t)xv >> 32)};
-                    __builtin_amdgcn_raw_buffer_store_b64(w, c.rX, qf_off(active, i * 8u), 0, kAuxNT);
-                } else {
-                    const bool okx = xf > -1.0f && xf < 256.0f;
-                    flags |= (active && !okx) ? UQ_QFL_X_RANGE : 0;
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(okx ? (int32_t)xf : 0), c.rX, qf_off(active, i), 0, 0);
-                }
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ex ? 1 : 0), c.rm, qf_off(active, i), 0, 0);
-                if (active && ex) a.ev[c.row + i] = r.v[q];            // at its coordinate (compacted later)
-            }
-        };
-        const uint32_t* RH = ring[mi][0];
-        const uint32_t* RL = ring[mi][1];
-        const uint32_t* RG = ring[mi][2];
-        auto round = [&](int64_t t, const In& cur, In& nxt, Rd& cr, const Rd& pr, bool fin) {
-            const uint32_t i0 = (uint32_t)(t * kMtN);
-            const int lastE = (int)((D - 1 - (int64_t)i0) < (kMtN - 1) ? (D - 1 - (int64_t)i0) : (kMtN - 1));
-            load_in(i0 + (uint32_t)kMtN, nxt);
-            produce(t + 1);                                      // this wave's stream, one round ahead
-            if (ok) ok = tri_wait_ge(&pubm[0], (int)(t + 2));
-            if (ok) ok = tri_wait_ge(&pubm[1], (int)(c.qL + t + 1 + (c.rL + lastE >= kMtN ? 1 : 0)));
-            if (ok) ok = tri_wait_ge(&pubm[2], (int)(c.qG + t + 1 + (c.rG + lastE >= kMtN ? 1 : 0)));
-            if (!ok) return;
-            const int bH = (int)(((t + 1) % kTriK) * kMtN);
-            const int bL = (int)(((c.qL + t) % kTriK) * kMtN) + c.rL, bG = (int)(((c.qG + t) % kTriK) * kMtN) + c.rG;
-            uint32_t wh[kTriG], wl[kTriG], wg[kTriG];
-#pragma unroll
-            for (int q = 0; q < kTriG; ++q) {
-                const int e0 = 64 * (grp[q] < 0 ? 0 : grp[q]) + lane;
-                const int e = e0 < kMtN ? e0 : 0;
-                const int pl = bL + e, pg = bG + e;
-                wh[q] = RH[bH + e];
-                wl[q] = RL[pl >= kTriK * kMtN ? pl - kTriK * kMtN : pl];
-                wg[q] = RG[pg >= kTriK * kMtN ? pg - kTriK * kMtN : pg];
-            }
-            wave_lds_fence();                                    // (the reads complete before done)
-            if (lane == 0) __hip_atomic_store(&donem[role], (int)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            float vv[kTriG], qq[kTriG];
-            uint32_t exm = 0;
-#pragma unroll
-            for (int q = 0; q < kTriG; ++q) {
-                vv[q] = cur.r[q] * c.sc;                               // AS:472
-                exm |= ((vv[q] > thr) || (vv[q] < -thr) ? 1u : 0u) << q;   // AS:478
-            }
-            div_n(vv, c.dp, qq, exm);
-            cr.ex = 0;
-            cr.act = 0;
-#pragma unroll
-            for (int q = 0; q < kTriG; ++q) {
-                const int e = 64 * (grp[q] < 0 ? 0 : grp[q]) + lane;
-                const bool active = grp[q] >= 0 && e < kMtN && (int64_t)i0 + e < D;
-                const uint32_t h = c.hpow2 ? (wh[q] & (c.h_len - 1u)) : (wh[q] % c.h_len);   // AS:465/469
-                cr.wg[q] = wg[q];
-                const bool ex = (exm >> q) & 1u;
-                const float qv = ex ? 0.f : qq[q];                       // AS:480-481
-                const float fl = floorf(qv);
-                const float p = qv - fl;                                 // AS:483
-                flags |= (active && !(p >= 0.f && p <= 1.f)) ? UQ_QFL_BAD_P : 0;
-                const float bern = (u24(wl[q]) < p) ? 1.f : 0.f;
-                const float iq = fl + bern;                              // AS:484
-                const float t1 = iq * c.fh;                              // AS:486 in f32
-                const float t2 = t1 + (float)h;
-                const float it = truncf(t2 + c.fhalf);
-                const bool inr = it >= -c.fnumel && it < c.fnumel;
-                flags |= (active && !inr) ? UQ_QFL_BAD_INDEX : 0;
-                int32_t idx = inr ? (int32_t)it : 0;
-                idx = idx < 0 ? idx + c.numel : idx;
-                const auto tt = __builtin_amdgcn_raw_buffer_load_b64(c.rt, (uint32_t)idx * 8u, 0, 0);   // AS:486-487
-                cr.t[q][0] = tt[0];
-                cr.t[q][1] = tt[1];
-                cr.v[q] = vv[q];
-                cr.ex |= (active && ex ? 1u : 0u) << q;
-                cr.act |= (active ? 1u : 0u) << q;
-            }
-            if (fin) finish(pr, i0 - (uint32_t)kMtN);
-        };
-        load_in(0, I0);
-        int64_t t = 0;
-        for (; t < nch && ok; t += 2) {
-            round(t, I0, I1, R0, R1, t > 0);
-            if (ok && t + 1 < nch) round(t + 1, I1, I0, R1, R0, true);
-        }
-        if (ok && nch > 0) finish(((nch - 1) & 1) ? R1 : R0, (uint32_t)((nch - 1) * kMtN));
-        if (ok) produce(nch - 1);                                // (G: its last block, for the state out)
-        if (!ok) flags |= UQ_QFL_TIMEOUT;
-        if (role == 2 && ok && a.px_state_out)
-            qfl_state_out(a.px_state_out + j * kQfStateWords, s, D, gleft, gnext, c.qG * kMtN + c.rG, lane);
-        for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
-        if (lane == 0 && flags) atomicOr(&sflags[mi], flags);
-        if (role == 0 && lane == 0) a.scale[j] = c.sc;
-    }
-    __syncthreads();
-    if (live && role == 0 && lane == 0) a.info[j] = sflags[mi];
-}
-
-// The exact values of KQ1x (at their coordinates) into index order, in place, and their
-// count: one wave per message, 16 mask bytes per lane per step, a wave scan of the counts.
-__global__ void __launch_bounds__(256)
-quicfl_exact_compact_kernel(const uint8_t* __restrict__ mask, float* __restrict__ ev, int32_t* __restrict__ ecount,
-                            int64_t n, int64_t D) {
-    const int lane = threadIdx.x & 63;
-    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (j >= n) return;
-    const uint8_t* mk = mask + j * D;
-    float* e = ev + j * D;
-    uint32_t base = 0;
-    for (int64_t i0 = 0; i0 < D; i0 += 64 * 16) {
-        const int64_t i = i0 + 16 * lane;
-        uint4 m = make_uint4(0, 0, 0, 0);
-        if (i + 16 <= D) m = *reinterpret_cast<const uint4*>(mk + i);
-        else
-            for (int c = 0; i + c < D && c < 16; ++c) ((uint8_t*)&m)[c] = mk[i + c];
-        const uint32_t w[4] = {m.x, m.y, m.z, m.w};
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) cnt += __popc(w[k] & 0x01010101u);
-        uint32_t inc = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += y;
-        }
-        uint32_t slot = base + inc - cnt;
-        const uint32_t tot = __shfl(inc, 63, 64);
-        // every lane reads its values before any lane writes: a slot (a rank) can be the index
-        // of an exact coordinate another lane of this step still has to read
-        float vals[16];
-#pragma unroll
-        for (int c = 0; c < 16; ++c) vals[c] = ((w[c >> 2] >> (8 * (c & 3))) & 1u) ? e[i + c] : 0.f;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (cnt) {                                                // (rare: ~0.4 % of coordinates)
-#pragma unroll
-            for (int c = 0; c < 16; ++c)
-                if ((w[c >> 2] >> (8 * (c & 3))) & 1u) e[slot++] = vals[c];
-        }
-        base += tot;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (lane == 0) ecount[j] = (int32_t)base;
-}
