@@ -3219,11 +3219,12 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     // multi-kernel path below when a threshold tie needs torch's choice
     if (d <= kSmallBiasedMax &&
         (tie_policy == UQ_TIES_LOWEST_INDEX || (host_check && n <= kSmallCheckMaxN))) {
-        static bool attr = false;
-        if (!attr) {
+        static std::atomic<uint64_t> attr_set{0};             // per device (bit = device index < 64)
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && !((attr_set.load() >> dev) & 1u)) {
             (void)hipFuncSetAttribute((const void*)biased_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)(kSmallBiasedMax * sizeof(uint32_t)));
-            attr = true;
+            attr_set.fetch_or(1ull << dev);
         }
         hipLaunchKernelGGL(biased_small_kernel, dim3((unsigned)n), dim3(256), (size_t)d * sizeof(uint32_t), st, x, out, d,
                            (float)m, (const float*)nullptr, l1buf, state);
