@@ -246,8 +246,6 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
     const int64_t D = c.D;
     const float thr = kQflExactT;
     int64_t etot = 0;
-    // the flags as wave masks (a compare and a scalar OR per test, not a select and an OR)
-    uint64_t bad_px = 0, bad_x = 0, bad_p = 0, bad_i = 0;
     // Two register sets for a round's inputs and for its pending stage 2, used alternately by
     // the loop unrolled by two: a set whose loads are in flight is never copied, so the next
     // round's loads and this round's gathers stay in flight across the round (with one set,
@@ -275,19 +273,19 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             const bool active = (r.act >> k) & 1u;
             const bool ex = (r.ex >> k) & 1u;
             const float tx = __uint_as_float(r.t[k][0]), tp = __uint_as_float(r.t[k][1]);
-            bad_px |= __ballot(active && !(tp >= 0.f && tp <= 1.f));
+            flags |= (active && !(tp >= 0.f && tp <= 1.f)) ? UQ_QFL_BAD_PX : 0;
             const float bx = (u24(r.wg[k]) < tp) ? 1.f : 0.f;
             const float xf = tx + bx;                                // AS:489
             if (XK == 0) {
                 const bool ok = xf > -9.2e18f && xf < 9.2e18f;
-                bad_x |= __ballot(active && !ok);
+                flags |= (active && !ok) ? UQ_QFL_X_RANGE : 0;
                 const int64_t xv = ok ? (int64_t)xf : 0;             // AS:490 .long()
                 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
                 const u32x2v w = {(uint32_t)xv, (uint32_t)((uint64_t)xv >> 32)};
                 __builtin_amdgcn_raw_buffer_store_b64(w, c.rX, qf_off(active, i * 8u), 0, kAuxNT);
             } else {
                 const bool ok = xf > -1.0f && xf < 256.0f;
-                bad_x |= __ballot(active && !ok);
+                flags |= (active && !ok) ? UQ_QFL_X_RANGE : 0;
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ok ? (int32_t)xf : 0), c.rX, qf_off(active, i), 0, 0);
             }
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ex ? 1 : 0), c.rm, qf_off(active, i), 0, 0);
@@ -338,14 +336,14 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             const float q = ex ? 0.f : qq[k];                         // AS:480-481 (= v / delta), q[exact] = 0
             const float fl = floorf(q);
             const float p = q - fl;                                   // AS:483
-            bad_p |= __ballot(active && !(p >= 0.f && p <= 1.f));
+            flags |= (active && !(p >= 0.f && p <= 1.f)) ? UQ_QFL_BAD_P : 0;
             const float bern = (u24(mt_temper(wl)) < p) ? 1.f : 0.f;
             const float iq = fl + bern;                               // AS:484
             const float t1 = iq * c.fh;                               // AS:486 in f32 (no fma: -ffp-contract=off)
             const float t2 = t1 + (float)cur.h[k];
             const float it = truncf(t2 + c.fhalf);                    // .long() truncates
             const bool inr = it >= -c.fnumel && it < c.fnumel;        // torch.take's range (NaN: out)
-            bad_i |= __ballot(active && !inr);
+            flags |= (active && !inr) ? UQ_QFL_BAD_INDEX : 0;
             int32_t idx = inr ? (int32_t)it : 0;
             idx = idx < 0 ? idx + c.numel : idx;                      // torch.take wraps negatives
             const auto t = __builtin_amdgcn_raw_buffer_load_b64(c.rt, (uint32_t)idx * 8u, 0, 0);   // AS:486-487
@@ -362,8 +360,6 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
         if (rd + 1 < c1) round(rd + 1, I1, I0, R1, R0, true);
     }
     if (c1 > c0) finish(((c1 - 1 - c0) & 1) ? R1 : R0, (uint32_t)((c1 - 1) * kMtN));
-    flags |= (bad_px ? UQ_QFL_BAD_PX : 0) | (bad_x ? UQ_QFL_X_RANGE : 0) | (bad_p ? UQ_QFL_BAD_P : 0) |
-             (bad_i ? UQ_QFL_BAD_INDEX : 0);
     return etot;
 }
 
@@ -660,7 +656,6 @@ __device__ __forceinline__ int32_t qfl_recv_rounds(const QflRecvArgs& a, const f
         }
     };
     int32_t flags = 0;
-    uint64_t bad_i = 0;                                          // (a wave mask: compare + scalar OR)
     // round c: X of c + 1 and the mask of c + 2 loaded, the values of c + 1 slotted from its mask
     // (loaded a round earlier); then the h stream's block and the outputs of round c
     auto round = [&](int64_t c, const Set& cur, Set& nx, Set& nx2) {
@@ -678,7 +673,7 @@ __device__ __forceinline__ int32_t qfl_recv_rounds(const QflRecvArgs& a, const f
             const uint32_t h = hpow2 ? (w & (hl - 1u)) : (w % hl);                     // AS:528 randint
             const int64_t it = (int64_t)((uint64_t)cur.x[k] * (uint64_t)hl + h);       // AS:530 (int64 arithmetic)
             const bool inr = it >= -(int64_t)tab_n && it < (int64_t)tab_n;
-            bad_i |= __ballot(act && !inr);
+            flags |= (act && !inr) ? UQ_QFL_BAD_INDEX : 0;
             const int32_t idx = inr ? (int32_t)(it < 0 ? it + tab_n : it) : 0;        // take wraps negatives
             vv[k] = cur.m[k] ? cur.v[k] : (inr ? tab[idx] : 0.f);                      // AS:531
         }
@@ -701,7 +696,7 @@ __device__ __forceinline__ int32_t qfl_recv_rounds(const QflRecvArgs& a, const f
         if (c + 2 < c1) round(c + 2, S2, S0, S1);
     }
     *eend = ebase;
-    return flags | (bad_i ? UQ_QFL_BAD_INDEX : 0);
+    return flags;
 }
 
 // KQ2 for batches: one wave per message, the table (<= 1024 floats) in LDS for the
