@@ -54,6 +54,24 @@ def _sign_rows(seeds: torch.Tensor, D: int, dev):
     """(table, row index per client).  Seeds 0..99 (the reference's range) share one cached
     table per (device, D); other seeds get rows generated for this call."""
     seeds_cpu = seeds.to("cpu", torch.int64)
+    if seeds_cpu.numel() == 1:                       # the per-vector drop-ins: (table, [0]) cached per seed
+        sd = int(seeds_cpu.reshape(-1)[0])
+        key = (dev.index, D, "one", sd)
+        with _cache_lock:
+            hit = _sign_cache.get(key)
+        if hit is not None:
+            return hit
+        if 0 <= sd < _SEEDS:
+            tab, _ = _sign_rows(torch.arange(_SEEDS), D, dev)
+            hit = (tab, torch.tensor([sd], dtype=torch.int32, device=dev))
+        else:
+            hit = (rht_signs(seeds_cpu.reshape(-1), D, dev), torch.zeros(1, dtype=torch.int32, device=dev))
+        with _cache_lock:
+            if len(_sign_cache) > 256:
+                for k in [k for k in _sign_cache if len(k) == 4][:128]:
+                    del _sign_cache[k]
+            _sign_cache[key] = hit
+        return hit
     if bool(((seeds_cpu >= 0) & (seeds_cpu < _SEEDS)).all()):
         key = (dev.index, D)
         with _cache_lock:

@@ -218,34 +218,45 @@ def quicfl_compress(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSende
     X = torch.empty((n, D), dtype=x_dtype, device=dev)
     mask = torch.empty((n, D), dtype=torch.bool, device=dev)
     ev = torch.empty((n, D), dtype=torch.float32, device=dev)
-    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
     scale = torch.empty(n, dtype=torch.float32, device=dev)
-    info = torch.zeros(n, dtype=torch.int32, device=dev)
-    st_in = st_out = pxs = None
+    # the small per-message inputs go over in ONE host-to-device copy (prng seeds, then the
+    # generator states or px seeds) and the small outputs come back in ONE copy (flags, exact
+    # counts, end states): each pageable copy would otherwise wait for the stream on its own
     if px_states is not None:
         w = np.asarray(px_states, np.uint32).reshape(n, STATE_WORDS)
         for r in w:
             _check_state(r)
-        st_in = torch.from_numpy(w.view(np.int32).copy()).to(dev)
-        st_out = torch.empty_like(st_in)
+        tail = w.view(np.int32).reshape(-1)
     else:
         if px_seeds is None:
             raise ValueError("px_seeds or px_states is required")
-        pxs = torch.as_tensor(px_seeds, dtype=torch.int64).reshape(-1)
-        if pxs.numel() != n:
+        pxs = np.asarray(torch.as_tensor(px_seeds, dtype=torch.int64).reshape(-1).numpy(), np.int64)
+        if pxs.size != n:
             raise ValueError("one px seed per message")
-        pxs = (pxs & 0xFFFFFFFF).to(torch.int64)
-        pxs = torch.where(pxs >= 1 << 31, pxs - (1 << 32), pxs).to(torch.int32).to(dev)
+        tail = (pxs & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+    hin = np.empty(n + tail.size, np.int32)
+    hin[:n] = ps.numpy().astype(np.int32)
+    hin[n:] = tail
+    din = torch.from_numpy(hin).to(dev)
+    ps_d, tail_d = din[:n], din[n:]
+    nst = n * STATE_WORDS if px_states is not None else 0
+    dout = torch.zeros(2 * n + nst, dtype=torch.int32, device=dev)
+    info, cnt_d = dout[:n], dout[n:2 * n]
+    st_in = tail_d.view(n, STATE_WORDS) if px_states is not None else None
+    pxs_d = tail_d if px_states is None else None
+    st_out = dout[2 * n:].view(n, STATE_WORDS) if px_states is not None else None
+    hout = np.zeros(2 * n + nst, np.int32)
     if n and d:
         tab, rows = _sign_rows(rs, D, dev)
         xp = sender.table_xp(nbits, dev)
         ws = _ws(n, d, dev)
         _lib.check(_lib.load().uq_quicfl_compress_f32(
             _ptr(x), n, d, _ptr(tab), _ptr(rows), _ptr(xp), xp.shape[0], int(dd["h_len"]),
-            float(np.float32(dd["delta"])), _ptr(ps.to(torch.int32).to(dev)), _ptr(st_in), _ptr(pxs), _ptr(st_out),
-            _ptr(X), 0 if x_dtype == torch.int64 else 1, _ptr(mask), _ptr(ev), _ptr(cnt), _ptr(scale), _ptr(info),
+            float(np.float32(dd["delta"])), _ptr(ps_d), _ptr(st_in), _ptr(pxs_d), _ptr(st_out),
+            _ptr(X), 0 if x_dtype == torch.int64 else 1, _ptr(mask), _ptr(ev), _ptr(cnt_d), _ptr(scale), _ptr(info),
             _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_quicfl_compress_f32")
-        flags = int(np.bitwise_or.reduce(info.cpu().numpy()))
+        hout = dout.cpu().numpy()
+        flags = int(np.bitwise_or.reduce(hout[:n])) if n else 0
         if flags & _FLAG_P:
             raise RuntimeError("Expected p_in >= 0 && p_in <= 1 to be true, but got false.")   # AS:484 bernoulli
         if flags & _FLAG_INDEX:
@@ -256,10 +267,10 @@ def quicfl_compress(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSende
             raise OverflowError("X outside 0..255: use x_dtype=torch.int64")
         if flags & _FLAG_TIMEOUT:
             raise RuntimeError("uq_quicfl_compress_f32: internal wait ran out (results invalid)")
-    msg = QuicFLMessages(X=X, exact_mask=mask, exact_vals=ev, exact_count=cnt.cpu(), scale=scale, prng_seeds=ps,
-                         rotation_seeds=rs, dim=d, nbits=nbits, h_len=int(dd["h_len"]))
+    msg = QuicFLMessages(X=X, exact_mask=mask, exact_vals=ev, exact_count=torch.from_numpy(hout[n:2 * n].copy()),
+                         scale=scale, prng_seeds=ps, rotation_seeds=rs, dim=d, nbits=nbits, h_len=int(dd["h_len"]))
     if _state_out:
-        new = st_out.cpu().numpy().view(np.uint32) if st_out is not None else None
+        new = hout[2 * n:].reshape(n, STATE_WORDS).view(np.uint32).copy() if nst else None
         return msg, new
     return msg
 
@@ -269,7 +280,7 @@ _X_KIND = {torch.int64: 0, torch.uint8: 1, torch.int32: 2}
 
 
 def quicfl_decompress(X, nbits: int, prng_seeds, rotation_seeds, scale, dim: int, recv_table, h_len: int | None = None,
-                      exact_mask=None, exact_vals=None, exact_count=None) -> torch.Tensor:
+                      exact_mask=None, exact_vals=None, exact_count=None, _defer_check: bool = False) -> torch.Tensor:
     """Batched QuicFLReceiver.decompress (AS:526-535).  X [n, D] integers (int64, uint8 or int32
     are read in place on the device) with D a power of two; recv_table [rows, h_len];
     exact_mask bool [n, D] with exact_vals f32 [n, D], or both None.  exact_vals is dense (the
@@ -300,29 +311,40 @@ def quicfl_decompress(X, nbits: int, prng_seeds, rotation_seeds, scale, dim: int
         raise ValueError("one prng seed, rotation seed and scale per message")
     if (exact_mask is None) != (exact_vals is None):
         raise ValueError("exact_mask and exact_vals go together")
-    m = v = cnt = None
+    m = v = None
+    compact = exact_count is not None
     if exact_mask is not None:
         m = torch.as_tensor(exact_mask).to(device=dev).reshape(n, D)
         m = (m if m.dtype in (torch.bool, torch.uint8) else m != 0).contiguous()
         v = torch.as_tensor(exact_vals, dtype=torch.float32).to(dev).reshape(n, D).contiguous()
-        if exact_count is not None:
-            cnt = torch.as_tensor(exact_count, dtype=torch.int32).reshape(-1).to(dev)
-            if cnt.numel() != n:
-                raise ValueError("one exact count per message")
     pre = torch.empty((n, D), dtype=torch.float32, device=dev)
+    info = torch.zeros(n, dtype=torch.int32, device=dev)
     if n:
-        seeds32 = (ps & 0xFFFFFFFF).to(torch.int64)
-        seeds32 = torch.where(seeds32 >= 1 << 31, seeds32 - (1 << 32), seeds32).to(torch.int32).to(dev)
-        info = torch.zeros(n, dtype=torch.int32, device=dev)
+        # prng seeds (and the exact counts) in one host-to-device copy
+        hin = np.empty(2 * n if (compact and m is not None) else n, np.int32)
+        hin[:n] = (ps.numpy() & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+        if hin.size > n:
+            c = np.asarray(torch.as_tensor(exact_count).reshape(-1).cpu().numpy(), np.int64)
+            if c.size != n:
+                raise ValueError("one exact count per message")
+            hin[n:] = c.astype(np.int32)
+        din = torch.from_numpy(hin).to(dev)
+        seeds32, cnt = din[:n], (din[n:] if hin.size > n else None)
         _lib.check(_lib.load().uq_quicfl_receive_f32(
             _ptr(Xd), _X_KIND[Xd.dtype], n, D, _ptr(tab), rows, hl, _ptr(seeds32), _ptr(m), _ptr(v),
-            0 if cnt is None else 1, _ptr(cnt), _ptr(sc), _ptr(pre), _ptr(info), _stream_ptr(dev)), "uq_quicfl_receive_f32")
-        flags = int(np.bitwise_or.reduce(info.cpu().numpy()))
-        if flags & _FLAG_INDEX:
-            raise IndexError("index out of range in self (AS:530 recv_table.take)")
-        if flags & _FLAG_EXACT:
-            raise RuntimeError("shape mismatch: exact_values do not match exact_indeces (AS:531)")
-    return randomized_inverse_hadamard_transform(pre, rs)[:, :dim]
+            1 if (compact and m is not None) else 0, _ptr(cnt), _ptr(sc), _ptr(pre), _ptr(info), _stream_ptr(dev)),
+            "uq_quicfl_receive_f32")
+        if not _defer_check:
+            _raise_recv_flags(int(np.bitwise_or.reduce(info.cpu().numpy())))
+    out = randomized_inverse_hadamard_transform(pre, rs)[:, :dim]
+    return (out, info) if _defer_check else out
+
+
+def _raise_recv_flags(flags: int) -> None:
+    if flags & _FLAG_INDEX:
+        raise IndexError("index out of range in self (AS:530 recv_table.take)")
+    if flags & _FLAG_EXACT:
+        raise RuntimeError("shape mismatch: exact_values do not match exact_indeces (AS:531)")
 
 
 def quicfl_decompress_messages(msg: QuicFLMessages, recv_table) -> torch.Tensor:
@@ -358,7 +380,19 @@ class QuicFLReceiver:
         with open(prefix + "data.txt") as f:
             return ast.literal_eval(f.read())
 
-    def decompress(self, data):
+    def _table(self, nbits):
+        """The receiver table on the device (copied once per device)."""
+        dev = _device()
+        key = ("_dev", int(nbits), dev.index)
+        t = self._dev_tables.get(key) if hasattr(self, "_dev_tables") else None
+        if t is None:
+            if not hasattr(self, "_dev_tables"):
+                self._dev_tables = {}
+            t = self.recv_table[int(nbits)].to(dev).contiguous()
+            self._dev_tables[key] = t
+        return t
+
+    def decompress(self, data, _defer_check: bool = False):
         """AS:526-535: the message dict of QuicFLSender.compress -> vec[:dim] (on the GPU)."""
         X = torch.as_tensor(data["X"]).reshape(1, -1)
         D = X.shape[1]
@@ -373,10 +407,13 @@ class QuicFLReceiver:
             vals = torch.zeros((1, D), dtype=torch.float32, device=dev)   # compact: the values, then room to D
             vals[0, :ev.numel()] = ev.to(dev)
             cnt = [ev.numel()]
-        out = quicfl_decompress(X, data["nbits"], [int(data["prng_seed"])], [int(data["rotation_seed"])],
-                                data["scale"], int(data["dim"]), self.recv_table[int(data["nbits"])],
-                                int(data["h_len"]), mask, vals, cnt)
-        return out.view(-1)
+        self.recv_table[int(data["nbits"])]                              # KeyError like the reference
+        res = quicfl_decompress(X, data["nbits"], [int(data["prng_seed"])], [int(data["rotation_seed"])],
+                                data["scale"], int(data["dim"]), self._table(data["nbits"]),
+                                int(data["h_len"]), mask, vals, cnt, _defer_check=_defer_check)
+        if _defer_check:
+            return res[0].view(-1), res[1]
+        return res.view(-1)
 
 
 def _dropin_pair():
@@ -404,7 +441,12 @@ def QUICFL_quantize(input_vector, bits_per_dimension=1):
     data = {"vec": v, "seed": int(torch.randint(0, 100, (1,)).item()), "nbits": bits_per_dimension,
             "rotation_seed": 123, "nlevels": 2 ** bits_per_dimension}
     data = sender.compress(data)
-    out = receiver.decompress(data)
+    out, info = receiver.decompress(data, _defer_check=True)
+    # the result and the receiver's flags come back in one synchronisation
     host = torch.empty(out.numel(), dtype=torch.float32, pin_memory=True)
-    host.copy_(out)
+    hflag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+    host.copy_(out, non_blocking=True)
+    hflag.copy_(info, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    _raise_recv_flags(int(hflag[0]))
     return host.numpy()
