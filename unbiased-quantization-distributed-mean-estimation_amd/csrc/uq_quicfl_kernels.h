@@ -453,6 +453,24 @@ constexpr int64_t kQfTeamMaxN = 64;                 // messages per call up to w
 // 15 ms at 2^23), far inside qfl_wait_flag's bound of 2^24 sleeps; longer vectors take the
 // one-wave-per-message kernel, which never waits
 constexpr int64_t kQfTeamMaxD = (int64_t)1 << 23;
+constexpr float kQfRunRatio = 0.885f;
+__device__ __forceinline__ void qfl_run_bounds(int64_t nch, int64_t (&cb)[kQfRuns + 1]) {
+    float w[kQfRuns], tot = 0.f, x = 1.f;
+    for (int r = 0; r < kQfRuns; ++r) {
+        w[r] = x;
+        tot += x;
+        x *= kQfRunRatio;
+    }
+    float acc = 0.f;
+    cb[0] = 0;
+    for (int r = 1; r < kQfRuns; ++r) {
+        acc += w[r - 1];
+        int64_t b = (int64_t)((float)nch * (acc / tot) + 0.5f);
+        b = b < cb[r - 1] ? cb[r - 1] : (b > nch ? nch : b);
+        cb[r] = b;
+    }
+    cb[kQfRuns] = nch;
+}
 __device__ __forceinline__ bool qfl_wait_flag(int* f) {
     for (int it = 0; it < (1 << 24); ++it) {
         if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) return true;
@@ -479,7 +497,11 @@ quicfl_send_team_kernel(QflSendArgs a) {
     const int64_t j = blockIdx.x;
     const int64_t D = a.D;
     const int64_t nch = (D + kMtN - 1) / kMtN;
-    const int64_t per = (nch + kQfRuns - 1) / kQfRuns;   // rounds per run
+    // run r takes rounds [cb[r], cb[r + 1]): lengths shrinking by kQfRunRatio, since a later
+    // run's pass B starts later (the scout reaches its block later) and a round of pass B
+    // costs ~9 twists, so all runs end together
+    int64_t cb[kQfRuns + 1];
+    qfl_run_bounds(nch, cb);
     for (int i = threadIdx.x; i < kQfRuns * 3; i += 64 * kQfTeamWaves) (&rdy[0][0])[i] = 0;
     if (threadIdx.x < kQfRuns) cnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) sflags = 0;
@@ -499,26 +521,30 @@ quicfl_send_team_kernel(QflSendArgs a) {
         __builtin_amdgcn_s_setprio(3);
         int64_t last = 0;
         for (int r = 0; r < kQfRuns; ++r)
-            if (r * per < nch) last = c.qL + r * per;
+            if (cb[r] < cb[r + 1]) last = c.qL + cb[r];
         for (int64_t k = 0; k <= last; ++k) {
             if (k) mt_twist_reg(s, lane);
-            if (k < nch && k % per == 0) qfl_give(LA[k / per], s, &rdy[k / per][0], lane);
             const int64_t kb = k - c.qL;
-            if (kb >= 0 && kb < nch && kb % per == 0) qfl_give(WL[kb / per] + (k & 1) * kMtN, s, &rdy[kb / per][1], lane);
+            for (int r = 0; r < kQfRuns; ++r) {
+                if (cb[r] >= cb[r + 1]) continue;
+                if (k == cb[r]) qfl_give(LA[r], s, &rdy[r][0], lane);
+                if (kb == cb[r]) qfl_give(WL[r] + (k & 1) * kMtN, s, &rdy[r][1], lane);
+            }
         }
     } else if (wv == 1) {                                // global scout
         __builtin_amdgcn_s_setprio(3);
         int64_t last = 0;
         for (int r = 0; r < kQfRuns; ++r)
-            if (r * per < nch) last = c.qG + r * per;
+            if (cb[r] < cb[r + 1]) last = c.qG + cb[r];
         for (int64_t k = 0; k <= last; ++k) {
             if (k) mt_twist_reg(s, lane);
             const int64_t kg = k - c.qG;
-            if (kg >= 0 && kg < nch && kg % per == 0) qfl_give(WG[kg / per] + (k & 1) * kMtN, s, &rdy[kg / per][2], lane);
+            for (int r = 0; r < kQfRuns; ++r)
+                if (cb[r] < cb[r + 1] && kg == cb[r]) qfl_give(WG[r] + (k & 1) * kMtN, s, &rdy[r][2], lane);
         }
     } else {                                             // run r: rounds [c0, c1)
         const int r = wv - 2;
-        const int64_t c0 = r * per, c1 = min(nch, c0 + per);
+        const int64_t c0 = cb[r], c1 = cb[r + 1];
         if (c0 < c1) {
             bool ok = qfl_wait_flag(&rdy[r][0]);
             if (ok) {
@@ -548,7 +574,7 @@ quicfl_send_team_kernel(QflSendArgs a) {
     if (wv == 0) {                                       // exact values of run r: [c0*624, +cnt) -> index order
         int64_t base = 0;
         for (int r = 0; r < kQfRuns; ++r) {
-            const int64_t src = r * per * kMtN, n_r = cnt[r];
+            const int64_t src = cb[r] * kMtN, n_r = cnt[r];
             for (int64_t i0 = 0; i0 < n_r; i0 += 64) {   // (base <= src: a downward move, chunk by chunk)
                 const int64_t i = i0 + lane;
                 const float v = i < n_r ? a.ev[c.row + src + i] : 0.f;
