@@ -3651,8 +3651,11 @@ static size_t quicfl_h_off(int64_t n, int64_t dim) {
 static size_t quicfl_wl_off(int64_t n, int64_t dim) {
     return (quicfl_h_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D + 255) & ~(size_t)255;
 }
-static size_t quicfl_ws_total(int64_t n, int64_t dim) {
-    return quicfl_wl_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D * 8;
+static size_t quicfl_cnt_off(int64_t n, int64_t dim) {
+    return (quicfl_wl_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D * 8 + 255) & ~(size_t)255;
+}
+static size_t quicfl_ws_total(int64_t n, int64_t dim) {     // + exact counts per 1024-coordinate chunk
+    return quicfl_cnt_off(n, dim) + (size_t)n * (size_t)((eden_layout(n, dim).D + 1023) / 1024) * 4;
 }
 
 int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
@@ -3738,15 +3741,17 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
         if ((rc = hip_check(hipMemsetAsync(info, 0, (size_t)n * sizeof(int32_t), st), "clear info"))) return rc;
         hipLaunchKernelGGL(quicfl_stream_kernel, dim3((unsigned)((3 * n + 3) / 4)), dim3(256), 0, st, sa);
         if ((rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch"))) return rc;
-        const int64_t per_msg = (w.D + 1023) / 1024;
-        if (n * per_msg > 0x7FFFFFFF) return fail(UQ_E_INVALID, "batch too large for one launch");
-        const dim3 cgrid((unsigned)(n * per_msg));
-        if (x_kind == 0) hipLaunchKernelGGL(quicfl_coord_kernel<0>, cgrid, dim3(256), 0, st, q, wl, wg);
-        else hipLaunchKernelGGL(quicfl_coord_kernel<1>, cgrid, dim3(256), 0, st, q, wl, wg);
+        const int64_t items = n * ((w.D + 1023) / 1024);
+        const dim3 cgrid((unsigned)std::min<int64_t>(items, 256 * 8));     // 8 workgroups per CU, striding
+        uint32_t* ccnt = (uint32_t*)(wsb + quicfl_cnt_off(n, dim));
+        if (x_kind == 0) hipLaunchKernelGGL(quicfl_coord_kernel<0>, cgrid, dim3(256), 0, st, q, wl, wg, ccnt);
+        else hipLaunchKernelGGL(quicfl_coord_kernel<1>, cgrid, dim3(256), 0, st, q, wl, wg, ccnt);
         if ((rc = hip_check(hipGetLastError(), "quicfl_coord_kernel launch"))) return rc;
-        hipLaunchKernelGGL(quicfl_exact_compact_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, exact_mask,
-                           exact_vals, exact_count, n, w.D);
-        return hip_check(hipGetLastError(), "quicfl_exact_compact_kernel launch");
+        hipLaunchKernelGGL(quicfl_chunk_scan_kernel, dim3((unsigned)n), dim3(256), 0, st, ccnt, (w.D + 1023) / 1024,
+                           exact_count);
+        if ((rc = hip_check(hipGetLastError(), "quicfl_chunk_scan_kernel launch"))) return rc;
+        hipLaunchKernelGGL(quicfl_exact_scatter_kernel, cgrid, dim3(256), 0, st, exact_mask, wg, ccnt, exact_vals, n, w.D);
+        return hip_check(hipGetLastError(), "quicfl_exact_scatter_kernel launch");
     }
     const dim3 grid((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG));
     if (x_kind == 0)

@@ -836,8 +836,9 @@ quicfl_recv_team_kernel(QflRecvArgs a) {
 // words: bernoulli(p), AS:484; the wave twists through the H half first) and G (the global
 // generator, AS:489) -- and store what each coordinate needs (h as a byte, the L and G words
 // tempered) to HBM, 9 bytes per coordinate; then every coordinate is independent and KQ1p
-// runs them with the whole GPU.  Exact values go to their coordinate and
-// quicfl_exact_compact_kernel moves them into index order.
+// runs them with the whole GPU.  Exact values are staged at their coordinate (over the G
+// words, read just before) with a count per 1024-coordinate chunk; a scan of the counts and a
+// scatter put them into index order.
 struct QflStreamArgs {
     int64_t n, D;
     const int32_t* prng_seeds;
@@ -932,15 +933,12 @@ quicfl_stream_kernel(QflStreamArgs a) {
     }
 }
 
-// KQ1p: every coordinate of every message, four per thread (AS:472-490, 494-495).
+// KQ1p, one chunk of 1024 coordinates of message j (AS:472-490, 494-495).
 template <int XK>
-__global__ void __launch_bounds__(256)
-quicfl_coord_kernel(QflSendArgs a, const uint32_t* __restrict__ wlbuf, const uint32_t* __restrict__ wgbuf) {
+__device__ __forceinline__ void qfl_coord_chunk(const QflSendArgs& a, const uint32_t* __restrict__ wlbuf,
+                                                uint32_t* __restrict__ wgbuf, uint32_t* __restrict__ ccnt, int64_t j,
+                                                int64_t ch, int64_t i0, bool first) {
     const int64_t D = a.D;
-    const int64_t per_msg = (D + 1023) / 1024;                   // workgroups per message
-    const int64_t j = blockIdx.x / per_msg;
-    const int64_t i0 = (blockIdx.x % per_msg) * 1024 + 4 * (int64_t)threadIdx.x;
-    if (j >= a.n) return;
     const int64_t row = j * D;
     const float sc = (1.0f / a.nrm[j]) * a.sqrtD;                // AS:466/470
     const DivPlan dp = div_plan_norm(a.delta);
@@ -948,6 +946,7 @@ quicfl_coord_kernel(QflSendArgs a, const uint32_t* __restrict__ wlbuf, const uin
     const int32_t numel = (int32_t)a.numel;
     const float thr = kQflExactT;
     int32_t flags = 0;
+    uint32_t nex = 0;
     float vv[4], qq[4];
     uint32_t wl[4], wg[4], hh[4];
     bool act[4];
@@ -1017,57 +1016,85 @@ quicfl_coord_kernel(QflSendArgs a, const uint32_t* __restrict__ wlbuf, const uin
             ((uint8_t*)a.X)[row + i] = (uint8_t)(okx ? (int32_t)xf : 0);
         }
         a.mask[row + i] = ex ? 1 : 0;
-        if (ex) a.ev[row + i] = vv[c];
+        if (ex) {                                                // staged at its coordinate (this thread read
+            wgbuf[row + i] = __float_as_uint(vv[c]);             // that word above), compacted afterwards
+            ++nex;
+        }
     }
-    for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
-    if ((threadIdx.x & 63) == 0 && flags) atomicOr(&a.info[j], flags);
-    if (threadIdx.x == 0 && blockIdx.x % per_msg == 0) a.scale[j] = sc;
+    if (flags) atomicOr(&a.info[j], flags);                      // (rare: only on a flagged coordinate)
+    if (first && threadIdx.x == 0) a.scale[j] = sc;
+    __shared__ uint32_t lds[4];
+    uint32_t tot;
+    (void)block_excl_scan_u32(nex, lds, &tot);
+    if (threadIdx.x == 0) ccnt[j * ((D + 1023) / 1024) + ch] = tot;
 }
 
-// The exact values of KQ1p (at their coordinates) into index order, in place, and their
-// count: one wave per message, 16 mask bytes per lane per step, a wave scan of the counts.
+// KQ1p: every coordinate of every message, four per thread, 1024 per workgroup step; a
+// grid of a few workgroups per CU strides over the (message, chunk) items.
+template <int XK>
 __global__ void __launch_bounds__(256)
-quicfl_exact_compact_kernel(const uint8_t* __restrict__ mask, float* __restrict__ ev, int32_t* __restrict__ ecount,
-                            int64_t n, int64_t D) {
-    const int lane = threadIdx.x & 63;
-    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (j >= n) return;
-    const uint8_t* mk = mask + j * D;
-    float* e = ev + j * D;
+quicfl_coord_kernel(QflSendArgs a, const uint32_t* __restrict__ wlbuf, uint32_t* __restrict__ wgbuf,
+                    uint32_t* __restrict__ ccnt) {
+    const int64_t per_msg = (a.D + 1023) / 1024;
+    const int64_t items = a.n * per_msg;
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const int64_t j = it / per_msg, ch = it % per_msg;
+        qfl_coord_chunk<XK>(a, wlbuf, wgbuf, ccnt, j, ch, ch * 1024 + 4 * (int64_t)threadIdx.x, ch == 0);
+    }
+}
+
+// Exact counts per 1024-coordinate chunk -> exclusive offsets in place, and each message's
+// total (exact_count): one workgroup per message.
+__global__ void __launch_bounds__(256)
+quicfl_chunk_scan_kernel(uint32_t* __restrict__ ccnt, int64_t per_msg, int32_t* __restrict__ ecount) {
+    __shared__ uint32_t lds[4];
+    const int64_t j = blockIdx.x;
+    uint32_t* c = ccnt + j * per_msg;
     uint32_t base = 0;
-    for (int64_t i0 = 0; i0 < D; i0 += 64 * 16) {
-        const int64_t i = i0 + 16 * lane;
-        uint4 m = make_uint4(0, 0, 0, 0);
-        if (i + 16 <= D) m = *reinterpret_cast<const uint4*>(mk + i);
-        else
-            for (int c = 0; i + c < D && c < 16; ++c) ((uint8_t*)&m)[c] = mk[i + c];
-        const uint32_t w[4] = {m.x, m.y, m.z, m.w};
-        uint32_t cnt = 0;
+    for (int64_t t0 = 0; t0 < per_msg; t0 += 1024) {
+        uint32_t v[4], sum = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) cnt += __popc(w[k] & 0x01010101u);
-        uint32_t inc = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += y;
+        for (int k = 0; k < 4; ++k) {
+            const int64_t t = t0 + 4 * (int64_t)threadIdx.x + k;
+            v[k] = t < per_msg ? c[t] : 0u;
+            sum += v[k];
         }
-        uint32_t slot = base + inc - cnt;
-        const uint32_t tot = __shfl(inc, 63, 64);
-        // every lane reads its values before any lane writes: a slot (a rank) can be the index
-        // of an exact coordinate another lane of this step still has to read
-        float vals[16];
+        uint32_t tot;
+        uint32_t pre = base + block_excl_scan_u32(sum, lds, &tot);
 #pragma unroll
-        for (int c = 0; c < 16; ++c) vals[c] = ((w[c >> 2] >> (8 * (c & 3))) & 1u) ? e[i + c] : 0.f;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (cnt) {                                                // (rare: ~0.4 % of coordinates)
-#pragma unroll
-            for (int c = 0; c < 16; ++c)
-                if ((w[c >> 2] >> (8 * (c & 3))) & 1u) e[slot++] = vals[c];
+        for (int k = 0; k < 4; ++k) {
+            const int64_t t = t0 + 4 * (int64_t)threadIdx.x + k;
+            if (t < per_msg) c[t] = pre;
+            pre += v[k];
         }
         base += tot;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
     }
-    if (lane == 0) ecount[j] = (int32_t)base;
+    if (threadIdx.x == 0) ecount[j] = (int32_t)base;
+}
+
+// The staged exact values into index order: each chunk from its offset, ranks by one block
+// scan (a grid of a few workgroups per CU striding over the chunks).
+__global__ void __launch_bounds__(256)
+quicfl_exact_scatter_kernel(const uint8_t* __restrict__ mask, const uint32_t* __restrict__ staged,
+                            const uint32_t* __restrict__ coff, float* __restrict__ ev, int64_t n, int64_t D) {
+    __shared__ uint32_t lds[4];
+    const int64_t per_msg = (D + 1023) / 1024;
+    const int64_t items = n * per_msg;
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const int64_t j = it / per_msg, ch = it % per_msg;
+        const int64_t row = j * D, i0 = ch * 1024 + 4 * (int64_t)threadIdx.x;
+        uint32_t m4 = 0;
+        if (i0 + 4 <= D) m4 = *reinterpret_cast<const uint32_t*>(mask + row + i0);
+        else
+            for (int c = 0; c < 4; ++c)
+                if (i0 + c < D) m4 |= (uint32_t)mask[row + i0 + c] << (8 * c);
+        const uint32_t cnt = __popc(m4 & 0x01010101u);
+        uint32_t tot;
+        uint32_t slot = coff[it] + block_excl_scan_u32(cnt, lds, &tot);
+        if (cnt) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if ((m4 >> (8 * c)) & 1u) ev[row + slot++] = __uint_as_float(staged[row + i0 + c]);
+        }
+    }
 }
