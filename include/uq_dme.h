@@ -46,10 +46,6 @@ const char* uq_build_id(void);
  * internal-error status) can be tested.  Returns the previous setting.  Never set by the
  * library; production callers leave it at 0. */
 int uq_test_force_replay_failure(int on);
-/* Test hook, process-wide: on != 0 makes batched QUIC-FL sends take the one-wave-per-message
- * kernel instead of the stream + coordinate kernels (the tests compare the two).  Returns the
- * previous setting. */
-int uq_test_quicfl_one_wave(int on);
 
 /* Thread-local description of the last error returned on this thread. */
 const char* uq_last_error(void);

@@ -214,56 +214,3 @@ def test_batch_states_and_many_messages(fx):
         assert np.array_equal(msg.X[j].cpu().numpy().astype(np.int64), exp["X"]), j
         assert np.float32(msg.scale[j].item()).view(np.uint32) == np.float32(exp["scale"]).view(np.uint32), j
         assert (new[j, 0], new[j, 1]) == (gst[0], gst[1]) and np.array_equal(new[j, 2:], gst[2]), j
-
-
-@pytest.mark.parametrize("nbits,n,dim", [(1, 70, 4096), (3, 65, 200), (2, 66, 1 << 15), (4, 67, 2)])
-def test_stream_coord_sender_equals_one_wave(fx, nbits, n, dim):
-    """Batches run the streams first (a wave each, their words to HBM) and then every
-    coordinate in parallel (exact values compacted afterwards); the one-wave-per-message
-    kernel (test hook) gives the same bits: X, mask, exact values and counts, scales, flags
-    and the generators' end states."""
-    import uqdme
-    import uqdme_amd.quicfl as q
-    from uqdme_amd._lib import load
-    meta, z, rmeta, rz = fx
-    snd = senders(meta)["pub"]
-    rng = np.random.default_rng(nbits * 1000 + n)
-    x = (rng.standard_normal((n, dim)) * rng.uniform(0.5, 3, (n, 1))).astype(np.float32)
-    x[3, : min(dim, 50)] = 1e4                        # exact coordinates in bulk on one row
-    seeds = [int(s) for s in rng.integers(0, 10 ** 6, n)]
-    states = np.empty((n, 626), np.uint32)
-    g = torch.Generator()
-    for j in range(n):
-        g.manual_seed(int(j * 31 + 5))
-        pre = int(rng.integers(0, 1500))
-        if pre:
-            torch.rand(pre, generator=g)
-        states[j] = q.generator_words(g)[1]
-    outs = []
-    for one in (0, 1):
-        load().uq_test_quicfl_one_wave(one)
-        try:
-            if dim == 200:                            # fresh generators from px seeds
-                outs.append((q.quicfl_compress(torch.from_numpy(x), nbits, seeds, [123] * n, sender=snd,
-                                               px_seeds=[j * 7 + 1 for j in range(n)]), None))
-            else:
-                outs.append(q.quicfl_compress(torch.from_numpy(x), nbits, seeds, [123] * n, sender=snd,
-                                              px_states=states, _state_out=True))
-        finally:
-            load().uq_test_quicfl_one_wave(0)
-    (a, sa), (b, sb) = outs
-    assert torch.equal(a.X, b.X) and torch.equal(a.exact_mask, b.exact_mask) and torch.equal(a.scale, b.scale)
-    assert torch.equal(a.exact_count, b.exact_count) and (sa is None or np.array_equal(sa, sb))
-    if dim == 200:
-        return
-    for j in range(n):
-        cnt = int(a.exact_count[j])
-        assert torch.equal(a.exact_vals[j, :cnt], b.exact_vals[j, :cnt]), j
-    tX, tp = sender_tables(nbits)
-    for j in (0, 3, n - 1):
-        st = (int(states[j, 0]), int(states[j, 1]), states[j, 2:])
-        exp, gst = _oracle_row(x[j], nbits, seeds[j], 123, tX, tp, DATA[nbits], st)
-        assert np.array_equal(a.X[j].cpu().numpy().astype(np.int64), exp["X"]), j
-        cnt = int(a.exact_count[j])
-        assert a.exact_vals[j, :cnt].cpu().numpy().view(np.uint32).tolist() == exp["exact_values"].view(np.uint32).tolist()
-        assert (sa[j, 0], sa[j, 1]) == (gst[0], gst[1]) and np.array_equal(sa[j, 2:], gst[2]), j

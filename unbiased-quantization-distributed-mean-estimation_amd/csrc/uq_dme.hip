@@ -2181,8 +2181,6 @@ codes_mean_kernel(const int8_t* __restrict__ codes, int64_t ldc, const float* __
 thread_local std::string g_err;
 // test hook (uq_test_force_replay_failure): every torch-tie replay takes its failure path
 std::atomic<int> g_force_replay_failure{0};
-// test hook (uq_test_quicfl_one_wave): batches take the one-wave-per-message sender
-std::atomic<int> g_qfl_one_wave{0};
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -2718,8 +2716,6 @@ int uq_version(void) { return 102; }
 const char* uq_build_id(void) { return UQ_BUILD_ID; }
 
 int uq_test_force_replay_failure(int on) { return g_force_replay_failure.exchange(on ? 1 : 0); }
-
-int uq_test_quicfl_one_wave(int on) { return g_qfl_one_wave.exchange(on ? 1 : 0); }
 
 const char* uq_last_error(void) { return g_err.c_str(); }
 
@@ -3647,21 +3643,10 @@ static size_t quicfl_h_off(int64_t n, int64_t dim) {
     return (eden_layout(n, dim).total + 255) & ~(size_t)255;
 }
 
-// ... then the batch path's stream words: L and G, u32 [n][D] each
-static size_t quicfl_wl_off(int64_t n, int64_t dim) {
-    return (quicfl_h_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D + 255) & ~(size_t)255;
-}
-static size_t quicfl_cnt_off(int64_t n, int64_t dim) {
-    return (quicfl_wl_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D * 8 + 255) & ~(size_t)255;
-}
-static size_t quicfl_ws_total(int64_t n, int64_t dim) {     // + exact counts per 1024-coordinate chunk
-    return quicfl_cnt_off(n, dim) + (size_t)n * (size_t)((eden_layout(n, dim).D + 1023) / 1024) * 4;
-}
-
 int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
     if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
     if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
-    *bytes_out = quicfl_ws_total(n, dim);
+    *bytes_out = quicfl_h_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D;
     return UQ_OK;
 }
 
@@ -3684,7 +3669,7 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     if (!px_state && !px_seeds) return fail(UQ_E_INVALID, "px_state or px_seeds is required");
     const EdenLayout w = eden_layout(n, dim);
     const size_t hoff = quicfl_h_off(n, dim);
-    if (!ws || ws_bytes < quicfl_ws_total(n, dim)) return fail(UQ_E_WORKSPACE, "workspace too small");
+    if (!ws || ws_bytes < hoff + (size_t)n * (size_t)w.D) return fail(UQ_E_WORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     FwhtArgs a;
@@ -3722,36 +3707,6 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
         else
             hipLaunchKernelGGL(quicfl_send_team_kernel<1>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
         return hip_check(hipGetLastError(), "quicfl_send_team_kernel launch");
-    }
-    if (!g_qfl_one_wave.load()) {
-        // batches: the three streams (a wave each) into HBM, then every coordinate in parallel
-        uint32_t* wl = (uint32_t*)(wsb + quicfl_wl_off(n, dim));
-        uint32_t* wg = wl + (size_t)n * (size_t)w.D;
-        QflStreamArgs sa{};
-        sa.n = n;
-        sa.D = w.D;
-        sa.prng_seeds = prng_seeds;
-        sa.px_state = px_state;
-        sa.px_seeds = px_seeds;
-        sa.px_state_out = px_state_out;
-        sa.h_len = h_len;
-        sa.hbuf = q.hbuf;
-        sa.wlbuf = wl;
-        sa.wgbuf = wg;
-        if ((rc = hip_check(hipMemsetAsync(info, 0, (size_t)n * sizeof(int32_t), st), "clear info"))) return rc;
-        hipLaunchKernelGGL(quicfl_stream_kernel, dim3((unsigned)((3 * n + 3) / 4)), dim3(256), 0, st, sa);
-        if ((rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch"))) return rc;
-        const int64_t items = n * ((w.D + 1023) / 1024);
-        const dim3 cgrid((unsigned)std::min<int64_t>(items, 256 * 8));     // 8 workgroups per CU, striding
-        uint32_t* ccnt = (uint32_t*)(wsb + quicfl_cnt_off(n, dim));
-        if (x_kind == 0) hipLaunchKernelGGL(quicfl_coord_kernel<0>, cgrid, dim3(256), 0, st, q, wl, wg, ccnt);
-        else hipLaunchKernelGGL(quicfl_coord_kernel<1>, cgrid, dim3(256), 0, st, q, wl, wg, ccnt);
-        if ((rc = hip_check(hipGetLastError(), "quicfl_coord_kernel launch"))) return rc;
-        hipLaunchKernelGGL(quicfl_chunk_scan_kernel, dim3((unsigned)n), dim3(256), 0, st, ccnt, (w.D + 1023) / 1024,
-                           exact_count);
-        if ((rc = hip_check(hipGetLastError(), "quicfl_chunk_scan_kernel launch"))) return rc;
-        hipLaunchKernelGGL(quicfl_exact_scatter_kernel, cgrid, dim3(256), 0, st, exact_mask, wg, ccnt, exact_vals, n, w.D);
-        return hip_check(hipGetLastError(), "quicfl_exact_scatter_kernel launch");
     }
     const dim3 grid((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG));
     if (x_kind == 0)

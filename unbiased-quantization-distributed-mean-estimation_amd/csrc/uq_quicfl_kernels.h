@@ -828,273 +828,3 @@ quicfl_recv_team_kernel(QflRecvArgs a) {
         a.info[j] = f;
     }
 }
-
-// ---- KQ1s + KQ1p: the sender for batches as streams, then coordinates ----------------------
-// One wave per message leaves the SIMD idle more than half the time (VALU busy 42 %): the
-// per-coordinate arithmetic sits behind three serial streams.  Here the streams run first,
-// one wave each -- H (the local generator's first D words: h, AS:465/469), L (its next D
-// words: bernoulli(p), AS:484; the wave twists through the H half first) and G (the global
-// generator, AS:489) -- and store what each coordinate needs (h as a byte, the L and G words
-// tempered) to HBM, 9 bytes per coordinate; then every coordinate is independent and KQ1p
-// runs them with the whole GPU.  Exact values are staged at their coordinate (over the G
-// words, read just before) with a count per 1024-coordinate chunk; a scan of the counts and a
-// scatter put them into index order.
-struct QflStreamArgs {
-    int64_t n, D;
-    const int32_t* prng_seeds;
-    const uint32_t* px_state;
-    const int32_t* px_seeds;
-    uint32_t* px_state_out;
-    int32_t h_len;
-    uint8_t* hbuf;              // [n][D] h
-    uint32_t* wlbuf;            // [n][D] tempered local words D + i
-    uint32_t* wgbuf;            // [n][D] tempered global words i
-};
-__global__ void __launch_bounds__(256)
-quicfl_stream_kernel(QflStreamArgs a) {
-    __shared__ uint32_t scr[4][kMtN];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t item = (int64_t)blockIdx.x * 4 + wv;         // (message, stream)
-    if (item >= a.n * 3) return;
-    const int64_t j = item / 3;
-    const int role = (int)(item % 3);
-    const int64_t D = a.D;
-    const uint32_t Du = (uint32_t)D;
-    const int64_t row = j * D;
-    uint32_t s[kMtGroups];
-    int32_t gleft = 1, gnext = 0;
-    if (role == 2) {
-        if (a.px_state) {
-            const uint32_t* st = a.px_state + j * kQfStateWords;
-            gleft = (int32_t)st[0];
-            gnext = (int32_t)st[1];
-            mt_load(s, st + 2, lane);
-        } else {
-            if (lane == 0) mt_seed(scr[wv], (uint32_t)a.px_seeds[j]);
-            wave_lds_fence();
-            mt_load(s, scr[wv], lane);
-        }
-    } else {
-        if (lane == 0) mt_seed(scr[wv], (uint32_t)a.prng_seeds[j]);
-        wave_lds_fence();
-        mt_load(s, scr[wv], lane);
-    }
-    const int64_t nch = (D + kMtN - 1) / kMtN;
-    if (role == 0) {                                             // h = word i % h_len, i < D
-        const uint32_t hl = (uint32_t)a.h_len;
-        const bool hpow2 = (hl & (hl - 1)) == 0;
-        const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.hbuf + row, Du);
-        for (int64_t b = 1; b <= nch; ++b) {
-            mt_twist_reg(s, lane);
-            const uint32_t i0 = (uint32_t)((b - 1) * kMtN);
-#pragma unroll
-            for (int g = 0; g < kMtGroups; ++g) {
-                const int e = 64 * g + lane;
-                const uint32_t w = mt_temper(s[g]);
-                const uint32_t h = hpow2 ? (w & (hl - 1u)) : (w % hl);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)h, rh, qf_off(e < kMtN, i0 + (uint32_t)e), 0, 0);
-            }
-        }
-        return;
-    }
-    // L: local words D + i (word index v = 624 + D + i counts the untwisted block 0);
-    // G: global words i from ATen's position (the first left - 1 words are state[next ..])
-    const int64_t v0 = role == 1 ? (int64_t)kMtN + D : (gleft > 1 ? (int64_t)gnext : (int64_t)kMtN);
-    const int64_t q0 = v0 / kMtN, qlast = (v0 + D - 1) / kMtN;
-    const __amdgpu_buffer_rsrc_t rw = make_rsrc(role == 1 ? (void*)(a.wlbuf + row) : (void*)(a.wgbuf + row), Du * 4u);
-    int64_t have = 0;
-    for (int64_t b = q0; b <= qlast; ++b) {
-        while (have < b) { mt_twist_reg(s, lane); ++have; }
-        const int64_t c0 = b * kMtN - v0;                        // coordinate of slot 0 (may be negative)
-#pragma unroll
-        for (int g = 0; g < kMtGroups; ++g) {
-            const int e = 64 * g + lane;
-            const int64_t i = c0 + e;
-            const bool ok = e < kMtN && i >= 0 && i < D;
-            __builtin_amdgcn_raw_buffer_store_b32(mt_temper(s[g]), rw, qf_off(ok, (uint32_t)(ok ? i : 0) * 4u), 0, 0);
-        }
-    }
-    if (role == 2 && a.px_state_out) {                           // the block holding word D - 1
-        uint32_t* so = a.px_state_out + j * kQfStateWords;
-        uint32_t left1, next1;
-        if (D <= (int64_t)gleft - 1) {
-            left1 = (uint32_t)(gleft - D);
-            next1 = (uint32_t)(gnext + D);
-        } else {
-            const int64_t pos = (v0 + D - 1) % kMtN;
-            next1 = (uint32_t)(pos + 1);
-            left1 = (uint32_t)(kMtN - pos);
-        }
-        mt_store(s, so + 2, lane);
-        if (lane == 0) {
-            so[0] = left1;
-            so[1] = next1;
-        }
-    }
-}
-
-// KQ1p, one chunk of 1024 coordinates of message j (AS:472-490, 494-495).
-template <int XK>
-__device__ __forceinline__ void qfl_coord_chunk(const QflSendArgs& a, const uint32_t* __restrict__ wlbuf,
-                                                uint32_t* __restrict__ wgbuf, uint32_t* __restrict__ ccnt, int64_t j,
-                                                int64_t ch, int64_t i0, bool first) {
-    const int64_t D = a.D;
-    const int64_t row = j * D;
-    const float sc = (1.0f / a.nrm[j]) * a.sqrtD;                // AS:466/470
-    const DivPlan dp = div_plan_norm(a.delta);
-    const float fh = (float)a.h_len, fhalf = (float)a.half, fnumel = (float)a.numel;
-    const int32_t numel = (int32_t)a.numel;
-    const float thr = kQflExactT;
-    int32_t flags = 0;
-    uint32_t nex = 0;
-    float vv[4], qq[4];
-    uint32_t wl[4], wg[4], hh[4];
-    bool act[4];
-    uint32_t exm = 0;
-    float rv[4];
-    if (i0 + 4 <= D) {                                           // (rows are 16-byte aligned: D a power of two >= 4)
-        const float4 r4 = *reinterpret_cast<const float4*>(a.rot + row + i0);
-        const uint4 l4 = *reinterpret_cast<const uint4*>(wlbuf + row + i0);
-        const uint4 g4 = *reinterpret_cast<const uint4*>(wgbuf + row + i0);
-        const uint32_t h4 = *reinterpret_cast<const uint32_t*>(a.hbuf + row + i0);
-        rv[0] = r4.x; rv[1] = r4.y; rv[2] = r4.z; rv[3] = r4.w;
-        wl[0] = l4.x; wl[1] = l4.y; wl[2] = l4.z; wl[3] = l4.w;
-        wg[0] = g4.x; wg[1] = g4.y; wg[2] = g4.z; wg[3] = g4.w;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            hh[c] = (h4 >> (8 * c)) & 0xFFu;
-            act[c] = true;
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int64_t i = i0 + c;
-            act[c] = i < D;
-            const int64_t ii = act[c] ? i : 0;
-            rv[c] = act[c] ? a.rot[row + ii] : 0.f;
-            wl[c] = wlbuf[row + ii];
-            wg[c] = wgbuf[row + ii];
-            hh[c] = a.hbuf[row + ii];
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        vv[c] = rv[c] * sc;                                       // AS:472
-        exm |= ((vv[c] > thr) || (vv[c] < -thr) ? 1u : 0u) << c; // AS:478
-    }
-    div_n(vv, dp, qq, exm);                                      // AS:480-481 (= v / delta)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int64_t i = i0 + c;
-        const bool active = act[c];
-        const bool ex = (exm >> c) & 1u;
-        const float q = ex ? 0.f : qq[c];
-        const float fl = floorf(q);
-        const float p = q - fl;                                  // AS:483
-        flags |= (active && !(p >= 0.f && p <= 1.f)) ? UQ_QFL_BAD_P : 0;
-        const float bern = (u24(wl[c]) < p) ? 1.f : 0.f;
-        const float iq = fl + bern;                              // AS:484
-        const float t1 = iq * fh;                                // AS:486 in f32
-        const float t2 = t1 + (float)hh[c];
-        const float it = truncf(t2 + fhalf);
-        const bool inr = it >= -fnumel && it < fnumel;
-        flags |= (active && !inr) ? UQ_QFL_BAD_INDEX : 0;
-        int32_t idx = inr ? (int32_t)it : 0;
-        idx = idx < 0 ? idx + numel : idx;
-        const float2 t = a.tab[idx];                             // AS:486-487
-        flags |= (active && !(t.y >= 0.f && t.y <= 1.f)) ? UQ_QFL_BAD_PX : 0;
-        const float bx = (u24(wg[c]) < t.y) ? 1.f : 0.f;
-        const float xf = t.x + bx;                               // AS:489
-        if (!active) continue;
-        if (XK == 0) {
-            const bool okx = xf > -9.2e18f && xf < 9.2e18f;
-            flags |= okx ? 0 : UQ_QFL_X_RANGE;
-            ((int64_t*)a.X)[row + i] = okx ? (int64_t)xf : 0;     // AS:490 .long()
-        } else {
-            const bool okx = xf > -1.0f && xf < 256.0f;
-            flags |= okx ? 0 : UQ_QFL_X_RANGE;
-            ((uint8_t*)a.X)[row + i] = (uint8_t)(okx ? (int32_t)xf : 0);
-        }
-        a.mask[row + i] = ex ? 1 : 0;
-        if (ex) {                                                // staged at its coordinate (this thread read
-            wgbuf[row + i] = __float_as_uint(vv[c]);             // that word above), compacted afterwards
-            ++nex;
-        }
-    }
-    if (flags) atomicOr(&a.info[j], flags);                      // (rare: only on a flagged coordinate)
-    if (first && threadIdx.x == 0) a.scale[j] = sc;
-    __shared__ uint32_t lds[4];
-    uint32_t tot;
-    (void)block_excl_scan_u32(nex, lds, &tot);
-    if (threadIdx.x == 0) ccnt[j * ((D + 1023) / 1024) + ch] = tot;
-}
-
-// KQ1p: every coordinate of every message, four per thread, 1024 per workgroup step; a
-// grid of a few workgroups per CU strides over the (message, chunk) items.
-template <int XK>
-__global__ void __launch_bounds__(256)
-quicfl_coord_kernel(QflSendArgs a, const uint32_t* __restrict__ wlbuf, uint32_t* __restrict__ wgbuf,
-                    uint32_t* __restrict__ ccnt) {
-    const int64_t per_msg = (a.D + 1023) / 1024;
-    const int64_t items = a.n * per_msg;
-    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
-        const int64_t j = it / per_msg, ch = it % per_msg;
-        qfl_coord_chunk<XK>(a, wlbuf, wgbuf, ccnt, j, ch, ch * 1024 + 4 * (int64_t)threadIdx.x, ch == 0);
-    }
-}
-
-// Exact counts per 1024-coordinate chunk -> exclusive offsets in place, and each message's
-// total (exact_count): one workgroup per message.
-__global__ void __launch_bounds__(256)
-quicfl_chunk_scan_kernel(uint32_t* __restrict__ ccnt, int64_t per_msg, int32_t* __restrict__ ecount) {
-    __shared__ uint32_t lds[4];
-    const int64_t j = blockIdx.x;
-    uint32_t* c = ccnt + j * per_msg;
-    uint32_t base = 0;
-    for (int64_t t0 = 0; t0 < per_msg; t0 += 1024) {
-        uint32_t v[4], sum = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t t = t0 + 4 * (int64_t)threadIdx.x + k;
-            v[k] = t < per_msg ? c[t] : 0u;
-            sum += v[k];
-        }
-        uint32_t tot;
-        uint32_t pre = base + block_excl_scan_u32(sum, lds, &tot);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t t = t0 + 4 * (int64_t)threadIdx.x + k;
-            if (t < per_msg) c[t] = pre;
-            pre += v[k];
-        }
-        base += tot;
-    }
-    if (threadIdx.x == 0) ecount[j] = (int32_t)base;
-}
-
-// The staged exact values into index order: each chunk from its offset, ranks by one block
-// scan (a grid of a few workgroups per CU striding over the chunks).
-__global__ void __launch_bounds__(256)
-quicfl_exact_scatter_kernel(const uint8_t* __restrict__ mask, const uint32_t* __restrict__ staged,
-                            const uint32_t* __restrict__ coff, float* __restrict__ ev, int64_t n, int64_t D) {
-    __shared__ uint32_t lds[4];
-    const int64_t per_msg = (D + 1023) / 1024;
-    const int64_t items = n * per_msg;
-    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
-        const int64_t j = it / per_msg, ch = it % per_msg;
-        const int64_t row = j * D, i0 = ch * 1024 + 4 * (int64_t)threadIdx.x;
-        uint32_t m4 = 0;
-        if (i0 + 4 <= D) m4 = *reinterpret_cast<const uint32_t*>(mask + row + i0);
-        else
-            for (int c = 0; c < 4; ++c)
-                if (i0 + c < D) m4 |= (uint32_t)mask[row + i0 + c] << (8 * c);
-        const uint32_t cnt = __popc(m4 & 0x01010101u);
-        uint32_t tot;
-        uint32_t slot = coff[it] + block_excl_scan_u32(cnt, lds, &tot);
-        if (cnt) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if ((m4 >> (8 * c)) & 1u) ev[row + slot++] = __uint_as_float(staged[row + i0 + c]);
-        }
-    }
-}
