@@ -448,7 +448,10 @@ quicfl_send_wave_kernel(QflSendArgs a) {
 // wait on anyone).
 constexpr int kQfTeamWaves = 8;                    // 2 scouts + 6 runs
 constexpr int kQfRuns = kQfTeamWaves - 2;
-constexpr int64_t kQfTeamMaxN = 64;                 // messages per call up to which the team kernel runs
+// messages per call up to which the team kernels run: a workgroup per message while they fit
+// the GPU about once (1024 x 2^20, bits 1: sender 128 / 256 messages 4.5 / 5.5 ms against
+// 11.4 ms one-wave; 1024 messages 19.4 ms against 15.6 -- there the one-wave kernels win)
+constexpr int64_t kQfTeamMaxN = 256;
 // padded dims up to which it runs: the last run waits for the scouts' 2D/624 twists (about
 // 15 ms at 2^23), far inside qfl_wait_flag's bound of 2^24 sleeps; longer vectors take the
 // one-wave-per-message kernel, which never waits
