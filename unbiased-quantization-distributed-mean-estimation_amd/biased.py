@@ -34,6 +34,7 @@ __all__ = ["Type_biased_quantize", "biased_quantize", "TIES_TORCH", "TIES_LOWEST
 TIES_TORCH = 0            # UQ_TIES_TORCH
 TIES_LOWEST_INDEX = 1     # UQ_TIES_LOWEST_INDEX
 _HOST_CHECK = 4           # UQ_TIES_HOST_CHECK
+_SMALL_MAX = 32767        # kSmallBiasedMax: one-launch vectors (shorter than torch's GRAIN)
 _tls = threading.local()
 FLAG_AMBIGUOUS = 1
 FLAG_NONFINITE = 2
@@ -86,6 +87,22 @@ def biased_quantize(x, bits_per_dimension=1, *, m: int | None = None, torch_thre
     return res[0] if len(res) == 1 else tuple(res)
 
 
+def _flags_and_status(dev, d: int, info) -> int:
+    """One synchronisation for row 0's flags and this workspace's status word (uq_check_status's
+    word at byte 8; check_status() would read every cached workspace of the stream)."""
+    ws = _workspace(dev, _biased_ws_bytes(1, d, get_torch_threads()))
+    hw = getattr(_tls, "pinned", None)
+    if hw is None:
+        hw = _tls.pinned = torch.empty(2, dtype=torch.int32, pin_memory=True)
+    hw[0:1].copy_(info[0, 1:2], non_blocking=True)
+    hw[1:2].copy_(ws[8:12].view(torch.int32), non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    flags, status = int(hw[0]), int(hw[1])
+    if status:
+        check_status()                            # raises with the library's message, clears the word
+    return flags
+
+
 def Type_biased_quantize(input_vector, bits_per_dimension=1):
     """Drop-in for NMSE_Results/Codes/All_Schemes.py:669 (same name for FLM:177's
     directory naming).  KeyError for an unknown rate (AS:684), bit-identical to the
@@ -107,19 +124,16 @@ def Type_biased_quantize(input_vector, bits_per_dimension=1):
         return v.clone()
     if not v.is_contiguous():
         v = v.contiguous()
-    out, info = biased_quantize(v.view(1, d), m=m, ties="torch", return_info=True, host_check=True)
-    # one synchronisation for the flags and this workspace's status word (uq_check_status's
-    # word at byte 8; check_status() would read every cached workspace of the stream)
-    ws = _workspace(dev, _biased_ws_bytes(1, d, get_torch_threads()))
-    hw = getattr(_tls, "pinned", None)
-    if hw is None:
-        hw = _tls.pinned = torch.empty(2, dtype=torch.int32, pin_memory=True)
-    hw[0:1].copy_(info[0, 1:2], non_blocking=True)
-    hw[1:2].copy_(ws[8:12].view(torch.int32), non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
-    flags, status = int(hw[0]), int(hw[1])
-    if status:
-        check_status()                            # raises with the library's message, clears the word
+    # below GRAIN the lowest-index rule runs as one launch (KB-small) and gives torch's bits
+    # unless a threshold tie straddles the selection (flag 1): read the flags once and rerun
+    # with the replay only then, so a tie-free call synchronises once
+    small = d <= _SMALL_MAX
+    out, info = biased_quantize(v.view(1, d), m=m, ties="lowest" if small else "torch", return_info=True,
+                                host_check=not small)
+    flags = _flags_and_status(dev, d, info)
+    if small and flags & FLAG_AMBIGUOUS:
+        out, info = biased_quantize(v.view(1, d), m=m, ties="torch", return_info=True, host_check=True)
+        flags = _flags_and_status(dev, d, info)
     if flags & FLAG_NONFINITE:
         raise ValueError("cannot convert float NaN to integer (m' is not finite, AS:656)")
     if flags & FLAG_RANGE:
