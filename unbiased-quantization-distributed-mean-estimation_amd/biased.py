@@ -18,6 +18,7 @@ indices instead (identical whenever info flag 1 is clear; see include/uq_dme.h).
 from __future__ import annotations
 
 import ctypes
+import functools
 import threading
 
 import numpy as np
@@ -45,6 +46,7 @@ _TIES = {"torch": TIES_TORCH, "lowest": TIES_LOWEST_INDEX, TIES_TORCH: TIES_TORC
          TIES_LOWEST_INDEX: TIES_LOWEST_INDEX}
 
 
+@functools.lru_cache(maxsize=256)
 def _biased_ws_bytes(n: int, d: int, T: int) -> int:
     out = ctypes.c_size_t(0)
     _lib.check(_lib.load().uq_biased_workspace_bytes(n, d, T, ctypes.byref(out)), "uq_biased_workspace_bytes")
