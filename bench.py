@@ -3,6 +3,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+Without an external launcher, --gpus N > 1 starts the N rank processes itself (spawn_ranks:
+child processes with the launcher's environment, rank 0's JSON line forwarded, non-zero exit
+if any rank fails); under a launcher --gpus must equal WORLD_SIZE.
 
 Workload (BASELINE.json configs[1], "C2"): per GPU, n=1024 client vectors of d=2^20
 i.i.d. N(0,1) f32, resident in HBM before timing; rate R=1 (m = 224426); L1 in the
@@ -45,9 +48,12 @@ METRIC = "quantize+dequantize M-vectors/sec at d=2^20 (1/2/4/8 GPU) + NMSE vs re
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Without an external launcher (WORLD_SIZE unset) N > 1 "
+                         "starts N rank processes itself; under torch.distributed.run it must equal "
+                         "WORLD_SIZE (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--clients", type=int, default=1024, help="clients per GPU")
@@ -76,7 +82,78 @@ def parse():
     ap.add_argument("--side-pipelines", action="store_true", default=True,
                     help="also time the other pipelines (reported under 'pipelines')")
     ap.add_argument("--no-side-pipelines", dest="side_pipelines", action="store_false")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int, cmd, env=None, port=None, out=None, grace_s: float = 30.0) -> int:
+    """`bench.py --gpus N` without an external launcher: start N rank processes of `cmd` (fresh
+    interpreters, no exec; this parent never touches the GPU) with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as torch.distributed.run would, forward rank
+    0's stdout (the JSON line) to `out`, send the other ranks' stdout to stderr, and return
+    0 only if every rank exits 0.  When one rank fails the others get `grace_s` seconds to end
+    (a peer blocked in a collective would otherwise wait forever) and are then terminated."""
+    import subprocess
+    import threading
+    out = out if out is not None else sys.stdout
+    port = port or free_port()
+    base = dict(os.environ if env is None else env)
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+
+    def pump():
+        for line in procs[0].stdout:
+            out.write(line)
+            out.flush()
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    failed_at = None
+    while True:
+        codes = [p.poll() for p in procs]
+        if all(c is not None for c in codes):
+            break
+        if failed_at is None and any(c not in (None, 0) for c in codes):
+            failed_at = time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.05)
+    th.join(5)
+    codes = [p.wait() for p in procs]
+    bad = [(r, c) for r, c in enumerate(codes) if c != 0]
+    if bad:
+        print(f"bench.py: rank(s) failed: {bad}", file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+def world_from_env(args) -> int:
+    """The launcher's WORLD_SIZE must agree with --gpus (SystemExit otherwise)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is None:
+        args.gpus = world
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (the launcher started "
+                         f"{world} rank(s)); pass the same N to both")
+    return world
 
 
 # RCCL (backend "nccl") is the product path.  UQDME_BENCH_BACKEND=gloo is a rehearsal knob
@@ -134,6 +211,11 @@ STEP_KERNELS = ("l1_partial_kernel", "l1_finalize_kernel", "quantize_stream_kern
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        # no external launcher: one child process per rank (started before anything here
+        # initialises the GPU; children are new processes, never an exec of this one)
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    world_from_env(args)
     dist, rank, world, local = dist_init(args)
     import uqdme
 

@@ -6,7 +6,8 @@
 #   tests:<f>   only tests/<f> (repeatable, e.g. tests:test_gpu_pipeline.py)
 #   smoke       __graft_entry__.smoke()       -> smoke.log
 #   bench       python bench.py               -> bench.json
-#   gloo2       2-rank gloo rehearsal of bench.py --gpus 2 (ranks share cuda:0)
+#   gloo2       2-rank gloo rehearsal of bench.py --gpus 2 under torch.distributed.run (ranks share cuda:0)
+#   self2       the same, bench.py --gpus 2 starting its own ranks (no external launcher)
 #   dropin      tools/dropin_latency.py       -> dropin_latency.json
 #   profile     tools/profile_round.sh (kernel-trace stats + PMC passes, codes pipeline)
 # Every GPU step runs under its own timeout and the first failure ends the call (set -e).
@@ -28,6 +29,8 @@ for s in $STEPS; do
     gloo2) UQDME_BENCH_BACKEND=gloo timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
              --master-addr 127.0.0.1 --master-port 29553 bench.py --gpus 2 --steps 5 --warmup 2 \
              > $O/bench_gloo2.json 2> $O/bench_gloo2.err ;;
+    self2) UQDME_BENCH_BACKEND=gloo timeout -k 10 240 python bench.py --gpus 2 --steps 5 --warmup 2 \
+             > $O/bench_self2.json 2> $O/bench_self2.err ;;
     dropin) timeout -k 10 200 python tools/dropin_latency.py > $O/dropin_latency.json 2> $O/dropin_latency.err ;;
     profile) bash tools/profile_round.sh $O codes > $O/profile.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
