@@ -46,6 +46,12 @@ const char* uq_build_id(void);
  * internal-error status) can be tested.  Returns the previous setting.  Never set by the
  * library; production callers leave it at 0. */
 int uq_test_force_replay_failure(int on);
+/* Test hooks of the QUIC-FL kernels, process-wide (never set by the library): bit 0 makes the
+ * runs of the few-message team kernels (sender KQ1t, receiver KQ2t) skip their waits and report
+ * UQ_QFL_TIMEOUT, so the callers' timeout handling can be tested; bit 1 sends every call to the
+ * one-wave-per-message kernels (KQ1 / KQ2), so both forms can be compared on the same message.
+ * Returns the previous flags. */
+int uq_test_set_quicfl_hooks(int flags);
 
 /* Thread-local description of the last error returned on this thread. */
 const char* uq_last_error(void);

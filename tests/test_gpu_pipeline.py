@@ -116,8 +116,9 @@ def test_output_pool_never_hands_out_a_held_result(gpu_ready):
     x = torch.randn(n, d, device="cuda")
     X = torch.rand(n)
     ref = uqdme.quantize_dequantize(x, 1, X=X, torch_threads=1).clone()
-    old = POOL.min_bytes
+    old, was_on = POOL.min_bytes, POOL.enabled
     POOL.min_bytes = 0
+    POOL.enabled = True
     POOL.clear()
     try:
         held = [uqdme.quantize_dequantize(x, 1, X=X, torch_threads=1) for _ in range(4)]
@@ -147,4 +148,5 @@ def test_output_pool_never_hands_out_a_held_result(gpu_ready):
         assert torch.equal(view, ref[3])
     finally:
         POOL.min_bytes = old
+        POOL.enabled = was_on
         POOL.clear()

@@ -139,3 +139,60 @@ def test_receiver_team_equals_wave(fx):
             assert torch.equal(full[:5].view(torch.int32), few.view(torch.int32)), (dt, c is None)
     exp = E.quicfl_decompress(X[3], tab, tab.shape[1], int(ps[3]), mask[3], dense[3][mask[3]], sc[3], int(rs[3]), D)
     assert few[3].cpu().numpy().view(np.uint32).tolist() == exp.view(np.uint32).tolist()
+
+
+def test_timeout_flag_raises_in_sender_and_receiver(fx):
+    """A run of a team kernel whose wait ran out (UQ_QFL_TIMEOUT, forced through the test hook
+    uq_test_set_quicfl_hooks) never writes its coordinates: the sender, the receiver and the
+    drop-in's deferred check all raise instead of returning them."""
+    import sys
+    import uqdme
+    from uqdme_amd import quicfl as q
+    from uqdme_amd._lib import load
+    sys.path.insert(0, HERE)
+    from quicfl_tables import DATA, sender_tables
+    meta, z = fx
+    snd = uqdme.QuicFLSender(tables={1: (*sender_tables(1), DATA[1])})
+    rx = uqdme.QuicFLReceiver(tables={1: z["recv1"]})
+    x = torch.randn(1, 1 << 14)
+    msg = q.quicfl_compress(x, 1, [3], [123], sender=snd, px_seeds=[5])
+    assert load().uq_test_set_quicfl_hooks(1) == 0
+    try:
+        with pytest.raises(RuntimeError, match="wait ran out"):
+            q.quicfl_compress(x, 1, [3], [123], sender=snd, px_seeds=[5])
+        with pytest.raises(RuntimeError, match="wait ran out"):
+            q.quicfl_decompress_messages(msg, z["recv1"])
+        d = {"X": msg.X[0].long(), "exact_values": msg.exact_vals[0, :int(msg.exact_count[0])],
+             "exact_indeces": msg.exact_mask[0], "prng_seed": int(msg.prng_seeds[0]), "rotation_seed": 123,
+             "dim": 1 << 14, "scale": msg.scale[0], "nbits": 1, "h_len": msg.h_len}
+        with pytest.raises(RuntimeError, match="wait ran out"):
+            rx.decompress(d)
+        _, info = rx.decompress(d, _defer_check=True)
+        with pytest.raises(RuntimeError, match="wait ran out"):
+            q._raise_recv_flags(int(info.cpu()[0]))
+    finally:
+        assert load().uq_test_set_quicfl_hooks(0) == 1
+    rx.decompress(d)                                   # hook off: the same message decodes
+
+
+def test_receiver_broadcasts_one_exact_value(fx):
+    """AS:531 vec[exact_indeces] = exact_values with a one-element exact_values broadcasts it
+    over every masked coordinate (and over none): the dict receiver accepts it like the
+    reference (vs the receiver oracle, whose numpy assignment broadcasts the same way)."""
+    import uqdme
+    meta, z = fx
+    rng = np.random.default_rng(11)
+    tab = z["recv2"]
+    rx = uqdme.QuicFLReceiver(tables={2: tab})
+    D, dim = 8192, 8000
+    X = rng.integers(0, 4, size=D)
+    for nmask in (0, 1, 37):
+        mask = np.zeros(D, bool)
+        mask[rng.choice(D, nmask, replace=False)] = True
+        val = np.array([2.75], np.float32)
+        msg = {"X": torch.from_numpy(X), "exact_values": torch.from_numpy(val), "exact_indeces": torch.from_numpy(mask),
+               "prng_seed": 4242, "rotation_seed": 17, "dim": dim, "scale": torch.tensor(1.5, dtype=torch.float32),
+               "nbits": 2, "h_len": tab.shape[1]}
+        out = rx.decompress(msg).cpu().numpy()
+        exp = E.quicfl_decompress(X, tab, tab.shape[1], 4242, mask, val, np.float32(1.5), 17, dim)
+        assert out.view(np.uint32).tolist() == exp.view(np.uint32).tolist(), nmask

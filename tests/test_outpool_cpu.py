@@ -56,14 +56,14 @@ def call(pool, clock, ms):
 
 def test_small_batches_bypass(monkeypatch):
     Clock(monkeypatch)
-    pool = outpool.OutputPool(min_bytes=1 << 20)
+    pool = outpool.OutputPool(enabled=True, min_bytes=1 << 20)
     (out,), tok = pool.acquire(DEV, SPEC)
     assert tok is None and out.shape == (4, 1024)
 
 
 def test_held_results_are_never_reused(monkeypatch):
     clock = Clock(monkeypatch)
-    pool = outpool.OutputPool(explore=3, keep=2, min_bytes=1)
+    pool = outpool.OutputPool(enabled=True, explore=3, keep=2, min_bytes=1)
     held = []
     for i in range(12):
         out, tok = call(pool, clock, 1.0 + i)
@@ -83,7 +83,7 @@ def test_held_results_are_never_reused(monkeypatch):
 
 def test_explores_then_serves_fastest(monkeypatch):
     clock = Clock(monkeypatch)
-    pool = outpool.OutputPool(explore=4, keep=2, min_bytes=1)
+    pool = outpool.OutputPool(enabled=True, explore=4, keep=2, min_bytes=1)
     times = [3.0, 1.0, 4.0, 2.0]
     ptrs = {}
     for ms in times:                              # results held one call at a time: the pool
@@ -103,7 +103,7 @@ def test_explores_then_serves_fastest(monkeypatch):
 
 def test_fastest_held_falls_back_to_second(monkeypatch):
     clock = Clock(monkeypatch)
-    pool = outpool.OutputPool(explore=3, keep=2, min_bytes=1)
+    pool = outpool.OutputPool(enabled=True, explore=3, keep=2, min_bytes=1)
     ptrs = {}
     for ms in (2.0, 1.0, 3.0):
         out, _ = call(pool, clock, ms)
@@ -116,12 +116,33 @@ def test_fastest_held_falls_back_to_second(monkeypatch):
 
 def test_memory_cap(monkeypatch):
     clock = Clock(monkeypatch, total=64 * 1024)    # 64 KiB "device": max_frac 1/4 -> one 16 KiB set
-    pool = outpool.OutputPool(explore=6, keep=2, min_bytes=1, max_frac=0.25, reserve_frac=0.0)
+    pool = outpool.OutputPool(enabled=True, explore=6, keep=2, min_bytes=1, max_frac=0.25, reserve_frac=0.0)
     a, ta = call(pool, clock, 1.0)
     b, tb = call(pool, clock, 1.0)                 # a is held and the cap is reached: plain tensor
     assert ta is not None and tb is None and b.data_ptr() != a.data_ptr()
     pool.clear()
     assert pool.report() == {}
+
+
+def test_opt_in_and_idle_release(monkeypatch):
+    clock = Clock(monkeypatch)
+    monkeypatch.delenv("UQDME_OUTPUT_POOL", raising=False)
+    off = outpool.OutputPool(min_bytes=1)
+    (o,), tok = off.acquire(DEV, SPEC)
+    assert not off.enabled and tok is None          # default: off, plain allocations
+    monkeypatch.setenv("UQDME_OUTPUT_POOL", "1")
+    assert outpool.OutputPool(min_bytes=1).enabled
+    pool = outpool.OutputPool(enabled=True, explore=3, keep=2, min_bytes=1, idle_s=0.05)
+    out, _ = call(pool, clock, 1.0)
+    held = out
+    out2, _ = call(pool, clock, 2.0)
+    del out2
+    import time
+    time.sleep(0.1)
+    (o,), _ = pool.acquire(DEV, [((2, 8), torch.float32)])  # any call releases idle free sets
+    sets = [st for e in pool._sets.values() for st in e["sets"]]
+    assert len(sets) == 2                           # the held set stays, the idle free one went
+    assert any(st.bufs[0].data_ptr() == held.data_ptr() for st in sets)
 
 
 if __name__ == "__main__":

@@ -2717,6 +2717,12 @@ const char* uq_build_id(void) { return UQ_BUILD_ID; }
 
 int uq_test_force_replay_failure(int on) { return g_force_replay_failure.exchange(on ? 1 : 0); }
 
+// test hooks of the QUIC-FL kernels (never set by the library itself): bit 0 makes every run
+// of the few-message team kernels skip its waits and report UQ_QFL_TIMEOUT; bit 1 sends every
+// call to the one-wave-per-message kernels (so a test can compare both forms on one message)
+std::atomic<int> g_quicfl_hooks{0};
+int uq_test_set_quicfl_hooks(int flags) { return g_quicfl_hooks.exchange(flags & 3); }
+
 const char* uq_last_error(void) { return g_err.c_str(); }
 
 int uq_rate_to_m(double bits, int64_t d, int64_t* m_out) {
@@ -3417,8 +3423,10 @@ int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, c
     r.scale = scale;
     r.out = out;
     r.info = info;
+    const int hooks = g_quicfl_hooks.load();
+    r.force_timeout = hooks & 1;
     // few messages: a workgroup per message (the h stream's scout + 7 runs); batches: a wave each
-    if (n <= kQfTeamMaxN && D >= (int64_t)kMtN * kQrRuns && D <= kQfTeamMaxD) {
+    if (!(hooks & 2) && n <= kQfTeamMaxN && D >= (int64_t)kMtN * kQrRuns && D <= kQfTeamMaxD) {
         const dim3 grid((unsigned)n), block(64 * kQfTeamWaves);
         if (x_kind == 0) hipLaunchKernelGGL(quicfl_recv_team_kernel<0>, grid, block, 0, st, r);
         else if (x_kind == 1) hipLaunchKernelGGL(quicfl_recv_team_kernel<1>, grid, block, 0, st, r);
@@ -3699,9 +3707,11 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.info = info;
     q.D = w.D;
     q.n = n;
+    const int hooks = g_quicfl_hooks.load();
+    q.force_timeout = hooks & 1;
     // few messages: a workgroup per message (scouts + runs: the streams' length is the critical
     // path, not the per-coordinate work); batches: a wave per message
-    if (n <= kQfTeamMaxN && w.D >= (int64_t)kMtN * kQfRuns && w.D <= kQfTeamMaxD) {
+    if (!(hooks & 2) && n <= kQfTeamMaxN && w.D >= (int64_t)kMtN * kQfRuns && w.D <= kQfTeamMaxD) {
         if (x_kind == 0)
             hipLaunchKernelGGL(quicfl_send_team_kernel<0>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
         else

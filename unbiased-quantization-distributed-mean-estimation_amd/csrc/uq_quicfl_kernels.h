@@ -148,6 +148,7 @@ struct QflSendArgs {
     int32_t* info;              // [n] UQ_QFL_* flags
     int64_t D;
     int64_t n;
+    int32_t force_timeout;      // test hook (uq_test_set_quicfl_hooks): team runs skip their waits
 };
 
 // Round state carried from stage 1 (words, flags, gather issued) to stage 2 (X, stores).
@@ -549,7 +550,7 @@ quicfl_send_team_kernel(QflSendArgs a) {
         const int r = wv - 2;
         const int64_t c0 = cb[r], c1 = cb[r + 1];
         if (c0 < c1) {
-            bool ok = qfl_wait_flag(&rdy[r][0]);
+            bool ok = !a.force_timeout && qfl_wait_flag(&rdy[r][0]);
             if (ok) {
                 uint32_t sa[kMtGroups];
                 mt_load(sa, LA[r], lane);
@@ -618,6 +619,7 @@ struct QflRecvArgs {
     const float* scale;             // [n]
     float* out;                     // [n][D]
     int32_t* info;                  // [n] or null
+    int32_t force_timeout;          // test hook (uq_test_set_quicfl_hooks): team runs skip their waits
 };
 
 // Rounds [c0, c1) of message j's receiver (AS:526-532): s holds the h stream's block c0 on
@@ -809,7 +811,7 @@ quicfl_recv_team_kernel(QflRecvArgs a) {
         const int r = wv - 1;
         const int64_t c0 = r * per, c1 = min(nch, c0 + per);
         if (c0 < c1) {
-            if (qfl_wait_flag(&rdy[r])) {
+            if (!a.force_timeout && qfl_wait_flag(&rdy[r])) {
                 uint32_t s[kMtGroups];
                 mt_load(s, SA[r], lane);
                 uint32_t base = 0, eend = 0;

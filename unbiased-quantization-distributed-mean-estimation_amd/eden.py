@@ -33,7 +33,58 @@ __all__ = ["EDEN_quantize_Hadamard", "eden_quantize", "eden_compress", "eden_dec
 
 _SEEDS = 100                       # AS:797 torch.randint(0, 100)
 _cache_lock = threading.Lock()
-_sign_cache: dict = {}
+
+
+class _SignCache:
+    """Device sign tables kept between calls, bounded by BYTES (least recently used first out):
+    the shared table of seeds 0..99 per (device, D) and the rows of other seeds (single seeds
+    of the drop-ins, sets of <= 4 seeds such as QUIC-FL's fixed 123).  The newest entry always
+    stays, so a table larger than the budget is still reused by the next call with that key.
+    The per-call row-index tensors (4 bytes each) are cached apart, by count."""
+
+    def __init__(self, budget_bytes: int = 2 << 30, max_rows: int = 4096):
+        from collections import OrderedDict
+        self.budget, self.max_rows = budget_bytes, max_rows
+        self.tabs = OrderedDict()      # key -> (tensor, nbytes)
+        self.rows = OrderedDict()      # key -> small int32 device tensor
+        self.bytes = 0
+
+    def get(self, key):
+        hit = self.tabs.get(key)
+        if hit is None:
+            return None
+        self.tabs.move_to_end(key)
+        return hit[0]
+
+    def put(self, key, tab):
+        nb = tab.numel() * tab.element_size()
+        old = self.tabs.pop(key, None)
+        if old is not None:
+            self.bytes -= old[1]
+        self.tabs[key] = (tab, nb)
+        self.bytes += nb
+        while self.bytes > self.budget and len(self.tabs) > 1:
+            _, (_, b) = self.tabs.popitem(last=False)
+            self.bytes -= b
+
+    def row(self, key, make):
+        r = self.rows.get(key)
+        if r is None:
+            r = make()
+            self.rows[key] = r
+            while len(self.rows) > self.max_rows:
+                self.rows.popitem(last=False)
+        else:
+            self.rows.move_to_end(key)
+        return r
+
+    def clear(self):
+        self.tabs.clear()
+        self.rows.clear()
+        self.bytes = 0
+
+
+_signs = _SignCache()
 
 
 def padded_dim(d: int) -> int:
@@ -50,47 +101,45 @@ def rht_signs(seeds, D: int, device=None) -> torch.Tensor:
     return out
 
 
+def _shared_table(D: int, dev):
+    key = (dev.index, D, "ref")
+    with _cache_lock:
+        tab = _signs.get(key)
+        if tab is None:
+            tab = rht_signs(torch.arange(_SEEDS), D, dev)
+            _signs.put(key, tab)
+        return tab
+
+
 def _sign_rows(seeds: torch.Tensor, D: int, dev):
     """(table, row index per client).  Seeds 0..99 (the reference's range) share one cached
-    table per (device, D); other seeds get rows generated for this call."""
-    seeds_cpu = seeds.to("cpu", torch.int64)
-    if seeds_cpu.numel() == 1:                       # the per-vector drop-ins: (table, [0]) cached per seed
-        sd = int(seeds_cpu.reshape(-1)[0])
+    table per (device, D); other seeds get rows of their own (cached for single seeds and sets
+    of up to four, within the cache's byte budget)."""
+    seeds_cpu = seeds.to("cpu", torch.int64).reshape(-1)
+    in_range = bool(((seeds_cpu >= 0) & (seeds_cpu < _SEEDS)).all())
+    if seeds_cpu.numel() == 1:                       # the per-vector drop-ins
+        sd = int(seeds_cpu[0])
+        if in_range:
+            tab = _shared_table(D, dev)
+            with _cache_lock:
+                return tab, _signs.row((dev.index, sd), lambda: torch.tensor([sd], dtype=torch.int32, device=dev))
         key = (dev.index, D, "one", sd)
         with _cache_lock:
-            hit = _sign_cache.get(key)
-        if hit is not None:
-            return hit
-        if 0 <= sd < _SEEDS:
-            tab, _ = _sign_rows(torch.arange(_SEEDS), D, dev)
-            hit = (tab, torch.tensor([sd], dtype=torch.int32, device=dev))
-        else:
-            hit = (rht_signs(seeds_cpu.reshape(-1), D, dev), torch.zeros(1, dtype=torch.int32, device=dev))
-        with _cache_lock:
-            if len(_sign_cache) > 256:
-                for k in [k for k in _sign_cache if len(k) == 4][:128]:
-                    del _sign_cache[k]
-            _sign_cache[key] = hit
-        return hit
-    if bool(((seeds_cpu >= 0) & (seeds_cpu < _SEEDS)).all()):
-        key = (dev.index, D)
-        with _cache_lock:
-            tab = _sign_cache.get(key)
+            tab = _signs.get(key)
             if tab is None:
-                tab = rht_signs(torch.arange(_SEEDS), D, dev)
-                _sign_cache[key] = tab
-        return tab, seeds_cpu.to(torch.int32).to(dev)
+                tab = rht_signs(seeds_cpu, D, dev)
+                _signs.put(key, tab)
+            return tab, _signs.row((dev.index, "zero"), lambda: torch.zeros(1, dtype=torch.int32, device=dev))
+    if in_range:
+        return _shared_table(D, dev), seeds_cpu.to(torch.int32).to(dev)
     uniq, inv = torch.unique(seeds_cpu, return_inverse=True)
     if uniq.numel() <= 4:                 # a few other seeds (e.g. QUIC-FL's fixed 123, AS:822): cached too
         key = (dev.index, D, tuple(uniq.tolist()))
         with _cache_lock:
-            tab = _sign_cache.get(key)
+            tab = _signs.get(key)
             if tab is None:
-                if len(_sign_cache) > 64:
-                    for k in [k for k in _sign_cache if len(k) == 3][:32]:
-                        del _sign_cache[k]
                 tab = rht_signs(uniq, D, dev)
-                _sign_cache[key] = tab
+                _signs.put(key, tab)
         return tab, inv.to(torch.int32).to(dev)
     return rht_signs(uniq, D, dev), inv.to(torch.int32).to(dev)
 

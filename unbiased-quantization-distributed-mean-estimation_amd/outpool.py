@@ -18,15 +18,24 @@ time.  For large batches the one-shot APIs therefore take their outputs from thi
     holds at most `max_frac` of device memory (then a call gets a plain allocation), and
     `POOL.clear()` releases everything it holds.
 
+The pool is OPT-IN (`uqdme.set_output_pool(True)` or UQDME_OUTPUT_POOL=1): it keeps device
+memory (up to explore + keep sets per shape, at most `max_frac` of the device) after the call
+returns, which a caller that goes on to allocate for other work may not expect.  Off, every
+call allocates plainly through torch's caching allocator (and draws a random placement).  On,
+sets left unused for `idle_s` seconds are released at the pool's next call, and `clear()`
+releases everything at once.
+
 Results are the same bits whichever set is used; only the time differs.
 """
 from __future__ import annotations
 
+import os
 import threading
+import time
 
 import torch
 
-__all__ = ["OutputPool", "POOL"]
+__all__ = ["OutputPool", "POOL", "set_output_pool"]
 
 
 def _use_count(t: torch.Tensor) -> int:
@@ -40,6 +49,7 @@ class _Set:
         self.ms_sum, self.ms_n = 0.0, 0
         self.pending = []                      # (start event, end event) not read yet
         self.stream = None                     # stream of the last launch writing the set
+        self.last_use = time.monotonic()
 
     def free(self, stream=None) -> bool:
         """Nothing outside the pool holds the set, and a launch on another stream than
@@ -64,14 +74,15 @@ class _Set:
 
 class OutputPool:
     def __init__(self, explore: int = 6, keep: int = 2, min_bytes: int = 1 << 28, reserve_frac: float = 0.25,
-                 max_frac: float = 0.125):
+                 max_frac: float = 0.125, idle_s: float = 30.0, enabled: bool | None = None):
         # max_frac: the pool never holds more than this share of device memory (36 GB of an
         # MI355X's 288 GB); beyond it a call gets a plain allocation
         self.explore, self.keep, self.min_bytes, self.reserve_frac = explore, keep, min_bytes, reserve_frac
         self.max_frac = max_frac
         self._lock = threading.Lock()
         self._sets: dict = {}
-        self.enabled = True
+        self.idle_s = idle_s
+        self.enabled = (os.environ.get("UQDME_OUTPUT_POOL", "0") == "1") if enabled is None else enabled
 
     def _alloc(self, dev, specs):
         return _Set([torch.empty(shape, dtype=dt, device=dev) for shape, dt in specs])
@@ -84,6 +95,7 @@ class OutputPool:
             return [torch.empty(s, dtype=dt, device=dev) for s, dt in specs], None
         key = (dev.index, tuple((tuple(s), dt) for s, dt in specs))
         with self._lock:
+            self._release_idle()
             ent = self._sets.setdefault(key, {"sets": [], "explored": False})
             sets = ent["sets"]
             for st in sets:
@@ -111,7 +123,20 @@ class OutputPool:
                 chosen = min(free, key=lambda st: st.mean() if st.ms_n else float("inf"))
             if chosen is None:                 # everything held and no room: a plain allocation
                 return [torch.empty(s, dtype=dt, device=dev) for s, dt in specs], None
+            chosen.last_use = time.monotonic()
             return [b.view(b.shape) for b in chosen.bufs], chosen
+
+    def _release_idle(self):
+        """Drop sets nobody holds that have not been handed out for idle_s seconds."""
+        now = time.monotonic()
+        for k in list(self._sets):
+            sets = self._sets[k]["sets"]
+            for st in list(sets):
+                st.harvest()
+                if now - st.last_use > self.idle_s and st.free() and not st.pending:
+                    sets.remove(st)
+            if not sets:
+                del self._sets[k]
 
     def _prune(self, sets):
         """Keep the `keep` fastest timed sets (and any set still held); release the rest."""
@@ -149,3 +174,10 @@ class OutputPool:
 
 
 POOL = OutputPool()
+
+
+def set_output_pool(on: bool) -> None:
+    """Turn the one-shot APIs' output pool on or off (off releases what it holds)."""
+    POOL.enabled = bool(on)
+    if not on:
+        POOL.clear()

@@ -103,8 +103,7 @@ class QuicFLSender:
         self._xp = {}
         if tables is not None:                      # {nbits: (table_X, table_p, data dict)}
             for b, (tx, tp, dd) in tables.items():
-                self._add(int(b), torch.as_tensor(tx, dtype=torch.float32), torch.as_tensor(tp, dtype=torch.float32),
-                          dict(dd))
+                self._add(int(b), torch.as_tensor(tx), torch.as_tensor(tp), dict(dd))
         else:
             prefix = default_tables_prefix() if prefix is None else prefix
             for b, s in zip(bits, sr_bits):
@@ -114,6 +113,19 @@ class QuicFLSender:
     def _add(self, b, tx, tp, dd):
         if tx.numel() != tp.numel():
             raise ValueError("sender_table_X and sender_table_p differ in size")
+        # AS:489 bernoulli(table_p[idx]) draws ONE 32-bit generator word per coordinate and
+        # compares in f32 only for a float32 p; ATen's bernoulli_distribution<double> (a float64
+        # p) takes one 64-bit draw (two words) and compares in double, which the kernel does not
+        # reproduce: such tables are refused rather than cast (the cast would shift the global
+        # generator for every later draw of the caller)
+        if tp.dtype != torch.float32:
+            raise TypeError(f"sender_table_p must be float32 (got {tp.dtype}): a {tp.dtype} p makes the reference's "
+                            "bernoulli draw other generator words (AS:489); not supported")
+        if tx.dtype != torch.float32:
+            t32 = tx.to(torch.float32)
+            if not torch.equal(t32.to(tx.dtype), tx):
+                raise TypeError(f"sender_table_X ({tx.dtype}) holds values float32 cannot represent exactly")
+            tx = t32
         self.sender_table_X[b], self.sender_table_p[b], self.data[b] = tx, tp, dd
         h = int(dd["h_len"])
         self.half_table_size[b] = ((tx.numel() // h) - 1) * h // 2                      # AS:443
@@ -121,8 +133,8 @@ class QuicFLSender:
     @staticmethod
     def sender_table(prefix, device=None):
         """AS:447-451 with safe loaders: torch.load(weights_only=True), ast.literal_eval."""
-        tx = torch.load(prefix + "sender_table_X.pt", weights_only=True).to(torch.float32)
-        tp = torch.load(prefix + "sender_table_p.pt", weights_only=True).to(torch.float32)
+        tx = torch.load(prefix + "sender_table_X.pt", weights_only=True)     # dtypes kept: checked in _add
+        tp = torch.load(prefix + "sender_table_p.pt", weights_only=True)
         with open(prefix + "data.txt") as f:
             dd = ast.literal_eval(f.read())
         return tx, tp, dd
@@ -341,6 +353,8 @@ def quicfl_decompress(X, nbits: int, prng_seeds, rotation_seeds, scale, dim: int
 
 
 def _raise_recv_flags(flags: int) -> None:
+    if flags & _FLAG_TIMEOUT:
+        raise RuntimeError("uq_quicfl_receive_f32: internal wait ran out (results invalid)")
     if flags & _FLAG_INDEX:
         raise IndexError("index out of range in self (AS:530 recv_table.take)")
     if flags & _FLAG_EXACT:
@@ -402,6 +416,12 @@ class QuicFLReceiver:
             dev = _device()
             mask = torch.as_tensor(ei).reshape(1, D).to(dev)
             ev = torch.as_tensor(data["exact_values"], dtype=torch.float32).reshape(-1)
+            if ev.numel() == 1:
+                # AS:531 vec[exact_indeces] = exact_values broadcasts a one-element value over
+                # every masked coordinate: expand it to the mask's popcount (compact layout)
+                k = int(torch.count_nonzero(mask).item())
+                if k != 1:
+                    ev = ev.expand(k)
             if ev.numel() > D:
                 raise RuntimeError("shape mismatch: more exact_values than coordinates (AS:531)")
             vals = torch.zeros((1, D), dtype=torch.float32, device=dev)   # compact: the values, then room to D
