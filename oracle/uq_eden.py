@@ -18,10 +18,15 @@ Float semantics pinned here against torch 2.10 CPU (tools in tests/golden/make_g
     randint(0, 100) = w % 100.
   * torch.norm(v, 2) (f32): 8 interleaved lanes, acc = fma(v, v, acc) sequentially,
     lanes added 0..7 in order, tail, f32 sqrt.
-  * torch.dot (AS:335) goes to MKL sdot, whose summation order is MKL's and
-    CPU-dependent: this restatement accumulates the dot in fp64 and rounds once.  The
-    EDEN scale is therefore pinned to a relative tolerance (1e-6), everything else
-    (rotation, bins, centroids, inverse rotation) bit-for-bit.
+  * torch.dot (AS:335) goes to MKL's cblas sdot (torch 2.10's BLAS, oneMKL 2024.2, one
+    thread: torch.set_num_threads(1) also sets MKL's).  Its AVX-512 path on the fixtures'
+    host, found by summation-order probing (tools/dot_order_probe.py) and pinned by
+    tests/golden/dot_vectors.* (torch.dot's own bits, n = 1 .. 2^22) and by every EDEN scale the
+    reference recorded: 4 accumulators of 16 lanes, element i -> accumulator (i / 16) % 4,
+    lane i % 16 of 64-element blocks, each lane a sequential fma chain; then
+    (acc0 + acc1) + (acc2 + acc3) lane-wise; then the 16 lanes as i + (i + 8), i + (i + 4),
+    (0 + 1) + (2 + 3).  Of a remainder below 64, a 32-element block goes into acc0 and acc1,
+    then 16-element chunks into acc0, the last one masked.  torch_dot below.
 """
 from __future__ import annotations
 
@@ -138,6 +143,37 @@ def torch_norm2(v: np.ndarray) -> f32:
     return f32(np.sqrt(s))
 
 
+def torch_dot(x: np.ndarray, y: np.ndarray) -> f32:
+    """torch.dot(x, y) of two f32 vectors on CPU (MKL sdot, see the module header).  fma is
+    evaluated in extended precision (64-bit significand: a 48-bit product plus a 24-bit
+    accumulator) and rounded once to f32 except in the rare case where the exact sum needs
+    more than 64 bits (oracle/uq_oracle.c uqo_torch_dot uses fmaf)."""
+    x = np.asarray(x, f32).reshape(-1)
+    y = np.asarray(y, f32).reshape(-1)
+    n = x.shape[0]
+    L = np.longdouble
+    acc = np.zeros(64, f32)                        # accumulator k lane l at 16 k + l
+    nb = n // 64
+    if nb:
+        xb = x[:nb * 64].reshape(nb, 64).astype(L)
+        yb = y[:nb * 64].reshape(nb, 64).astype(L)
+        pr = xb * yb                               # exact products
+        for b in range(nb):
+            acc = (acc.astype(L) + pr[b]).astype(f32)
+    i0 = nb * 64
+    if n - i0 >= 32:                               # remainder: a 32-element block into acc0, acc1
+        acc[:32] = (acc[:32].astype(L) + x[i0:i0 + 32].astype(L) * y[i0:i0 + 32].astype(L)).astype(f32)
+        i0 += 32
+    for i0 in range(i0, n, 16):                    # then 16-element chunks into acc0 (last masked)
+        m = min(16, n - i0)
+        acc[:m] = (acc[:m].astype(L) + x[i0:i0 + m].astype(L) * y[i0:i0 + m].astype(L)).astype(f32)
+        acc[m:16] = (acc[m:16] + f32(0)).astype(f32)                          # masked lanes: + 0 * 0
+    v = ((acc[0:16] + acc[16:32]).astype(f32) + (acc[32:48] + acc[48:64]).astype(f32)).astype(f32)
+    v = (v[:8] + v[8:]).astype(f32)
+    v = (v[:4] + v[4:]).astype(f32)
+    return f32(f32(v[0] + v[1]) + f32(v[2] + v[3]))
+
+
 def bucketize(x: np.ndarray, b: np.ndarray) -> np.ndarray:
     """torch.bucketize(x, b) (right=False): number of boundaries strictly below x."""
     return np.searchsorted(b, x, side="left").astype(np.int64)
@@ -151,8 +187,9 @@ def eden_compress(x: np.ndarray, nbits: int, seed: int):
     sq = f32(np.sqrt(D))                                   # vec.numel() ** 0.5 -> f32 operand
     bins = bucketize(((vec * sq).astype(f32) / nrm).astype(f32), boundaries(nbits))
     c = centroids(nbits)[bins]
-    dot = f32(np.dot(c.astype(np.float64), vec.astype(np.float64)))   # MKL sdot: tolerance
-    scale = f32(f32(nrm * nrm) / dot)
+    dot = torch_dot(c, vec)                                # AS:335 torch.dot (MKL sdot order)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        scale = f32(f32(nrm * nrm) / dot)
     return bins, scale, vec, D
 
 

@@ -210,3 +210,30 @@ float uqo_torch_norm2(const float* v, int64_t d) {
     }
     return sqrtf(s);
 }
+
+/* torch.dot(x, y) on CPU f32 (All_Schemes.py:335, EDEN's scale), MKL's sdot on the fixtures'
+ * host (oracle/uq_eden.py:torch_dot, tools/dot_order_probe.py): 4 accumulators x 16 lanes over
+ * 64-element blocks, fma chains; of the remainder, a 32-element block into accumulators 0
+ * and 1, then 16-element chunks into accumulator 0 (the last one masked: lanes beyond n add
+ * 0 * 0); (acc0 + acc1) + (acc2 + acc3) lane-wise; lanes i + (i + 8), i + (i + 4), then
+ * (0 + 1) + (2 + 3). */
+float uqo_torch_dot(const float* x, const float* y, int64_t n) {
+    float acc[64];
+    for (int l = 0; l < 64; ++l) acc[l] = 0.0f;
+    const int64_t nb = n / 64;
+    for (int64_t b = 0; b < nb; ++b)
+        for (int l = 0; l < 64; ++l) acc[l] = fmaf(x[64 * b + l], y[64 * b + l], acc[l]);
+    int64_t i0 = nb * 64;
+    if (n - i0 >= 32) {                          /* a 32-element block: accumulators 0 and 1 */
+        for (int l = 0; l < 32; ++l) acc[l] = fmaf(x[i0 + l], y[i0 + l], acc[l]);
+        i0 += 32;
+    }
+    for (; i0 < n; i0 += 16)                     /* 16-element chunks, the last masked: acc 0 */
+        for (int l = 0; l < 16; ++l)
+            acc[l] = i0 + l < n ? fmaf(x[i0 + l], y[i0 + l], acc[l]) : fmaf(0.0f, 0.0f, acc[l]);
+    float v[16];
+    for (int l = 0; l < 16; ++l) v[l] = (acc[l] + acc[16 + l]) + (acc[32 + l] + acc[48 + l]);
+    for (int l = 0; l < 8; ++l) v[l] = v[l] + v[l + 8];
+    for (int l = 0; l < 4; ++l) v[l] = v[l] + v[l + 4];
+    return (v[0] + v[1]) + (v[2] + v[3]);
+}

@@ -41,6 +41,8 @@ def lib():
         L.uqo_torch_sum.argtypes = [p, i64, ctypes.c_int]
         L.uqo_torch_norm2.restype = f
         L.uqo_torch_norm2.argtypes = [p, i64]
+        L.uqo_torch_dot.restype = f
+        L.uqo_torch_dot.argtypes = [p, p, i64]
         L.uqc_bound.restype = ctypes.c_uint64
         L.uqc_bound.argtypes = [i64]
         L.uqc_encode.restype = ctypes.c_uint64
@@ -114,6 +116,14 @@ def torch_norm2(v) -> np.float32:
     """torch.norm(v, 2) in torch's CPU f32 order (8 fma lanes; oracle/uq_eden.py:torch_norm2)."""
     v = np.ascontiguousarray(v, dtype=np.float32).reshape(-1)
     return np.float32(lib().uqo_torch_norm2(_ptr(v), v.shape[0]))
+
+
+def torch_dot(x, y) -> np.float32:
+    """torch.dot(x, y) in MKL sdot's CPU f32 order (oracle/uq_eden.py:torch_dot), exact fmaf."""
+    x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1)
+    y = np.ascontiguousarray(y, dtype=np.float32).reshape(-1)
+    assert x.shape == y.shape
+    return np.float32(lib().uqo_torch_dot(_ptr(x), _ptr(y), x.shape[0]))
 
 
 def torch_sum(v, torch_threads: int = 1):

@@ -1,7 +1,8 @@
 """CPU: the EDEN + RHT restatement (oracle/uq_eden.py) against the reference's own outputs
-(tests/golden/eden_vectors.*, from make_golden_eden.py).  Rotation diagonal and bins are
-bit-exact; the scale (and so the output) within 1e-6 relative: the reference's dot product
-runs in MKL's CPU-dependent order (AS:335), the restatement accumulates it in fp64."""
+(tests/golden/eden_vectors.*, from make_golden_eden.py) and the EDEN scales the reference's
+driver loop recorded (tests/golden/nd_nmse_schemes*.json): rotation diagonal, bins, scale and
+outputs bit for bit.  The scale's torch.dot (AS:335) is restated in MKL sdot's order on the
+fixtures' host (oracle/uq_eden.py:torch_dot, pinned in tests/test_dot_oracle.py)."""
 import numpy as np
 import pytest
 
@@ -38,13 +39,47 @@ def test_eden_oracle_vs_reference(fx):
         bins, scale, _, D = E.eden_compress(x, case["nbits"], case["rseed"])
         assert D == case["D"]
         assert G.sha(bins.astype(np.uint8)) == case["bins_sha"], case["idx"]
-        assert abs(float(scale) - case["scale"]) <= RTOL * abs(case["scale"]), case["idx"]
+        assert np.float32(scale) == np.float32(case["scale"]), case["idx"]       # bit for bit
         out = E.eden_decompress(bins, scale, case["nbits"], case["rseed"], case["d"])
         i = case["idx"]
+        assert G.sha(out) == case["out_sha"], i
         if f"out{i}" in z.files:
-            np.testing.assert_allclose(out, z[f"out{i}"], rtol=RTOL, atol=0)
+            assert G.bits_equal(out, z[f"out{i}"]), i
         else:
-            np.testing.assert_allclose(out[z[f"pos{i}"]], z[f"outs{i}"], rtol=RTOL, atol=0)
+            assert G.bits_equal(out[z[f"pos{i}"]], z[f"outs{i}"]), i
+
+
+ND_GENS = {"normal": lambda d: np.random.normal(0, 1, d),
+           "laplace": lambda d: np.random.laplace(loc=1, scale=2, size=d),
+           "gamma": lambda d: np.random.gamma(shape=2, scale=2, size=d),
+           "bernoulli": lambda d: np.random.choice(np.arange(2), size=d, p=[0.3, 0.7]),
+           "lognormal": lambda d: np.random.lognormal(mean=1, sigma=2, size=d)}
+
+
+@pytest.mark.parametrize("fixture,per_dist", [("nd_nmse_schemes.json", None), ("nd_nmse_schemes_d4194304.json", 1)])
+def test_eden_scales_of_the_reference_loop(fixture, per_dist):
+    """Every EDEN scale the reference's driver loop recorded (EdenSender.compress outputs,
+    make_golden_nmse_schemes.py): d = 2048, all five distributions; at C4's d = 2^22 the first
+    scale of each distribution (the NumPy restatement takes seconds per 2^22 vector; the GPU
+    tests check all of them)."""
+    import json
+    import os
+    ref = json.load(open(os.path.join(G.GOLDEN, fixture)))
+    dim = ref["dim"]
+    checked = 0
+    for dist, entries in ref["eden_scales"].items():
+        st = np.random.get_state()
+        try:
+            np.random.seed(42)                      # ND:14-15, vectors in the loop's order
+            vecs = {(n, inst, j): np.asarray(ND_GENS[dist](dim), np.float64).astype(np.float32)
+                    for n in (1, 6) for inst in range(2) for j in range(n)}
+        finally:
+            np.random.set_state(st)
+        for n, inst, client, bits, seed, sbits in entries[:per_dist]:
+            _, sc, _, _ = E.eden_compress(vecs[(n, inst, client)], bits, seed)
+            assert int(np.float32(sc).view(np.uint32)) == sbits, (dist, n, inst, client, bits)
+            checked += 1
+    assert checked == (140 if per_dist is None else 5)
 
 
 def test_hadamard_is_an_involution_up_to_rounding():

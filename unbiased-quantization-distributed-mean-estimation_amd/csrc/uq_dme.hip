@@ -2404,6 +2404,14 @@ int launch_segnorm(const float* v, int64_t n, int64_t D, char* region, float* nr
     return hip_check(hipGetLastError(), "eden segmented norm launch");
 }
 
+// AS:335: the scale's dot in MKL sdot's order (KE4), scale = f32(nrm * nrm) / dot per client
+int launch_eden_dot(const float* v, int64_t n, int64_t D, float sqrtD, const float* nrm, const EdenTables& tab,
+                    float* scale, hipStream_t st) {
+    hipLaunchKernelGGL(eden_dot_kernel, dim3((unsigned)((n + kDotWaves - 1) / kDotWaves)), dim3(64 * kDotWaves), 0, st,
+                       v, D, sqrtD, nrm, tab, scale, n);
+    return hip_check(hipGetLastError(), "eden_dot_kernel launch");
+}
+
 int launch_chainnorm(const float* v, int64_t n, int64_t D, float* nrm, hipStream_t st) {
     const dim3 grid((unsigned)((n + kNormClients - 1) / kNormClients));
     if (D % kNormChunk == 0)
@@ -2414,7 +2422,7 @@ int launch_chainnorm(const float* v, int64_t n, int64_t D, float* nrm, hipStream
 }
 
 struct EdenLayout {
-    size_t vec_off, nrm_off, part_off, bins_off, scale_off, seg_off, total;
+    size_t vec_off, nrm_off, bins_off, scale_off, seg_off, total;
     int64_t D;
     int32_t tiles;
     bool seg;                 // the segmented norm (its region at seg_off)
@@ -2427,8 +2435,7 @@ EdenLayout eden_layout(int64_t n, int64_t dim) {
     w.tiles = (int32_t)((w.D + kEdenTile - 1) / kEdenTile);
     w.vec_off = kCtrlBytes;
     w.nrm_off = up(w.vec_off + (size_t)n * w.D * sizeof(float));
-    w.part_off = up(w.nrm_off + (size_t)n * sizeof(float));
-    w.bins_off = up(w.part_off + (size_t)n * w.tiles * sizeof(double));
+    w.bins_off = up(w.nrm_off + (size_t)n * sizeof(float));
     w.scale_off = up(w.bins_off + (size_t)n * w.D);
     w.seg_off = up(w.scale_off + (size_t)n * sizeof(float));
     w.seg = segnorm_applies(n, w.D);
@@ -3562,18 +3569,15 @@ int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, 
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     float* nrm = (float*)(wsb + w.nrm_off);
-    double* part = (double*)(wsb + w.part_off);
     FwhtArgs a;
     float* vec = nullptr;
     rc = eden_front(x, n, dim, tab, signs, sign_row, w, wsb, a, &vec, st);
     if (rc) return rc;
     hipLaunchKernelGGL(eden_bins_kernel, dim3((unsigned)w.tiles, (unsigned)n), dim3(256), 0, st, vec, w.D, a.sqrtD,
-                       nrm, tab, bins, part, w.tiles);
-    rc = hip_check(hipGetLastError(), "eden_bins_kernel launch");                  // AS:329-335
+                       nrm, tab, bins);
+    rc = hip_check(hipGetLastError(), "eden_bins_kernel launch");                  // AS:329-333
     if (rc) return rc;
-    hipLaunchKernelGGL(eden_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, w.tiles, nrm, n,
-                       scale);
-    return hip_check(hipGetLastError(), "eden_scale_kernel launch");
+    return launch_eden_dot(vec, n, w.D, a.sqrtD, nrm, tab, scale, st);              // AS:335
 }
 
 int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, int64_t dim, int32_t nbits,
@@ -3620,10 +3624,11 @@ int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbit
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     float* nrm = (float*)(wsb + w.nrm_off);
-    double* part = (double*)(wsb + w.part_off);
     FwhtArgs a;
     float* rot = nullptr;
     rc = eden_front(x, n, dim, tab, signs, sign_row, w, wsb, a, &rot, st);
+    if (rc) return rc;
+    rc = launch_eden_dot(rot, n, w.D, a.sqrtD, nrm, tab, scale, st);                // AS:335 (reads rot first)
     if (rc) return rc;
     // KE3 fused with the receiver's first pass (the bins stay in registers), in place: a
     // workgroup reads its whole 4096-element tile before it writes it
@@ -3632,13 +3637,8 @@ int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbit
     b.in = rot;
     b.out = buf;
     b.nrm = nrm;
-    b.part = part;
     hipLaunchKernelGGL((fwht_low4096_kernel<3, false, false>), dim3((unsigned)w.tiles, (unsigned)n), dim3(256), 0, st, b);
-    rc = hip_check(hipGetLastError(), "fwht_low4096_kernel (bins) launch");        // AS:329-335, 383
-    if (rc) return rc;
-    hipLaunchKernelGGL(eden_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, w.tiles, nrm, n,
-                       scale);
-    rc = hip_check(hipGetLastError(), "eden_scale_kernel launch");
+    rc = hip_check(hipGetLastError(), "fwht_low4096_kernel (bins) launch");        // AS:329-333, 383
     if (rc) return rc;
     FwhtArgs r = a;                                                                  // AS:378-413
     r.scale = scale;

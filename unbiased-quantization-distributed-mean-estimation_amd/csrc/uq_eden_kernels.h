@@ -18,9 +18,18 @@
 //                          lookup (receiver), the last pass / sqrt(D) (and * diag * scale,
 //                          truncation to dim on the receiver)
 //   KE2 eden_norm_kernel   torch.norm(v, 2) in torch CPU order: 8 lanes of fma, lanes in order
-//   KE3 eden_bins_kernel   bucketize -> u8 bins, fp64 partial dot per tile (the round trip
-//                          fuses it into the receiver's first low pass, MODE 3)
-//   KE4 eden_scale_kernel  dot partials in tile order, scale = f32(nrm*nrm) / f32(dot)
+//   KE3 eden_bins_kernel   bucketize -> u8 bins (the round trip fuses it into the
+//                          receiver's first low pass, MODE 3)
+//   KE4 eden_dot_kernel    AS:335 torch.dot(centroids[bins], v) in MKL sdot's order (one wave
+//                          per client, a lane per accumulator lane), scale = f32(nrm*nrm) / dot
+
+// Orders one wave's LDS accesses across lanes: the compiler sees single-lane addresses only
+// (s[i] and s[i + 1] never alias for ONE lane) and could otherwise move a read past another
+// lane's write; the wave's LDS operations themselves execute in program order.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+}
 
 constexpr int kFwhtT = 256;            // threads per FWHT workgroup
 constexpr int kFwhtLowBits = 12;       // first pass: contiguous tiles of 4096
@@ -87,7 +96,7 @@ rht_signs_kernel(const int32_t* __restrict__ seeds, int64_t D, int8_t* __restric
 // value = centroid.  LAST: divide by sqrt(D) as f32 (AS:114); RECV_LAST additionally
 // multiplies by the diagonal and the per-client scale and writes only [0, dim).
 // MODE 3 (fwht_low4096_kernel only, the round trip uq_eden_f32): in = rotated vectors;
-// KE3's bins and partial dots, then the receiver's first pass on the centroids.
+// KE3's bins, then the receiver's first pass on the centroids.
 struct FwhtArgs {
     const void* in;
     float* out;
@@ -95,7 +104,6 @@ struct FwhtArgs {
     const int32_t* sign_row;    // [n] row of each client
     const float* scale;         // [n] (receiver last pass)
     const float* nrm;           // [n] norms (MODE 3)
-    double* part;               // [n][tiles] partial dots (MODE 3)
     int64_t D, dim;
     float sqrtD;
     EdenTables tab;
@@ -193,20 +201,10 @@ __device__ __forceinline__ int pad17(int e) { return e + (e >> 4); }
 // Low pass over 4096 contiguous elements, index e = b0 + 16 b1 + 256 b2: round 1 thread
 // (b1, b2) holds b0 = 0..15 (bits 0-3), round 2 thread (b0, b2) holds b1 (bits 4-7),
 // round 3 thread (b0, b1) holds b2 (bits 8-11).
-// KE3's per-tile fp64 dot: butterfly sums inside each wave, the 4 wave sums in order
-// (one order for both kernels that compute it, so the same partials).
-__device__ __forceinline__ void dot_to_waves(double dot, int tid, double* red) {
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) dot += __shfl_xor(dot, o, kWave);
-    if ((tid & (kWave - 1)) == 0) red[tid / kWave] = dot;
-}
-__device__ __forceinline__ double dot_of_waves(const double* red) { return ((red[0] + red[1]) + red[2]) + red[3]; }
-
 template <int MODE, bool LAST, bool RECV_LAST>
 __global__ void __launch_bounds__(256)
 fwht_low4096_kernel(FwhtArgs a) {
     __shared__ float s[4096 + 256];
-    __shared__ double red[MODE == 3 ? 4 : 1];
     const int64_t vec = blockIdx.y;
     const int tid = threadIdx.x;
     const int64_t D = a.D;
@@ -239,11 +237,9 @@ fwht_low4096_kernel(FwhtArgs a) {
             for (int i = 0; i < 16; ++i) v[i] = a.tab.c[bb[i]];                  // AS:383
         } else if (MODE == 3) {
             // round trip (uq_eden_f32): KE3 on the rotated vector, then the receiver's first
-            // pass on the centroids -- the bins never leave registers.  Same per-thread dot
-            // order and reduction as eden_bins_kernel, so the same partials.
+            // pass on the centroids -- the bins never leave registers (the dot: KE4, before)
             const float* p = (const float*)a.in + vec * D + i0;
             const DivPlan dp = div_plan_norm(a.nrm[vec]);
-            double dot = 0.0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
@@ -257,10 +253,8 @@ fwht_low4096_kernel(FwhtArgs a) {
                     int b = 0;
                     for (int j = 0; j < a.tab.nb; ++j) b += !(a.tab.b[j] >= z) ? 1 : 0;   // NaN -> nb, as torch.bucketize
                     v[4 * q + c] = a.tab.c[b];                                  // AS:383
-                    dot += (double)a.tab.c[b] * (double)xs[c];                  // AS:335
                 }
             }
-            dot_to_waves(dot, tid, red);              // read back after round 1's barrier
         } else {
             const float* p = (const float*)a.in + vec * D + i0;
 #pragma unroll
@@ -275,7 +269,6 @@ fwht_low4096_kernel(FwhtArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[pad17(i + 16 * b1r1 + 256 * b2r1)] = v[i];
     __syncthreads();
-    if (MODE == 3 && tid == 0) a.part[vec * gridDim.x + blockIdx.x] = dot_of_waves(red);
     const int b0 = tid & 15, b2 = tid >> 4;                        // round 2: (b0, b2)
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = s[pad17(b0 + 16 * i + 256 * b2)];
@@ -1011,17 +1004,16 @@ eden_segwalk_kernel(const float* __restrict__ v, int64_t D, const float* __restr
     }
 }
 
-// ---- KE3: bins and partial dots ---------------------------------------------------------
+// ---- KE3: bins --------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 eden_bins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm,
-                 EdenTables tab, uint8_t* __restrict__ bins, double* __restrict__ part, int32_t tiles) {
+                 EdenTables tab, uint8_t* __restrict__ bins) {
     const int64_t vec = blockIdx.y;
     const int tid = threadIdx.x;
     const float nv = nrm[vec];
     const float* p = v + vec * D;
     uint8_t* bp = bins + vec * D;
     const int64_t i0 = (int64_t)blockIdx.x * kEdenTile + (int64_t)tid * 16;
-    double dot = 0.0;
     if (i0 + 16 <= D) {
         float x[16];
 #pragma unroll
@@ -1046,7 +1038,6 @@ eden_bins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const floa
             int b = 0;
             for (int j = 0; j < tab.nb; ++j) b += !(tab.b[j] >= z) ? 1 : 0;   // bucketize, right=False (NaN -> nb)
             w[i >> 2] |= (uint32_t)b << (8 * (i & 3));
-            dot += (double)tab.c[b] * (double)x[i];                // AS:335 dot(centroids[bins], vec)
         }
         *reinterpret_cast<uint4*>(bp + i0) = make_uint4(w[0], w[1], w[2], w[3]);
     } else {
@@ -1056,32 +1047,99 @@ eden_bins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const floa
             int b = 0;
             for (int j = 0; j < tab.nb; ++j) b += !(tab.b[j] >= z) ? 1 : 0;
             bp[i] = (uint8_t)b;
-            dot += (double)tab.c[b] * (double)x;
         }
     }
-    __shared__ double red[4];
-    dot_to_waves(dot, tid, red);
-    __syncthreads();
-    if (tid == 0) part[vec * tiles + blockIdx.x] = dot_of_waves(red);
 }
 
-// ---- KE4: scale per client ---------------------------------------------------------------
-__global__ void __launch_bounds__(256)
-eden_scale_kernel(const double* __restrict__ part, int32_t tiles, const float* __restrict__ nrm, int64_t n,
-                  float* __restrict__ scale) {
-    const int64_t vec = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (vec >= n) return;
-    double dot = 0.0;
-    const double* pp = part + vec * tiles;
-    int t = 0;
-    for (; t + 16 <= tiles; t += 16) {                   // 16 loads in flight, adds in tile order
-        double q[16];
+// ---- KE4: the scale's dot product in MKL sdot's order ------------------------------------
+// AS:335 scale = norm ** 2 / torch.dot(take(centroids, bins), vec).  torch's CPU dot is MKL's
+// sdot; its order on the fixtures' host (oracle/uq_eden.py:torch_dot, tools/dot_order_probe.py,
+// pinned by tests/golden/dot_vectors.json and every EDEN scale the reference recorded): 4
+// accumulators x 16 lanes over 64-element blocks, each lane a sequential fma chain, so element
+// i belongs to chain i % 64 at step i / 64; of a remainder below 64, a 32-element block into
+// accumulators 0 and 1 and then 16-element chunks into accumulator 0 (the last masked: 0 * 0);
+// then (acc0 + acc1) + (acc2 + acc3) lane-wise and the 16 lanes as i + (i + 8), i + (i + 4),
+// (0 + 1) + (2 + 3).  One wave per client: lane l runs chain l over the client's rotated
+// vector (64 consecutive floats per step: one coalesced 256-byte load per wave), recomputing
+// each bin as KE3 does (the same f32 multiply and division), two register sets of kDotU steps
+// of loads in flight.  The chains are the exact reference sums, not an approximation.
+constexpr int kDotWaves = 4;
+constexpr int kDotU = 16;
+
+__device__ __forceinline__ float eden_centroid(const EdenTables& tab, float z) {
+    int b = 0;
+    for (int j = 0; j < tab.nb; ++j) b += !(tab.b[j] >= z) ? 1 : 0;     // bucketize (NaN -> nb)
+    float c = tab.c[0];
+    c = b >= 1 ? tab.c[1] : c;
+    c = b >= 2 ? tab.c[2] : c;
+    c = b >= 3 ? tab.c[3] : c;
+    return c;                                                              // AS:335 take(centroids, bins)
+}
+
+__global__ void __launch_bounds__(64 * kDotWaves)
+eden_dot_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm, EdenTables tab,
+                float* __restrict__ scale, int64_t n) {
+    __shared__ float red[kDotWaves][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * kDotWaves + wv;
+    if (j >= n) return;                                                    // whole wave
+    const float nv = nrm[j];
+    const DivPlan dp = div_plan_norm(nv);
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(v + j * D, (uint32_t)(D * 4));
+    float acc = 0.f;
+    auto step = [&](float x) {                                             // acc = fma(c[bin(x)], x, acc)
+        const float z = div1(x * sqrtD, dp);
+        acc = fmaf(eden_centroid(tab, z), x, acc);
+    };
+    const int64_t steps = D / 64;
+    if (steps >= 2 * kDotU && steps % (2 * kDotU) == 0) {
+        float A[kDotU], B[kDotU];
+        auto load = [&](float (&R)[kDotU], int64_t s0) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) q[k] = pp[t + k];
+            for (int k = 0; k < kDotU; ++k)
+                R[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    rv, (uint32_t)((s0 + k) * 64 + lane) * 4u, 0, kAuxNT));     // beyond D: 0, unused
+        };
+        auto run = [&](const float (&R)[kDotU]) {
+            float ys[kDotU], zs[kDotU];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) dot += q[k];
+            for (int k = 0; k < kDotU; ++k) ys[k] = R[k] * sqrtD;         // AS:329 vec * sqrt(D)
+            div_n(ys, dp, zs);                                             // / norm (exact quotient)
+#pragma unroll
+            for (int k = 0; k < kDotU; ++k) acc = fmaf(eden_centroid(tab, zs[k]), R[k], acc);
+        };
+        load(A, 0);
+        for (int64_t s0 = 0; s0 < steps; s0 += 2 * kDotU) {
+            load(B, s0 + kDotU);
+            run(A);
+            load(A, s0 + 2 * kDotU);
+            run(B);
+        }
+    } else {
+        int64_t i0 = 0;
+        for (; i0 + 64 <= D; i0 += 64) step(v[j * D + i0 + lane]);
+        if (D - i0 >= 32) {                                                // remainder: acc 0 and 1
+            if (lane < 32) step(v[j * D + i0 + lane]);
+            i0 += 32;
+        }
+        for (; i0 < D; i0 += 16)                                           // then acc 0, masked
+            if (lane < 16) {
+                if (i0 + lane < D) step(v[j * D + i0 + lane]);
+                else acc = fmaf(0.f, 0.f, acc);
+            }
     }
-    for (; t < tiles; ++t) dot += pp[t];
-    const float nv = nrm[vec];
-    scale[vec] = (nv * nv) / (float)dot;                    // AS:335 norm ** 2 / dot
+    red[wv][lane] = acc;
+    wave_lds_fence();
+    if (lane == 0) {
+        const float* a = red[wv];
+        float w[16];
+#pragma unroll
+        for (int l = 0; l < 16; ++l) w[l] = (a[l] + a[16 + l]) + (a[32 + l] + a[48 + l]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) w[l] = w[l] + w[l + 8];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) w[l] = w[l] + w[l + 4];
+        const float dot = (w[0] + w[1]) + (w[2] + w[3]);
+        scale[j] = (nv * nv) / dot;                                        // AS:335 norm ** 2 / dot
+    }
 }

@@ -61,14 +61,6 @@ __device__ __forceinline__ void mt_seed(uint32_t* mt, uint32_t seed) {     // in
     for (int i = 1; i < kMtN; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
 }
 
-// Orders one wave's LDS accesses across lanes: the compiler sees single-lane addresses only
-// (s[i] and s[i + 1] never alias for ONE lane) and could otherwise move a read past another
-// lane's write; the wave's LDS operations themselves execute in program order.
-__device__ __forceinline__ void wave_lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
-    __builtin_amdgcn_wave_barrier();
-}
-
 // A block in registers: word 64 g + lane in s[g] (g = 9: lanes < 48).  One wave twists it into
 // the next block (ATen's next_state): word i takes s[i], s[i + 1] (old) and s[(i + 397) % 624],
 // which is old for i < 227 and new (227 words back) otherwise.  Operands move between lanes by
