@@ -297,6 +297,21 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
                            const int32_t* prng_seeds, const uint32_t* px_state, const int32_t* px_seeds,
                            uint32_t* px_state_out, void* X, int32_t x_kind, uint8_t* exact_mask, float* exact_vals,
                            int32_t* exact_count, float* scale, int32_t* info, void* ws, size_t ws_bytes, void* stream);
+/* uq_quicfl_quantize_f32: QUICFL_quantize (All_Schemes.py:814-832) for a batch: the sender of
+ * uq_quicfl_compress_f32 (same arguments, same generators, px_state_out likewise) with the
+ * receiver QuicFLReceiver.decompress (AS:526-535) on each message fused into it: out[j][:dim]
+ * = inverse RHT of (exact ? v : recv_table[X * h_len + h]) / scale, where h is the sender's
+ * own randint stream (the receiver regenerates the same words from the same prng seed).  No
+ * message is written.  recv_table: device f32 [recv_numel] (<= 1024; torch.take's flat index
+ * range, negatives wrap, others flag UQ_QFL_RECV_INDEX: the reference's receiver raises
+ * IndexError after its sender returned).  scale [n] (or NULL) = the messages' scales.  info as
+ * uq_quicfl_compress_f32 plus UQ_QFL_RECV_INDEX.  Workspace: uq_quicfl_workspace_bytes. */
+#define UQ_QFL_RECV_INDEX 64
+int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
+                           const float* table_xp, int64_t table_numel, int32_t h_len, float delta,
+                           const float* recv_table, int32_t recv_numel, const int32_t* prng_seeds,
+                           const uint32_t* px_state, const int32_t* px_seeds, uint32_t* px_state_out, float* out,
+                           float* scale, int32_t* info, void* ws, size_t ws_bytes, void* stream);
 /* xxHash64 of `len` bytes (AS:457 hashes str(seed) with seed 0); host-only, no GPU. */
 uint64_t uq_xxh64(const void* data, size_t len, uint64_t seed);
 int uq_eden_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out);

@@ -214,3 +214,69 @@ def test_batch_states_and_many_messages(fx):
         assert np.array_equal(msg.X[j].cpu().numpy().astype(np.int64), exp["X"]), j
         assert np.float32(msg.scale[j].item()).view(np.uint32) == np.float32(exp["scale"]).view(np.uint32), j
         assert (new[j, 0], new[j, 1]) == (gst[0], gst[1]) and np.array_equal(new[j, 2:], gst[2]), j
+
+
+@pytest.mark.parametrize("hooks", [0, 2])
+def test_fused_quantize_equals_compress_then_decompress(fx, hooks):
+    """quicfl_quantize (uq_quicfl_quantize_f32: the receiver fused into the sender's stage 2 with
+    the sender's own h, AS:526-532) gives the bits of compress -> decompress and the same end
+    generator states, through the team kernels (hooks 0) and the one-wave kernels (hooks 2)."""
+    import uqdme
+    import uqdme_amd.quicfl as q
+    from uqdme_amd._lib import load
+    meta, z, rmeta, rz = fx
+    snd = senders(meta)["pub"]
+    rng = np.random.default_rng(40 + hooks)
+    prev = load().uq_test_set_quicfl_hooks(hooks)
+    try:
+        for nbits, n, dim in ((1, 3, 20000), (2, 2, 4099), (4, 1, 1 << 16), (3, 4, 700)):
+            x = (rng.standard_normal((n, dim)) * 2).astype(np.float32)
+            x[0, 5] = 500.0                                          # exact coordinates too
+            seeds = [int(s) for s in rng.integers(0, 100, n)]
+            rots = [int(s) for s in rng.integers(0, 100, n)]
+            g = torch.Generator()
+            states = []
+            for j in range(n):
+                g.manual_seed(1000 + j)
+                torch.rand(int(rng.integers(0, 700)), generator=g)
+                states.append(q.generator_words(g)[1])
+            states = np.stack(states)
+            msg, new = q.quicfl_compress(torch.from_numpy(x), nbits, seeds, rots, sender=snd, px_states=states,
+                                         x_dtype=torch.int64, _state_out=True)
+            ref = uqdme.quicfl_decompress_messages(msg, rz[f"recv{nbits}"]).cpu().numpy()
+            out, fnew, sc = uqdme.quicfl_quantize(torch.from_numpy(x), nbits, seeds, rots, sender=snd,
+                                                  recv_table=rz[f"recv{nbits}"], px_states=states)
+            assert out.cpu().numpy().view(np.uint32).tolist() == ref.view(np.uint32).tolist(), (nbits, n, dim)
+            assert np.array_equal(fnew, new) and torch.equal(sc, msg.scale)
+    finally:
+        load().uq_test_set_quicfl_hooks(prev)
+
+
+def test_fused_receiver_index_error_after_sender(fx, tmp_path):
+    """A receiver table too short for X * h_len + h: the reference's receiver raises IndexError
+    after its sender returned (the global generator advanced by the sender's draws); the fused
+    drop-in raises the same and leaves the generator where the reference does."""
+    import uqdme
+    meta, z, rmeta, rz = fx
+    for b in (1, 2, 3, 4):
+        fn = str(tmp_path / f"{b}_X_{SR_BITS[b]}_h_256_q_")
+        X, p = sender_tables(b)
+        torch.save(torch.from_numpy(X), fn + "sender_table_X.pt")
+        torch.save(torch.from_numpy(p), fn + "sender_table_p.pt")
+        torch.save(torch.from_numpy(rz[f"recv{b}"][:1]), fn + "recv_table.pt")    # one row only
+        open(fn + "data.txt", "w").write(data_txt(b))
+    uqdme.set_tables_prefix(str(tmp_path))
+    try:
+        x = np.random.default_rng(3).standard_normal(5000).astype(np.float32)
+        torch.manual_seed(77)
+        snd = uqdme.QuicFLSender(prefix=str(tmp_path) + "/")
+        data = {"vec": torch.from_numpy(x), "seed": int(torch.randint(0, 100, (1,)).item()), "nbits": 2,
+                "rotation_seed": 123}
+        snd.compress(data)                                   # what the reference's sender draws
+        expect = state_words()
+        torch.manual_seed(77)
+        with pytest.raises(IndexError):
+            uqdme.QUICFL_quantize(x, 2)
+        assert np.array_equal(state_words(), expect)
+    finally:
+        uqdme.set_tables_prefix(None)

@@ -17,7 +17,7 @@ from .biased import Type_biased_quantize, biased_quantize
 from .eden import (EDEN_quantize_Hadamard, eden_quantize, eden_compress, eden_decompress, EdenMessage, rht_signs,
                    randomized_hadamard_transform, randomized_inverse_hadamard_transform)
 from .quicfl import (QuicFLReceiver, QuicFLSender, QuicFLMessages, QUICFL_quantize, quicfl_compress,
-                     quicfl_decompress, quicfl_decompress_messages, set_tables_prefix)
+                     quicfl_decompress, quicfl_decompress_messages, quicfl_quantize, set_tables_prefix)
 from ._lib import UQError, load as load_library, library_path
 from .distributed import ShardedDME, shard_range, sharded_client_mean, sharded_quantize_mean
 from .dme import DISTRIBUTIONS, nmse_simulation
@@ -27,7 +27,7 @@ from .outpool import set_output_pool
 
 __all__ = [
     "QuicFLReceiver", "QuicFLSender", "QuicFLMessages", "QUICFL_quantize", "quicfl_compress", "quicfl_decompress",
-    "quicfl_decompress_messages", "set_tables_prefix",
+    "quicfl_decompress_messages", "quicfl_quantize", "set_tables_prefix",
     "RATE_TABLE", "rate_to_m", "Type_unbiased_quantize", "quantize_dequantize", "client_mean",
     "quantize_mean", "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
     "check_status", "UQError", "load_library", "library_path", "shard_range", "sharded_client_mean",

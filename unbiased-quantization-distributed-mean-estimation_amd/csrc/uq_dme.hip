@@ -3658,6 +3658,8 @@ int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
     return UQ_OK;
 }
 
+static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, hipStream_t st);
+
 int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
                            const float* table_xp, int64_t table_numel, int32_t h_len, float delta,
                            const int32_t* prng_seeds, const uint32_t* px_state, const int32_t* px_seeds,
@@ -3707,11 +3709,16 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.info = info;
     q.D = w.D;
     q.n = n;
+    return launch_quicfl_send(q, x_kind, st);
+}
+
+// KQ1 / KQ1t by batch size: few messages a workgroup each (scouts + runs: the streams' length
+// is the critical path, not the per-coordinate work); batches a wave per message
+static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, hipStream_t st) {
     const int hooks = g_quicfl_hooks.load();
     q.force_timeout = hooks & 1;
-    // few messages: a workgroup per message (scouts + runs: the streams' length is the critical
-    // path, not the per-coordinate work); batches: a wave per message
-    if (!(hooks & 2) && n <= kQfTeamMaxN && w.D >= (int64_t)kMtN * kQfRuns && w.D <= kQfTeamMaxD) {
+    const int64_t n = q.n;
+    if (!(hooks & 2) && n <= kQfTeamMaxN && q.D >= (int64_t)kMtN * kQfRuns && q.D <= kQfTeamMaxD) {
         if (x_kind == 0)
             hipLaunchKernelGGL(quicfl_send_team_kernel<0>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
         else
@@ -3724,6 +3731,83 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     else
         hipLaunchKernelGGL(quicfl_send_wave_kernel<1>, grid, dim3(64 * kQfWavesPerWG), 0, st, q);
     return hip_check(hipGetLastError(), "quicfl_send_wave_kernel launch");
+}
+
+// QUICFL_quantize (AS:814-832) for a batch: the sender as uq_quicfl_compress_f32 with the
+// receiver fused into its stage 2 (no second h stream, no message in HBM), then the receiver's
+// inverse RHT into out [n][dim].
+int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
+                           const float* table_xp, int64_t table_numel, int32_t h_len, float delta,
+                           const float* recv_table, int32_t recv_numel, const int32_t* prng_seeds,
+                           const uint32_t* px_state, const int32_t* px_seeds, uint32_t* px_state_out, float* out,
+                           float* scale, int32_t* info, void* ws, size_t ws_bytes, void* stream) {
+    if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
+    if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 messages per call");
+    if (dim > ((int64_t)1 << 28)) return fail(UQ_E_INVALID, "dim must be <= 2^28");
+    if (h_len < 1 || h_len > 256) return fail(UQ_E_INVALID, "h_len must be 1..256");
+    if (table_numel < h_len || table_numel % h_len) return fail(UQ_E_INVALID, "table_numel must be a multiple of h_len");
+    if (table_numel >= ((int64_t)1 << 24)) return fail(UQ_E_INVALID, "table_numel must be below 2^24");
+    if (recv_numel < 1 || recv_numel > kQflRecvTab) return fail(UQ_E_INVALID, "receiver table must hold 1..1024 entries");
+    if (n == 0 || dim == 0) return UQ_OK;
+    if (!x || !signs || !table_xp || !recv_table || !prng_seeds || !out || !info)
+        return fail(UQ_E_INVALID, "null pointer");
+    if (!px_state && !px_seeds) return fail(UQ_E_INVALID, "px_state or px_seeds is required");
+    const EdenLayout w = eden_layout(n, dim);
+    const size_t hoff = quicfl_h_off(n, dim);
+    if (!ws || ws_bytes < hoff + (size_t)n * (size_t)w.D) return fail(UQ_E_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* wsb = (char*)ws;
+    FwhtArgs a;
+    float* rot = nullptr;
+    int rc = eden_front(x, n, dim, EdenTables{}, signs, sign_row, w, wsb, a, &rot, st);     // AS:460-470
+    if (rc) return rc;
+    QflSendArgs q{};
+    q.rot = rot;
+    q.nrm = (const float*)(wsb + w.nrm_off);
+    q.tab = (const float2*)table_xp;
+    q.numel = table_numel;
+    q.half = ((table_numel / h_len) - 1) * h_len / 2;                                        // AS:443
+    q.h_len = h_len;
+    q.delta = delta;
+    q.sqrtD = (float)std::sqrt((double)w.D);
+    q.prng_seeds = prng_seeds;
+    q.px_state = px_state;
+    q.px_seeds = px_seeds;
+    q.px_state_out = px_state_out;
+    q.hbuf = (uint8_t*)(wsb + hoff);
+    q.scale = scale;
+    q.info = info;
+    q.D = w.D;
+    q.n = n;
+    q.rtab = recv_table;
+    q.rtab_n = recv_numel;
+    q.pre = rot;                       // in place: a coordinate's rot is loaded a round before its value is stored
+    rc = launch_quicfl_send(q, 0, st);                                                        // AS:455-503, 526-532
+    if (rc) return rc;
+    // AS:533-535: the receiver's inverse RHT (H, then * diag), [:dim]
+    const int p = ilog2_pow2(w.D);
+    int lo = 0, k = std::min(p, kFwhtLowBits);
+    for (;;) {
+        const bool last = lo + k >= p;
+        const int cols = lo == 0 ? 1 : kFwhtCols;
+        const int64_t tiles = w.D / (((int64_t)1 << k) * cols);
+        FwhtArgs b{};
+        b.in = rot;
+        b.out = last ? out : rot;
+        b.signs = signs;
+        b.sign_row = sign_row;
+        b.scale = nullptr;
+        b.D = w.D;
+        b.dim = dim;
+        b.sqrtD = q.sqrtD;
+        const dim3 grid((unsigned)tiles, (unsigned)n);
+        if (last) fwht_dispatch<0, true, true>(grid, b, lo, k, st);
+        else fwht_dispatch<0, false, false>(grid, b, lo, k, st);
+        rc = hip_check(hipGetLastError(), "fwht_pass_kernel launch");
+        if (rc || last) return rc;
+        lo += k;
+        k = std::min(p - lo, kFwhtHighBits);
+    }
 }
 
 // xxHash64 (the public XXH64 algorithm), for AS:457's prng seed

@@ -37,6 +37,7 @@ constexpr int kMtGroups = 10;          // 64-word groups per block (the last one
 constexpr int kQfWavesPerWG = 4;       // messages per workgroup (one wave each)
 constexpr float kQflExactT = 2.8856349124267573f;   // f32(norm.ppf(1 - 2^-9)) (AS:475-478)
 constexpr int kQfStateWords = 2 + kMtN;             // (left, next, words) per generator state
+constexpr int kQflRecvTab = 1024;                    // receiver table entries (LDS), as kQflTab below
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= y >> 11;
@@ -141,6 +142,13 @@ struct QflSendArgs {
     int64_t D;
     int64_t n;
     int32_t force_timeout;      // test hook (uq_test_set_quicfl_hooks): team runs skip their waits
+    // fused receiver (the drop-in, AS:814-832): when `pre` is set, stage 2 writes the receiver's
+    // values before its inverse RHT, pre[i] = (exact ? v : rtab[X * h_len + h]) / scale
+    // (AS:526-532), instead of X / mask / exact values: h is the sender's own (the receiver
+    // regenerates the same randint words from the same seed, AS:465 / AS:528)
+    const float* rtab;          // receiver table (rtab_n <= 1024 floats)
+    int32_t rtab_n;
+    float* pre;                 // [n][D] (may alias rot: each coordinate is read before it is written)
 };
 
 // Round state carried from stage 1 (words, flags, gather issued) to stage 2 (X, stores).
@@ -150,6 +158,7 @@ struct QflRound {
     float v[kMtGroups];
     uint32_t ex;                // bit k: element k of this lane is exact
     uint32_t act;               // bit k: element k of this lane exists
+    uint32_t hp[3];             // h of element k in byte k % 4 of hp[k / 4] (fused receiver)
 };
 
 __device__ __forceinline__ uint32_t qf_off(bool ok, uint32_t off) { return ok ? off : 0xFFFFFFFFu; }  // dropped
@@ -159,9 +168,11 @@ struct QflCtx {
     int64_t row, D;
     int64_t qL, qG;             // block of the first pass-B word of round 0 (local, global)
     int rL, rG;                 // its slot
-    __amdgpu_buffer_rsrc_t rr, rh, rm, rX, rt;
+    __amdgpu_buffer_rsrc_t rr, rh, rm, rX, rt, rP;
     float sc, fh, fhalf, fnumel;
-    DivPlan dp;
+    DivPlan dp, dps;            // / delta (AS:480), / scale (the fused receiver, AS:532)
+    int32_t rtab_n;
+    bool fused;
     int32_t numel;
     uint32_t h_len;
     bool hpow2;
@@ -186,6 +197,10 @@ __device__ __forceinline__ QflCtx qfl_ctx(const QflSendArgs& a, int64_t j, int32
     c.rt = make_rsrc(a.tab, (uint32_t)a.numel * 8u);
     c.sc = (1.0f / a.nrm[j]) * a.sqrtD;                             // AS:466/470 (IEEE 1/x, then f32 mul)
     c.dp = div_plan_norm(a.delta);                                  // q = v / delta: reciprocal + Markstein (exact)
+    c.dps = div_plan_norm(c.sc);
+    c.fused = a.pre != nullptr;
+    c.rP = make_rsrc(c.fused ? (void*)(a.pre + c.row) : (void*)a.rot, c.fused ? Du * 4u : 0u);
+    c.rtab_n = a.rtab_n;
     c.fh = (float)a.h_len;
     c.fhalf = (float)a.half;
     c.fnumel = (float)a.numel;                                      // exact: numel < 2^24 (host check)
@@ -235,7 +250,7 @@ template <int XK>
 __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict__ ev, uint32_t (&sL)[kMtGroups],
                                               uint32_t* WL, int64_t& haveL, uint32_t (&sG)[kMtGroups], uint32_t* WG,
                                               int64_t& haveG, int64_t c0, int64_t c1, int64_t ev_base, int32_t& flags,
-                                              int lane) {
+                                              const float* rtab, int lane) {
     const int64_t D = c.D;
     const float thr = kQflExactT;
     int64_t etot = 0;
@@ -269,6 +284,20 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             flags |= (active && !(tp >= 0.f && tp <= 1.f)) ? UQ_QFL_BAD_PX : 0;
             const float bx = (u24(r.wg[k]) < tp) ? 1.f : 0.f;
             const float xf = tx + bx;                                // AS:489
+            if (c.fused) {                                           // the receiver, AS:526-532
+                const bool ok = xf > -9.2e18f && xf < 9.2e18f;
+                flags |= (active && !ok) ? UQ_QFL_X_RANGE : 0;
+                const int64_t xv = ok ? (int64_t)xf : 0;             // AS:490 .long()
+                const uint32_t h = (r.hp[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                const int64_t it = (int64_t)((uint64_t)xv * (uint64_t)c.h_len + h);   // AS:530 (int64)
+                const bool inr = it >= -(int64_t)c.rtab_n && it < (int64_t)c.rtab_n;
+                flags |= (active && !inr) ? UQ_QFL_RECV_INDEX : 0;
+                const int32_t idx = inr ? (int32_t)(it < 0 ? it + c.rtab_n : it) : 0;   // take wraps negatives
+                const float val = ex ? r.v[k] : (inr ? rtab[idx] : 0.f);                 // AS:531
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(div1(val, c.dps)), c.rP,
+                                                      qf_off(active, i * 4u), 0, 0);   // AS:532 / scale
+                continue;
+            }
             if (XK == 0) {
                 const bool ok = xf > -9.2e18f && xf < 9.2e18f;
                 flags |= (active && !ok) ? UQ_QFL_X_RANGE : 0;
@@ -303,6 +332,7 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
         const int bL = (int)(((c.qL + rd) & 1) * kMtN) + c.rL, bG = (int)(((c.qG + rd) & 1) * kMtN) + c.rG;
         cr.ex = 0;
         cr.act = 0;
+        cr.hp[0] = cr.hp[1] = cr.hp[2] = 0u;
         // AS:472-481: v, the exact mask, q = v / delta for the lane's ten elements at once
         // (exact elements' quotients are discarded, so they stay out of the division's guard)
         float vv[kMtGroups], qq[kMtGroups];
@@ -345,6 +375,7 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             cr.v[k] = v;
             cr.ex |= (active && ex ? 1u : 0u) << k;
             cr.act |= (active ? 1u : 0u) << k;
+            cr.hp[k >> 2] |= (cur.h[k] & 0xFFu) << (8 * (k & 3));
         }
         if (fin) finish(pr, i0 - (uint32_t)kMtN);
     };
@@ -400,6 +431,11 @@ __global__ void __launch_bounds__(64 * kQfWavesPerWG)
 quicfl_send_wave_kernel(QflSendArgs a) {
     __shared__ uint32_t WLsh[kQfWavesPerWG][2 * kMtN];    // local stream ring per wave (first: the seed scratch)
     __shared__ uint32_t WGsh[kQfWavesPerWG][2 * kMtN];    // global stream ring per wave
+    __shared__ float rtab[kQflRecvTab];                   // the fused receiver's table
+    if (a.pre) {
+        for (int i = threadIdx.x; i < a.rtab_n; i += 64 * kQfWavesPerWG) rtab[i] = a.rtab[i];
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
     if (j >= a.n) return;                                       // whole wave: no barrier below
@@ -419,13 +455,13 @@ quicfl_send_wave_kernel(QflSendArgs a) {
     mt_store(sL, WL + (haveL & 1) * kMtN, lane);
     mt_store(sG, WG, lane);
     int32_t flags = 0;
-    const int64_t etot = qfl_pass_b<XK>(c, a.ev, sL, WL, haveL, sG, WG, haveG, 0, nch, 0, flags, lane);
+    const int64_t etot = qfl_pass_b<XK>(c, a.ev, sL, WL, haveL, sG, WG, haveG, 0, nch, 0, flags, rtab, lane);
     for (int s = 32; s >= 1; s >>= 1) flags |= __shfl_xor(flags, s);
     if (a.px_state_out)
         qfl_state_out(a.px_state_out + j * kQfStateWords, sG, a.D, gleft, gnext, c.qG * kMtN + c.rG, lane);
     if (lane == 0) {
-        a.ecount[j] = (int32_t)etot;
-        a.scale[j] = c.sc;
+        if (a.ecount) a.ecount[j] = (int32_t)etot;
+        if (a.scale) a.scale[j] = c.sc;
         a.info[j] = flags;
     }
 }
@@ -489,8 +525,11 @@ quicfl_send_team_kernel(QflSendArgs a) {
     __shared__ int rdy[kQfRuns][3];
     __shared__ int64_t cnt[kQfRuns];
     __shared__ int32_t sflags;
+    __shared__ float rtab[kQflRecvTab];                  // the fused receiver's table
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t j = blockIdx.x;
+    if (a.pre)
+        for (int i = threadIdx.x; i < a.rtab_n; i += 64 * kQfTeamWaves) rtab[i] = a.rtab[i];
     const int64_t D = a.D;
     const int64_t nch = (D + kMtN - 1) / kMtN;
     // run r takes rounds [cb[r], cb[r + 1]): lengths shrinking by kQfRunRatio, since a later
@@ -555,7 +594,7 @@ quicfl_send_team_kernel(QflSendArgs a) {
                 mt_load(sL, WL[r] + (haveL & 1) * kMtN, lane);
                 mt_load(sG, WG[r] + (haveG & 1) * kMtN, lane);
                 const int64_t e = qfl_pass_b<XK>(c, a.ev, sL, WL[r], haveL, sG, WG[r], haveG, c0, c1, c0 * kMtN, flags,
-                                                 lane);
+                                                 rtab, lane);
                 if (lane == 0) cnt[r] = e;
                 if (c1 == nch && a.px_state_out)
                     qfl_state_out(a.px_state_out + j * kQfStateWords, sG, D, gleft, gnext, c.qG * kMtN + c.rG, lane);
@@ -569,7 +608,7 @@ quicfl_send_team_kernel(QflSendArgs a) {
     __syncthreads();
     if (wv == 0) {                                       // exact values of run r: [c0*624, +cnt) -> index order
         int64_t base = 0;
-        for (int r = 0; r < kQfRuns; ++r) {
+        for (int r = 0; r < kQfRuns && !c.fused; ++r) {
             const int64_t src = cb[r] * kMtN, n_r = cnt[r];
             for (int64_t i0 = 0; i0 < n_r; i0 += 64) {   // (base <= src: a downward move, chunk by chunk)
                 const int64_t i = i0 + lane;
@@ -579,8 +618,8 @@ quicfl_send_team_kernel(QflSendArgs a) {
             base += n_r;
         }
         if (lane == 0) {
-            a.ecount[j] = (int32_t)base;
-            a.scale[j] = c.sc;
+            if (a.ecount) a.ecount[j] = (int32_t)base;
+            if (a.scale) a.scale[j] = c.sc;
             a.info[j] = sflags;
         }
     }

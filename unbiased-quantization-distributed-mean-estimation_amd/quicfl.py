@@ -37,10 +37,10 @@ from .eden import _sign_rows, padded_dim, randomized_inverse_hadamard_transform
 from .quantizer import _as_device_f32_2d, _device, _ptr, _stream_ptr, _workspace
 
 __all__ = ["QuicFLReceiver", "QuicFLSender", "QuicFLMessages", "QUICFL_quantize", "quicfl_compress",
-           "quicfl_decompress", "quicfl_decompress_messages", "prng_seed", "set_tables_prefix"]
+           "quicfl_decompress", "quicfl_decompress_messages", "quicfl_quantize", "prng_seed", "set_tables_prefix"]
 
 STATE_WORDS = 626                  # UQ_QFL_STATE_WORDS: (left, next, 624 words)
-_FLAG_P, _FLAG_INDEX, _FLAG_PX, _FLAG_X, _FLAG_TIMEOUT, _FLAG_EXACT = 1, 2, 4, 8, 16, 32   # UQ_QFL_*
+_FLAG_P, _FLAG_INDEX, _FLAG_PX, _FLAG_X, _FLAG_TIMEOUT, _FLAG_EXACT, _FLAG_RECV_INDEX = 1, 2, 4, 8, 16, 32, 64  # UQ_QFL_*
 _tables_prefix = None
 _dropin_lock = threading.Lock()
 _dropin: dict = {}
@@ -207,6 +207,45 @@ def _ws(n, d, dev):
     return _workspace(dev, int(b.value))
 
 
+def _send_inputs(ps, n, px_seeds, px_states, dev):
+    """The small per-message inputs in ONE host-to-device copy (prng seeds, then the generator
+    states or the px seeds): each pageable copy would otherwise wait for the stream on its own.
+    -> (prng seeds, states or None, px seeds or None, state words out)."""
+    if px_states is not None:
+        w = np.asarray(px_states, np.uint32).reshape(n, STATE_WORDS)
+        for r in w:
+            _check_state(r)
+        tail = w.view(np.int32).reshape(-1)
+    else:
+        if px_seeds is None:
+            raise ValueError("px_seeds or px_states is required")
+        pxs = np.asarray(torch.as_tensor(px_seeds, dtype=torch.int64).reshape(-1).numpy(), np.int64)
+        if pxs.size != n:
+            raise ValueError("one px seed per message")
+        tail = (pxs & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+    hin = np.empty(n + tail.size, np.int32)
+    hin[:n] = ps.numpy().astype(np.int32)
+    hin[n:] = tail
+    din = torch.from_numpy(hin).to(dev)
+    ps_d, tail_d = din[:n], din[n:]
+    if px_states is not None:
+        return ps_d, tail_d.view(n, STATE_WORDS), None, n * STATE_WORDS
+    return ps_d, None, tail_d, 0
+
+
+def _raise_send_flags(flags: int) -> None:
+    if flags & _FLAG_P:
+        raise RuntimeError("Expected p_in >= 0 && p_in <= 1 to be true, but got false.")   # AS:484 bernoulli
+    if flags & _FLAG_INDEX:
+        raise IndexError("out of range: a sender-table index outside the table (AS:486 torch.take)")
+    if flags & _FLAG_PX:
+        raise RuntimeError("Expected p_in >= 0 && p_in <= 1 to be true, but got false.")   # AS:489 bernoulli
+    if flags & _FLAG_X:
+        raise OverflowError("X outside 0..255: use x_dtype=torch.int64")
+    if flags & _FLAG_TIMEOUT:
+        raise RuntimeError("uq_quicfl_compress_f32: internal wait ran out (results invalid)")
+
+
 def quicfl_compress(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSender, px_seeds=None, px_states=None,
                     x_dtype=torch.uint8, _state_out: bool = False):
     """QuicFLSender.compress (AS:455-503) for every row of x [n, d].  seeds: the messages'
@@ -231,32 +270,10 @@ def quicfl_compress(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSende
     mask = torch.empty((n, D), dtype=torch.bool, device=dev)
     ev = torch.empty((n, D), dtype=torch.float32, device=dev)
     scale = torch.empty(n, dtype=torch.float32, device=dev)
-    # the small per-message inputs go over in ONE host-to-device copy (prng seeds, then the
-    # generator states or px seeds) and the small outputs come back in ONE copy (flags, exact
-    # counts, end states): each pageable copy would otherwise wait for the stream on its own
-    if px_states is not None:
-        w = np.asarray(px_states, np.uint32).reshape(n, STATE_WORDS)
-        for r in w:
-            _check_state(r)
-        tail = w.view(np.int32).reshape(-1)
-    else:
-        if px_seeds is None:
-            raise ValueError("px_seeds or px_states is required")
-        pxs = np.asarray(torch.as_tensor(px_seeds, dtype=torch.int64).reshape(-1).numpy(), np.int64)
-        if pxs.size != n:
-            raise ValueError("one px seed per message")
-        tail = (pxs & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
-    hin = np.empty(n + tail.size, np.int32)
-    hin[:n] = ps.numpy().astype(np.int32)
-    hin[n:] = tail
-    din = torch.from_numpy(hin).to(dev)
-    ps_d, tail_d = din[:n], din[n:]
-    nst = n * STATE_WORDS if px_states is not None else 0
+    ps_d, st_in, pxs_d, nst = _send_inputs(ps, n, px_seeds, px_states, dev)
     dout = torch.zeros(2 * n + nst, dtype=torch.int32, device=dev)
     info, cnt_d = dout[:n], dout[n:2 * n]
-    st_in = tail_d.view(n, STATE_WORDS) if px_states is not None else None
-    pxs_d = tail_d if px_states is None else None
-    st_out = dout[2 * n:].view(n, STATE_WORDS) if px_states is not None else None
+    st_out = dout[2 * n:].view(n, STATE_WORDS) if nst else None
     hout = np.zeros(2 * n + nst, np.int32)
     if n and d:
         tab, rows = _sign_rows(rs, D, dev)
@@ -268,17 +285,7 @@ def quicfl_compress(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSende
             _ptr(X), 0 if x_dtype == torch.int64 else 1, _ptr(mask), _ptr(ev), _ptr(cnt_d), _ptr(scale), _ptr(info),
             _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_quicfl_compress_f32")
         hout = dout.cpu().numpy()
-        flags = int(np.bitwise_or.reduce(hout[:n])) if n else 0
-        if flags & _FLAG_P:
-            raise RuntimeError("Expected p_in >= 0 && p_in <= 1 to be true, but got false.")   # AS:484 bernoulli
-        if flags & _FLAG_INDEX:
-            raise IndexError("out of range: a sender-table index outside the table (AS:486 torch.take)")
-        if flags & _FLAG_PX:
-            raise RuntimeError("Expected p_in >= 0 && p_in <= 1 to be true, but got false.")   # AS:489 bernoulli
-        if flags & _FLAG_X:
-            raise OverflowError("X outside 0..255: use x_dtype=torch.int64")
-        if flags & _FLAG_TIMEOUT:
-            raise RuntimeError("uq_quicfl_compress_f32: internal wait ran out (results invalid)")
+        _raise_send_flags(int(np.bitwise_or.reduce(hout[:n])) if n else 0)
     msg = QuicFLMessages(X=X, exact_mask=mask, exact_vals=ev, exact_count=torch.from_numpy(hout[n:2 * n].copy()),
                          scale=scale, prng_seeds=ps, rotation_seeds=rs, dim=d, nbits=nbits, h_len=int(dd["h_len"]))
     if _state_out:
@@ -448,25 +455,89 @@ def _dropin_pair():
     return pair
 
 
+def quicfl_quantize(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSender, recv_table, px_seeds=None,
+                    px_states=None, _host_out: bool = False):
+    """QUICFL_quantize (AS:814-832) on every row of x [n, d]: the sender of quicfl_compress with
+    the receiver (AS:526-535, recv_table) fused into it (uq_quicfl_quantize_f32: the receiver's
+    h is the sender's own randint stream, so it is not regenerated, and no message is written),
+    then the inverse RHT.  Returns (out [n, d], end states [n, 626] or None, scale [n]).
+    Raises like the sender, then like the receiver (IndexError from its take, AS:530)."""
+    dev = _device()
+    dd = sender.data[nbits]
+    x = _as_device_f32_2d(x, dev)
+    n, d = x.shape
+    D = padded_dim(d)
+    s = [int(v) for v in torch.as_tensor(seeds).reshape(-1).tolist()] if not isinstance(seeds, (list, tuple)) else list(seeds)
+    rs = torch.as_tensor(rotation_seeds, dtype=torch.int64).reshape(-1)
+    if len(s) != n or rs.numel() != n:
+        raise ValueError("one seed and one rotation seed per message")
+    ps = torch.tensor([prng_seed(v) for v in s], dtype=torch.int64)
+    rt = torch.as_tensor(recv_table, dtype=torch.float32).to(dev).contiguous().reshape(-1)
+    ps_d, st_in, pxs_d, nst = _send_inputs(ps, n, px_seeds, px_states, dev)
+    out = torch.empty((n, d), dtype=torch.float32, device=dev)
+    scale = torch.empty(n, dtype=torch.float32, device=dev)
+    dout = torch.zeros(n + nst, dtype=torch.int32, device=dev)
+    info = dout[:n]
+    st_out = dout[n:].view(n, STATE_WORDS) if nst else None
+    if n and d:
+        tab, rows = _sign_rows(rs, D, dev)
+        xp = sender.table_xp(nbits, dev)
+        ws = _ws(n, d, dev)
+        _lib.check(_lib.load().uq_quicfl_quantize_f32(
+            _ptr(x), n, d, _ptr(tab), _ptr(rows), _ptr(xp), xp.shape[0], int(dd["h_len"]),
+            float(np.float32(dd["delta"])), _ptr(rt), rt.numel(), _ptr(ps_d), _ptr(st_in), _ptr(pxs_d), _ptr(st_out),
+            _ptr(out), _ptr(scale), _ptr(info), _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_quicfl_quantize_f32")
+    if _host_out:                          # the result and the flags / states in one synchronisation
+        host = torch.empty(out.numel(), dtype=torch.float32, pin_memory=True)
+        hsmall = torch.empty(dout.numel(), dtype=torch.int32, pin_memory=True)
+        host.copy_(out.view(-1), non_blocking=True)
+        hsmall.copy_(dout, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        out, hout = host.view(n, d), hsmall.numpy()
+    else:
+        hout = dout.cpu().numpy()
+    flags = int(np.bitwise_or.reduce(hout[:n])) if n else 0
+    _raise_send_flags(flags)
+    new = hout[n:].reshape(n, STATE_WORDS).view(np.uint32).copy() if nst else None
+    if flags & _FLAG_RECV_INDEX:           # the sender returned (its draws happened), the receiver raises
+        raise _RecvIndexError(new)
+    return out, new, scale
+
+
+class _RecvIndexError(IndexError):
+    """The receiver's take raised after the sender had drawn (the caller restores the states)."""
+
+    def __init__(self, states):
+        super().__init__("index out of range in self (AS:530 recv_table.take)")
+        self.states = states
+
+
 def QUICFL_quantize(input_vector, bits_per_dimension=1):
     """Drop-in for AS:814-832 (same name for the drivers' result keys): one torch.randint(0, 100)
-    draw of the global CPU generator (the message seed), compress (bernoulli(p_X) from the same
-    generator), decompress; returns a NumPy f32 array of length d."""
+    draw of the global CPU generator (the message seed), the sender (bernoulli(p_X) from the same
+    generator, left where the reference leaves it) and the receiver fused in one pass
+    (quicfl_quantize); returns a NumPy f32 array of length d."""
     dev = _device()
     if torch.is_tensor(input_vector):
         v = input_vector.detach().to(device=dev, dtype=torch.float32).reshape(-1)
     else:
         v = torch.tensor(np.asarray(input_vector), dtype=torch.float32, device=dev).reshape(-1)
     sender, receiver = _dropin_pair()
-    data = {"vec": v, "seed": int(torch.randint(0, 100, (1,)).item()), "nbits": bits_per_dimension,
-            "rotation_seed": 123, "nlevels": 2 ** bits_per_dimension}
-    data = sender.compress(data)
-    out, info = receiver.decompress(data, _defer_check=True)
-    # the result and the receiver's flags come back in one synchronisation
-    host = torch.empty(out.numel(), dtype=torch.float32, pin_memory=True)
-    hflag = torch.empty(1, dtype=torch.int32, pin_memory=True)
-    host.copy_(out, non_blocking=True)
-    hflag.copy_(info, non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
-    _raise_recv_flags(int(hflag[0]))
-    return host.numpy()
+    seed = int(torch.randint(0, 100, (1,)).item())
+    nbits = bits_per_dimension
+    sender.data[nbits]                                                    # KeyError like the sender
+    if v.numel() == 0:
+        raise ValueError("empty vector (the reference's RHT and norm of an empty vector are degenerate)")
+    if nbits not in receiver.recv_table:                                  # the reference's receiver raises
+        sender.compress({"vec": v, "seed": seed, "nbits": nbits, "rotation_seed": 123})   # after its sender
+        receiver.recv_table[nbits]
+    gen = torch.default_generator
+    st, words = generator_words(gen)
+    try:
+        out, new, _ = quicfl_quantize(v.view(1, -1), nbits, [seed], [123], sender=sender,
+                                      recv_table=receiver._table(nbits), px_states=words[None, :], _host_out=True)
+    except _RecvIndexError as e:
+        set_generator_words(gen, st, e.states[0])
+        raise IndexError(str(e)) from None
+    set_generator_words(gen, st, new[0])
+    return out.view(-1).numpy()
