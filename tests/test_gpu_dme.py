@@ -120,10 +120,12 @@ def test_multi_scheme_nmse_known_answers(gpu_ready, fixture):
             assert np.array_equal(mine[key].view(np.uint32), np.asarray(sc_ref, np.uint32)), (dist, key)
 
 
-def test_nd_loop_with_quicfl_known_answers(gpu_ready):
+@pytest.mark.parametrize("fixture", ["nd_nmse_schemes_quicfl.json", "nd_nmse_schemes_d4194304_quicfl.json"])
+def test_nd_loop_with_quicfl_known_answers(gpu_ready, fixture):
     """The driver loop with QUICFL_quantize in its place (ND:141-142, after the biased
     quantizer) against the reference's own loop on synthetic sender tables
-    (tests/golden/nd_nmse_schemes_quicfl.json, make_golden_nmse_schemes.py --quicfl): the
+    (tests/golden/nd_nmse_schemes_quicfl.json at d = 2048 and nd_nmse_schemes_d4194304_quicfl.json
+    at config C4's d = 2^22, normal and laplace; make_golden_nmse_schemes.py --quicfl): the
     QUIC-FL draws (a message seed, then D bernoulli(p_X) words of the global generator per
     call) interleave with EDEN's and the unbiased quantizer's, so every scheme's NMSE is
     checked within 1e-6 relative, QUIC-FL bit for bit.""" 
@@ -134,7 +136,7 @@ def test_nd_loop_with_quicfl_known_answers(gpu_ready):
     from tests.golden_data import GOLDEN
     sys.path.insert(0, GOLDEN)
     from quicfl_tables import DATA, sender_tables
-    ref = json.load(open(os.path.join(GOLDEN, "nd_nmse_schemes_quicfl.json")))
+    ref = json.load(open(os.path.join(GOLDEN, fixture)))
     rz = np.load(os.path.join(GOLDEN, "quicfl_recv_vectors.npz"))
     tx = uqdme.QuicFLSender(tables={b: (*sender_tables(b), DATA[b]) for b in (1, 2, 3, 4)})
     rx = uqdme.QuicFLReceiver(tables={b: rz[f"recv{b}"] for b in (1, 2, 3, 4)})

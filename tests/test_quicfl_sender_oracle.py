@@ -161,3 +161,26 @@ def test_large_message_sha(fx):
         k = c["idx"]
         assert z[f"rxs{k}"].size == 4096 and len(c["rx_sha"]) == 64
     assert hashlib  # the sha itself is checked on the GPU (tests/test_gpu_quicfl_sender.py)
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_oracle_matches_reference_sender_2pow22(k):
+    """Config C4's size (tests/golden/make_golden_quicfl_c4.py): the reference's messages at
+    D = 2^22 (padded dim 2^22 - 5 at 1 bit; 2^22 at 2 bits, generator one block in) by SHA-256
+    of X, the mask and the exact values, the scale and the generator's end state."""
+    from quicfl_tables import DATA
+    meta = json.load(open(os.path.join(HERE, "quicfl_c4_vectors.json")))
+    z = np.load(os.path.join(HERE, "quicfl_c4_vectors.npz"))
+    c = meta["cases"][k]
+    x = gen(c["kind"], c["vseed"], c["dim"])
+    st = Q.seeded_state(c["gseed"])
+    if c["pre"]:
+        _, st = Q.mt_draw(st, c["pre"])
+    tX, tp = sender_tables(c["nbits"])
+    msg, gst = Q.compress(x, c["nbits"], c["seed"], 123, tX, tp, DATA[c["nbits"]]["delta"], DATA[c["nbits"]]["h_len"], st)
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+    assert sha(msg["X"].astype(np.int64)) == c["X_sha"]
+    assert sha(msg["exact_indeces"].astype(np.bool_)) == c["mask_sha"]
+    assert sha(msg["exact_values"].astype(np.float32)) == c["ev_sha"]
+    assert int(np.float32(msg["scale"]).view(np.uint32)) == c["scale_bits"]
+    assert (gst[0], gst[1]) == (c["left1"], c["next1"]) and np.array_equal(gst[2], z[f"st1_{k}"])

@@ -2404,12 +2404,13 @@ int launch_segnorm(const float* v, int64_t n, int64_t D, char* region, float* nr
     return hip_check(hipGetLastError(), "eden segmented norm launch");
 }
 
-// AS:335: the scale's dot in MKL sdot's order (KE4), scale = f32(nrm * nrm) / dot per client
-int launch_eden_dot(const float* v, int64_t n, int64_t D, float sqrtD, const float* nrm, const EdenTables& tab,
-                    float* scale, hipStream_t st) {
-    hipLaunchKernelGGL(eden_dot_kernel, dim3((unsigned)((n + kDotWaves - 1) / kDotWaves)), dim3(64 * kDotWaves), 0, st,
-                       v, D, sqrtD, nrm, tab, scale, n);
-    return hip_check(hipGetLastError(), "eden_dot_kernel launch");
+// AS:329-335: the bins and the scale's dot in MKL sdot's order (KE4), scale = f32(nrm * nrm) / dot
+int launch_eden_dotbins(const float* v, int64_t n, int64_t D, float sqrtD, const float* nrm, const EdenTables& tab,
+                        uint8_t* bins, float* scale, hipStream_t st) {
+    const dim3 grid((unsigned)((n + kDotWaves - 1) / kDotWaves)), block(64 * kDotWaves);
+    if (tab.nb == 1) hipLaunchKernelGGL(eden_dotbins_kernel<1>, grid, block, 0, st, v, D, sqrtD, nrm, tab, bins, scale, n);
+    else hipLaunchKernelGGL(eden_dotbins_kernel<3>, grid, block, 0, st, v, D, sqrtD, nrm, tab, bins, scale, n);
+    return hip_check(hipGetLastError(), "eden_dotbins_kernel launch");
 }
 
 int launch_chainnorm(const float* v, int64_t n, int64_t D, float* nrm, hipStream_t st) {
@@ -3573,11 +3574,7 @@ int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, 
     float* vec = nullptr;
     rc = eden_front(x, n, dim, tab, signs, sign_row, w, wsb, a, &vec, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(eden_bins_kernel, dim3((unsigned)w.tiles, (unsigned)n), dim3(256), 0, st, vec, w.D, a.sqrtD,
-                       nrm, tab, bins);
-    rc = hip_check(hipGetLastError(), "eden_bins_kernel launch");                  // AS:329-333
-    if (rc) return rc;
-    return launch_eden_dot(vec, n, w.D, a.sqrtD, nrm, tab, scale, st);              // AS:335
+    return launch_eden_dotbins(vec, n, w.D, a.sqrtD, nrm, tab, bins, scale, st);   // AS:329-335
 }
 
 int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, int64_t dim, int32_t nbits,
@@ -3604,45 +3601,14 @@ int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, i
 
 int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
                 const int32_t* sign_row, float* scale_out, void* ws, size_t ws_bytes, void* stream) {
+    // compress (RHT, norm, bins + the MKL-order dot) then decompress: the receiver's first
+    // pass reads the 1-byte bins KE4 wrote instead of the 4-byte rotated vector
     const EdenLayout w = eden_layout(n < 0 ? 0 : n, dim < 0 ? 0 : dim);
     uint8_t* bins = (uint8_t*)((char*)ws + w.bins_off);
     float* scale = scale_out ? scale_out : (float*)((char*)ws + w.scale_off);
-    if (w.D <= ((int64_t)1 << kFwhtLowBits) || n > 65535 || w.D == ((int64_t)1 << (kFwhtLow16Bits + kFwhtHighBits))) {
-        // a single FWHT pass (or an invalid n, reported there), or D = 2^22 whose 14 + 8
-        // passes (two each way, without the fused bins of the 12-bit pass) move fewer bytes
-        // than the fused 12 + 8 + 2: compress, then decompress
-        int rc = uq_eden_compress_f32(x, n, dim, nbits, signs, sign_row, bins, scale, ws, ws_bytes, stream);
-        if (rc) return rc;
-        return uq_eden_decompress_f32(bins, scale, n, dim, nbits, signs, sign_row, out, ws, ws_bytes, stream);
-    }
-    EdenTables tab;
-    int rc = eden_check(n, dim, nbits, signs, &tab);
+    int rc = uq_eden_compress_f32(x, n, dim, nbits, signs, sign_row, bins, scale, ws, ws_bytes, stream);
     if (rc) return rc;
-    if (n == 0 || dim == 0) return UQ_OK;
-    if (!x || !out) return fail(UQ_E_INVALID, "null pointer");
-    if (!ws || ws_bytes < w.total) return fail(UQ_E_WORKSPACE, "workspace too small");
-    hipStream_t st = (hipStream_t)stream;
-    char* wsb = (char*)ws;
-    float* nrm = (float*)(wsb + w.nrm_off);
-    FwhtArgs a;
-    float* rot = nullptr;
-    rc = eden_front(x, n, dim, tab, signs, sign_row, w, wsb, a, &rot, st);
-    if (rc) return rc;
-    rc = launch_eden_dot(rot, n, w.D, a.sqrtD, nrm, tab, scale, st);                // AS:335 (reads rot first)
-    if (rc) return rc;
-    // KE3 fused with the receiver's first pass (the bins stay in registers), in place: a
-    // workgroup reads its whole 4096-element tile before it writes it
-    float* buf = rot;
-    FwhtArgs b = a;
-    b.in = rot;
-    b.out = buf;
-    b.nrm = nrm;
-    hipLaunchKernelGGL((fwht_low4096_kernel<3, false, false>), dim3((unsigned)w.tiles, (unsigned)n), dim3(256), 0, st, b);
-    rc = hip_check(hipGetLastError(), "fwht_low4096_kernel (bins) launch");        // AS:329-333, 383
-    if (rc) return rc;
-    FwhtArgs r = a;                                                                  // AS:378-413
-    r.scale = scale;
-    return launch_fwht(r, n, true, buf, out, st, nullptr, kFwhtLowBits);
+    return uq_eden_decompress_f32(bins, scale, n, dim, nbits, signs, sign_row, out, ws, ws_bytes, stream);
 }
 
 // ---- QUIC-FL sender ----------------------------------------------------------------------

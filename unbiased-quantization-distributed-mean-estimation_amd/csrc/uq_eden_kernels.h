@@ -18,10 +18,10 @@
 //                          lookup (receiver), the last pass / sqrt(D) (and * diag * scale,
 //                          truncation to dim on the receiver)
 //   KE2 eden_norm_kernel   torch.norm(v, 2) in torch CPU order: 8 lanes of fma, lanes in order
-//   KE3 eden_bins_kernel   bucketize -> u8 bins (the round trip fuses it into the
-//                          receiver's first low pass, MODE 3)
-//   KE4 eden_dot_kernel    AS:335 torch.dot(centroids[bins], v) in MKL sdot's order (one wave
-//                          per client, a lane per accumulator lane), scale = f32(nrm*nrm) / dot
+//   KE4 eden_dotbins_kernel bucketize -> u8 bins and AS:335 torch.dot(centroids[bins], v) in
+//                          MKL sdot's order (one wave per client, a lane per accumulator
+//                          lane), scale = f32(nrm*nrm) / dot; the receiver's first pass reads
+//                          the bins (MODE 2)
 
 // Orders one wave's LDS accesses across lanes: the compiler sees single-lane addresses only
 // (s[i] and s[i + 1] never alias for ONE lane) and could otherwise move a read past another
@@ -45,6 +45,31 @@ struct EdenTables {
     float b[3];      // boundaries, 2^nbits - 1 entries
     int nb;          // number of boundaries
 };
+
+// torch.bucketize(z, boundaries) (right=False: boundaries strictly below z; NaN -> nb) and
+// take(centroids, bin) with the table in registers: a dynamically indexed kernel-argument array
+// is read from memory per element, and the compiler turns a select chain over its entries back
+// into such a load unless the values are opaque (the empty asm)
+struct EdenCents {
+    float c0, c1, c2, c3;
+};
+__device__ __forceinline__ EdenCents eden_cents(const EdenTables& t) {
+    EdenCents r{t.c[0], t.c[1], t.c[2], t.c[3]};
+    __asm__ volatile("" : "+v"(r.c0), "+v"(r.c1), "+v"(r.c2), "+v"(r.c3));
+    return r;
+}
+__device__ __forceinline__ int eden_bin(const EdenTables& t, float z) {
+    int b = !(t.b[0] >= z) ? 1 : 0;
+    if (t.nb > 1) b += (!(t.b[1] >= z) ? 1 : 0) + (!(t.b[2] >= z) ? 1 : 0);
+    return b;
+}
+__device__ __forceinline__ float eden_cent(const EdenCents& t, int b) {
+    // bit masks instead of selects (a select chain is rewritten into an indexed table load)
+    const uint32_t m0 = 0u - (uint32_t)(b == 0), m1 = 0u - (uint32_t)(b == 1), m2 = 0u - (uint32_t)(b == 2),
+                   m3 = 0u - (uint32_t)(b == 3);
+    return __uint_as_float((__float_as_uint(t.c0) & m0) | (__float_as_uint(t.c1) & m1) |
+                           (__float_as_uint(t.c2) & m2) | (__float_as_uint(t.c3) & m3));
+}
 
 // ---- KE0: MT19937 -> diagonal ---------------------------------------------------------
 // One workgroup per seed; the in-place twist runs in its three dependency phases
@@ -95,15 +120,12 @@ rht_signs_kernel(const int32_t* __restrict__ seeds, int64_t D, int8_t* __restric
 // `dim`, zero-padded, times the diagonal.  MODE 2 (first receiver pass): in = u8 bins,
 // value = centroid.  LAST: divide by sqrt(D) as f32 (AS:114); RECV_LAST additionally
 // multiplies by the diagonal and the per-client scale and writes only [0, dim).
-// MODE 3 (fwht_low4096_kernel only, the round trip uq_eden_f32): in = rotated vectors;
-// KE3's bins, then the receiver's first pass on the centroids.
 struct FwhtArgs {
     const void* in;
     float* out;
     const int8_t* signs;        // [rows][D] diagonal rows
     const int32_t* sign_row;    // [n] row of each client
     const float* scale;         // [n] (receiver last pass)
-    const float* nrm;           // [n] norms (MODE 3)
     int64_t D, dim;
     float sqrtD;
     EdenTables tab;
@@ -140,7 +162,7 @@ fwht_pass_kernel(FwhtArgs a, int lo, int k) {
             v = v * (float)sg[i];                               // AS:132/137 * diag
         } else if (MODE == 2) {
             const uint8_t* bins = (const uint8_t*)a.in + vec * D;
-            v = a.tab.c[bins[i]];                               // AS:383 take(centroids, bins)
+            v = eden_cent(eden_cents(a.tab), bins[i]);          // AS:383 take(centroids, bins)
         } else {
             v = ((const float*)a.in)[vec * D + i];
         }
@@ -208,6 +230,7 @@ fwht_low4096_kernel(FwhtArgs a) {
     const int64_t vec = blockIdx.y;
     const int tid = threadIdx.x;
     const int64_t D = a.D;
+    const EdenCents cs = eden_cents(a.tab);
     const int64_t base = (int64_t)blockIdx.x * 4096;
     const int8_t* sg = a.signs + (int64_t)(a.sign_row ? a.sign_row[vec] : 0) * D;
     float v[16];
@@ -234,27 +257,7 @@ fwht_low4096_kernel(FwhtArgs a) {
             const int4 bv = *reinterpret_cast<const int4*>((const uint8_t*)a.in + vec * D + i0);
             const uint8_t* bb = reinterpret_cast<const uint8_t*>(&bv);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = a.tab.c[bb[i]];                  // AS:383
-        } else if (MODE == 3) {
-            // round trip (uq_eden_f32): KE3 on the rotated vector, then the receiver's first
-            // pass on the centroids -- the bins never leave registers (the dot: KE4, before)
-            const float* p = (const float*)a.in + vec * D + i0;
-            const DivPlan dp = div_plan_norm(a.nrm[vec]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
-                const float xs[4] = {t.x, t.y, t.z, t.w};
-                const float ys[4] = {xs[0] * a.sqrtD, xs[1] * a.sqrtD, xs[2] * a.sqrtD, xs[3] * a.sqrtD};
-                float zs[4];
-                div4(ys, dp, zs);                                               // AS:329 / norm
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float z = zs[c];
-                    int b = 0;
-                    for (int j = 0; j < a.tab.nb; ++j) b += !(a.tab.b[j] >= z) ? 1 : 0;   // NaN -> nb, as torch.bucketize
-                    v[4 * q + c] = a.tab.c[b];                                  // AS:383
-                }
-            }
+            for (int i = 0; i < 16; ++i) v[i] = eden_cent(cs, bb[i]);            // AS:383
         } else {
             const float* p = (const float*)a.in + vec * D + i0;
 #pragma unroll
@@ -326,6 +329,7 @@ fwht_low16k_kernel(FwhtArgs a) {
     const int64_t vec = blockIdx.y;
     const int tid = threadIdx.x;
     const int64_t D = a.D;
+    const EdenCents cs = eden_cents(a.tab);
     const int64_t base = (int64_t)blockIdx.x * 16384;
     float v[16];
     {   // round-1 layout: 16 contiguous elements
@@ -352,7 +356,7 @@ fwht_low16k_kernel(FwhtArgs a) {
             const int4 bv = *reinterpret_cast<const int4*>((const uint8_t*)a.in + vec * D + i0);
             const uint8_t* bb = reinterpret_cast<const uint8_t*>(&bv);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = a.tab.c[bb[i]];                  // AS:383
+            for (int i = 0; i < 16; ++i) v[i] = eden_cent(cs, bb[i]);            // AS:383
         }
     }
     const int b3 = tid >> 8, o3 = 4096 * b3;
@@ -1004,92 +1008,65 @@ eden_segwalk_kernel(const float* __restrict__ v, int64_t D, const float* __restr
     }
 }
 
-// ---- KE3: bins --------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
-eden_bins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm,
-                 EdenTables tab, uint8_t* __restrict__ bins) {
-    const int64_t vec = blockIdx.y;
-    const int tid = threadIdx.x;
-    const float nv = nrm[vec];
-    const float* p = v + vec * D;
-    uint8_t* bp = bins + vec * D;
-    const int64_t i0 = (int64_t)blockIdx.x * kEdenTile + (int64_t)tid * 16;
-    if (i0 + 16 <= D) {
-        float x[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 t = *reinterpret_cast<const float4*>(p + i0 + 4 * q);
-            x[4 * q] = t.x; x[4 * q + 1] = t.y; x[4 * q + 2] = t.z; x[4 * q + 3] = t.w;
-        }
-        uint32_t w[4] = {0, 0, 0, 0};
-        const DivPlan dp = div_plan_norm(nv);
-        float zs[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float ys[4] = {x[4 * q] * sqrtD, x[4 * q + 1] * sqrtD, x[4 * q + 2] * sqrtD, x[4 * q + 3] * sqrtD};
-            float zq[4];
-            div4(ys, dp, zq);                                      // AS:329 vec * sqrt(D) / norm
-#pragma unroll
-            for (int c = 0; c < 4; ++c) zs[4 * q + c] = zq[c];
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float z = zs[i];
-            int b = 0;
-            for (int j = 0; j < tab.nb; ++j) b += !(tab.b[j] >= z) ? 1 : 0;   // bucketize, right=False (NaN -> nb)
-            w[i >> 2] |= (uint32_t)b << (8 * (i & 3));
-        }
-        *reinterpret_cast<uint4*>(bp + i0) = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-        for (int64_t i = i0; i < std::min<int64_t>(D, i0 + 16); ++i) {
-            const float x = p[i];
-            const float z = (x * sqrtD) / nv;
-            int b = 0;
-            for (int j = 0; j < tab.nb; ++j) b += !(tab.b[j] >= z) ? 1 : 0;
-            bp[i] = (uint8_t)b;
-        }
-    }
-}
-
-// ---- KE4: the scale's dot product in MKL sdot's order ------------------------------------
-// AS:335 scale = norm ** 2 / torch.dot(take(centroids, bins), vec).  torch's CPU dot is MKL's
-// sdot; its order on the fixtures' host (oracle/uq_eden.py:torch_dot, tools/dot_order_probe.py,
-// pinned by tests/golden/dot_vectors.json and every EDEN scale the reference recorded): 4
-// accumulators x 16 lanes over 64-element blocks, each lane a sequential fma chain, so element
-// i belongs to chain i % 64 at step i / 64; of a remainder below 64, a 32-element block into
-// accumulators 0 and 1 and then 16-element chunks into accumulator 0 (the last masked: 0 * 0);
-// then (acc0 + acc1) + (acc2 + acc3) lane-wise and the 16 lanes as i + (i + 8), i + (i + 4),
+// ---- KE4: bins and the scale's dot product in MKL sdot's order ---------------------------
+// AS:329-335 bins = bucketize(vec * sqrt(D) / norm, boundaries); scale = norm ** 2 /
+// torch.dot(take(centroids, bins), vec).  torch's CPU dot is MKL's sdot; its order on the
+// fixtures' host (oracle/uq_eden.py:torch_dot, tools/dot_order_probe.py, pinned by
+// tests/golden/dot_vectors.json and every EDEN scale the reference recorded): 4 accumulators x
+// 16 lanes over 64-element blocks, each lane a sequential fma chain, so element i belongs to
+// chain i % 64 at step i / 64; of a remainder below 64, a 32-element block into accumulators 0
+// and 1 and then 16-element chunks into accumulator 0 (the last masked: 0 * 0); then
+// (acc0 + acc1) + (acc2 + acc3) lane-wise and the 16 lanes as i + (i + 8), i + (i + 4),
 // (0 + 1) + (2 + 3).  One wave per client: lane l runs chain l over the client's rotated
-// vector (64 consecutive floats per step: one coalesced 256-byte load per wave), recomputing
-// each bin as KE3 does (the same f32 multiply and division), two register sets of kDotU steps
-// of loads in flight.  The chains are the exact reference sums, not an approximation.
+// vector (64 consecutive floats per step: one coalesced 256-byte load per wave), writes each
+// coordinate's bin (u8) and folds c[bin] * v into its chain; two register sets of kDotU steps of
+// loads in flight.  The bin needs no division per element: y = v * f32(sqrt D) (AS:329) falls
+// in bin sum_j [!(y <= T_j)] where T_j is the largest f32 y with RN(y / norm) <= boundary j --
+// y -> RN(y / norm) is non-decreasing for a positive finite norm, so this is exactly
+// torch.bucketize of the quotient (NaN included); T_j is found once per client by bisection
+// over the floats' order.  Other norms (0, inf, NaN) take the per-element division.
 constexpr int kDotWaves = 4;
 constexpr int kDotU = 16;
 
-__device__ __forceinline__ float eden_centroid(const EdenTables& tab, float z) {
-    int b = 0;
-    for (int j = 0; j < tab.nb; ++j) b += !(tab.b[j] >= z) ? 1 : 0;     // bucketize (NaN -> nb)
-    float c = tab.c[0];
-    c = b >= 1 ? tab.c[1] : c;
-    c = b >= 2 ? tab.c[2] : c;
-    c = b >= 3 ? tab.c[3] : c;
-    return c;                                                              // AS:335 take(centroids, bins)
+__device__ __forceinline__ uint32_t ford_key(float y) {          // order-preserving u32 image
+    const uint32_t u = __float_as_uint(y);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ford_val(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+// the largest f32 y with RN(y / nv) <= b (nv positive and finite)
+__device__ __forceinline__ float eden_thresh(float b, float nv) {
+    uint32_t lo = ford_key(-INFINITY), hi = ford_key(INFINITY);   // lo satisfies, hi does not
+    while (hi - lo > 1u) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (ford_val(mid) / nv <= b) lo = mid;
+        else hi = mid;
+    }
+    return ford_val(lo);
 }
 
-__global__ void __launch_bounds__(64 * kDotWaves)
-eden_dot_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm, EdenTables tab,
-                float* __restrict__ scale, int64_t n) {
-    __shared__ float red[kDotWaves][64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t j = (int64_t)blockIdx.x * kDotWaves + wv;
-    if (j >= n) return;                                                    // whole wave
-    const float nv = nrm[j];
-    const DivPlan dp = div_plan_norm(nv);
-    const __amdgpu_buffer_rsrc_t rv = make_rsrc(v + j * D, (uint32_t)(D * 4));
+// One client's bins and chains (lane l: chain l); THR: bins by the thresholds T, else by the
+// per-element division (norms that are not positive and finite).  Returns the lane's chain.
+template <int NB, bool THR>
+__device__ __forceinline__ float dotbins_chains(const float* __restrict__ vj, int64_t D, float sqrtD, float nv,
+                                                const EdenTables& tab, const EdenCents& cs, const float (&T)[NB],
+                                                uint8_t* __restrict__ bj, int lane) {
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(vj, (uint32_t)(D * 4));
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(bj, (uint32_t)D);
     float acc = 0.f;
-    auto step = [&](float x) {                                             // acc = fma(c[bin(x)], x, acc)
-        const float z = div1(x * sqrtD, dp);
-        acc = fmaf(eden_centroid(tab, z), x, acc);
+    auto step = [&](float x, int64_t i) {                                  // bins[i], acc = fma(c[bin], x, acc)
+        const float y = x * sqrtD;                                          // AS:329 vec * sqrt(D)
+        int b;
+        if (THR) {
+            b = !(y <= T[0]) ? 1 : 0;
+#pragma unroll
+            for (int q = 1; q < NB; ++q) b += !(y <= T[q]) ? 1 : 0;
+        } else {
+            b = eden_bin(tab, y / nv);
+        }
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, rb, (uint32_t)i, 0, 0);
+        acc = fmaf(eden_cent(cs, b), x, acc);                               // AS:335
     };
     const int64_t steps = D / 64;
     if (steps >= 2 * kDotU && steps % (2 * kDotU) == 0) {
@@ -1100,34 +1077,52 @@ eden_dot_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float
                 R[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                     rv, (uint32_t)((s0 + k) * 64 + lane) * 4u, 0, kAuxNT));     // beyond D: 0, unused
         };
-        auto run = [&](const float (&R)[kDotU]) {
-            float ys[kDotU], zs[kDotU];
+        auto run = [&](const float (&R)[kDotU], int64_t s0) {
 #pragma unroll
-            for (int k = 0; k < kDotU; ++k) ys[k] = R[k] * sqrtD;         // AS:329 vec * sqrt(D)
-            div_n(ys, dp, zs);                                             // / norm (exact quotient)
-#pragma unroll
-            for (int k = 0; k < kDotU; ++k) acc = fmaf(eden_centroid(tab, zs[k]), R[k], acc);
+            for (int k = 0; k < kDotU; ++k) step(R[k], (s0 + k) * 64 + lane);
         };
         load(A, 0);
         for (int64_t s0 = 0; s0 < steps; s0 += 2 * kDotU) {
             load(B, s0 + kDotU);
-            run(A);
+            run(A, s0);
             load(A, s0 + 2 * kDotU);
-            run(B);
+            run(B, s0 + kDotU);
         }
-    } else {
-        int64_t i0 = 0;
-        for (; i0 + 64 <= D; i0 += 64) step(v[j * D + i0 + lane]);
-        if (D - i0 >= 32) {                                                // remainder: acc 0 and 1
-            if (lane < 32) step(v[j * D + i0 + lane]);
-            i0 += 32;
-        }
-        for (; i0 < D; i0 += 16)                                           // then acc 0, masked
-            if (lane < 16) {
-                if (i0 + lane < D) step(v[j * D + i0 + lane]);
-                else acc = fmaf(0.f, 0.f, acc);
-            }
+        return acc;
     }
+    int64_t i0 = 0;
+    for (; i0 + 64 <= D; i0 += 64) step(vj[i0 + lane], i0 + lane);
+    if (D - i0 >= 32) {                                                    // remainder: acc 0 and 1
+        if (lane < 32) step(vj[i0 + lane], i0 + lane);
+        i0 += 32;
+    }
+    for (; i0 < D; i0 += 16)                                               // then acc 0, masked
+        if (lane < 16) {
+            if (i0 + lane < D) step(vj[i0 + lane], i0 + lane);
+            else acc = fmaf(0.f, 0.f, acc);
+        }
+    return acc;
+}
+
+template <int NB>       // boundaries: 1 (1 bit) or 3 (2 bits)
+__global__ void __launch_bounds__(64 * kDotWaves)
+eden_dotbins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm, EdenTables tab,
+                    uint8_t* __restrict__ bins, float* __restrict__ scale, int64_t n) {
+    __shared__ float red[kDotWaves][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * kDotWaves + wv;
+    if (j >= n) return;                                                    // whole wave
+    const float nv = nrm[j];
+    const EdenCents cs = eden_cents(tab);
+    const bool thr = nv > 0.f && nv < INFINITY;                            // wave-uniform
+    float T[NB];
+    {
+        const float t = (thr && lane < NB) ? eden_thresh(tab.b[lane < NB ? lane : 0], nv) : 0.f;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) T[q] = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(t), q));
+    }
+    const float acc = thr ? dotbins_chains<NB, true>(v + j * D, D, sqrtD, nv, tab, cs, T, bins + j * D, lane)
+                          : dotbins_chains<NB, false>(v + j * D, D, sqrtD, nv, tab, cs, T, bins + j * D, lane);
     red[wv][lane] = acc;
     wave_lds_fence();
     if (lane == 0) {

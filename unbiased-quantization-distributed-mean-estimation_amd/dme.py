@@ -31,7 +31,7 @@ import torch
 from .biased import biased_quantize
 from .eden import eden_compress, eden_decompress, eden_quantize
 from .quantizer import client_mean, quantize_dequantize
-from .quicfl import quicfl_compress, quicfl_decompress_messages
+from .quicfl import quicfl_quantize
 
 SCHEME_ORDER = ("eden", "unbiased", "biased", "quicfl")     # ND:135-142 call order
 
@@ -118,8 +118,8 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                 elif sc == "quicfl":
                     seeds = [s_ for s_, _ in draws[(sc, r)]]
                     states = np.stack([w for _, w in draws[(sc, r)]])
-                    msg = quicfl_compress(xd, r, seeds, [123] * n, sender=qsend, px_states=states)   # AS:822
-                    q = quicfl_decompress_messages(msg, qrecv.recv_table[r])
+                    q, _, _ = quicfl_quantize(xd, r, seeds, [123] * n, sender=qsend,                 # AS:814-832
+                                              recv_table=qrecv.recv_table[r], px_states=states)
                 elif eden_scales is None and eden_scales_out is None:
                     q = eden_quantize(xd, r, seeds=draws[(sc, r)])
                 else:                                 # compress, (record / replace the scale), decompress
