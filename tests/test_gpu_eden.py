@@ -171,6 +171,17 @@ def test_eden_dims_across_pass_shapes_vs_oracle(uq, d):
             assert G.bits_equal(out[j], E.eden_decompress(bins, sc, nbits, seeds[j], d)), (d, nbits, j)
 
 
+def _adv_rows(rng, kind, n, D):
+    if kind == "wide":                                   # roundings in every add
+        return (rng.standard_normal((n, D)) * np.exp2(rng.integers(-20, 21, (n, D)))).astype(np.float32)
+    if kind == "smallint":                               # few distinct values: exact ties in the chains
+        return rng.integers(-3, 4, (n, D)).astype(np.float32)
+    x = rng.standard_normal((n, D)).astype(np.float32)   # "tiny": quotients that underflow (lowest bin)
+    x[:, ::97] = np.float32(1e-44)
+    x[:, 1] = np.float32(3e38)
+    return x
+
+
 @pytest.mark.parametrize("n", [1, 5, 300])
 def test_scale_dot_order_adversarial(uq, n):
     """The scale's dot (eden_dot_kernel) against the C oracle's MKL-order dot on vectors whose
@@ -193,3 +204,29 @@ def test_scale_dot_order_adversarial(uq, n):
                 with np.errstate(all="ignore"):
                     exp = np.float32(np.float32(nrm * nrm) / C.torch_dot(c, rot))
                 assert same_f32(sc[j], exp), (D, nbits, j)
+
+
+@pytest.mark.parametrize("kind", ["wide", "smallint", "tiny"])
+def test_scale_dot_segmented_and_one_wave_agree(uq, kind):
+    """The dot's two forms (KE4s segments for <= kDotSegMaxN clients, one wave per client
+    otherwise) on the same rows: identical bins and scales, both equal to the C oracle's
+    MKL-order dot, at D = 2^14 .. 2^22 (ties, binade crossings, underflowing quotients)."""
+    from oracle import uq_oracle_c as C
+    rng = np.random.default_rng(hash(kind) % 1000)
+    for D in (1 << 14, 1 << 17, 1 << 20, 1 << 22):
+        x = _adv_rows(rng, kind, 2, D)
+        seeds = [int(s) for s in rng.integers(0, 100, 2)]
+        for nbits in (1, 2):
+            few = uq.eden_compress(torch.as_tensor(x).cuda(), nbits, seeds=seeds)            # segmented
+            many = uq.eden_compress(torch.as_tensor(np.concatenate([x] * 40)).cuda(), nbits,   # one wave each
+                                    seeds=seeds * 40)
+            assert torch.equal(few.bins, many.bins[:2]), (D, nbits)
+            a, b = few.scale.cpu().numpy(), many.scale.cpu().numpy()[:2]
+            for j in range(2):
+                assert same_f32(a[j], b[j]), (kind, D, nbits, j)
+                rot = E.rht(x[j], seeds[j])
+                nrm = E.torch_norm2(rot)
+                c = E.centroids(nbits)[few.bins.cpu().numpy()[j]]
+                with np.errstate(all="ignore"):
+                    exp = np.float32(np.float32(nrm * nrm) / C.torch_dot(c, rot))
+                assert same_f32(a[j], exp), (kind, D, nbits, j)

@@ -63,11 +63,22 @@ def main():
     import uqdme
     schemes = tuple(a.schemes.split(","))
     res = {"dim": a.dim, "instances": a.instances, "schemes": schemes, "curves": {}, "vs_published": {}}
+    qfl = None
+    if "quicfl" in schemes:          # the reference's sender tables are absent: the fixtures' synthetic ones
+        gdir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+        sys.path.insert(0, gdir)
+        from quicfl_tables import DATA, sender_tables
+        rz = np.load(os.path.join(gdir, "quicfl_recv_vectors.npz"))
+        qfl = (uqdme.QuicFLSender(tables={b: (*sender_tables(b), DATA[b]) for b in (1, 2, 3, 4)}),
+               uqdme.QuicFLReceiver(tables={b: rz[f"recv{b}"] for b in (1, 2, 3, 4)}))
+        res["quicfl_tables"] = ("synthetic sender tables (tests/golden/quicfl_tables.py, the reference's data.txt "
+                                "parameters; the published sender tables are not in the reference) with the "
+                                "reference's receiver tables: QUIC-FL curves are the pipeline's, not the paper's")
     for dist in a.dists.split(","):
         users = tuple(USERS[dist]) if a.users is None else tuple(int(u) for u in a.users.split(","))
         t0 = time.time()
         out = uqdme.nmse_simulation(dist, dim=a.dim, users=users, num_instances=a.instances, schemes=schemes,
-                                    torch_threads=1,
+                                    torch_threads=1, quicfl=qfl,
                                     progress=lambda n, i: print(f"{dist} n={n} inst={i} {time.time() - t0:.0f} s",
                                                                 flush=True))
         if schemes == ("unbiased",):

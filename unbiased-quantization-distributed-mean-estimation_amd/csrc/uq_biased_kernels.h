@@ -9,8 +9,15 @@
 //   KB1  L1 = |x|.sum()                  K1 cascade, AbsOp           (AS:680)
 //   KB2  m' = k'.sum(), k' = floor(m p + 0.5)  K1 cascade, RezKOp    (AS:648-649)
 //   KB3  Delta = int(m' - m) -> |Delta| selections                    (AS:651-656)
-//   KB4  radix select (3 passes, 11/11/10-bit digits) of the |Delta|-th largest key of
-//        +delta' (Delta > 0) or -delta' (Delta < 0), delta' = k' - m p  (AS:655-665)
+//   KB4a the bucket of the |Delta|-th largest selection value v (+delta' for Delta > 0,
+//        -delta' for Delta < 0; delta' = k' - m p, AS:655-665) among KB2's 2048 "fine" bins,
+//        linear in |v| over [-0.5, 0.5] (rez_fbin: ~0.1 % of a Gaussian row per bin at R = 1)
+//   KB6f ("fine" clients, the bucket small) out for every coordinate: bins above the bucket
+//        are selected, below are not, the bucket's coordinates provisionally unselected and
+//        listed (index, key); KB4d radix-selects the threshold key among the listed keys and
+//        KB6p patches the listed coordinates that are selected -- x is read three times in all
+//   KB4b (other clients: a bucket too large, tie-heavy data) radix select (3 passes, 11/11/10-bit
+//        digits of the order key) over the whole row, then KB6
 //   KB5  (ambiguous clients only) tie counts per tile, for the index-order tie rank
 //   KB6  out = (L1 * sign(x)) * (k'' / m), k'' = k' -+ 1 on the selected set (AS:661/665/687)
 // torch.topk compares values (as doubles): equal values are ties whatever their index.
@@ -29,7 +36,8 @@ enum RezFlags : int32_t {
     kRezNonFinite = 2,     // m' is NaN/inf: the reference raises in int(m' - m) (AS:656)
     kRezRange = 4,         // |Delta| > d: torch.topk raises (cannot happen for finite input)
     kRezTorchTies = 8,     // selection set replayed with torch's tie choice (KB7)
-    kRezCompact = 16,      // threshold digits 2-3 found on the compacted first-digit bucket
+    kRezFine = 16,         // threshold found among the fine bucket's keys listed by KB6f
+    kRezFull = 32,         // threshold found by full-row radix passes (bucket too large)
 };
 
 struct RezState {          // 32 bytes per client; (delta, flags) are the public info pair
@@ -40,7 +48,7 @@ struct RezState {          // 32 bytes per client; (delta, flags) are the public
     uint32_t kleft;        // selections still to place at/below the prefix
     uint32_t eq;           // keys equal to the threshold (after the last pass)
     uint32_t need;         // how many of those are selected
-    uint32_t pad;
+    uint32_t fbin;         // kRezFine: the threshold's fine bin
 };
 
 // Order-preserving u32 image of the selection value (+delta' for Delta > 0, -delta'
@@ -52,6 +60,11 @@ __device__ __forceinline__ uint32_t rez_key_of(float dp, bool up) {
     uint32_t u = __float_as_uint(v);
     if (v != v) u = 0x7FC00000u;
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// The selection value a key encodes (its inverse image; NaN keys decode to NaN).
+__device__ __forceinline__ float rez_key_val(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
 // k' and the key of one coordinate, exactly the reference's f32 ops (no contraction):
@@ -140,7 +153,7 @@ rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
     using RP = RadixPass<PASS>;
     const int64_t vec = blockIdx.y;
     const uint32_t kleft = st[vec].kleft;
-    if (kleft == 0 || (st[vec].flags & kRezCompact)) return;
+    if (kleft == 0 || !(st[vec].flags & kRezFull)) return;
     const uint32_t prefix = st[vec].prefix;
     const bool up = st[vec].delta > 0;
     __shared__ uint32_t h[kRadixBins];
@@ -173,40 +186,41 @@ rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         }
     }
     __syncthreads();
-    uint32_t* g = hist + ((size_t)vec * 3 + PASS) * kRadixBins;
+    uint32_t* g = hist + ((size_t)vec * kHistSlots + PASS) * kRadixBins;
     for (int b = tid; b < kRadixBins; b += 256)
         if (h[b]) atomicAdd(&g[b], h[b]);
 }
 
-// KB4b: pick the digit holding the kleft-th largest key (one workgroup per client).
-// Pass 0 reads the histogram of +delta' made inside the k' sum (KB2) and mirrors it for
-// Delta < 0 (key(-v) = ~key(v) except for v = 0 and NaN, counted apart in zn).  When the
-// chosen first-digit bucket holds at most `cap` keys the client switches to candidate
-// compaction (KB4c/KB4d) instead of passes 1-2.
-template <int PASS>
+// KB4a / KB4b: pick the digit holding the kleft-th largest key (one workgroup per client).
+// FINE (KB4a): KB2's fine bins of +delta', mirrored for Delta < 0 (zeros and NaNs counted
+// apart in zn); a bucket of at most `capf` coordinates makes the client kRezFine (its keys are
+// listed by KB6f), a larger one kRezFull.  Otherwise (KB4b) pass PASS of the key digits over
+// the full row, kRezFull clients only.
+template <int PASS, bool FINE>
 __global__ void __launch_bounds__(256)
 rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ zn,
-                  uint32_t cap) {
+                  uint32_t capf) {
     using RP = RadixPass<PASS>;
-    constexpr int nb = (int)RP::dmask + 1;
+    constexpr int nb = FINE ? kRadixBins : (int)RP::dmask + 1;
     constexpr int per = nb / 256;
     const int64_t vec = blockIdx.x;
     const uint32_t kleft = st[vec].kleft;
     if (kleft == 0) return;
-    if (PASS > 0 && (st[vec].flags & kRezCompact)) return;
+    if (!FINE && !(st[vec].flags & kRezFull)) return;
     __shared__ uint32_t lds[4];
+    __shared__ int s_found;
     const int tid = threadIdx.x;
-    const uint32_t* h = hist + ((size_t)vec * 3 + PASS) * kRadixBins;
-    const bool mirror = PASS == 0 && st[vec].delta < 0;
-    const uint32_t z = PASS == 0 ? zn[vec * 2] : 0u, nn = PASS == 0 ? zn[vec * 2 + 1] : 0u;
+    if (tid == 0) s_found = 0;
+    const uint32_t* h = hist + ((size_t)vec * kHistSlots + (FINE ? kFineSlot : PASS)) * kRadixBins;
+    const bool mirror = FINE && st[vec].delta < 0;
+    const uint32_t z = FINE ? zn[vec * 2] : 0u, nn = FINE ? zn[vec * 2 + 1] : 0u;
     auto count = [&](int b) -> uint32_t {
         if (!mirror) return h[b];
-        const int src = nb - 1 - b;              // top digit of ~key
-        uint32_t c = h[src];
-        if (src == 1024) c -= z;                 // zeros and NaNs do not move
-        if (src == 2046) c -= nn;
+        uint32_t c = h[nb - 1 - b];              // fbin(-v) = 2047 - fbin(v) but for 0 and NaN
+        if (b == 1023) c -= z;
         if (b == 1024) c += z;
-        if (b == 2046) c += nn;
+        if (b == 0) c -= nn;
+        if (b == 2047) c += nn;
         return c;
     };
     // thread t owns bins [nb - (t+1)*per, nb - t*per): thread 0 the highest digits
@@ -225,116 +239,43 @@ rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist, 
             if (above + c[k] >= kleft) {
                 const uint32_t digit = (uint32_t)(hi - 1 - k);
                 RezState s = st[vec];
-                s.prefix |= digit << RP::shift;
-                s.kleft = kleft - above;
-                if (PASS == 0 && c[k] <= cap) {
-                    s.flags |= kRezCompact;
-                    s.eq = c[k];                 // keys in the bucket = candidates to compact
-                }
-                if (PASS == 2) {
-                    s.eq = c[k];
-                    s.need = s.kleft;
-                    if (s.eq > s.need) s.flags |= kRezAmbiguous;
+                if (FINE) {
+                    if (c[k] <= capf) {
+                        s.flags |= kRezFine;
+                        s.fbin = digit;
+                        s.kleft = kleft - above;         // to select inside the bucket
+                        s.eq = c[k];                     // its coordinates = the candidates KB6f lists
+                    } else {
+                        s.flags |= kRezFull;
+                    }
+                } else {
+                    s.prefix |= digit << RP::shift;
+                    s.kleft = kleft - above;
+                    if (PASS == 2) {
+                        s.eq = c[k];
+                        s.need = s.kleft;
+                        if (s.eq > s.need) s.flags |= kRezAmbiguous;
+                    }
                 }
                 st[vec] = s;
+                s_found = 1;
                 break;
             }
             above += c[k];
         }
     }
+    __syncthreads();
+    if (FINE && tid == 0 && !s_found) st[vec].flags |= kRezFull;     // (cannot happen: sum = d >= kleft)
 }
 
-// KB4c: compact the keys of the chosen first-digit bucket (compact-mode clients).  Each
-// thread keeps its kCompactItems keys in registers (float4 loads, coalesced, non-temporal),
-// counts the matches; one block scan + one atomic per workgroup reserves the output range.
-// The matches are staged in LDS (branch-free: a non-match goes to the thread's junk slot) and
-// copied out coalesced; a workgroup with more than kCompactStage matches (tie-heavy data)
-// writes them straight from registers.  32 keys per thread (was 64: the VGPRs held three
-// workgroups per CU, 1.11 ms = 3.9 TB/s at 1024 x 2^20).
-constexpr int kCompactStage = 4096;
-constexpr int kCompactItems = 32;
-constexpr int kCompactSpan = 256 * kCompactItems;
-template <bool CHECK>
-__device__ __forceinline__ uint64_t compact_keys(const float* __restrict__ xv, int64_t d, int64_t b0, int tid,
-                                                 const DivPlan& dp, float fm, bool up, uint32_t prefix,
-                                                 uint32_t (&key)[kCompactItems]) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    uint64_t match = 0;
-#pragma unroll
-    for (int j = 0; j < kCompactItems / 4; ++j) {
-        const int64_t i = b0 + 4 * ((int64_t)j * 256 + tid);          // elements i .. i+3
-        float v[4];
-        if (!CHECK) {
-            const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(xv + i));
-            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-        } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) v[c] = (i + c < d) ? xv[i + c] : 0.f;
-        }
-        float kp[4];
-        uint32_t k4[4];
-        rez_elem4(v, dp, fm, up, kp, k4);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            key[4 * j + c] = k4[c];
-            if ((!CHECK || i + c < d) && (k4[c] & 0xFFE00000u) == prefix) match |= 1ull << (4 * j + c);
-        }
-    }
-    return match;
-}
-
-template <bool VEC4>
-__global__ void __launch_bounds__(256)
-rez_compact_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
-                   const RezState* __restrict__ st, uint32_t* __restrict__ cand, uint32_t* __restrict__ cand_n,
-                   uint32_t cap) {
-    const int64_t vec = blockIdx.y;
-    if (st[vec].kleft == 0 || !(st[vec].flags & kRezCompact)) return;
-    const uint32_t prefix = st[vec].prefix;
-    const bool up = st[vec].delta > 0;
-    const DivPlan dp = div_plan(l1[vec]);
-    const float* xv = x + vec * d;
-    const int tid = threadIdx.x;
-    const int64_t b0 = (int64_t)blockIdx.x * kCompactSpan;
-    __shared__ uint32_t lds[4];
-    __shared__ uint32_t s_base;
-    __shared__ uint32_t s_cand[kCompactStage + 256];             // staged matches + junk slots
-    uint32_t key[kCompactItems];
-    const uint64_t match = (VEC4 && b0 + kCompactSpan <= d)
-                               ? compact_keys<false>(xv, d, b0, tid, dp, fm, up, prefix, key)
-                               : compact_keys<true>(xv, d, b0, tid, dp, fm, up, prefix, key);
-    uint32_t tot;
-    uint32_t off = block_excl_scan_u32((uint32_t)__popcll(match), lds, &tot);
-    if (tid == 0) s_base = tot ? atomicAdd(&cand_n[vec], tot) : 0u;
-    uint32_t* cv = cand + (size_t)vec * cap;
-    if (tot <= (uint32_t)kCompactStage) {                        // block-uniform
-        const uint32_t junk = kCompactStage + tid;
-#pragma unroll
-        for (int e = 0; e < kCompactItems; ++e) {
-            const uint32_t bit = (uint32_t)(match >> e) & 1u;
-            s_cand[bit ? off : junk] = key[e];
-            off += bit;
-        }
-        __syncthreads();
-        const uint32_t base = s_base;
-        for (uint32_t k = tid; k < tot; k += 256)
-            if (base + k < cap) cv[base + k] = s_cand[k];
-    } else {
-        __syncthreads();
-        off += s_base;
-#pragma unroll
-        for (int e = 0; e < kCompactItems; ++e)
-            if (((match >> e) & 1ull) && off < cap) cv[off++] = key[e];
-    }
-}
-
-// KB4d: digits 2 and 3 on the candidates (one workgroup per compact-mode client).
-// cand_pick: the digit of candidate pass `pass` (1: bits 10-20, 2: bits 0-9) holding the
-// kleft-th largest key, from the pass's histogram h (nb bins); updates s in every thread.
+// KB4d: the threshold key among a fine client's listed candidates (key digits 11/11/10 over
+// the (index, key) pairs KB6f wrote; the candidates share the fine bin, not a key prefix).
+// cand_pick: the digit of candidate pass `pass` holding the kleft-th largest key, from the
+// pass's histogram h; updates s in every thread.
 __device__ __forceinline__ void cand_pick(const uint32_t* h, int pass, RezState& s, uint32_t* lds) {
     const int tid = threadIdx.x;
-    const int shift = pass == 1 ? 10 : 0;
-    const int nb = pass == 1 ? 2048 : 1024;
+    const int shift = pass == 0 ? 21 : (pass == 1 ? 10 : 0);
+    const int nb = pass == 2 ? 1024 : 2048;
     const int per = nb / 256;
     const int hi = nb - tid * per;
     uint32_t c[8], sum = 0;
@@ -368,21 +309,27 @@ __device__ __forceinline__ void cand_pick(const uint32_t* h, int pass, RezState&
     __syncthreads();
 }
 
+__device__ __forceinline__ void cand_pass_masks(int pass, int& shift, uint32_t& dmask, uint32_t& hmask) {
+    shift = pass == 0 ? 21 : (pass == 1 ? 10 : 0);
+    dmask = pass == 2 ? 0x3FFu : 0x7FFu;
+    hmask = pass == 0 ? 0u : (pass == 1 ? 0xFFE00000u : 0xFFFFFC00u);
+}
+
 __global__ void __launch_bounds__(256)
-rez_cand_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ cand,
-                       const uint32_t* __restrict__ cand_n, uint32_t cap) {
+rez_cand_select_kernel(RezState* __restrict__ st, const uint2* __restrict__ cand, const uint32_t* __restrict__ cand_n,
+                       uint32_t capf) {
     const int64_t vec = blockIdx.x;
-    if (st[vec].kleft == 0 || !(st[vec].flags & kRezCompact)) return;
+    if (st[vec].kleft == 0 || !(st[vec].flags & kRezFine)) return;
     __shared__ uint32_t h[kRadixBins];
     __shared__ uint32_t lds[4];
     const int tid = threadIdx.x;
-    const uint32_t nc = std::min(cand_n[vec], cap);
-    const uint32_t* cv = cand + (size_t)vec * cap;
+    const uint32_t nc = std::min(cand_n[vec], capf);
+    const uint2* cv = cand + (size_t)vec * capf;
     RezState s = st[vec];
-    for (int pass = 1; pass <= 2; ++pass) {
-        const int shift = pass == 1 ? 10 : 0;
-        const uint32_t dmask = pass == 1 ? 0x7FFu : 0x3FFu;
-        const uint32_t hmask = pass == 1 ? 0xFFE00000u : 0xFFFFFC00u;
+    for (int pass = 0; pass <= 2; ++pass) {
+        int shift;
+        uint32_t dmask, hmask;
+        cand_pass_masks(pass, shift, dmask, hmask);
         for (int b = tid; b < kRadixBins; b += 256) h[b] = 0u;
         __syncthreads();
         // 8 independent candidate loads in flight per thread, then their LDS atomics
@@ -390,13 +337,13 @@ rez_cand_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ c
         for (; i + 7 * 256 < nc; i += 8 * 256) {
             uint32_t kk[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) kk[u] = __builtin_nontemporal_load(cv + i + u * 256);
+            for (int u = 0; u < 8; ++u) kk[u] = cv[i + u * 256].y;
 #pragma unroll
             for (int u = 0; u < 8; ++u)
                 if ((kk[u] & hmask) == s.prefix) atomicAdd(&h[(kk[u] >> shift) & dmask], 1u);
         }
         for (; i < nc; i += 256) {
-            const uint32_t key = cv[i];
+            const uint32_t key = cv[i].y;
             if ((key & hmask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
         }
         __syncthreads();
@@ -405,41 +352,43 @@ rez_cand_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ c
     if (tid == 0) st[vec] = s;
 }
 
-// The same two passes for a few clients with long candidate lists (the per-call drop-in):
-// KB4d1 histograms kCandSpan candidates per workgroup into the client's pass histogram
-// (hist[vec][pass], zero until then: the full-vector passes skip compact-mode clients),
+// The same three passes for a few clients with long candidate lists (tie-heavy rows in the
+// per-call drop-in): KB4d1 histograms kCandSpan candidates per workgroup into the client's
+// pass histogram (hist[vec][pass], zero until then: the full-row passes skip fine clients),
 // KB4d2 picks the digit from it with cand_pick (same bits as rez_cand_select_kernel).
 constexpr int kCandSpan = 256 * 32;
 template <int PASS>
 __global__ void __launch_bounds__(256)
-rez_cand_hist_kernel(const RezState* __restrict__ st, const uint32_t* __restrict__ cand,
-                     const uint32_t* __restrict__ cand_n, uint32_t cap, uint32_t* __restrict__ hist) {
+rez_cand_hist_kernel(const RezState* __restrict__ st, const uint2* __restrict__ cand,
+                     const uint32_t* __restrict__ cand_n, uint32_t capf, uint32_t* __restrict__ hist) {
     const int64_t vec = blockIdx.y;
-    if (st[vec].kleft == 0 || !(st[vec].flags & kRezCompact)) return;
-    const uint32_t nc = std::min(cand_n[vec], cap);
+    if (st[vec].kleft == 0 || !(st[vec].flags & kRezFine)) return;
+    const uint32_t nc = std::min(cand_n[vec], capf);
     const uint32_t b0 = blockIdx.x * (uint32_t)kCandSpan;
     if (b0 >= nc) return;
-    constexpr int shift = PASS == 1 ? 10 : 0;
-    constexpr uint32_t dmask = PASS == 1 ? 0x7FFu : 0x3FFu;
-    constexpr uint32_t hmask = PASS == 1 ? 0xFFE00000u : 0xFFFFFC00u;
+    constexpr int shift = PASS == 0 ? 21 : (PASS == 1 ? 10 : 0);
+    constexpr uint32_t dmask = PASS == 2 ? 0x3FFu : 0x7FFu;
+    constexpr uint32_t hmask = PASS == 0 ? 0u : (PASS == 1 ? 0xFFE00000u : 0xFFFFFC00u);
     constexpr int nb = (int)dmask + 1;
     __shared__ uint32_t h[nb];
     const int tid = threadIdx.x;
     for (int b = tid; b < nb; b += 256) h[b] = 0u;
     __syncthreads();
     const uint32_t prefix = st[vec].prefix;
-    const uint32_t* cv = cand + (size_t)vec * cap;
+    const uint2* cv = cand + (size_t)vec * capf;
     uint32_t kk[kCandSpan / 256];
 #pragma unroll
     for (int u = 0; u < kCandSpan / 256; ++u) {
         const uint32_t i = b0 + tid + 256u * u;
-        kk[u] = i < nc ? cv[i] : ~prefix;                     // ~prefix never matches
+        kk[u] = i < nc ? cv[i].y : ~prefix;                   // ~prefix never matches (hmask != 0)
     }
 #pragma unroll
-    for (int u = 0; u < kCandSpan / 256; ++u)
-        if ((kk[u] & hmask) == prefix) atomicAdd(&h[(kk[u] >> shift) & dmask], 1u);
+    for (int u = 0; u < kCandSpan / 256; ++u) {
+        const uint32_t i = b0 + tid + 256u * u;
+        if (i < nc && (kk[u] & hmask) == prefix) atomicAdd(&h[(kk[u] >> shift) & dmask], 1u);
+    }
     __syncthreads();
-    uint32_t* g = hist + ((size_t)vec * 3 + PASS) * kRadixBins;
+    uint32_t* g = hist + ((size_t)vec * kHistSlots + PASS) * kRadixBins;
     for (int b = tid; b < nb; b += 256)
         if (h[b]) atomicAdd(&g[b], h[b]);
 }
@@ -448,11 +397,11 @@ template <int PASS>
 __global__ void __launch_bounds__(256)
 rez_cand_pick_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist) {
     const int64_t vec = blockIdx.x;
-    if (st[vec].kleft == 0 || !(st[vec].flags & kRezCompact)) return;
+    if (st[vec].kleft == 0 || !(st[vec].flags & kRezFine)) return;
     __shared__ uint32_t h[kRadixBins];
     __shared__ uint32_t lds[4];
     const int tid = threadIdx.x;
-    const uint32_t* g = hist + ((size_t)vec * 3 + PASS) * kRadixBins;
+    const uint32_t* g = hist + ((size_t)vec * kHistSlots + PASS) * kRadixBins;
     for (int b = tid; b < kRadixBins; b += 256) h[b] = g[b];
     __syncthreads();
     RezState s = st[vec];
@@ -523,8 +472,11 @@ rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t 
     const bool on = s.kleft != 0;
     const bool amb = on && (s.flags & kRezAmbiguous);
     // part 0: every client; 1: clients without a tie at the threshold (run while KB7 replays
-    // the others on a side stream); 2: only those with one (after KB7)
+    // the others on a side stream); 2: only those with one (after KB7).  Fine clients without
+    // a tie were written by KB6f + KB6p (with one, this kernel rewrites them: index-order or
+    // replayed tie ranks need the whole row)
     if ((part == 1 && amb) || (part == 2 && !amb)) return;
+    if (on && (s.flags & kRezFine) && !amb) return;
     const bool replay = amb && (s.flags & kRezTorchTies);
     const bool up = s.delta > 0;
     const float L = l1[vec];
@@ -650,6 +602,126 @@ rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t 
 #pragma unroll
         for (int j = 0; j < kSelItems; ++j)
             if (e0 + j < d) ov[e0 + j] = q[j];
+    }
+}
+
+// KB6f: fine clients (kRezFine) -- out for every coordinate with the selection decided by the
+// fine bin (above the threshold's bin: selected; below: not); the threshold bin's coordinates
+// are written unselected and listed as (index, key) pairs for KB4d (one atomic per workgroup
+// reserves the list range).  The same arithmetic as KB6, so KB6p's patch gives KB6's bits.
+template <bool VEC4>
+__global__ void __launch_bounds__(256)
+rez_output_fine_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, const float* __restrict__ l1,
+                       float fm, const RezState* __restrict__ st, uint2* __restrict__ cand,
+                       uint32_t* __restrict__ cand_n, uint32_t capf) {
+    const int64_t vec = blockIdx.y;
+    const RezState s = st[vec];
+    if (s.kleft == 0 || !(s.flags & kRezFine)) return;
+    const bool up = s.delta > 0;
+    const float L = l1[vec];
+    const DivPlan dp = div_plan(L);
+    const DivPlan dpm = div_plan_m(fm);
+    const float adj = up ? -1.f : 1.f;
+    const uint32_t fb = s.fbin;
+    const float* xv = x + vec * d;
+    float* ov = out + vec * d;
+    const int tid = threadIdx.x;
+    const int64_t tb = (int64_t)blockIdx.x * kSelTile;
+    __shared__ uint32_t lds[4];
+    __shared__ uint32_t s_base;
+    uint32_t ck[kSelItems];                    // listed keys of this thread (indices alongside)
+    uint32_t ci[kSelItems];
+    uint32_t nck = 0;
+    auto one = [&](float v, float kp, uint32_t key, int64_t i, float& kq) {
+        const uint32_t b = rez_fbin(rez_key_val(key));
+        kq = b > fb ? kp + adj : kp;                           // k'' (the bucket provisionally unselected)
+        if (b == fb) {
+            ck[nck] = key;
+            ci[nck] = (uint32_t)i;
+            ++nck;
+        }
+    };
+    if (VEC4 && tb + kSelTile <= d) {
+        // lane-interleaved float4s (one coalesced 1 KB row per wave per load), non-temporal
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v* x4 = reinterpret_cast<const f4v*>(xv + tb);
+        f4v* o4 = reinterpret_cast<f4v*>(ov + tb);
+        f4v a[kSelItems / 4];
+#pragma unroll
+        for (int j = 0; j < kSelItems / 4; ++j) a[j] = __builtin_nontemporal_load(x4 + j * 256 + tid);
+#pragma unroll
+        for (int j = 0; j < kSelItems / 4; ++j) {
+            const float v4[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
+            float k4[4], q4[4], r4[4];
+            uint32_t y4[4];
+            rez_elem4(v4, dp, fm, up, k4, y4);
+            const int64_t i0 = tb + 4 * ((int64_t)j * 256 + tid);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) one(v4[c], k4[c], y4[c], i0 + c, q4[c]);
+            div4(q4, dpm, r4);                                 // RN(k'' / m)
+            f4v o;
+            o.x = (L * torch_signf(v4[0])) * r4[0];            // AS:687 (L1 * signs) * (k'' / m)
+            o.y = (L * torch_signf(v4[1])) * r4[1];
+            o.z = (L * torch_signf(v4[2])) * r4[2];
+            o.w = (L * torch_signf(v4[3])) * r4[3];
+            __builtin_nontemporal_store(o, o4 + j * 256 + tid);
+        }
+    } else {
+        const int64_t e0 = tb + (int64_t)tid * kSelItems;
+#pragma unroll
+        for (int j = 0; j < kSelItems / 4; ++j) {
+            float v4[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v4[c] = (e0 + 4 * j + c < d) ? xv[e0 + 4 * j + c] : 0.f;
+            float k4[4], q4[4], r4[4];
+            uint32_t y4[4];
+            rez_elem4(v4, dp, fm, up, k4, y4);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (e0 + 4 * j + c < d) one(v4[c], k4[c], y4[c], e0 + 4 * j + c, q4[c]);
+                else q4[c] = 0.f;
+            }
+            div4(q4, dpm, r4);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (e0 + 4 * j + c < d) ov[e0 + 4 * j + c] = (L * torch_signf(v4[c])) * r4[c];
+        }
+    }
+    uint32_t tot;
+    const uint32_t off = block_excl_scan_u32(nck, lds, &tot);
+    if (tot == 0) return;                                      // block-uniform
+    if (tid == 0) s_base = atomicAdd(&cand_n[vec], tot);
+    __syncthreads();
+    uint2* cv = cand + (size_t)vec * capf;
+    const uint32_t base = s_base + off;
+    for (uint32_t k = 0; k < nck; ++k)
+        if (base + k < capf) cv[base + k] = make_uint2(ci[k], ck[k]);
+}
+
+// KB6p: the listed coordinates of a fine client without a threshold tie that are selected
+// (key >= the threshold key: every tie is selected) get k'' = k' -+ 1.
+constexpr int kPatchBlocks = 4;
+__global__ void __launch_bounds__(256)
+rez_fine_patch_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, const float* __restrict__ l1,
+                      float fm, const RezState* __restrict__ st, const uint2* __restrict__ cand,
+                      const uint32_t* __restrict__ cand_n, uint32_t capf) {
+    const int64_t vec = blockIdx.y;
+    const RezState s = st[vec];
+    if (s.kleft == 0 || !(s.flags & kRezFine) || (s.flags & kRezAmbiguous)) return;
+    const uint32_t nc = std::min(cand_n[vec], capf);
+    const uint2* cv = cand + (size_t)vec * capf;
+    const bool up = s.delta > 0;
+    const float L = l1[vec];
+    const DivPlan dp = div_plan(L);
+    const DivPlan dpm = div_plan_m(fm);
+    const float adj = up ? -1.f : 1.f;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nc; i += gridDim.x * 256) {
+        const uint2 c = cv[i];
+        if (c.y < s.prefix) continue;
+        const float v = x[vec * d + c.x];
+        float kp;
+        (void)rez_elem(v, dp, fm, up, kp);
+        out[vec * d + c.x] = (L * torch_signf(v)) * div1(kp + adj, dpm);     // AS:687 with k''
     }
 }
 

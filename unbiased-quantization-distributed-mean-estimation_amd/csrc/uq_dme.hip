@@ -277,9 +277,23 @@ struct RezKOp {           // AS:648-649  k' = floor(m * p + 0.5), p = |x| / (L1 
         for (int c = 0; c < 4; ++c) a[c] += floorf(fm * qs[c] + 0.5f);
     }
 };
-// RezKOp that also counts the top 11 bits of the order key of +delta' = k' - m p into
-// h[2048] (the biased quantizer's first radix digit, KB4 pass 0), and delta' == 0 / NaN
-// elements into zn[0] / zn[1] so that the histogram of -delta' can be mirrored from it.
+constexpr int kHistSlots = 4;                       // per biased client: key-digit passes 0-2, KB2's fine bins
+constexpr int kFineSlot = 3;
+// The fine bin of a selection value v: non-decreasing in v (so in the key), 2^11 bins linear
+// in |v| (delta' lies in [-0.5, 0.5]): v > 0 -> 1024 + min(1023, floor(2048 |v|)), v < 0 ->
+// 1023 - min(1023, floor(2048 |v|)), +-0 -> 1024, NaN -> 2047 (ATen's topk puts NaN first).
+// For v != 0 and not NaN, fbin(-v) = 2047 - fbin(v): KB2 counts +delta' and KB4a mirrors the
+// counts for Delta < 0, moving zeros (1023 -> 1024) and NaNs (0 -> 2047) back.
+__device__ __forceinline__ uint32_t rez_fbin(float v) {
+    if (v != v) return 2047u;
+    const float a = fabsf(v) * 2048.0f;                   // exact (a power-of-two scale)
+    const uint32_t q = a >= 1023.0f ? 1023u : (uint32_t)a;
+    return v > 0.f ? 1024u + q : (v < 0.f ? 1023u - q : 1024u);
+}
+
+// RezKOp that also counts the fine bin (rez_fbin) of +delta' = k' - m p into h[2048] (KB4a's
+// histogram), and delta' == 0 / NaN elements into zn[0] / zn[1] so that the histogram of
+// -delta' can be mirrored from it.
 // h / zn point to LDS in K1a (flushed per workgroup) and to global memory in K1b.
 struct RezKHistOp {
     static constexpr bool kHist = true;
@@ -291,13 +305,10 @@ struct RezKHistOp {
     }
     __device__ float count(float mp) const {
         const float kp = floorf(mp + 0.5f);
-        float dp = (kp - mp) + 0.0f;
-        uint32_t u = __float_as_uint(dp);
-        if (dp != dp) u = 0x7FC00000u;
-        const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-        atomicAdd(&h[key >> 21], 1u);
-        if (key == 0x80000000u) atomicAdd(&zn[0], 1u);
-        else if (key == 0xFFC00000u) atomicAdd(&zn[1], 1u);
+        const float dp = (kp - mp) + 0.0f;                 // the value rez_key_of(dp, true) encodes
+        atomicAdd(&h[rez_fbin(dp)], 1u);
+        if (dp == 0.0f) atomicAdd(&zn[0], 1u);
+        else if (dp != dp) atomicAdd(&zn[1], 1u);
         return kp;
     }
     __device__ float operator()(float v) const { return count(fm * div1(fabsf(v), dp)); }
@@ -368,7 +379,7 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
     }
     if (Op::kHist) {
         for (int b = tid; b < 2048; b += blockDim.x)
-            if (hs[b]) atomicAdd(&hist_g[(size_t)vec * 3 * 2048 + b], hs[b]);
+            if (hs[b]) atomicAdd(&hist_g[((size_t)vec * kHistSlots + kFineSlot) * 2048 + b], hs[b]);
         if (tid < 2 && hs[2048 + tid]) atomicAdd(&zn_g[vec * 2 + tid], hs[2048 + tid]);
     }
 }
@@ -575,7 +586,7 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
     __syncthreads();
     if (Op::kHist) {
         for (int b = threadIdx.x; b < 2048; b += blockDim.x)
-            if (hs[b]) atomicAdd(&hist_g[(size_t)vec * 3 * 2048 + b], hs[b]);
+            if (hs[b]) atomicAdd(&hist_g[((size_t)vec * kHistSlots + kFineSlot) * 2048 + b], hs[b]);
         if (threadIdx.x < 2 && hs[2048 + threadIdx.x]) atomicAdd(&zn_g[vec * 2 + threadIdx.x], hs[2048 + threadIdx.x]);
     }
     // second pass of the two-pass reduction: out = 0 + cascade sum of the T-element buffer
@@ -2299,7 +2310,8 @@ struct BiasedLayout {
         pos_off, list_off, tls_off, tcnt2_off, alist_off, total;
     int32_t tiles;
     int32_t slots;
-    uint32_t cap;      // candidate capacity per client (compaction of the first-digit bucket)
+    uint32_t cap;      // candidate region per client in u32 (KB6f lists cap / 2 (index, key) pairs)
+    uint32_t capf;     // listed pairs per client at most: a larger fine bucket takes the full-row passes
 };
 
 BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
@@ -2312,7 +2324,8 @@ BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.st_off = up(w.msum_off + (size_t)n * sizeof(float));
     w.hist_off = up(w.st_off + (size_t)n * sizeof(RezState));
     w.cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(d, 1), std::max<int64_t>(4096, d / 8));
-    w.zn_off = up(w.hist_off + (size_t)n * 3 * kRadixBins * sizeof(uint32_t));
+    w.capf = w.cap / 2;
+    w.zn_off = up(w.hist_off + (size_t)n * kHistSlots * kRadixBins * sizeof(uint32_t));
     w.cn_off = w.zn_off + (size_t)n * 2 * sizeof(uint32_t);           // zn and cand_n adjacent
     w.cand_off = up(w.cn_off + (size_t)n * sizeof(uint32_t));
     w.tcnt_off = up(w.cand_off + (size_t)n * w.cap * sizeof(uint32_t));
@@ -2357,6 +2370,9 @@ int ilog2_pow2(int64_t D) {
 // ones.  KE2 keeps batches above kSegNormMaxN: it hides its chains behind the reads there,
 // while KE2s reads the vectors twice.
 constexpr int64_t kSegNormMaxN = 256;
+// ... and the dot's (KE4s): its one-wave-per-client form runs 6-19 VALU per step, so the
+// segmented form pays for its second read only with few clients
+constexpr int64_t kDotSegMaxN = 64;
 // biased quantizer: batches of at most this many clients run the candidate digits (KB4d) over
 // many workgroups per client (one workgroup per client walks up to d/8 keys twice)
 constexpr int64_t kCandMultiMaxN = 16;
@@ -2366,7 +2382,7 @@ bool segnorm_applies(int64_t n, int64_t D) {
 }
 
 struct SegNormLayout {
-    size_t segsum, g, e, kind, cnt, tseg, tab, total;      // offsets from the region start
+    size_t segsum, g, e, kind, cnt, tseg, tab, thr, acc, total;      // offsets from the region start
 };
 SegNormLayout segnorm_layout(int64_t n, int64_t D) {
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
@@ -2380,7 +2396,9 @@ SegNormLayout segnorm_layout(int64_t n, int64_t D) {
     L.tseg = up(L.cnt + (size_t)n * sizeof(int32_t));
     const size_t cap = (size_t)seg_tab_cap(D);
     L.tab = up(L.tseg + (size_t)n * cap * sizeof(int32_t));
-    L.total = up(L.tab + (size_t)n * cap * kSegTab * sizeof(float));
+    L.thr = up(L.tab + (size_t)n * cap * kSegTab * sizeof(float));   // KE4s: thresholds [n][4]
+    L.acc = up(L.thr + (size_t)n * 4 * sizeof(float));                 //       chain ends [n][64]
+    L.total = up(L.acc + (size_t)n * 64 * sizeof(float));
     return L;
 }
 
@@ -2404,12 +2422,44 @@ int launch_segnorm(const float* v, int64_t n, int64_t D, char* region, float* nr
     return hip_check(hipGetLastError(), "eden segmented norm launch");
 }
 
+// KE4s (few clients): the bins and the dot's 64 chains in segments, in the segmented norm's
+// region (the norm is done with it); the same bits as eden_dotbins_kernel
+int launch_eden_dotseg(const float* v, int64_t n, int64_t D, float sqrtD, const float* nrm, const EdenTables& tab,
+                       uint8_t* bins, float* scale, char* region, hipStream_t st) {
+    const SegNormLayout L = segnorm_layout(n, D);
+    double* segsum = (double*)(region + L.segsum);
+    float* g = (float*)(region + L.g);
+    float* e = (float*)(region + L.e);
+    int32_t* kind = (int32_t*)(region + L.kind);
+    int32_t* cnt = (int32_t*)(region + L.cnt);
+    int32_t* tseg = (int32_t*)(region + L.tseg);
+    float* tabv = (float*)(region + L.tab);
+    float* thr4 = (float*)(region + L.thr);
+    float* acc64 = (float*)(region + L.acc);
+    const int64_t K = D / kEdenTile;
+    const int cap = seg_tab_cap(D);
+    hipLaunchKernelGGL(eden_thresh_kernel, dim3((unsigned)n), dim3(64), 0, st, nrm, tab, thr4);
+    hipLaunchKernelGGL(eden_dseg_sum_kernel, dim3((unsigned)K, (unsigned)n), dim3(256), 0, st, v, D, sqrtD, nrm, thr4, tab,
+                       bins, segsum);
+    hipLaunchKernelGGL(eden_segscan_l_kernel<64>, dim3(64u, (unsigned)n), dim3(256), 0, st, segsum, K, g, cnt);
+    hipLaunchKernelGGL(eden_dseg_chain_kernel, dim3((unsigned)(K / kDSegTiles), (unsigned)n), dim3(256), 0, st, v, D, sqrtD,
+                       nrm, thr4, tab, g, e, kind, cnt, tseg, cap);
+    hipLaunchKernelGGL(eden_dseg_tab_kernel, dim3((unsigned)cap, (unsigned)n), dim3(256), 0, st, v, D, sqrtD, nrm, thr4, tab,
+                       g, cnt, tseg, tabv, cap);
+    hipLaunchKernelGGL(eden_dseg_walk_kernel, dim3(8u, (unsigned)n), dim3(512), 0, st, v, D, sqrtD, nrm, thr4, tab, g, e,
+                       kind, tabv, acc64, cap);
+    hipLaunchKernelGGL(eden_dseg_final_kernel, dim3((unsigned)n), dim3(64), 0, st, acc64, nrm, scale);
+    return hip_check(hipGetLastError(), "eden segmented dot launch");
+}
+
 // AS:329-335: the bins and the scale's dot in MKL sdot's order (KE4), scale = f32(nrm * nrm) / dot
 int launch_eden_dotbins(const float* v, int64_t n, int64_t D, float sqrtD, const float* nrm, const EdenTables& tab,
-                        uint8_t* bins, float* scale, hipStream_t st) {
+                        uint8_t* bins, float* scale, hipStream_t st, const int32_t* redo = nullptr) {
     const dim3 grid((unsigned)((n + kDotWaves - 1) / kDotWaves)), block(64 * kDotWaves);
-    if (tab.nb == 1) hipLaunchKernelGGL(eden_dotbins_kernel<1>, grid, block, 0, st, v, D, sqrtD, nrm, tab, bins, scale, n);
-    else hipLaunchKernelGGL(eden_dotbins_kernel<3>, grid, block, 0, st, v, D, sqrtD, nrm, tab, bins, scale, n);
+    if (tab.nb == 1)
+        hipLaunchKernelGGL(eden_dotbins_kernel<1>, grid, block, 0, st, v, D, sqrtD, nrm, tab, bins, scale, n, redo);
+    else
+        hipLaunchKernelGGL(eden_dotbins_kernel<3>, grid, block, 0, st, v, D, sqrtD, nrm, tab, bins, scale, n, redo);
     return hip_check(hipGetLastError(), "eden_dotbins_kernel launch");
 }
 
@@ -2423,7 +2473,7 @@ int launch_chainnorm(const float* v, int64_t n, int64_t D, float* nrm, hipStream
 }
 
 struct EdenLayout {
-    size_t vec_off, nrm_off, bins_off, scale_off, seg_off, total;
+    size_t vec_off, nrm_off, bins_off, scale_off, redo_off, seg_off, total;
     int64_t D;
     int32_t tiles;
     bool seg;                 // the segmented norm (its region at seg_off)
@@ -2438,7 +2488,8 @@ EdenLayout eden_layout(int64_t n, int64_t dim) {
     w.nrm_off = up(w.vec_off + (size_t)n * w.D * sizeof(float));
     w.bins_off = up(w.nrm_off + (size_t)n * sizeof(float));
     w.scale_off = up(w.bins_off + (size_t)n * w.D);
-    w.seg_off = up(w.scale_off + (size_t)n * sizeof(float));
+    w.redo_off = up(w.scale_off + (size_t)n * sizeof(float));
+    w.seg_off = up(w.redo_off + (size_t)n * sizeof(int32_t));
     w.seg = segnorm_applies(n, w.D);
     w.total = w.seg_off + (w.seg ? segnorm_layout(n, w.D).total : 0);
     return w;
@@ -3275,33 +3326,40 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     const bool vec4 = aligned16(x) && aligned16(out) && d % 4 == 0;
     const dim3 hgrid((unsigned)((d + kHistSpan - 1) / kHistSpan), (unsigned)n);
     const dim3 tgrid((unsigned)w.tiles, (unsigned)n);
-    hipLaunchKernelGGL(rez_select_kernel<0>, dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.cap);
-    // compact-mode clients: the chosen bucket's keys, then digits 2-3 on them
-    const dim3 cgrid((unsigned)((d + kCompactSpan - 1) / kCompactSpan), (unsigned)n);
-    if (vec4)
-        hipLaunchKernelGGL(rez_compact_kernel<true>, cgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
-    else
-        hipLaunchKernelGGL(rez_compact_kernel<false>, cgrid, dim3(256), 0, st, x, d, l1buf, fm, state, cand, cand_n, w.cap);
-    const unsigned cspans = (unsigned)((w.cap + kCandSpan - 1) / kCandSpan);
-    if (n <= kCandMultiMaxN && cspans > 1) {         // few clients: digits 2-3 over many workgroups
-        hipLaunchKernelGGL(rez_cand_hist_kernel<1>, dim3(cspans, (unsigned)n), dim3(256), 0, st, state, cand, cand_n,
-                           w.cap, hist);
-        hipLaunchKernelGGL(rez_cand_pick_kernel<1>, dim3((unsigned)n), dim3(256), 0, st, state, hist);
-        hipLaunchKernelGGL(rez_cand_hist_kernel<2>, dim3(cspans, (unsigned)n), dim3(256), 0, st, state, cand, cand_n,
-                           w.cap, hist);
-        hipLaunchKernelGGL(rez_cand_pick_kernel<2>, dim3((unsigned)n), dim3(256), 0, st, state, hist);
-    } else {
-        hipLaunchKernelGGL(rez_cand_select_kernel, dim3((unsigned)n), dim3(256), 0, st, state, cand, cand_n, w.cap);
-    }
-    // the others: full-vector histogram passes for digits 2-3
+    const dim3 fgrid((unsigned)((d + kSelTile - 1) / kSelTile), (unsigned)n);
+    uint2* fcand = (uint2*)cand;
+    // KB4a: the threshold's fine bin; a small bucket makes the client "fine", a large one "full"
+    hipLaunchKernelGGL((rez_select_kernel<0, true>), dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.capf);
+    // full clients (tie-heavy rows): the key digits by three full-row histogram passes
 #define UQ_RADIX(P)                                                                                          \
     if (vec4)                                                                                                \
         hipLaunchKernelGGL((rez_hist_kernel<P, true>), hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist); \
     else                                                                                                     \
         hipLaunchKernelGGL((rez_hist_kernel<P, false>), hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist); \
-    hipLaunchKernelGGL(rez_select_kernel<P>, dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.cap);
-    UQ_RADIX(1) UQ_RADIX(2)
+    hipLaunchKernelGGL((rez_select_kernel<P, false>), dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.capf);
+    UQ_RADIX(0) UQ_RADIX(1) UQ_RADIX(2)
 #undef UQ_RADIX
+    // fine clients: KB6f writes every output and lists the bucket, KB4d finds the threshold
+    // key among the listed keys, KB6p patches the selected listed coordinates (tie-free clients)
+    if (vec4)
+        hipLaunchKernelGGL(rez_output_fine_kernel<true>, fgrid, dim3(256), 0, st, x, out, d, l1buf, fm, state, fcand,
+                           cand_n, w.capf);
+    else
+        hipLaunchKernelGGL(rez_output_fine_kernel<false>, fgrid, dim3(256), 0, st, x, out, d, l1buf, fm, state, fcand,
+                           cand_n, w.capf);
+    const unsigned cspans = (unsigned)((w.capf + kCandSpan - 1) / kCandSpan);
+    if (n <= kCandMultiMaxN && cspans > 1) {         // few clients: the passes over many workgroups
+#define UQ_CAND(P)                                                                                           \
+        hipLaunchKernelGGL(rez_cand_hist_kernel<P>, dim3(cspans, (unsigned)n), dim3(256), 0, st, state, fcand, cand_n, \
+                           w.capf, hist);                                                                    \
+        hipLaunchKernelGGL(rez_cand_pick_kernel<P>, dim3((unsigned)n), dim3(256), 0, st, state, hist);
+        UQ_CAND(0) UQ_CAND(1) UQ_CAND(2)
+#undef UQ_CAND
+    } else {
+        hipLaunchKernelGGL(rez_cand_select_kernel, dim3((unsigned)n), dim3(256), 0, st, state, fcand, cand_n, w.capf);
+    }
+    hipLaunchKernelGGL(rez_fine_patch_kernel, dim3(kPatchBlocks, (unsigned)n), dim3(256), 0, st, x, out, d, l1buf, fm,
+                       state, fcand, cand_n, w.capf);
     rc = hip_check(hipGetLastError(), "radix select launch");
     if (rc) return rc;
     auto output = [&](hipStream_t os, int part) {
@@ -3570,11 +3628,34 @@ int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, 
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     float* nrm = (float*)(wsb + w.nrm_off);
+    if (!w.seg && tab.nb == 1 && w.D % kNormChunk == 0) {
+        // 1 bit, many clients: the norm, the bins and the dot in one read (KE2+4), then KE4 for
+        // the clients it flags (a norm that is not positive and finite, an underflowing quotient)
+        FwhtArgs a{};
+        a.in = x;
+        a.signs = signs;
+        a.sign_row = sign_row;
+        a.D = w.D;
+        a.dim = dim;
+        a.sqrtD = (float)std::sqrt((double)w.D);
+        float* vec = (float*)(wsb + w.vec_off);
+        float* rot = nullptr;
+        rc = launch_fwht(a, n, false, vec, vec, st, &rot);                          // AS:123-141
+        if (rc) return rc;
+        int32_t* redo = (int32_t*)(wsb + w.redo_off);
+        hipLaunchKernelGGL(eden_normdot1_kernel, dim3((unsigned)((n + kNormClients - 1) / kNormClients)),
+                           dim3(kNDThreads), 0, st, rot, n, w.D, a.sqrtD, tab, nrm, bins, scale, redo);
+        rc = hip_check(hipGetLastError(), "eden_normdot1_kernel launch");           // AS:329-335
+        if (rc) return rc;
+        return launch_eden_dotbins(rot, n, w.D, a.sqrtD, nrm, tab, bins, scale, st, redo);
+    }
     FwhtArgs a;
     float* vec = nullptr;
     rc = eden_front(x, n, dim, tab, signs, sign_row, w, wsb, a, &vec, st);
     if (rc) return rc;
-    return launch_eden_dotbins(vec, n, w.D, a.sqrtD, nrm, tab, bins, scale, st);   // AS:329-335
+    if (w.seg && n <= kDotSegMaxN)                                                   // AS:329-335
+        return launch_eden_dotseg(vec, n, w.D, a.sqrtD, nrm, tab, bins, scale, wsb + w.seg_off, st);
+    return launch_eden_dotbins(vec, n, w.D, a.sqrtD, nrm, tab, bins, scale, st);
 }
 
 int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, int64_t dim, int32_t nbits,

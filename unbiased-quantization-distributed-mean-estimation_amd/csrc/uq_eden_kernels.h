@@ -1107,11 +1107,12 @@ __device__ __forceinline__ float dotbins_chains(const float* __restrict__ vj, in
 template <int NB>       // boundaries: 1 (1 bit) or 3 (2 bits)
 __global__ void __launch_bounds__(64 * kDotWaves)
 eden_dotbins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm, EdenTables tab,
-                    uint8_t* __restrict__ bins, float* __restrict__ scale, int64_t n) {
+                    uint8_t* __restrict__ bins, float* __restrict__ scale, int64_t n, const int32_t* __restrict__ redo) {
     __shared__ float red[kDotWaves][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t j = (int64_t)blockIdx.x * kDotWaves + wv;
     if (j >= n) return;                                                    // whole wave
+    if (redo && !redo[j]) return;                                          // (after KE2+4: its flagged clients)
     const float nv = nrm[j];
     const EdenCents cs = eden_cents(tab);
     const bool thr = nv > 0.f && nv < INFINITY;                            // wave-uniform
@@ -1136,5 +1137,465 @@ eden_dotbins_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const f
         for (int l = 0; l < 4; ++l) w[l] = w[l] + w[l + 4];
         const float dot = (w[0] + w[1]) + (w[2] + w[3]);
         scale[j] = (nv * nv) / dot;                                        // AS:335 norm ** 2 / dot
+    }
+}
+
+// ---- KE4s: the same bins and dot for small batches, its chains cut into segments ----------
+// eden_dotbins_kernel runs each client's 64 chains of D/64 dependent fmas on one wave: with a
+// few clients the chain is the kernel (D/64 steps of ~6-19 VALU each: 0.35 ms at n = 1,
+// D = 2^20).  As KE2s does for the norm, the chains are cut into segments of kSegSteps steps;
+// a segment of all 64 chains is one 4096-element tile (chain l, step 64 k + i = element
+// 4096 k + 64 i + l).  Every chain here is non-decreasing (c[bin] has the sign of v, so each
+// product is >= 0), and the KE2s argument applies unchanged with p = c * v instead of v * v:
+//   KE4a  bins, and the fp64 sum of c * v per (chain, segment)                (approximate)
+//   KE4b  guesses g = f32(fp64 exclusive prefix) per segment (eden_segscan_kernel<64>)
+//   KE4c  the segment's f32 fma chain from g -> e; segments whose chain crosses a binade,
+//         meets (or cannot rule out) a tie, or starts / ends near a binade edge are listed
+//   KE4t  the chain run from each of the kSegTab starts around g for the listed segments
+//   KE4d  one wave per chain walks its segments from 0 (wave scans of e - g, tables, steps)
+//   KE4f  the 64 chains in MKL's order, scale = f32(nrm * nrm) / dot
+// The per-client thresholds of the bins (eden_thresh) are computed once by KE4p.
+constexpr int kDSegTiles = 4;                            // KE4c: tiles (segments) per workgroup
+
+struct DotElem {                                         // c[bin(v)] of one client
+    float sqrtD, nv, T0, T1, T2;
+    bool thr;
+    EdenTables tab;
+    EdenCents cs;
+    __device__ __forceinline__ int bin(float x) const {
+        const float y = x * sqrtD;                       // AS:329 vec * sqrt(D)
+        if (!thr) return eden_bin(tab, y / nv);
+        int b = !(y <= T0) ? 1 : 0;
+        if (tab.nb > 1) b += (!(y <= T1) ? 1 : 0) + (!(y <= T2) ? 1 : 0);
+        return b;
+    }
+    __device__ __forceinline__ float cent(float x) const { return eden_cent(cs, bin(x)); }
+};
+__device__ __forceinline__ DotElem dot_elem(const float* thr4, const float* nrm, int64_t j, float sqrtD,
+                                            const EdenTables& tab) {
+    DotElem e;
+    e.sqrtD = sqrtD;
+    e.nv = nrm[j];
+    e.T0 = thr4[j * 4];
+    e.T1 = thr4[j * 4 + 1];
+    e.T2 = thr4[j * 4 + 2];
+    e.thr = thr4[j * 4 + 3] != 0.f;
+    e.tab = tab;
+    e.cs = eden_cents(tab);
+    return e;
+}
+
+// KE4p: thresholds per client (lane q: boundary q), thr4[j] = (T0, T1, T2, valid)
+__global__ void __launch_bounds__(64)
+eden_thresh_kernel(const float* __restrict__ nrm, EdenTables tab, float* __restrict__ thr4) {
+    const int64_t j = blockIdx.x;
+    const int lane = threadIdx.x;
+    const float nv = nrm[j];
+    const bool ok = nv > 0.f && nv < INFINITY;
+    if (lane < 3) thr4[j * 4 + lane] = (ok && lane < tab.nb) ? eden_thresh(tab.b[lane], nv) : 0.f;
+    if (lane == 3) thr4[j * 4 + 3] = ok ? 1.f : 0.f;
+}
+
+// KE4a: one tile per workgroup; thread (g, l) sums steps 16 g .. 16 g + 15 of chain l
+__global__ void __launch_bounds__(256)
+eden_dseg_sum_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm,
+                     const float* __restrict__ thr4, EdenTables tab, uint8_t* __restrict__ bins,
+                     double* __restrict__ segsum) {
+    __shared__ double part[4][64];
+    const int tid = threadIdx.x, l = tid & 63, g = tid >> 6;
+    const int64_t client = blockIdx.y, k = blockIdx.x, K = D / kEdenTile;
+    const DotElem de = dot_elem(thr4, nrm, client, sqrtD, tab);
+    const float* t = v + client * D + k * kEdenTile;
+    uint8_t* bt = bins + client * D + k * kEdenTile;
+    float x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = t[64 * (16 * g + i) + l];
+    double acc = 0.0;                                    // an approximation: any order will do
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int b = de.bin(x[i]);
+        bt[64 * (16 * g + i) + l] = (uint8_t)b;
+        acc += (double)eden_cent(de.cs, b) * (double)x[i];
+    }
+    part[g][l] = acc;
+    __syncthreads();
+    if (tid < 64) segsum[(client * 64 + l) * K + k] = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
+}
+
+// KE4b: exclusive prefix per (chain, client) of its K segment sums (the norm's scan, 64 chains)
+template <int L>
+__global__ void __launch_bounds__(256)
+eden_segscan_l_kernel(const double* __restrict__ segsum, int64_t K, float* __restrict__ g, int32_t* __restrict__ tabcnt) {
+    __shared__ double wsum[256 / kWave];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+    const int l = blockIdx.x;
+    const int64_t client = blockIdx.y;
+    if (tid == 0 && l == 0) tabcnt[client] = 0;
+    const double* src = segsum + (client * L + l) * K;
+    float* dst = g + (client * L + l) * K;
+    double carry = 0.0;
+    for (int64_t r0 = 0; r0 < K; r0 += 1024) {
+        double xs[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t i = r0 + 4 * tid + q;
+            xs[q] = i < K ? src[i] : 0.0;
+        }
+        const double t = (xs[0] + xs[1]) + (xs[2] + xs[3]);
+        const double incl = wave_incl_scan(t, lane);
+        if (lane == kWave - 1) wsum[wid] = incl;
+        __syncthreads();
+        double run = carry + wave_prev(incl), tot = carry;
+#pragma unroll
+        for (int w = 0; w < 256 / kWave; ++w) {
+            if (w < wid) run += wsum[w];
+            tot += wsum[w];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t i = r0 + 4 * tid + q;
+            if (i < K) dst[i] = (float)run;
+            run += xs[q];
+        }
+        carry = tot;
+    }
+}
+
+// KE4c: thread (tile k, chain l) runs its segment's 64 steps from the guess (the KE2c tests)
+__global__ void __launch_bounds__(256)
+eden_dseg_chain_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm,
+                       const float* __restrict__ thr4, EdenTables tab, const float* __restrict__ g,
+                       float* __restrict__ e, int32_t* __restrict__ kind, int32_t* __restrict__ tabcnt,
+                       int32_t* __restrict__ tabseg, int cap) {
+    const int tid = threadIdx.x, l = tid & 63;
+    const int64_t client = blockIdx.y, K = D / kEdenTile;
+    const int64_t k = (int64_t)blockIdx.x * kDSegTiles + (tid >> 6);
+    const DotElem de = dot_elem(thr4, nrm, client, sqrtD, tab);
+    const float* t = v + client * D + k * kEdenTile + l;
+    const int64_t idx = (client * 64 + l) * K + k;
+    const float g0 = g[idx];
+    float b = g0;
+    bool tie = false;
+#pragma unroll 16
+    for (int i = 0; i < kSegSteps; ++i) {
+        const float x = t[64 * i];
+        const float c = de.cent(x);
+        // a negative product (a tiny v whose quotient underflowed into the lowest bin) breaks
+        // the chain's monotonicity: list the segment (its table or its steps are sequential)
+        tie = tie || (((fbits(c) ^ fbits(x)) >> 31) && x != 0.0f && c != 0.0f);
+        const float r = fmaf(c, x, b);
+        // (b + c*x) - r exactly: a midpoint is u/2, or u/4 just below a power of two (KE2c)
+        const int er = fexp(r);
+        const double u = __longlong_as_double((long long)((uint64_t)(std::max(er, 1) - 150 + 1023) << 52));
+        const double res = fabs(fma((double)c, (double)x, (double)b - (double)r));
+        tie = tie || res == 0.5 * u || res == 0.25 * u || (b != 0.0f && er - fexp(b) > 28);
+        b = r;
+    }
+    const int eg = fexp(g0);
+    const bool finite = eg < 255 && fexp(b) < 255;
+    const bool cross = fexp(b) != eg;
+    const bool near_bottom = eg > 0 && (fbits(g0) & 0x7FFFFFu) < (uint32_t)(kSegTab / 2);
+    const bool near_top = !cross && (((uint32_t)(eg + 1) << 23) - fbits(b)) <= (uint32_t)(kSegTab / 2);
+    int32_t kk = 0;
+    if (!finite || cross || tie || near_bottom || near_top) {
+        const int slot = atomicAdd(&tabcnt[client], 1);
+        if (slot < cap) {
+            kk = slot + 1;
+            tabseg[client * cap + slot] = (int32_t)(k * 64 + l);
+        } else {
+            kk = -1;                                     // no table: KE4d runs its steps
+        }
+    }
+    e[idx] = b;
+    kind[idx] = kk;
+}
+
+// KE4t: the listed segment's chain from each of the kSegTab starts around its guess
+__global__ void __launch_bounds__(256)
+eden_dseg_tab_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm,
+                     const float* __restrict__ thr4, EdenTables tab, const float* __restrict__ g,
+                     const int32_t* __restrict__ tabcnt, const int32_t* __restrict__ tabseg, float* __restrict__ tabv,
+                     int cap) {
+    __shared__ float xs[kSegSteps], cs_[kSegSteps];
+    const int64_t client = blockIdx.y;
+    const int slot = blockIdx.x;
+    if (slot >= std::min(tabcnt[client], cap)) return;                   // uniform
+    const int tid = threadIdx.x;
+    const int32_t code = tabseg[client * cap + slot];
+    const int64_t k = code >> 6;
+    const int l = code & 63;
+    const int64_t K = D / kEdenTile;
+    if (tid < kSegSteps) {
+        const DotElem de = dot_elem(thr4, nrm, client, sqrtD, tab);
+        const float x = v[client * D + k * kEdenTile + 64 * tid + l];
+        xs[tid] = x;
+        cs_[tid] = de.cent(x);
+    }
+    __syncthreads();
+    const int64_t gb = fbits(g[(client * 64 + l) * K + k]);
+    constexpr int kPer = kSegTab / 256;
+    float a[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int64_t sb = gb + tid + 256 * q - kSegTab / 2;
+        a[q] = sb < 0 ? __uint_as_float(0x7FC00000u) : __uint_as_float((uint32_t)sb);   // (never looked up)
+    }
+    for (int i = 0; i < kSegSteps; ++i) {
+        const float x = xs[i], c = cs_[i];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) a[q] = fmaf(c, x, a[q]);
+    }
+    float* out = tabv + ((int64_t)client * cap + slot) * kSegTab;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) out[tid + 256 * q] = a[q];
+}
+
+// KE4d: wave w of workgroup b walks chain 8 b + w of client blockIdx.y (KE2d's walk); the
+// chain's end goes to acc64[client][chain]
+__global__ void __launch_bounds__(512)
+eden_dseg_walk_kernel(const float* __restrict__ v, int64_t D, float sqrtD, const float* __restrict__ nrm,
+                      const float* __restrict__ thr4, EdenTables tab, const float* __restrict__ g,
+                      const float* __restrict__ e, const int32_t* __restrict__ kind, const float* __restrict__ tabv,
+                      float* __restrict__ acc64, int cap) {
+    const int tid = threadIdx.x, lane = tid & (kWave - 1);
+    const int l = blockIdx.x * 8 + tid / kWave;
+    const int64_t client = blockIdx.y;
+    const int64_t K = D / kEdenTile;
+    const int64_t base = (client * 64 + l) * K;
+    const DotElem de = dot_elem(thr4, nrm, client, sqrtD, tab);
+    float cg[kWalkChunks], ce[kWalkChunks], ng[kWalkChunks] = {}, ne[kWalkChunks] = {};
+    int32_t ck[kWalkChunks], nk[kWalkChunks] = {};
+    auto fetch = [&](int64_t tile, float (&fg)[kWalkChunks], float (&fe)[kWalkChunks], int32_t (&fk)[kWalkChunks]) {
+#pragma unroll
+        for (int q = 0; q < kWalkChunks; ++q) {
+            const int64_t s = (tile * kWalkChunks + q) * kWave + lane;
+            fg[q] = s < K ? g[base + s] : 0.0f;
+            fe[q] = s < K ? e[base + s] : 0.0f;
+            fk[q] = s < K ? kind[base + s] : 0;
+        }
+    };
+    float A = 0.0f;                                    // wave-uniform
+    int64_t s0 = 0;
+    auto step = [&](int64_t c, float sg, float se, int32_t sk) {
+        const int o = (int)(s0 - c * kWave);
+        const bool inb = lane >= o && c * kWave + lane < K;
+        const bool fin = fexp(sg) < 255 && fexp(se) < 255;
+        const double tau = (inb && fin) ? (double)se - (double)sg : 0.0;   // >= 0: chains never decrease
+        const double Aj = (double)A + wave_prev(wave_incl_scan(tau, lane));
+        const bool span = A > 0.0f && fexp(A) < 255;
+        const double lim = __longlong_as_double((long long)((uint64_t)(std::max(fexp(A), 1) - 127 + 28 + 1023) << 52));
+        const float af = (float)Aj;
+        const float r = af + (float)tau;
+        const bool valid = inb && fin && (lane == o || (span && Aj + tau < lim)) && (double)af == Aj &&
+                           (af == sg || (sk == 0 && fexp(af) == fexp(sg) && fexp(r) == fexp(sg)));
+        const uint64_t bad = __ballot(inb && !valid);
+        const uint64_t inm = __ballot(inb);
+        const int first = bad ? __builtin_ctzll(bad) : 64 - __builtin_clzll(inm);
+        if (first > o) {
+            const float res = af == sg ? se : r;
+            A = __shfl(res, first - 1, kWave);
+            s0 = c * kWave + first;
+            return;
+        }
+        const int32_t kk = __shfl(sk, o, kWave);
+        const float gg = __shfl(sg, o, kWave);
+        bool done = false;
+        if (kk > 0) {
+            const int64_t dd = (int64_t)fbits(A) - (int64_t)fbits(gg) + kSegTab / 2;
+            if (dd >= 0 && dd < kSegTab) {
+                A = tabv[((int64_t)client * cap + (kk - 1)) * kSegTab + dd];
+                done = true;
+            }
+        }
+        if (!done) {
+            const float x = v[client * D + s0 * kEdenTile + 64 * lane + l];
+            const float c = de.cent(x);
+            for (int i = 0; i < kSegSteps; ++i) {
+                const float xi = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)fbits(x), i));
+                const float ci = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)fbits(c), i));
+                A = fmaf(ci, xi, A);
+            }
+        }
+        s0 += 1;
+    };
+    fetch(0, cg, ce, ck);
+    const int64_t tiles = (K + kWalkChunks * kWave - 1) / (kWalkChunks * kWave);
+    for (int64_t t = 0; t < tiles; ++t) {
+        if (t + 1 < tiles) fetch(t + 1, ng, ne, nk);
+#pragma unroll
+        for (int q = 0; q < kWalkChunks; ++q) {
+            const int64_t c = t * kWalkChunks + q;
+            const int64_t cend = std::min<int64_t>(K, (c + 1) * kWave);
+            while (s0 < cend) step(c, cg[q], ce[q], ck[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < kWalkChunks; ++q) {
+            cg[q] = ng[q];
+            ce[q] = ne[q];
+            ck[q] = nk[q];
+        }
+    }
+    if (lane == 0) acc64[client * 64 + l] = A;
+}
+
+// KE4f: the 64 chains in MKL's order, scale = f32(nrm * nrm) / dot (AS:335)
+__global__ void __launch_bounds__(64)
+eden_dseg_final_kernel(const float* __restrict__ acc64, const float* __restrict__ nrm, float* __restrict__ scale) {
+    const int64_t j = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    const float* a = acc64 + j * 64;
+    float w[16];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) w[l] = (a[l] + a[16 + l]) + (a[32 + l] + a[48 + l]);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) w[l] = w[l] + w[l + 8];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) w[l] = w[l] + w[l + 4];
+    const float dot = (w[0] + w[1]) + (w[2] + w[3]);
+    const float nv = nrm[j];
+    scale[j] = (nv * nv) / dot;
+}
+
+// ---- KE2+4: the 1-bit norm, bins and dot in one read (batches of more than 256 clients) --
+// With one boundary at 0, bucketize(v * sqrt(D) / norm) is v's sign -- 1 for v > 0 (and NaN),
+// else 0 -- unless the quotient underflows to 0 (a positive v below ~2^-149 * norm / sqrt(D))
+// or the norm is not positive and finite.  So the bins, and with them the dot's chains, need no
+// norm: KE2's workgroup (4 clients, loader waves staging chunks in LDS, one wave on the
+// norm's 32 chains) gets one more wave per client that runs that client's 64 dot chains from
+// the same LDS image, and the loaders write the bins and track the smallest positive v * sqrt(D).
+// At the end the norm is known: a client whose norm is not positive and finite, or whose
+// smallest positive product underflows, is flagged and recomputed by the exact KE4
+// (eden_dotbins_kernel with `redo`); every other client's bins and scale are KE4's bits.
+constexpr int kNDThreads = 64 + 256 + 64 * kNormClients;
+__global__ void __launch_bounds__(kNDThreads)
+eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sqrtD, EdenTables tab,
+                     float* __restrict__ nrm, uint8_t* __restrict__ bins, float* __restrict__ scale,
+                     int32_t* __restrict__ redo) {
+    __shared__ __attribute__((aligned(16))) float s[3][kNormBuf];
+    __shared__ float dacc[kNormClients][64];
+    __shared__ uint32_t minpos[kNormClients];
+    const int tid = threadIdx.x;
+    const int64_t v0 = (int64_t)blockIdx.x * kNormClients;
+    const int64_t nchunks = D / kNormChunk;
+    const bool chain = tid < kWave;
+    const bool loader = tid >= kWave && tid < kWave + 256;
+    const bool dotw = tid >= kWave + 256;
+    const int lt = tid - kWave, lk = lt >> 6, lj = lt & 63;
+    const bool lvalid = loader && v0 + lk < n;
+    const float* lp = v + (lvalid ? v0 + lk : 0) * D;
+    uint8_t* lb = bins + (lvalid ? v0 + lk : 0) * D;
+    if (tid < kNormClients) minpos[tid] = 0x7F800000u;                 // +inf
+    constexpr int kLQ = kNormChunk / 256;
+    float4 na[kLQ], nb[kLQ];
+    uint32_t mymin = 0x7F800000u;                                      // bits of the smallest positive y
+    auto load = [&](float4 (&nx)[kLQ], int64_t ch) {
+        if (!lvalid || ch >= nchunks) return;
+#pragma unroll
+        for (int q = 0; q < kLQ; ++q) nx[q] = ld_stream(reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q)));
+    };
+    auto store = [&](const float4 (&nx)[kLQ], float* sb, int64_t ch) {
+        if (!loader) return;
+#pragma unroll
+        for (int q = 0; q < kLQ; ++q) {
+            const int e = 4 * (lj + 64 * q);
+            const int i = e >> 3, l = e & 7;
+            float* base = sb + lk * kNormClientStride + i;
+            base[(l + 0) * kNormRow] = nx[q].x;
+            base[(l + 1) * kNormRow] = nx[q].y;
+            base[(l + 2) * kNormRow] = nx[q].z;
+            base[(l + 3) * kNormRow] = nx[q].w;
+            if (lvalid) {                                              // the bins of these 4 (sign rule)
+                const float xs[4] = {nx[q].x, nx[q].y, nx[q].z, nx[q].w};
+                uint32_t w = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float y = xs[c] * sqrtD;
+                    w |= (!(y <= 0.f) ? 1u : 0u) << (8 * c);
+                    if (y > 0.f) mymin = min(mymin, __float_as_uint(y));
+                }
+                *reinterpret_cast<uint32_t*>(lb + ch * kNormChunk + e) = w;
+            }
+        }
+    };
+    const int ck = (tid >> 3) & (kNormClients - 1), cl = tid & 7;
+    float acc = 0.f;
+    const int dk = (tid - kWave - 256) >> 6, dl = tid & 63;           // dot wave: client dk, chain dl
+    const EdenCents cs = eden_cents(tab);
+    auto chainstep = [&](int64_t ch) {
+        if (chain) {
+            const float* row = s[ch % 3] + ck * kNormClientStride + cl * kNormRow;
+            for (int i = 0; i < kNormChunk / 8; i += 16) {
+                float4 t[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const float4*>(row + i + 4 * u);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc = fmaf(t[u].x, t[u].x, acc);
+                    acc = fmaf(t[u].y, t[u].y, acc);
+                    acc = fmaf(t[u].z, t[u].z, acc);
+                    acc = fmaf(t[u].w, t[u].w, acc);
+                }
+            }
+        } else if (dotw) {
+            // element 64 s + dl of the chunk sits at lane (dl % 8), step 8 s + dl / 8 of the image
+            const float* row = s[ch % 3] + dk * kNormClientStride + (dl & 7) * kNormRow + (dl >> 3);
+#pragma unroll 8
+            for (int st = 0; st < kNormChunk / 64; ++st) {
+                const float x = row[8 * st];
+                const float c = !(x * sqrtD <= 0.f) ? cs.c1 : cs.c0;   // AS:335 take(centroids, bins)
+                acc = fmaf(c, x, acc);
+            }
+        }
+    };
+    if (loader) {
+        load(na, 0);
+        store(na, s[0], 0);
+        load(na, 1);
+        load(nb, 2);
+    }
+    __syncthreads();
+    for (int64_t ch = 0; ch < nchunks; ch += 2) {
+        chainstep(ch);
+        if (loader && ch + 1 < nchunks) {
+            store(na, s[(ch + 1) % 3], ch + 1);
+            load(na, ch + 3);
+        }
+        __syncthreads();
+        if (ch + 1 >= nchunks) break;
+        chainstep(ch + 1);
+        if (loader && ch + 2 < nchunks) {
+            store(nb, s[(ch + 2) % 3], ch + 2);
+            load(nb, ch + 4);
+        }
+        __syncthreads();
+    }
+    if (lvalid) atomicMin(&minpos[lk], mymin);
+    if (dotw) dacc[dk][dl] = acc;
+    float nv = 0.f;
+    if (chain) {
+        const int base = tid & ~7;
+        float tot = __shfl(acc, base, kWave);
+        for (int j = 1; j < 8; ++j) tot = tot + __shfl(acc, base + j, kWave);
+        nv = sqrtf(tot);
+        const int64_t vec = v0 + ck;
+        if (tid < 8 * kNormClients && cl == 0 && vec < n) nrm[vec] = nv;
+    }
+    __syncthreads();
+    if (chain && tid < 8 * kNormClients && cl == 0 && v0 + ck < n) {
+        const int64_t vec = v0 + ck;
+        const float* a = dacc[ck];
+        float w[16];
+#pragma unroll
+        for (int l = 0; l < 16; ++l) w[l] = (a[l] + a[16 + l]) + (a[32 + l] + a[48 + l]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) w[l] = w[l] + w[l + 8];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) w[l] = w[l] + w[l + 4];
+        const float dot = (w[0] + w[1]) + (w[2] + w[3]);
+        scale[vec] = (nv * nv) / dot;                                  // AS:335 norm ** 2 / dot
+        const float mp = __uint_as_float(minpos[ck]);
+        const bool ok = nv > 0.f && nv < INFINITY && (mp == INFINITY || mp / nv > 0.f);
+        redo[vec] = ok ? 0 : 1;
     }
 }
