@@ -273,7 +273,10 @@ int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, c
  *   idx = ((floor(q) + b) * h_len + h) + half_table in f32, truncated (torch.take wraps
  *       negatives), half_table = ((table_numel / h_len) - 1) * h_len / 2   (AS:443, AS:486);
  *   X = table[idx].X + bernoulli(table[idx].p) from a second generator, truncated (AS:489-490).
- * table_xp: device f32 [table_numel][2] = (sender_table_X, sender_table_p) pairs.
+ * table_xp: device f32 [table_numel][2] = (sender_table_X, sender_table_p) pairs; table_packed
+ *   (or NULL): the same table as u32 (X << 25) | ceil(p * 2^24), valid when every X is an integer
+ *   in 0..127 and every p in [0, 1] (the caller checks): one 4-byte gather per coordinate instead
+ *   of 8 -- bernoulli(p) draws low24(w) * 2^-24 < p, i.e. low24(w) < ceil(p * 2^24), the same bits.
  * The second generator (the reference's global torch generator): px_state [n][626] u32 =
  *   (left, next, state[624]) of ATen's mt19937 per message (next = 625 - left unless left = 1),
  *   or px_state = NULL and px_seeds [n] (fresh generators, manual_seed(px_seeds[j]));
@@ -293,7 +296,8 @@ int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, c
 #define UQ_QFL_STATE_WORDS 626
 int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out);
 int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
-                           const float* table_xp, int64_t table_numel, int32_t h_len, float delta,
+                           const float* table_xp, const uint32_t* table_packed, int64_t table_numel, int32_t h_len,
+                           float delta,
                            const int32_t* prng_seeds, const uint32_t* px_state, const int32_t* px_seeds,
                            uint32_t* px_state_out, void* X, int32_t x_kind, uint8_t* exact_mask, float* exact_vals,
                            int32_t* exact_count, float* scale, int32_t* info, void* ws, size_t ws_bytes, void* stream);
@@ -308,8 +312,8 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
  * uq_quicfl_compress_f32 plus UQ_QFL_RECV_INDEX.  Workspace: uq_quicfl_workspace_bytes. */
 #define UQ_QFL_RECV_INDEX 64
 int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
-                           const float* table_xp, int64_t table_numel, int32_t h_len, float delta,
-                           const float* recv_table, int32_t recv_numel, const int32_t* prng_seeds,
+                           const float* table_xp, const uint32_t* table_packed, int64_t table_numel, int32_t h_len,
+                           float delta, const float* recv_table, int32_t recv_numel, const int32_t* prng_seeds,
                            const uint32_t* px_state, const int32_t* px_seeds, uint32_t* px_state_out, float* out,
                            float* scale, int32_t* info, void* ws, size_t ws_bytes, void* stream);
 /* xxHash64 of `len` bytes (AS:457 hashes str(seed) with seed 0); host-only, no GPU. */

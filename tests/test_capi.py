@@ -176,16 +176,16 @@ def test_xxh64_and_quicfl_argument_checks(lib):
         assert lib.uq_xxh64(b, len(b), 0) == Q.xxh64(b)
     sz = ctypes.c_size_t()
     assert lib.uq_quicfl_workspace_bytes(4, 1000, ctypes.byref(sz)) == 0 and sz.value >= 4 * 1024 * 5
-    args = [None, 1, 1000, None, None, None, 64 * 3, 64, 0.5, None, None, None, None, None, 0, None, None, None,
-            None, None, None, 0, None]
+    args = [None, 1, 1000, None, None, None, None, 64 * 3, 64, 0.5, None, None, None, None, None, 0, None, None,
+            None, None, None, None, 0, None]
     bad = list(args)
-    bad[7] = 300                                   # h_len > 256
+    bad[8] = 300                                   # h_len > 256
     assert lib.uq_quicfl_compress_f32(*bad) == -1
     bad = list(args)
-    bad[6] = 100                                   # numel not a multiple of h_len
+    bad[7] = 100                                   # numel not a multiple of h_len
     assert lib.uq_quicfl_compress_f32(*bad) == -1
     bad = list(args)
-    bad[14] = 2                                    # x_kind
+    bad[15] = 2                                    # x_kind
     assert lib.uq_quicfl_compress_f32(*bad) == -1
     assert lib.uq_quicfl_compress_f32(*args) == -1  # null pointers
     empty = list(args)

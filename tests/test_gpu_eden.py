@@ -230,3 +230,30 @@ def test_scale_dot_segmented_and_one_wave_agree(uq, kind):
                 with np.errstate(all="ignore"):
                     exp = np.float32(np.float32(nrm * nrm) / C.torch_dot(c, rot))
                 assert same_f32(a[j], exp), (kind, D, nbits, j)
+
+
+def test_one_bit_batch_fused_norm_dot_and_its_redo(uq):
+    """1 bit, > 256 clients, D a multiple of 2048: the norm, the bins and the dot in one read
+    (eden_normdot1_kernel), with the exact KE4 rerun for the clients it flags -- a zero row
+    (0 / 0 quotients: NaN -> the last bin), rows whose tiny coordinates' quotients underflow to
+    0 (the lowest bin although positive), a row with a NaN -- against the oracle, bit for bit."""
+    from oracle import uq_oracle_c as C
+    rng = np.random.default_rng(77)
+    n, d = 300, 1 << 14
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    x[3] = 0.0
+    x[10, ::50] = np.float32(1e-44)
+    x[10, 7] = np.float32(3e38)
+    x[11] = (rng.standard_normal(d) * 1e-30).astype(np.float32)
+    x[12, 100] = np.nan
+    seeds = [int(s) for s in rng.integers(0, 100, n)]
+    msg = uq.eden_compress(torch.as_tensor(x).cuda(), 1, seeds=seeds)
+    bins, sc = msg.bins.cpu().numpy(), msg.scale.cpu().numpy()
+    for j in [0, 1, 3, 10, 11, 12, 150, 299]:
+        with np.errstate(all="ignore"):
+            eb, es, _, _ = E.eden_compress(x[j], 1, seeds[j])
+        assert np.array_equal(bins[j], eb), j
+        assert same_f32(sc[j], es), (j, sc[j], es)
+    out = uq.eden_quantize(torch.as_tensor(x).cuda(), 1, seeds=seeds).cpu().numpy()
+    for j in [0, 10, 299]:
+        assert G.bits_equal(out[j], E.eden_decompress(bins[j], sc[j], 1, seeds[j], d)), j

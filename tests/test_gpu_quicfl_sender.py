@@ -280,3 +280,32 @@ def test_fused_receiver_index_error_after_sender(fx, tmp_path):
         assert np.array_equal(state_words(), expect)
     finally:
         uqdme.set_tables_prefix(None)
+
+
+def test_packed_table_same_bits(fx, monkeypatch):
+    """The sender's 4-byte packed table ((X << 25) | ceil(p * 2^24): one gather per coordinate)
+    and the (X, p) pairs give the same messages and end states, in batches (one wave per
+    message) and few-message calls (team kernels); a table with a non-integer X is not packed."""
+    import uqdme
+    import uqdme_amd.quicfl as q
+    meta, z, rmeta, rz = fx
+    snd = senders(meta)["pub"]
+    rng = np.random.default_rng(21)
+    for n, dim, nbits in ((300, 4096, 1), (3, 1 << 16, 2), (2, 20000, 4)):
+        x = rng.standard_normal((n, dim)).astype(np.float32)
+        seeds = [int(s) for s in rng.integers(0, 100, n)]
+        pxs = [int(s) for s in rng.integers(0, 2 ** 31, n)]
+        res = []
+        for packed in (True, False):
+            monkeypatch.setattr(q, "_USE_PACKED", packed)
+            m = q.quicfl_compress(torch.from_numpy(x), nbits, seeds, [123] * n, sender=snd, px_seeds=pxs)
+            res.append(m)
+        assert snd.table_packed(nbits, torch.device("cuda", 0)) is not None
+        a, b = res
+        assert torch.equal(a.X, b.X) and torch.equal(a.exact_mask, b.exact_mask) and torch.equal(a.scale, b.scale)
+        assert torch.equal(a.exact_count, b.exact_count)
+    tX, tp = sender_tables(1)
+    tX = tX.copy()
+    tX[0, 0] = 0.5
+    odd = uqdme.QuicFLSender(tables={1: (tX, tp, DATA[1])})
+    assert odd.table_packed(1, torch.device("cuda", 0)) is None

@@ -47,11 +47,11 @@ SIGNATURES = {
     "uq_quicfl_prepare_f32": (ctypes.c_int, [_p, _i64, _i64, _p, _i32, _i32, _p, _p, _p, _p, _p, _p]),
     "uq_quicfl_receive_f32": (ctypes.c_int, [_p, _i32, _i64, _i64, _p, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p, _p, _p]),
     "uq_quicfl_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
-    # x, n, dim, signs, sign_row, table_xp, numel, h_len, delta, recv_table, recv_numel, prng_seeds,
+    # x, n, dim, signs, sign_row, table_xp, table_packed, numel, h_len, delta, recv_table, recv_numel, prng_seeds,
     # px_state, px_seeds, px_state_out, out, scale, info, ws, ws_bytes, stream
-    "uq_quicfl_quantize_f32": (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _i64, _i32, _f32, _p, _i32, _p, _p, _p, _p,
+    "uq_quicfl_quantize_f32": (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _p, _i64, _i32, _f32, _p, _i32, _p, _p, _p, _p,
                                               _p, _p, _p, _p, _sz, _p]),
-    "uq_quicfl_compress_f32": (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _i64, _i32, _f32, _p, _p, _p, _p, _p, _i32,
+    "uq_quicfl_compress_f32": (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _p, _i64, _i32, _f32, _p, _p, _p, _p, _p, _i32,
                                               _p, _p, _p, _p, _p, _p, _sz, _p]),
     "uq_xxh64": (ctypes.c_uint64, [ctypes.c_char_p, _sz, ctypes.c_uint64]),
     "uq_eden_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),

@@ -3708,8 +3708,8 @@ int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
 static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, hipStream_t st);
 
 int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
-                           const float* table_xp, int64_t table_numel, int32_t h_len, float delta,
-                           const int32_t* prng_seeds, const uint32_t* px_state, const int32_t* px_seeds,
+                           const float* table_xp, const uint32_t* table_packed, int64_t table_numel, int32_t h_len,
+                           float delta, const int32_t* prng_seeds, const uint32_t* px_state, const int32_t* px_seeds,
                            uint32_t* px_state_out, void* X, int32_t x_kind, uint8_t* exact_mask, float* exact_vals,
                            int32_t* exact_count, float* scale, int32_t* info, void* ws, size_t ws_bytes,
                            void* stream) {
@@ -3737,6 +3737,7 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.rot = rot;
     q.nrm = (const float*)(wsb + w.nrm_off);
     q.tab = (const float2*)table_xp;
+    q.tabp = table_packed;
     q.numel = table_numel;
     q.half = ((table_numel / h_len) - 1) * h_len / 2;                                        // AS:443
     q.h_len = h_len;
@@ -3784,8 +3785,8 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, hipStream_t st) {
 // receiver fused into its stage 2 (no second h stream, no message in HBM), then the receiver's
 // inverse RHT into out [n][dim].
 int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
-                           const float* table_xp, int64_t table_numel, int32_t h_len, float delta,
-                           const float* recv_table, int32_t recv_numel, const int32_t* prng_seeds,
+                           const float* table_xp, const uint32_t* table_packed, int64_t table_numel, int32_t h_len,
+                           float delta, const float* recv_table, int32_t recv_numel, const int32_t* prng_seeds,
                            const uint32_t* px_state, const int32_t* px_seeds, uint32_t* px_state_out, float* out,
                            float* scale, int32_t* info, void* ws, size_t ws_bytes, void* stream) {
     if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
@@ -3812,6 +3813,7 @@ int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.rot = rot;
     q.nrm = (const float*)(wsb + w.nrm_off);
     q.tab = (const float2*)table_xp;
+    q.tabp = table_packed;
     q.numel = table_numel;
     q.half = ((table_numel / h_len) - 1) * h_len / 2;                                        // AS:443
     q.h_len = h_len;

@@ -122,6 +122,7 @@ struct QflSendArgs {
     const float* rot;           // [n][D] rotated vectors (the RHT's output)
     const float* nrm;           // [n] torch.norm of each
     const float2* tab;          // [numel] (table_X, table_p) pairs
+    const uint32_t* tabp;       // or [numel] packed (X << 25) | ceil(p * 2^24): X in 0..127, p in [0, 1]
     int64_t numel;
     int64_t half;               // AS:443 half_table_size
     int32_t h_len;
@@ -169,6 +170,7 @@ struct QflCtx {
     int64_t qL, qG;             // block of the first pass-B word of round 0 (local, global)
     int rL, rG;                 // its slot
     __amdgpu_buffer_rsrc_t rr, rh, rm, rX, rt, rP;
+    bool packed;
     float sc, fh, fhalf, fnumel;
     DivPlan dp, dps;            // / delta (AS:480), / scale (the fused receiver, AS:532)
     int32_t rtab_n;
@@ -194,7 +196,8 @@ __device__ __forceinline__ QflCtx qfl_ctx(const QflSendArgs& a, int64_t j, int32
     c.rh = make_rsrc(a.hbuf + c.row, Du);
     c.rm = make_rsrc(a.mask + c.row, Du);
     c.rX = make_rsrc(XK == 0 ? (void*)((int64_t*)a.X + c.row) : (void*)((uint8_t*)a.X + c.row), XK == 0 ? Du * 8u : Du);
-    c.rt = make_rsrc(a.tab, (uint32_t)a.numel * 8u);
+    c.packed = a.tabp != nullptr;
+    c.rt = c.packed ? make_rsrc(a.tabp, (uint32_t)a.numel * 4u) : make_rsrc(a.tab, (uint32_t)a.numel * 8u);
     c.sc = (1.0f / a.nrm[j]) * a.sqrtD;                             // AS:466/470 (IEEE 1/x, then f32 mul)
     c.dp = div_plan_norm(a.delta);                                  // q = v / delta: reciprocal + Markstein (exact)
     c.dps = div_plan_norm(c.sc);
@@ -280,9 +283,16 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             const uint32_t i = i0 + 64u * k + lane;
             const bool active = (r.act >> k) & 1u;
             const bool ex = (r.ex >> k) & 1u;
-            const float tx = __uint_as_float(r.t[k][0]), tp = __uint_as_float(r.t[k][1]);
-            flags |= (active && !(tp >= 0.f && tp <= 1.f)) ? UQ_QFL_BAD_PX : 0;
-            const float bx = (u24(r.wg[k]) < tp) ? 1.f : 0.f;
+            float tx, bx;
+            if (c.packed) {          // bernoulli(p): low24(w) * 2^-24 < p  <=>  low24(w) < ceil(p * 2^24)
+                tx = (float)(r.t[k][0] >> 25);
+                bx = ((r.wg[k] & 0xFFFFFFu) < (r.t[k][0] & 0x1FFFFFFu)) ? 1.f : 0.f;
+            } else {
+                tx = __uint_as_float(r.t[k][0]);
+                const float tp = __uint_as_float(r.t[k][1]);
+                flags |= (active && !(tp >= 0.f && tp <= 1.f)) ? UQ_QFL_BAD_PX : 0;
+                bx = (u24(r.wg[k]) < tp) ? 1.f : 0.f;
+            }
             const float xf = tx + bx;                                // AS:489
             if (c.fused) {                                           // the receiver, AS:526-532
                 const bool ok = xf > -9.2e18f && xf < 9.2e18f;
@@ -369,9 +379,14 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             flags |= (active && !inr) ? UQ_QFL_BAD_INDEX : 0;
             int32_t idx = inr ? (int32_t)it : 0;
             idx = idx < 0 ? idx + c.numel : idx;                      // torch.take wraps negatives
-            const auto t = __builtin_amdgcn_raw_buffer_load_b64(c.rt, (uint32_t)idx * 8u, 0, 0);   // AS:486-487
-            cr.t[k][0] = t[0];
-            cr.t[k][1] = t[1];
+            if (c.packed) {                                           // AS:486-487, one 4-byte gather
+                cr.t[k][0] = __builtin_amdgcn_raw_buffer_load_b32(c.rt, (uint32_t)idx * 4u, 0, 0);
+                cr.t[k][1] = 0u;
+            } else {
+                const auto t = __builtin_amdgcn_raw_buffer_load_b64(c.rt, (uint32_t)idx * 8u, 0, 0);
+                cr.t[k][0] = t[0];
+                cr.t[k][1] = t[1];
+            }
             cr.v[k] = v;
             cr.ex |= (active && ex ? 1u : 0u) << k;
             cr.act |= (active ? 1u : 0u) << k;

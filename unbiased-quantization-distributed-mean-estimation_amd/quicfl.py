@@ -42,6 +42,7 @@ __all__ = ["QuicFLReceiver", "QuicFLSender", "QuicFLMessages", "QUICFL_quantize"
 STATE_WORDS = 626                  # UQ_QFL_STATE_WORDS: (left, next, 624 words)
 _FLAG_P, _FLAG_INDEX, _FLAG_PX, _FLAG_X, _FLAG_TIMEOUT, _FLAG_EXACT, _FLAG_RECV_INDEX = 1, 2, 4, 8, 16, 32, 64  # UQ_QFL_*
 _tables_prefix = None
+_USE_PACKED = os.environ.get("UQDME_QUICFL_PACKED", "1") == "1"     # the 4-byte table when it is valid
 _dropin_lock = threading.Lock()
 _dropin: dict = {}
 
@@ -50,7 +51,8 @@ def set_tables_prefix(prefix) -> None:
     """Directory (with trailing separator or not) holding the QUIC-FL tables the drop-in
     QUICFL_quantize loads, as the reference's `str(path) + '/tables/'` (AS:431, AS:509)."""
     global _tables_prefix
-    _tables_prefix = None if prefix is None else os.path.join(str(prefix), "")
+    _tables_prefix = None
+_USE_PACKED = os.environ.get("UQDME_QUICFL_PACKED", "1") == "1"     # the 4-byte table when it is valid if prefix is None else os.path.join(str(prefix), "")
 
 
 def default_tables_prefix() -> str:
@@ -138,6 +140,23 @@ class QuicFLSender:
         with open(prefix + "data.txt") as f:
             dd = ast.literal_eval(f.read())
         return tx, tp, dd
+
+    def table_packed(self, nbits: int, dev):
+        """The table as u32 (X << 25) | ceil(p * 2^24) on the device (one 4-byte gather per
+        coordinate), or None when some X is not an integer in 0..127 or some p is outside
+        [0, 1] (then the (X, p) pairs, whose kernel path also flags a bad p like AS:489)."""
+        key = ("packed", nbits, dev.index)
+        if key not in self._xp:
+            X = self.sender_table_X[nbits].reshape(-1).to(torch.float64)
+            p = self.sender_table_p[nbits].reshape(-1).to(torch.float64)
+            ok = bool(((X == torch.round(X)) & (X >= 0) & (X <= 127)).all() and ((p >= 0) & (p <= 1)).all())
+            t = None
+            if ok:          # p * 2^24 is exact (a power-of-two scale of an f32), its ceil <= 2^24
+                P = torch.ceil(p * float(1 << 24)).to(torch.int64)
+                t = ((X.to(torch.int64) << 25) | P).to(torch.int64)
+                t = torch.where(t >= (1 << 31), t - (1 << 32), t).to(torch.int32).to(dev).contiguous()
+            self._xp[key] = t
+        return self._xp[key]
 
     def table_xp(self, nbits: int, dev) -> torch.Tensor:
         """(X, p) pairs [numel, 2] f32 on the device (one 8-byte gather per coordinate)."""
@@ -278,9 +297,10 @@ def quicfl_compress(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSende
     if n and d:
         tab, rows = _sign_rows(rs, D, dev)
         xp = sender.table_xp(nbits, dev)
+        tp = sender.table_packed(nbits, dev) if _USE_PACKED else None
         ws = _ws(n, d, dev)
         _lib.check(_lib.load().uq_quicfl_compress_f32(
-            _ptr(x), n, d, _ptr(tab), _ptr(rows), _ptr(xp), xp.shape[0], int(dd["h_len"]),
+            _ptr(x), n, d, _ptr(tab), _ptr(rows), _ptr(xp), _ptr(tp), xp.shape[0], int(dd["h_len"]),
             float(np.float32(dd["delta"])), _ptr(ps_d), _ptr(st_in), _ptr(pxs_d), _ptr(st_out),
             _ptr(X), 0 if x_dtype == torch.int64 else 1, _ptr(mask), _ptr(ev), _ptr(cnt_d), _ptr(scale), _ptr(info),
             _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_quicfl_compress_f32")
@@ -482,9 +502,10 @@ def quicfl_quantize(x, nbits: int, seeds, rotation_seeds, *, sender: QuicFLSende
     if n and d:
         tab, rows = _sign_rows(rs, D, dev)
         xp = sender.table_xp(nbits, dev)
+        tp = sender.table_packed(nbits, dev) if _USE_PACKED else None
         ws = _ws(n, d, dev)
         _lib.check(_lib.load().uq_quicfl_quantize_f32(
-            _ptr(x), n, d, _ptr(tab), _ptr(rows), _ptr(xp), xp.shape[0], int(dd["h_len"]),
+            _ptr(x), n, d, _ptr(tab), _ptr(rows), _ptr(xp), _ptr(tp), xp.shape[0], int(dd["h_len"]),
             float(np.float32(dd["delta"])), _ptr(rt), rt.numel(), _ptr(ps_d), _ptr(st_in), _ptr(pxs_d), _ptr(st_out),
             _ptr(out), _ptr(scale), _ptr(info), _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_quicfl_quantize_f32")
     if _host_out:                          # the result and the flags / states in one synchronisation
