@@ -48,3 +48,13 @@ def test_prefix_tables_keep_their_dtype(tmp_path):
     assert tp.dtype == torch.float64 and d2 == dd
     with pytest.raises(TypeError):
         uqdme.QuicFLSender(device="cpu", bits=[1], sr_bits=[6], prefix=str(tmp_path) + "/")
+
+
+def test_tables_prefix(monkeypatch):
+    q.set_tables_prefix("/some/dir")
+    try:
+        assert q.default_tables_prefix() == "/some/dir/"
+    finally:
+        q.set_tables_prefix(None)
+    monkeypatch.setenv("UQDME_QUICFL_TABLES", "/env/dir")
+    assert q.default_tables_prefix() == "/env/dir/"

@@ -51,8 +51,7 @@ def set_tables_prefix(prefix) -> None:
     """Directory (with trailing separator or not) holding the QUIC-FL tables the drop-in
     QUICFL_quantize loads, as the reference's `str(path) + '/tables/'` (AS:431, AS:509)."""
     global _tables_prefix
-    _tables_prefix = None
-_USE_PACKED = os.environ.get("UQDME_QUICFL_PACKED", "1") == "1"     # the 4-byte table when it is valid if prefix is None else os.path.join(str(prefix), "")
+    _tables_prefix = None if prefix is None else os.path.join(str(prefix), "")
 
 
 def default_tables_prefix() -> str:
