@@ -1,0 +1,34 @@
+"""The NMSE harness's draw-ahead thread gives the drivers' legacy np.random stream (ND:88-91)."""
+import numpy as np
+
+import uqdme  # noqa: F401  (registers the uqdme_amd package)
+
+
+def test_draw_ahead_matches_inline_draws():
+    from uqdme_amd.dme import _draw_ahead, draw_vectors
+    users, inst, dim = (1, 3, 2), 2, 257
+    for dist in ("normal", "laplace", "bernoulli"):
+        rs = np.random.RandomState(42)
+        want = []
+        for n in users:
+            for _ in range(inst):
+                vecs, vns = draw_vectors(dist, n, dim, rs)
+                want.append((np.stack([v.astype(np.float32) for v in vecs]), vns))
+        got = list(_draw_ahead(dist, users, inst, dim, np.random.RandomState(42)))
+        assert len(got) == len(want)
+        for (gb, gv), (wb, wv) in zip(got, want):
+            assert gb.dtype == np.float32 and np.array_equal(gb, wb) and gv == wv
+
+
+def test_draw_ahead_stops_early_and_raises():
+    from uqdme_amd.dme import _draw_ahead
+    it = _draw_ahead("normal", (1, 2), 3, 16, np.random.RandomState(0))
+    next(it)
+    it.close()                                    # the thread is told to stop
+    bad = _draw_ahead("no-such", (1,), 1, 16, np.random.RandomState(0))
+    try:
+        next(bad)
+    except KeyError:
+        pass
+    else:
+        raise AssertionError("expected KeyError")

@@ -64,6 +64,50 @@ def draw_vectors(dist: str, n: int, dim: int, rs=np.random):
     return vecs, float(sum(norms))
 
 
+def _draw_ahead(dist: str, users, num_instances: int, dim: int, rs):
+    """The instances' batches in the drivers' order, drawn one instance ahead on a thread:
+    yields (f32 batch [n, dim] as numpy, sum ||v||^2).  The legacy generator is sequential and
+    used by this thread alone, so the stream is the same as drawing inline; numpy's legacy
+    samplers and the f64 -> f32 casts release the GIL, so at large d (config C4, 2^22) the draws
+    overlap the quantization instead of adding to it."""
+    import queue
+    import threading
+
+    q: queue.Queue = queue.Queue(maxsize=1)
+    stop = threading.Event()
+
+    def work():
+        try:
+            for n in users:
+                for _ in range(num_instances):
+                    vecs, vns = draw_vectors(dist, n, dim, rs)
+                    batch = np.empty((n, dim), np.float32)
+                    for i, v in enumerate(vecs):
+                        batch[i] = v                                          # ND:91 f64 -> f32
+                    del vecs
+                    while not stop.is_set():
+                        try:
+                            q.put((batch, vns), timeout=0.5)
+                            break
+                        except queue.Full:
+                            pass
+                    if stop.is_set():
+                        return
+        except BaseException as e:                                            # re-raised by the consumer
+            q.put(e)
+
+    t = threading.Thread(target=work, daemon=True)
+    t.start()
+    try:
+        for _ in range(len(users) * num_instances):
+            item = q.get()
+            if isinstance(item, BaseException):
+                raise item
+            yield item
+    finally:
+        stop.set()
+
+
 def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_instances: int = 50,
                     num_trials: int = 50, rates=(1, 2), seed: int = 42, torch_threads: int = 1,
                     device=None, schemes=("unbiased",), progress=None, eden_scales=None, eden_scales_out=None,
@@ -91,10 +135,11 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
     gen = torch.Generator().manual_seed(seed)        # == torch.manual_seed(seed) CPU stream
     keys = [(sc, r) for sc in order for r in rates]
     script = {k: np.zeros((len(users), num_instances), np.float64) for k in keys}
+    batches = _draw_ahead(dist, users, num_instances, dim, rs)
     for ui, n in enumerate(users):
         for inst in range(num_instances):
-            vecs, vns = draw_vectors(dist, n, dim, rs)
-            xs = torch.stack([torch.as_tensor(v, dtype=torch.float32) for v in vecs])     # ND:91
+            batch, vns = next(batches)
+            xs = torch.from_numpy(batch)                                                   # ND:91
             emp = xs.sum(dim=0) / n                                                        # ND:95 (CPU)
             draws = {k: [] for k in keys}
             for _ in range(n):                        # ND:133-140: client-major, scheme/rate-minor
