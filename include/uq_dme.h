@@ -48,10 +48,17 @@ const char* uq_build_id(void);
 int uq_test_force_replay_failure(int on);
 /* Test hooks of the QUIC-FL kernels, process-wide (never set by the library): bit 0 makes the
  * runs of the few-message team kernels (sender KQ1t, receiver KQ2t) skip their waits and report
- * UQ_QFL_TIMEOUT, so the callers' timeout handling can be tested; bit 1 sends every call to the
- * one-wave-per-message kernels (KQ1 / KQ2), so both forms can be compared on the same message.
- * Returns the previous flags. */
+ * UQ_QFL_TIMEOUT, so the callers' timeout handling can be tested (the sender then takes KQ1t);
+ * bit 1 sends every call to the one-wave-per-message kernels (KQ1 / KQ2); bit 2 sends the
+ * sender's few-message calls to the team kernel KQ1t instead of the jump path (KQ0j + KQ1j), so
+ * the forms can be compared on the same message.  Returns the previous flags. */
 int uq_test_set_quicfl_hooks(int flags);
+/* Host-only, for tests and tools: the MT19937 state (ATen's 624-word array, block-aligned) that
+ * `blocks` twists ahead of state624, computed the way the QUIC-FL sender's jump path does it
+ * (t^(624 (blocks - 1)) mod phi, phi from Berlekamp-Massey; the correlation with the stream's
+ * first 19937 + 623 words; one twist) -- see uq_mt_poly.cpp.  Replaces nothing in the
+ * reference: its generators (All_Schemes.py:457, 465, 484, 489) are walked word by word. */
+int uq_mt_jump_host(const uint32_t* state624, int64_t blocks, uint32_t* out624);
 
 /* Thread-local description of the last error returned on this thread. */
 const char* uq_last_error(void);

@@ -1,8 +1,8 @@
 """GPU: QUIC-FL at config C4's size, D = 2^22 (AS:429-535, AS:814-832), bit for bit against the
 reference's own sender, receiver and drop-in run on the synthetic sender tables
 (tests/golden/make_golden_quicfl_c4.py): dim = 2^22 and 2^22 - 5 (padded), 1 and 2 bits,
-through the few-message team kernels (KQ1t / KQ2t) and, by the test hook, the one-wave
-kernels (KQ1 / KQ2) -- X, mask, exact values, scale, the global generator's end state and the
+through the few-message paths (the sender's jump path KQ0j + KQ1j, the receiver's team kernel
+KQ2t) and, by the test hooks, the one-wave kernels (KQ1 / KQ2) and the sender's team kernel KQ1t -- X, mask, exact values, scale, the global generator's end state and the
 receiver's output; QUICFL_quantize at 2^22 through the fused receiver."""
 import hashlib
 import json
@@ -42,7 +42,7 @@ def state_words():
     return q.generator_words(torch.default_generator)[1]
 
 
-@pytest.mark.parametrize("hooks", [0, 2])
+@pytest.mark.parametrize("hooks", [0, 2, 4])
 def test_sender_receiver_2pow22_vs_reference(fx, hooks):
     import uqdme
     from uqdme_amd._lib import load

@@ -196,9 +196,9 @@ def test_batch_states_and_many_messages(fx):
         states[j] = q.generator_words(g)[1]
     msg, new = q.quicfl_compress(torch.from_numpy(x), nbits, seeds, [123] * n, sender=snd, px_states=states,
                                  _state_out=True)
-    # the first 20 messages again as a few-message call (one workgroup per message: scout
-    # waves hand each run its generator blocks): the same bits and end states as the batch's
-    # one-wave-per-message kernel
+    # the first 20 messages again as a few-message call (the jump path: every run's generator
+    # blocks by jump-ahead, KQ0j): the same bits and end states as the batch's one-wave-per-
+    # message kernel
     few, fnew = q.quicfl_compress(torch.from_numpy(x[:20]), nbits, seeds[:20], [123] * 20, sender=snd,
                                   px_states=states[:20], _state_out=True)
     assert torch.equal(few.X, msg.X[:20]) and torch.equal(few.exact_mask, msg.exact_mask[:20])
@@ -207,6 +207,18 @@ def test_batch_states_and_many_messages(fx):
         cnt = int(few.exact_count[j])
         assert torch.equal(few.exact_vals[j, :cnt], msg.exact_vals[j, :cnt]), j
     assert np.array_equal(fnew, new[:20])
+    # and through the team kernel (scouts + runs, test hook 4): the same again
+    from uqdme_amd._lib import load
+    prev = load().uq_test_set_quicfl_hooks(4)
+    try:
+        team, tnew = q.quicfl_compress(torch.from_numpy(x[:20]), nbits, seeds[:20], [123] * 20, sender=snd,
+                                       px_states=states[:20], _state_out=True)
+    finally:
+        load().uq_test_set_quicfl_hooks(prev)
+    assert torch.equal(team.X, few.X) and torch.equal(team.exact_count, few.exact_count) and np.array_equal(tnew, fnew)
+    for j in range(20):
+        cnt = int(few.exact_count[j])
+        assert torch.equal(team.exact_vals[j, :cnt], few.exact_vals[j, :cnt]), j
     tX, tp = sender_tables(nbits)
     for j in list(range(0, n, 37)) + [n - 1]:
         st = (int(states[j, 0]), int(states[j, 1]), states[j, 2:])
@@ -216,11 +228,12 @@ def test_batch_states_and_many_messages(fx):
         assert (new[j, 0], new[j, 1]) == (gst[0], gst[1]) and np.array_equal(new[j, 2:], gst[2]), j
 
 
-@pytest.mark.parametrize("hooks", [0, 2])
+@pytest.mark.parametrize("hooks", [0, 2, 4])
 def test_fused_quantize_equals_compress_then_decompress(fx, hooks):
     """quicfl_quantize (uq_quicfl_quantize_f32: the receiver fused into the sender's stage 2 with
     the sender's own h, AS:526-532) gives the bits of compress -> decompress and the same end
-    generator states, through the team kernels (hooks 0) and the one-wave kernels (hooks 2)."""
+    generator states, through the jump path (hooks 0: KQ0j + KQ1j), the one-wave kernels
+    (hooks 2) and the team kernels (hooks 4)."""
     import uqdme
     import uqdme_amd.quicfl as q
     from uqdme_amd._lib import load

@@ -14,6 +14,8 @@ import sys
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(PKG_DIR, "csrc", "uq_dme.hip")
+# host-only C++ (the MT19937 jump polynomials): g++, linked into the same library
+HOST_SRC = os.path.join(PKG_DIR, "csrc", "uq_mt_poly.cpp")
 OUT_DIR = os.path.join(PKG_DIR, "_build")
 SO = os.path.join(OUT_DIR, "libuq_dme.so")
 
@@ -26,6 +28,9 @@ HIPCC_FLAGS = [
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-fno-gpu-flush-denormals-to-zero", "-Wall",
 ]
+
+
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall"]
 
 
 def hipcc() -> str:
@@ -50,7 +55,7 @@ def build_id() -> str:
         h.update((os.path.basename(path) + "\0").encode())
         with open(path, "rb") as fh:
             h.update(fh.read())
-    h.update("\0".join(HIPCC_FLAGS).encode())
+    h.update("\0".join(HIPCC_FLAGS + HOST_FLAGS).encode())
     return h.hexdigest()
 
 
@@ -67,10 +72,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OUT_DIR, exist_ok=True)
     bid = build_id()
     tmp = SO + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, f'-DUQ_BUILD_ID="{bid}"', "-o", tmp, SRC]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    obj = os.path.join(OUT_DIR, "uq_mt_poly.o")
+    cmds = [[os.environ.get("CXX", "g++"), *HOST_FLAGS, "-c", "-o", obj, HOST_SRC],
+            [hipcc(), *HIPCC_FLAGS, f'-DUQ_BUILD_ID="{bid}"', "-o", tmp, SRC, "-x", "none", obj]]
+    for cmd in cmds:
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
     os.replace(tmp, SO)
     with open(ID_FILE, "w") as f:
         f.write(bid + "\n")

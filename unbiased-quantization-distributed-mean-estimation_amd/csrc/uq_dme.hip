@@ -22,7 +22,11 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <tuple>
+#include <vector>
 
 #include "../../include/uq_dme.h"
 
@@ -2780,7 +2784,7 @@ int uq_test_force_replay_failure(int on) { return g_force_replay_failure.exchang
 // of the few-message team kernels skip its waits and report UQ_QFL_TIMEOUT; bit 1 sends every
 // call to the one-wave-per-message kernels (so a test can compare both forms on one message)
 std::atomic<int> g_quicfl_hooks{0};
-int uq_test_set_quicfl_hooks(int flags) { return g_quicfl_hooks.exchange(flags & 3); }
+int uq_test_set_quicfl_hooks(int flags) { return g_quicfl_hooks.exchange(flags & 7); }
 
 const char* uq_last_error(void) { return g_err.c_str(); }
 
@@ -3693,19 +3697,94 @@ int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbit
 }
 
 // ---- QUIC-FL sender ----------------------------------------------------------------------
-// Workspace: the EDEN layout (rotated vectors, norms, segmented-norm region) + h [n][D] u8.
+// The jump path (KQ0s + KQ0j + KQ1j + KQ1f, uq_quicfl_kernels.h) for few messages: R runs of L
+// rounds per message, R from a cost model of the phases (measured round-5 constants): the
+// streams (~20 us), the jumps (~tJ of the whole GPU per jump) and a round of passes A + B on one
+// wave (~tR; a run wave per SIMD).  The one-wave kernel when the model gives the jumps no gain.
+struct QflJumpPlan {
+    bool use = false;
+    int32_t R = 0;
+    int64_t L = 0, qL = 0;
+};
+static QflJumpPlan qfl_jump_plan(int64_t n, int64_t D) {
+    QflJumpPlan p;
+    const int64_t nch = (D + kMtN - 1) / kMtN;
+    if (n < 1 || n > kQfTeamMaxN || nch < 8 || D > ((int64_t)1 << 28)) return p;
+    const double tS = 20.0, tJ = 0.12, tR = 7.5;
+    double best = 1e300;
+    for (int64_t R = 1; R <= 1024 && R <= nch; ++R) {
+        const int64_t L = (nch + R - 1) / R, Ru = (nch + L - 1) / L;
+        if (Ru != R || n * R > 1024) continue;
+        const double t = tS + (double)(n * (3 * R - 2)) * tJ + (double)L * tR;
+        if (t < best) {
+            best = t;
+            p.R = (int32_t)R;
+            p.L = L;
+        }
+    }
+    p.use = best < 0.8 * (double)((n + 1023) / 1024) * (double)nch * tR;
+    p.qL = ((int64_t)kMtN + D) / kMtN;               // block of the first pass-B local word (qfl_ctx)
+    return p;
+}
+
+extern "C" int uq_mtpoly_progression(int64_t b0, int64_t step, int32_t count, uint32_t* out);   // uq_mt_poly.cpp
+
+// t^(624 b) mod phi for the plan's run starts, on the device, cached per (device, qL, L, R):
+// rows [0, R) = polyA (row r: b = r L - 1; row 0 unused), rows [R, 2R) = polyB (b = qL + r L - 1)
+static int qfl_jump_polys(const QflJumpPlan& p, const uint32_t** out) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int64_t, int64_t, int32_t>, uint32_t*> cache;
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_tuple(dev, p.qL, p.L, p.R);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+        *out = it->second;
+        return UQ_OK;
+    }
+    std::vector<uint32_t> h((size_t)2 * p.R * kMtN, 0u);
+    if ((p.R > 1 && uq_mtpoly_progression(p.L - 1, p.L, p.R - 1, h.data() + kMtN)) ||
+        uq_mtpoly_progression(p.qL - 1, p.L, p.R, h.data() + (size_t)p.R * kMtN))
+        return fail(UQ_E_INVALID, "MT19937 jump polynomials unavailable");
+    uint32_t* d = nullptr;
+    rc = hip_check(hipMalloc(&d, h.size() * sizeof(uint32_t)), "hipMalloc jump polynomials");
+    if (rc) return rc;
+    rc = hip_check(hipMemcpy(d, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "copy jump polynomials");
+    if (rc) {
+        (void)hipFree(d);
+        return rc;
+    }
+    cache.emplace(key, d);
+    *out = d;
+    return UQ_OK;
+}
+
+// Workspace: the EDEN layout (rotated vectors, norms, segmented-norm region) + h [n][D] u8 +
+// the jump path's blocks [n][R][3][624] u32 and run records [n][R][2] i32.
 static size_t quicfl_h_off(int64_t n, int64_t dim) {
     return (eden_layout(n, dim).total + 255) & ~(size_t)255;
+}
+static size_t quicfl_jump_off(int64_t n, int64_t dim) {
+    return (quicfl_h_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D + 255) & ~(size_t)255;
+}
+// jump region: streams [n][2][kMjX], parts [n][R][3][kMjParts][624], run records [n][R][2]
+static size_t quicfl_ws_total(int64_t n, int64_t dim) {
+    const QflJumpPlan p = qfl_jump_plan(n, eden_layout(n, dim).D);
+    const size_t jb =
+        p.use ? ((size_t)n * 2 * kMjX + (size_t)n * p.R * (3 * kMjParts * kMtN + 2)) * sizeof(uint32_t) : 0;
+    return quicfl_jump_off(n, dim) + jb;
 }
 
 int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
     if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
     if (n < 0 || dim < 0) return fail(UQ_E_INVALID, "n and dim must be >= 0");
-    *bytes_out = quicfl_h_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D;
+    *bytes_out = quicfl_ws_total(n, dim);
     return UQ_OK;
 }
 
-static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, hipStream_t st);
+static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, char* wsb, int64_t dim, hipStream_t st);
 
 int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
                            const float* table_xp, const uint32_t* table_packed, int64_t table_numel, int32_t h_len,
@@ -3726,7 +3805,7 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     if (!px_state && !px_seeds) return fail(UQ_E_INVALID, "px_state or px_seeds is required");
     const EdenLayout w = eden_layout(n, dim);
     const size_t hoff = quicfl_h_off(n, dim);
-    if (!ws || ws_bytes < hoff + (size_t)n * (size_t)w.D) return fail(UQ_E_WORKSPACE, "workspace too small");
+    if (!ws || ws_bytes < quicfl_ws_total(n, dim)) return fail(UQ_E_WORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     FwhtArgs a;
@@ -3757,16 +3836,60 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.info = info;
     q.D = w.D;
     q.n = n;
-    return launch_quicfl_send(q, x_kind, st);
+    return launch_quicfl_send(q, x_kind, wsb, dim, st);
 }
 
-// KQ1 / KQ1t by batch size: few messages a workgroup each (scouts + runs: the streams' length
-// is the critical path, not the per-coordinate work); batches a wave per message
-static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, hipStream_t st) {
+// By batch size: few messages take the jump path (KQ0j + KQ1j + KQ1f: every run of every
+// message at once from jumped stream blocks); batches a wave per message (KQ1).  Test hooks:
+// bit 1 the one-wave kernel, bit 2 (or bit 0, whose timeouts only its runs can report) the team
+// kernel KQ1t (scouts + runs in one workgroup per message).
+static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, char* wsb, int64_t dim, hipStream_t st) {
     const int hooks = g_quicfl_hooks.load();
     q.force_timeout = hooks & 1;
     const int64_t n = q.n;
-    if (!(hooks & 2) && n <= kQfTeamMaxN && q.D >= (int64_t)kMtN * kQfRuns && q.D <= kQfTeamMaxD) {
+    const QflJumpPlan jp = qfl_jump_plan(n, q.D);
+    if (!(hooks & 7) && jp.use) {
+        const uint32_t* polys = nullptr;
+        int rc = qfl_jump_polys(jp, &polys);
+        if (rc) return rc;
+        uint32_t* xs = (uint32_t*)(wsb + quicfl_jump_off(n, dim));
+        uint32_t* parts = xs + (size_t)n * 2 * kMjX;
+        QflJumpArgs ja{};
+        ja.prng_seeds = q.prng_seeds;
+        ja.px_state = q.px_state;
+        ja.px_seeds = q.px_seeds;
+        ja.polyA = polys;
+        ja.polyB = polys + (size_t)jp.R * kMtN;
+        ja.xs = xs;
+        ja.parts = parts;
+        ja.R = jp.R;
+        ja.n = n;
+        hipLaunchKernelGGL(quicfl_stream_kernel, dim3((unsigned)((2 * n + 3) / 4)), dim3(256), 0, st, ja);
+        rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch");
+        if (rc) return rc;
+        hipLaunchKernelGGL(quicfl_jump_kernel, dim3((unsigned)(n * jp.R * 3 * kMjParts)), dim3(256), 0, st, ja);
+        rc = hip_check(hipGetLastError(), "quicfl_jump_kernel launch");
+        if (rc) return rc;
+        QflRunArgs ra{};
+        ra.parts = parts;
+        ra.runinfo = (int32_t*)(parts + (size_t)n * jp.R * 3 * kMjParts * kMtN);
+        ra.R = jp.R;
+        ra.L = jp.L;
+        const dim3 rgrid((unsigned)((n * jp.R + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk(64 * kQfWavesPerWG);
+        if (!q.pre) {
+            hipLaunchKernelGGL(quicfl_send_count_kernel, rgrid, blk, 0, st, q, ra);
+            rc = hip_check(hipGetLastError(), "quicfl_send_count_kernel launch");
+            if (rc) return rc;
+        }
+        if (x_kind == 0) hipLaunchKernelGGL(quicfl_send_runs_kernel<0>, rgrid, blk, 0, st, q, ra);
+        else hipLaunchKernelGGL(quicfl_send_runs_kernel<1>, rgrid, blk, 0, st, q, ra);
+        rc = hip_check(hipGetLastError(), "quicfl_send_runs_kernel launch");
+        if (rc) return rc;
+        hipLaunchKernelGGL(quicfl_send_fin_kernel, dim3((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk, 0, st,
+                           q, ra);
+        return hip_check(hipGetLastError(), "quicfl_send_fin_kernel launch");
+    }
+    if (!(hooks & 2) && (hooks & 5) && n <= kQfTeamMaxN && q.D >= (int64_t)kMtN * kQfRuns && q.D <= kQfTeamMaxD) {
         if (x_kind == 0)
             hipLaunchKernelGGL(quicfl_send_team_kernel<0>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
         else
@@ -3802,7 +3925,7 @@ int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     if (!px_state && !px_seeds) return fail(UQ_E_INVALID, "px_state or px_seeds is required");
     const EdenLayout w = eden_layout(n, dim);
     const size_t hoff = quicfl_h_off(n, dim);
-    if (!ws || ws_bytes < hoff + (size_t)n * (size_t)w.D) return fail(UQ_E_WORKSPACE, "workspace too small");
+    if (!ws || ws_bytes < quicfl_ws_total(n, dim)) return fail(UQ_E_WORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     FwhtArgs a;
@@ -3831,7 +3954,7 @@ int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.rtab = recv_table;
     q.rtab_n = recv_numel;
     q.pre = rot;                       // in place: a coordinate's rot is loaded a round before its value is stored
-    rc = launch_quicfl_send(q, 0, st);                                                        // AS:455-503, 526-532
+    rc = launch_quicfl_send(q, 0, wsb, dim, st);                                                        // AS:455-503, 526-532
     if (rc) return rc;
     // AS:533-535: the receiver's inverse RHT (H, then * diag), [:dim]
     const int p = ilog2_pow2(w.D);

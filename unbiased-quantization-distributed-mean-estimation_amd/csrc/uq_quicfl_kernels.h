@@ -640,6 +640,326 @@ quicfl_send_team_kernel(QflSendArgs a) {
     }
 }
 
+// ---- jump path: the three streams' run starts by MT19937 jump-ahead (KQ0j), then every run
+// at once (KQ1j) ------------------------------------------------------------------------------
+// The team kernel's critical path is its scouts walking the streams (2D/624 twists of the local
+// stream: ~13 ms at 2^22).  Instead, each run's starting blocks are computed directly: the
+// state 624 b words ahead is the correlation window_J = XOR_{k : g_k = 1} x[k .. k + 623] of
+// g = t^(624 (b - 1)) mod phi (uq_mt_poly.cpp) with the stream's first 19937 + 623 words, then
+// one twist (the window's word 0 carries only its top bit).  Runs of L rounds then start
+// together, R of them per message, each with the passes of KQ1 (pass A for its h, pass B for its
+// coordinates), so a message takes ~(jump + L rounds) instead of ~2D/624 twists.
+//   KQ0s quicfl_stream_kernel   one wave per (message, stream): the base block and 32 twists,
+//        x[0 .. 33 * 624), to HBM (read by every jump of that stream from L2).
+//   KQ0j quicfl_jump_kernel   four 256-thread workgroups per (message, run, stream), each taking a
+//        quarter of the polynomial's 624 words (39 per wave) with the stream words they read
+//        staged in LDS (22 KB: several workgroups per CU); a wave XORs 4-word quads of x per set
+//        coefficient (one ds_read_b128 per quad, a scalar branch per coefficient nibble); the
+//        partial windows go to HBM, and the run XORs the four and twists once.
+//   KQ1c quicfl_send_count_kernel   (compress only) one wave per (message, run): its exact
+//        coordinates, so that the runs write their exact values straight into index order.
+//   KQ1j quicfl_send_runs_kernel   one wave per (message, run), four per workgroup: pass A over
+//        its rounds from the local block c0 (run 0: the seed), pass B from local block qL + c0
+//        and global block c0 (run 0: the generator's own state); flags per run.
+//   KQ1f quicfl_send_fin_kernel   one wave per message: flags ORed, ecount, scale.
+constexpr int kMjBlocks = 33;                 // x[0 .. 33 * 624) covers k + w <= 19936 + 623 (+ quad tails)
+constexpr int kMjX = kMjBlocks * kMtN;        // stream words kept per (message, stream)
+constexpr int kMjParts = 4;                   // workgroups per jump, 156 coefficient words each
+constexpr int kMjSlice = 39;                  // coefficient words per wave (4 waves x 4 parts x 39 = 624)
+constexpr int kMjPartWords = 4 * kMjSlice * 32 + 632;   // LDS words of a part: its coefficients + the window
+
+struct QflJumpArgs {
+    const int32_t* prng_seeds;  // local streams: init_genrand(prng_seeds[j])
+    const uint32_t* px_state;   // global streams: ATen state (left, next, words) per message, or null
+    const int32_t* px_seeds;    //   or fresh generators
+    const uint32_t* polyA;      // [R][624]: row r = t^(624 (r L - 1)) mod phi (row 0 unused)
+    const uint32_t* polyB;      // [R][624]: row r = t^(624 (qL + r L - 1)) mod phi
+    uint32_t* xs;               // [n][2][kMjX]: the local and the global stream's first words
+    uint32_t* parts;            // [n][R][3][kMjParts][624]: partial windows (local r L, local qL + r L, global r L)
+    int32_t R;
+    int64_t n;
+};
+
+// KQ0s: x[0 .. kMjX) of each message's two streams (base block, then 32 twists), one wave each
+__global__ void __launch_bounds__(256)
+quicfl_stream_kernel(QflJumpArgs a) {
+    __shared__ uint32_t scratch[4][kMtN];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t id = (int64_t)blockIdx.x * 4 + wv;
+    const int64_t j = id >> 1;
+    const int s = (int)(id & 1);                         // 0 local, 1 global
+    if (j >= a.n) return;
+    uint32_t st[kMtGroups];
+    if (s == 1 && a.px_state) {
+        mt_load(st, a.px_state + j * kQfStateWords + 2, lane);
+    } else {
+        if (lane == 0) mt_seed(scratch[wv], (uint32_t)(s == 1 ? a.px_seeds[j] : a.prng_seeds[j]));
+        wave_lds_fence();
+        mt_load(st, scratch[wv], lane);
+    }
+    uint32_t* x = a.xs + (j * 2 + s) * kMjX;
+    __builtin_amdgcn_s_setprio(3);
+    mt_store(st, x, lane);
+    for (int b = 1; b < kMjBlocks; ++b) {
+        mt_twist_reg(st, lane);
+        mt_store(st, x + b * kMtN, lane);
+    }
+}
+
+// acc[i] ^= XOR over the set bits t of NIB of E[t + i], E = (E0, E1): coefficient k0 + t applied
+// to the four window words w0 .. w0 + 3 (x[k0 + t + w0 + i]); two terms per v_bitop3 (XOR3)
+__device__ __forceinline__ uint32_t mj_xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+template <int NIB>
+__device__ __forceinline__ void mj_apply(uint32_t (&acc)[4], const uint4& E0, const uint4& E1) {
+    const uint32_t E[8] = {E0.x, E0.y, E0.z, E0.w, E1.x, E1.y, E1.z, E1.w};
+    constexpr int t0 = (NIB & 1) ? 0 : (NIB & 2) ? 1 : (NIB & 4) ? 2 : 3;           // lowest set bit
+    constexpr int R1 = NIB & (NIB - 1);                                              // the others
+    constexpr int t1 = (R1 & 1) ? 0 : (R1 & 2) ? 1 : (R1 & 4) ? 2 : 3;
+    constexpr int R2 = R1 & (R1 - 1);
+    constexpr int t2 = (R2 & 1) ? 0 : (R2 & 2) ? 1 : (R2 & 4) ? 2 : 3;
+    constexpr int R3 = R2 & (R2 - 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (R1 == 0) {
+            acc[i] ^= E[t0 + i];
+        } else {
+            acc[i] = mj_xor3(acc[i], E[t0 + i], E[t1 + i]);
+            if (R2 != 0 && R3 == 0) acc[i] ^= E[t2 + i];
+            if (R3 != 0) acc[i] = mj_xor3(acc[i], E[t2 + i], E[3 + i]);
+        }
+    }
+}
+template <int NIB>
+__device__ __forceinline__ void mj_apply3(uint32_t (&acc)[3][4], const uint4 (&E0)[3], const uint4 (&E1)[3]) {
+#pragma unroll
+    for (int g = 0; g < 3; ++g) mj_apply<NIB>(acc[g], E0[g], E1[g]);
+}
+__device__ __forceinline__ uint4 mj_quad(const uint32_t* p) {      // one ds_read_b128, never split
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const volatile u32x4v lds_q;
+    const u32x4v v = *(lds_q*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// KQ0j: one 256-thread workgroup per (message, run, stream, part); part p's wave v takes the
+// polynomial's words [156 p + 39 v, + 39) against window words 0..623 (lane quads: w0 = 256 g +
+// 4 lane, group 2 lanes < 28), the stream words it reads staged in LDS; the 4 waves' partial
+// windows are XORed and written out (the runs XOR the 4 parts and twist once).
+__global__ void __launch_bounds__(256)
+quicfl_jump_kernel(QflJumpArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t X[kMjPartWords];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t bid = blockIdx.x;
+    const int p = (int)(bid % kMjParts);
+    const int64_t job = bid / kMjParts;
+    const int s = (int)(job % 3);
+    const int64_t jr = job / 3;
+    const int r = (int)(jr % a.R);
+    const int64_t j = jr / a.R;
+    if (j >= a.n || (r == 0 && s != 1)) return;          // run 0's local-A and global blocks are the bases
+    const uint32_t* poly = (s == 1 ? a.polyB : a.polyA) + (size_t)r * kMtN;
+    const int wb0 = p * 4 * kMjSlice + wv * kMjSlice;
+    const uint32_t pv = lane < kMjSlice ? poly[wb0 + lane] : 0u;           // the wave's coefficient words
+    const int k_lo = p * 4 * kMjSlice * 32;
+    const uint32_t* x = a.xs + (j * 2 + (s == 2 ? 1 : 0)) * kMjX;
+    {                                                    // stage x[k_lo ..): every load in flight at once
+        constexpr int kQ = kMjPartWords / 4, kPer = (kQ + 255) / 256;
+        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+        u32x4v v[kPer];
+#pragma unroll
+        for (int t = 0; t < kPer; ++t) {
+            const int q = threadIdx.x + 256 * t;
+            v[t] = q < kQ && k_lo + 4 * q < kMjX ? *(const u32x4v*)(x + k_lo + 4 * q) : u32x4v{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int t = 0; t < kPer; ++t) {
+            const int q = threadIdx.x + 256 * t;
+            if (q < kQ) *(u32x4v*)(X + 4 * q) = v[t];
+        }
+    }
+    __syncthreads();
+    uint32_t acc[3][4];
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[g][i] = 0u;
+    int w0[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) w0[g] = g < 2 || lane < 28 ? 256 * g + 4 * lane : 0;
+    for (int wi = 0; wi < kMjSlice; ++wi) {
+        const uint32_t pw = (uint32_t)__builtin_amdgcn_readlane((int)pv, wi);
+        if (!pw) continue;
+        const int k0 = (wb0 + wi) * 32 - k_lo;
+        uint4 E0[3], E1[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) E0[g] = mj_quad(X + k0 + w0[g]);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+#pragma unroll
+            for (int g = 0; g < 3; ++g) E1[g] = mj_quad(X + k0 + 4 * m + 4 + w0[g]);
+            switch ((pw >> (4 * m)) & 15u) {
+                case 1: mj_apply3<1>(acc, E0, E1); break;
+                case 2: mj_apply3<2>(acc, E0, E1); break;
+                case 3: mj_apply3<3>(acc, E0, E1); break;
+                case 4: mj_apply3<4>(acc, E0, E1); break;
+                case 5: mj_apply3<5>(acc, E0, E1); break;
+                case 6: mj_apply3<6>(acc, E0, E1); break;
+                case 7: mj_apply3<7>(acc, E0, E1); break;
+                case 8: mj_apply3<8>(acc, E0, E1); break;
+                case 9: mj_apply3<9>(acc, E0, E1); break;
+                case 10: mj_apply3<10>(acc, E0, E1); break;
+                case 11: mj_apply3<11>(acc, E0, E1); break;
+                case 12: mj_apply3<12>(acc, E0, E1); break;
+                case 13: mj_apply3<13>(acc, E0, E1); break;
+                case 14: mj_apply3<14>(acc, E0, E1); break;
+                case 15: mj_apply3<15>(acc, E0, E1); break;
+                default: break;
+            }
+#pragma unroll
+            for (int g = 0; g < 3; ++g) E0[g] = E1[g];
+        }
+    }
+    __syncthreads();                                     // every wave is done with x
+    uint32_t* P = X + wv * 640;                          // partial windows, 640 words apart
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        const int w = 256 * g + 4 * lane;
+        if (w < kMtN) *(uint4*)(P + w) = make_uint4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+    }
+    __syncthreads();
+    uint32_t* out = a.parts + (((j * a.R + r) * 3 + s) * kMjParts + p) * kMtN;
+    for (int i = threadIdx.x; i < kMtN; i += 256) out[i] = X[i] ^ X[640 + i] ^ X[1280 + i] ^ X[1920 + i];
+}
+
+// A run's block from KQ0j's parts: the window (XOR of the parts), then one twist (block b - 1's
+// word 0 carries only its top bit; every word of block b is exact)
+__device__ __forceinline__ void mj_block(uint32_t (&st)[kMtGroups], const uint32_t* parts, int lane) {
+#pragma unroll
+    for (int g = 0; g < kMtGroups; ++g) {
+        const int i = 64 * g + lane;
+        const int ii = i < kMtN ? i : 0;
+        st[g] = parts[ii] ^ parts[kMtN + ii] ^ parts[2 * kMtN + ii] ^ parts[3 * kMtN + ii];
+    }
+    mt_twist_reg(st, lane);
+}
+
+struct QflRunArgs {
+    const uint32_t* parts;      // KQ0j's partial windows [n][R][3][kMjParts][624]
+    int32_t* runinfo;           // [n][R][2]: exact values of the run (KQ1c), its UQ_QFL_* flags (KQ1j)
+    int32_t R;
+    int64_t L;                  // rounds per run (the last run may have fewer)
+};
+
+// KQ1c (compress only): the exact coordinates of each run (AS:472-478: v = rot * scale, |v| > T
+// in f32, as pass B decides them), so that every run writes its exact values straight to their
+// index-order slots (after the earlier runs' counts).  One wave per (message, run).
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_send_count_kernel(QflSendArgs a, QflRunArgs ra) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t id = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    const int64_t j = id / ra.R;
+    const int r = (int)(id % ra.R);
+    if (j >= a.n) return;
+    const float sc = (1.0f / a.nrm[j]) * a.sqrtD;            // AS:466/470, as qfl_ctx
+    const float thr = kQflExactT;
+    const int64_t e0 = (int64_t)r * ra.L * kMtN, e1 = min(a.D, e0 + ra.L * kMtN);
+    const float* rot = a.rot + j * a.D;
+    int32_t cnt = 0;
+    for (int64_t i = e0 + lane; i < e1; i += 64) {
+        const float v = rot[i] * sc;
+        cnt += (v > thr) || (v < -thr) ? 1 : 0;
+    }
+    for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if (lane == 0) ra.runinfo[(j * ra.R + r) * 2] = cnt;
+}
+
+template <int XK>
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_send_runs_kernel(QflSendArgs a, QflRunArgs ra) {
+    __shared__ uint32_t WLsh[kQfWavesPerWG][2 * kMtN];
+    __shared__ uint32_t WGsh[kQfWavesPerWG][2 * kMtN];
+    __shared__ float rtab[kQflRecvTab];
+    if (a.pre) {
+        for (int i = threadIdx.x; i < a.rtab_n; i += 64 * kQfWavesPerWG) rtab[i] = a.rtab[i];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t id = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    const int64_t j = id / ra.R;
+    const int r = (int)(id % ra.R);
+    if (j >= a.n) return;                                // whole wave: no barrier below
+    const int64_t nch = (a.D + kMtN - 1) / kMtN;
+    const int64_t c0 = (int64_t)r * ra.L, c1 = min(nch, c0 + ra.L);
+    int32_t* info = ra.runinfo + (j * ra.R + r) * 2;
+    if (c0 >= c1) {
+        if (lane == 0) info[1] = 0;
+        return;
+    }
+    uint32_t* WL = WLsh[wv];
+    uint32_t* WG = WGsh[wv];
+    const uint32_t* st = ra.parts + (j * ra.R + r) * 3 * kMjParts * kMtN;
+    int32_t gleft = a.px_state ? (int32_t)a.px_state[j * kQfStateWords] : 1;
+    int32_t gnext = a.px_state ? (int32_t)a.px_state[j * kQfStateWords + 1] : 0;
+    const QflCtx c = qfl_ctx<XK>(a, j, gleft, gnext);
+    uint32_t sL[kMtGroups], sG[kMtGroups];
+    if (r == 0) {                                        // local block 0: the seed itself
+        if (lane == 0) mt_seed(WL, (uint32_t)a.prng_seeds[j]);
+        wave_lds_fence();
+        mt_load(sL, WL, lane);
+        wave_lds_fence();
+    } else {
+        mj_block(sL, st, lane);                          // local block c0
+    }
+    qfl_pass_a(c, sL, c0, c1, lane);                     // AS:465 h for the run's rounds
+    int64_t haveL = c.qL + c0, haveG = c0;
+    mj_block(sL, st + kMjParts * kMtN, lane);            // local block qL + c0
+    if (r == 0) {
+        qfl_gen_init(a, j, sG, WG, gleft, gnext, lane);  // the global generator's own block 0
+        wave_lds_fence();
+    } else {
+        mj_block(sG, st + 2 * kMjParts * kMtN, lane);    // global block c0
+    }
+    mt_store(sL, WL + (haveL & 1) * kMtN, lane);
+    mt_store(sG, WG + (haveG & 1) * kMtN, lane);
+    int64_t ebase = 0;                                   // the exact values of the earlier runs (KQ1c)
+    if (!c.fused) {
+        for (int q = lane; q < r; q += 64) ebase += ra.runinfo[(j * ra.R + q) * 2];
+        for (int o = 32; o >= 1; o >>= 1) ebase += __shfl_xor(ebase, o);
+    }
+    int32_t flags = 0;
+    qfl_pass_b<XK>(c, a.ev, sL, WL, haveL, sG, WG, haveG, c0, c1, ebase, flags, rtab, lane);
+    for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
+    if (c1 == nch && a.px_state_out)
+        qfl_state_out(a.px_state_out + j * kQfStateWords, sG, a.D, gleft, gnext, c.qG * kMtN + c.rG, lane);
+    if (lane == 0) info[1] = flags;
+}
+
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_send_fin_kernel(QflSendArgs a, QflRunArgs ra) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    if (j >= a.n) return;
+    const int32_t* info = ra.runinfo + j * ra.R * 2;
+    int32_t flags = 0;
+    int64_t tot = 0;
+    for (int r = lane; r < ra.R; r += 64) {
+        flags |= info[2 * r + 1];
+        if (!a.pre) tot += info[2 * r];
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        flags |= __shfl_xor(flags, o);
+        tot += __shfl_xor(tot, o);
+    }
+    if (lane == 0) {
+        if (a.ecount) a.ecount[j] = (int32_t)tot;
+        if (a.scale) a.scale[j] = (1.0f / a.nrm[j]) * a.sqrtD;      // AS:466/470, as qfl_ctx
+        a.info[j] = flags;
+    }
+}
+
 // ---- receiver: QuicFLReceiver.decompress before its inverse RHT (AS:526-532) -----------------
 // h = torch.randint(0, h_len, (D,)) of a generator seeded with prng_seed (word % h_len), then
 // v = recv_table.take(X * h_len + h) (AS:530: -numel <= index < numel, negatives wrap, anything
