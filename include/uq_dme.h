@@ -267,6 +267,15 @@ int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, c
                           int32_t table_rows, int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask,
                           const float* exact_vals, int32_t exact_layout, const int32_t* exact_count, const float* scale,
                           float* out, int32_t* info, void* stream);
+/* uq_quicfl_receive_ws_f32: uq_quicfl_receive_f32 with a device workspace of
+ * uq_quicfl_receive_workspace_bytes(n, D) bytes (0 means none is used; NULL is accepted then):
+ * with it, few-message calls start every run of the h stream at once from jumped generator
+ * blocks (MT19937 jump-ahead, uq_mt_poly.cpp) instead of walking the stream; same results. */
+int uq_quicfl_receive_workspace_bytes(int64_t n, int64_t D, size_t* bytes_out);
+int uq_quicfl_receive_ws_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, const float* recv_table,
+                             int32_t table_rows, int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask,
+                             const float* exact_vals, int32_t exact_layout, const int32_t* exact_count,
+                             const float* scale, float* out, int32_t* info, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- QUIC-FL sender (baseline) --------------------------------------
  * QuicFLSender.compress (NMSE_Results/Codes/All_Schemes.py:455-503) for a batch of n messages,
@@ -334,6 +343,20 @@ int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, i
                            void* stream);
 int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
                 const int32_t* sign_row, float* scale_out, void* ws, size_t ws_bytes, void* stream);
+/* The same three with the diagonal rows also as bits: sign_bits [rows][ceil(D / 32)] u32, bit
+ * i % 32 of word i / 32 set where signs[row][i] is -1 (uq_rht_sign_bits makes them from the
+ * int8 rows); the passes that apply the diagonal (the sender's first, the receiver's last) read
+ * 1/8 byte per coordinate instead of 1.  sign_bits NULL: the int8 rows, as above.  Same results. */
+int uq_rht_sign_bits(const int8_t* signs, int64_t rows, int64_t D, uint32_t* bits, void* stream);
+int uq_eden_compress_f32_sb(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
+                            const int32_t* sign_row, const uint32_t* sign_bits, uint8_t* bins, float* scale, void* ws,
+                            size_t ws_bytes, void* stream);
+int uq_eden_decompress_f32_sb(const uint8_t* bins, const float* scale, int64_t n, int64_t dim, int32_t nbits,
+                              const int8_t* signs, const int32_t* sign_row, const uint32_t* sign_bits, float* out,
+                              void* ws, size_t ws_bytes, void* stream);
+int uq_eden_f32_sb(const float* x, float* out, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
+                   const int32_t* sign_row, const uint32_t* sign_bits, float* scale_out, void* ws, size_t ws_bytes,
+                   void* stream);
 /* torch.norm(v[j], 2) of each row of v [n][D] f32 in torch's CPU order (AS:329: 8 lanes of
  * fma chains, lanes added in order, sqrt), the norm the EDEN entry points use:
  *   mode 1: the sequential chains (one chain per torch lane; what batches above 256 rows use)

@@ -257,3 +257,46 @@ def test_one_bit_batch_fused_norm_dot_and_its_redo(uq):
     out = uq.eden_quantize(torch.as_tensor(x).cuda(), 1, seeds=seeds).cpu().numpy()
     for j in [0, 10, 299]:
         assert G.bits_equal(out[j], E.eden_decompress(bins[j], sc[j], 1, seeds[j], d)), j
+
+
+@pytest.mark.parametrize("d", [5000, 1 << 20, (1 << 22) - 5])
+def test_sign_bits_equal_int8_rows(uq, d):
+    """The diagonal as bits (uq_rht_sign_bits; uq_eden_*_sb, what the Python layer calls) and
+    as int8 rows (uq_eden_f32 etc.) give the same bits: the sender's first pass (4096- and
+    16384-element low passes, padded rows) and the receiver's last pass, 1 and 2 bits, with a
+    NaN and infinities in the input."""
+    import ctypes
+    from uqdme_amd import eden as Ed
+    from uqdme_amd._lib import load, check
+    rng = np.random.default_rng(d % 1009)
+    n = 3
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    x[1, 7] = np.inf
+    x[2, 3] = np.nan
+    xt = torch.as_tensor(x).cuda()
+    D = Ed.padded_dim(d)
+    seeds = torch.tensor([0, 17, 99])
+    tab, rows = Ed._sign_rows(seeds, D, xt.device)
+    bits = Ed.rht_sign_bits(tab)
+    exp_bits = np.packbits((tab.cpu().numpy() < 0).astype(np.uint8), axis=1, bitorder="little")
+    assert np.array_equal(bits.cpu().numpy().view(np.uint8), exp_bits)
+    L = load()
+    b = ctypes.c_size_t()
+    check(L.uq_eden_workspace_bytes(n, d, ctypes.byref(b)), "ws")
+    ws = torch.empty(b.value, dtype=torch.uint8, device="cuda")
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    for nbits in (1, 2):
+        o8 = torch.empty((n, d), device="cuda")
+        ob = torch.empty((n, d), device="cuda")
+        s8 = torch.empty(n, device="cuda")
+        sb = torch.empty(n, device="cuda")
+        check(L.uq_eden_f32(p(xt), p(o8), n, d, nbits, p(tab), p(rows), p(s8), p(ws), b.value, None), "int8")
+        check(L.uq_eden_f32_sb(p(xt), p(ob), n, d, nbits, p(tab), p(rows), p(bits), p(sb), p(ws), b.value, None),
+              "bits")
+        torch.cuda.synchronize()
+        assert G.bits_equal(o8.cpu().numpy(), ob.cpu().numpy()), nbits
+        assert torch.equal(s8.view(torch.int32), sb.view(torch.int32)), nbits
+    # and the Python drop-in path (bits) against the oracle on one row
+    if d <= 1 << 20:
+        out = uq.eden_quantize(xt[:1], 1, seeds=[17]).cpu().numpy()[0]
+        assert G.bits_equal(out, E.eden_quantize(x[0], 1, 17))

@@ -141,6 +141,50 @@ def test_receiver_team_equals_wave(fx):
     assert few[3].cpu().numpy().view(np.uint32).tolist() == exp.view(np.uint32).tolist()
 
 
+@pytest.mark.parametrize("D", [1 << 16, 1 << 20])
+def test_receiver_jump_equals_team_and_wave(fx, D):
+    """A few messages of 2^16 / 2^20 coordinates take the receiver's jump path (KQ0s + KQ0j on
+    the h stream, every run at once, compact slots from KQ2c's counts): the same bits as the
+    team kernel (test hook 4) and the one-wave kernel (hook 2), both exact layouts, and the
+    oracle on one message."""
+    import uqdme
+    from uqdme_amd._lib import load
+    meta, z = fx
+    rng = np.random.default_rng(D % 977)
+    nbits, n = 1, 3
+    tab = z[f"recv{nbits}"]
+    X = rng.integers(0, tab.shape[0], size=(n, D))
+    mask = rng.random((n, D)) < 0.004
+    dense = np.where(mask, rng.standard_normal((n, D)), 0).astype(np.float32)
+    compact = np.zeros((n, D), np.float32)
+    cnt = mask.sum(1)
+    for j in range(n):
+        compact[j, :cnt[j]] = dense[j][mask[j]]
+    ps = rng.integers(0, 1 << 16, size=n)
+    rs = rng.integers(0, 100, size=n)
+    sc = (rng.random(n) * 3 + 0.5).astype(np.float32)
+    md = torch.from_numpy(mask).cuda()
+    Xd = torch.from_numpy(X).to(torch.uint8).cuda()
+    outs = {}
+    for hooks in (0, 2, 4):
+        prev = load().uq_test_set_quicfl_hooks(hooks)
+        try:
+            for vals, c in ((dense, None), (compact, cnt)):
+                outs[(hooks, c is None)] = uqdme.quicfl_decompress(Xd, nbits, ps, rs, sc, D, tab, None, md,
+                                                                   torch.from_numpy(vals).cuda(), c)
+        finally:
+            load().uq_test_set_quicfl_hooks(prev)
+    for k, v in outs.items():
+        assert torch.equal(v.view(torch.int32), outs[(0, True)].view(torch.int32)), k
+    exp = E.quicfl_decompress(X[1], tab, tab.shape[1], int(ps[1]), mask[1], dense[1][mask[1]], sc[1], int(rs[1]), D)
+    assert outs[(0, False)][1].cpu().numpy().view(np.uint32).tolist() == exp.view(np.uint32).tolist()
+    # a wrong exact count is still reported (the jump path's KQ2f)
+    bad = cnt.copy()
+    bad[2] += 1
+    with pytest.raises(RuntimeError, match="shape mismatch"):
+        uqdme.quicfl_decompress(Xd, nbits, ps, rs, sc, D, tab, None, md, torch.from_numpy(compact).cuda(), bad)
+
+
 def test_timeout_flag_raises_in_sender_and_receiver(fx):
     """A run of a team kernel whose wait ran out (UQ_QFL_TIMEOUT, forced through the test hook
     uq_test_set_quicfl_hooks) never writes its coordinates: the sender, the receiver and the

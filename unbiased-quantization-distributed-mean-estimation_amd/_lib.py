@@ -47,6 +47,9 @@ SIGNATURES = {
     "uq_rht_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _sz, _p]),
     "uq_quicfl_prepare_f32": (ctypes.c_int, [_p, _i64, _i64, _p, _i32, _i32, _p, _p, _p, _p, _p, _p]),
     "uq_quicfl_receive_f32": (ctypes.c_int, [_p, _i32, _i64, _i64, _p, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p, _p, _p]),
+    "uq_quicfl_receive_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
+    "uq_quicfl_receive_ws_f32": (ctypes.c_int, [_p, _i32, _i64, _i64, _p, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p, _p,
+                                                _p, _sz, _p]),
     "uq_quicfl_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
     # x, n, dim, signs, sign_row, table_xp, table_packed, numel, h_len, delta, recv_table, recv_numel, prng_seeds,
     # px_state, px_seeds, px_state_out, out, scale, info, ws, ws_bytes, stream
@@ -59,6 +62,10 @@ SIGNATURES = {
     "uq_eden_compress_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _sz, _p]),
     "uq_eden_decompress_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "uq_eden_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
+    "uq_rht_sign_bits": (ctypes.c_int, [_p, _i64, _i64, _p, _p]),
+    "uq_eden_compress_f32_sb": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "uq_eden_decompress_f32_sb": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _sz, _p]),
+    "uq_eden_f32_sb": (ctypes.c_int, [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _sz, _p]),
     "uq_eden_norm_workspace_bytes": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
     "uq_eden_norm_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _sz, _p]),
     "uq_tc_bound": (ctypes.c_int, [_i64, ctypes.POINTER(_sz)]),

@@ -3463,10 +3463,118 @@ int uq_rht_signs(const int32_t* seeds, int64_t rows, int64_t D, int8_t* signs, v
     return hip_check(hipGetLastError(), "rht_signs_kernel launch");
 }
 
+// The jump path (KQ0s + KQ0j + KQ1j + KQ1f, uq_quicfl_kernels.h) for few messages: R runs of L
+// rounds per message, R from a cost model of the phases (measured round-5 constants): the
+// streams (~20 us), the jumps (~tJ of the whole GPU per jump) and a round of passes A + B on one
+// wave (~tR; a run wave per SIMD).  The one-wave kernel when the model gives the jumps no gain.
+struct QflJumpPlan {
+    bool use = false;
+    int32_t R = 0;
+    int64_t L = 0, qL = 0;
+};
+// (Up to 128 messages: at 256 x 2^20 only R = 4 runs fit beside each other and the team kernel
+// measured 5.4 against 6.0 ms; 128 x 2^20: 3.4 against 4.5 ms, profiles/r5h_quicfl_batch_sizes.jsonl.)
+constexpr int64_t kQfJumpMaxN = 128;
+static QflJumpPlan qfl_jump_plan(int64_t n, int64_t D) {
+    QflJumpPlan p;
+    const int64_t nch = (D + kMtN - 1) / kMtN;
+    if (n < 1 || n > kQfJumpMaxN || nch < 8 || D > ((int64_t)1 << 28)) return p;
+    const double tS = 20.0, tJ = 0.12, tR = 7.5;
+    double best = 1e300;
+    for (int64_t R = 1; R <= 1024 && R <= nch; ++R) {
+        const int64_t L = (nch + R - 1) / R, Ru = (nch + L - 1) / L;
+        if (Ru != R || n * R > 1024) continue;
+        const double t = tS + (double)(n * (3 * R - 2)) * tJ + (double)L * tR;
+        if (t < best) {
+            best = t;
+            p.R = (int32_t)R;
+            p.L = L;
+        }
+    }
+    p.use = best < 0.8 * (double)((n + 1023) / 1024) * (double)nch * tR;
+    p.qL = ((int64_t)kMtN + D) / kMtN;               // block of the first pass-B local word (qfl_ctx)
+    return p;
+}
+
+// The receiver's jump path: one stream, one jump per run; a round (one wave: the h word, the
+// table gather, X, the mask and the exact value) ~tR.  Taken when it beats the team kernel
+// (~1 us per round of the h scout's twists and the runs behind it).
+static QflJumpPlan qfl_recv_jump_plan(int64_t n, int64_t D) {
+    QflJumpPlan p;
+    const int64_t nch = (D + kMtN - 1) / kMtN;
+    if (n < 1 || n > kQfTeamMaxN || nch < 8 || D > ((int64_t)1 << 28)) return p;
+    const double tS = 20.0, tJ = 0.12, tR = 3.0;
+    double best = 1e300;
+    for (int64_t R = 1; R <= 1024 && R <= nch; ++R) {
+        const int64_t L = (nch + R - 1) / R, Ru = (nch + L - 1) / L;
+        if (Ru != R || n * R > 1024) continue;
+        const double t = tS + (double)(n * (R - 1)) * tJ + (double)L * tR;
+        if (t < best) {
+            best = t;
+            p.R = (int32_t)R;
+            p.L = L;
+        }
+    }
+    p.use = best < 0.8 * (double)nch;
+    return p;
+}
+
+extern "C" int uq_mtpoly_progression(int64_t b0, int64_t step, int32_t count, uint32_t* out);   // uq_mt_poly.cpp
+
+// t^(624 b) mod phi for the plan's run starts, on the device, cached per (device, qL, L, R):
+// rows [0, R) = polyA (row r: b = r L - 1; row 0 unused), rows [R, 2R) = polyB (b = qL + r L - 1)
+static int qfl_jump_polys(const QflJumpPlan& p, bool a_only, const uint32_t** out) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int64_t, int64_t, int32_t>, uint32_t*> cache;
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_tuple(dev, a_only ? (int64_t)-1 : p.qL, p.L, p.R);   // (A rows only: no qL)
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+        *out = it->second;
+        return UQ_OK;
+    }
+    std::vector<uint32_t> h((size_t)2 * p.R * kMtN, 0u);
+    if ((p.R > 1 && uq_mtpoly_progression(p.L - 1, p.L, p.R - 1, h.data() + kMtN)) ||
+        (!a_only && uq_mtpoly_progression(p.qL - 1, p.L, p.R, h.data() + (size_t)p.R * kMtN)))
+        return fail(UQ_E_INVALID, "MT19937 jump polynomials unavailable");
+    uint32_t* d = nullptr;
+    rc = hip_check(hipMalloc(&d, h.size() * sizeof(uint32_t)), "hipMalloc jump polynomials");
+    if (rc) return rc;
+    rc = hip_check(hipMemcpy(d, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "copy jump polynomials");
+    if (rc) {
+        (void)hipFree(d);
+        return rc;
+    }
+    cache.emplace(key, d);
+    *out = d;
+    return UQ_OK;
+}
+
+static int quicfl_recv_jump(const QflRecvArgs& r, int32_t x_kind, const QflJumpPlan& jp, char* wsb, hipStream_t st);
+
 int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, const float* recv_table,
                           int32_t table_rows, int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask,
                           const float* exact_vals, int32_t exact_layout, const int32_t* exact_count, const float* scale,
                           float* out, int32_t* info, void* stream) {
+    return uq_quicfl_receive_ws_f32(X, x_kind, n, D, recv_table, table_rows, h_len, prng_seeds, exact_mask, exact_vals,
+                                    exact_layout, exact_count, scale, out, info, nullptr, 0, stream);
+}
+
+int uq_quicfl_receive_workspace_bytes(int64_t n, int64_t D, size_t* bytes_out) {
+    if (!bytes_out) return fail(UQ_E_INVALID, "null bytes_out");
+    if (n < 0 || D < 0) return fail(UQ_E_INVALID, "n and D must be >= 0");
+    const QflJumpPlan p = qfl_recv_jump_plan(n, D);
+    *bytes_out = p.use ? ((size_t)n * kMjX + (size_t)n * p.R * (kMjParts * kMtN + 2)) * sizeof(uint32_t) : 0;
+    return UQ_OK;
+}
+
+int uq_quicfl_receive_ws_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, const float* recv_table,
+                             int32_t table_rows, int32_t h_len, const int32_t* prng_seeds, const uint8_t* exact_mask,
+                             const float* exact_vals, int32_t exact_layout, const int32_t* exact_count,
+                             const float* scale, float* out, int32_t* info, void* ws, size_t ws_bytes, void* stream) {
     if (n < 0 || D < 0) return fail(UQ_E_INVALID, "n and D must be >= 0");
     if (n > 65535) return fail(UQ_E_INVALID, "at most 65535 clients per call");
     if (D > ((int64_t)1 << 28)) return fail(UQ_E_INVALID, "at most 2^28 coordinates per message");
@@ -3495,7 +3603,12 @@ int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, c
     r.info = info;
     const int hooks = g_quicfl_hooks.load();
     r.force_timeout = hooks & 1;
-    // few messages: a workgroup per message (the h stream's scout + 7 runs); batches: a wave each
+    // few messages: every run at once from jumped blocks of the h stream (given a workspace), or
+    // a workgroup per message (the h stream's scout + 7 runs); batches: a wave each
+    const QflJumpPlan jp = qfl_recv_jump_plan(n, D);
+    size_t need = 0;
+    (void)uq_quicfl_receive_workspace_bytes(n, D, &need);
+    if (!(hooks & 7) && jp.use && ws && ws_bytes >= need) return quicfl_recv_jump(r, x_kind, jp, (char*)ws, st);
     if (!(hooks & 2) && n <= kQfTeamMaxN && D >= (int64_t)kMtN * kQrRuns && D <= kQfTeamMaxD) {
         const dim3 grid((unsigned)n), block(64 * kQfTeamWaves);
         if (x_kind == 0) hipLaunchKernelGGL(quicfl_recv_team_kernel<0>, grid, block, 0, st, r);
@@ -3508,6 +3621,45 @@ int uq_quicfl_receive_f32(const void* X, int32_t x_kind, int64_t n, int64_t D, c
     else if (x_kind == 1) hipLaunchKernelGGL(quicfl_recv_wave_kernel<1>, grid, block, 0, st, r);
     else hipLaunchKernelGGL(quicfl_recv_wave_kernel<2>, grid, block, 0, st, r);
     return hip_check(hipGetLastError(), "quicfl_recv_wave_kernel launch");
+}
+
+// KQ0s + KQ0j (the h stream, one block per run) + KQ2c + KQ2j + KQ2f
+static int quicfl_recv_jump(const QflRecvArgs& r, int32_t x_kind, const QflJumpPlan& jp, char* wsb, hipStream_t st) {
+    const int64_t n = r.n;
+    const uint32_t* polys = nullptr;
+    int rc = qfl_jump_polys(jp, true, &polys);
+    if (rc) return rc;
+    uint32_t* xs = (uint32_t*)wsb;
+    uint32_t* parts = xs + (size_t)n * kMjX;
+    QflJumpArgs ja{};
+    ja.prng_seeds = r.prng_seeds;
+    ja.polyA = polys;
+    ja.polyB = polys;                                    // (unused: one kind)
+    ja.xs = xs;
+    ja.parts = parts;
+    ja.R = jp.R;
+    ja.n = n;
+    ja.nstreams = 1;
+    ja.kinds = 1;
+    hipLaunchKernelGGL(quicfl_stream_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, ja);
+    if ((rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch"))) return rc;
+    hipLaunchKernelGGL(quicfl_jump_kernel, dim3((unsigned)(n * jp.R * kMjParts)), dim3(256), 0, st, ja);
+    if ((rc = hip_check(hipGetLastError(), "quicfl_jump_kernel launch"))) return rc;
+    QflRunArgs ra{};
+    ra.parts = parts;
+    ra.runinfo = (int32_t*)(parts + (size_t)n * jp.R * kMjParts * kMtN);
+    ra.R = jp.R;
+    ra.L = jp.L;
+    const dim3 rgrid((unsigned)((n * jp.R + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk(64 * kQfWavesPerWG);
+    hipLaunchKernelGGL(quicfl_recv_count_kernel, rgrid, blk, 0, st, r, ra);
+    if ((rc = hip_check(hipGetLastError(), "quicfl_recv_count_kernel launch"))) return rc;
+    if (x_kind == 0) hipLaunchKernelGGL(quicfl_recv_runs_kernel<0>, rgrid, blk, 0, st, r, ra);
+    else if (x_kind == 1) hipLaunchKernelGGL(quicfl_recv_runs_kernel<1>, rgrid, blk, 0, st, r, ra);
+    else hipLaunchKernelGGL(quicfl_recv_runs_kernel<2>, rgrid, blk, 0, st, r, ra);
+    if ((rc = hip_check(hipGetLastError(), "quicfl_recv_runs_kernel launch"))) return rc;
+    hipLaunchKernelGGL(quicfl_recv_fin_kernel, dim3((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk, 0, st, r,
+                       ra);
+    return hip_check(hipGetLastError(), "quicfl_recv_fin_kernel launch");
 }
 
 int uq_quicfl_prepare_f32(const int32_t* X, int64_t n, int64_t D, const float* recv_table, int32_t table_rows,
@@ -3579,12 +3731,14 @@ int uq_eden_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
 // The sender up to the norms: RHT (AS:123-141) and torch.norm (AS:329); *rot = the rotated
 // vectors (one of the workspace's two vector buffers).
 int eden_front(const float* x, int64_t n, int64_t dim, const EdenTables& tab, const int8_t* signs,
-               const int32_t* sign_row, const EdenLayout& w, char* wsb, FwhtArgs& a, float** rot, hipStream_t st) {
+               const int32_t* sign_row, const EdenLayout& w, char* wsb, FwhtArgs& a, float** rot, hipStream_t st,
+               const uint32_t* sbits = nullptr) {
     float* nrm = (float*)(wsb + w.nrm_off);
     a = FwhtArgs{};
     a.in = x;
     a.signs = signs;
     a.sign_row = sign_row;
+    a.sbits = sbits;
     a.D = w.D;
     a.dim = dim;
     a.sqrtD = (float)std::sqrt((double)w.D);                 // np.sqrt(d) -> f32 operand
@@ -3622,6 +3776,22 @@ int uq_eden_norm_f32(const float* v, int64_t n, int64_t D, int32_t mode, float* 
 int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
                          const int32_t* sign_row, uint8_t* bins, float* scale, void* ws, size_t ws_bytes,
                          void* stream) {
+    return uq_eden_compress_f32_sb(x, n, dim, nbits, signs, sign_row, nullptr, bins, scale, ws, ws_bytes, stream);
+}
+
+int uq_rht_sign_bits(const int8_t* signs, int64_t rows, int64_t D, uint32_t* bits, void* stream) {
+    if (rows < 0 || D < 0) return fail(UQ_E_INVALID, "rows and D must be >= 0");
+    if (rows == 0 || D == 0) return UQ_OK;
+    if (!signs || !bits) return fail(UQ_E_INVALID, "null pointer");
+    const int64_t words = rows * ((D + 31) / 32);
+    hipLaunchKernelGGL(rht_sign_bits_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       signs, rows, D, bits);
+    return hip_check(hipGetLastError(), "rht_sign_bits_kernel launch");
+}
+
+int uq_eden_compress_f32_sb(const float* x, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
+                            const int32_t* sign_row, const uint32_t* sign_bits, uint8_t* bins, float* scale, void* ws,
+                            size_t ws_bytes, void* stream) {
     EdenTables tab;
     int rc = eden_check(n, dim, nbits, signs, &tab);
     if (rc) return rc;
@@ -3639,6 +3809,7 @@ int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, 
         a.in = x;
         a.signs = signs;
         a.sign_row = sign_row;
+        a.sbits = sign_bits;
         a.D = w.D;
         a.dim = dim;
         a.sqrtD = (float)std::sqrt((double)w.D);
@@ -3655,7 +3826,7 @@ int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, 
     }
     FwhtArgs a;
     float* vec = nullptr;
-    rc = eden_front(x, n, dim, tab, signs, sign_row, w, wsb, a, &vec, st);
+    rc = eden_front(x, n, dim, tab, signs, sign_row, w, wsb, a, &vec, st, sign_bits);
     if (rc) return rc;
     if (w.seg && n <= kDotSegMaxN)                                                   // AS:329-335
         return launch_eden_dotseg(vec, n, w.D, a.sqrtD, nrm, tab, bins, scale, wsb + w.seg_off, st);
@@ -3665,6 +3836,12 @@ int uq_eden_compress_f32(const float* x, int64_t n, int64_t dim, int32_t nbits, 
 int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, int64_t dim, int32_t nbits,
                            const int8_t* signs, const int32_t* sign_row, float* out, void* ws, size_t ws_bytes,
                            void* stream) {
+    return uq_eden_decompress_f32_sb(bins, scale, n, dim, nbits, signs, sign_row, nullptr, out, ws, ws_bytes, stream);
+}
+
+int uq_eden_decompress_f32_sb(const uint8_t* bins, const float* scale, int64_t n, int64_t dim, int32_t nbits,
+                              const int8_t* signs, const int32_t* sign_row, const uint32_t* sign_bits, float* out,
+                              void* ws, size_t ws_bytes, void* stream) {
     EdenTables tab;
     int rc = eden_check(n, dim, nbits, signs, &tab);
     if (rc) return rc;
@@ -3676,6 +3853,7 @@ int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, i
     a.in = bins;
     a.signs = signs;
     a.sign_row = sign_row;
+    a.sbits = sign_bits;
     a.scale = scale;
     a.D = w.D;
     a.dim = dim;
@@ -3686,81 +3864,23 @@ int uq_eden_decompress_f32(const uint8_t* bins, const float* scale, int64_t n, i
 
 int uq_eden_f32(const float* x, float* out, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
                 const int32_t* sign_row, float* scale_out, void* ws, size_t ws_bytes, void* stream) {
+    return uq_eden_f32_sb(x, out, n, dim, nbits, signs, sign_row, nullptr, scale_out, ws, ws_bytes, stream);
+}
+
+int uq_eden_f32_sb(const float* x, float* out, int64_t n, int64_t dim, int32_t nbits, const int8_t* signs,
+                   const int32_t* sign_row, const uint32_t* sign_bits, float* scale_out, void* ws, size_t ws_bytes,
+                   void* stream) {
     // compress (RHT, norm, bins + the MKL-order dot) then decompress: the receiver's first
     // pass reads the 1-byte bins KE4 wrote instead of the 4-byte rotated vector
     const EdenLayout w = eden_layout(n < 0 ? 0 : n, dim < 0 ? 0 : dim);
     uint8_t* bins = (uint8_t*)((char*)ws + w.bins_off);
     float* scale = scale_out ? scale_out : (float*)((char*)ws + w.scale_off);
-    int rc = uq_eden_compress_f32(x, n, dim, nbits, signs, sign_row, bins, scale, ws, ws_bytes, stream);
+    int rc = uq_eden_compress_f32_sb(x, n, dim, nbits, signs, sign_row, sign_bits, bins, scale, ws, ws_bytes, stream);
     if (rc) return rc;
-    return uq_eden_decompress_f32(bins, scale, n, dim, nbits, signs, sign_row, out, ws, ws_bytes, stream);
+    return uq_eden_decompress_f32_sb(bins, scale, n, dim, nbits, signs, sign_row, sign_bits, out, ws, ws_bytes, stream);
 }
 
 // ---- QUIC-FL sender ----------------------------------------------------------------------
-// The jump path (KQ0s + KQ0j + KQ1j + KQ1f, uq_quicfl_kernels.h) for few messages: R runs of L
-// rounds per message, R from a cost model of the phases (measured round-5 constants): the
-// streams (~20 us), the jumps (~tJ of the whole GPU per jump) and a round of passes A + B on one
-// wave (~tR; a run wave per SIMD).  The one-wave kernel when the model gives the jumps no gain.
-struct QflJumpPlan {
-    bool use = false;
-    int32_t R = 0;
-    int64_t L = 0, qL = 0;
-};
-static QflJumpPlan qfl_jump_plan(int64_t n, int64_t D) {
-    QflJumpPlan p;
-    const int64_t nch = (D + kMtN - 1) / kMtN;
-    if (n < 1 || n > kQfTeamMaxN || nch < 8 || D > ((int64_t)1 << 28)) return p;
-    const double tS = 20.0, tJ = 0.12, tR = 7.5;
-    double best = 1e300;
-    for (int64_t R = 1; R <= 1024 && R <= nch; ++R) {
-        const int64_t L = (nch + R - 1) / R, Ru = (nch + L - 1) / L;
-        if (Ru != R || n * R > 1024) continue;
-        const double t = tS + (double)(n * (3 * R - 2)) * tJ + (double)L * tR;
-        if (t < best) {
-            best = t;
-            p.R = (int32_t)R;
-            p.L = L;
-        }
-    }
-    p.use = best < 0.8 * (double)((n + 1023) / 1024) * (double)nch * tR;
-    p.qL = ((int64_t)kMtN + D) / kMtN;               // block of the first pass-B local word (qfl_ctx)
-    return p;
-}
-
-extern "C" int uq_mtpoly_progression(int64_t b0, int64_t step, int32_t count, uint32_t* out);   // uq_mt_poly.cpp
-
-// t^(624 b) mod phi for the plan's run starts, on the device, cached per (device, qL, L, R):
-// rows [0, R) = polyA (row r: b = r L - 1; row 0 unused), rows [R, 2R) = polyB (b = qL + r L - 1)
-static int qfl_jump_polys(const QflJumpPlan& p, const uint32_t** out) {
-    static std::mutex mu;
-    static std::map<std::tuple<int, int64_t, int64_t, int32_t>, uint32_t*> cache;
-    int dev = 0;
-    int rc = hip_check(hipGetDevice(&dev), "hipGetDevice");
-    if (rc) return rc;
-    std::lock_guard<std::mutex> lk(mu);
-    const auto key = std::make_tuple(dev, p.qL, p.L, p.R);
-    auto it = cache.find(key);
-    if (it != cache.end()) {
-        *out = it->second;
-        return UQ_OK;
-    }
-    std::vector<uint32_t> h((size_t)2 * p.R * kMtN, 0u);
-    if ((p.R > 1 && uq_mtpoly_progression(p.L - 1, p.L, p.R - 1, h.data() + kMtN)) ||
-        uq_mtpoly_progression(p.qL - 1, p.L, p.R, h.data() + (size_t)p.R * kMtN))
-        return fail(UQ_E_INVALID, "MT19937 jump polynomials unavailable");
-    uint32_t* d = nullptr;
-    rc = hip_check(hipMalloc(&d, h.size() * sizeof(uint32_t)), "hipMalloc jump polynomials");
-    if (rc) return rc;
-    rc = hip_check(hipMemcpy(d, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "copy jump polynomials");
-    if (rc) {
-        (void)hipFree(d);
-        return rc;
-    }
-    cache.emplace(key, d);
-    *out = d;
-    return UQ_OK;
-}
-
 // Workspace: the EDEN layout (rotated vectors, norms, segmented-norm region) + h [n][D] u8 +
 // the jump path's blocks [n][R][3][624] u32 and run records [n][R][2] i32.
 static size_t quicfl_h_off(int64_t n, int64_t dim) {
@@ -3839,10 +3959,10 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     return launch_quicfl_send(q, x_kind, wsb, dim, st);
 }
 
-// By batch size: few messages take the jump path (KQ0j + KQ1j + KQ1f: every run of every
-// message at once from jumped stream blocks); batches a wave per message (KQ1).  Test hooks:
-// bit 1 the one-wave kernel, bit 2 (or bit 0, whose timeouts only its runs can report) the team
-// kernel KQ1t (scouts + runs in one workgroup per message).
+// By batch size: up to 128 messages the jump path (KQ0s + KQ0j + KQ1j + KQ1f: every run of
+// every message at once from jumped stream blocks), up to 256 the team kernel KQ1t (scouts + runs
+// in one workgroup per message), batches a wave per message (KQ1).  Test hooks: bit 1 the
+// one-wave kernel, bit 2 (or bit 0, whose timeouts only the team's runs can report) KQ1t.
 static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, char* wsb, int64_t dim, hipStream_t st) {
     const int hooks = g_quicfl_hooks.load();
     q.force_timeout = hooks & 1;
@@ -3850,7 +3970,7 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, char* wsb, int64_t
     const QflJumpPlan jp = qfl_jump_plan(n, q.D);
     if (!(hooks & 7) && jp.use) {
         const uint32_t* polys = nullptr;
-        int rc = qfl_jump_polys(jp, &polys);
+        int rc = qfl_jump_polys(jp, false, &polys);
         if (rc) return rc;
         uint32_t* xs = (uint32_t*)(wsb + quicfl_jump_off(n, dim));
         uint32_t* parts = xs + (size_t)n * 2 * kMjX;
@@ -3864,6 +3984,8 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, char* wsb, int64_t
         ja.parts = parts;
         ja.R = jp.R;
         ja.n = n;
+        ja.nstreams = 2;
+        ja.kinds = 3;
         hipLaunchKernelGGL(quicfl_stream_kernel, dim3((unsigned)((2 * n + 3) / 4)), dim3(256), 0, st, ja);
         rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch");
         if (rc) return rc;
@@ -3889,7 +4011,8 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, char* wsb, int64_t
                            q, ra);
         return hip_check(hipGetLastError(), "quicfl_send_fin_kernel launch");
     }
-    if (!(hooks & 2) && (hooks & 5) && n <= kQfTeamMaxN && q.D >= (int64_t)kMtN * kQfRuns && q.D <= kQfTeamMaxD) {
+    if (!(hooks & 2) && ((hooks & 5) || !jp.use) && n <= kQfTeamMaxN && q.D >= (int64_t)kMtN * kQfRuns &&
+        q.D <= kQfTeamMaxD) {
         if (x_kind == 0)
             hipLaunchKernelGGL(quicfl_send_team_kernel<0>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
         else

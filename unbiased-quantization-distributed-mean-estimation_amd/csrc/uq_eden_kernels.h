@@ -113,6 +113,30 @@ rht_signs_kernel(const int32_t* __restrict__ seeds, int64_t D, int8_t* __restric
     }
 }
 
+// KE0b: the diagonal rows as bits (bit i % 32 of word i / 32 set where the sign is -1), so the
+// passes that apply the diagonal read 1/8 byte per coordinate instead of 1
+__global__ void __launch_bounds__(256)
+rht_sign_bits_kernel(const int8_t* __restrict__ signs, int64_t rows, int64_t D, uint32_t* __restrict__ bits) {
+    const int64_t W = (D + 31) / 32;
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= rows * W) return;
+    const int64_t r = q / W, w = q % W;
+    const int8_t* s = signs + r * D + 32 * w;
+    const int n = (int)min((int64_t)32, D - 32 * w);
+    uint32_t b = 0;
+    for (int k = 0; k < n; ++k) b |= (s[k] < 0 ? 1u : 0u) << k;
+    bits[q] = b;
+}
+
+// +-1.0f from bit 0 (set: -1) as an opaque operand, so that the multiply stays a v_mul_f32 as
+// with the int8 rows (the compiler would otherwise fold x * (b ? -1 : 1) into a sign flip,
+// which differs from the multiply on NaN inputs)
+__device__ __forceinline__ float sign_pm1(uint32_t b) {
+    float m = (b & 1u) ? -1.0f : 1.0f;
+    asm volatile("" : "+v"(m));
+    return m;
+}
+
 // ---- KE1: one FWHT pass ----------------------------------------------------------------
 // Stages for index bits [lo, lo + k).  lo == 0: tiles of 2^k contiguous elements.
 // lo > 0: tiles of 2^k rows x 32 columns (row r, column c -> hi + (r << lo) + c0 + c).
@@ -125,6 +149,7 @@ struct FwhtArgs {
     float* out;
     const int8_t* signs;        // [rows][D] diagonal rows
     const int32_t* sign_row;    // [n] row of each client
+    const uint32_t* sbits;      // [rows][ceil(D / 32)] the same rows as bits (KE0b), or null
     const float* scale;         // [n] (receiver last pass)
     int64_t D, dim;
     float sqrtD;
@@ -249,10 +274,17 @@ fwht_low4096_kernel(FwhtArgs a) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) v[i] = (i0 + i < a.dim) ? x[i0 + i] : 0.f;
             }
-            const int4 sgv = *reinterpret_cast<const int4*>(sg + i0);       // 16 signs
-            const int8_t* sb = reinterpret_cast<const int8_t*>(&sgv);
+            if (a.sbits) {                                                     // 16 signs as bits
+                const int64_t W = (D + 31) / 32;
+                const uint32_t bw = a.sbits[(int64_t)(a.sign_row ? a.sign_row[vec] : 0) * W + (i0 >> 5)] >> (i0 & 31);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = v[i] * (float)sb[i];            // AS:132/137 * diag
+                for (int i = 0; i < 16; ++i) v[i] = v[i] * sign_pm1(bw >> i);      // AS:132/137 * diag
+            } else {
+                const int4 sgv = *reinterpret_cast<const int4*>(sg + i0);       // 16 signs
+                const int8_t* sb = reinterpret_cast<const int8_t*>(&sgv);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = v[i] * (float)sb[i];            // AS:132/137 * diag
+            }
         } else if (MODE == 2) {
             const int4 bv = *reinterpret_cast<const int4*>((const uint8_t*)a.in + vec * D + i0);
             const uint8_t* bb = reinterpret_cast<const uint8_t*>(&bv);
@@ -348,10 +380,17 @@ fwht_low16k_kernel(FwhtArgs a) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) v[i] = (i0 + i < a.dim) ? x[i0 + i] : 0.f;
             }
-            const int4 sgv = *reinterpret_cast<const int4*>(sg + i0);       // 16 signs
-            const int8_t* sb = reinterpret_cast<const int8_t*>(&sgv);
+            if (a.sbits) {                                                     // 16 signs as bits
+                const int64_t W = (D + 31) / 32;
+                const uint32_t bw = a.sbits[(int64_t)(a.sign_row ? a.sign_row[vec] : 0) * W + (i0 >> 5)] >> (i0 & 31);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = v[i] * (float)sb[i];            // AS:132/137 * diag
+                for (int i = 0; i < 16; ++i) v[i] = v[i] * sign_pm1(bw >> i);      // AS:132/137 * diag
+            } else {
+                const int4 sgv = *reinterpret_cast<const int4*>(sg + i0);       // 16 signs
+                const int8_t* sb = reinterpret_cast<const int8_t*>(&sgv);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = v[i] * (float)sb[i];            // AS:132/137 * diag
+            }
         } else {
             const int4 bv = *reinterpret_cast<const int4*>((const uint8_t*)a.in + vec * D + i0);
             const uint8_t* bb = reinterpret_cast<const uint8_t*>(&bv);
@@ -427,7 +466,12 @@ fwht_high256_kernel(FwhtArgs a, int lo) {
     // the tile's diagonal as sign bits (2 KB of LDS keeps two workgroups per CU): thread
     // tid packs the 32 sign bytes of half a row
     __shared__ uint32_t sgb[RECV_LAST ? 2 * 256 : 1];
-    if (RECV_LAST) {
+    if (RECV_LAST && a.sbits) {                          // the bits as they are (64 columns: 2 words)
+        const int row = tid >> 1, half = tid & 1;
+        const int64_t W = (D + 31) / 32;
+        sgb[tid] = a.sbits[(int64_t)(a.sign_row ? a.sign_row[vec] : 0) * W +
+                           ((hi + ((int64_t)row << lo) + c0 + 32 * half) >> 5)];
+    } else if (RECV_LAST) {
         const int row = tid >> 1, half = tid & 1;
         const int4* sr = reinterpret_cast<const int4*>(sg + hi + ((int64_t)row << lo) + c0 + 32 * half);
         const int4 w0 = sr[0], w1 = sr[1];

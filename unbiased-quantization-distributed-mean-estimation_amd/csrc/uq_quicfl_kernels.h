@@ -674,10 +674,12 @@ struct QflJumpArgs {
     const int32_t* px_seeds;    //   or fresh generators
     const uint32_t* polyA;      // [R][624]: row r = t^(624 (r L - 1)) mod phi (row 0 unused)
     const uint32_t* polyB;      // [R][624]: row r = t^(624 (qL + r L - 1)) mod phi
-    uint32_t* xs;               // [n][2][kMjX]: the local and the global stream's first words
-    uint32_t* parts;            // [n][R][3][kMjParts][624]: partial windows (local r L, local qL + r L, global r L)
+    uint32_t* xs;               // [n][nstreams][kMjX]: the local (and the global) stream's first words
+    uint32_t* parts;            // [n][R][kinds][kMjParts][624]: partial windows (local r L, local qL + r L, global r L)
     int32_t R;
     int64_t n;
+    int32_t nstreams;           // 2: the sender (local + global); 1: the receiver (local)
+    int32_t kinds;              // 3: the sender's three blocks per run; 1: the receiver's local block r L
 };
 
 // KQ0s: x[0 .. kMjX) of each message's two streams (base block, then 32 twists), one wave each
@@ -686,8 +688,8 @@ quicfl_stream_kernel(QflJumpArgs a) {
     __shared__ uint32_t scratch[4][kMtN];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t id = (int64_t)blockIdx.x * 4 + wv;
-    const int64_t j = id >> 1;
-    const int s = (int)(id & 1);                         // 0 local, 1 global
+    const int64_t j = id / a.nstreams;
+    const int s = (int)(id % a.nstreams);                // 0 local, 1 global
     if (j >= a.n) return;
     uint32_t st[kMtGroups];
     if (s == 1 && a.px_state) {
@@ -697,7 +699,7 @@ quicfl_stream_kernel(QflJumpArgs a) {
         wave_lds_fence();
         mt_load(st, scratch[wv], lane);
     }
-    uint32_t* x = a.xs + (j * 2 + s) * kMjX;
+    uint32_t* x = a.xs + (j * a.nstreams + s) * kMjX;
     __builtin_amdgcn_s_setprio(3);
     mt_store(st, x, lane);
     for (int b = 1; b < kMjBlocks; ++b) {
@@ -755,8 +757,8 @@ quicfl_jump_kernel(QflJumpArgs a) {
     const int64_t bid = blockIdx.x;
     const int p = (int)(bid % kMjParts);
     const int64_t job = bid / kMjParts;
-    const int s = (int)(job % 3);
-    const int64_t jr = job / 3;
+    const int s = (int)(job % a.kinds);
+    const int64_t jr = job / a.kinds;
     const int r = (int)(jr % a.R);
     const int64_t j = jr / a.R;
     if (j >= a.n || (r == 0 && s != 1)) return;          // run 0's local-A and global blocks are the bases
@@ -764,7 +766,7 @@ quicfl_jump_kernel(QflJumpArgs a) {
     const int wb0 = p * 4 * kMjSlice + wv * kMjSlice;
     const uint32_t pv = lane < kMjSlice ? poly[wb0 + lane] : 0u;           // the wave's coefficient words
     const int k_lo = p * 4 * kMjSlice * 32;
-    const uint32_t* x = a.xs + (j * 2 + (s == 2 ? 1 : 0)) * kMjX;
+    const uint32_t* x = a.xs + (j * a.nstreams + (s == 2 ? 1 : 0)) * kMjX;
     {                                                    // stage x[k_lo ..): every load in flight at once
         constexpr int kQ = kMjPartWords / 4, kPer = (kQ + 255) / 256;
         typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
@@ -830,7 +832,7 @@ quicfl_jump_kernel(QflJumpArgs a) {
         if (w < kMtN) *(uint4*)(P + w) = make_uint4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
     }
     __syncthreads();
-    uint32_t* out = a.parts + (((j * a.R + r) * 3 + s) * kMjParts + p) * kMtN;
+    uint32_t* out = a.parts + (((j * a.R + r) * a.kinds + s) * kMjParts + p) * kMtN;
     for (int i = threadIdx.x; i < kMtN; i += 256) out[i] = X[i] ^ X[640 + i] ^ X[1280 + i] ^ X[1920 + i];
 }
 
@@ -1198,4 +1200,84 @@ quicfl_recv_team_kernel(QflRecvArgs a) {
         if (a.compact && a.exact_count && (int64_t)tot != (int64_t)a.exact_count[j]) f |= UQ_QFL_BAD_EXACT;
         a.info[j] = f;
     }
+}
+
+// ---- receiver jump path (few messages): the h stream's run starts by jump-ahead ---------------
+// KQ0s + KQ0j on the local stream only (one block per run: local block c0, the sender's polyA),
+// then KQ2c counts each run's exact coordinates (compact slots), KQ2j runs every run of every
+// message at once (qfl_recv_rounds), KQ2f ORs the flags and checks the exact count.
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_recv_count_kernel(QflRecvArgs a, QflRunArgs ra) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t id = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    const int64_t j = id / ra.R;
+    const int r = (int)(id % ra.R);
+    if (j >= a.n) return;
+    int32_t cnt = 0;
+    if (a.compact && a.exact_mask) {
+        const uint8_t* mk = a.exact_mask + j * a.D;
+        const int64_t e0 = (int64_t)r * ra.L * kMtN, e1 = min(a.D, e0 + ra.L * kMtN);
+        for (int64_t i = e0 + lane; i < e1; i += 64) cnt += mk[i] != 0;
+        for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+    }
+    if (lane == 0) ra.runinfo[(j * ra.R + r) * 2] = cnt;
+}
+
+template <int XK>
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_recv_runs_kernel(QflRecvArgs a, QflRunArgs ra) {
+    __shared__ float tab[kQflTab];
+    __shared__ uint32_t seed[kQfWavesPerWG][kMtN];
+    for (int i = threadIdx.x; i < a.tab_n; i += 64 * kQfWavesPerWG) tab[i] = a.table[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t id = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    const int64_t j = id / ra.R;
+    const int r = (int)(id % ra.R);
+    if (j >= a.n) return;
+    const int64_t nch = (a.D + kMtN - 1) / kMtN;
+    const int64_t c0 = (int64_t)r * ra.L, c1 = min(nch, c0 + ra.L);
+    int32_t* info = ra.runinfo + (j * ra.R + r) * 2;
+    if (c0 >= c1) {
+        if (lane == 0) info[1] = 0;
+        return;
+    }
+    uint32_t sL[kMtGroups];
+    if (r == 0) {                                        // the h stream's block 0: the seed itself
+        if (lane == 0) mt_seed(seed[wv], (uint32_t)a.prng_seeds[j]);
+        wave_lds_fence();
+        mt_load(sL, seed[wv], lane);
+    } else {
+        mj_block(sL, ra.parts + (j * ra.R + r) * kMjParts * kMtN, lane);
+    }
+    uint32_t ebase = 0;                                  // compact slots of the earlier runs (KQ2c)
+    if (a.compact && a.exact_mask) {
+        for (int q = lane; q < r; q += 64) ebase += (uint32_t)ra.runinfo[(j * ra.R + q) * 2];
+        for (int o = 32; o >= 1; o >>= 1) ebase += __shfl_xor(ebase, o);
+    }
+    uint32_t eend = 0;
+    int32_t flags = qfl_recv_rounds<XK>(a, tab, j, sL, c0, c1, ebase, &eend, lane);
+    for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
+    if (lane == 0) info[1] = flags;
+}
+
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_recv_fin_kernel(QflRecvArgs a, QflRunArgs ra) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    if (j >= a.n) return;
+    const int32_t* info = ra.runinfo + j * ra.R * 2;
+    int32_t flags = 0;
+    int64_t tot = 0;
+    for (int r = lane; r < ra.R; r += 64) {
+        flags |= info[2 * r + 1];
+        tot += info[2 * r];
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        flags |= __shfl_xor(flags, o);
+        tot += __shfl_xor(tot, o);
+    }
+    // AS:531 vec[exact_indeces] = exact_values raises unless the counts agree
+    if (a.compact && a.exact_count && tot != (int64_t)a.exact_count[j]) flags |= UQ_QFL_BAD_EXACT;
+    if (lane == 0 && a.info) a.info[j] = flags;
 }

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import threading
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -144,6 +145,38 @@ def _sign_rows(seeds: torch.Tensor, D: int, dev):
     return rht_signs(uniq, D, dev), inv.to(torch.int32).to(dev)
 
 
+def rht_sign_bits(tab: torch.Tensor) -> torch.Tensor:
+    """int32 [rows, ceil(D / 32)]: the diagonal rows of `tab` as bits (bit set where the sign is
+    -1), which the EDEN passes that apply the diagonal read instead of the int8 rows."""
+    rows, D = tab.shape
+    out = torch.empty((rows, (D + 31) // 32), dtype=torch.int32, device=tab.device)
+    _lib.check(_lib.load().uq_rht_sign_bits(_ptr(tab), rows, D, _ptr(out), _stream_ptr(tab.device)),
+               "uq_rht_sign_bits")
+    return out
+
+
+_bits_of: dict = {}          # id(table) -> (weak reference to the table, its bit rows)
+
+
+def _bits_for(tab: torch.Tensor) -> torch.Tensor:
+    """The bit rows of a sign table, kept exactly as long as the table itself lives."""
+    with _cache_lock:
+        e = _bits_of.get(id(tab))
+        if e is not None and e[0]() is tab:
+            return e[1]
+    bits = rht_sign_bits(tab)
+    k = id(tab)
+    with _cache_lock:
+        _bits_of[k] = (weakref.ref(tab, lambda _r, k=k: _bits_of.pop(k, None)), bits)
+    return bits
+
+
+def _sign_rows_bits(seeds: torch.Tensor, D: int, dev):
+    """(table, row index per client, the table's rows as bits)."""
+    tab, rows = _sign_rows(seeds, D, dev)
+    return tab, rows, _bits_for(tab)
+
+
 def _ws(n, d, dev):
     b = ctypes.c_size_t(0)
     _lib.check(_lib.load().uq_eden_workspace_bytes(n, d, ctypes.byref(b)), "uq_eden_workspace_bytes")
@@ -185,10 +218,11 @@ def eden_compress(x, bits_per_dimension=1, seeds=None, *, generator=None) -> Ede
     bins = torch.empty((n, D), dtype=torch.uint8, device=dev)
     scale = torch.empty(n, dtype=torch.float32, device=dev)
     if n and d:
-        tab, rows = _sign_rows(s, D, dev)
+        tab, rows, sb = _sign_rows_bits(s, D, dev)
         ws = _ws(n, d, dev)
-        _lib.check(_lib.load().uq_eden_compress_f32(_ptr(x), n, d, nb, _ptr(tab), _ptr(rows), _ptr(bins), _ptr(scale),
-                                                    _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_eden_compress_f32")
+        _lib.check(_lib.load().uq_eden_compress_f32_sb(_ptr(x), n, d, nb, _ptr(tab), _ptr(rows), _ptr(sb), _ptr(bins),
+                                                       _ptr(scale), _ptr(ws), ws.numel(), _stream_ptr(dev)),
+                   "uq_eden_compress_f32_sb")
     return EdenMessage(bins=bins, scale=scale, seeds=s, nbits=nb, dim=d)
 
 
@@ -201,11 +235,11 @@ def eden_decompress(msg: EdenMessage) -> torch.Tensor:
     d = msg.dim
     out = torch.empty((n, d), dtype=torch.float32, device=dev)
     if n and d:
-        tab, rows = _sign_rows(torch.as_tensor(msg.seeds), bins.shape[1], dev)
+        tab, rows, sb = _sign_rows_bits(torch.as_tensor(msg.seeds), bins.shape[1], dev)
         ws = _ws(n, d, dev)
-        _lib.check(_lib.load().uq_eden_decompress_f32(_ptr(bins), _ptr(scale), n, d, msg.nbits, _ptr(tab), _ptr(rows),
-                                                      _ptr(out), _ptr(ws), ws.numel(), _stream_ptr(dev)),
-                   "uq_eden_decompress_f32")
+        _lib.check(_lib.load().uq_eden_decompress_f32_sb(_ptr(bins), _ptr(scale), n, d, msg.nbits, _ptr(tab),
+                                                         _ptr(rows), _ptr(sb), _ptr(out), _ptr(ws), ws.numel(),
+                                                         _stream_ptr(dev)), "uq_eden_decompress_f32_sb")
     return out
 
 
@@ -219,10 +253,10 @@ def eden_quantize(x, bits_per_dimension=1, seeds=None, *, return_scale: bool = F
     out = torch.empty((n, d), dtype=torch.float32, device=dev)
     scale = torch.empty(n, dtype=torch.float32, device=dev)
     if n and d:
-        tab, rows = _sign_rows(s, padded_dim(d), dev)
+        tab, rows, sb = _sign_rows_bits(s, padded_dim(d), dev)
         ws = _ws(n, d, dev)
-        _lib.check(_lib.load().uq_eden_f32(_ptr(x), _ptr(out), n, d, nb, _ptr(tab), _ptr(rows), _ptr(scale), _ptr(ws),
-                                           ws.numel(), _stream_ptr(dev)), "uq_eden_f32")
+        _lib.check(_lib.load().uq_eden_f32_sb(_ptr(x), _ptr(out), n, d, nb, _ptr(tab), _ptr(rows), _ptr(sb),
+                                              _ptr(scale), _ptr(ws), ws.numel(), _stream_ptr(dev)), "uq_eden_f32_sb")
     return (out, scale) if return_scale else out
 
 

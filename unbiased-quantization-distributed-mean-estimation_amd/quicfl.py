@@ -368,10 +368,14 @@ def quicfl_decompress(X, nbits: int, prng_seeds, rotation_seeds, scale, dim: int
             hin[n:] = c.astype(np.int32)
         din = torch.from_numpy(hin).to(dev)
         seeds32, cnt = din[:n], (din[n:] if hin.size > n else None)
-        _lib.check(_lib.load().uq_quicfl_receive_f32(
+        L = _lib.load()
+        wb = ctypes.c_size_t()
+        _lib.check(L.uq_quicfl_receive_workspace_bytes(n, D, ctypes.byref(wb)), "uq_quicfl_receive_workspace_bytes")
+        ws = torch.empty(max(int(wb.value), 1), dtype=torch.uint8, device=dev)
+        _lib.check(L.uq_quicfl_receive_ws_f32(
             _ptr(Xd), _X_KIND[Xd.dtype], n, D, _ptr(tab), rows, hl, _ptr(seeds32), _ptr(m), _ptr(v),
-            1 if (compact and m is not None) else 0, _ptr(cnt), _ptr(sc), _ptr(pre), _ptr(info), _stream_ptr(dev)),
-            "uq_quicfl_receive_f32")
+            1 if (compact and m is not None) else 0, _ptr(cnt), _ptr(sc), _ptr(pre), _ptr(info), _ptr(ws), wb.value,
+            _stream_ptr(dev)), "uq_quicfl_receive_ws_f32")
         if not _defer_check:
             _raise_recv_flags(int(np.bitwise_or.reduce(info.cpu().numpy())))
     out = randomized_inverse_hadamard_transform(pre, rs)[:, :dim]
