@@ -19,7 +19,8 @@ FLOORS = {
     "biased": [
         ("l1_partial_kernel<true, (anonymous namespace)::AbsOp", 4 * D * N, "KB1: read x"),
         ("l1_partial_kernel<true, (anonymous namespace)::RezKHistOp", 4 * D * N, "KB2: read x (k' and digit 1)"),
-        ("rez_compact_kernel", 4 * D * N, "KB4b: read x (bucket keys)"),
+        ("rez_compact_kernel", 4 * D * N, "KB4b: read x (bucket keys; round 4 only)"),
+        ("rez_output_fine_kernel", 8 * D * N, "KB6f: read x, write q, list the threshold bin (round 5)"),
         ("rez_output_kernel", 8 * D * N, "KB6: read x, write q (all clients over its two launches)"),
         ("rez_tiecount_kernel", 0, "KB5: ambiguous clients only"),
     ],

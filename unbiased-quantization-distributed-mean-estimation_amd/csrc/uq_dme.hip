@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -333,10 +334,14 @@ struct RezKHistOp {
 // BIG: cascade steps 64-256 (one chunk of more than 2^28 elements, e.g. T = 1 beyond
 // d = 2^28): 256 threads, each taking leaves b, b + 32, ...; 32 KB of leaf sums.
 // =====================================================================================
+// gpw level-1 groups per workgroup, one after the other (the histogram op: its 2048-bin LDS
+// histogram is flushed -- one global atomic per nonzero bin, ~1700 per 8192 coordinates of
+// Gaussian rows -- once per gpw groups instead of once per group).
 template <bool VEC4, class Op, bool BIG = false>
 __global__ void __launch_bounds__(256)
 l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __restrict__ part,
-                  const float* __restrict__ l1, float fm, uint32_t* __restrict__ hist_g, uint32_t* __restrict__ zn_g) {
+                  const float* __restrict__ l1, float fm, uint32_t* __restrict__ hist_g, uint32_t* __restrict__ zn_g,
+                  int gpw = 1) {
     const int64_t vec = blockIdx.y;
     Op op = Op::make(l1, fm, vec);
     __shared__ uint32_t hs[Op::kHist ? 2048 + 2 : 1];
@@ -346,14 +351,17 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
         op.h = hs;
         op.zn = hs + 2048;
     }
-    int32_t G = blockIdx.x;
+    __shared__ float leaf[(BIG ? 256 : 32) * 32];   // [leaf][32]
+    const int32_t G0 = (int32_t)blockIdx.x * gpw;
+    const int32_t G1 = min((int32_t)plan.total_groups, G0 + gpw);
+    for (int32_t G = G0; G < G1; ++G) {
+    if (G > G0) __syncthreads();              // the previous group's leaf sums are read
     const int c = plan.chunk_of_group(G);
     const int32_t g = G - plan.gbase(c);
     const int lp = plan.geo(c).lp;
     const int step = 1 << lp;
     const int tid = threadIdx.x;
     const int nthreads = 8 * step;            // 8 quads x step leaves
-    __shared__ float leaf[(BIG ? 256 : 32) * 32];   // [leaf][32]
     const float* base = x + vec * d + plan.off(c) + (int64_t)g * step * step * 32;
     for (int b = tid >> 3; BIG ? b < step : tid < nthreads; b += 32) {
         const int q = tid & 7;
@@ -381,7 +389,10 @@ l1_partial_kernel(const float* __restrict__ x, int64_t d, L1Plan plan, float* __
         for (int b = 0; b < step; ++b) acc += leaf[b * 32 + tid];
         part[(vec * plan.total_groups + G) * 32 + tid] = acc;
     }
+    }
     if (Op::kHist) {
+        const int tid = threadIdx.x;
+        __syncthreads();                      // every group's LDS counts are in
         for (int b = tid; b < 2048; b += blockDim.x)
             if (hs[b]) atomicAdd(&hist_g[((size_t)vec * kHistSlots + kFineSlot) * 2048 + b], hs[b]);
         if (tid < 2 && hs[2048 + tid]) atomicAdd(&zn_g[vec * 2 + tid], hs[2048 + tid]);
@@ -2231,6 +2242,17 @@ WsLayout layout(int64_t n, int64_t d, const L1Plan& plan) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// KB2 (the k' sum with the fine-bin histogram): at most this many level-1 groups per
+// workgroup, fewer while that would leave fewer than ~4096 workgroups (a few-client call keeps
+// one group each).  1024 x 2^20: KB2 1.16 -> 0.97 ms at 4 (torch-tie batch 5.43 -> 5.21 ms,
+// lowest-index 4.23 -> 3.97 ms on one box; 8: 5.21 / 3.96), profiles/r5n_biased_gpw.jsonl.
+// Env UQDME_HIST_GPW overrides the cap (measurements).
+static const int kHistGroupsPerWG = [] {
+    const char* e = std::getenv("UQDME_HIST_GPW");
+    const int v = e ? std::atoi(e) : 8;
+    return v >= 1 && v <= 64 ? v : 8;
+}();
+
 template <class Op>
 int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, float* part, float* sum_out,
                    const float* l1, float fm, hipStream_t st, uint32_t* hist = nullptr, uint32_t* zn = nullptr) {
@@ -2239,20 +2261,25 @@ int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, flo
         vec4 = vec4 && (plan.nchunks == 1 || plan.cs % 4 == 0);
         int maxstep = std::max(16, 1 << plan.last.lp);
         if (plan.nchunks > 1) maxstep = std::max(maxstep, 1 << plan.full.lp);
-        dim3 grid(plan.total_groups, (unsigned)n);
+        const int gpw = Op::kHist ? (int)std::max<int64_t>(1, std::min<int64_t>(kHistGroupsPerWG,
+                                                                                (int64_t)plan.total_groups * n / 4096))
+                                  : 1;
+        dim3 grid((unsigned)((plan.total_groups + gpw - 1) / gpw), (unsigned)n);
         if (maxstep > 32) {              // steps 64..256 (chunk_geo stops at 256)
             if (vec4)
                 hipLaunchKernelGGL((l1_partial_kernel<true, Op, true>), grid, dim3(256), 0, st, x, d, plan, part, l1, fm,
-                                   hist, zn);
+                                   hist, zn, gpw);
             else
                 hipLaunchKernelGGL((l1_partial_kernel<false, Op, true>), grid, dim3(256), 0, st, x, d, plan, part, l1, fm,
-                                   hist, zn);
+                                   hist, zn, gpw);
         } else {
             dim3 block(8 * maxstep);
             if (vec4)
-                hipLaunchKernelGGL((l1_partial_kernel<true, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn);
+                hipLaunchKernelGGL((l1_partial_kernel<true, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn,
+                                   gpw);
             else
-                hipLaunchKernelGGL((l1_partial_kernel<false, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn);
+                hipLaunchKernelGGL((l1_partial_kernel<false, Op>), grid, block, 0, st, x, d, plan, part, l1, fm, hist, zn,
+                                   gpw);
         }
         int rc = hip_check(hipGetLastError(), "l1_partial_kernel launch");
         if (rc) return rc;
