@@ -3445,18 +3445,20 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         SideStream* sb = nullptr;
         rc = side_stream(&sb);
         if (rc) return rc;
+        // the tie list (and cleared tie bits) before the fork: both streams read it
+        rc = torch_ties_prepare(n, d, state, bits, wsb, w, st);
+        if (rc) return rc;
         rc = hip_check(hipEventRecord(sb->fork, st), "record fork");
         if (rc) return rc;
         rc = hip_check(hipStreamWaitEvent(sb->s, sb->fork, 0), "wait fork");
         if (rc) return rc;
         // KB6 for the clients without a tie is enqueued first: the side chain below is ~60
-        // short launches, and the GPU must not idle while the host issues them
+        // short launches, and the GPU must not idle while the host issues them; the tie counts
+        // of unlisted clients (independent of the replays) follow it on this stream, off the
+        // replay chain's critical path (they were 62 us of early-exit workgroups on it)
         rc = output(st, 1);
         if (rc) return rc;
-        rc = torch_ties_prepare(n, d, state, bits, wsb, w, sb->s);
-        if (rc) return rc;
-        // tie counts of unlisted clients first: independent of the replays
-        rc = tiecount(sb->s, (const uint32_t*)(wsb + w.list_off));
+        rc = tiecount(st, (const uint32_t*)(wsb + w.list_off));
         if (rc) return rc;
         const TieLevelState* tls = nullptr;
         rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls);
@@ -3499,6 +3501,7 @@ struct QflJumpPlan {
     int32_t R = 0;
     int64_t L = 0, qL = 0;
 };
+
 // (Up to 128 messages: at 256 x 2^20 only R = 4 runs fit beside each other and the team kernel
 // measured 5.4 against 6.0 ms; 128 x 2^20: 3.4 against 4.5 ms, profiles/r5h_quicfl_batch_sizes.jsonl.)
 constexpr int64_t kQfJumpMaxN = 128;
@@ -3931,7 +3934,55 @@ int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
     return UQ_OK;
 }
 
-static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, char* wsb, int64_t dim, hipStream_t st);
+// The jump path's first two phases (KQ0s + KQ0j) depend only on the generators, so they are
+// issued first, on the side stream, and run beside the RHT and the norm on the caller's stream
+// (~80 us of small kernels for one 2^20 message); the runs wait for them.
+struct QflJumpLaunch {
+    bool use = false;
+    QflJumpPlan jp;
+    uint32_t* parts = nullptr;
+    SideStream* sb = nullptr;
+};
+static int quicfl_jump_fork(int64_t n, int64_t D, int64_t dim, const int32_t* prng_seeds, const uint32_t* px_state,
+                            const int32_t* px_seeds, char* wsb, hipStream_t st, QflJumpLaunch* jl) {
+    *jl = QflJumpLaunch{};
+    const int hooks = g_quicfl_hooks.load();
+    const QflJumpPlan jp = qfl_jump_plan(n, D);
+    if ((hooks & 7) || !jp.use) return UQ_OK;
+    const uint32_t* polys = nullptr;
+    int rc = qfl_jump_polys(jp, false, &polys);
+    if (rc) return rc;
+    SideStream* sb = nullptr;
+    if ((rc = side_stream(&sb))) return rc;
+    if ((rc = hip_check(hipEventRecord(sb->fork, st), "record fork"))) return rc;
+    if ((rc = hip_check(hipStreamWaitEvent(sb->s, sb->fork, 0), "wait fork"))) return rc;
+    uint32_t* xs = (uint32_t*)(wsb + quicfl_jump_off(n, dim));
+    uint32_t* parts = xs + (size_t)n * 2 * kMjX;
+    QflJumpArgs ja{};
+    ja.prng_seeds = prng_seeds;
+    ja.px_state = px_state;
+    ja.px_seeds = px_seeds;
+    ja.polyA = polys;
+    ja.polyB = polys + (size_t)jp.R * kMtN;
+    ja.xs = xs;
+    ja.parts = parts;
+    ja.R = jp.R;
+    ja.n = n;
+    ja.nstreams = 2;
+    ja.kinds = 3;
+    hipLaunchKernelGGL(quicfl_stream_kernel, dim3((unsigned)((2 * n + 3) / 4)), dim3(256), 0, sb->s, ja);
+    if ((rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch"))) return rc;
+    hipLaunchKernelGGL(quicfl_jump_kernel, dim3((unsigned)(n * jp.R * 3 * kMjParts)), dim3(256), 0, sb->s, ja);
+    if ((rc = hip_check(hipGetLastError(), "quicfl_jump_kernel launch"))) return rc;
+    if ((rc = hip_check(hipEventRecord(sb->join, sb->s), "record join"))) return rc;
+    jl->use = true;
+    jl->jp = jp;
+    jl->parts = parts;
+    jl->sb = sb;
+    return UQ_OK;
+}
+
+static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunch& jl, hipStream_t st);
 
 int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
                            const float* table_xp, const uint32_t* table_packed, int64_t table_numel, int32_t h_len,
@@ -3955,9 +4006,12 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     if (!ws || ws_bytes < quicfl_ws_total(n, dim)) return fail(UQ_E_WORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
+    QflJumpLaunch jl;
+    int rc = quicfl_jump_fork(n, w.D, dim, prng_seeds, px_state, px_seeds, wsb, st, &jl);
+    if (rc) return rc;
     FwhtArgs a;
     float* rot = nullptr;
-    int rc = eden_front(x, n, dim, EdenTables{}, signs, sign_row, w, wsb, a, &rot, st);     // AS:460-470
+    rc = eden_front(x, n, dim, EdenTables{}, signs, sign_row, w, wsb, a, &rot, st);     // AS:460-470
     if (rc) return rc;
     QflSendArgs q{};
     q.rot = rot;
@@ -3983,48 +4037,27 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.info = info;
     q.D = w.D;
     q.n = n;
-    return launch_quicfl_send(q, x_kind, wsb, dim, st);
+    return launch_quicfl_send(q, x_kind, jl, st);
 }
 
 // By batch size: up to 128 messages the jump path (KQ0s + KQ0j + KQ1j + KQ1f: every run of
 // every message at once from jumped stream blocks), up to 256 the team kernel KQ1t (scouts + runs
 // in one workgroup per message), batches a wave per message (KQ1).  Test hooks: bit 1 the
 // one-wave kernel, bit 2 (or bit 0, whose timeouts only the team's runs can report) KQ1t.
-static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, char* wsb, int64_t dim, hipStream_t st) {
+static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunch& jl, hipStream_t st) {
     const int hooks = g_quicfl_hooks.load();
     q.force_timeout = hooks & 1;
     const int64_t n = q.n;
     const QflJumpPlan jp = qfl_jump_plan(n, q.D);
-    if (!(hooks & 7) && jp.use) {
-        const uint32_t* polys = nullptr;
-        int rc = qfl_jump_polys(jp, false, &polys);
-        if (rc) return rc;
-        uint32_t* xs = (uint32_t*)(wsb + quicfl_jump_off(n, dim));
-        uint32_t* parts = xs + (size_t)n * 2 * kMjX;
-        QflJumpArgs ja{};
-        ja.prng_seeds = q.prng_seeds;
-        ja.px_state = q.px_state;
-        ja.px_seeds = q.px_seeds;
-        ja.polyA = polys;
-        ja.polyB = polys + (size_t)jp.R * kMtN;
-        ja.xs = xs;
-        ja.parts = parts;
-        ja.R = jp.R;
-        ja.n = n;
-        ja.nstreams = 2;
-        ja.kinds = 3;
-        hipLaunchKernelGGL(quicfl_stream_kernel, dim3((unsigned)((2 * n + 3) / 4)), dim3(256), 0, st, ja);
-        rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch");
-        if (rc) return rc;
-        hipLaunchKernelGGL(quicfl_jump_kernel, dim3((unsigned)(n * jp.R * 3 * kMjParts)), dim3(256), 0, st, ja);
-        rc = hip_check(hipGetLastError(), "quicfl_jump_kernel launch");
+    if (jl.use) {
+        int rc = hip_check(hipStreamWaitEvent(st, jl.sb->join, 0), "wait join");   // KQ0s + KQ0j done
         if (rc) return rc;
         QflRunArgs ra{};
-        ra.parts = parts;
-        ra.runinfo = (int32_t*)(parts + (size_t)n * jp.R * 3 * kMjParts * kMtN);
-        ra.R = jp.R;
-        ra.L = jp.L;
-        const dim3 rgrid((unsigned)((n * jp.R + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk(64 * kQfWavesPerWG);
+        ra.parts = jl.parts;
+        ra.runinfo = (int32_t*)(jl.parts + (size_t)n * jl.jp.R * 3 * kMjParts * kMtN);
+        ra.R = jl.jp.R;
+        ra.L = jl.jp.L;
+        const dim3 rgrid((unsigned)((n * jl.jp.R + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk(64 * kQfWavesPerWG);
         if (!q.pre) {
             hipLaunchKernelGGL(quicfl_send_count_kernel, rgrid, blk, 0, st, q, ra);
             rc = hip_check(hipGetLastError(), "quicfl_send_count_kernel launch");
@@ -4078,9 +4111,12 @@ int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     if (!ws || ws_bytes < quicfl_ws_total(n, dim)) return fail(UQ_E_WORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
+    QflJumpLaunch jl;
+    int rc = quicfl_jump_fork(n, w.D, dim, prng_seeds, px_state, px_seeds, wsb, st, &jl);
+    if (rc) return rc;
     FwhtArgs a;
     float* rot = nullptr;
-    int rc = eden_front(x, n, dim, EdenTables{}, signs, sign_row, w, wsb, a, &rot, st);     // AS:460-470
+    rc = eden_front(x, n, dim, EdenTables{}, signs, sign_row, w, wsb, a, &rot, st);     // AS:460-470
     if (rc) return rc;
     QflSendArgs q{};
     q.rot = rot;
@@ -4104,7 +4140,7 @@ int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.rtab = recv_table;
     q.rtab_n = recv_numel;
     q.pre = rot;                       // in place: a coordinate's rot is loaded a round before its value is stored
-    rc = launch_quicfl_send(q, 0, wsb, dim, st);                                                        // AS:455-503, 526-532
+    rc = launch_quicfl_send(q, 0, jl, st);                                                        // AS:455-503, 526-532
     if (rc) return rc;
     // AS:533-535: the receiver's inverse RHT (H, then * diag), [:dim]
     const int p = ilog2_pow2(w.D);
