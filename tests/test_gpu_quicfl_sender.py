@@ -322,4 +322,3 @@ def test_packed_table_same_bits(fx, monkeypatch):
     tX[0, 0] = 0.5
     odd = uqdme.QuicFLSender(tables={1: (tX, tp, DATA[1])})
     assert odd.table_packed(1, torch.device("cuda", 0)) is None
-
