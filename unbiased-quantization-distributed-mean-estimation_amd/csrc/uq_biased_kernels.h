@@ -607,8 +607,12 @@ rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t 
 
 // KB6f: fine clients (kRezFine) -- out for every coordinate with the selection decided by the
 // fine bin (above the threshold's bin: selected; below: not); the threshold bin's coordinates
-// are written unselected and listed as (index, key) pairs for KB4d (one atomic per workgroup
-// reserves the list range).  The same arithmetic as KB6, so KB6p's patch gives KB6's bits.
+// are written unselected and listed as (index, key) pairs for KB4d: staged in LDS by LDS
+// atomics, then one global atomic per workgroup reserves the list range (a per-thread list
+// indexed by a running count lived in scratch: 1.77 ms against 1.72-1.74 here, the batch
+// 0.01-0.05 ms faster, profiles/r5p_exp_biased_kb6f_lds.jsonl).  The same arithmetic as KB6, so
+// KB6p's patch gives KB6's bits.
+constexpr uint32_t kFineStage = 256;
 template <bool VEC4>
 __global__ void __launch_bounds__(256)
 rez_output_fine_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, const float* __restrict__ l1,
@@ -627,18 +631,22 @@ rez_output_fine_kernel(const float* __restrict__ x, float* __restrict__ out, int
     float* ov = out + vec * d;
     const int tid = threadIdx.x;
     const int64_t tb = (int64_t)blockIdx.x * kSelTile;
-    __shared__ uint32_t lds[4];
-    __shared__ uint32_t s_base;
-    uint32_t ck[kSelItems];                    // listed keys of this thread (indices alongside)
-    uint32_t ci[kSelItems];
-    uint32_t nck = 0;
+    // past kFineStage pairs (tie-heavy tiles), straight to the global list
+    __shared__ uint2 stage[kFineStage];
+    __shared__ uint32_t s_cnt, s_base;
+    if (tid == 0) s_cnt = 0u;
+    __syncthreads();
     auto one = [&](float v, float kp, uint32_t key, int64_t i, float& kq) {
         const uint32_t b = rez_fbin(rez_key_val(key));
         kq = b > fb ? kp + adj : kp;                           // k'' (the bucket provisionally unselected)
         if (b == fb) {
-            ck[nck] = key;
-            ci[nck] = (uint32_t)i;
-            ++nck;
+            const uint32_t slot = atomicAdd(&s_cnt, 1u);
+            if (slot < kFineStage) {
+                stage[slot] = make_uint2((uint32_t)i, key);
+            } else {
+                const uint32_t g = atomicAdd(&cand_n[vec], 1u);
+                if (g < capf) cand[(size_t)vec * capf + g] = make_uint2((uint32_t)i, key);
+            }
         }
     };
     if (VEC4 && tb + kSelTile <= d) {
@@ -687,15 +695,14 @@ rez_output_fine_kernel(const float* __restrict__ x, float* __restrict__ out, int
                 if (e0 + 4 * j + c < d) ov[e0 + 4 * j + c] = (L * torch_signf(v4[c])) * r4[c];
         }
     }
-    uint32_t tot;
-    const uint32_t off = block_excl_scan_u32(nck, lds, &tot);
+    __syncthreads();
+    const uint32_t tot = min(s_cnt, (uint32_t)kFineStage);
     if (tot == 0) return;                                      // block-uniform
     if (tid == 0) s_base = atomicAdd(&cand_n[vec], tot);
     __syncthreads();
     uint2* cv = cand + (size_t)vec * capf;
-    const uint32_t base = s_base + off;
-    for (uint32_t k = 0; k < nck; ++k)
-        if (base + k < capf) cv[base + k] = make_uint2(ci[k], ck[k]);
+    for (uint32_t t = tid; t < tot; t += 256)
+        if (s_base + t < capf) cv[s_base + t] = stage[t];
 }
 
 // KB6p: the listed coordinates of a fine client without a threshold tie that are selected
