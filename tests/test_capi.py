@@ -199,3 +199,23 @@ def test_build_id_matches_sources(lib):
     from uqdme_amd import build_ext
     assert lib.uq_build_id().decode() == build_ext.build_id()
     assert not build_ext.needs_build()
+
+
+def test_quicfl_workspaces_cover_the_jump_paths(lib):
+    """The QUIC-FL workspaces grow by the jump path's scratch where it applies (few messages of
+    >= 8 rounds: the sender's streams, partial windows and run records; the receiver's with a
+    workspace entry) and stay as before elsewhere (host-only: no kernel runs)."""
+    sz = ctypes.c_size_t()
+    base = {}
+    for n, d in ((1, 2048), (1, 1 << 20), (128, 1 << 20), (300, 1 << 20)):
+        assert lib.uq_quicfl_workspace_bytes(n, d, ctypes.byref(sz)) == 0
+        base[(n, d)] = sz.value
+        assert sz.value >= n * d * 5                       # rotated vectors + h at least
+    # one 2^20 message: 2 streams x 33 blocks + >= 1 run's 3 x 4 partial windows more than its vectors
+    assert base[(1, 1 << 20)] - (1 << 20) * 5 >= (2 * 33 * 624 + 12 * 624) * 4
+    assert lib.uq_quicfl_receive_workspace_bytes(1, 2048, ctypes.byref(sz)) == 0 and sz.value == 0
+    assert lib.uq_quicfl_receive_workspace_bytes(1, 1 << 20, ctypes.byref(sz)) == 0 and sz.value >= 33 * 624 * 4
+    assert lib.uq_quicfl_receive_workspace_bytes(1024, 1 << 20, ctypes.byref(sz)) == 0 and sz.value == 0
+    assert lib.uq_quicfl_receive_workspace_bytes(-1, 16, ctypes.byref(sz)) < 0
+    assert lib.uq_rht_sign_bits(None, -1, 16, None, None) < 0
+    assert lib.uq_rht_sign_bits(None, 0, 16, None, None) == 0        # nothing to pack

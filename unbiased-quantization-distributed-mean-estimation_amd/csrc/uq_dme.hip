@@ -3570,6 +3570,18 @@ static int qfl_jump_polys(const QflJumpPlan& p, bool a_only, const uint32_t** ou
     if ((p.R > 1 && uq_mtpoly_progression(p.L - 1, p.L, p.R - 1, h.data() + kMtN)) ||
         (!a_only && uq_mtpoly_progression(p.qL - 1, p.L, p.R, h.data() + (size_t)p.R * kMtN)))
         return fail(UQ_E_INVALID, "MT19937 jump polynomials unavailable");
+    if (cache.size() >= 64) {                // bounded: many layouts (sizes) in one process; this
+        rc = hip_check(hipDeviceSynchronize(), "sync before freeing jump polynomials");   // device's
+        if (rc) return rc;                   // entries are idle after the synchronisation
+        for (auto it2 = cache.begin(); it2 != cache.end();) {
+            if (std::get<0>(it2->first) == dev) {
+                (void)hipFree(it2->second);
+                it2 = cache.erase(it2);
+            } else {
+                ++it2;
+            }
+        }
+    }
     uint32_t* d = nullptr;
     rc = hip_check(hipMalloc(&d, h.size() * sizeof(uint32_t)), "hipMalloc jump polynomials");
     if (rc) return rc;
