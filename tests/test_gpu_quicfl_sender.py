@@ -322,3 +322,46 @@ def test_packed_table_same_bits(fx, monkeypatch):
     tX[0, 0] = 0.5
     odd = uqdme.QuicFLSender(tables={1: (tX, tp, DATA[1])})
     assert odd.table_packed(1, torch.device("cuda", 0)) is None
+
+
+@pytest.mark.parametrize("n,dim", [(1, 4096), (1, 5000), (3, 9000), (17, 1 << 15), (128, 1 << 14), (2, (1 << 21) + 7),
+                                   (1, 3 << 18), (5, 1 << 20)])
+def test_jump_path_equals_one_wave_across_shapes(fx, n, dim):
+    """The jump path (its run count and length come from a cost model of (n, D), so every shape
+    cuts the streams differently) against the one-wave kernel (test hook 2) on the same
+    messages: X, mask, exact values, scales, generator end states; px states off the block
+    edge and fresh px seeds."""
+    import uqdme_amd.quicfl as q
+    from uqdme_amd._lib import load
+    meta, z, rmeta, rz = fx
+    snd = senders(meta)["pub"]
+    rng = np.random.default_rng(n * 1000 + dim % 997)
+    x = (rng.standard_normal((n, dim)) * rng.uniform(0.5, 4, (n, 1))).astype(np.float32)
+    x[0, 1] = 1e4                                                 # an exact coordinate at least
+    seeds = [int(s) for s in rng.integers(0, 100, n)]
+    rots = [int(s) for s in rng.integers(0, 100, n)]
+    g = torch.Generator()
+    states = np.empty((n, 626), np.uint32)
+    for j in range(n):
+        g.manual_seed(int(rng.integers(0, 2 ** 31)))
+        pre = int(rng.integers(0, 1300))
+        if pre:
+            torch.rand(pre, generator=g)
+        states[j] = q.generator_words(g)[1]
+    for nbits in (1, 3):
+        for kw in ({"px_states": states}, {"px_seeds": [int(s) for s in rng.integers(0, 2 ** 31, n)]}):
+            out = {}
+            for hooks in (0, 2):
+                prev = load().uq_test_set_quicfl_hooks(hooks)
+                try:
+                    out[hooks] = q.quicfl_compress(torch.from_numpy(x), nbits, seeds, rots, sender=snd,
+                                                   _state_out=True, **kw)
+                finally:
+                    load().uq_test_set_quicfl_hooks(prev)
+            (a, sa), (b, sb) = out[0], out[2]
+            assert torch.equal(a.X, b.X) and torch.equal(a.exact_mask, b.exact_mask), (nbits, kw.keys())
+            assert torch.equal(a.exact_count, b.exact_count) and torch.equal(a.scale, b.scale)
+            for j in range(n):
+                c = int(a.exact_count[j])
+                assert torch.equal(a.exact_vals[j, :c], b.exact_vals[j, :c]), j
+            assert (sa is None and sb is None) or np.array_equal(sa, sb)
