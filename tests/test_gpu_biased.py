@@ -229,6 +229,39 @@ def test_torch_ties_batch_multiworkgroup_levels(uq):
     uq.check_status()
 
 
+def test_torch_ties_gaussian_ambiguous_fine_clients(uq):
+    """Gaussian rows whose threshold key repeats (~2 % of rows at d = 2^18, picked with the
+    oracle): their threshold bin is small, so KB6f writes the rows, KB7a replays the ties and
+    KB6t patches the selected bin coordinates (no full-row rewrite).  A 40-client batch (KB7a),
+    every client bit-exact against the oracle."""
+    rng = np.random.default_rng(91)
+    d = 1 << 18
+    m = rate_to_m(1, d)
+    amb_rows = []
+    for _ in range(600):
+        x = rng.standard_normal(d).astype(f32)
+        if C.biased_quantize(x, m, 1, 0)[3]:
+            amb_rows.append(x)
+            if len(amb_rows) == 6:
+                break
+    assert len(amb_rows) >= 3
+    n = 40
+    x = rng.standard_normal((n, d)).astype(f32)
+    slots = [1, 7, 8, 20, 33, 39][:len(amb_rows)]
+    for j, r in zip(slots, amb_rows):
+        x[j] = r
+    out, info = uq.biased_quantize(torch.as_tensor(x).cuda(), m=m, torch_threads=1, ties="torch", return_info=True)
+    out = out.cpu().numpy()
+    info = info.cpu().numpy()
+    for j in range(n):
+        exp, _, D, A = C.biased_quantize(x[j], m, 1, 0)
+        assert info[j, 0] == D and bool(info[j, 1] & 1) == A, j
+        assert G.bits_equal(out[j], exp), j
+        if j in slots:
+            assert A, j
+    uq.check_status()
+
+
 def test_torch_ties_many_listed_clients_stop_levels_early(uq):
     """>= 128 listed clients: KB7a's levels stop at ranges of 65536 and the 1024-thread
     replays resume those slots after the join (plus the list entries beyond the 256 slots).

@@ -463,21 +463,22 @@ __device__ __forceinline__ float torch_signf(float v) {
 // KB6: apply the selection and dequantize.  Selected = key > tau, or key == tau and
 // (all ties are selected | rank among ties in index order < need | marked by KB7).
 template <bool VEC4>
-__global__ void __launch_bounds__(256)
-rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, const float* __restrict__ l1,
-                  float fm, const RezState* __restrict__ st, const uint32_t* __restrict__ tilecnt, int32_t tiles,
-                  const uint32_t* __restrict__ tie_bits, int part) {
-    const int64_t vec = blockIdx.y;
+__device__ __forceinline__ void rez_output_tile(const float* __restrict__ x, float* __restrict__ out, int64_t d,
+                                                const float* __restrict__ l1, float fm, const RezState* __restrict__ st,
+                                                const uint32_t* __restrict__ tilecnt, int32_t tiles,
+                                                const uint32_t* __restrict__ tie_bits, int part, int64_t vec) {
     const RezState s = st[vec];
     const bool on = s.kleft != 0;
     const bool amb = on && (s.flags & kRezAmbiguous);
     // part 0: every client; 1: clients without a tie at the threshold (run while KB7 replays
     // the others on a side stream); 2: only those with one (after KB7).  Fine clients without
-    // a tie were written by KB6f + KB6p (with one, this kernel rewrites them: index-order or
-    // replayed tie ranks need the whole row)
+    // a tie were written by KB6f + KB6p; with a replayed tie KB6t patches them; with an
+    // index-order tie (a failed replay, or the lowest-index rule) this kernel rewrites them:
+    // the ranks need the whole row
     if ((part == 1 && amb) || (part == 2 && !amb)) return;
     if (on && (s.flags & kRezFine) && !amb) return;
     const bool replay = amb && (s.flags & kRezTorchTies);
+    if (replay && (s.flags & kRezFine)) return;
     const bool up = s.delta > 0;
     const float L = l1[vec];
     const DivPlan dp = div_plan(L);
@@ -605,6 +606,22 @@ rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t 
     }
 }
 
+// list: null -- client blockIdx.y; else the clients list[1 ..= list[0]] (KB7's, part 2), the
+// grid's y dimension striding over them, so the launch is not n x tiles mostly idle workgroups
+template <bool VEC4>
+__global__ void __launch_bounds__(256)
+rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, const float* __restrict__ l1,
+                  float fm, const RezState* __restrict__ st, const uint32_t* __restrict__ tilecnt, int32_t tiles,
+                  const uint32_t* __restrict__ tie_bits, int part, const uint32_t* __restrict__ list) {
+    if (!list) {
+        rez_output_tile<VEC4>(x, out, d, l1, fm, st, tilecnt, tiles, tie_bits, part, blockIdx.y);
+        return;
+    }
+    const uint32_t nl = list[0];
+    for (uint32_t li = blockIdx.y; li < nl; li += gridDim.y)
+        rez_output_tile<VEC4>(x, out, d, l1, fm, st, tilecnt, tiles, tie_bits, part, list[1 + li]);
+}
+
 // KB6f: fine clients (kRezFine) -- out for every coordinate with the selection decided by the
 // fine bin (above the threshold's bin: selected; below: not); the threshold bin's coordinates
 // are written unselected and listed as (index, key) pairs for KB4d: staged in LDS by LDS
@@ -708,6 +725,7 @@ rez_output_fine_kernel(const float* __restrict__ x, float* __restrict__ out, int
 // KB6p: the listed coordinates of a fine client without a threshold tie that are selected
 // (key >= the threshold key: every tie is selected) get k'' = k' -+ 1.
 constexpr int kPatchBlocks = 4;
+constexpr int64_t kListedGridY = 64;      // list-strided launches after KB7: y extent
 __global__ void __launch_bounds__(256)
 rez_fine_patch_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, const float* __restrict__ l1,
                       float fm, const RezState* __restrict__ st, const uint2* __restrict__ cand,
@@ -729,6 +747,41 @@ rez_fine_patch_kernel(const float* __restrict__ x, float* __restrict__ out, int6
         float kp;
         (void)rez_elem(v, dp, fm, up, kp);
         out[vec * d + c.x] = (L * torch_signf(v)) * div1(kp + adj, dpm);     // AS:687 with k''
+    }
+}
+
+// KB6t: the fine clients whose threshold ties KB7 replayed.  KB6f wrote their rows with the
+// threshold's bin unselected and listed the bin; the listed coordinates that are selected (key
+// above the threshold key, or equal to it with KB7's bit) get k'' = k' -+ 1.  Grid (blocks,
+// <= list length): y strides over KB7's client list.
+__global__ void __launch_bounds__(256)
+rez_tie_patch_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t d, const float* __restrict__ l1,
+                     float fm, const RezState* __restrict__ st, const uint2* __restrict__ cand,
+                     const uint32_t* __restrict__ cand_n, uint32_t capf, const uint32_t* __restrict__ tie_bits,
+                     const uint32_t* __restrict__ list) {
+    const uint32_t nl = list[0];
+    for (uint32_t li = blockIdx.y; li < nl; li += gridDim.y) {
+        const int64_t vec = list[1 + li];
+        const RezState s = st[vec];
+        constexpr int32_t want = kRezFine | kRezAmbiguous | kRezTorchTies;
+        if (s.kleft == 0 || (s.flags & want) != want) continue;
+        const uint32_t nc = std::min(cand_n[vec], capf);
+        const uint2* cv = cand + (size_t)vec * capf;
+        const uint32_t* bits = tie_bits + vec * ((d + 31) / 32);
+        const bool up = s.delta > 0;
+        const float L = l1[vec];
+        const DivPlan dp = div_plan(L);
+        const DivPlan dpm = div_plan_m(fm);
+        const float adj = up ? -1.f : 1.f;
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nc; i += gridDim.x * 256) {
+            const uint2 c = cv[i];
+            if (c.y < s.prefix) continue;
+            if (c.y == s.prefix && !((bits[c.x >> 5] >> (c.x & 31)) & 1u)) continue;
+            const float v = x[vec * d + c.x];
+            float kp;
+            (void)rez_elem(v, dp, fm, up, kp);
+            out[vec * d + c.x] = (L * torch_signf(v)) * div1(kp + adj, dpm);     // AS:687 with k''
+        }
     }
 }
 

@@ -403,9 +403,19 @@ struct TieLevelState {
 __global__ void __launch_bounds__(256)
 kt_fill_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
                const RezState* __restrict__ st, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ list,
-               TieLevelState* __restrict__ tls) {
+               TieLevelState* __restrict__ tls, uint32_t* __restrict__ tie_bits) {
     const int64_t a = blockIdx.y;
     const uint32_t nlist = list[0];
+    {   // the tie bits of every listed client (no other row is read): cleared here, off the
+        // main stream, instead of a memset of all n rows before the fork
+        const int64_t words = (d + 31) / 32;
+        const int64_t wseg = (words + gridDim.x - 1) / gridDim.x;
+        const int64_t w0 = (int64_t)blockIdx.x * wseg, w1 = min(words, w0 + wseg);
+        for (int64_t e = a; e < (int64_t)nlist; e += gridDim.y) {
+            uint32_t* row = tie_bits + (int64_t)list[1 + e] * words;
+            for (int64_t i = w0 + threadIdx.x; i < w1; i += 256) row[i] = 0u;
+        }
+    }
     if (a >= (int64_t)nlist) {                         // unused slot: nothing stale may run
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             tls[a].filled = 0;

@@ -2657,10 +2657,14 @@ int side_stream(SideStream** out) {
 // *tls_out is set: the caller then runs launch_torch_ties_rest (part 2: heap-path clients
 // and list entries beyond the slots) once the output kernel on its own stream is done.
 // KB7's client list and cleared tie bits (before launch_torch_ties and the tie counts).
+// clear_bits: without KB7a (which clears the listed clients' rows in kt_fill) every row here.
 int torch_ties_prepare(int64_t n, int64_t d, RezState* state, uint32_t* bits, char* wsb, const BiasedLayout& w,
-                       hipStream_t st) {
-    int rc = hip_check(hipMemsetAsync(bits, 0, (size_t)n * ((d + 31) / 32) * sizeof(uint32_t), st), "memset tie bits");
-    if (rc) return rc;
+                       hipStream_t st, bool clear_bits) {
+    if (clear_bits) {
+        const int rc = hip_check(hipMemsetAsync(bits, 0, (size_t)n * ((d + 31) / 32) * sizeof(uint32_t), st),
+                                 "memset tie bits");
+        if (rc) return rc;
+    }
     hipLaunchKernelGGL(rez_tie_list_kernel, dim3(1), dim3(1024), 0, st, state, n, (uint32_t*)(wsb + w.list_off));
     return hip_check(hipGetLastError(), "rez_tie_list_kernel launch");
 }
@@ -2743,7 +2747,8 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     TieLevelState* tls = (TieLevelState*)(wsb + w.tls_off);
     uint32_t* cnt = (uint32_t*)(wsb + w.tcnt2_off);
     const unsigned S = (unsigned)w.slots;
-    hipLaunchKernelGGL(kt_fill_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, x, d, l1, fm, state, qbuf, list, tls);
+    hipLaunchKernelGGL(kt_fill_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, x, d, l1, fm, state, qbuf, list, tls,
+                       bits);
     if ((rc = hip_check(hipGetLastError(), "kt_fill_kernel launch"))) return rc;
     // a level keeps the side of the cut that holds nth (measured: ranges reach kTieLevelMin
     // after ~8 levels from 2^20), so enough levels for 0.6 per level, plus two; an idle level
@@ -3396,11 +3401,29 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     auto output = [&](hipStream_t os, int part) {
         if (vec4)
             hipLaunchKernelGGL(rez_output_kernel<true>, tgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
-                               w.tiles, bits, part);
+                               w.tiles, bits, part, (const uint32_t*)nullptr);
         else
             hipLaunchKernelGGL(rez_output_kernel<false>, tgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
-                               w.tiles, bits, part);
+                               w.tiles, bits, part, (const uint32_t*)nullptr);
         return hip_check(hipGetLastError(), "rez_output_kernel launch");
+    };
+    // after KB7: its listed clients only (a list-strided grid, not n x tiles workgroups that
+    // mostly exit): full rows for index-order ranks and full clients, KB6t's patch of the
+    // listed threshold bin for the replayed fine clients
+    auto output_listed = [&](hipStream_t os) {
+        const uint32_t* list = (const uint32_t*)(wsb + w.list_off);
+        const dim3 lgrid((unsigned)w.tiles, (unsigned)std::min<int64_t>(n, kListedGridY));
+        if (vec4)
+            hipLaunchKernelGGL(rez_output_kernel<true>, lgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
+                               w.tiles, bits, 2, list);
+        else
+            hipLaunchKernelGGL(rez_output_kernel<false>, lgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
+                               w.tiles, bits, 2, list);
+        int orc = hip_check(hipGetLastError(), "rez_output_kernel launch");
+        if (orc) return orc;
+        hipLaunchKernelGGL(rez_tie_patch_kernel, dim3(kPatchBlocks, (unsigned)std::min<int64_t>(n, kListedGridY)),
+                           dim3(256), 0, os, x, out, d, l1buf, fm, state, fcand, cand_n, w.capf, bits, list);
+        return hip_check(hipGetLastError(), "rez_tie_patch_kernel launch");
     };
     auto tiecount = [&](hipStream_t ts, const uint32_t* list) {
         // index-order tie ranks (ambiguous clients that KB7 does not replay)
@@ -3419,15 +3442,15 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         // UQ_TIES_HOST_CHECK (synchronous few-client callers): one stream; after the tie list
         // is built, wait for it and skip the replay chain -- KB7a's ~65 level launches --
         // when no client is listed; then every client's output in one launch
-        rc = torch_ties_prepare(n, d, state, bits, wsb, w, st);
+        // (no tie counts: every ambiguous client is listed and replayed; a failed replay
+        // counts its own tiles)
+        rc = torch_ties_prepare(n, d, state, bits, wsb, w, st, false);
         if (rc) return rc;
         SideStream* sb = nullptr;
         rc = side_stream(&sb);                            // (its pinned word)
         if (rc) return rc;
         rc = hip_check(hipMemcpyAsync(sb->count, wsb + w.list_off, sizeof(uint32_t), hipMemcpyDeviceToHost, st),
                        "copy tie list length");
-        if (rc) return rc;
-        rc = tiecount(st, (const uint32_t*)(wsb + w.list_off));
         if (rc) return rc;
         rc = hip_check(hipStreamSynchronize(st), "sync");
         if (rc) return rc;
@@ -3436,8 +3459,9 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
             rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, st, &tls);
             if (rc) return rc;
             if (tls && (rc = launch_torch_ties_rest(x, d, l1buf, fm, state, bits, wsb, w, tls, st))) return rc;
+            if ((rc = output_listed(st))) return rc;
         }
-        rc = output(st, 0);
+        rc = output(st, 1);
         if (rc) return rc;
     } else if (tie_policy == UQ_TIES_TORCH) {
         // fork: KB7 (few workgroups, latency-bound) on the side stream while KB6 writes the
@@ -3445,20 +3469,18 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         SideStream* sb = nullptr;
         rc = side_stream(&sb);
         if (rc) return rc;
-        // the tie list (and cleared tie bits) before the fork: both streams read it
-        rc = torch_ties_prepare(n, d, state, bits, wsb, w, st);
+        // the tie list (and, without KB7a, cleared tie bits) before the fork: both streams read it
+        rc = torch_ties_prepare(n, d, state, bits, wsb, w, st, !kb7a);
         if (rc) return rc;
         rc = hip_check(hipEventRecord(sb->fork, st), "record fork");
         if (rc) return rc;
         rc = hip_check(hipStreamWaitEvent(sb->s, sb->fork, 0), "wait fork");
         if (rc) return rc;
         // KB6 for the clients without a tie is enqueued first: the side chain below is ~60
-        // short launches, and the GPU must not idle while the host issues them; the tie counts
-        // of unlisted clients (independent of the replays) follow it on this stream, off the
-        // replay chain's critical path (they were 62 us of early-exit workgroups on it)
+        // short launches, and the GPU must not idle while the host issues them.  No tie counts:
+        // every ambiguous client is listed and replayed (a failed replay counts its own tiles;
+        // the launch was 66 us of early-exit workgroups beside the chain)
         rc = output(st, 1);
-        if (rc) return rc;
-        rc = tiecount(st, (const uint32_t*)(wsb + w.list_off));
         if (rc) return rc;
         const TieLevelState* tls = nullptr;
         rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls);
@@ -3471,7 +3493,7 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
             rc = launch_torch_ties_rest(x, d, l1buf, fm, state, bits, wsb, w, tls, st);
             if (rc) return rc;
         }
-        rc = output(st, 2);
+        rc = output_listed(st);
         if (rc) return rc;
     } else {
         rc = tiecount(st, nullptr);
