@@ -26,19 +26,20 @@
 
 constexpr int kTieSlots = 256;       // workgroups (and scratch slots) of KB7: one per CU
 constexpr int kTieThreads = 1024;    // 16 waves per client (full replays)
-constexpr int kTieThreadsLds = 256;  // LDS tails after KB7a: small enough to dispatch beside KB6
 constexpr int kTieWaves = kTieThreads / kWave;
 constexpr int kTieU = 8;             // independent loads in flight per lane
-constexpr int kTieLdsPairs = 4096;   // ranges this short finish in LDS
+constexpr int kTieLdsPairs = 8192;   // ranges this short finish in LDS (96 KB with the stop lists)
+constexpr int kTieWaveMax = 1024;    // ... the last levels, below this, in one wave (no barriers)
 
 #define TT_DECL() do {} while (0)
 #define TT_T0() do {} while (0)
 #define TT_ACC(k) do {} while (0)
+#define TT_CNT(k) do {} while (0)
 
 struct TieShared {
     uint32_t wl[kTieWaves], wr[kTieWaves];   // per-wave stop counts of one partition
     int64_t first, last;
-    int depth;
+    int depth, ret;
     uint32_t piv;
     uint32_t marked;
 };
@@ -56,11 +57,36 @@ struct Queue {
         K[a] = K[b]; I[a] = I[b];
         K[b] = ka; I[b] = ia;
     }
+    __device__ uint4 key4(int64_t q) const { return *reinterpret_cast<const uint4*>(K + q); }   // q % 4 == 0
+};
+
+// The same queue in LDS, through address-space-3 pointers: ds_read / ds_write (a generic
+// pointer to LDS compiles to flat accesses, several times their latency).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+struct LdsQueue {
+    lds_u32* K;
+    lds_u32* I;
+    __device__ uint32_t key(int64_t i) const { return K[i]; }
+    __device__ uint64_t get(int64_t i) const { return ((uint64_t)K[i] << 32) | I[i]; }
+    __device__ void set(int64_t i, uint64_t v) const { K[i] = (uint32_t)(v >> 32); I[i] = (uint32_t)v; }
+    __device__ void swap(int64_t a, int64_t b) const {
+        const uint32_t ka = K[a], ia = I[a];
+        K[a] = K[b]; I[a] = I[b];
+        K[b] = ka; I[b] = ia;
+    }
+    __device__ uint4 key4(int64_t q) const {                 // q % 4 == 0: one ds_read_b128
+        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) const u32x4v lds_q;
+        const u32x4v v = *(lds_q*)(K + q);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
 };
 
 __device__ __forceinline__ uint32_t pkey(uint64_t p) { return (uint32_t)(p >> 32); }
 
-__device__ void tt_adjust_heap(const Queue& A, int64_t f, int64_t hole, int64_t len, uint64_t value) {
+template <class Q>
+__device__ void tt_adjust_heap(const Q& A, int64_t f, int64_t hole, int64_t len, uint64_t value) {
     const int64_t top = hole;
     int64_t second = hole;
     while (second < (len - 1) / 2) {
@@ -83,7 +109,8 @@ __device__ void tt_adjust_heap(const Queue& A, int64_t f, int64_t hole, int64_t 
     A.set(f + hole, value);
 }
 
-__device__ void tt_make_heap(const Queue& A, int64_t f, int64_t len) {
+template <class Q>
+__device__ void tt_make_heap(const Q& A, int64_t f, int64_t len) {
     if (len < 2) return;
     for (int64_t parent = (len - 2) / 2;; --parent) {
         tt_adjust_heap(A, f, parent, len, A.get(f + parent));
@@ -92,7 +119,8 @@ __device__ void tt_make_heap(const Queue& A, int64_t f, int64_t len) {
 }
 
 // heap_select(A + f, A + m, A + l) by one wave (lanes 0..63 of the caller).
-__device__ void tt_heap_select_wave(const Queue& A, int64_t f, int64_t m, int64_t l, int lane) {
+template <class Q>
+__device__ void tt_heap_select_wave(const Q& A, int64_t f, int64_t m, int64_t l, int lane) {
     if (lane == 0) tt_make_heap(A, f, m - f);
     uint32_t top = __shfl(lane == 0 ? A.key(f) : 0u, 0, kWave);
     for (int64_t base = m; base < l; base += kWave) {
@@ -116,7 +144,8 @@ __device__ void tt_heap_select_wave(const Queue& A, int64_t f, int64_t m, int64_
     }
 }
 
-__device__ void tt_move_median_to_first(const Queue& A, int64_t r, int64_t a, int64_t b, int64_t c) {
+template <class Q>
+__device__ void tt_move_median_to_first(const Q& A, int64_t r, int64_t a, int64_t b, int64_t c) {
     const uint32_t ka = A.key(a), kb = A.key(b), kc = A.key(c);
     if (ka > kb) {
         if (kb > kc) A.swap(r, b);
@@ -127,7 +156,8 @@ __device__ void tt_move_median_to_first(const Queue& A, int64_t r, int64_t a, in
     else A.swap(r, b);
 }
 
-__device__ void tt_insertion_sort(const Queue& A, int64_t f, int64_t l) {
+template <class Q>
+__device__ void tt_insertion_sort(const Q& A, int64_t f, int64_t l) {
     if (f == l) return;
     for (int64_t i = f + 1; i != l; ++i) {
         const uint64_t v = A.get(i);
@@ -153,8 +183,8 @@ __device__ __forceinline__ int floor_log2_i64(int64_t n) {
 
 // Stops of [s0, s1) (one wave's segment) in index order: FN(i, left, right) per element,
 // lanes own i = b + u*64 + lane, kTieU loads in flight.
-template <class FN>
-__device__ __forceinline__ void tt_scan_segment(const Queue& A, int64_t first, int64_t s0, int64_t s1, uint32_t piv,
+template <class Q, class FN>
+__device__ __forceinline__ void tt_scan_segment(const Q& A, int64_t first, int64_t s0, int64_t s1, uint32_t piv,
                                                 int lane, FN&& fn) {
     for (int64_t b = s0; b < s1; b += (int64_t)kWave * kTieU) {
         uint32_t k[kTieU];
@@ -177,8 +207,8 @@ __device__ __forceinline__ void tt_scan_segment(const Queue& A, int64_t first, i
 // relative to the queue view; positions listed as PosT).  Each wave lists the stops of
 // its contiguous segment: one counting pass, a 16-entry prefix, one listing pass.
 // Returns the cut, or -1 on an internal inconsistency.
-template <typename PosT, int NT>
-__device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t first, int64_t last,
+template <class Q, typename PosT, typename PosPtr, int NT>
+__device__ int64_t tt_partition(const Q& A, PosPtr Lpos, PosPtr Rpos, int64_t first, int64_t last,
                                 uint32_t piv, TieShared& sh) {
     TT_DECL();
     TT_T0();
@@ -199,7 +229,7 @@ __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t 
 #pragma unroll
             for (int u = 0; u < kCU; ++u) {
                 const int64_t q = b + 4 * ((int64_t)u * kWave + lane);
-                kv[u] = q < s1 ? *reinterpret_cast<const uint4*>(A.K + q) : make_uint4(0, 0, 0, 0);
+                kv[u] = q < s1 ? A.key4(q) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < kCU; ++u) {
@@ -294,8 +324,8 @@ __device__ int64_t tt_partition(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t 
 // introselect's main loop on the queue view (element i of the vector at view index i - o)
 // while the range is longer than `stop`.  Returns 0 (range now <= stop), 1 (finished
 // through the heap fallback) or -1 (internal inconsistency).
-template <typename PosT, int NT>
-__device__ int tt_select_loop(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t o, int64_t nth, int64_t stop,
+template <class Q, typename PosT, typename PosPtr, int NT>
+__device__ int tt_select_loop(const Q& A, PosPtr Lpos, PosPtr Rpos, int64_t o, int64_t nth, int64_t stop,
                               TieShared& sh) {
     TT_DECL();
     const int tid = threadIdx.x;
@@ -319,7 +349,7 @@ __device__ int tt_select_loop(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t o,
         }
         __syncthreads();
         TT_ACC(4);
-        const int64_t cut = tt_partition<PosT, NT>(A, Lpos, Rpos, first, last, sh.piv, sh);
+        const int64_t cut = tt_partition<Q, PosT, PosPtr, NT>(A, Lpos, Rpos, first, last, sh.piv, sh);
         if (cut < 0) return -1;
         if (tid == 0) {
             if (cut + o <= nth) sh.first = cut + o; else sh.last = cut + o;
@@ -327,6 +357,122 @@ __device__ int tt_select_loop(const Queue& A, PosT* Lpos, PosT* Rpos, int64_t o,
         }
         __syncthreads();
     }
+}
+
+// LDS operations of one wave are performed in order; this keeps the compiler from moving
+// them across the points where lanes read what other lanes wrote
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// introselect's loop on the LDS window (view index = vector index - o) by ONE wave, down to
+// ranges of 3 (tt_select_loop's moves, without a barrier per step: a workgroup-wide
+// partition of a few thousand keys is a dozen barriers and serial lane-0 steps, the wave's
+// one ordered pass appends its stops directly).  first / last / depth in and out (vector
+// indices).  Returns 0 (range <= 3), 1 (finished through the heap fallback), -1 (internal
+// inconsistency).
+__device__ int tt_select_wave(const LdsQueue& A, lds_u16* lL, lds_u16* lR, int64_t o, int64_t nth, int64_t& first_io,
+                              int64_t& last_io, int& depth_io, int lane) {
+    constexpr int kU = 4;                                   // keys in flight per lane
+    int32_t first = (int32_t)(first_io - o), last = (int32_t)(last_io - o);
+    const int32_t nv = (int32_t)(nth - o);
+    int depth = depth_io;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int ret = 0;
+    TT_DECL();
+    TT_T0();
+    for (;;) {
+        if (last - first <= 3) break;
+        TT_CNT(11);
+        if (depth == 0) {                                   // heap_select(first, nth+1, last)
+            tt_heap_select_wave(A, first, nv + 1, last, lane);
+            wave_lds_sync();
+            if (lane == 0) A.swap(first, nv);
+            wave_lds_sync();
+            ret = 1;
+            break;
+        }
+        if (lane == 0) tt_move_median_to_first(A, first, first + 1, first + (last - first) / 2, last - 1);
+        wave_lds_sync();
+        const uint32_t piv = A.key(first);
+        uint32_t nL = 0, nR = 0;
+        TT_ACC(15);
+        for (int32_t b = first; b < last; b += kWave * kU) {        // stops in index order
+            uint32_t k[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int32_t i = b + u * kWave + lane;
+                k[u] = i < last ? A.key(i) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int32_t i = b + u * kWave + lane;
+                const bool in = i < last;
+                const bool lf = in && i > first && k[u] <= piv;     // !comp(A[i], pivot)
+                const bool rf = in && k[u] >= piv;                  // !comp(pivot, A[i])
+                const uint64_t ml = __ballot(lf), mr = __ballot(rf);
+                if (lf) lL[nL + (uint32_t)__popcll(ml & lt)] = (uint16_t)i;
+                if (rf) lR[nR + (uint32_t)__popcll(mr & lt)] = (uint16_t)i;
+                nL += (uint32_t)__popcll(ml);
+                nR += (uint32_t)__popcll(mr);
+            }
+        }
+        wave_lds_sync();
+        TT_ACC(12);
+        int32_t lo = 0, hi = (int32_t)(nL < nR ? nL : nR);  // J: L_J < R_J holds for a prefix
+        while (lo < hi) {
+            const int32_t step = (hi - lo + kWave - 1) / kWave;
+            const int32_t cand = lo + (lane + 1) * step;
+            const bool f = cand <= hi && (int32_t)lL[cand - 1] < (int32_t)lR[nR - cand];
+            const int c = __popcll(__ballot(f));
+            if (c == 0) {
+                hi = lo + step - 1;
+            } else {
+                lo = lo + c * step;
+                hi = min(hi, lo + step - 1);
+            }
+        }
+        const int32_t J = lo;
+        int32_t cut = INT32_MAX;
+        if (J < (int32_t)nL) cut = lL[J];
+        if (J > 0) cut = min(cut, (int32_t)lR[nR - J]);
+        TT_ACC(13);
+        for (int32_t j0 = 0; j0 < J; j0 += kWave * kU) {              // J disjoint swaps
+            int32_t pa[kU], pb[kU];
+            uint32_t ka[kU], kb[kU], ia[kU], ib[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int32_t j = j0 + u * kWave + lane;
+                pa[u] = j < J ? (int32_t)lL[j] : -1;
+                pb[u] = j < J ? (int32_t)lR[nR - 1 - j] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (pa[u] >= 0) {
+                    ka[u] = A.K[pa[u]]; ia[u] = A.I[pa[u]];
+                    kb[u] = A.K[pb[u]]; ib[u] = A.I[pb[u]];
+                }
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (pa[u] >= 0) {
+                    A.K[pa[u]] = kb[u]; A.I[pa[u]] = ib[u];
+                    A.K[pb[u]] = ka[u]; A.I[pb[u]] = ia[u];
+                }
+        }
+        wave_lds_sync();
+        TT_ACC(14);
+        if (cut <= first || cut >= last) {
+            ret = -1;
+            break;
+        }
+        if (cut <= nv) first = cut; else last = cut;
+        --depth;
+    }
+    first_io = first + o;
+    last_io = last + o;
+    depth_io = depth;
+    return ret;
 }
 
 // std::nth_element(A, A + nth, A + d) by the whole workgroup (false on an inconsistency),
@@ -344,7 +490,7 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
         sh.depth = depth0;
     }
     __syncthreads();
-    int r = tt_select_loop<uint32_t, NT>(A, Lpos, Rpos, 0, nth, kTieLdsPairs, sh);
+    int r = tt_select_loop<Queue, uint32_t, uint32_t*, NT>(A, Lpos, Rpos, 0, nth, kTieLdsPairs, sh);
     if (r < 0) return false;
     TT_T0();
     if (r == 0 && sh.last - sh.first > 3) {                // finish the short range in LDS
@@ -354,9 +500,27 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
             lI[i] = A.I[f0 + i];
         }
         __syncthreads();
-        const Queue L{lK, lI};
-        r = tt_select_loop<uint16_t, NT>(L, lL, lR, f0, nth, 3, sh);
+        TT_ACC(8);
+        const LdsQueue L{(lds_u32*)lK, (lds_u32*)lI};
+        // the whole workgroup while the range is long, one wave below kTieWaveMax
+        r = tt_select_loop<LdsQueue, uint16_t, lds_u16*, NT>(L, (lds_u16*)lL, (lds_u16*)lR, f0, nth, kTieWaveMax, sh);
+        __syncthreads();                                     // every wave has read sh's range
+        TT_ACC(7);
+        if (r == 0 && tid < kWave) {
+            int64_t f = sh.first, l = sh.last;
+            int dep = sh.depth;
+            const int rw = tt_select_wave(L, (lds_u16*)lL, (lds_u16*)lR, f0, nth, f, l, dep, tid);
+            if (tid == 0) {
+                sh.first = f;
+                sh.last = l;
+                sh.depth = dep;
+                sh.ret = rw;
+            }
+        }
+        if (r != 0 && tid == 0) sh.ret = r;
         __syncthreads();
+        TT_ACC(9);
+        r = sh.ret;
         for (int64_t i = tid; i < len; i += NT) {
             A.K[f0 + i] = lK[i];
             A.I[f0 + i] = lI[i];
@@ -367,6 +531,7 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
     TT_ACC(5);
     if (r == 0 && tid == 0) tt_insertion_sort(A, sh.first, sh.last);
     __syncthreads();
+    TT_ACC(10);
     return true;
 }
 
@@ -379,17 +544,21 @@ __device__ bool tt_introselect(const Queue& A, uint32_t* Lpos, uint32_t* Rpos, i
 // scans), so rez_ties_kernel resumes from the saved (first, last, depth) with the same
 // queue it would have built itself.  Slot a serves list entry a (a < kTieSlots).
 constexpr int64_t kTieLevelMin = kTieLdsPairs;   // shorter ranges finish in rez_ties_kernel's LDS
-// KB7a's levels stop at ranges of this length; the 256-thread replays beside KB6 (part 1)
-// take it from there (global-memory levels, then the LDS tail): 3 fewer levels of five
-// dependent launches each at d = 2^20, 5.28-5.34 -> 5.16-5.24 ms per torch-tie batch (two
-// boxes, bit-identical; stopping at 65536 gained nothing: profiles/r3f_exp_biased_levels.jsonl)
+// KB7a's levels run while a range is longer than kTieLevelStop, level count ceil(log2(d /
+// stop)) + kTieLevelMargin (median-of-3 pivots halve a range per level on average; an idle
+// level is five dependent ~6 us launches).  The 1024-thread replays (part 1, right after the
+// levels on the side stream) take every slot KB7a resumed from where it stopped: global-memory
+// levels while longer than kTieLdsPairs, then the LDS levels (workgroup-wide, the last ones in
+// one wave).  Stop / margin on one box (ms per C2-sized torch-tie batch, tools/exp/run_r5x.sh,
+// run_r5z.sh): 16384 / 2 4.57, 16384 / 3 4.55, 8192 / 3 4.54, 32768 / 2 4.58, 65536 / 2 4.60.
+// (Round 3 stopped at 2^14 after levels for 0.6 per level + 2 and ran the LDS tails with
+// 256 threads through generic pointers: 4.63 on the same box as this form's 4.59.)
 constexpr int64_t kTieLevelStop = 16384;
+constexpr int kTieLevelMargin = 3;
 constexpr int64_t kTieLevelMinClients = 32;      // KB7a for batches of at least this many clients
 // ... and for any batch of vectors this long: one replay workgroup walking 2^22 keys took
 // ~9 ms (a 6-client batch at d = 2^22 with one ambiguous client), KB7a's idle launches 0.35 ms
 constexpr int64_t kTieLevelBigD = (int64_t)1 << 21;
-constexpr uint32_t kTieManyClients = 128;          // this many listed clients: levels only down to
-constexpr int64_t kTieLevelMinMany = 65536;        //   this range (tie-heavy batches)
 constexpr int kTieSegs = 256;               // segments per partition (one wave each)
 constexpr int kTieFillSegs = 64;            // workgroups per client for the queue fill
 
@@ -464,15 +633,12 @@ kt_fill_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__
 constexpr int kTieGrid = 2048;              // workgroups of the per-level launches (4 waves each)
 __global__ void __launch_bounds__(kTieSlots)
 kt_pivot_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ list,
-                TieLevelState* __restrict__ tls, int slots, uint32_t* __restrict__ alist) {
+                TieLevelState* __restrict__ tls, int slots, uint32_t* __restrict__ alist, int64_t stop) {
     __shared__ uint32_t wc[kTieSlots / 64];
     const int a = threadIdx.x, lane = a & 63, w = a >> 6;
     bool act = false;
     if (a < slots) {
         TieLevelState& t = tls[a];
-        // with many listed clients the 1024-thread replays fill the GPU by themselves: the
-        // levels stop at kTieLevelMinMany and part 2 finishes those slots
-        const int64_t stop = list[0] >= kTieManyClients ? kTieLevelMinMany : kTieLevelStop;
         act = a < (int)list[0] && t.filled && !t.err && t.depth > 0 && t.last - t.first > stop;
         t.active = act ? 1 : 0;
         if (act) {
@@ -809,8 +975,8 @@ __device__ void tt_fallback_tilecounts(const float* __restrict__ xv, int64_t d, 
 }
 
 // NT threads per workgroup.  part 0: every listed client (slots walk the list).  With
-// KB7a's level state `tls`: part 1 finishes the clients KB7a resumed (slot a = list entry a,
-// LDS tails: NT = kTieThreadsLds), part 2 every other listed client.
+// KB7a's level state `tls`: part 1 finishes the clients KB7a resumed (slot a = list entry a),
+// part 2 every other listed client.
 template <int NT>
 __global__ void __launch_bounds__(NT)
 rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
@@ -843,10 +1009,8 @@ rez_ties_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         TT_T0();
         // resumed: KB7a filled this slot's queue and ran introselect's first levels
         const bool resumed = tls && li == blockIdx.x && tls[li].filled;
-        // part 1: resumed slots whose range fits the LDS tail; part 2: everything else
-        // (resumed slots KB7a left longer resume from their saved state in 1024 threads)
-        const bool tail = resumed && (tls[li].err || tls[li].last - tls[li].first <= kTieLevelStop);
-        if ((part == 1 && !tail) || (part == 2 && tail)) continue;
+        // part 1: resumed slots (from KB7a's saved state); part 2: everything else
+        if ((part == 1 && !resumed) || (part == 2 && resumed)) continue;
         // queue[j] = (value, j) (TopKImpl.h); 4 coordinates per lane and load
         const bool xv4 = ((uintptr_t)xv & 15u) == 0;
         for (int64_t i0 = 0; i0 < (resumed ? 0 : d); i0 += (int64_t)NT * 4 * kTieU) {

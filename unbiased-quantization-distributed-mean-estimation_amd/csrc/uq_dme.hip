@@ -2750,18 +2750,30 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     hipLaunchKernelGGL(kt_fill_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, x, d, l1, fm, state, qbuf, list, tls,
                        bits);
     if ((rc = hip_check(hipGetLastError(), "kt_fill_kernel launch"))) return rc;
-    // a level keeps the side of the cut that holds nth (measured: ranges reach kTieLevelMin
-    // after ~8 levels from 2^20), so enough levels for 0.6 per level, plus two; an idle level
-    // costs five ~5 us launches, and a range still longer goes global in rez_ties_kernel
-    int levels = 2;
-    for (double r = (double)d; r > (double)kTieLevelStop; r *= 0.6) ++levels;
+    // a level keeps the side of the cut that holds nth, half the range on average; an idle
+    // level costs five ~6 us launches, and a range still longer continues in part 1's
+    // workgroup (UQDME_TIE_STOP / UQDME_TIE_MARGIN: experiments only)
+    static const int64_t tie_stop = [] {
+        const char* e = std::getenv("UQDME_TIE_STOP");
+        const long long v = e ? std::atoll(e) : 0;
+        return v >= kTieLevelMin ? (int64_t)v : kTieLevelStop;
+    }();
+    static const int tie_margin = [] {
+        const char* e = std::getenv("UQDME_TIE_MARGIN");
+        const int v = e ? std::atoi(e) : -1;
+        return v >= 0 && v <= 8 ? v : kTieLevelMargin;
+    }();
+    int levels = tie_margin;
+    for (int64_t r = d; r > tie_stop; r = (r + 1) / 2) ++levels;
+    levels = std::max(levels, 1);
     uint32_t* alist = (uint32_t*)(wsb + w.alist_off);
     // the per-level launches take (active slot, segment) items, one per wave: S slots need at
     // most S * kTieSegs / 4 workgroups (a one-client call launched 2048, 1984 of them idle)
     const unsigned lgrid = (unsigned)std::min<int64_t>(kTieGrid, (int64_t)S * kTieSegs / 4);
     auto levels_on = [&](hipStream_t ls) {
         for (int lv = 0; lv < levels; ++lv) {
-            hipLaunchKernelGGL(kt_pivot_kernel, dim3(1), dim3(kTieSlots), 0, ls, d, qbuf, list, tls, (int)S, alist);
+            hipLaunchKernelGGL(kt_pivot_kernel, dim3(1), dim3(kTieSlots), 0, ls, d, qbuf, list, tls, (int)S, alist,
+                               tie_stop);
             hipLaunchKernelGGL(kt_count_kernel, dim3(lgrid), dim3(256), 0, ls, d, qbuf, tls, cnt, alist);
             hipLaunchKernelGGL(kt_list_kernel, dim3(lgrid), dim3(256), 0, ls, d, qbuf, pos, tls, cnt, alist);
             hipLaunchKernelGGL(kt_jcut_kernel, dim3(S), dim3(kJcutThreads), 0, ls, d, pos, tls, cnt, alist);
@@ -2783,7 +2795,7 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     }
     hipLaunchKernelGGL(kt_mark_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, d, qbuf, list, state, tls, bits);
     if ((rc = hip_check(hipGetLastError(), "kt_mark_kernel launch"))) return rc;
-    hipLaunchKernelGGL(rez_ties_kernel<kTieThreadsLds>, dim3(S), dim3(kTieThreadsLds), 0, st, x, d, l1, fm, state, bits,
+    hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3(S), dim3(kTieThreads), 0, st, x, d, l1, fm, state, bits,
                        qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)tls, 1, (uint32_t*)(wsb + w.tcnt_off),
                        w.tiles, g_force_replay_failure.load());
     *tls_out = tls;
