@@ -560,144 +560,186 @@ constexpr int64_t kTieLevelMinClients = 32;      // KB7a for batches of at least
 // ~9 ms (a 6-client batch at d = 2^22 with one ambiguous client), KB7a's idle launches 0.35 ms
 constexpr int64_t kTieLevelBigD = (int64_t)1 << 21;
 constexpr int kTieSegs = 256;               // segments per partition (one wave each)
-constexpr int kTieFillSegs = 64;            // workgroups per client for the queue fill
+constexpr int kTieMarkSegs = 64;            // workgroups per client for kt_mark
 
 struct TieLevelState {
     int64_t first, last, nth;
     int64_t J, nL, nR;
+    int64_t mpos;               // the median's position before its move to `first` (-1: moved)
     int32_t depth, active, filled, err;
-    uint32_t piv, marked;       // marked: ties at the threshold in [0, first) (kt_mark_kernel)
+    uint32_t piv, kfirst;       // the pivot; the key at `first` before the move
+    uint32_t marked;            // ties at the threshold in [0, first) (kt_mark_kernel)
 };
 
-__global__ void __launch_bounds__(256)
-kt_fill_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
-               const RezState* __restrict__ st, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ list,
-               TieLevelState* __restrict__ tls, uint32_t* __restrict__ tie_bits) {
-    const int64_t a = blockIdx.y;
-    const uint32_t nlist = list[0];
-    {   // the tie bits of every listed client (no other row is read): cleared here, off the
-        // main stream, instead of a memset of all n rows before the fork
-        const int64_t words = (d + 31) / 32;
-        const int64_t wseg = (words + gridDim.x - 1) / gridDim.x;
-        const int64_t w0 = (int64_t)blockIdx.x * wseg, w1 = min(words, w0 + wseg);
-        for (int64_t e = a; e < (int64_t)nlist; e += gridDim.y) {
-            uint32_t* row = tie_bits + (int64_t)list[1 + e] * words;
-            for (int64_t i = w0 + threadIdx.x; i < w1; i += 256) row[i] = 0u;
-        }
+// tt_move_median_to_first's choice: which of a, b, c (keys ka, kb, kc) moves to `first`
+__device__ __forceinline__ int64_t tt_median_pos(uint32_t ka, uint32_t kb, uint32_t kc, int64_t a, int64_t b,
+                                                 int64_t c) {
+    if (ka > kb) {
+        if (kb > kc) return b;
+        return ka > kc ? c : a;
     }
-    if (a >= (int64_t)nlist) {                         // unused slot: nothing stale may run
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            tls[a].filled = 0;
-            tls[a].active = 0;
-        }
-        return;
-    }
-    const int64_t vec = list[1 + a];
-    const RezState s = st[vec];
-    const bool up = s.delta > 0;
-    const int64_t k = up ? s.delta : -(int64_t)s.delta;
-    if (k * 64 <= d) {                                 // partial_sort's heap path: rez_ties_kernel alone
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            tls[a].filled = 0;
-            tls[a].active = 0;
-        }
-        return;
-    }
-    const int64_t dpad = (d + 3) & ~(int64_t)3;
-    uint32_t* K = qbuf + (size_t)a * 2 * dpad;
-    uint32_t* I = K + dpad;
-    const DivPlan dp = div_plan(l1[vec]);
-    const float* xv = x + vec * d;
-    const int64_t seg = (((d + kTieFillSegs - 1) / kTieFillSegs) + 3) & ~(int64_t)3;
-    const int64_t b = (int64_t)blockIdx.x * seg, e = min(d, b + seg);
-    for (int64_t i = b + threadIdx.x; i < e; i += 256) {
-        float kp;
-        K[i] = rez_elem(xv[i], dp, fm, up, kp);
-        I[i] = (uint32_t)i;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        TieLevelState t{};
-        t.first = 0;
-        t.last = d;
-        t.nth = k - 1;
-        t.depth = 2 * floor_log2_i64(d);
-        t.filled = 1;
-        tls[a] = t;
-    }
+    if (ka > kc) return a;
+    return kb > kc ? c : b;
 }
 
-// level step 1 (one workgroup, one thread per slot, slots <= kTieSlots): the pivot, or
-// retire the slot; the active slots are compacted into alist (alist[0] = count), so the
-// level's other launches spread over the active slots only and an idle level costs a few
-// short launches.
 constexpr int kTieGrid = 2048;              // workgroups of the per-level launches (4 waves each)
-__global__ void __launch_bounds__(kTieSlots)
-kt_pivot_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ list,
-                TieLevelState* __restrict__ tls, int slots, uint32_t* __restrict__ alist, int64_t stop) {
-    __shared__ uint32_t wc[kTieSlots / 64];
-    const int a = threadIdx.x, lane = a & 63, w = a >> 6;
-    bool act = false;
-    if (a < slots) {
-        TieLevelState& t = tls[a];
-        act = a < (int)list[0] && t.filled && !t.err && t.depth > 0 && t.last - t.first > stop;
-        t.active = act ? 1 : 0;
-        if (act) {
-            const int64_t dpad = (d + 3) & ~(int64_t)3;
-            const Queue A{qbuf + (size_t)a * 2 * dpad, qbuf + (size_t)a * 2 * dpad + dpad};
-            const int64_t mid = t.first + (t.last - t.first) / 2;
-            tt_move_median_to_first(A, t.first, t.first + 1, mid, t.last - 1);
-            t.piv = A.key(t.first);
-        }
-    }
-    const uint64_t m = __ballot(act);
-    if (lane == 0) wc[w] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (int q = 0; q < kTieSlots / 64; ++q) {
-        off += q < w ? wc[q] : 0u;
-        tot += wc[q];
-    }
-    if (act) alist[1 + off + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)a;
-    if (a == 0) alist[0] = tot;
-}
 
 // segment s of [first, last) for one wave
-__device__ __forceinline__ void kt_seg(const TieLevelState& t, int s, int64_t& s0, int64_t& s1) {
-    const int64_t len = t.last - t.first;
+__device__ __forceinline__ void kt_seg(int64_t first, int64_t last, int s, int64_t& s0, int64_t& s1) {
+    const int64_t len = last - first;
     const int64_t seg = (((len + kTieSegs - 1) / kTieSegs) + 63) & ~(int64_t)63;
-    s0 = min(t.last, t.first + (int64_t)s * seg);
-    s1 = min(t.last, s0 + seg);
+    s0 = min(last, first + (int64_t)s * seg);
+    s1 = min(last, s0 + seg);
 }
 
-// level step 2: left / right stop counts per segment (cnt [slots][kTieSegs][2]); items
-// (active slot, segment) over the grid
-__global__ void __launch_bounds__(256)
-kt_count_kernel(int64_t d, const uint32_t* __restrict__ qbuf, const TieLevelState* __restrict__ tls,
-                uint32_t* __restrict__ cnt, const uint32_t* __restrict__ alist) {
-    const int lane = threadIdx.x & 63;
-    const int64_t items = (int64_t)alist[0] * kTieSegs;
-    for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < items; it += (int64_t)gridDim.x * 4) {
-        const int a = (int)alist[1 + it / kTieSegs], sg = (int)(it % kTieSegs);
+// A slot's introselect state at this level: level 0 from the client (queue [0, d), depth
+// 2 floor(log2 d); listed nth_element clients only -- partial_sort's heap path and unused
+// slots stay unfilled, rez_ties_kernel part 2 replays those), later levels from tls.
+struct KtLevel {
+    int64_t vec, k, first, last;
+    int depth;
+    bool filled, act;
+};
+__device__ __forceinline__ KtLevel kt_level(int a, int64_t d, uint32_t nlist, const RezState* __restrict__ st,
+                                            const uint32_t* __restrict__ list, const TieLevelState* __restrict__ tls,
+                                            int64_t stop, bool level0) {
+    KtLevel v{};
+    if (a >= (int)nlist) return v;
+    v.vec = list[1 + a];
+    if (level0) {
+        const int32_t delta = st[v.vec].delta;
+        v.k = delta > 0 ? delta : -(int64_t)delta;
+        v.first = 0;
+        v.last = d;
+        v.depth = 2 * floor_log2_i64(d);
+        v.filled = v.k * 64 > d;
+        v.act = v.filled && v.depth > 0 && d > stop;
+    } else {
         const TieLevelState& t = tls[a];
-        const int64_t dpad = (d + 3) & ~(int64_t)3;
-        const uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+        v.first = t.first;
+        v.last = t.last;
+        v.depth = t.depth;
+        v.filled = t.filled != 0;
+        v.act = v.filled && !t.err && v.depth > 0 && v.last - v.first > stop;
+    }
+    return v;
+}
+
+// level step 1: the pivot and the left / right stop counts per segment (cnt [slots][kTieSegs]
+// [2]); at level 0 also the queue fill from x (the tie bits of the listed clients cleared
+// beside it: no other row is read).  Workgroup 0 (one thread per slot) keeps the slots'
+// state (level 0: sets it up), their active flags and the compacted active list (alist[0] =
+// count) that the level's other launches spread over.  Items (slot, segment), one per wave:
+// every wave of a slot computes the median of 3 itself, so the pivot costs no launch of its
+// own.  The move of the median to `first` is written by the fill at level 0; at later levels
+// the counts and the lists see it as a substitution (positions first and mpos) and kt_jcut
+// moves the pair in memory, when no kernel reads the keys.
+__global__ void __launch_bounds__(256)
+kt_count_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
+                const RezState* __restrict__ st, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ list,
+                TieLevelState* __restrict__ tls, uint32_t* __restrict__ cnt, uint32_t* __restrict__ alist,
+                uint32_t* __restrict__ tie_bits, int slots, int64_t stop, int level0) {
+    const uint32_t nlist = list[0];
+    const int lane = threadIdx.x & 63;
+    const int64_t dpad = (d + 3) & ~(int64_t)3;
+    if (blockIdx.x == 0) {
+        __shared__ uint32_t wc[kTieSlots / 64];
+        const int a = threadIdx.x, w = a >> 6;
+        bool act = false;
+        if (a < slots) {
+            const KtLevel v = kt_level(a, d, nlist, st, list, tls, stop, level0 != 0);
+            act = v.act;
+            TieLevelState& t = tls[a];
+            if (level0) {                           // field by field: piv is the segment-0 wave's
+                t.first = 0;
+                t.last = d;
+                t.nth = v.k - 1;
+                t.J = t.nL = t.nR = 0;
+                t.depth = v.depth;
+                t.filled = v.filled ? 1 : 0;
+                t.err = 0;
+                t.marked = 0u;
+            }
+            t.active = act ? 1 : 0;
+        }
+        const uint64_t m = __ballot(act);
+        if (lane == 0) wc[w] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t off = 0, tot = 0;
+        for (int q = 0; q < kTieSlots / 64; ++q) {
+            off += q < w ? wc[q] : 0u;
+            tot += wc[q];
+        }
+        if (act) alist[1 + off + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)a;
+        if (a == 0) alist[0] = tot;
+    }
+    const int nsl = min((int)nlist, slots);
+    const int64_t items = (int64_t)nsl * kTieSegs;
+    for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < items; it += (int64_t)gridDim.x * 4) {
+        const int a = (int)(it / kTieSegs), sg = (int)(it % kTieSegs);
+        if (level0) {
+            const int64_t words = (d + 31) / 32;
+            const int64_t wseg = (words + kTieSegs - 1) / kTieSegs;
+            const int64_t w0 = (int64_t)sg * wseg, w1 = min(words, w0 + wseg);
+            for (int64_t e = a; e < (int64_t)nlist; e += slots) {
+                uint32_t* row = tie_bits + (int64_t)list[1 + e] * words;
+                for (int64_t i = w0 + lane; i < w1; i += 64) row[i] = 0u;
+            }
+        }
+        const KtLevel v = kt_level(a, d, nlist, st, list, tls, stop, level0 != 0);
+        if (!v.filled || (!level0 && !v.act)) continue;
+        uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+        uint32_t* I = K + dpad;
+        const float* xv = x ? x + v.vec * d : nullptr;
+        DivPlan dp{};
+        bool up = false;
+        if (level0) {
+            dp = div_plan(l1[v.vec]);
+            up = st[v.vec].delta > 0;
+        }
+        auto key_at = [&](int64_t i) -> uint32_t {
+            float kp;
+            return level0 ? rez_elem(xv[i], dp, fm, up, kp) : K[i];
+        };
+        // the median of 3 to `first` (tt_move_median_to_first), when this level runs
+        int64_t mpos = -1;
+        uint32_t piv = 0u, kfirst = 0u;
+        if (v.act) {
+            const int64_t mid = v.first + (v.last - v.first) / 2;
+            kfirst = key_at(v.first);
+            const uint32_t ka = key_at(v.first + 1), kb = key_at(mid), kc = key_at(v.last - 1);
+            mpos = tt_median_pos(ka, kb, kc, v.first + 1, mid, v.last - 1);
+            piv = mpos == v.first + 1 ? ka : (mpos == mid ? kb : kc);
+        }
         int64_t s0, s1;
-        kt_seg(t, sg, s0, s1);
+        kt_seg(v.first, v.last, sg, s0, s1);
+        const bool sub = mpos >= 0 && ((v.first >= s0 && v.first < s1) || (mpos >= s0 && mpos < s1));
         uint32_t cl = 0, cr = 0;
         for (int64_t b = s0; b < s1; b += 64 * kTieU) {
             uint32_t kk[kTieU];
 #pragma unroll
             for (int u = 0; u < kTieU; ++u) {
                 const int64_t i = b + (int64_t)u * 64 + lane;
-                kk[u] = i < s1 ? K[i] : 0u;
+                kk[u] = i < s1 ? key_at(i) : 0u;
             }
 #pragma unroll
             for (int u = 0; u < kTieU; ++u) {
                 const int64_t i = b + (int64_t)u * 64 + lane;
-                cl += (i < s1 && i > t.first && kk[u] <= t.piv) ? 1u : 0u;
-                cr += (i < s1 && kk[u] >= t.piv) ? 1u : 0u;
+                if (i >= s1) continue;
+                uint32_t key = kk[u], idx = (uint32_t)i;
+                if (sub) {
+                    if (i == v.first) { key = piv; idx = (uint32_t)mpos; }
+                    else if (i == mpos) { key = kfirst; idx = (uint32_t)v.first; }
+                }
+                if (level0) {
+                    K[i] = key;
+                    I[i] = idx;
+                }
+                cl += ((!sub || i > v.first) && key <= piv) ? 1u : 0u;
+                cr += (key >= piv) ? 1u : 0u;
             }
         }
+        if (!v.act) continue;                           // level 0 fill of a slot whose range is short
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             cl += __shfl_xor(cl, o, 64);
@@ -706,6 +748,11 @@ kt_count_kernel(int64_t d, const uint32_t* __restrict__ qbuf, const TieLevelStat
         if (lane == 0) {
             cnt[((size_t)a * kTieSegs + sg) * 2] = cl;
             cnt[((size_t)a * kTieSegs + sg) * 2 + 1] = cr;
+            if (sg == 0) {
+                tls[a].piv = piv;
+                tls[a].kfirst = kfirst;
+                tls[a].mpos = level0 ? -1 : mpos;
+            }
         }
     }
 }
@@ -735,8 +782,13 @@ kt_list_kernel(int64_t d, const uint32_t* __restrict__ qbuf, uint32_t* __restric
             ol += __shfl_xor(ol, o, 64);
             orr += __shfl_xor(orr, o, 64);
         }
+        const int64_t first = t.first, mpos = t.mpos;
+        const uint32_t piv = t.piv, kfirst = t.kfirst;
         int64_t s0, s1;
-        kt_seg(t, sg, s0, s1);
+        kt_seg(first, t.last, sg, s0, s1);
+        // the median move as a substitution: only the (at most two) segments holding `first`
+        // or mpos take the slow form (wave-uniform)
+        const bool sub = (first >= s0 && first < s1) || (mpos >= s0 && mpos < s1);
         for (int64_t b = s0; b < s1; b += 64 * kTieU) {
             uint32_t kk[kTieU];
 #pragma unroll
@@ -747,8 +799,10 @@ kt_list_kernel(int64_t d, const uint32_t* __restrict__ qbuf, uint32_t* __restric
 #pragma unroll
             for (int u = 0; u < kTieU; ++u) {
                 const int64_t i = b + (int64_t)u * 64 + lane;
-                const bool lf = i < s1 && i > t.first && kk[u] <= t.piv;
-                const bool rf = i < s1 && kk[u] >= t.piv;
+                uint32_t key = kk[u];
+                if (sub) key = i == first ? piv : (i == mpos ? kfirst : key);
+                const bool lf = i < s1 && (!sub || i > first) && key <= piv;
+                const bool rf = i < s1 && key >= piv;
                 const uint64_t ml = __ballot(lf), mr = __ballot(rf);
                 if (lf) Lpos[ol + __popcll(ml & lt)] = (uint32_t)i;
                 if (rf) Rpos[orr + __popcll(mr & lt)] = (uint32_t)i;
@@ -766,7 +820,7 @@ kt_list_kernel(int64_t d, const uint32_t* __restrict__ qbuf, uint32_t* __restric
 constexpr int kJcutThreads = 256;
 
 __global__ void __launch_bounds__(kJcutThreads)
-kt_jcut_kernel(int64_t d, const uint32_t* __restrict__ pos, TieLevelState* __restrict__ tls,
+kt_jcut_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ pos, TieLevelState* __restrict__ tls,
                const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ alist) {
     constexpr int kW = kJcutThreads / kWave;
     __shared__ uint32_t red[2][kW];
@@ -809,6 +863,16 @@ kt_jcut_kernel(int64_t d, const uint32_t* __restrict__ pos, TieLevelState* __res
         }
     }
     if (tid == 0) {
+        if (t.mpos >= 0) {                  // the median's move to `first` (kt_count_kernel)
+            const int64_t dpad = (d + 3) & ~(int64_t)3;
+            uint32_t* K = qbuf + (size_t)a * 2 * dpad;
+            uint32_t* I = K + dpad;
+            const uint32_t im = I[t.mpos], i0 = I[t.first];
+            K[t.first] = t.piv;
+            I[t.first] = im;
+            K[t.mpos] = t.kfirst;
+            I[t.mpos] = i0;
+        }
         const int64_t J = lo;
         int64_t cut = INT64_MAX;
         if (J < (int64_t)nL) cut = (int64_t)Lpos[J];

@@ -2657,7 +2657,7 @@ int side_stream(SideStream** out) {
 // *tls_out is set: the caller then runs launch_torch_ties_rest (part 2: heap-path clients
 // and list entries beyond the slots) once the output kernel on its own stream is done.
 // KB7's client list and cleared tie bits (before launch_torch_ties and the tie counts).
-// clear_bits: without KB7a (which clears the listed clients' rows in kt_fill) every row here.
+// clear_bits: without KB7a (whose level-0 kt_count clears the listed clients' rows) every row here.
 int torch_ties_prepare(int64_t n, int64_t d, RezState* state, uint32_t* bits, char* wsb, const BiasedLayout& w,
                        hipStream_t st, bool clear_bits) {
     if (clear_bits) {
@@ -2747,11 +2747,8 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     TieLevelState* tls = (TieLevelState*)(wsb + w.tls_off);
     uint32_t* cnt = (uint32_t*)(wsb + w.tcnt2_off);
     const unsigned S = (unsigned)w.slots;
-    hipLaunchKernelGGL(kt_fill_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, x, d, l1, fm, state, qbuf, list, tls,
-                       bits);
-    if ((rc = hip_check(hipGetLastError(), "kt_fill_kernel launch"))) return rc;
     // a level keeps the side of the cut that holds nth, half the range on average; an idle
-    // level costs five ~6 us launches, and a range still longer continues in part 1's
+    // level costs four ~6 us launches, and a range still longer continues in part 1's
     // workgroup (UQDME_TIE_STOP / UQDME_TIE_MARGIN: experiments only)
     static const int64_t tie_stop = [] {
         const char* e = std::getenv("UQDME_TIE_STOP");
@@ -2770,21 +2767,27 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     // the per-level launches take (active slot, segment) items, one per wave: S slots need at
     // most S * kTieSegs / 4 workgroups (a one-client call launched 2048, 1984 of them idle)
     const unsigned lgrid = (unsigned)std::min<int64_t>(kTieGrid, (int64_t)S * kTieSegs / 4);
+    // level 0's pivot and counts with the queue fill from x (x, l1 and the states are
+    // per-call arguments: launched directly, not captured)
+    hipLaunchKernelGGL(kt_count_kernel, dim3(lgrid), dim3(256), 0, st, x, d, l1, fm, (const RezState*)state, qbuf, list,
+                       tls, cnt, alist, bits, (int)S, tie_stop, 1);
+    if ((rc = hip_check(hipGetLastError(), "kt_count_kernel launch"))) return rc;
     auto levels_on = [&](hipStream_t ls) {
         for (int lv = 0; lv < levels; ++lv) {
-            hipLaunchKernelGGL(kt_pivot_kernel, dim3(1), dim3(kTieSlots), 0, ls, d, qbuf, list, tls, (int)S, alist,
-                               tie_stop);
-            hipLaunchKernelGGL(kt_count_kernel, dim3(lgrid), dim3(256), 0, ls, d, qbuf, tls, cnt, alist);
+            if (lv > 0)
+                hipLaunchKernelGGL(kt_count_kernel, dim3(lgrid), dim3(256), 0, ls, (const float*)nullptr, d,
+                                   (const float*)nullptr, fm, (const RezState*)nullptr, qbuf, list, tls, cnt, alist,
+                                   (uint32_t*)nullptr, (int)S, tie_stop, 0);
             hipLaunchKernelGGL(kt_list_kernel, dim3(lgrid), dim3(256), 0, ls, d, qbuf, pos, tls, cnt, alist);
-            hipLaunchKernelGGL(kt_jcut_kernel, dim3(S), dim3(kJcutThreads), 0, ls, d, pos, tls, cnt, alist);
+            hipLaunchKernelGGL(kt_jcut_kernel, dim3(S), dim3(kJcutThreads), 0, ls, d, qbuf, pos, tls, cnt, alist);
             hipLaunchKernelGGL(kt_swap_kernel, dim3(lgrid), dim3(256), 0, ls, d, qbuf, pos, tls, alist);
         }
         return hip_check(hipGetLastError(), "KB7a level launch");
     };
-    // The level chain (~13 levels x 5 dependent launches, whether or not a client is listed)
-    // is replayed as a captured HIP graph: its arguments are workspace pointers, d and S
-    // only, so one capture serves every call on the same workspace (per-call host cost was
-    // ~65 launches, more than the chain's GPU time for a few-client call).
+    // The rest of the level chain (4 dependent launches per level, whether or not a client is
+    // listed) is replayed as a captured HIP graph: its arguments are workspace pointers, d, S
+    // and the stop only, so one capture serves every call on the same workspace (per-call
+    // host cost was ~65 launches, more than the chain's GPU time for a few-client call).
     hipGraphExec_t exec = nullptr;
     rc = level_graph(LevelPtrs{qbuf, list, tls, cnt, pos, alist}, d, S, levels, st, levels_on, &exec);
     if (rc) return rc;
@@ -2793,7 +2796,7 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     } else if ((rc = levels_on(st))) {
         return rc;
     }
-    hipLaunchKernelGGL(kt_mark_kernel, dim3(kTieFillSegs, S), dim3(256), 0, st, d, qbuf, list, state, tls, bits);
+    hipLaunchKernelGGL(kt_mark_kernel, dim3(kTieMarkSegs, S), dim3(256), 0, st, d, qbuf, list, state, tls, bits);
     if ((rc = hip_check(hipGetLastError(), "kt_mark_kernel launch"))) return rc;
     hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3(S), dim3(kTieThreads), 0, st, x, d, l1, fm, state, bits,
                        qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)tls, 1, (uint32_t*)(wsb + w.tcnt_off),
