@@ -11,17 +11,18 @@ Workload (BASELINE.json configs[1], "C2"): per GPU, n=1024 client vectors of d=2
 i.i.d. N(0,1) f32, resident in HBM before timing; rate R=1 (m = 224426); L1 in the
 torch-CPU order of 1 thread.  One step = one pass of the hot path over the batch:
     K1 torch-order L1 (AS:624)  ->  K2 fused quantize/dequantize (AS:625-640; writes the
-    dequantized q and the int8 type codes)  ->  K3c client-ordered mean from the codes
-    (ND:137-138, bit-identical to the mean of q)  ->  [N>1] one RCCL reduce of est to rank 0.
-(--pipeline q: K2 writes q only and K3 reads q; --pipeline encode: codes only.)
+    dequantized q and the type codes as 4-bit fields)  ->  K3n client-ordered mean from the
+    codes (ND:137-138, bit-identical to the mean of q)  ->  [N>1] one RCCL reduce of est to rank 0.
+(--pipeline auto = codes4 where its counts fit (R <= 2, n >= 256, d % 4096 == 0), else codes:
+int8 codes; q: K2 writes q only and K3 reads q; encode: int8 codes only.)
 Clients shard across GPUs with no data-path collective except that final reduce
 (weak scaling: 1024 clients per GPU).  value = all clients processed / max-over-ranks
 time, in M-vectors/s.
 
 Rank 0 prints ONE JSON line.  `roofline` is computed for K2 from HIP events recorded
 around its launches inside the timed region.  Algorithmic bytes follow SURVEY.md §8(d):
-8*d per vector for quantize+dequantize (read x, write q); the int8 code stream K2 also
-writes (1*d) is implementation traffic, reported apart (`impl_bytes_per_launch`) and never
+8*d per vector for quantize+dequantize (read x, write q); the code stream K2 also writes
+(0.5*d as 4-bit fields, 1*d as int8) is implementation traffic, reported apart (`impl_bytes_per_launch`) and never
 counted as achieved bandwidth; --pipeline encode (no q) counts 4*d.  `roofline.step` prices
 the whole step the same way (8*d per vector / ms_per_step) and sets the PMC traffic of all
 the step's kernels against it.  W warmup steps run first.  `cpu_baseline` times the C
@@ -68,7 +69,7 @@ def parse(argv=None):
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/pmc_*.json)")
     ap.add_argument("--mean-mode", choices=["reduce", "ordered"], default="reduce",
                     help="N>1: one RCCL reduce of per-rank partial means, or the bit-exact ordered chain")
-    ap.add_argument("--pipeline", choices=["q", "codes", "encode"], default="codes",
+    ap.add_argument("--pipeline", choices=["auto", "q", "codes", "codes4", "encode"], default="auto",
                     help="q: K2 writes the dequantized q, mean reads q (the reference's drop-in semantics); "
                          "codes: K2 writes q AND type codes, mean decodes codes; "
                          "encode: K2 writes codes only, the mean kernel dequantizes (DME wire pipeline)")
@@ -202,11 +203,12 @@ PIPELINE_WHAT = {
          "the client mean reads q (ND:137-138)",
     "codes": "K2 writes q and int8 type codes, the client mean decodes the codes (same est bits)",
     "encode": "K2 writes int8 type codes only (no per-client q), the mean kernel dequantizes them",
+    "codes4": "K2 writes q and 4-bit type codes, the client mean decodes them (same est bits; kmax > 7 from q)",
 }
 
 # kernels launched once per bench step (tools/summarize_profile.py keeps one entry per name)
 STEP_KERNELS = ("l1_partial_kernel", "l1_finalize_kernel", "quantize_stream_kernel", "codes_mean_kernel",
-                "client_mean_kernel")
+                "nibbles_mean_kernel", "client_mean_kernel")
 
 
 def main():
@@ -223,6 +225,8 @@ def main():
     n, d = args.clients, args.dim
     m = uqdme.rate_to_m(args.bits, d)
     T = args.torch_threads
+    if args.pipeline == "auto":         # 4-bit codes where every count fits (pipeline.py)
+        args.pipeline = "codes4" if uqdme.codes4_fits(n, d, args.bits) else "codes"
     n_total = n * world
 
     # ---- synthetic inputs resident in HBM (generation is outside the timed region) ----
@@ -245,7 +249,8 @@ def main():
     # is probed once (pipeline.py: K2's speed follows where q and the codes land).
     if args.mean_mode == "ordered" and args.pipeline == "encode" and world > 1:
         raise SystemExit("--mean-mode ordered folds q across ranks: use --pipeline codes or q")
-    sh = uqdme.ShardedDME(n, d, n_total, m=m, torch_threads=T, pipeline="codes", mode=args.mean_mode)
+    sh = uqdme.ShardedDME(n, d, n_total, m=m, torch_threads=T, pipeline="codes4" if args.pipeline == "codes4" else "codes",
+                          mode=args.mean_mode)
     pipe = sh.pipe
     probe = sh.probe_outputs(x, X, candidates=args.probe_candidates, min_candidates=args.probe_min) \
         if args.probe_candidates > 1 else None
@@ -312,8 +317,8 @@ def main():
     q_ms = float(seg_ms[1])
     # algorithmic bytes per K2 launch: read x (4d) + write q (4d); the int8
     # code stream (1d) is this design's own traffic and is reported apart, not as achieved
-    alg_bytes = float(d * n) * (8 if args.pipeline in ("q", "codes") else 4)
-    impl_bytes = float(d * n) * (1 if args.pipeline != "q" else 0)
+    alg_bytes = float(d * n) * (8 if args.pipeline in ("q", "codes", "codes4") else 4)
+    impl_bytes = float(d * n) * {"q": 0.0, "codes4": 0.5}.get(args.pipeline, 1.0)
     achieved = alg_bytes / (q_ms * 1e-3) / 1e9
     traffic, traffic_src, step_traffic = load_traffic(args.traffic_json, d, n, args.pipeline)
     step_alg = float(d * n_total) * 8 / world      # quantize+dequantize bytes of one rank's clients
@@ -324,8 +329,8 @@ def main():
         base, parity = cpu_baseline(args, x, X_cpu, q, m, T)
     side = {}
     if args.side_pipelines and world == 1:
-        for pl in ("q", "codes", "encode"):
-            if pl != args.pipeline:
+        for pl in ("q", "codes", "encode", "codes4"):
+            if pl != args.pipeline and (pl != "codes4" or uqdme.codes4_fits(n, d, args.bits)):
                 ms = time_pipeline(pl, max(3, args.steps // 2))
                 side[pl] = {"ms_per_step": round(ms, 4), "value": round(n_total / ms / 1e3, 6),
                             "what": PIPELINE_WHAT[pl]}
@@ -372,8 +377,9 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes, "impl_bytes_per_launch": impl_bytes,
-                         "alg_bytes_rule": ("8*d per vector (read x, write q), SURVEY.md §8(d); the int8 codes "
-                                            "(1*d) K2 also writes are implementation traffic"
+                         "alg_bytes_rule": ("8*d per vector (read x, write q), SURVEY.md §8(d); the type codes "
+                                            f"({'0.5*d as 4-bit fields' if args.pipeline == 'codes4' else '1*d as int8'})"
+                                            " K2 also writes are implementation traffic"
                                             if args.pipeline != "encode" else "4*d per vector (read x); no q"),
                          "step": {"alg_bytes": step_alg, "ms": round(ms_per_step, 4),
                                   "achieved": round(step_achieved, 2),

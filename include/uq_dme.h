@@ -131,6 +131,26 @@ int uq_type_unbiased_codes_ld_f32(const float* x, float* out, int64_t ldq, int8_
                                   const float* l1, float* l1_out, int32_t torch_threads, void* ws,
                                   size_t ws_bytes, void* stream);
 
+/* 4-bit type codes (the bench pipeline "codes4"): as uq_type_unbiased_codes_ld_f32 writing q
+ * (required) and the codes as 4-bit fields, two per byte (element 2i in the low nibble of byte
+ * i of row j at nib + j*ldn, ldn >= d/2 bytes): the low nibble of the int8 code, i.e. k for
+ * sign >= 0 and 15-k for -k-1, exact while k <= 7.  kmax as for the int8 codes (the largest
+ * count, 128 above 127); a client with kmax > 7 is read from q by uq_nibbles_q_mean_ld_f32.
+ * Stream form only: n >= 256, d % 4096 == 0, d <= 2^29, 16-byte aligned rows (UQ_E_INVALID
+ * otherwise).  Internal format between K2 and the mean; no wire format (the UQR1 codec takes
+ * the int8 codes). */
+int uq_type_unbiased_nibbles_ld_f32(const float* x, float* out, int64_t ldq, uint8_t* nib, int64_t ldn,
+                                    int32_t* kmax, int64_t n, int64_t d, int64_t m, const float* X,
+                                    const float* l1, float* l1_out, int32_t torch_threads, void* ws,
+                                    size_t ws_bytes, void* stream);
+
+/* est[i] (+)= q[j][i] / n_div, clients in order, from the 4-bit codes above: bit-identical to
+ * uq_client_mean_f32(q); clients with kmax[j] > 7 add q[j][i] / n_div (q required).
+ * d % 4096 == 0, ldq >= d, ldn >= d/2, 16-byte aligned est and q. */
+int uq_nibbles_q_mean_ld_f32(const uint8_t* nib, int64_t ldn, const float* q, int64_t ldq, const float* l1,
+                             const int32_t* kmax, int64_t n, int64_t d, int64_t m, float n_div,
+                             int32_t accumulate, float* est, void* stream);
+
 /* q[j][i] = decode(codes[j][i]; l1[j], m). */
 int uq_codes_decode_f32(const int8_t* codes, const float* l1, int64_t n, int64_t d, int64_t m,
                         float* out, void* stream);

@@ -150,3 +150,65 @@ def test_output_pool_never_hands_out_a_held_result(gpu_ready):
         POOL.min_bytes = old
         POOL.enabled = was_on
         POOL.clear()
+
+
+def _unpack_nibbles(nib: torch.Tensor) -> torch.Tensor:
+    """uint8 [n, d/2] 4-bit fields -> int8 [n, d] codes (sign-extended nibbles)."""
+    lo = (nib & 0xF).to(torch.int16)
+    hi = (nib >> 4).to(torch.int16)
+    v = torch.stack([lo, hi], dim=-1).reshape(nib.shape[0], -1)
+    return torch.where(v >= 8, v - 16, v).to(torch.int8)
+
+
+@pytest.mark.parametrize("bits", [1, 2])
+def test_codes4_pipeline_matches_batched_apis(gpu_ready, bits):
+    """The 4-bit code pipeline (bench default): est and q bit-identical to the batched APIs,
+    before and after the placement probe and with accumulate; its nibbles are the int8
+    codes' low nibbles; clients whose counts exceed 7 (an outlier coordinate) or 127 (one
+    nonzero coordinate) or whose L1 is not finite are read from q (ND:137-138, AS:609-641)."""
+    import uqdme
+    n, d = 300, 8192                                   # 9 full 32-client groups + 12 in the tail
+    g = torch.Generator(device="cuda").manual_seed(21 + bits)
+    x = torch.randn(n, d, generator=g, device="cuda")
+    x[5, 77] = 60.0                                    # 7 < kmax <= 127
+    x[40].zero_()
+    x[40, 100] = -2.5                                  # kmax = 128
+    x[299, 3] = float("inf")                           # L1 not finite
+    X = torch.rand(n, generator=torch.Generator().manual_seed(5)).cuda()
+    q_ref = uqdme.quantize_dequantize(x, bits, X=X, torch_threads=1)
+    est_ref = uqdme.client_mean(q_ref, float(n))
+    ref8 = uqdme.DMEPipeline(n, d, bits, torch_threads=1, pipeline="codes")
+    ref8.step(x, X)
+    p = uqdme.DMEPipeline(n, d, bits, torch_threads=1, pipeline="codes4")
+    for probe in (False, True):
+        if probe:
+            rep = p.probe_outputs(x, X, candidates=3, reps=1)
+            assert 1 < rep["candidates"] <= 3
+        est = p.step(x, X)
+        p.check_status()
+        assert torch.equal(p.q.view(torch.int32), q_ref.view(torch.int32)), probe
+        assert torch.equal(est.view(torch.int32), est_ref.view(torch.int32)), probe
+        assert torch.equal(p.kmax, ref8.kmax)
+        fits = (p.kmax <= 7).nonzero().flatten()
+        assert fits.numel() >= n - 3 and int(p.kmax[5]) > 7 and int(p.kmax[40]) == 128
+        assert torch.equal(_unpack_nibbles(p.nib)[fits], ref8.codes[fits]), probe
+        assert p.overflowed() >= 3
+    e1 = p.step(x, X, n_div=float(2 * n)).clone()
+    e2 = p.step(x, X, n_div=float(2 * n), accumulate=True, est=e1)
+    ref2 = uqdme.client_mean(torch.cat([q_ref, q_ref]), float(2 * n))
+    assert torch.equal(e2.view(torch.int32), ref2.view(torch.int32))
+    # no client above 7: the straight-line mean (every client from its nibbles)
+    xg = torch.randn(n, d, generator=g, device="cuda")
+    qg = uqdme.quantize_dequantize(xg, bits, X=X, torch_threads=1)
+    eg = p.step(xg, X)
+    assert p.overflowed() == 0
+    assert torch.equal(eg.view(torch.int32), uqdme.client_mean(qg, float(n)).view(torch.int32))
+    # a step overridden to the int8 kinds and back (the bench's side lines on one pipeline)
+    for pl in ("codes", "q", "encode", "codes4"):
+        e = p.step(x, X, pipeline=pl)
+        if pl != "encode":
+            assert torch.equal(e.view(torch.int32), est_ref.view(torch.int32)), pl
+    assert uqdme.codes4_fits(n, d, bits) and not uqdme.codes4_fits(n, d, 3) and not uqdme.codes4_fits(255, d, 1)
+    for bad in ((255, d), (n, d + 16)):
+        with pytest.raises(ValueError):
+            uqdme.DMEPipeline(*bad, bits, pipeline="codes4")

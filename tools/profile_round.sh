@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round profile on the GPU box: kernel-trace stats + separate PMC passes.
-# usage (repo root): bash tools/profile_round.sh gpurun_out/<tag> [pipeline: q|codes|encode]
+# usage (repo root): bash tools/profile_round.sh gpurun_out/<tag> [pipeline: q|codes|codes4|encode]
 # then: PROFILE_STEPS=40 python tools/summarize_profile.py gpurun_out/<tag> <tag> <pipeline>
 set -e
 PIPE=${2:-codes}

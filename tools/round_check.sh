@@ -32,7 +32,7 @@ for s in $STEPS; do
     self2) UQDME_BENCH_BACKEND=gloo timeout -k 10 240 python bench.py --gpus 2 --steps 5 --warmup 2 \
              > $O/bench_self2.json 2> $O/bench_self2.err ;;
     dropin) timeout -k 10 200 python tools/dropin_latency.py > $O/dropin_latency.json 2> $O/dropin_latency.err ;;
-    profile) bash tools/profile_round.sh $O codes > $O/profile.log 2>&1 ;;
+    profile) bash tools/profile_round.sh $O codes4 > $O/profile.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   echo "$TAG: $s ok"

@@ -4,8 +4,9 @@ FETCH_SIZE reads half the bytes of wide coalesced streaming loads -> x2; MI355X_
 import csv, glob, json, os, shutil, sys
 src, tag = sys.argv[1], sys.argv[2]
 pipeline = sys.argv[3] if len(sys.argv) > 3 else "codes"
-# quantize_stream_kernel<WQ, WC, CVEC> instance used by each bench pipeline
-VARIANT = {"q": "<true, false, true>", "codes": "<true, true, true>", "encode": "<false, true, true>"}
+# quantize_stream_kernel<WQ, WC, CVEC, NIB> instance used by each bench pipeline
+VARIANT = {"q": "<true, false, true, false>", "codes": "<true, true, true, false>",
+           "encode": "<false, true, true, false>", "codes4": "<true, true, true, true>"}
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)

@@ -21,7 +21,7 @@ from .quicfl import (QuicFLReceiver, QuicFLSender, QuicFLMessages, QUICFL_quanti
 from ._lib import UQError, load as load_library, library_path
 from .distributed import ShardedDME, shard_range, sharded_client_mean, sharded_quantize_mean
 from .dme import DISTRIBUTIONS, nmse_simulation
-from .pipeline import DMEPipeline
+from .pipeline import DMEPipeline, codes4_fits
 from .fl_stats import compute_nmse_stats_auto, data_format, round_nmse
 from .outpool import set_output_pool
 
@@ -35,5 +35,5 @@ __all__ = [
     "TypeCodes", "Type_biased_quantize", "biased_quantize", "EDEN_quantize_Hadamard", "eden_quantize",
     "eden_compress", "eden_decompress", "EdenMessage", "rht_signs", "randomized_hadamard_transform",
     "randomized_inverse_hadamard_transform", "compute_nmse_stats_auto", "data_format", "round_nmse",
-    "DMEPipeline", "ShardedDME", "TypeMessages", "encode_messages", "decode_messages", "set_output_pool",
+    "DMEPipeline", "codes4_fits", "ShardedDME", "TypeMessages", "encode_messages", "decode_messages", "set_output_pool",
 ]

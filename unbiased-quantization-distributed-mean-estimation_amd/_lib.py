@@ -41,6 +41,9 @@ SIGNATURES = {
     "uq_type_unbiased_codes_ld_f32": (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _p, _p, _p, _i32,
                                                      _p, _sz, _p]),
     "uq_codes_q_mean_ld_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _i32, _p, _p]),
+    "uq_type_unbiased_nibbles_ld_f32": (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _p, _p, _p, _i32,
+                                                       _p, _sz, _p]),
+    "uq_nibbles_q_mean_ld_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _i32, _p, _p]),
     "uq_biased_workspace_bytes": (ctypes.c_int, [_i64, _i64, _i32, ctypes.POINTER(_sz)]),
     "uq_type_biased_f32": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _sz, _p]),
     "uq_rht_signs": (ctypes.c_int, [_p, _i64, _i64, _p, _p]),

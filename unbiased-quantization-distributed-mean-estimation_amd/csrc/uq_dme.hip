@@ -1240,8 +1240,9 @@ __device__ __forceinline__ uint32_t code_of(float mps, float kf) {
     return (uint32_t)(((int)kf ^ mask) & 0xFF);
 }
 
-// pass 2; WQ: outputs into the LDS image s_o, WC: this thread's 16 codes into cw.
-template <bool WQ, bool WC>
+// pass 2; WQ: outputs into the LDS image s_o, WC: this thread's 16 codes into cw (NIB: as
+// 4-bit codes, element e of the thread in bits 4e..4e+3 of cw[0..1]).
+template <bool WQ, bool WC, bool NIB = false>
 __device__ __forceinline__ void tile_pass2(float* s_o, const TileVals& tv, const float* s_tab, int tid, double base,
                                            float L, float fm, float Xv, uint32_t (&cw)[4], float& kmax) {
     double s = base;                           // exact prefix before this thread's first element
@@ -1268,7 +1269,8 @@ __device__ __forceinline__ void tile_pass2(float* s_o, const TileVals& tv, const
             m4 = fmaxf(m4, kf);
             // AS:640 via the table, sign(v) from mps; k >= kTab is recomputed below (rare)
             if (WQ) o[c] = copysignf(s_tab[(int)kf & (kTab - 1)], mps);
-            if (WC) w |= code_of(mps, kf) << (8 * c);          // padding elements: mps = 0, r = 0
+            if (WC) w |= NIB ? (code_of(mps, kf) & 0xFu) << (4 * c)       // padding elements: mps = 0, r = 0
+                             : code_of(mps, kf) << (8 * c);
         }
         if (WC) kmax = fmaxf(kmax, m4);
         if (WQ && __builtin_expect(!(m4 < (float)kTab) || arith, 0)) {
@@ -1278,7 +1280,8 @@ __device__ __forceinline__ void tile_pass2(float* s_o, const TileVals& tv, const
                     o[c] = (copysignf(L, tv.mps[4 * k4 + c]) * kfs[c]) / fm;   // ((L1*sign)*(fl+r))/m
         }
         if (WQ) *reinterpret_cast<float4*>(&s_o[swz(tid, k4)]) = make_float4(o[0], o[1], o[2], o[3]);
-        if (WC) cw[k4] = w;
+        if (WC && !NIB) cw[k4] = w;
+        if (WC && NIB) cw[k4 >> 1] = (k4 & 1) ? (cw[k4 >> 1] | (w << 16)) : w;
     }
 }
 
@@ -1295,10 +1298,14 @@ __device__ __forceinline__ void store_codes(int8_t* __restrict__ ct, const uint3
 
 // codes of tile t0 (element offset) of one row: one 16-byte buffer store per thread
 // (beyond d: dropped by the range check), or bytewise when d % 16 != 0.
-template <bool CVEC>
+template <bool CVEC, bool NIB = false>
 __device__ __forceinline__ void store_codes_buf(__amdgpu_buffer_rsrc_t rc, int8_t* __restrict__ crow,
                                                 const uint32_t (&cw)[4], uint32_t t0, int64_t d, int tid) {
-    if (CVEC) {
+    if (NIB) {                                   // 4-bit codes: 8 bytes per thread (d % 32 == 0)
+        typedef uint32_t u32x2n __attribute__((ext_vector_type(2)));
+        const u32x2n v = {cw[0], cw[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(v, rc, (t0 + (uint32_t)(tid * kQItems)) / 2u, 0, kAuxNT);
+    } else if (CVEC) {
         const u32x4v v = {cw[0], cw[1], cw[2], cw[3]};
         __builtin_amdgcn_raw_buffer_store_b128(v, rc, t0 + (uint32_t)(tid * kQItems), 0, kAuxNT);
     } else {
@@ -1360,7 +1367,7 @@ __device__ __forceinline__ void store_tile(const float* s_data, float* __restric
 // s = b % nseg, starting from the exact P = pre[first tile] (the per-client fold of the
 // small-batch form) -- or from P = 0 over the whole vector when nseg == 1 (pre == nullptr).
 // The tile loop of one workgroup (tiles [tb, te) of client `vec` from the exact start P).
-template <bool WQ, bool WC, bool CVEC>
+template <bool WQ, bool WC, bool CVEC, bool NIB = false>
 __device__ __forceinline__ void stream_tiles(const float* __restrict__ x, float* __restrict__ out,
                                              int8_t* __restrict__ codes, int32_t* __restrict__ overflow, int64_t d,
                                              int32_t tb, int32_t te, float fm, float Xv, float L, int32_t nseg,
@@ -1371,7 +1378,8 @@ __device__ __forceinline__ void stream_tiles(const float* __restrict__ x, float*
     const uint32_t row_bytes = (uint32_t)(d * 4);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + vec * d, row_bytes);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(WQ ? out + vec * ldo : x, row_bytes);
-    const __amdgpu_buffer_rsrc_t rc = make_rsrc(WC ? (const void*)(codes + vec * ldc) : (const void*)x, row_bytes / 4u);
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(WC ? (const void*)(codes + vec * ldc) : (const void*)x,
+                                                row_bytes / (NIB ? 8u : 4u));
     TileRegs pre_x;
     load_tile_buf(pre_x, rx, (uint32_t)tb * (uint32_t)(kQTile * 4), tid);
     build_table(s_tab, tid, L, fm);
@@ -1383,7 +1391,7 @@ __device__ __forceinline__ void stream_tiles(const float* __restrict__ x, float*
         if (tile > tb) {
             const uint32_t tp = (uint32_t)(tile - 1) * (uint32_t)kQTile;
             if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);      // beyond d: dropped by the range check
-            if (WC) store_codes_buf<CVEC>(rc, codes + vec * ldc, cw, tp, d, tid);
+            if (WC) store_codes_buf<CVEC, NIB>(rc, codes + vec * ldc, cw, tp, d, tid);
         }
         if (tile + 1 < te) load_tile_buf(pre_x, rx, (uint32_t)(tile + 1) * (uint32_t)(kQTile * 4), tid);
         const int64_t t0 = (int64_t)tile * kQTile;
@@ -1399,14 +1407,14 @@ __device__ __forceinline__ void stream_tiles(const float* __restrict__ x, float*
             tile_pass1<false, true>(s_x, tv, sl, tid, len, dp, fm, B, st);
         double pnext;
         const double base = resolve_exact(P, B, st, tv, s_x, sl, tid, pnext);
-        tile_pass2<WQ, WC>(s_o, tv, s_tab, tid, base, L, fm, Xv, cw, kmax);
+        tile_pass2<WQ, WC, NIB>(s_o, tv, s_tab, tid, base, L, fm, Xv, cw, kmax);
         P = pnext;
     }
     __syncthreads();
     const uint32_t tp = (uint32_t)(te - 1) * (uint32_t)kQTile;
     if (WQ) store_tile_buf(s_o, ro, tp * 4u, tid);
     if (WC) {
-        store_codes_buf<CVEC>(rc, codes + vec * ldc, cw, tp, d, tid);
+        store_codes_buf<CVEC, NIB>(rc, codes + vec * ldc, cw, tp, d, tid);
         if (nseg == 1)
             store_kmax_block(kmax, L, overflow, vec, tid, reinterpret_cast<int*>(sl.wave));
         else
@@ -1414,7 +1422,7 @@ __device__ __forceinline__ void stream_tiles(const float* __restrict__ x, float*
     }
 }
 
-template <bool WQ, bool WC, bool CVEC>
+template <bool WQ, bool WC, bool CVEC, bool NIB = false>
 __global__ void __launch_bounds__(kQBlock, 4)
 quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int8_t* __restrict__ codes,
                        int32_t* __restrict__ overflow, int64_t d, int32_t tiles, float fm,
@@ -1429,8 +1437,8 @@ quantize_stream_kernel(const float* __restrict__ x, float* __restrict__ out, int
     const int32_t te = min(tiles, tb + seg_tiles);
     const float Xv = Xs ? Xs[vec] : Xval;            // one vector per call: X passed by value
     const double P = pre ? __longlong_as_double((long long)pre[vec * tiles + tb]) : 0.0;
-    stream_tiles<WQ, WC, CVEC>(x, out, codes, overflow, d, tb, te, fm, Xv, l1[vec], nseg, P, ldo, ldc, vec, s_x, s_o,
-                               s_tab, sl);
+    stream_tiles<WQ, WC, CVEC, NIB>(x, out, codes, overflow, d, tb, te, fm, Xv, l1[vec], nseg, P, ldo, ldc, vec, s_x,
+                                    s_o, s_tab, sl);
 }
 
 // torch CPU `f(x).sum()` of one vector shorter than GRAIN (one cascade, the same for every
@@ -2197,6 +2205,117 @@ codes_mean_kernel(const int8_t* __restrict__ codes, int64_t ldc, const float* __
     }
 }
 
+// ---- 4-bit type codes (the bench pipeline "codes4") ------------------------------------
+// uq_type_unbiased_nibbles_ld_f32 writes the type codes of K2 as 4-bit fields (element 2i in
+// the low nibble of byte i): the byte code's low nibble, i.e. k for sign >= 0 and 15 - k for
+// ~k, exact while k <= kNibMax.  At R <= 2 the counts stay below that for all but extreme
+// tails (k <= 2 at R = 1 for |x| < 11 sigma), and a client with kmax > kNibMax is read from q.
+// Half the code bytes of K2's write and K3's read: K2 1.69 -> 1.66 ms, K3 0.187 -> 0.148 ms on
+// the C2 batch (timing probe tools/exp/variants.py, profiles/r5ai_nibble_codes_probe.jsonl).
+constexpr int kNibMax = 7;
+constexpr int64_t kNibAlign = kCodesMeanThreads * kMeanCpt;   // d % 4096 == 0: whole mean threads
+
+__device__ __forceinline__ void nib_load_batch(uint32_t (&w)[kMeanUnroll], const uint8_t* cp, int64_t ldn) {
+#pragma unroll
+    for (int u = 0; u < kMeanUnroll; ++u) w[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(cp + (int64_t)u * ldn));
+}
+
+__device__ __forceinline__ void nib_add_batch(float (&e)[kMeanCpt], const uint32_t (&w)[kMeanUnroll],
+                                              const float (*tab)[16], int jj) {
+#pragma unroll
+    for (int u = 0; u < kMeanUnroll; ++u) {
+        const float* tb = tab[jj + u];
+#pragma unroll
+        for (int k = 0; k < kMeanCpt; ++k) e[k] += tb[(w[u] >> (4 * k)) & 0xFu];
+    }
+}
+
+// tab[jj][c]: nibble c of client j0 + jj = RN(RN(RN(L1*k)/m)/n_div) with k = c (c <= 7) and
+// its negation at c = 15 - k (the byte table's values, so est keeps K3c's bits)
+__device__ __forceinline__ void nib_build_tables(float (*tab)[16], const float* __restrict__ l1,
+                                                 const int32_t* __restrict__ kmaxv, int64_t j0, int nb, int wid,
+                                                 int lane, float fm, float n_div) {
+    for (int jj = wid; jj < nb; jj += kCodesMeanThreads / kWave) {
+        const float L = l1[j0 + jj];
+        const int km = min(kNibMax, max(0, kmaxv[j0 + jj]));
+        if (lane <= km) {
+            const float v = ((L * (float)lane) / fm) / n_div;
+            tab[jj][lane] = v;
+            tab[jj][15 - lane] = -v;
+        }
+    }
+}
+
+// K3n: est[i] (+)= q_j[i] / n_div, clients in order, from the 4-bit codes (4 bytes per client
+// per thread's 8 columns), double-buffered batches of kMeanUnroll clients as K3c.  d % 4096 ==
+// 0 (every thread's columns inside d).  Any client with kmax > kNibMax sends the launch down
+// the mixed loop: those clients add q[j][i] / n_div (q is required).
+__global__ void __launch_bounds__(kCodesMeanThreads)
+nibbles_mean_kernel(const uint8_t* __restrict__ nib, int64_t ldn, const float* __restrict__ l1,
+                    const int32_t* __restrict__ kmaxv, int64_t n, int64_t d, float fm, float n_div, int accumulate,
+                    float* __restrict__ est, const float* __restrict__ q, int64_t ldq) {
+    __shared__ float tab[kMeanClients][16];
+    __shared__ uint32_t s_ovf;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const int64_t i0 = ((int64_t)blockIdx.x * kCodesMeanThreads + tid) * kMeanCpt;
+    float e[kMeanCpt];
+    if (accumulate) {
+        const float4 a = *reinterpret_cast<const float4*>(est + i0), b = *reinterpret_cast<const float4*>(est + i0 + 4);
+        e[0] = a.x; e[1] = a.y; e[2] = a.z; e[3] = a.w; e[4] = b.x; e[5] = b.y; e[6] = b.z; e[7] = b.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kMeanCpt; ++k) e[k] = 0.0f;
+    }
+    if (tid == 0) s_ovf = 0u;
+    __syncthreads();
+    bool a = false;
+    for (int64_t j = tid; j < n; j += kCodesMeanThreads) a = a || kmaxv[j] > kNibMax;
+    if (a) s_ovf = 1u;
+    __syncthreads();
+    const bool any = s_ovf != 0u;
+    const uint8_t* cbase = nib + i0 / 2;
+    const int64_t groups = n / kMeanClients;
+    if (!any) {
+        uint32_t wa[kMeanUnroll], wb[kMeanUnroll];
+        if (groups > 0) nib_load_batch(wa, cbase, ldn);
+        for (int64_t g = 0; g < groups; ++g) {
+            const int64_t j0 = g * kMeanClients;
+            __syncthreads();
+            nib_build_tables(tab, l1, kmaxv, j0, kMeanClients, wid, lane, fm, n_div);
+            __syncthreads();
+            nib_load_batch(wb, cbase + (j0 + kMeanUnroll) * ldn, ldn);
+            nib_add_batch(e, wa, tab, 0);
+            const int64_t jn = (j0 + kMeanClients + kMeanUnroll <= n) ? j0 + kMeanClients : n - kMeanUnroll;
+            nib_load_batch(wa, cbase + jn * ldn, ldn);
+            nib_add_batch(e, wb, tab, kMeanUnroll);
+        }
+    }
+    for (int64_t j0 = any ? 0 : groups * kMeanClients; j0 < n; j0 += kMeanClients) {   // mixed / the rest
+        const int nb = (int)min((int64_t)kMeanClients, n - j0);
+        __syncthreads();
+        nib_build_tables(tab, l1, kmaxv, j0, nb, wid, lane, fm, n_div);
+        __syncthreads();
+        for (int jj = 0; jj < nb; ++jj) {
+            const int64_t j = j0 + jj;
+            if (kmaxv[j] > kNibMax) {
+                const float4 a4 = *reinterpret_cast<const float4*>(q + j * ldq + i0);
+                const float4 b4 = *reinterpret_cast<const float4*>(q + j * ldq + i0 + 4);
+                const float qq[kMeanCpt] = {a4.x, a4.y, a4.z, a4.w, b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+                for (int k = 0; k < kMeanCpt; ++k) e[k] += qq[k] / n_div;
+            } else {
+                const uint32_t w = *reinterpret_cast<const uint32_t*>(cbase + j * ldn);
+#pragma unroll
+                for (int k = 0; k < kMeanCpt; ++k) e[k] += tab[jj][(w >> (4 * k)) & 0xFu];
+            }
+        }
+    }
+    *reinterpret_cast<float4*>(est + i0) = make_float4(e[0], e[1], e[2], e[3]);
+    *reinterpret_cast<float4*>(est + i0 + 4) = make_float4(e[4], e[5], e[6], e[7]);
+}
+
 #include "uq_biased_kernels.h"
 #include "uq_biased_torch_ties.h"
 #include "uq_eden_kernels.h"
@@ -2882,15 +3001,17 @@ namespace {
 // draw passed by value in Xval (the per-call drop-in: no host-to-device copy of X).
 // Row j of q at out + j*ldo, of the codes at codes + j*ldc (ldo, ldc >= d: row pitches let the
 // caller stagger the rows' physical placement, see DMEPipeline).
+// nib: codes as 4-bit fields (uq_type_unbiased_nibbles_ld_f32; the caller checked the stream
+// form's conditions and ldc is then the row pitch in bytes of the packed rows).
 int unbiased_codes_impl(const float* x, float* out, int64_t ldo, int8_t* codes, int64_t ldc, int32_t* overflow,
                         int64_t n, int64_t d, int64_t m, const float* X, float Xval, const float* l1, float* l1_out,
-                        int32_t T, void* ws, size_t ws_bytes, void* stream) {
+                        int32_t T, void* ws, size_t ws_bytes, void* stream, bool nib = false) {
     L1Plan plan;
     WsLayout w;
     int rc = check_common(x, n, d, T, ws, ws_bytes, &plan, &w);
     if (rc) return rc;
     if (m < 0) return fail(UQ_E_INVALID, "m must be >= 0");
-    if ((out && ldo < d) || (codes && ldc < d)) return fail(UQ_E_INVALID, "row pitches must be >= d");
+    if ((out && ldo < d) || (codes && ldc < (nib ? d / 2 : d))) return fail(UQ_E_INVALID, "row pitches must be >= d");
     if (n == 0 || d == 0) return UQ_OK;
     if (!X && n != 1) return fail(UQ_E_INVALID, "null X");
     if (!out && !codes) return fail(UQ_E_INVALID, "nothing to write: out and codes are both NULL");
@@ -2900,7 +3021,7 @@ int unbiased_codes_impl(const float* x, float* out, int64_t ldo, int8_t* codes, 
     float* l1buf = (float*)(wsb + w.l1_off);
     const float* l1use = l1;
     const bool vec4s = aligned16(x) && (!out || aligned16(out)) && ((d % 4 == 0 && ldo % 4 == 0) || n == 1);
-    if (d <= kSmallL1Max && vec4s && n <= 0x7FFFFFFF) {
+    if (!nib && d <= kSmallL1Max && vec4s && n <= 0x7FFFFFFF) {
         // shorter than GRAIN: L1 (one torch cascade for any thread count) and the exact scan
         // in one workgroup per client, one launch
         const float fm = (float)m;
@@ -2938,6 +3059,12 @@ int unbiased_codes_impl(const float* x, float* out, int64_t ldo, int8_t* codes, 
     const bool cvec = !codes || (aligned16(codes) && d % 16 == 0 && (ldc % 16 == 0 || n == 1));
     const int wq = out ? 1 : 0, wc = codes ? 1 : 0;
     const int sel = (vec4 ? 8 : 0) | (wq ? 4 : 0) | (wc ? 2 : 0) | (cvec ? 1 : 0);
+    if (nib) {
+        if (!stream_form || !out || !codes) return fail(UQ_E_INVALID, "internal: 4-bit codes outside the stream form");
+        hipLaunchKernelGGL((quantize_stream_kernel<true, true, true, true>), dim3((unsigned)n), dim3(kQBlock), 0, st, x,
+                           out, codes, overflow, d, w.tiles, fm, X, Xval, l1use, w.tiles, 1, nullptr, ldo, ldc);
+        return hip_check(hipGetLastError(), "quantize_stream_kernel (4-bit codes) launch");
+    }
     if (stream_form) {
         // enough clients to fill the GPU: one workgroup per client vector
 #define UQ_STREAM(Q, C, CV)                                                                                 \
@@ -3048,6 +3175,37 @@ int uq_type_unbiased_codes_ld_f32(const float* x, float* out, int64_t ldq, int8_
     if (n > 0 && d > 0 && !X) return fail(UQ_E_INVALID, "null X");
     return unbiased_codes_impl(x, out, ldq, codes, ldc, overflow, n, d, m, X, 0.0f, l1, l1_out, T, ws, ws_bytes,
                                stream);
+}
+
+int uq_type_unbiased_nibbles_ld_f32(const float* x, float* out, int64_t ldq, uint8_t* nib, int64_t ldn,
+                                    int32_t* kmax, int64_t n, int64_t d, int64_t m, const float* X, const float* l1,
+                                    float* l1_out, int32_t T, void* ws, size_t ws_bytes, void* stream) {
+    if (n < 0 || d < 0) return fail(UQ_E_INVALID, "n and d must be >= 0");
+    if (n == 0 || d == 0) return UQ_OK;
+    if (!x || !out || !nib || !kmax || !X) return fail(UQ_E_INVALID, "null pointer (x, out, codes, kmax and X are required)");
+    if (n < kStreamMinClients || d % kNibAlign != 0 || d > ((int64_t)1 << 29))
+        return fail(UQ_E_INVALID, "4-bit codes need n >= 256 and d a multiple of 4096 (<= 2^29)");
+    if (ldq < d || ldq % 4 != 0 || ldn < d / 2 || ldn % 16 != 0 || !aligned16(x) || !aligned16(out) || !aligned16(nib))
+        return fail(UQ_E_INVALID, "4-bit codes need 16-byte aligned rows: ldq >= d, ldq % 4 == 0, ldn >= d/2, ldn % 16 == 0");
+    return unbiased_codes_impl(x, out, ldq, (int8_t*)nib, ldn, kmax, n, d, m, X, 0.0f, l1, l1_out, T, ws, ws_bytes,
+                               stream, true);
+}
+
+int uq_nibbles_q_mean_ld_f32(const uint8_t* nib, int64_t ldn, const float* q, int64_t ldq, const float* l1,
+                             const int32_t* kmax, int64_t n, int64_t d, int64_t m, float n_div, int32_t accumulate,
+                             float* est, void* stream) {
+    if (n < 0 || d < 0 || m < 0) return fail(UQ_E_INVALID, "n, d and m must be >= 0");
+    if (d == 0) return UQ_OK;
+    if (!est || (n > 0 && (!nib || !l1 || !kmax || !q))) return fail(UQ_E_INVALID, "null pointer (q is required)");
+    if (d % kNibAlign != 0 || ldq < d || ldq % 4 != 0 || ldn < d / 2 || ldn % 4 != 0 || !aligned16(est) ||
+        (n > 0 && (!aligned16(q) || ((uintptr_t)nib & 3u))))
+        return fail(UQ_E_INVALID, "4-bit code mean: d % 4096 == 0, ldq >= d (multiple of 4), ldn >= d/2 (multiple of 4), "
+                                  "16-byte aligned est and q");
+    const int64_t blocks = d / (kCodesMeanThreads * kMeanCpt);
+    if (blocks > 0x7FFFFFFF) return fail(UQ_E_INVALID, "d too large");
+    hipLaunchKernelGGL(nibbles_mean_kernel, dim3((unsigned)blocks), dim3(kCodesMeanThreads), 0, (hipStream_t)stream, nib,
+                       ldn, l1, kmax, n, d, (float)m, n_div, accumulate, est, q, ldq);
+    return hip_check(hipGetLastError(), "nibbles_mean_kernel launch");
 }
 
 int uq_type_unbiased_codes_f32(const float* x, float* out, int8_t* codes, int32_t* overflow, int64_t n, int64_t d,

@@ -12,6 +12,11 @@ Pipelines (what K2 writes and what the mean reads; est has the same bits in all 
     "q"       q only; the mean reads q (4 B per coordinate) -- the drop-in's output form
     "encode"  codes only (no q); the mean reads the codes.  An overflowed client cannot be
               recovered without q: check_status() raises OverflowError for it.
+    "codes4"  q and the type codes as 4-bit fields (p.nib, uint8 [n, d/2]: the int8 code's low
+              nibble, exact for counts <= 7 -- every client at R <= 2 but for extreme tails);
+              the mean reads the nibbles (0.5 B per coordinate) and a client with kmax > 7
+              from q (uq_nibbles_q_mean_ld_f32).  n >= 256 and d % 4096 == 0 (stream form).
+              `codes4_fits(n, d, bits)` says when it applies; the bench's default.
 
 Output placement.  K2 writes q (4*d B per client) and the int8 codes (1*d) while reading x.
 On MI355X its time depends on where the OUTPUT buffers land in physical memory: with x fixed
@@ -38,9 +43,16 @@ import torch
 from . import _lib
 from .rates import rate_to_m
 
-__all__ = ["DMEPipeline", "PIPELINES"]
+__all__ = ["DMEPipeline", "PIPELINES", "codes4_fits"]
 
-PIPELINES = ("codes", "q", "encode")
+PIPELINES = ("codes", "q", "encode", "codes4")
+
+
+def codes4_fits(n: int, d: int, bits_per_dimension=1) -> bool:
+    """The 4-bit code pipeline's shape conditions, and a rate whose counts stay <= 7 for
+    Gaussian-like clients (m <= 0.64 d: R <= 2)."""
+    from .rates import RATE_TABLE
+    return n >= 256 and d % 4096 == 0 and d <= (1 << 29) and RATE_TABLE.get(bits_per_dimension, 1e9) <= 0.64
 
 
 def _p(t) -> int:
@@ -54,6 +66,8 @@ class DMEPipeline:
             raise RuntimeError("uqdme requires a ROCm GPU (no CPU fallback by design)")
         if pipeline not in PIPELINES:
             raise ValueError(f"pipeline must be one of {PIPELINES}")
+        if pipeline == "codes4" and not (n >= 256 and d % 4096 == 0 and d <= (1 << 29)):
+            raise ValueError("pipeline 'codes4' needs n >= 256 and d a multiple of 4096 (<= 2^29)")
         self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.n, self.d = int(n), int(d)
         self.m = int(m) if m is not None else rate_to_m(bits_per_dimension, d)
@@ -67,9 +81,12 @@ class DMEPipeline:
         self.l1 = torch.empty(self.n, dtype=torch.float32, device=self.dev)
         self.kmax = torch.zeros(self.n, dtype=torch.int32, device=self.dev)
         self.est = torch.empty(self.d, dtype=torch.float32, device=self.dev)
-        self.q, self.codes = self._alloc_outputs()
+        self.codes = self.nib = None
+        self.q, c = self._alloc_outputs()
+        self._set_codes(c)
         self.probe_report = None
         self._codes_valid = False       # the last K2 launch wrote codes (and kmax)
+        self._nib_valid = False         # ... as 4-bit fields
         self._mean_without_q = False    # the last mean read codes with no q to fall back to
 
     @property
@@ -77,10 +94,31 @@ class DMEPipeline:
         return self.pipeline != "encode"
 
     # ---- buffers ---------------------------------------------------------------------
+    def _alloc_codes(self, pipeline):
+        if pipeline == "codes4":
+            return torch.empty((self.n, self.d // 2), dtype=torch.uint8, device=self.dev)
+        return torch.empty((self.n, self.d), dtype=torch.int8, device=self.dev) if pipeline != "q" else None
+
     def _alloc_outputs(self):
         q = torch.empty((self.n, self.d), dtype=torch.float32, device=self.dev) if self.write_q else None
-        c = torch.empty((self.n, self.d), dtype=torch.int8, device=self.dev) if self.pipeline != "q" else None
-        return q, c
+        return q, self._alloc_codes(self.pipeline)
+
+    def _set_codes(self, c):
+        if self.pipeline == "codes4":
+            self.nib = c
+        else:
+            self.codes = c
+
+    def _codes_for(self, pl):
+        """The code buffer a launch of pipeline `pl` uses (int8 codes or 4-bit fields), made on
+        first use when a step overrides the pipeline's own kind."""
+        if pl == "codes4":
+            if self.nib is None:
+                self.nib = self._alloc_codes("codes4")
+            return self.nib
+        if self.codes is None:
+            self.codes = self._alloc_codes("codes")
+        return self.codes
 
     @staticmethod
     def _ld(t) -> int:
@@ -100,11 +138,20 @@ class DMEPipeline:
         this launch ("q": q only, "encode": codes only, "codes": both)."""
         pl = pipeline or self.pipeline
         q = (self.q if q is None else q) if pl != "encode" else None
-        codes = (self.codes if codes is None else codes) if pl != "q" else None
         if pl != "encode" and q is None:
             raise ValueError("this pipeline holds no q buffer")
-        if pl != "q" and codes is None:
-            raise ValueError("this pipeline holds no codes buffer (pipeline 'q')")
+        if pl == "codes4":
+            nib = self._codes_for(pl) if codes is None else codes
+            _lib.check(self.lib.uq_type_unbiased_nibbles_ld_f32(_p(x), _p(q), max(self._ld(q), self.d), _p(nib),
+                                                                max(self._ld(nib), self.d // 2), _p(self.kmax), self.n,
+                                                                self.d, self.m, _p(X), _p(self.l1), None, self.T,
+                                                                _p(self.ws), self.ws_bytes, self._stream()),
+                       "uq_type_unbiased_nibbles_ld_f32")
+            self._codes_valid = True
+            self._nib_valid = True
+            return
+        self._nib_valid = False
+        codes = (self._codes_for(pl) if codes is None else codes) if pl != "q" else None
         _lib.check(self.lib.uq_type_unbiased_codes_ld_f32(_p(x), _p(q), max(self._ld(q), self.d), _p(codes),
                                                           max(self._ld(codes), self.d),
                                                           _p(self.kmax if codes is not None else None), self.n, self.d,
@@ -122,6 +169,12 @@ class DMEPipeline:
             _lib.check(self.lib.uq_client_mean_f32(_p(self.q), self.n, self.d, max(self._ld(self.q), self.d),
                                                    float(n_div), int(bool(accumulate)), _p(est), self._stream()),
                        "uq_client_mean_f32")
+        elif pl == "codes4":
+            self._mean_without_q = False
+            _lib.check(self.lib.uq_nibbles_q_mean_ld_f32(_p(self.nib), max(self._ld(self.nib), self.d // 2), _p(self.q),
+                                                         max(self._ld(self.q), self.d), _p(self.l1), _p(self.kmax),
+                                                         self.n, self.d, self.m, float(n_div), int(bool(accumulate)),
+                                                         _p(est), self._stream()), "uq_nibbles_q_mean_ld_f32")
         else:
             q = self.q if pl == "codes" else None
             self._mean_without_q = q is None
@@ -174,8 +227,9 @@ class DMEPipeline:
         caller allocating fresh outputs gets on average)."""
         self._check(x, X)
         self.l1_norms(x)
-        sets, times = [(self.q, self.codes)], []
-        set_bytes = self.n * self.d * ((4 if self.write_q else 0) + (1 if self.pipeline != "q" else 0))
+        sets, times = [(self.q, self.nib if self.pipeline == "codes4" else self.codes)], []
+        code_bytes = {"q": 0.0, "codes4": 0.5}.get(self.pipeline, 1.0)
+        set_bytes = int(self.n * self.d * ((4 if self.write_q else 0) + code_bytes))
 
         def time_set(q, c):
             for _ in range(2):
@@ -205,7 +259,8 @@ class DMEPipeline:
             if capped:
                 break
         best = min(range(len(sets)), key=lambda i: times[i])
-        self.q, self.codes = sets[best]
+        self.q, c = sets[best]
+        self._set_codes(c)
         del sets
         torch.cuda.empty_cache()
         self.probe_report = {"candidates": len(times), "k2_ms": [round(t, 4) for t in times], "chosen": best,
@@ -215,10 +270,11 @@ class DMEPipeline:
         return self.probe_report
 
     def overflowed(self) -> int:
-        """Clients of the last step whose counts overflowed their int8 codes (synchronises)."""
+        """Clients of the last step whose counts overflowed their codes (int8: > 127; 4-bit:
+        > 7, read from q by the mean) (synchronises)."""
         if not self._codes_valid:
             return 0
-        return int(torch.count_nonzero(self.kmax > 127).item())
+        return int(torch.count_nonzero(self.kmax > (7 if self._nib_valid else 127)).item())
 
     def check_status(self):
         """Synchronise; raise if an in-kernel wait timed out, or if the last mean was taken
