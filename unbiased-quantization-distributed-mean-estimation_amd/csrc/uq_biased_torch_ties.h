@@ -555,6 +555,8 @@ constexpr int64_t kTieLevelMin = kTieLdsPairs;   // shorter ranges finish in rez
 // 256 threads through generic pointers: 4.63 on the same box as this form's 4.59.)
 constexpr int64_t kTieLevelStop = 16384;
 constexpr int kTieLevelMargin = 3;
+// KB6's first part waits for this many KB7a levels (launch_torch_ties' `mid`)
+constexpr int kTieHeavyLevels = 2;
 constexpr int64_t kTieLevelMinClients = 32;      // KB7a for batches of at least this many clients
 // ... and for any batch of vectors this long: one replay workgroup walking 2^22 keys took
 // ~9 ms (a 6-client batch at d = 2^22 with one ambiguous client), KB7a's idle launches 0.35 ms
@@ -623,6 +625,41 @@ __device__ __forceinline__ KtLevel kt_level(int a, int64_t d, uint32_t nlist, co
         v.act = v.filled && !t.err && v.depth > 0 && v.last - v.first > stop;
     }
     return v;
+}
+
+// One wave's segment [s0, s1) of a level: its stop counts with the median move substituted
+// (sub: the segment holds `first` or mpos); L0: keys from x, and the queue written (d < 2^31:
+// 32-bit indices; the 64-bit index arithmetic was most of this loop's VALU work).
+template <bool L0>
+__device__ __forceinline__ void kt_count_seg(const float* __restrict__ xv, const DivPlan& dp, float fm, bool up,
+                                             uint32_t* __restrict__ K, uint32_t* __restrict__ I, int32_t s0, int32_t s1,
+                                             int32_t first, int32_t mpos, uint32_t piv, uint32_t kfirst, bool sub,
+                                             int lane, uint32_t& cl, uint32_t& cr) {
+    for (int32_t b = s0; b < s1; b += 64 * kTieU) {
+        uint32_t kk[kTieU];
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int32_t i = b + u * 64 + lane;
+            float kp;
+            kk[u] = i < s1 ? (L0 ? rez_elem(xv[i], dp, fm, up, kp) : K[i]) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kTieU; ++u) {
+            const int32_t i = b + u * 64 + lane;
+            if (i >= s1) continue;
+            uint32_t key = kk[u], idx = (uint32_t)i;
+            if (sub) {
+                if (i == first) { key = piv; idx = (uint32_t)mpos; }
+                else if (i == mpos) { key = kfirst; idx = (uint32_t)first; }
+            }
+            if (L0) {
+                K[i] = key;
+                I[i] = idx;
+            }
+            cl += ((!sub || i > first) && key <= piv) ? 1u : 0u;
+            cr += (key >= piv) ? 1u : 0u;
+        }
+    }
 }
 
 // level step 1: the pivot and the left / right stop counts per segment (cnt [slots][kTieSegs]
@@ -715,30 +752,12 @@ kt_count_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
         kt_seg(v.first, v.last, sg, s0, s1);
         const bool sub = mpos >= 0 && ((v.first >= s0 && v.first < s1) || (mpos >= s0 && mpos < s1));
         uint32_t cl = 0, cr = 0;
-        for (int64_t b = s0; b < s1; b += 64 * kTieU) {
-            uint32_t kk[kTieU];
-#pragma unroll
-            for (int u = 0; u < kTieU; ++u) {
-                const int64_t i = b + (int64_t)u * 64 + lane;
-                kk[u] = i < s1 ? key_at(i) : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < kTieU; ++u) {
-                const int64_t i = b + (int64_t)u * 64 + lane;
-                if (i >= s1) continue;
-                uint32_t key = kk[u], idx = (uint32_t)i;
-                if (sub) {
-                    if (i == v.first) { key = piv; idx = (uint32_t)mpos; }
-                    else if (i == mpos) { key = kfirst; idx = (uint32_t)v.first; }
-                }
-                if (level0) {
-                    K[i] = key;
-                    I[i] = idx;
-                }
-                cl += ((!sub || i > v.first) && key <= piv) ? 1u : 0u;
-                cr += (key >= piv) ? 1u : 0u;
-            }
-        }
+        if (level0)
+            kt_count_seg<true>(xv, dp, fm, up, K, I, (int32_t)s0, (int32_t)s1, (int32_t)v.first, (int32_t)mpos, piv,
+                               kfirst, sub, lane, cl, cr);
+        else
+            kt_count_seg<false>(xv, dp, fm, up, K, I, (int32_t)s0, (int32_t)s1, (int32_t)v.first, (int32_t)mpos, piv,
+                                kfirst, sub, lane, cl, cr);
         if (!v.act) continue;                           // level 0 fill of a slot whose range is short
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -789,20 +808,21 @@ kt_list_kernel(int64_t d, const uint32_t* __restrict__ qbuf, uint32_t* __restric
         // the median move as a substitution: only the (at most two) segments holding `first`
         // or mpos take the slow form (wave-uniform)
         const bool sub = (first >= s0 && first < s1) || (mpos >= s0 && mpos < s1);
-        for (int64_t b = s0; b < s1; b += 64 * kTieU) {
+        const int32_t e1 = (int32_t)s1, f32 = (int32_t)first, m32 = (int32_t)mpos;      // d < 2^31
+        for (int32_t b = (int32_t)s0; b < e1; b += 64 * kTieU) {
             uint32_t kk[kTieU];
 #pragma unroll
             for (int u = 0; u < kTieU; ++u) {
-                const int64_t i = b + (int64_t)u * 64 + lane;
-                kk[u] = i < s1 ? K[i] : 0u;
+                const int32_t i = b + u * 64 + lane;
+                kk[u] = i < e1 ? K[i] : 0u;
             }
 #pragma unroll
             for (int u = 0; u < kTieU; ++u) {
-                const int64_t i = b + (int64_t)u * 64 + lane;
+                const int32_t i = b + u * 64 + lane;
                 uint32_t key = kk[u];
-                if (sub) key = i == first ? piv : (i == mpos ? kfirst : key);
-                const bool lf = i < s1 && (!sub || i > first) && key <= piv;
-                const bool rf = i < s1 && key >= piv;
+                if (sub) key = i == f32 ? piv : (i == m32 ? kfirst : key);
+                const bool lf = i < e1 && (!sub || i > f32) && key <= piv;
+                const bool rf = i < e1 && key >= piv;
                 const uint64_t ml = __ballot(lf), mr = __ballot(rf);
                 if (lf) Lpos[ol + __popcll(ml & lt)] = (uint32_t)i;
                 if (rf) Rpos[orr + __popcll(mr & lt)] = (uint32_t)i;
@@ -908,25 +928,25 @@ kt_swap_kernel(int64_t d, uint32_t* __restrict__ qbuf, const uint32_t* __restric
     uint32_t* I = K + dpad;
     const uint32_t* Lpos = pos + (size_t)a * 2 * d;
     const uint32_t* Rpos = Lpos + d;
-    const int64_t J = t.J, nR = t.nR;
+    const int32_t J = (int32_t)t.J, nR = (int32_t)t.nR;      // d < 2^31
     const int tid = threadIdx.x;
-    for (int64_t j0 = c * 256 * kB; j0 < J; j0 += C * 256 * kB) {
+    for (int32_t j0 = (int32_t)c * 256 * kB; j0 < J; j0 += (int32_t)C * 256 * kB) {
         uint32_t pa[kB], pb[kB], ka[kB], kb[kB], ia[kB], ib[kB];
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            const int64_t j = j0 + (int64_t)u * 256 + tid;
+            const int32_t j = j0 + u * 256 + tid;
             pa[u] = j < J ? Lpos[j] : 0u;
             pb[u] = j < J ? Rpos[nR - 1 - j] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < kB; ++u)
-            if (j0 + (int64_t)u * 256 + tid < J) {
+            if (j0 + u * 256 + tid < J) {
                 ka[u] = K[pa[u]]; ia[u] = I[pa[u]];
                 kb[u] = K[pb[u]]; ib[u] = I[pb[u]];
             }
 #pragma unroll
         for (int u = 0; u < kB; ++u)
-            if (j0 + (int64_t)u * 256 + tid < J) {
+            if (j0 + u * 256 + tid < J) {
                 K[pa[u]] = kb[u]; I[pa[u]] = ib[u];
                 K[pb[u]] = ka[u]; I[pb[u]] = ia[u];
             }

@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -2736,7 +2737,7 @@ int eden_check(int64_t n, int64_t dim, int32_t nbits, const int8_t* signs, EdenT
 // beside the caller's stream inside one call; joined back before the call returns.
 struct SideStream {
     hipStream_t s;
-    hipEvent_t fork, join;
+    hipEvent_t fork, join, mid;         // mid: KB7a's bandwidth-heavy first levels done
     uint32_t* count;            // pinned host word (UQ_TIES_HOST_CHECK reads the tie list's length)
     void* states;               // pinned host RezStates (the small-vector path's flags), kSmallCheckMaxN
 };
@@ -2760,6 +2761,8 @@ int side_stream(SideStream** out) {
         rc = hip_check(hipEventCreateWithFlags(&cache[dev].fork, hipEventDisableTiming), "create event");
         if (rc) return rc;
         rc = hip_check(hipEventCreateWithFlags(&cache[dev].join, hipEventDisableTiming), "create event");
+        if (rc) return rc;
+        rc = hip_check(hipEventCreateWithFlags(&cache[dev].mid, hipEventDisableTiming), "create event");
         if (rc) return rc;
         rc = hip_check(hipHostMalloc((void**)&cache[dev].count, sizeof(uint32_t), hipHostMallocDefault), "pinned word");
         if (rc) return rc;
@@ -2805,7 +2808,7 @@ int level_graph(const LevelPtrs& wsb, int64_t d, unsigned S, int levels, hipStre
         LevelPtrs wsb;
         int64_t d;
         unsigned S;
-        int levels;
+        int levels;                     // lv0 * 256 + lv1: the captured range of levels
         hipGraphExec_t exec;
     };
     static thread_local Entry cache[8] = {};
@@ -2843,8 +2846,13 @@ int level_graph(const LevelPtrs& wsb, int64_t d, unsigned S, int levels, hipStre
     return UQ_OK;
 }
 
+// mid (may be empty): called once KB7a's first kTieHeavyLevels levels are enqueued on `st`
+// (with KB7a; before anything else otherwise) -- the fork records an event there and lets KB6
+// part 1 wait for it, so the bandwidth-heavy first levels (the listed clients' full rows)
+// do not share HBM with KB6 and KB6 runs beside the later, latency-bound levels instead.
 int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, float fm, RezState* state,
-                      uint32_t* bits, char* wsb, const BiasedLayout& w, hipStream_t st, const TieLevelState** tls_out) {
+                      uint32_t* bits, char* wsb, const BiasedLayout& w, hipStream_t st, const TieLevelState** tls_out,
+                      const std::function<int()>& mid) {
     *tls_out = nullptr;
     int rc = UQ_OK;
     uint32_t* list = (uint32_t*)(wsb + w.list_off);
@@ -2856,6 +2864,7 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     // one-workgroup replay takes milliseconds; a few-client call at smaller d (the per-vector
     // drop-ins) replays in one kernel when it has to
     if (d <= kTieLevelMin || (n < kTieLevelMinClients && d < kTieLevelBigD)) {
+        if (mid && (rc = mid())) return rc;
         hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
                            state, bits, qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)nullptr, 0,
                            (uint32_t*)(wsb + w.tcnt_off), w.tiles, g_force_replay_failure.load());
@@ -2891,8 +2900,15 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     hipLaunchKernelGGL(kt_count_kernel, dim3(lgrid), dim3(256), 0, st, x, d, l1, fm, (const RezState*)state, qbuf, list,
                        tls, cnt, alist, bits, (int)S, tie_stop, 1);
     if ((rc = hip_check(hipGetLastError(), "kt_count_kernel launch"))) return rc;
+    static const int heavy = [] {
+        const char* e = std::getenv("UQDME_TIE_HEAVY");
+        const int v = e ? std::atoi(e) : -1;
+        return v >= 0 && v <= 16 ? v : kTieHeavyLevels;
+    }();
+    const int lsplit = std::min(heavy, levels);
+    int lv0 = 0, lv1 = levels;                  // the range levels_on enqueues
     auto levels_on = [&](hipStream_t ls) {
-        for (int lv = 0; lv < levels; ++lv) {
+        for (int lv = lv0; lv < lv1; ++lv) {
             if (lv > 0)
                 hipLaunchKernelGGL(kt_count_kernel, dim3(lgrid), dim3(256), 0, ls, (const float*)nullptr, d,
                                    (const float*)nullptr, fm, (const RezState*)nullptr, qbuf, list, tls, cnt, alist,
@@ -2907,14 +2923,19 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     // listed) is replayed as a captured HIP graph: its arguments are workspace pointers, d, S
     // and the stop only, so one capture serves every call on the same workspace (per-call
     // host cost was ~65 launches, more than the chain's GPU time for a few-client call).
-    hipGraphExec_t exec = nullptr;
-    rc = level_graph(LevelPtrs{qbuf, list, tls, cnt, pos, alist}, d, S, levels, st, levels_on, &exec);
-    if (rc) return rc;
-    if (exec) {
-        if ((rc = hip_check(hipGraphLaunch(exec, st), "KB7a level graph launch"))) return rc;
-    } else if ((rc = levels_on(st))) {
-        return rc;
-    }
+    auto run_levels = [&](int a, int b) {
+        if (a >= b) return (int)UQ_OK;
+        lv0 = a;
+        lv1 = b;
+        hipGraphExec_t exec = nullptr;
+        int grc = level_graph(LevelPtrs{qbuf, list, tls, cnt, pos, alist}, d, S, a * 256 + b, st, levels_on, &exec);
+        if (grc) return grc;
+        if (exec) return hip_check(hipGraphLaunch(exec, st), "KB7a level graph launch");
+        return levels_on(st);
+    };
+    if ((rc = run_levels(0, lsplit))) return rc;
+    if (mid && (rc = mid())) return rc;
+    if ((rc = run_levels(lsplit, levels))) return rc;
     hipLaunchKernelGGL(kt_mark_kernel, dim3(kTieMarkSegs, S), dim3(256), 0, st, d, qbuf, list, state, tls, bits);
     if ((rc = hip_check(hipGetLastError(), "kt_mark_kernel launch"))) return rc;
     hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3(S), dim3(kTieThreads), 0, st, x, d, l1, fm, state, bits,
@@ -3629,7 +3650,7 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         if (rc) return rc;
         if (*sb->count != 0u) {
             const TieLevelState* tls = nullptr;
-            rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, st, &tls);
+            rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, st, &tls, nullptr);
             if (rc) return rc;
             if (tls && (rc = launch_torch_ties_rest(x, d, l1buf, fm, state, bits, wsb, w, tls, st))) return rc;
             if ((rc = output_listed(st))) return rc;
@@ -3649,14 +3670,17 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         if (rc) return rc;
         rc = hip_check(hipStreamWaitEvent(sb->s, sb->fork, 0), "wait fork");
         if (rc) return rc;
-        // KB6 for the clients without a tie is enqueued first: the side chain below is ~60
-        // short launches, and the GPU must not idle while the host issues them.  No tie counts:
-        // every ambiguous client is listed and replayed (a failed replay counts its own tiles;
-        // the launch was 66 us of early-exit workgroups beside the chain)
-        rc = output(st, 1);
-        if (rc) return rc;
+        // KB6 for the clients without a tie waits for KB7a's first (bandwidth-heavy) levels
+        // and then runs beside the later, latency-bound ones (the chain is the critical path).
+        // No tie counts: every ambiguous client is listed and replayed (a failed replay counts
+        // its own tiles; the launch was 66 us of early-exit workgroups beside the chain)
         const TieLevelState* tls = nullptr;
-        rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls);
+        rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls, [&]() {
+            int mrc = hip_check(hipEventRecord(sb->mid, sb->s), "record mid");
+            if (!mrc) mrc = hip_check(hipStreamWaitEvent(st, sb->mid, 0), "wait mid");
+            if (!mrc) mrc = output(st, 1);
+            return mrc;
+        });
         if (rc) return rc;
         rc = hip_check(hipEventRecord(sb->join, sb->s), "record join");
         if (rc) return rc;
