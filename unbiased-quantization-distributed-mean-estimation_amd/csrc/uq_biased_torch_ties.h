@@ -182,20 +182,20 @@ __device__ __forceinline__ int floor_log2_i64(int64_t n) {
 }
 
 // Stops of [s0, s1) (one wave's segment) in index order: FN(i, left, right) per element,
-// lanes own i = b + u*64 + lane, kTieU loads in flight.
+// lanes own i = b + u*64 + lane, kTieU loads in flight.  (Indices are 32-bit: d < 2^31.)
 template <class Q, class FN>
-__device__ __forceinline__ void tt_scan_segment(const Q& A, int64_t first, int64_t s0, int64_t s1, uint32_t piv,
+__device__ __forceinline__ void tt_scan_segment(const Q& A, int32_t first, int32_t s0, int32_t s1, uint32_t piv,
                                                 int lane, FN&& fn) {
-    for (int64_t b = s0; b < s1; b += (int64_t)kWave * kTieU) {
+    for (int32_t b = s0; b < s1; b += kWave * kTieU) {
         uint32_t k[kTieU];
 #pragma unroll
         for (int u = 0; u < kTieU; ++u) {
-            const int64_t i = b + (int64_t)u * kWave + lane;
+            const int32_t i = b + u * kWave + lane;
             k[u] = i < s1 ? A.key(i) : 0u;
         }
 #pragma unroll
         for (int u = 0; u < kTieU; ++u) {
-            const int64_t i = b + (int64_t)u * kWave + lane;
+            const int32_t i = b + u * kWave + lane;
             const bool valid = i < s1 && i >= first;
             fn(i, valid && i > first && k[u] <= piv,      // left stop:  !comp(A[i], pivot)
                valid && k[u] >= piv);                     // right stop: !comp(pivot, A[i])
@@ -206,38 +206,39 @@ __device__ __forceinline__ void tt_scan_segment(const Q& A, int64_t first, int64
 // One unguarded Hoare partition of [first+1, last) around the pivot at `first` (indices
 // relative to the queue view; positions listed as PosT).  Each wave lists the stops of
 // its contiguous segment: one counting pass, a 16-entry prefix, one listing pass.
-// Returns the cut, or -1 on an internal inconsistency.
+// Returns the cut, or -1 on an internal inconsistency.  32-bit index arithmetic (d < 2^31).
 template <class Q, typename PosT, typename PosPtr, int NT>
-__device__ int64_t tt_partition(const Q& A, PosPtr Lpos, PosPtr Rpos, int64_t first, int64_t last,
+__device__ int64_t tt_partition(const Q& A, PosPtr Lpos, PosPtr Rpos, int64_t first64, int64_t last64,
                                 uint32_t piv, TieShared& sh) {
     TT_DECL();
     TT_T0();
+    const int32_t first = (int32_t)first64, last = (int32_t)last64;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     // segments start at multiples of 4 (16-byte aligned in the 16-byte aligned view); indices
     // below `first` belong to no stop list
-    const int64_t a0 = first & ~(int64_t)3;
+    const int32_t a0 = first & ~3;
     constexpr int NW = NT / kWave;
-    const int64_t seg = ((((last - a0) + NW - 1) / NW) + 4 * kWave - 1) & ~(int64_t)(4 * kWave - 1);
-    const int64_t s0 = std::min<int64_t>(last, a0 + (int64_t)w * seg);
-    const int64_t s1 = std::min<int64_t>(last, s0 + seg);
+    const int32_t seg = ((((last - a0) + NW - 1) / NW) + 4 * kWave - 1) & ~(4 * kWave - 1);
+    const int32_t s0 = min(last, a0 + w * seg);
+    const int32_t s1 = min(last, s0 + seg);
     uint32_t cl = 0, cr = 0;
     {   // counting pass: 4 keys per lane and load, lane-local counts, one wave reduction
         constexpr int kCU = 4;
-        for (int64_t b = s0; b < s1; b += (int64_t)kWave * 4 * kCU) {
+        for (int32_t b = s0; b < s1; b += kWave * 4 * kCU) {
             uint4 kv[kCU];
 #pragma unroll
             for (int u = 0; u < kCU; ++u) {
-                const int64_t q = b + 4 * ((int64_t)u * kWave + lane);
+                const int32_t q = b + 4 * (u * kWave + lane);
                 kv[u] = q < s1 ? A.key4(q) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < kCU; ++u) {
-                const int64_t q = b + 4 * ((int64_t)u * kWave + lane);
+                const int32_t q = b + 4 * (u * kWave + lane);
                 const uint32_t k4[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const int64_t i = q + c;
+                    const int32_t i = q + c;
                     const bool in = i < s1 && i >= first;
                     cl += (in && i > first && k4[c] <= piv) ? 1u : 0u;
                     cr += (in && k4[c] >= piv) ? 1u : 0u;
@@ -264,7 +265,7 @@ __device__ int64_t tt_partition(const Q& A, PosPtr Lpos, PosPtr Rpos, int64_t fi
         nL += a;
         nR += b;
     }
-    tt_scan_segment(A, first, s0, s1, piv, lane, [&](int64_t i, bool lf, bool rf) {
+    tt_scan_segment(A, first, s0, s1, piv, lane, [&](int32_t i, bool lf, bool rf) {
         const uint64_t ml = __ballot(lf), mr = __ballot(rf);
         if (lf) Lpos[ol + __popcll(ml & lt)] = (PosT)i;
         if (rf) Rpos[orr + __popcll(mr & lt)] = (PosT)i;
@@ -275,33 +276,34 @@ __device__ int64_t tt_partition(const Q& A, PosPtr Lpos, PosPtr Rpos, int64_t fi
     TT_ACC(1);
     // J = number of swaps = largest J with L_J < R_J (1-based; R counted from the right),
     // found by a block-parallel search (the predicate holds for a prefix of J).
-    int64_t lo = 0, hi = nL < nR ? nL : nR;
+    int32_t lo = 0, hi = (int32_t)(nL < nR ? nL : nR);
+    const int32_t nRi = (int32_t)nR;
     while (lo < hi) {
-        const int64_t step = (hi - lo + NT - 1) / NT;
-        const int64_t cand = lo + (int64_t)(tid + 1) * step;
-        const bool f = cand <= hi && (int64_t)Lpos[cand - 1] < (int64_t)Rpos[nR - cand];
+        const int32_t step = (hi - lo + NT - 1) / NT;
+        const int32_t cand = lo + (tid + 1) * step;
+        const bool f = cand <= hi && (int32_t)Lpos[cand - 1] < (int32_t)Rpos[nRi - cand];
         const int cnt = __syncthreads_count(f);
         if (cnt == 0) {
             hi = lo + step - 1;
         } else {
-            lo = lo + (int64_t)cnt * step;
-            hi = std::min<int64_t>(hi, lo + step - 1);
+            lo = lo + cnt * step;
+            hi = min(hi, lo + step - 1);
         }
     }
     TT_ACC(2);
-    const int64_t J = lo;
-    int64_t cut = INT64_MAX;
-    if (J < (int64_t)nL) cut = (int64_t)Lpos[J];
-    if (J > 0) cut = std::min<int64_t>(cut, (int64_t)Rpos[nR - J]);
+    const int32_t J = lo;
+    int32_t cut = INT32_MAX;
+    if (J < (int32_t)nL) cut = (int32_t)Lpos[J];
+    if (J > 0) cut = min(cut, (int32_t)Rpos[nRi - J]);
     // the J swaps are disjoint pairs: kTieU of them per lane, independent loads
-    for (int64_t j0 = 0; j0 < J; j0 += (int64_t)NT * kTieU) {
-        int64_t a[kTieU], b[kTieU];
+    for (int32_t j0 = 0; j0 < J; j0 += NT * kTieU) {
+        int32_t a[kTieU], b[kTieU];
         uint32_t ka[kTieU], kb[kTieU], ia[kTieU], ib[kTieU];
 #pragma unroll
         for (int u = 0; u < kTieU; ++u) {
-            const int64_t j = j0 + (int64_t)u * NT + tid;
-            a[u] = j < J ? (int64_t)Lpos[j] : -1;
-            b[u] = j < J ? (int64_t)Rpos[nR - 1 - j] : -1;
+            const int32_t j = j0 + u * NT + tid;
+            a[u] = j < J ? (int32_t)Lpos[j] : -1;
+            b[u] = j < J ? (int32_t)Rpos[nRi - 1 - j] : -1;
         }
 #pragma unroll
         for (int u = 0; u < kTieU; ++u)
@@ -318,7 +320,7 @@ __device__ int64_t tt_partition(const Q& A, PosPtr Lpos, PosPtr Rpos, int64_t fi
     }
     __syncthreads();
     TT_ACC(3);
-    return (cut <= first || cut >= last) ? -1 : cut;
+    return (cut <= first || cut >= last) ? -1 : (int64_t)cut;
 }
 
 // introselect's main loop on the queue view (element i of the vector at view index i - o)
