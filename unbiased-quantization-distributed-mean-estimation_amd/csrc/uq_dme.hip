@@ -2232,34 +2232,37 @@ __device__ __forceinline__ void nib_add_batch(float (&e)[kMeanCpt], const uint32
 }
 
 // tab[jj][c]: nibble c of client j0 + jj = RN(RN(RN(L1*k)/m)/n_div) with k = c (c <= 7) and
-// its negation at c = 15 - k (the byte table's values, so est keeps K3c's bits)
+// its negation at c = 15 - k (the byte table's values, so est keeps K3c's bits).  All nb
+// clients of a chunk at once, entries spread over the workgroup: one round of l1 / kmax loads
+// per chunk (per 32-client group, those loads' latency and two barriers were most of K3n).
+constexpr int kNibChunk = 1024;                 // clients whose tables sit in LDS at a time (64 KB)
 __device__ __forceinline__ void nib_build_tables(float (*tab)[16], const float* __restrict__ l1,
-                                                 const int32_t* __restrict__ kmaxv, int64_t j0, int nb, int wid,
-                                                 int lane, float fm, float n_div) {
-    for (int jj = wid; jj < nb; jj += kCodesMeanThreads / kWave) {
+                                                 const int32_t* __restrict__ kmaxv, int64_t j0, int nb, float fm,
+                                                 float n_div) {
+    for (int e = threadIdx.x; e < nb * 8; e += kCodesMeanThreads) {
+        const int jj = e >> 3, k = e & 7;
         const float L = l1[j0 + jj];
         const int km = min(kNibMax, max(0, kmaxv[j0 + jj]));
-        if (lane <= km) {
-            const float v = ((L * (float)lane) / fm) / n_div;
-            tab[jj][lane] = v;
-            tab[jj][15 - lane] = -v;
+        if (k <= km) {
+            const float v = ((L * (float)k) / fm) / n_div;
+            tab[jj][k] = v;
+            tab[jj][15 - k] = -v;
         }
     }
 }
 
 // K3n: est[i] (+)= q_j[i] / n_div, clients in order, from the 4-bit codes (4 bytes per client
-// per thread's 8 columns), double-buffered batches of kMeanUnroll clients as K3c.  d % 4096 ==
-// 0 (every thread's columns inside d).  Any client with kmax > kNibMax sends the launch down
-// the mixed loop: those clients add q[j][i] / n_div (q is required).
+// per thread's 8 columns): the tables of up to kNibChunk clients built once, then the code
+// loads in double-buffered batches of kMeanUnroll clients with no barrier between them.
+// d % 4096 == 0 (every thread's columns inside d).  Any client with kmax > kNibMax sends the
+// launch down the mixed loop: those clients add q[j][i] / n_div (q is required).
 __global__ void __launch_bounds__(kCodesMeanThreads)
 nibbles_mean_kernel(const uint8_t* __restrict__ nib, int64_t ldn, const float* __restrict__ l1,
                     const int32_t* __restrict__ kmaxv, int64_t n, int64_t d, float fm, float n_div, int accumulate,
                     float* __restrict__ est, const float* __restrict__ q, int64_t ldq) {
-    __shared__ float tab[kMeanClients][16];
+    __shared__ float tab[kNibChunk][16];
     __shared__ uint32_t s_ovf;
     const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);
     const int64_t i0 = ((int64_t)blockIdx.x * kCodesMeanThreads + tid) * kMeanCpt;
     float e[kMeanCpt];
     if (accumulate) {
@@ -2277,29 +2280,27 @@ nibbles_mean_kernel(const uint8_t* __restrict__ nib, int64_t ldn, const float* _
     __syncthreads();
     const bool any = s_ovf != 0u;
     const uint8_t* cbase = nib + i0 / 2;
-    const int64_t groups = n / kMeanClients;
-    if (!any) {
-        uint32_t wa[kMeanUnroll], wb[kMeanUnroll];
-        if (groups > 0) nib_load_batch(wa, cbase, ldn);
-        for (int64_t g = 0; g < groups; ++g) {
-            const int64_t j0 = g * kMeanClients;
-            __syncthreads();
-            nib_build_tables(tab, l1, kmaxv, j0, kMeanClients, wid, lane, fm, n_div);
-            __syncthreads();
-            nib_load_batch(wb, cbase + (j0 + kMeanUnroll) * ldn, ldn);
-            nib_add_batch(e, wa, tab, 0);
-            const int64_t jn = (j0 + kMeanClients + kMeanUnroll <= n) ? j0 + kMeanClients : n - kMeanUnroll;
-            nib_load_batch(wa, cbase + jn * ldn, ldn);
-            nib_add_batch(e, wb, tab, kMeanUnroll);
+    for (int64_t c0 = 0; c0 < n; c0 += kNibChunk) {
+        const int nc = (int)min((int64_t)kNibChunk, n - c0);
+        __syncthreads();                               // the previous chunk's tables no longer read
+        nib_build_tables(tab, l1, kmaxv, c0, nc, fm, n_div);
+        __syncthreads();
+        const int full = any ? 0 : nc / kMeanClients * kMeanClients;
+        if (full > 0) {
+            uint32_t wa[kMeanUnroll], wb[kMeanUnroll];
+            const uint8_t* cb = cbase + c0 * ldn;
+            nib_load_batch(wa, cb, ldn);
+            for (int g = 0; g < full; g += kMeanClients) {
+                nib_load_batch(wb, cb + (int64_t)(g + kMeanUnroll) * ldn, ldn);
+                nib_add_batch(e, wa, tab, g);
+                // the next group's first batch (clamped to a row inside the chunk when none)
+                const int gn = (g + kMeanClients + kMeanUnroll <= nc) ? g + kMeanClients : nc - kMeanUnroll;
+                nib_load_batch(wa, cb + (int64_t)gn * ldn, ldn);
+                nib_add_batch(e, wb, tab, g + kMeanUnroll);
+            }
         }
-    }
-    for (int64_t j0 = any ? 0 : groups * kMeanClients; j0 < n; j0 += kMeanClients) {   // mixed / the rest
-        const int nb = (int)min((int64_t)kMeanClients, n - j0);
-        __syncthreads();
-        nib_build_tables(tab, l1, kmaxv, j0, nb, wid, lane, fm, n_div);
-        __syncthreads();
-        for (int jj = 0; jj < nb; ++jj) {
-            const int64_t j = j0 + jj;
+        for (int jj = full; jj < nc; ++jj) {           // mixed / the chunk's last clients
+            const int64_t j = c0 + jj;
             if (kmaxv[j] > kNibMax) {
                 const float4 a4 = *reinterpret_cast<const float4*>(q + j * ldq + i0);
                 const float4 b4 = *reinterpret_cast<const float4*>(q + j * ldq + i0 + 4);
