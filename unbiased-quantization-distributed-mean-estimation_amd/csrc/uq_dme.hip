@@ -2780,6 +2780,11 @@ int side_stream(SideStream** out) {
 // *tls_out is set: the caller then runs launch_torch_ties_rest (part 2: heap-path clients
 // and list entries beyond the slots) once the output kernel on its own stream is done.
 // KB7's client list and cleared tie bits (before launch_torch_ties and the tie counts).
+// KB7 replays through KB7a's multi-workgroup levels (else one rez_ties_kernel launch)
+inline bool kb7a_path(int64_t n, int64_t d) {
+    return !(d <= kTieLevelMin || (n < kTieLevelMinClients && d < kTieLevelBigD));
+}
+
 // clear_bits: without KB7a (whose level-0 kt_count clears the listed clients' rows) every row here.
 int torch_ties_prepare(int64_t n, int64_t d, RezState* state, uint32_t* bits, char* wsb, const BiasedLayout& w,
                        hipStream_t st, bool clear_bits) {
@@ -2864,7 +2869,7 @@ int launch_torch_ties(const float* x, int64_t n, int64_t d, const float* l1, flo
     // several replays would share one workgroup each, and for vectors of 2^21 and more, whose
     // one-workgroup replay takes milliseconds; a few-client call at smaller d (the per-vector
     // drop-ins) replays in one kernel when it has to
-    if (d <= kTieLevelMin || (n < kTieLevelMinClients && d < kTieLevelBigD)) {
+    if (!kb7a_path(n, d)) {
         if (mid && (rc = mid())) return rc;
         hipLaunchKernelGGL(rez_ties_kernel<kTieThreads>, dim3((unsigned)w.slots), dim3(kTieThreads), 0, st, x, d, l1, fm,
                            state, bits, qbuf, pos, list, (uint32_t*)wsb, (const TieLevelState*)nullptr, 0,
@@ -3589,10 +3594,17 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     } else {
         hipLaunchKernelGGL(rez_cand_select_kernel, dim3((unsigned)n), dim3(256), 0, st, state, fcand, cand_n, w.capf);
     }
-    hipLaunchKernelGGL(rez_fine_patch_kernel, dim3(kPatchBlocks, (unsigned)n), dim3(256), 0, st, x, out, d, l1buf, fm,
-                       state, fcand, cand_n, w.capf);
     rc = hip_check(hipGetLastError(), "radix select launch");
     if (rc) return rc;
+    // KB6p: the tie-free fine clients' selected bin coordinates (independent of KB7: with the
+    // torch-tie fork it runs on the caller's stream beside the replay chain, off its path)
+    auto fine_patch = [&](hipStream_t ps) {
+        hipLaunchKernelGGL(rez_fine_patch_kernel, dim3(kPatchBlocks, (unsigned)n), dim3(256), 0, ps, x, out, d, l1buf,
+                           fm, state, fcand, cand_n, w.capf);
+        return hip_check(hipGetLastError(), "rez_fine_patch_kernel launch");
+    };
+    const bool fork_ties = tie_policy == UQ_TIES_TORCH && !(host_check && kb7a_path(n, d));
+    if (!fork_ties && (rc = fine_patch(st))) return rc;
     auto output = [&](hipStream_t os, int part) {
         if (vec4)
             hipLaunchKernelGGL(rez_output_kernel<true>, tgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
@@ -3632,7 +3644,7 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     };
     // (the check pays only where the replay would be KB7a's level chain; a one-kernel replay
     // costs less than the synchronisation)
-    const bool kb7a = !(d <= kTieLevelMin || (n < kTieLevelMinClients && d < kTieLevelBigD));
+    const bool kb7a = kb7a_path(n, d);
     if (tie_policy == UQ_TIES_TORCH && host_check && kb7a) {
         // UQ_TIES_HOST_CHECK (synchronous few-client callers): one stream; after the tie list
         // is built, wait for it and skip the replay chain -- KB7a's ~65 level launches --
@@ -3680,6 +3692,7 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
             int mrc = hip_check(hipEventRecord(sb->mid, sb->s), "record mid");
             if (!mrc) mrc = hip_check(hipStreamWaitEvent(st, sb->mid, 0), "wait mid");
             if (!mrc) mrc = output(st, 1);
+            if (!mrc) mrc = fine_patch(st);
             return mrc;
         });
         if (rc) return rc;
