@@ -147,11 +147,10 @@ rez_setup_kernel(const float* __restrict__ msum, float fm, int64_t d, int64_t n,
 
 // KB4a: histogram of the PASS-th digit over keys matching the prefix.
 template <int PASS, bool VEC4>
-__global__ void __launch_bounds__(256)
-rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
-                const RezState* __restrict__ st, uint32_t* __restrict__ hist) {
+__device__ __forceinline__ void rez_hist_one(const float* __restrict__ x, int64_t d, const float* __restrict__ l1,
+                                             float fm, const RezState* __restrict__ st, uint32_t* __restrict__ hist,
+                                             int64_t vec) {
     using RP = RadixPass<PASS>;
-    const int64_t vec = blockIdx.y;
     const uint32_t kleft = st[vec].kleft;
     if (kleft == 0 || !(st[vec].flags & kRezFull)) return;
     const uint32_t prefix = st[vec].prefix;
@@ -189,6 +188,16 @@ rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
     uint32_t* g = hist + ((size_t)vec * kHistSlots + PASS) * kRadixBins;
     for (int b = tid; b < kRadixBins; b += 256)
         if (h[b]) atomicAdd(&g[b], h[b]);
+    __syncthreads();                                   // h is reused by the next listed client
+}
+
+// Grid (spans, <= list length): y strides over KB4a's list of full clients (flist[0] = count).
+template <int PASS, bool VEC4>
+__global__ void __launch_bounds__(256)
+rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
+                const RezState* __restrict__ st, uint32_t* __restrict__ hist, const uint32_t* __restrict__ flist) {
+    const uint32_t nf = flist[0];
+    for (uint32_t li = blockIdx.y; li < nf; li += gridDim.y) rez_hist_one<PASS, VEC4>(x, d, l1, fm, st, hist, flist[1 + li]);
 }
 
 // KB4a / KB4b: pick the digit holding the kleft-th largest key (one workgroup per client).
@@ -197,19 +206,19 @@ rez_hist_kernel(const float* __restrict__ x, int64_t d, const float* __restrict_
 // listed by KB6f), a larger one kRezFull.  Otherwise (KB4b) pass PASS of the key digits over
 // the full row, kRezFull clients only.
 template <int PASS, bool FINE>
-__global__ void __launch_bounds__(256)
-rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ zn,
-                  uint32_t capf) {
+__device__ __forceinline__ void rez_select_one(RezState* __restrict__ st, const uint32_t* __restrict__ hist,
+                                               const uint32_t* __restrict__ zn, uint32_t capf,
+                                               uint32_t* __restrict__ flist, int64_t vec) {
     using RP = RadixPass<PASS>;
     constexpr int nb = FINE ? kRadixBins : (int)RP::dmask + 1;
     constexpr int per = nb / 256;
-    const int64_t vec = blockIdx.x;
     const uint32_t kleft = st[vec].kleft;
     if (kleft == 0) return;
     if (!FINE && !(st[vec].flags & kRezFull)) return;
     __shared__ uint32_t lds[4];
     __shared__ int s_found;
     const int tid = threadIdx.x;
+    __syncthreads();                                   // the previous listed client's s_found / lds
     if (tid == 0) s_found = 0;
     const uint32_t* h = hist + ((size_t)vec * kHistSlots + (FINE ? kFineSlot : PASS)) * kRadixBins;
     const bool mirror = FINE && st[vec].delta < 0;
@@ -247,6 +256,7 @@ rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist, 
                         s.eq = c[k];                     // its coordinates = the candidates KB6f lists
                     } else {
                         s.flags |= kRezFull;
+                        flist[1 + atomicAdd(&flist[0], 1u)] = (uint32_t)vec;      // for KB4b's passes
                     }
                 } else {
                     s.prefix |= digit << RP::shift;
@@ -265,7 +275,24 @@ rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist, 
         }
     }
     __syncthreads();
-    if (FINE && tid == 0 && !s_found) st[vec].flags |= kRezFull;     // (cannot happen: sum = d >= kleft)
+    if (FINE && tid == 0 && !s_found) {                  // (cannot happen: sum = d >= kleft)
+        st[vec].flags |= kRezFull;
+        flist[1 + atomicAdd(&flist[0], 1u)] = (uint32_t)vec;
+    }
+}
+
+// FINE (KB4a): one workgroup per client, the full ones appended to flist; else (KB4b) the
+// workgroups stride over flist.
+template <int PASS, bool FINE>
+__global__ void __launch_bounds__(256)
+rez_select_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ zn,
+                  uint32_t capf, uint32_t* __restrict__ flist) {
+    if (FINE) {
+        rez_select_one<PASS, FINE>(st, hist, zn, capf, flist, blockIdx.x);
+        return;
+    }
+    const uint32_t nf = flist[0];
+    for (uint32_t li = blockIdx.x; li < nf; li += gridDim.x) rez_select_one<PASS, FINE>(st, hist, zn, capf, flist, flist[1 + li]);
 }
 
 // KB4d: the threshold key among a fine client's listed candidates (key digits 11/11/10 over

@@ -2458,8 +2458,8 @@ int check_common(const void* x, int64_t n, int64_t d, int32_t T, void* ws, size_
 // [tie counts n x tiles u32][tie bits n x ceil(d/32) u32]
 // [KB7 slots: keys + indices S x 2d u32][KB7 positions S x 2d u32], S = min(n, kTieSlots)
 struct BiasedLayout {
-    size_t part_off, l1_off, msum_off, st_off, hist_off, zn_off, cn_off, cand_off, tcnt_off, bits_off, pairs_off,
-        pos_off, list_off, tls_off, tcnt2_off, alist_off, total;
+    size_t part_off, l1_off, msum_off, st_off, hist_off, zn_off, cn_off, fl_off, cand_off, tcnt_off, bits_off,
+        pairs_off, pos_off, list_off, tls_off, tcnt2_off, alist_off, total;
     int32_t tiles;
     int32_t slots;
     uint32_t cap;      // candidate region per client in u32 (KB6f lists cap / 2 (index, key) pairs)
@@ -2479,7 +2479,8 @@ BiasedLayout biased_layout(int64_t n, int64_t d, const L1Plan& plan) {
     w.capf = w.cap / 2;
     w.zn_off = up(w.hist_off + (size_t)n * kHistSlots * kRadixBins * sizeof(uint32_t));
     w.cn_off = w.zn_off + (size_t)n * 2 * sizeof(uint32_t);           // zn and cand_n adjacent
-    w.cand_off = up(w.cn_off + (size_t)n * sizeof(uint32_t));
+    w.fl_off = w.cn_off + (size_t)n * sizeof(uint32_t);               // the full clients' list (zeroed count)
+    w.cand_off = up(w.fl_off + (size_t)(n + 1) * sizeof(uint32_t));
     w.tcnt_off = up(w.cand_off + (size_t)n * w.cap * sizeof(uint32_t));
     w.bits_off = up(w.tcnt_off + (size_t)n * w.tiles * sizeof(uint32_t));
     w.slots = (int32_t)std::min<int64_t>(n, kTieSlots);
@@ -3560,19 +3561,24 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     rc = hip_check(hipGetLastError(), "rez_setup_kernel launch");
     if (rc) return rc;
     const bool vec4 = aligned16(x) && aligned16(out) && d % 4 == 0;
-    const dim3 hgrid((unsigned)((d + kHistSpan - 1) / kHistSpan), (unsigned)n);
     const dim3 tgrid((unsigned)w.tiles, (unsigned)n);
     const dim3 fgrid((unsigned)((d + kSelTile - 1) / kSelTile), (unsigned)n);
     uint2* fcand = (uint2*)cand;
     // KB4a: the threshold's fine bin; a small bucket makes the client "fine", a large one "full"
-    hipLaunchKernelGGL((rez_select_kernel<0, true>), dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.capf);
+    // full clients are listed by KB4a (flist[0] = count, in the zeroed range): the key-digit
+    // passes below stride over the list, not over n x spans workgroups that mostly exit
+    uint32_t* flist = (uint32_t*)(wsb + w.fl_off);
+    hipLaunchKernelGGL((rez_select_kernel<0, true>), dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.capf, flist);
+    const unsigned fy = (unsigned)std::min<int64_t>(n, kListedGridY);
+    const dim3 hlgrid((unsigned)((d + kHistSpan - 1) / kHistSpan), fy);
     // full clients (tie-heavy rows): the key digits by three full-row histogram passes
 #define UQ_RADIX(P)                                                                                          \
     if (vec4)                                                                                                \
-        hipLaunchKernelGGL((rez_hist_kernel<P, true>), hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist); \
+        hipLaunchKernelGGL((rez_hist_kernel<P, true>), hlgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist, flist); \
     else                                                                                                     \
-        hipLaunchKernelGGL((rez_hist_kernel<P, false>), hgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist); \
-    hipLaunchKernelGGL((rez_select_kernel<P, false>), dim3((unsigned)n), dim3(256), 0, st, state, hist, zn, w.capf);
+        hipLaunchKernelGGL((rez_hist_kernel<P, false>), hlgrid, dim3(256), 0, st, x, d, l1buf, fm, state, hist, flist); \
+    hipLaunchKernelGGL((rez_select_kernel<P, false>), dim3((unsigned)std::min<int64_t>(n, kTieSlots)), dim3(256), 0, st, \
+                       state, hist, zn, w.capf, flist);
     UQ_RADIX(0) UQ_RADIX(1) UQ_RADIX(2)
 #undef UQ_RADIX
     // fine clients: KB6f writes every output and lists the bucket, KB4d finds the threshold
