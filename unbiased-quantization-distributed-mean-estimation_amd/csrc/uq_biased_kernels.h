@@ -213,7 +213,10 @@ __device__ __forceinline__ void rez_select_one(RezState* __restrict__ st, const 
     constexpr int nb = FINE ? kRadixBins : (int)RP::dmask + 1;
     constexpr int per = nb / 256;
     const uint32_t kleft = st[vec].kleft;
-    if (kleft == 0) return;
+    if (kleft == 0) {                                  // no selection: KB6 writes it (listed with the full)
+        if (FINE && threadIdx.x == 0) flist[1 + atomicAdd(&flist[0], 1u)] = (uint32_t)vec;
+        return;
+    }
     if (!FINE && !(st[vec].flags & kRezFull)) return;
     __shared__ uint32_t lds[4];
     __shared__ int s_found;
@@ -436,25 +439,15 @@ rez_cand_pick_kernel(RezState* __restrict__ st, const uint32_t* __restrict__ his
     if (tid == 0) st[vec] = s;
 }
 
-// KB5: keys equal to the threshold per tile (ambiguous clients only).  `list` (torch ties:
-// KB7's client list, ascending; null otherwise): listed clients are replayed, so they need
-// no index-order rank (a failed replay is reported as an internal error).
+// KB5: keys equal to the threshold per tile (ambiguous clients only), for the index-order
+// ranks of the lowest-index rule.  Grid (tiles, <= list length): y strides over `list` (the
+// ambiguous clients, rez_tie_list_kernel), not over n mostly-exiting client rows.
 template <bool VEC4>
-__global__ void __launch_bounds__(256)
-rez_tiecount_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
-                    const RezState* __restrict__ st, uint32_t* __restrict__ tilecnt, int32_t tiles,
-                    const uint32_t* __restrict__ list) {
-    const int64_t vec = blockIdx.y;
+__device__ __forceinline__ void rez_tiecount_tile(const float* __restrict__ x, int64_t d, const float* __restrict__ l1,
+                                                  float fm, const RezState* __restrict__ st,
+                                                  uint32_t* __restrict__ tilecnt, int32_t tiles, int64_t vec) {
     const int32_t fl = st[vec].flags;
     if (!(fl & kRezAmbiguous) || (fl & kRezTorchTies)) return;
-    if (list) {                                          // binary search of the sorted list
-        uint32_t lo = 0, hi = list[0];
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (list[1 + mid] < (uint32_t)vec) lo = mid + 1; else hi = mid;
-        }
-        if (lo < list[0] && list[1 + lo] == (uint32_t)vec) return;
-    }
     const uint32_t tau = st[vec].prefix;
     const bool up = st[vec].delta > 0;
     const DivPlan dp = div_plan(l1[vec]);
@@ -481,6 +474,17 @@ rez_tiecount_kernel(const float* __restrict__ x, int64_t d, const float* __restr
     uint32_t total;
     (void)block_excl_scan_u32(cnt, lds, &total);
     if (tid == 0) tilecnt[vec * tiles + blockIdx.x] = total;
+    __syncthreads();                                   // lds is reused by the next listed client
+}
+
+template <bool VEC4>
+__global__ void __launch_bounds__(256)
+rez_tiecount_kernel(const float* __restrict__ x, int64_t d, const float* __restrict__ l1, float fm,
+                    const RezState* __restrict__ st, uint32_t* __restrict__ tilecnt, int32_t tiles,
+                    const uint32_t* __restrict__ list) {
+    const uint32_t nl = list[0];
+    for (uint32_t li = blockIdx.y; li < nl; li += gridDim.y)
+        rez_tiecount_tile<VEC4>(x, d, l1, fm, st, tilecnt, tiles, list[1 + li]);
 }
 
 __device__ __forceinline__ float torch_signf(float v) {
@@ -498,11 +502,13 @@ __device__ __forceinline__ void rez_output_tile(const float* __restrict__ x, flo
     const bool on = s.kleft != 0;
     const bool amb = on && (s.flags & kRezAmbiguous);
     // part 0: every client; 1: clients without a tie at the threshold (run while KB7 replays
-    // the others on a side stream); 2: only those with one (after KB7).  Fine clients without
+    // the others on a side stream); 2: only those with one (after KB7); 3: only the fine ones
+    // with one (the lowest-index rule's second, list-strided launch).  Fine clients without
     // a tie were written by KB6f + KB6p; with a replayed tie KB6t patches them; with an
     // index-order tie (a failed replay, or the lowest-index rule) this kernel rewrites them:
     // the ranks need the whole row
     if ((part == 1 && amb) || (part == 2 && !amb)) return;
+    if (part == 3 && !(amb && (s.flags & kRezFine))) return;   // (the listed full clients took part 0)
     if (on && (s.flags & kRezFine) && !amb) return;
     const bool replay = amb && (s.flags & kRezTorchTies);
     if (replay && (s.flags & kRezFine)) return;
@@ -645,8 +651,10 @@ rez_output_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t 
         return;
     }
     const uint32_t nl = list[0];
-    for (uint32_t li = blockIdx.y; li < nl; li += gridDim.y)
+    for (uint32_t li = blockIdx.y; li < nl; li += gridDim.y) {
         rez_output_tile<VEC4>(x, out, d, l1, fm, st, tilecnt, tiles, tie_bits, part, list[1 + li]);
+        __syncthreads();                               // the rank scans' LDS, reused by the next client
+    }
 }
 
 // KB6f: fine clients (kRezFine) -- out for every coordinate with the selection decided by the

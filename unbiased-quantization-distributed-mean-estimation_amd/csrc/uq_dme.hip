@@ -3561,7 +3561,6 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     rc = hip_check(hipGetLastError(), "rez_setup_kernel launch");
     if (rc) return rc;
     const bool vec4 = aligned16(x) && aligned16(out) && d % 4 == 0;
-    const dim3 tgrid((unsigned)w.tiles, (unsigned)n);
     const dim3 fgrid((unsigned)((d + kSelTile - 1) / kSelTile), (unsigned)n);
     uint2* fcand = (uint2*)cand;
     // KB4a: the threshold's fine bin; a small bucket makes the client "fine", a large one "full"
@@ -3611,13 +3610,21 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     };
     const bool fork_ties = tie_policy == UQ_TIES_TORCH && !(host_check && kb7a_path(n, d));
     if (!fork_ties && (rc = fine_patch(st))) return rc;
-    auto output = [&](hipStream_t os, int part) {
+    // KB6 for the clients of a list (list-strided grid): part 0 / 1 over KB4a's list (the full
+    // clients and those without a selection -- every client KB6f did not write), part 3 over
+    // the ambiguous ones (their fine clients)
+    // ol == nullptr: the n x tiles grid (part 1 beside the torch-tie chain: the list-strided
+    // form was 0.01-0.02 ms slower there, profiles/r5aw_*; the lowest-index batch gains 0.075 ms
+    // from it, its launches being on the critical path)
+    const dim3 lgrid((unsigned)w.tiles, (unsigned)std::min<int64_t>(n, kListedGridY));
+    auto output = [&](hipStream_t os, int part, const uint32_t* ol) {
+        const dim3 ogrid((unsigned)w.tiles, (unsigned)(ol ? std::min<int64_t>(n, kListedGridY) : n));
         if (vec4)
-            hipLaunchKernelGGL(rez_output_kernel<true>, tgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
-                               w.tiles, bits, part, (const uint32_t*)nullptr);
+            hipLaunchKernelGGL(rez_output_kernel<true>, ogrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
+                               w.tiles, bits, part, ol);
         else
-            hipLaunchKernelGGL(rez_output_kernel<false>, tgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
-                               w.tiles, bits, part, (const uint32_t*)nullptr);
+            hipLaunchKernelGGL(rez_output_kernel<false>, ogrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
+                               w.tiles, bits, part, ol);
         return hip_check(hipGetLastError(), "rez_output_kernel launch");
     };
     // after KB7: its listed clients only (a list-strided grid, not n x tiles workgroups that
@@ -3625,7 +3632,6 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
     // listed threshold bin for the replayed fine clients
     auto output_listed = [&](hipStream_t os) {
         const uint32_t* list = (const uint32_t*)(wsb + w.list_off);
-        const dim3 lgrid((unsigned)w.tiles, (unsigned)std::min<int64_t>(n, kListedGridY));
         if (vec4)
             hipLaunchKernelGGL(rez_output_kernel<true>, lgrid, dim3(256), 0, os, x, out, d, l1buf, fm, state, tcnt,
                                w.tiles, bits, 2, list);
@@ -3639,12 +3645,12 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         return hip_check(hipGetLastError(), "rez_tie_patch_kernel launch");
     };
     auto tiecount = [&](hipStream_t ts, const uint32_t* list) {
-        // index-order tie ranks (ambiguous clients that KB7 does not replay)
+        // index-order tie ranks of the listed (ambiguous) clients
         if (vec4)
-            hipLaunchKernelGGL(rez_tiecount_kernel<true>, tgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles,
+            hipLaunchKernelGGL(rez_tiecount_kernel<true>, lgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles,
                                list);
         else
-            hipLaunchKernelGGL(rez_tiecount_kernel<false>, tgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles,
+            hipLaunchKernelGGL(rez_tiecount_kernel<false>, lgrid, dim3(256), 0, ts, x, d, l1buf, fm, state, tcnt, w.tiles,
                                list);
         return hip_check(hipGetLastError(), "rez_tiecount_kernel launch");
     };
@@ -3674,7 +3680,7 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
             if (tls && (rc = launch_torch_ties_rest(x, d, l1buf, fm, state, bits, wsb, w, tls, st))) return rc;
             if ((rc = output_listed(st))) return rc;
         }
-        rc = output(st, 1);
+        rc = output(st, 1, nullptr);
         if (rc) return rc;
     } else if (tie_policy == UQ_TIES_TORCH) {
         // fork: KB7 (few workgroups, latency-bound) on the side stream while KB6 writes the
@@ -3697,7 +3703,7 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         rc = launch_torch_ties(x, n, d, l1buf, fm, state, bits, wsb, w, sb->s, &tls, [&]() {
             int mrc = hip_check(hipEventRecord(sb->mid, sb->s), "record mid");
             if (!mrc) mrc = hip_check(hipStreamWaitEvent(st, sb->mid, 0), "wait mid");
-            if (!mrc) mrc = output(st, 1);
+            if (!mrc) mrc = output(st, 1, nullptr);
             if (!mrc) mrc = fine_patch(st);
             return mrc;
         });
@@ -3713,10 +3719,14 @@ int uq_type_biased_f32(const float* x, float* out, int64_t n, int64_t d, int64_t
         rc = output_listed(st);
         if (rc) return rc;
     } else {
-        rc = tiecount(st, nullptr);
+        // the lowest-index rule: the ambiguous clients' list (rez_tie_list_kernel), their tie
+        // counts, then KB6 over the full / no-selection clients and over the ambiguous fine ones
+        rc = torch_ties_prepare(n, d, state, bits, wsb, w, st, false);
         if (rc) return rc;
-        rc = output(st, 0);
-        if (rc) return rc;
+        const uint32_t* amb = (const uint32_t*)(wsb + w.list_off);
+        if ((rc = tiecount(st, amb))) return rc;
+        if ((rc = output(st, 0, flist))) return rc;
+        if ((rc = output(st, 3, amb))) return rc;
     }
     return finish();
 }
