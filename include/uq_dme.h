@@ -60,6 +60,23 @@ int uq_test_set_quicfl_hooks(int flags);
  * reference: its generators (All_Schemes.py:457, 465, 484, 489) are walked word by word. */
 int uq_mt_jump_host(const uint32_t* state624, int64_t blocks, uint32_t* out624);
 
+/* Host-only: the NMSE drivers' input vectors, bit-identical to numpy's legacy RandomState and
+ * multi-threaded (uq_legacy_rng.cpp).  Replaces the per-vector draws of
+ * NMSE_Results/Codes/Normal_dist.py:88-91 (np.random.normal(0, 1, size=d)), Laplace_dist.py:89,
+ * Gamma_dist.py:86, Bernoulli_dist.py:90 (choice(arange(2), p)) and Lognormal_dist.py:90:
+ * n successive size-d calls on the state (key624, pos, has_gauss, gauss) -- numpy's
+ * get_state() tuple, advanced in place -- into out [n][d] as f32 (the drivers' cast to a f32
+ * tensor), and norm2[i] = np.linalg.norm(v_i) ** 2 summed in f64 in a fixed order.
+ * dist / (a, b): 0 normal (loc, scale), 1 laplace (loc, scale), 2 gamma (shape > 1, scale),
+ * 3 choice of {0, 1} (the normalised cdf), 4 lognormal (mean, sigma), 5 uniform (low,
+ * high - low).  threads: host threads (1 = sequential).  Returns 0, -1 bad arguments, -2 jump
+ * unavailable, -3 internal inconsistency.  Does not set uq_last_error. */
+int uq_legacy_draw_f32(uint32_t* key624, int32_t* pos, int32_t* has_gauss, double* gauss, int32_t dist,
+                       double a, double b, int64_t n, int64_t d, float* out, double* norm2, int32_t threads);
+/* Test hook: set the parallel draw's chunking (words per chunk, words of overlap; 0 keeps) and
+ * read-and-reset its counters (waves run, chunk meetings missed). */
+int uq_legacy_test_params(int64_t min_chunk, int64_t overlap, int64_t* waves, int64_t* misses);
+
 /* Thread-local description of the last error returned on this thread. */
 const char* uq_last_error(void);
 

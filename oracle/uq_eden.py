@@ -148,6 +148,8 @@ def torch_dot(x: np.ndarray, y: np.ndarray) -> f32:
     evaluated in extended precision (64-bit significand: a 48-bit product plus a 24-bit
     accumulator) and rounded once to f32 except in the rare case where the exact sum needs
     more than 64 bits (oracle/uq_oracle.c uqo_torch_dot uses fmaf)."""
+    if np.finfo(np.longdouble).nmant < 63:     # fma stand-in needs x87's 64-bit significand
+        raise RuntimeError("torch_dot oracle needs an 80-bit long double (x86); use uq_oracle_c.torch_dot")
     x = np.asarray(x, f32).reshape(-1)
     y = np.asarray(y, f32).reshape(-1)
     n = x.shape[0]

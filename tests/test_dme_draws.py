@@ -1,5 +1,7 @@
-"""The NMSE harness's draw-ahead thread gives the drivers' legacy np.random stream (ND:88-91)."""
+"""The NMSE harness's draw-ahead thread gives the drivers' legacy np.random stream (ND:88-95):
+the batches, sum ||v||^2 and the CPU empirical mean, in the drivers' order."""
 import numpy as np
+import torch
 
 import uqdme  # noqa: F401  (registers the uqdme_amd package)
 
@@ -7,17 +9,20 @@ import uqdme  # noqa: F401  (registers the uqdme_amd package)
 def test_draw_ahead_matches_inline_draws():
     from uqdme_amd.dme import _draw_ahead, draw_vectors
     users, inst, dim = (1, 3, 2), 2, 257
-    for dist in ("normal", "laplace", "bernoulli"):
+    for dist in ("normal", "laplace", "gamma", "bernoulli", "lognormal"):
         rs = np.random.RandomState(42)
         want = []
         for n in users:
             for _ in range(inst):
                 vecs, vns = draw_vectors(dist, n, dim, rs)
-                want.append((np.stack([v.astype(np.float32) for v in vecs]), vns))
-        got = list(_draw_ahead(dist, users, inst, dim, np.random.RandomState(42)))
+                b = np.stack([v.astype(np.float32) for v in vecs])
+                want.append((b, vns, torch.from_numpy(b).sum(dim=0) / n))
+        got = list(_draw_ahead(dist, users, inst, dim, np.random.RandomState(42), threads=4))
         assert len(got) == len(want)
-        for (gb, gv), (wb, wv) in zip(got, want):
-            assert gb.dtype == np.float32 and np.array_equal(gb, wb) and gv == wv
+        for (gb, gv, ge), (wb, wv, we) in zip(got, want):
+            assert gb.dtype == torch.float32 and np.array_equal(gb.numpy(), wb)
+            assert abs(gv - wv) <= 1e-13 * wv
+            assert torch.equal(ge, we)
 
 
 def test_draw_ahead_stops_early_and_raises():

@@ -25,6 +25,8 @@ SIGNATURES = {
     "uq_test_force_replay_failure": (ctypes.c_int, [ctypes.c_int]),
     "uq_test_set_quicfl_hooks": (ctypes.c_int, [ctypes.c_int]),
     "uq_mt_jump_host": (ctypes.c_int, [_p, _i64, _p]),
+    "uq_legacy_draw_f32": (ctypes.c_int, [_p, _p, _p, _p, _i32, _f64, _f64, _i64, _i64, _p, _p, _i32]),
+    "uq_legacy_test_params": (ctypes.c_int, [_i64, _i64, _p, _p]),
     "uq_rate_to_m": (ctypes.c_int, [_f64, _i64, ctypes.POINTER(_i64)]),
     "uq_workspace_bytes": (ctypes.c_int, [_i64, _i64, _i32, ctypes.POINTER(_sz)]),
     "uq_l1_torch_order_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _sz, _p]),

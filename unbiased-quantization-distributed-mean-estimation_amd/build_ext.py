@@ -14,8 +14,10 @@ import sys
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(PKG_DIR, "csrc", "uq_dme.hip")
-# host-only C++ (the MT19937 jump polynomials): g++, linked into the same library
-HOST_SRC = os.path.join(PKG_DIR, "csrc", "uq_mt_poly.cpp")
+# host-only C++, g++, linked into the same library: the MT19937 jump polynomials, and numpy's
+# legacy RandomState samplers for the NMSE harness (uq_legacy_rng.cpp: -ffp-contract=off, every
+# product and sum rounded on its own as in numpy's baseline build; log/exp from the host libm)
+HOST_SRCS = [os.path.join(PKG_DIR, "csrc", f) for f in ("uq_mt_poly.cpp", "uq_legacy_rng.cpp")]
 OUT_DIR = os.path.join(PKG_DIR, "_build")
 SO = os.path.join(OUT_DIR, "libuq_dme.so")
 
@@ -30,7 +32,7 @@ HIPCC_FLAGS = [
 ]
 
 
-HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall"]
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-ffp-contract=off", "-fno-fast-math"]
 
 
 def hipcc() -> str:
@@ -72,9 +74,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OUT_DIR, exist_ok=True)
     bid = build_id()
     tmp = SO + ".tmp"
-    obj = os.path.join(OUT_DIR, "uq_mt_poly.o")
-    cmds = [[os.environ.get("CXX", "g++"), *HOST_FLAGS, "-c", "-o", obj, HOST_SRC],
-            [hipcc(), *HIPCC_FLAGS, f'-DUQ_BUILD_ID="{bid}"', "-o", tmp, SRC, "-x", "none", obj]]
+    objs = [os.path.join(OUT_DIR, os.path.basename(f)[:-4] + ".o") for f in HOST_SRCS]
+    cmds = [[os.environ.get("CXX", "g++"), *HOST_FLAGS, "-c", "-o", o, f] for f, o in zip(HOST_SRCS, objs)]
+    cmds.append([hipcc(), *HIPCC_FLAGS, f'-DUQ_BUILD_ID="{bid}"', "-o", tmp, SRC, "-x", "none", *objs, "-lpthread"])
     for cmd in cmds:
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -3819,18 +3819,9 @@ static int qfl_jump_polys(const QflJumpPlan& p, bool a_only, const uint32_t** ou
     if ((p.R > 1 && uq_mtpoly_progression(p.L - 1, p.L, p.R - 1, h.data() + kMtN)) ||
         (!a_only && uq_mtpoly_progression(p.qL - 1, p.L, p.R, h.data() + (size_t)p.R * kMtN)))
         return fail(UQ_E_INVALID, "MT19937 jump polynomials unavailable");
-    if (cache.size() >= 64) {                // bounded: many layouts (sizes) in one process; this
-        rc = hip_check(hipDeviceSynchronize(), "sync before freeing jump polynomials");   // device's
-        if (rc) return rc;                   // entries are idle after the synchronisation
-        for (auto it2 = cache.begin(); it2 != cache.end();) {
-            if (std::get<0>(it2->first) == dev) {
-                (void)hipFree(it2->second);
-                it2 = cache.erase(it2);
-            } else {
-                ++it2;
-            }
-        }
-    }
+    // Entries live for the life of the process: a pointer handed out above may still be waiting
+    // to be launched on another thread's stream, so nothing here is ever freed.  The key space is
+    // one entry per (device, layout) in use -- 2 R * 624 words each, a few KB to ~1 MB.
     uint32_t* d = nullptr;
     rc = hip_check(hipMalloc(&d, h.size() * sizeof(uint32_t)), "hipMalloc jump polynomials");
     if (rc) return rc;
@@ -4217,6 +4208,10 @@ static int quicfl_jump_fork(int64_t n, int64_t D, int64_t dim, const int32_t* pr
     if ((rc = side_stream(&sb))) return rc;
     if ((rc = hip_check(hipEventRecord(sb->fork, st), "record fork"))) return rc;
     if ((rc = hip_check(hipStreamWaitEvent(sb->s, sb->fork, 0), "wait fork"))) return rc;
+    auto join_on_error = [&](int err) {      // whatever reached the side stream finishes before st moves on
+        if (hipEventRecord(sb->join, sb->s) == hipSuccess) (void)hipStreamWaitEvent(st, sb->join, 0);
+        return err;
+    };
     uint32_t* xs = (uint32_t*)(wsb + quicfl_jump_off(n, dim));
     uint32_t* parts = xs + (size_t)n * 2 * kMjX;
     QflJumpArgs ja{};
@@ -4232,10 +4227,10 @@ static int quicfl_jump_fork(int64_t n, int64_t D, int64_t dim, const int32_t* pr
     ja.nstreams = 2;
     ja.kinds = 3;
     hipLaunchKernelGGL(quicfl_stream_kernel, dim3((unsigned)((2 * n + 3) / 4)), dim3(256), 0, sb->s, ja);
-    if ((rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch"))) return rc;
+    if ((rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch"))) return join_on_error(rc);
     hipLaunchKernelGGL(quicfl_jump_kernel, dim3((unsigned)(n * jp.R * 3 * kMjParts)), dim3(256), 0, sb->s, ja);
-    if ((rc = hip_check(hipGetLastError(), "quicfl_jump_kernel launch"))) return rc;
-    if ((rc = hip_check(hipEventRecord(sb->join, sb->s), "record join"))) return rc;
+    if ((rc = hip_check(hipGetLastError(), "quicfl_jump_kernel launch"))) return join_on_error(rc);
+    if ((rc = hip_check(hipEventRecord(sb->join, sb->s), "record join"))) return join_on_error(rc);
     jl->use = true;
     jl->jp = jp;
     jl->parts = parts;
@@ -4244,6 +4239,17 @@ static int quicfl_jump_fork(int64_t n, int64_t D, int64_t dim, const int32_t* pr
 }
 
 static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunch& jl, hipStream_t st);
+
+// Once the fork has happened, the caller's stream waits on the side stream's join on every exit
+// path: KQ0s / KQ0j write into the caller's workspace, which may be freed or reused after an
+// early error return.  (Waiting twice on the join is harmless.)
+struct QflJoinGuard {
+    const QflJumpLaunch& jl;
+    hipStream_t st;
+    ~QflJoinGuard() {
+        if (jl.use) (void)hipStreamWaitEvent(st, jl.sb->join, 0);
+    }
+};
 
 int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t* signs, const int32_t* sign_row,
                            const float* table_xp, const uint32_t* table_packed, int64_t table_numel, int32_t h_len,
@@ -4270,6 +4276,7 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     QflJumpLaunch jl;
     int rc = quicfl_jump_fork(n, w.D, dim, prng_seeds, px_state, px_seeds, wsb, st, &jl);
     if (rc) return rc;
+    const QflJoinGuard join_guard{jl, st};
     FwhtArgs a;
     float* rot = nullptr;
     rc = eden_front(x, n, dim, EdenTables{}, signs, sign_row, w, wsb, a, &rot, st);     // AS:460-470
@@ -4375,6 +4382,7 @@ int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     QflJumpLaunch jl;
     int rc = quicfl_jump_fork(n, w.D, dim, prng_seeds, px_state, px_seeds, wsb, st, &jl);
     if (rc) return rc;
+    const QflJoinGuard join_guard{jl, st};
     FwhtArgs a;
     float* rot = nullptr;
     rc = eden_front(x, n, dim, EdenTables{}, signs, sign_row, w, wsb, a, &rot, st);     // AS:460-470

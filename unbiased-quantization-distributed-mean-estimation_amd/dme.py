@@ -25,9 +25,13 @@ equals that of a driver calling only the selected schemes.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import numpy as np
 import torch
 
+from . import _lib
 from .biased import biased_quantize
 from .eden import eden_compress, eden_decompress, eden_quantize
 from .quantizer import client_mean, quantize_dequantize
@@ -35,7 +39,7 @@ from .quicfl import quicfl_quantize
 
 SCHEME_ORDER = ("eden", "unbiased", "biased", "quicfl")     # ND:135-142 call order
 
-__all__ = ["DISTRIBUTIONS", "draw_vectors", "nmse_simulation", "USERS_ND"]
+__all__ = ["DISTRIBUTIONS", "draw_vectors", "legacy_draw", "nmse_simulation", "USERS_ND"]
 
 # ND:43 (also Lognormal_dist.py:43): num_users_list = arange(1, 102, 5); Laplace/Gamma/
 # Bernoulli drivers use arange(1, 101, 5).
@@ -64,30 +68,98 @@ def draw_vectors(dist: str, n: int, dim: int, rs=np.random):
     return vecs, float(sum(norms))
 
 
-def _draw_ahead(dist: str, users, num_instances: int, dim: int, rs):
+def _cdf2(p):
+    """choice(arange(2), p=p)'s cdf as legacy RandomState.choice builds it (cumsum, / last)."""
+    c = np.asarray(p, np.float64).cumsum()
+    c /= c[-1]
+    return float(c[0]), float(c[1])
+
+
+# dist -> (uq_legacy_draw_f32 code, a, b): the arguments of DISTRIBUTIONS above
+LEGACY = {
+    "normal": (0, 0.0, 1.0),
+    "laplace": (1, 1.0, 2.0),
+    "gamma": (2, 2.0, 2.0),
+    "bernoulli": (3, *_cdf2([0.3, 0.7])),
+    "lognormal": (4, 1.0, 2.0),
+    "uniform": (5, -1.0, 2.0),
+}
+
+
+def host_threads() -> int:
+    """Host threads for the draws: the CPUs this process may run on, capped by
+    $UQDME_DRAW_THREADS or $OMP_NUM_THREADS (the GPU box sets 16, its share of the host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    for var in ("UQDME_DRAW_THREADS", "OMP_NUM_THREADS"):
+        v = os.environ.get(var, "")
+        if v.isdigit() and int(v) > 0:
+            return max(1, min(n, int(v)))
+    return max(1, min(n, 64))
+
+
+def legacy_draw(rs: np.random.RandomState, dist: str, n: int, dim: int, threads: int | None = None,
+                out: np.ndarray | None = None):
+    """n successive rs.<dist>(size=dim) draws of the drivers (DISTRIBUTIONS), bit-identical to
+    RandomState's own, on host threads (uq_legacy_draw_f32, csrc/uq_legacy_rng.cpp); rs is left
+    exactly where the n calls leave it.  Returns (f32 batch [n, dim] -- ND:91's cast --, [n] f64
+    ||v||^2 as np.linalg.norm(v) ** 2, to the last bits of its summation order)."""
+    code, a, b = LEGACY[dist]
+    name, key, pos, has_gauss, gauss = rs.get_state(legacy=True)
+    if name != "MT19937":
+        raise ValueError("legacy MT19937 RandomState required")
+    key = np.array(key, dtype=np.uint32)
+    pos_, hg_, g_ = ctypes.c_int32(int(pos)), ctypes.c_int32(int(has_gauss)), ctypes.c_double(float(gauss))
+    if out is None:
+        out = np.empty((n, dim), np.float32)
+    elif out.dtype != np.float32 or out.shape != (n, dim) or not out.flags.c_contiguous:
+        raise ValueError("out must be a C-contiguous f32 [n, dim] array")
+    norms = np.zeros(n, np.float64)
+    rc = _lib.load().uq_legacy_draw_f32(key.ctypes.data, ctypes.addressof(pos_), ctypes.addressof(hg_),
+                                        ctypes.addressof(g_), code, a, b, n, dim, out.ctypes.data,
+                                        norms.ctypes.data, int(threads or host_threads()))
+    if rc != 0:
+        raise RuntimeError(f"uq_legacy_draw_f32 failed ({rc})")
+    rs.set_state(("MT19937", key, pos_.value, hg_.value, g_.value))
+    return out, norms
+
+
+def _draw_ahead(dist: str, users, num_instances: int, dim: int, rs, device=None, threads=None):
     """The instances' batches in the drivers' order, drawn one instance ahead on a thread:
-    yields (f32 batch [n, dim] as numpy, sum ||v||^2).  The legacy generator is sequential and
-    used by this thread alone, so the stream is the same as drawing inline; numpy's legacy
-    samplers and the f64 -> f32 casts release the GIL, so at large d (config C4, 2^22) the draws
-    overlap the quantization instead of adding to it."""
+    yields (f32 batch [n, dim] on `device` (numpy if None), sum ||v||^2 (ND:94, summed in the
+    drivers' order), emp (ND:95: the batch's f32 sum over clients / n, torch CPU)).  The legacy
+    stream is drawn by legacy_draw on host threads, used by this thread alone, so it is the
+    drivers' stream; the draws, the CPU sum and the host-to-device copy (on a side stream, ready
+    when yielded) overlap the previous instance's quantization.
+    Host memory: up to three batches (the one in use, one queued, one being drawn) plus the
+    draw's f64 values of the batch being drawn: about 20 n * dim bytes at the peak."""
     import queue
     import threading
 
     q: queue.Queue = queue.Queue(maxsize=1)
     stop = threading.Event()
+    side = torch.cuda.Stream(device) if device is not None else None
 
     def work():
         try:
             for n in users:
                 for _ in range(num_instances):
-                    vecs, vns = draw_vectors(dist, n, dim, rs)
-                    batch = np.empty((n, dim), np.float32)
-                    for i, v in enumerate(vecs):
-                        batch[i] = v                                          # ND:91 f64 -> f32
-                    del vecs
+                    batch, norms = legacy_draw(rs, dist, n, dim, threads)                  # ND:88-91
+                    vns = 0
+                    for v in norms.tolist():                                               # ND:94 sum(list)
+                        vns += v
+                    xs = torch.from_numpy(batch)
+                    emp = xs.sum(dim=0) / n                                                # ND:95 (CPU)
+                    if side is not None:
+                        with torch.cuda.stream(side):
+                            xs = xs.to(device)
+                        side.synchronize()
+                    del batch
                     while not stop.is_set():
                         try:
-                            q.put((batch, vns), timeout=0.5)
+                            q.put((xs, float(vns), emp), timeout=0.5)
                             break
                         except queue.Full:
                             pass
@@ -111,7 +183,7 @@ def _draw_ahead(dist: str, users, num_instances: int, dim: int, rs):
 def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_instances: int = 50,
                     num_trials: int = 50, rates=(1, 2), seed: int = 42, torch_threads: int = 1,
                     device=None, schemes=("unbiased",), progress=None, eden_scales=None, eden_scales_out=None,
-                    quicfl=None):
+                    quicfl=None, threads=None):
     """NMSE curves of the selected schemes with the reference's normalisation.
 
     Returns {rate: {...}} for the default unbiased-only run, else {(scheme, rate): {...}};
@@ -119,7 +191,8 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
     "standard_max".  `progress(n, inst)` is called after each instance (long runs).
     eden_scales {(n, inst, rate): [scale per client]} replaces EDEN's scale (AS:348) by the
     given values (the receiver then runs on them); eden_scales_out, a dict, receives the
-    scales computed here under the same keys."""
+    scales computed here under the same keys.  threads: host threads for the draws
+    (legacy_draw; default host_threads())."""
     device = device or torch.device("cuda", torch.cuda.current_device())
     schemes = tuple(schemes)
     for sc in schemes:
@@ -128,19 +201,18 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
     order = [sc for sc in SCHEME_ORDER if sc in schemes]
     if "quicfl" in order:
         from .eden import padded_dim
-        from .quicfl import _dropin_pair, generator_words
+        from .quicfl import _dropin_pair, advance_generator, generator_words
         qsend, qrecv = quicfl if quicfl is not None else _dropin_pair()
         qD = padded_dim(dim)
     rs = np.random.RandomState(seed)                 # legacy stream == np.random.seed(seed)
     gen = torch.Generator().manual_seed(seed)        # == torch.manual_seed(seed) CPU stream
     keys = [(sc, r) for sc in order for r in rates]
     script = {k: np.zeros((len(users), num_instances), np.float64) for k in keys}
-    batches = _draw_ahead(dist, users, num_instances, dim, rs)
+    batches = _draw_ahead(dist, users, num_instances, dim, rs, device=device, threads=threads)
     for ui, n in enumerate(users):
         for inst in range(num_instances):
-            batch, vns = next(batches)
-            xs = torch.from_numpy(batch)                                                   # ND:91
-            emp = xs.sum(dim=0) / n                                                        # ND:95 (CPU)
+            xd, vns, emp = next(batches)                                                   # ND:88-95
+            xd.record_stream(torch.cuda.current_stream(device))   # drawn on the side stream, used here
             draws = {k: [] for k in keys}
             for _ in range(n):                        # ND:133-140: client-major, scheme/rate-minor
                 for sc in order:
@@ -152,8 +224,7 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                         elif sc == "quicfl":
                             seed = int(torch.randint(0, 100, (1,), generator=gen))                    # AS:820
                             draws[(sc, r)].append((seed, generator_words(gen)[1]))
-                            torch.rand(qD, generator=gen)          # the D bernoulli(p_X) words (AS:489)
-            xd = xs.to(device)
+                            advance_generator(gen, qD)             # past the D bernoulli(p_X) words (AS:489)
             for sc, r in keys:
                 if sc == "unbiased":
                     q = quantize_dequantize(xd, r, X=torch.tensor(draws[(sc, r)], dtype=torch.float32),

@@ -88,6 +88,29 @@ def set_generator_words(gen: torch.Generator, st: np.ndarray, words: np.ndarray)
     gen.set_state(torch.frombuffer(bytearray(b), dtype=torch.uint8).clone())
 
 
+def advance_generator(gen: torch.Generator, nwords: int) -> None:
+    """Leave the CPU generator where `nwords` 32-bit draws leave it -- torch.rand(nwords,
+    generator=gen) on CPU takes one word per f32 element, so this stands for the D bernoulli(p_X)
+    words of AS:489 -- by MT19937 jump-ahead (uq_mt_jump_host) instead of drawing them."""
+    if nwords < 0:
+        raise ValueError("nwords must be >= 0")
+    st, w = generator_words(gen)
+    left, nxt = int(w[0]), int(w[1])
+    rem = left - 1                                   # words left in the current block
+    if nwords <= rem:
+        w[0], w[1] = left - nwords, nxt + nwords
+    else:
+        after = nwords - rem                         # words read from the following blocks
+        k = (after + 623) // 624                     # twists
+        r = after - 624 * (k - 1)                    # words read from the last one (1..624)
+        out = np.empty(624, np.uint32)
+        key = np.ascontiguousarray(w[2:], np.uint32)
+        _lib.check(_lib.load().uq_mt_jump_host(key.ctypes.data, k, out.ctypes.data), "uq_mt_jump_host")
+        w[2:] = out
+        w[0], w[1] = 625 - r, r
+    set_generator_words(gen, st, w)
+
+
 def _check_state(words: np.ndarray) -> None:
     left, nxt = int(words[0]), int(words[1])
     if not 1 <= left <= 624 or (left > 1 and nxt != 625 - left):
