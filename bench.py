@@ -180,6 +180,29 @@ def dist_init(args):
     return None, 0, 1, 0
 
 
+def rank_record(rank, local, seg_ms, probe, elapsed_s, reduce_alone=None):
+    """One rank's own timings for the per_rank list of rank 0's line: each rank draws its own
+    output placement (pipeline.py probe), so a slow rank must be visible next to rank 0."""
+    return {"rank": int(rank), "local_rank": int(local),
+            "l1_ms": round(float(seg_ms[0]), 4), "quantize_ms": round(float(seg_ms[1]), 4),
+            "client_mean_ms": round(float(seg_ms[2]), 4), "reduce_segment_ms": round(float(seg_ms[3]), 4),
+            "quantize_ms_probed": probe["k2_ms_chosen"] if probe else None,
+            "quantize_ms_median_unprobed": probe["k2_ms_median_unprobed"] if probe else None,
+            "probe_spread_ms": (round(max(probe["k2_ms"]) - min(probe["k2_ms"]), 4) if probe and probe.get("k2_ms")
+                                else None),
+            "elapsed_s": round(float(elapsed_s), 6), "reduce_alone_ms": reduce_alone}
+
+
+def gather_per_rank(dist, rank, record):
+    """Every rank's record on rank 0 (a list ordered by rank), None on the others; [record]
+    without a process group."""
+    if dist is None:
+        return [record]
+    objs = [None] * dist.get_world_size() if rank == 0 else None
+    dist.gather_object(record, objs, dst=0)
+    return objs
+
+
 def load_traffic(path, d, n, pipeline):
     """Per-launch HBM bytes of the quantize kernel from a committed PMC summary of the
     same workload and pipeline (profiles/pmc_*.json, written by tools/summarize_profile.py)."""
@@ -289,6 +312,7 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_local = elapsed
     pipe.check_status()                           # status after the timed steps
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if BACKEND == "nccl" else "cpu")
@@ -311,6 +335,7 @@ def main():
 
     seg = np.array([[evs[k][i].elapsed_time(evs[k][i + 1]) for i in range(4)] for k in range(args.steps)])
     seg_ms = seg.mean(axis=0)  # l1, quantize, mean, reduce
+    per_rank = gather_per_rank(dist, rank, rank_record(rank, local, seg_ms, probe, elapsed_local, reduce_alone))
     ms_per_step = elapsed * 1e3 / args.steps
     value = n_total * args.steps / elapsed / 1e6
 
@@ -371,6 +396,7 @@ def main():
                           # reduce_alone = the collective timed by itself after the steps
                           ("reduce_enqueue" if overlap else "reduce"): round(float(seg_ms[3]), 4),
                           "reduce_alone": reduce_alone},
+            "per_rank": per_rank,
             "pipelines": side,
             "output_placement_probe": probe,
             "roofline": {"kernel": "quantize_stream_kernel (K2)", "bound": "hbm", "achieved": round(achieved, 2),

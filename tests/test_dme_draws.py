@@ -19,10 +19,21 @@ def test_draw_ahead_matches_inline_draws():
                 want.append((b, vns, torch.from_numpy(b).sum(dim=0) / n))
         got = list(_draw_ahead(dist, users, inst, dim, np.random.RandomState(42), threads=4))
         assert len(got) == len(want)
-        for (gb, gv, ge), (wb, wv, we) in zip(got, want):
+        for (gb, gv, ge, _), (wb, wv, we) in zip(got, want):
             assert gb.dtype == torch.float32 and np.array_equal(gb.numpy(), wb)
             assert abs(gv - wv) <= 1e-13 * wv
             assert torch.equal(ge, we)
+
+
+def test_draw_ahead_reports_the_state_before_each_batch():
+    from uqdme_amd.dme import _draw_ahead, draw_vectors
+    rs = np.random.RandomState(42)
+    for x, _, _, st in _draw_ahead("gamma", (1, 2), 2, 301, np.random.RandomState(42), threads=2):
+        mine = np.random.RandomState(0)
+        mine.set_state(st)
+        assert mine.get_state()[2:] == rs.get_state()[2:] and np.array_equal(mine.get_state()[1], rs.get_state()[1])
+        vecs, _ = draw_vectors("gamma", x.shape[0], 301, rs)
+        assert np.array_equal(x.numpy(), np.stack(vecs).astype(np.float32))
 
 
 def test_draw_ahead_stops_early_and_raises():

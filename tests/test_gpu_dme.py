@@ -31,6 +31,27 @@ def test_nd_harness_known_answers(uq):
                 k += 1
 
 
+def test_checkpoint_resume_equals_one_run(uq, tmp_path):
+    """A run suspended at a user-count boundary and resumed from its checkpoint gives the rows
+    of one uninterrupted run bit for bit (both generator streams continue exactly), with the
+    QUIC-FL generator advance (jump-ahead) in the loop."""
+    from uqdme_amd.dme import Suspended
+    kw = dict(dim=1000, users=(1, 6, 11), num_instances=2, schemes=("eden", "unbiased", "biased"))
+    whole = uq.nmse_simulation("gamma", **kw)
+    ck = str(tmp_path / "ck.npz")
+    with pytest.raises(Suspended):
+        uq.nmse_simulation("gamma", checkpoint=ck, time_limit_s=0.0, **kw)      # stops before n = 6
+    with pytest.raises(Suspended):
+        uq.nmse_simulation("gamma", checkpoint=ck, time_limit_s=0.0, **kw)      # one more user count
+    part = uq.nmse_simulation("gamma", checkpoint=ck, **kw)
+    again = uq.nmse_simulation("gamma", checkpoint=ck, **kw)                    # finished: same rows
+    for k in whole:
+        assert np.array_equal(whole[k]["script"], part[k]["script"]), k
+        assert np.array_equal(whole[k]["script"], again[k]["script"]), k
+    with pytest.raises(ValueError):
+        uq.nmse_simulation("normal", checkpoint=ck, **kw)
+
+
 @pytest.mark.parametrize("dist", ["gamma", "bernoulli", "lognormal", "uniform"])
 def test_other_distributions_vs_oracle(uq, dist):
     """Same harness, every scheme call checked bit-for-bit against the CPU oracle."""

@@ -30,6 +30,16 @@ def main():
     d = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 22
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     g = torch.Generator(device="cuda").manual_seed(4)
+    qfl = None
+    if only is None or "quicfl" in only:        # synthetic sender tables (the published ones are absent)
+        import numpy as np
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        gdir = os.path.join(root, "tests", "golden")
+        sys.path.insert(0, gdir)
+        from quicfl_tables import DATA, sender_tables
+        rz = np.load(os.path.join(gdir, "quicfl_recv_vectors.npz"))
+        qfl = (uqdme.QuicFLSender(tables={b: (*sender_tables(b), DATA[b]) for b in (1, 2)}),
+               uqdme.QuicFLReceiver(tables={b: rz[f"recv{b}"] for b in (1, 2)}))
     for n in (1, 6, 11, 51, 101, 256):
         x = torch.randn(n, d, generator=g, device="cuda")
         X = torch.rand(n, generator=torch.Generator().manual_seed(n))
@@ -37,7 +47,10 @@ def main():
         m = uqdme.rate_to_m(1, d)
         for name, f in (("unbiased", lambda: uqdme.quantize_dequantize(x, 1, X=X, torch_threads=1)),
                         ("biased", lambda: uqdme.biased_quantize(x, m=m, torch_threads=1, ties="torch")),
-                        ("eden", lambda: uqdme.eden_quantize(x, 1, seeds=seeds))):
+                        ("eden", lambda: uqdme.eden_quantize(x, 1, seeds=seeds)),
+                        ("quicfl", lambda: uqdme.quicfl_quantize(x, 1, seeds.tolist(), [123] * n, sender=qfl[0],
+                                                                 recv_table=qfl[1].recv_table[1],
+                                                                 px_seeds=seeds))):
             if only and name not in only:
                 continue
             ms = timed(f)

@@ -59,6 +59,12 @@ def main():
     ap.add_argument("--schemes", default="eden,unbiased,biased")
     ap.add_argument("--out", default="gpurun_out/nmse_curves.json")
     ap.add_argument("--users", default=None, help="comma-separated client counts (default: the drivers' grids)")
+    ap.add_argument("--checkpoint", default=None,
+                    help="checkpoint file pattern with {dist} (saved at every user count; resumed from if present)")
+    ap.add_argument("--resume-from", default=None,
+                    help="pattern with {dist}: a checkpoint copied to --checkpoint before the run (a previous call's)")
+    ap.add_argument("--time-limit", type=float, default=None,
+                    help="seconds per distribution: stop at the next user count after that (checkpoint kept)")
     a = ap.parse_args()
     import uqdme
     schemes = tuple(a.schemes.split(","))
@@ -77,10 +83,25 @@ def main():
     for dist in a.dists.split(","):
         users = tuple(USERS[dist]) if a.users is None else tuple(int(u) for u in a.users.split(","))
         t0 = time.time()
-        out = uqdme.nmse_simulation(dist, dim=a.dim, users=users, num_instances=a.instances, schemes=schemes,
-                                    torch_threads=1, quicfl=qfl,
-                                    progress=lambda n, i: print(f"{dist} n={n} inst={i} {time.time() - t0:.0f} s",
-                                                                flush=True))
+        stats = {}
+        ck = a.checkpoint.format(dist=dist) if a.checkpoint else None
+        if ck and a.resume_from and os.path.exists(a.resume_from.format(dist=dist)):
+            import shutil
+            os.makedirs(os.path.dirname(os.path.abspath(ck)), exist_ok=True)
+            shutil.copyfile(a.resume_from.format(dist=dist), ck)
+        try:
+            out = uqdme.nmse_simulation(dist, dim=a.dim, users=users, num_instances=a.instances, schemes=schemes,
+                                        torch_threads=1, quicfl=qfl, stats=stats, checkpoint=ck,
+                                        time_limit_s=a.time_limit,
+                                        progress=lambda n, i: print(
+                                            f"{dist} n={n} inst={i} {time.time() - t0:.0f} s "
+                                            f"(waited for draws {stats.get('wait_s', 0):.0f} s)", flush=True))
+        except uqdme.Suspended as e:
+            print(f"{dist}: {e} after {time.time() - t0:.0f} s", flush=True)
+            res.setdefault("suspended", {})[dist] = str(e)
+            continue
+        res.setdefault("timing", {})[dist] = {"total_s": round(time.time() - t0, 1),
+                                              "wait_for_draws_s": round(stats.get("wait_s", 0.0), 1)}
         if schemes == ("unbiased",):
             out = {("unbiased", r): v for r, v in out.items()}
         for (sc, r), v in out.items():

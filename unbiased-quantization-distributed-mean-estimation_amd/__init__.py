@@ -20,7 +20,7 @@ from .quicfl import (QuicFLReceiver, QuicFLSender, QuicFLMessages, QUICFL_quanti
                      quicfl_decompress, quicfl_decompress_messages, quicfl_quantize, set_tables_prefix)
 from ._lib import UQError, load as load_library, library_path
 from .distributed import ShardedDME, shard_range, sharded_client_mean, sharded_quantize_mean
-from .dme import DISTRIBUTIONS, nmse_simulation
+from .dme import DISTRIBUTIONS, Suspended, legacy_draw, nmse_simulation
 from .pipeline import DMEPipeline, codes4_fits
 from .fl_stats import compute_nmse_stats_auto, data_format, round_nmse
 from .outpool import set_output_pool
@@ -31,7 +31,7 @@ __all__ = [
     "RATE_TABLE", "rate_to_m", "Type_unbiased_quantize", "quantize_dequantize", "client_mean",
     "quantize_mean", "l1_torch_order", "draw_uniforms", "set_torch_threads", "get_torch_threads",
     "check_status", "UQError", "load_library", "library_path", "shard_range", "sharded_client_mean",
-    "sharded_quantize_mean", "DISTRIBUTIONS", "nmse_simulation", "quantize_encode", "decode", "codes_mean",
+    "sharded_quantize_mean", "DISTRIBUTIONS", "Suspended", "legacy_draw", "nmse_simulation", "quantize_encode", "decode", "codes_mean",
     "TypeCodes", "Type_biased_quantize", "biased_quantize", "EDEN_quantize_Hadamard", "eden_quantize",
     "eden_compress", "eden_decompress", "EdenMessage", "rht_signs", "randomized_hadamard_transform",
     "randomized_inverse_hadamard_transform", "compute_nmse_stats_auto", "data_format", "round_nmse",

@@ -1558,7 +1558,9 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
                     w |= (!(y <= 0.f) ? 1u : 0u) << (8 * c);
                     if (y > 0.f) mymin = min(mymin, __float_as_uint(y));
                 }
+#if !defined(UQ_EXP_NO_BINS)
                 *reinterpret_cast<uint32_t*>(lb + ch * kNormChunk + e) = w;
+#endif
             }
         }
     };
@@ -1568,7 +1570,37 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
     const EdenCents cs = eden_cents(tab);
     auto chainstep = [&](int64_t ch) {
         if (chain) {
+#if defined(UQ_EXP_NO_CHAIN)
+            return;
+#endif
             const float* row = s[ch % 3] + ck * kNormClientStride + cl * kNormRow;
+#if defined(UQ_EXP_CHAIN_PIPE)
+            // LDS reads one 16-step group ahead of the fma chain (the chain is the wave's
+            // critical path: 256 dependent fmas per chunk)
+            float4 ta[4], tb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) ta[u] = *reinterpret_cast<const float4*>(row + 4 * u);
+            auto chain16 = [&](const float4 (&t)[4]) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc = fmaf(t[u].x, t[u].x, acc);
+                    acc = fmaf(t[u].y, t[u].y, acc);
+                    acc = fmaf(t[u].z, t[u].z, acc);
+                    acc = fmaf(t[u].w, t[u].w, acc);
+                }
+            };
+#pragma unroll
+            for (int i = 0; i < kNormChunk / 8; i += 32) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) tb[u] = *reinterpret_cast<const float4*>(row + i + 16 + 4 * u);
+                chain16(ta);
+                if (i + 32 < kNormChunk / 8) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) ta[u] = *reinterpret_cast<const float4*>(row + i + 32 + 4 * u);
+                }
+                chain16(tb);
+            }
+#else
             for (int i = 0; i < kNormChunk / 8; i += 16) {
                 float4 t[4];
 #pragma unroll
@@ -1581,7 +1613,11 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
                     acc = fmaf(t[u].w, t[u].w, acc);
                 }
             }
+#endif
         } else if (dotw) {
+#if defined(UQ_EXP_NO_DOT)
+            return;
+#endif
             // element 64 s + dl of the chunk sits at lane (dl % 8), step 8 s + dl / 8 of the image
             const float* row = s[ch % 3] + dk * kNormClientStride + (dl & 7) * kNormRow + (dl >> 3);
 #pragma unroll 8

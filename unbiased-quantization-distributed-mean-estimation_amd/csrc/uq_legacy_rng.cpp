@@ -38,9 +38,18 @@
 // rounded through sqrt and squared as np.linalg.norm(v) ** 2 does.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <sys/mman.h>
+#include <unistd.h>
 #include <thread>
 #include <vector>
 
@@ -85,35 +94,129 @@ inline void twist(uint32_t* s) {          // one MT19937 block, in place (numpy'
 // of block a / 624 (block b = b twists of block 0).  A RandomState at pos p reads word p next.
 struct Stream {
     uint32_t s[kN];
+    uint32_t t[kN];                       // s tempered (the words as drawn)
     int64_t blk = 0;
     int idx = 0;
 
+    void temper_all() {
+        for (int i = 0; i < kN; ++i) t[i] = temper(s[i]);
+    }
     bool seek(const uint32_t* key, int64_t a) {
         blk = a / kN;
         idx = (int)(a % kN);
         std::memcpy(s, key, sizeof(s));
         if (blk <= 64) {
             for (int64_t b = 0; b < blk; ++b) twist(s);
-            return true;
+        } else {
+            uint32_t out[kN];
+            if (uq_mt_jump_host(key, blk, out)) return false;
+            std::memcpy(s, out, sizeof(s));
         }
-        uint32_t out[kN];
-        if (uq_mt_jump_host(key, blk, out)) return false;
-        std::memcpy(s, out, sizeof(s));
+        temper_all();
         return true;
     }
     int64_t pos() const { return blk * kN + idx; }
     inline uint32_t next() {
         if (idx == kN) {
             twist(s);
+            temper_all();
             ++blk;
             idx = 0;
         }
-        return temper(s[idx++]);
+        return t[idx++];
     }
     inline double next_double() {
         const int32_t a = (int32_t)(next() >> 5), b = (int32_t)(next() >> 6);
         return (a * 67108864.0 + b) / 9007199254740992.0;
     }
+};
+
+// Value buffers come from a process-wide pool: a C4 call draws ~3.4 GB of f64 values, and
+// fresh pages for them every call (mmap'd, first-touch faults from every thread) cost more than
+// the draws on a VM host.  New buffers are 2 MB aligned and advised as huge pages; returned ones
+// are kept up to a quarter of physical memory (at most 32 GB).
+class Pool {
+  public:
+    static Pool& get() {
+        static Pool p;
+        return p;
+    }
+    double* take(size_t& cap) {                         // at least cap doubles; cap := the real size
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            auto it = free_.lower_bound(cap);
+            if (it != free_.end()) {
+                cap = it->first;
+                double* b = it->second;
+                held_ -= it->first * sizeof(double);
+                free_.erase(it);
+                return b;
+            }
+        }
+        const size_t bytes = ((cap * sizeof(double) + kAlign - 1) / kAlign) * kAlign;
+        void* m = nullptr;
+        if (posix_memalign(&m, kAlign, bytes)) return nullptr;
+        madvise(m, bytes, MADV_HUGEPAGE);
+        cap = bytes / sizeof(double);
+        return static_cast<double*>(m);
+    }
+    void give(double* b, size_t cap) {
+        if (!b) return;
+        std::lock_guard<std::mutex> g(mu_);
+        if (held_ + cap * sizeof(double) > limit_) {
+            std::free(b);
+            return;
+        }
+        held_ += cap * sizeof(double);
+        free_.emplace(cap, b);
+    }
+
+  private:
+    Pool() {
+        const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+        const double phys = pages > 0 && psz > 0 ? (double)pages * (double)psz : 16e9;
+        limit_ = (size_t)std::min(32e9, phys / 4);
+    }
+    static constexpr size_t kAlign = 2u << 20;
+    std::mutex mu_;
+    std::multimap<size_t, double*> free_;
+    size_t held_ = 0, limit_ = 0;
+};
+
+// A growable array of doubles that does not initialise what it allocates.
+struct DBuf {
+    double* p = nullptr;
+    size_t n = 0, cap = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    DBuf(DBuf&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
+    DBuf& operator=(DBuf&& o) noexcept {
+        if (this != &o) {
+            Pool::get().give(p, cap);
+            p = o.p; n = o.n; cap = o.cap;
+            o.p = nullptr; o.n = o.cap = 0;
+        }
+        return *this;
+    }
+    ~DBuf() { Pool::get().give(p, cap); }
+    void reserve(size_t c) {
+        if (c <= cap) return;
+        size_t nc = c;
+        double* q = Pool::get().take(nc);
+        if (!q) throw std::bad_alloc();
+        if (n) std::memcpy(q, p, n * sizeof(double));
+        Pool::get().give(p, cap);
+        p = q;
+        cap = nc;
+    }
+    void push_back(double v) {
+        if (n == cap) reserve(cap ? 2 * cap : 1024);
+        p[n++] = v;
+    }
+    double* data() { return p; }
+    const double* data() const { return p; }
+    size_t size() const { return n; }
 };
 
 struct PState {
@@ -205,7 +308,7 @@ struct JState {
 struct Chunk {
     int64_t w0 = 0, w1 = 0, stop = 0;
     PState start{};
-    std::vector<double> vals;
+    DBuf vals;
     std::vector<PState> head;       // state before value j, j = 0.., while p < w0 + overlap
     std::vector<JState> tail;       // states with p >= w1, in order
     std::vector<JState> ckpt;       // every kCkpt-th state, in order
@@ -251,6 +354,35 @@ struct Parser {
         ++j;
         record();
     }
+    // The same steps while st.p < limit (<= c->w1), for a parse past its head window: locals in
+    // registers, checkpoints only at their boundaries; a state reaching w1 is recorded as tail.
+    void run_body(const Par& q, int64_t limit) {
+        if (st.p >= limit) return;
+        int32_t hh = h;
+        double gg = g;
+        int64_t jj = j, p = st.p;
+        DBuf& V = c->vals;
+        const double wpv = words_per_value(D);
+        while (p < limit) {
+            const int64_t cnt = (jj / kCkpt + 1) * kCkpt - jj;
+            if (V.cap < V.n + (size_t)cnt)
+                V.reserve(std::max(V.n + (size_t)cnt, V.n + (size_t)((double)(limit - p) / wpv * 1.02) + 64));
+            double* o = V.data() + V.n;
+            int64_t k = 0;
+            for (; k < cnt && p < limit; ++k) {
+                o[k] = draw<D>(w, hh, gg, q);
+                p = w.pos();
+            }
+            V.n += (size_t)k;
+            jj += k;
+            if (jj % kCkpt == 0) c->ckpt.push_back(JState{jj, PState{p, hh, gg}});
+        }
+        h = hh;
+        g = gg;
+        j = jj;
+        st = PState{p, hh, gg};
+        if (st.p >= c->w1) c->tail.push_back(JState{j, st});
+    }
 };
 
 // Gamma's phase: with p the word position and h the cache flag, (p / 2 + h) mod 2 is kept by
@@ -266,9 +398,15 @@ void parse_chunk(const uint32_t* key, const Par& q, Chunk& c, bool speculative) 
         c.ok = false;
         return;
     }
-    if (D != kGamma || !speculative) {
+    auto finish = [&]() {                    // A from here to its stop
+        if (speculative)
+            while (A.st.p < A.head_end && A.st.p < c.stop) A.step(q);
+        A.run_body(q, std::min(c.w1, c.stop));
         while (A.st.p < c.stop) A.step(q);
         c.end = A.st;
+    };
+    if (D != kGamma || !speculative) {
+        finish();
         return;
     }
     c.alt.resize(1);
@@ -283,18 +421,19 @@ void parse_chunk(const uint32_t* key, const Par& q, Chunk& c, bool speculative) 
         return;
     }
     for (;;) {
-        if (!c.merged && A.st.p == B.st.p && same_state(A.st, B.st, true)) {
+        if (A.st.p == B.st.p && same_state(A.st, B.st, true)) {
             c.merged = true;
             c.alt_j = B.j;
             c.pri_j = A.j;
+            break;
         }
-        const bool a_live = A.st.p < c.stop, b_live = !c.merged && B.st.p < c.stop;
+        const bool a_live = A.st.p < c.stop, b_live = B.st.p < c.stop;
         if (b_live && (!a_live || B.st.p <= A.st.p)) B.step(q);
         else if (a_live) A.step(q);
         else break;
     }
-    c.end = A.st;
     b.end = B.st;
+    finish();
 }
 
 // Chunk c's alternative parse as the chunk itself (merged: its prefix, then the primary's rest).
@@ -302,8 +441,11 @@ void take_alt(Chunk& c) {
     Chunk& b = c.alt[0];
     if (c.merged) {
         const int64_t shift = c.alt_j - c.pri_j;
-        b.vals.resize((size_t)c.alt_j);
-        b.vals.insert(b.vals.end(), c.vals.begin() + c.pri_j, c.vals.end());
+        b.vals.n = (size_t)c.alt_j;
+        const size_t rest = c.vals.size() - (size_t)c.pri_j;
+        b.vals.reserve(b.vals.n + rest);
+        if (rest) std::memcpy(b.vals.data() + b.vals.n, c.vals.data() + c.pri_j, rest * sizeof(double));
+        b.vals.n += rest;
         auto cut = [](std::vector<JState>& v, int64_t j) {
             v.erase(std::remove_if(v.begin(), v.end(), [j](const JState& x) { return x.j > j; }), v.end());
         };
@@ -315,7 +457,7 @@ void take_alt(Chunk& c) {
             if (x.j > c.pri_j) b.ckpt.push_back(JState{x.j + shift, x.st});
         b.end = c.end;
     }
-    c.vals.swap(b.vals);
+    std::swap(c.vals, b.vals);
     c.head.swap(b.head);
     c.tail.swap(b.tail);
     c.ckpt.swap(b.ckpt);
@@ -372,6 +514,7 @@ int64_t find_head(const Chunk& nx, const PState& x, bool ug) {
 template <int D>
 int draw_all(uint32_t* key, int32_t* pos, int32_t* has_gauss, double* gauss_v, const Par& q, int64_t n, int64_t d,
              float* out, double* norm2, int threads) {
+    const auto t_start = std::chrono::steady_clock::now();
     const bool ug = uses_gauss(D);
     const int64_t total = n * d;
     PState cur{(int64_t)*pos, ug ? *has_gauss : 0, ug ? *gauss_v : 0.0};
@@ -458,6 +601,7 @@ int draw_all(uint32_t* key, int32_t* pos, int32_t* has_gauss, double* gauss_v, c
         if (wave_vals > 0) wpv = std::max(1.0, (double)(wave_end.p - cur.p) / (double)wave_vals);
         cur = wave_end;
     }
+    const auto t_scatter = std::chrono::steady_clock::now();
     // scatter: f32 values and ||v||^2 of each vector, in a fixed order of the vector's elements
     const int64_t nb = (d + kNormBlock - 1) / kNormBlock;
     std::vector<double> part((size_t)(n * nb), 0.0);
@@ -492,6 +636,10 @@ int draw_all(uint32_t* key, int32_t* pos, int32_t* has_gauss, double* gauss_v, c
         const double r = std::sqrt(s);
         norm2[i] = r * r;                       // np.linalg.norm(v) ** 2
     }
+    if (std::getenv("UQDME_LEGACY_PROF"))
+        std::fprintf(stderr, "legacy_draw: parse %.1f ms, scatter %.1f ms\n",
+                     std::chrono::duration<double, std::milli>(t_scatter - t_start).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_scatter).count());
     // the RandomState after the draws: key = the block holding word cur.p - 1, pos = its index + 1
     if (cur.p != (int64_t)*pos) {
         const int64_t last = cur.p - 1;

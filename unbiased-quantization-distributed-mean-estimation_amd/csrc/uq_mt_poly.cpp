@@ -106,6 +106,17 @@ __attribute__((target("pclmul"))) inline void clmul64_hw(uint64_t a, uint64_t b,
     hi = (uint64_t)_mm_cvtsi128_si64(_mm_unpackhi_epi64(p, p));
 }
 
+// acc[w] ^= x[k + w] for every set coefficient k of g: the jump's correlation (AVX2 where the
+// CPU has it: 624 words are 78 ymm XORs per coefficient, ~10^4 coefficients per jump)
+__attribute__((target_clones("avx2", "default"))) void correlate(const uint64_t* g, const uint32_t* x,
+                                                                 uint32_t* acc) {
+    for (int k = 0; k < kDeg; ++k)
+        if ((g[k >> 6] >> (k & 63)) & 1u) {
+            const uint32_t* xk = x + k;
+            for (int w = 0; w < kMtN; ++w) acc[w] ^= xk[w];
+        }
+}
+
 class MtPoly {
   public:
     static MtPoly& get() {
@@ -148,9 +159,7 @@ class MtPoly {
             std::memcpy(x.data() + (size_t)blk * kMtN, m.s, kMtN * 4);
         }
         uint32_t acc[kMtN] = {};
-        for (int k = 0; k < kDeg; ++k)
-            if ((g.w[k >> 6] >> (k & 63)) & 1u)
-                for (int w = 0; w < kMtN; ++w) acc[w] ^= x[(size_t)k + w];
+        correlate(g.w, x.data(), acc);
         std::memcpy(m.s, acc, sizeof(acc));           // block b - 1 (word 0's low 31 bits aside)
         m.twist();                                    // block b: every word exact
         std::memcpy(out, m.s, kMtN * 4);

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import time
 
 import numpy as np
 import torch
@@ -39,7 +40,7 @@ from .quicfl import quicfl_quantize
 
 SCHEME_ORDER = ("eden", "unbiased", "biased", "quicfl")     # ND:135-142 call order
 
-__all__ = ["DISTRIBUTIONS", "draw_vectors", "legacy_draw", "nmse_simulation", "USERS_ND"]
+__all__ = ["DISTRIBUTIONS", "draw_vectors", "legacy_draw", "nmse_simulation", "Suspended", "USERS_ND"]
 
 # ND:43 (also Lognormal_dist.py:43): num_users_list = arange(1, 102, 5); Laplace/Gamma/
 # Bernoulli drivers use arange(1, 101, 5).
@@ -127,52 +128,94 @@ def legacy_draw(rs: np.random.RandomState, dist: str, n: int, dim: int, threads:
 
 
 def _draw_ahead(dist: str, users, num_instances: int, dim: int, rs, device=None, threads=None):
-    """The instances' batches in the drivers' order, drawn one instance ahead on a thread:
-    yields (f32 batch [n, dim] on `device` (numpy if None), sum ||v||^2 (ND:94, summed in the
-    drivers' order), emp (ND:95: the batch's f32 sum over clients / n, torch CPU)).  The legacy
-    stream is drawn by legacy_draw on host threads, used by this thread alone, so it is the
-    drivers' stream; the draws, the CPU sum and the host-to-device copy (on a side stream, ready
-    when yielded) overlap the previous instance's quantization.
-    Host memory: up to three batches (the one in use, one queued, one being drawn) plus the
-    draw's f64 values of the batch being drawn: about 20 n * dim bytes at the peak."""
+    """The instances' batches in the drivers' order, in a three-stage pipeline ahead of the
+    caller: yields (x [n, dim] f32 -- on `device`, a CPU tensor if None --, sum ||v||^2 (ND:94,
+    summed in the drivers' order), emp (ND:95: the batch's f32 sum over clients / n on the CPU,
+    as torch computes it), the legacy state before this batch was drawn).
+      * drawer thread: legacy_draw (host threads, the drivers' exact stream; rs is used by this
+        thread alone) straight into one of three reusable (pinned, with a device) host buffers;
+      * prep thread: emp, and the host-to-device copy on a side stream (ready when yielded;
+        the caller records its own stream on the tensor before using it);
+      * the caller quantizes the previous batch meanwhile.
+    Host memory: three buffers of max(users) * dim f32, plus the draw's f64 values of the batch
+    being drawn (8 n * dim bytes, pooled inside the library)."""
     import queue
     import threading
 
-    q: queue.Queue = queue.Queue(maxsize=1)
+    total = len(users) * num_instances
     stop = threading.Event()
+    nmax = max(users) if len(users) else 0
+    ring: queue.Queue = queue.Queue()
+    for _ in range(3 if total else 0):
+        ring.put(torch.empty((nmax, dim), dtype=torch.float32, pin_memory=device is not None))
+    q1: queue.Queue = queue.Queue(maxsize=1)
+    q2: queue.Queue = queue.Queue(maxsize=1)
     side = torch.cuda.Stream(device) if device is not None else None
 
-    def work():
+    def put(q, item):
+        while not stop.is_set():
+            try:
+                q.put(item, timeout=0.5)
+                return True
+            except queue.Full:
+                pass
+        return False
+
+    def get(q):
+        while not stop.is_set():
+            try:
+                return q.get(timeout=0.5)
+            except queue.Empty:
+                pass
+        return None
+
+    def draw():
         try:
             for n in users:
                 for _ in range(num_instances):
-                    batch, norms = legacy_draw(rs, dist, n, dim, threads)                  # ND:88-91
+                    buf = get(ring)
+                    if buf is None:
+                        return
+                    st = rs.get_state(legacy=True)
+                    _, norms = legacy_draw(rs, dist, n, dim, threads, out=buf[:n].numpy())   # ND:88-91
                     vns = 0
                     for v in norms.tolist():                                               # ND:94 sum(list)
                         vns += v
-                    xs = torch.from_numpy(batch)
-                    emp = xs.sum(dim=0) / n                                                # ND:95 (CPU)
-                    if side is not None:
-                        with torch.cuda.stream(side):
-                            xs = xs.to(device)
-                        side.synchronize()
-                    del batch
-                    while not stop.is_set():
-                        try:
-                            q.put((xs, float(vns), emp), timeout=0.5)
-                            break
-                        except queue.Full:
-                            pass
-                    if stop.is_set():
+                    if not put(q1, (buf, n, float(vns), st)):
                         return
         except BaseException as e:                                            # re-raised by the consumer
-            q.put(e)
+            put(q1, e)
 
-    t = threading.Thread(target=work, daemon=True)
-    t.start()
+    def prep():
+        try:
+            for _ in range(total):
+                item = get(q1)
+                if item is None:
+                    return
+                if isinstance(item, BaseException):
+                    put(q2, item)
+                    return
+                buf, n, vns, st = item
+                xs = buf[:n]
+                emp = xs.sum(dim=0) / n                                            # ND:95 (CPU)
+                if side is not None:
+                    with torch.cuda.stream(side):
+                        x = xs.to(device, non_blocking=True)
+                    side.synchronize()
+                else:
+                    x = xs.clone()
+                ring.put(buf)
+                if not put(q2, (x, vns, emp, st)):
+                    return
+        except BaseException as e:
+            put(q2, e)
+
+    workers = [threading.Thread(target=f, daemon=True) for f in (draw, prep)]
+    for w in workers:
+        w.start()
     try:
-        for _ in range(len(users) * num_instances):
-            item = q.get()
+        for _ in range(total):
+            item = q2.get()
             if isinstance(item, BaseException):
                 raise item
             yield item
@@ -180,10 +223,24 @@ def _draw_ahead(dist: str, users, num_instances: int, dim: int, rs, device=None,
         stop.set()
 
 
+class Suspended(Exception):
+    """nmse_simulation stopped at a user-count boundary (time_limit_s); its checkpoint file
+    holds everything needed to resume there."""
+
+
+def _save_checkpoint(path, meta, ui, rs_state, gen_state, script):
+    tmp = path + ".tmp.npz"
+    _, key, pos, hg, g = rs_state
+    np.savez(tmp, meta=np.frombuffer(repr(meta).encode(), np.uint8), ui=ui, key=np.asarray(key, np.uint32),
+             pos=pos, has_gauss=hg, gauss=g, gen=gen_state.numpy(),
+             **{f"script_{sc}_{r}": v for (sc, r), v in script.items()})
+    os.replace(tmp, path)
+
+
 def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_instances: int = 50,
                     num_trials: int = 50, rates=(1, 2), seed: int = 42, torch_threads: int = 1,
                     device=None, schemes=("unbiased",), progress=None, eden_scales=None, eden_scales_out=None,
-                    quicfl=None, threads=None):
+                    quicfl=None, threads=None, stats=None, checkpoint=None, time_limit_s=None):
     """NMSE curves of the selected schemes with the reference's normalisation.
 
     Returns {rate: {...}} for the default unbiased-only run, else {(scheme, rate): {...}};
@@ -192,7 +249,12 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
     eden_scales {(n, inst, rate): [scale per client]} replaces EDEN's scale (AS:348) by the
     given values (the receiver then runs on them); eden_scales_out, a dict, receives the
     scales computed here under the same keys.  threads: host threads for the draws
-    (legacy_draw; default host_threads())."""
+    (legacy_draw; default host_threads()).  stats, a dict, receives "wait_s": the time spent
+    waiting for drawn batches (the part of the run the host draws did not hide).
+    checkpoint: a file path; at the start of every user count the run saves there the legacy and
+    torch generator states and the finished rows, and a call with an existing checkpoint of the
+    same configuration resumes from it (the streams continue exactly).  time_limit_s: stop at
+    the first user-count boundary after that many seconds, raising Suspended (checkpoint saved)."""
     device = device or torch.device("cuda", torch.cuda.current_device())
     schemes = tuple(schemes)
     for sc in schemes:
@@ -208,11 +270,34 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
     gen = torch.Generator().manual_seed(seed)        # == torch.manual_seed(seed) CPU stream
     keys = [(sc, r) for sc in order for r in rates]
     script = {k: np.zeros((len(users), num_instances), np.float64) for k in keys}
-    batches = _draw_ahead(dist, users, num_instances, dim, rs, device=device, threads=threads)
-    for ui, n in enumerate(users):
+    users = tuple(int(u) for u in users)
+    meta = (dist, dim, users, num_instances, num_trials, tuple(rates), seed, torch_threads, tuple(order))
+    start_ui = 0
+    if checkpoint is not None and os.path.exists(checkpoint):
+        with np.load(checkpoint, allow_pickle=False) as ck:
+            if bytes(ck["meta"]).decode() != repr(meta):
+                raise ValueError(f"checkpoint {checkpoint} is of another configuration")
+            start_ui = int(ck["ui"])
+            rs.set_state(("MT19937", ck["key"], int(ck["pos"]), int(ck["has_gauss"]), float(ck["gauss"])))
+            gen.set_state(torch.from_numpy(ck["gen"].copy()))
+            for sc, r in keys:
+                script[(sc, r)][:] = ck[f"script_{sc}_{r}"]
+    t_start = time.perf_counter()
+    batches = _draw_ahead(dist, users[start_ui:], num_instances, dim, rs, device=device, threads=threads)
+    for ui in range(start_ui, len(users)):
+        n = users[ui]
         for inst in range(num_instances):
-            xd, vns, emp = next(batches)                                                   # ND:88-95
-            xd.record_stream(torch.cuda.current_stream(device))   # drawn on the side stream, used here
+            t_wait = time.perf_counter()
+            xd, vns, emp, rs_before = next(batches)                                        # ND:88-95
+            if stats is not None:
+                stats["wait_s"] = stats.get("wait_s", 0.0) + time.perf_counter() - t_wait
+            if inst == 0 and checkpoint is not None:       # both streams as they stand before this user count
+                _save_checkpoint(checkpoint, meta, ui, rs_before, gen.get_state(), script)
+                if time_limit_s is not None and ui > start_ui and time.perf_counter() - t_start > time_limit_s:
+                    batches.close()
+                    raise Suspended(f"suspended before user count {n} (index {ui}); resume from {checkpoint}")
+            if xd.is_cuda:
+                xd.record_stream(torch.cuda.current_stream(device))   # copied on the side stream, used here
             draws = {k: [] for k in keys}
             for _ in range(n):                        # ND:133-140: client-major, scheme/rate-minor
                 for sc in order:
@@ -249,6 +334,8 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                 script[(sc, r)][ui, inst] = float(torch.norm(est - emp).pow(2) / (num_trials * vns * n))   # ND:155
             if progress is not None:
                 progress(n, inst)
+    if checkpoint is not None:                        # finished: a rerun returns the same rows
+        _save_checkpoint(checkpoint, meta, len(users), rs.get_state(legacy=True), gen.get_state(), script)
     out = {}
     for k in keys:
         sv = script[k].astype(np.float32)             # the reference stores NMSE in f32 tensors
