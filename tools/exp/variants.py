@@ -28,9 +28,11 @@ def build(spec_path):
     spec.loader.exec_module(be)
     variants = json.load(open(spec_path))
     shutil.rmtree(OUT, ignore_errors=True)
-    obj = os.path.join(OUT, "uq_mt_poly.o")
     os.makedirs(OUT)
-    subprocess.run(["g++", *be.HOST_FLAGS, "-c", "-o", obj, os.path.join(PKG, "csrc", "uq_mt_poly.cpp")], check=True)
+    objs = []                                      # the tree's host code (no GPU work) in every variant
+    for f in be.HOST_SRCS:
+        objs.append(os.path.join(OUT, os.path.basename(f)[:-4] + ".o"))
+        subprocess.run(["g++", *be.HOST_FLAGS, "-c", "-o", objs[-1], f], check=True)
     procs = []
     for name, subs in variants.items():
         top = os.path.join(OUT, name)
@@ -49,6 +51,9 @@ def build(spec_path):
         else:
             for f in os.listdir(os.path.join(PKG, "csrc")):
                 shutil.copy(os.path.join(PKG, "csrc", f), src)
+        for f in os.listdir(src):                  # host sources are linked from objs
+            if f.endswith(".cpp"):
+                os.remove(os.path.join(src, f))
         for fname, old, new in subs:
             p = os.path.join(src, fname)
             t = open(p).read()
@@ -56,7 +61,7 @@ def build(spec_path):
             open(p, "w").write(t.replace(old, new))
         so = os.path.join(top, "libuq_dme.so")
         procs.append((name, subprocess.Popen([be.hipcc(), *be.HIPCC_FLAGS, "-o", so, os.path.join(src, "uq_dme.hip"),
-                                              "-x", "none", obj])))
+                                              "-x", "none", *objs, "-lpthread"])))
     bad = [n for n, p in procs if p.wait() != 0]
     if bad:
         raise SystemExit(f"variant builds failed: {bad}")

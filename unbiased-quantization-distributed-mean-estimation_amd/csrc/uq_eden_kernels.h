@@ -1538,6 +1538,13 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
 #pragma unroll
         for (int q = 0; q < kLQ; ++q) nx[q] = ld_stream(reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q)));
     };
+    // The bins of a chunk are computed when it is staged and stored after the next loads are
+    // issued (flush_bins): vmcnt retires in issue order, so a store issued just before a load
+    // would make the wait for that load also wait for the store's acknowledgement
+    // (1-bit 1024 x 2^20 round trip 6.58 -> 6.44 ms, profiles/r6c_ab_eden.jsonl; without the
+    // bins stores at all 6.08 ms, r6b_eden_ab.jsonl).
+    uint32_t bw[kLQ];
+    int64_t bch = -1;
     auto store = [&](const float4 (&nx)[kLQ], float* sb, int64_t ch) {
         if (!loader) return;
 #pragma unroll
@@ -1549,20 +1556,24 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
             base[(l + 1) * kNormRow] = nx[q].y;
             base[(l + 2) * kNormRow] = nx[q].z;
             base[(l + 3) * kNormRow] = nx[q].w;
-            if (lvalid) {                                              // the bins of these 4 (sign rule)
-                const float xs[4] = {nx[q].x, nx[q].y, nx[q].z, nx[q].w};
-                uint32_t w = 0;
+            const float xs[4] = {nx[q].x, nx[q].y, nx[q].z, nx[q].w};   // the bins of these 4 (sign rule)
+            uint32_t w = 0;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float y = xs[c] * sqrtD;
-                    w |= (!(y <= 0.f) ? 1u : 0u) << (8 * c);
-                    if (y > 0.f) mymin = min(mymin, __float_as_uint(y));
-                }
-#if !defined(UQ_EXP_NO_BINS)
-                *reinterpret_cast<uint32_t*>(lb + ch * kNormChunk + e) = w;
-#endif
+            for (int c = 0; c < 4; ++c) {
+                const float y = xs[c] * sqrtD;
+                w |= (!(y <= 0.f) ? 1u : 0u) << (8 * c);
+                if (lvalid && y > 0.f) mymin = min(mymin, __float_as_uint(y));
             }
+            bw[q] = w;
         }
+        bch = ch;
+    };
+    auto flush_bins = [&]() {
+        if (!lvalid || bch < 0) return;
+#pragma unroll
+        for (int q = 0; q < kLQ; ++q)
+            __builtin_nontemporal_store(bw[q], reinterpret_cast<uint32_t*>(lb + bch * kNormChunk + 4 * (lj + 64 * q)));
+        bch = -1;
     };
     const int ck = (tid >> 3) & (kNormClients - 1), cl = tid & 7;
     float acc = 0.f;
@@ -1570,37 +1581,7 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
     const EdenCents cs = eden_cents(tab);
     auto chainstep = [&](int64_t ch) {
         if (chain) {
-#if defined(UQ_EXP_NO_CHAIN)
-            return;
-#endif
             const float* row = s[ch % 3] + ck * kNormClientStride + cl * kNormRow;
-#if defined(UQ_EXP_CHAIN_PIPE)
-            // LDS reads one 16-step group ahead of the fma chain (the chain is the wave's
-            // critical path: 256 dependent fmas per chunk)
-            float4 ta[4], tb[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) ta[u] = *reinterpret_cast<const float4*>(row + 4 * u);
-            auto chain16 = [&](const float4 (&t)[4]) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    acc = fmaf(t[u].x, t[u].x, acc);
-                    acc = fmaf(t[u].y, t[u].y, acc);
-                    acc = fmaf(t[u].z, t[u].z, acc);
-                    acc = fmaf(t[u].w, t[u].w, acc);
-                }
-            };
-#pragma unroll
-            for (int i = 0; i < kNormChunk / 8; i += 32) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) tb[u] = *reinterpret_cast<const float4*>(row + i + 16 + 4 * u);
-                chain16(ta);
-                if (i + 32 < kNormChunk / 8) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) ta[u] = *reinterpret_cast<const float4*>(row + i + 32 + 4 * u);
-                }
-                chain16(tb);
-            }
-#else
             for (int i = 0; i < kNormChunk / 8; i += 16) {
                 float4 t[4];
 #pragma unroll
@@ -1613,11 +1594,7 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
                     acc = fmaf(t[u].w, t[u].w, acc);
                 }
             }
-#endif
         } else if (dotw) {
-#if defined(UQ_EXP_NO_DOT)
-            return;
-#endif
             // element 64 s + dl of the chunk sits at lane (dl % 8), step 8 s + dl / 8 of the image
             const float* row = s[ch % 3] + dk * kNormClientStride + (dl & 7) * kNormRow + (dl >> 3);
 #pragma unroll 8
@@ -1633,6 +1610,7 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
         store(na, s[0], 0);
         load(na, 1);
         load(nb, 2);
+        flush_bins();
     }
     __syncthreads();
     for (int64_t ch = 0; ch < nchunks; ch += 2) {
@@ -1640,6 +1618,7 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
         if (loader && ch + 1 < nchunks) {
             store(na, s[(ch + 1) % 3], ch + 1);
             load(na, ch + 3);
+            flush_bins();
         }
         __syncthreads();
         if (ch + 1 >= nchunks) break;
@@ -1647,6 +1626,7 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
         if (loader && ch + 2 < nchunks) {
             store(nb, s[(ch + 2) % 3], ch + 2);
             load(nb, ch + 4);
+            flush_bins();
         }
         __syncthreads();
     }
