@@ -1538,13 +1538,14 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
 #pragma unroll
         for (int q = 0; q < kLQ; ++q) nx[q] = ld_stream(reinterpret_cast<const float4*>(lp + ch * kNormChunk + 4 * (lj + 64 * q)));
     };
-    // The bins of a chunk are computed when it is staged and stored after the next loads are
-    // issued (flush_bins): vmcnt retires in issue order, so a store issued just before a load
-    // would make the wait for that load also wait for the store's acknowledgement
-    // (1-bit 1024 x 2^20 round trip 6.58 -> 6.44 ms, profiles/r6c_ab_eden.jsonl; without the
-    // bins stores at all 6.08 ms, r6b_eden_ab.jsonl).
-    uint32_t bw[kLQ];
-    int64_t bch = -1;
+    // The bins of a chunk are computed when it is staged, kept in LDS (sbins, two chunks), and
+    // written after the next barrier by the loaders as 16-byte non-temporal stores (a wave
+    // writes 1 KB of one client's bins per instruction), issued after the next loads: vmcnt
+    // retires in issue order, so a store issued just before a load would make the wait for
+    // that load also wait for the store's acknowledgement.  (1-bit 1024 x 2^20 round trip:
+    // dword stores before the loads 6.58 ms, after them 6.44 ms, profiles/r6c_ab_eden.jsonl;
+    // no bins stores at all 6.08 ms, r6b_eden_ab.jsonl.)
+    __shared__ __attribute__((aligned(16))) uint32_t sbins[2][kNormClients][kNormChunk / 4];
     auto store = [&](const float4 (&nx)[kLQ], float* sb, int64_t ch) {
         if (!loader) return;
 #pragma unroll
@@ -1564,16 +1565,18 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
                 w |= (!(y <= 0.f) ? 1u : 0u) << (8 * c);
                 if (lvalid && y > 0.f) mymin = min(mymin, __float_as_uint(y));
             }
-            bw[q] = w;
+            sbins[ch & 1][lk][lj + 64 * q] = w;
         }
-        bch = ch;
     };
-    auto flush_bins = [&]() {
-        if (!lvalid || bch < 0) return;
+    auto flush_bins = [&](int64_t ch) {          // chunk ch's bins, staged before the last barrier
+        if (!lvalid) return;
+        typedef uint32_t u32x4b __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int q = 0; q < kLQ; ++q)
-            __builtin_nontemporal_store(bw[q], reinterpret_cast<uint32_t*>(lb + bch * kNormChunk + 4 * (lj + 64 * q)));
-        bch = -1;
+        for (int r = 0; r < kNormChunk / 4 / 256; ++r) {
+            const int w0 = 4 * (lj + 64 * r);
+            const u32x4b t = *reinterpret_cast<const u32x4b*>(&sbins[ch & 1][lk][w0]);
+            __builtin_nontemporal_store(t, reinterpret_cast<u32x4b*>(lb + ch * kNormChunk + 4 * w0));
+        }
     };
     const int ck = (tid >> 3) & (kNormClients - 1), cl = tid & 7;
     float acc = 0.f;
@@ -1610,7 +1613,6 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
         store(na, s[0], 0);
         load(na, 1);
         load(nb, 2);
-        flush_bins();
     }
     __syncthreads();
     for (int64_t ch = 0; ch < nchunks; ch += 2) {
@@ -1618,16 +1620,16 @@ eden_normdot1_kernel(const float* __restrict__ v, int64_t n, int64_t D, float sq
         if (loader && ch + 1 < nchunks) {
             store(na, s[(ch + 1) % 3], ch + 1);
             load(na, ch + 3);
-            flush_bins();
         }
+        if (loader) flush_bins(ch);
         __syncthreads();
         if (ch + 1 >= nchunks) break;
         chainstep(ch + 1);
         if (loader && ch + 2 < nchunks) {
             store(nb, s[(ch + 2) % 3], ch + 2);
             load(nb, ch + 4);
-            flush_bins();
         }
+        if (loader) flush_bins(ch + 1);
         __syncthreads();
     }
     if (lvalid) atomicMin(&minpos[lk], mymin);
