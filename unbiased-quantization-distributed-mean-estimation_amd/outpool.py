@@ -1,6 +1,6 @@
 """Output pool for the one-shot batched APIs (quantize_dequantize, quantize_encode,
 quantize_mean): K2's speed depends on where its OUTPUT buffers sit in physical memory
-("two speeds": q + codes 1.66-1.76 ms or 1.93-2.03 ms per 1024 x 2^20 batch,
+(DESIGN.md §8 and NOTES.md §4, "two speeds": q + codes 1.66-1.76 ms or 1.93-2.03 ms per 1024 x 2^20 batch,
 a property of the buffer set, not of the moment).  DMEPipeline probes its resident outputs
 once; a caller that asks for fresh outputs on every call would draw a new placement each
 time.  For large batches the one-shot APIs therefore take their outputs from this pool:
