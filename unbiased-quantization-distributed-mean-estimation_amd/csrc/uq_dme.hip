@@ -487,7 +487,13 @@ __device__ float lds_torch_sum(const float* a, int s, int lane) {
 // WAVES = 1 when there is one torch chunk (T = 1 or d < 32768): the eight waves' staging
 // buffers (64 KB of LDS) held two workgroups per CU for one working wave (37 us at
 // 1024 x 2^20, T = 1).
-template <class Op, int WAVES = kFinWaves>
+// WIDE (one chunk, a few clients: WAVES = 8, host choice): the level-2 group sums
+// B_h = sum of `step` level-1 block sums in order are independent of each other, so all eight
+// waves form them at once (step loads in flight per thread) and only acc3 = sum of B_h in order
+// stays serial: one client's chain of ng1 dependent adds through eight LDS stages took 65 us at
+// d = 2^22 (half of the n = 1 call, profiles/r6d_c4_unbiased_kernel_stats.csv).  Same adds in
+// the same order.
+template <class Op, int WAVES = kFinWaves, bool WIDE = false>
 __global__ void __launch_bounds__(64 * WAVES)
 l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
                    const float* __restrict__ part, float* __restrict__ l1_out,
@@ -517,6 +523,34 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
     float* s_stage = s_stage_w[wv];
     float* s_tail = s_tail_w[wv];
     for (int t = plan.nchunks + (int)threadIdx.x; t < plan.nbuf; t += 64 * WAVES) s_chunk[t] = 0.0f;
+    float wide_acc3 = 0.f;                            // WIDE: acc3 of chunk 0, lanes < 32 of wave 0
+    if (WIDE) {
+        const ChunkGeo& geo = plan.geo(0);
+        const int64_t step = (int64_t)1 << geo.lp;
+        const int64_t ng2 = geo.ng1 / step;
+        const float* pc = part + (vec * plan.total_groups + plan.gbase(0)) * 32;
+        float* sB = &s_stage_w[0][0];                 // WAVES * kFinStage groups x 32 streams
+        constexpr int kG = WAVES * kFinStage;
+        for (int64_t h0 = 0; h0 < ng2; h0 += kG) {
+            const int nh = (int)std::min<int64_t>(kG, ng2 - h0);
+            for (int t = threadIdx.x; t < nh * 32; t += 64 * WAVES) {
+                const float* src = pc + ((h0 + t / 32) * step) * 32 + (t & 31);
+                float b = 0.f;
+                for (int64_t j0 = 0; j0 < step; j0 += 16) {
+                    float v[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) v[u] = src[(j0 + u) * 32];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) b += v[u];
+                }
+                sB[t] = b;
+            }
+            __syncthreads();
+            if (wv == 0 && lane < 32)
+                for (int h = 0; h < nh; ++h) wide_acc3 += sB[h * 32 + lane];
+            __syncthreads();
+        }
+    }
     for (int c = wv; c < plan.nchunks; c += WAVES) {
         const int64_t off = plan.off(c);
         const ChunkGeo& geo = plan.geo(c);
@@ -546,7 +580,12 @@ l1_finalize_kernel(const float* __restrict__ x, int64_t d, L1Plan plan,
             const float* pc = part + (vec * plan.total_groups + plan.gbase(c)) * 32;
             float acc3 = 0.f, acc2 = 0.f, b2 = 0.f;
             const int64_t n3 = ng2 * step;
-            for (int64_t k0 = 0; k0 < ng1; k0 += kFinStage) {
+            if (WIDE) {                               // B_h formed above; the rest after n3 in order
+                acc3 = wide_acc3;
+                if (lane < 32)
+                    for (int64_t k = n3; k < ng1; ++k) acc2 += pc[k * 32 + lane];
+            }
+            for (int64_t k0 = WIDE ? ng1 : 0; k0 < ng1; k0 += kFinStage) {
                 const int nk = (int)std::min<int64_t>(kFinStage, ng1 - k0);
                 wave_sync();
                 const float4* src = reinterpret_cast<const float4*>(pc + k0 * 32);
@@ -2441,6 +2480,11 @@ int launch_cascade(const float* x, int64_t n, int64_t d, const L1Plan& plan, flo
         }
         int rc = hip_check(hipGetLastError(), "l1_partial_kernel launch");
         if (rc) return rc;
+    }
+    if (plan.nchunks == 1 && n <= 128 && plan.last.size >= 8 && plan.last.ng1 >= 64 && !std::getenv("UQDME_K1B_NARROW")) {
+        hipLaunchKernelGGL((l1_finalize_kernel<Op, kFinWaves, true>), dim3((unsigned)n), dim3(64 * kFinWaves),
+                           (size_t)plan.nbuf * sizeof(float), st, x, d, plan, part, sum_out, l1, fm, hist, zn);
+        return hip_check(hipGetLastError(), "l1_finalize_kernel (wide) launch");
     }
     if (plan.nchunks == 1) {
         hipLaunchKernelGGL((l1_finalize_kernel<Op, 1>), dim3((unsigned)n), dim3(64), (size_t)plan.nbuf * sizeof(float), st,
