@@ -1717,7 +1717,7 @@ template <bool VEC4>
 __global__ void __launch_bounds__(kQBlock)
 tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm, const float* __restrict__ l1,
                 const uint64_t* __restrict__ agg, uint64_t* __restrict__ map0, uint64_t* __restrict__ map1,
-                TileRec* __restrict__ recs, uint32_t* __restrict__ reccnt) {
+                TileRec* __restrict__ recs, uint32_t* __restrict__ reccnt, int32_t prefixed) {
     __shared__ __attribute__((aligned(16))) float s_x[kQTile];
     __shared__ ScanLds sl;
     const int tid = threadIdx.x;
@@ -1726,8 +1726,21 @@ tile_map_kernel(const float* __restrict__ x, int64_t d, int32_t tiles, float fm,
     const int64_t idx = vec * tiles + tile;
     TileRegs r;
     load_tile<VEC4>(r, x, d, tiles, (uint32_t)idx, tid);
-    // P'_t = the approximate tile sums before t (tile_prefix_kernel; it only picks the binade)
-    const double Pg = uniform_d(__longlong_as_double((long long)agg[idx]));
+    // P'_t = the approximate tile sums before t, in any order (it only picks the binade): from
+    // tile_prefix_kernel (prefixed), or summed here (a single client: the extra launch costs
+    // more than 1024 tiles' predecessors from L2, 0.155 -> 0.171 ms per call at 2^22)
+    double Pg;
+    if (prefixed) {
+        Pg = uniform_d(__longlong_as_double((long long)agg[idx]));
+    } else {
+        double acc = 0.0;
+        for (int32_t j = tid; j < tile; j += kQBlock) acc += __longlong_as_double((long long)agg[vec * tiles + j]);
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
+        if ((tid & (kWave - 1)) == 0) sl.wave[tid / kWave] = acc;
+        __syncthreads();
+        Pg = uniform_d(((sl.wave[0] + sl.wave[1]) + sl.wave[2]) + sl.wave[3]);
+    }
     const Binade B = binade_of(Pg);
     stage_tile<VEC4>(r, s_x, tid);
     __syncthreads();
@@ -3223,19 +3236,22 @@ int unbiased_codes_impl(const float* x, float* out, int64_t ldo, int8_t* codes, 
         }
         rc = hip_check(hipGetLastError(), "tile sums launch");
         if (rc) return rc;
-        hipLaunchKernelGGL(tile_prefix_kernel, dim3((unsigned)nj), dim3(kQBlock), 0, st, agg, w.tiles);
-        rc = hip_check(hipGetLastError(), "tile_prefix_kernel launch");
-        if (rc) return rc;
+        const int32_t prefixed = nj >= 4 ? 1 : 0;
+        if (prefixed) {
+            hipLaunchKernelGGL(tile_prefix_kernel, dim3((unsigned)nj), dim3(kQBlock), 0, st, agg, w.tiles);
+            rc = hip_check(hipGetLastError(), "tile_prefix_kernel launch");
+            if (rc) return rc;
+        }
         if (vec4) {
             hipLaunchKernelGGL(tile_map_kernel<true>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg, pre, map1, recs,
-                               reccnt);
+                               reccnt, prefixed);
             rc = hip_check(hipGetLastError(), "tile_map_kernel launch");
             if (rc) return rc;
             hipLaunchKernelGGL(exact_fold_kernel<true>, dim3((unsigned)nj), dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j,
                                pre, map1, agg, recs, reccnt);
         } else {
             hipLaunchKernelGGL(tile_map_kernel<false>, tgrid, dim3(kQBlock), 0, st, xj, d, w.tiles, fm, l1j, agg, pre, map1, recs,
-                               reccnt);
+                               reccnt, prefixed);
             rc = hip_check(hipGetLastError(), "tile_map_kernel launch");
             if (rc) return rc;
             hipLaunchKernelGGL(exact_fold_kernel<false>, dim3((unsigned)nj), dim3(kQBlock), 0, st, xj, d, w.tiles, fm,
