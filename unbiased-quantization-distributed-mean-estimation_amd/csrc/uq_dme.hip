@@ -4272,10 +4272,11 @@ static size_t quicfl_jump_off(int64_t n, int64_t dim) {
     return (quicfl_h_off(n, dim) + (size_t)n * (size_t)eden_layout(n, dim).D + 255) & ~(size_t)255;
 }
 // jump region: streams [n][2][kMjX], parts [n][R][3][kMjParts][624], run records [n][R][2]
+// (without the jump path: the local blocks after KQ1a, [n][624])
 static size_t quicfl_ws_total(int64_t n, int64_t dim) {
     const QflJumpPlan p = qfl_jump_plan(n, eden_layout(n, dim).D);
-    const size_t jb =
-        p.use ? ((size_t)n * 2 * kMjX + (size_t)n * p.R * (3 * kMjParts * kMtN + 2)) * sizeof(uint32_t) : 0;
+    const size_t jb = p.use ? ((size_t)n * 2 * kMjX + (size_t)n * p.R * (3 * kMjParts * kMtN + 2)) * sizeof(uint32_t)
+                            : (size_t)n * kMtN * sizeof(uint32_t);
     return quicfl_jump_off(n, dim) + jb;
 }
 
@@ -4291,16 +4292,56 @@ int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
 // (~80 us of small kernels for one 2^20 message); the runs wait for them.
 struct QflJumpLaunch {
     bool use = false;
+    bool passa = false;             // KQ1a runs on the side stream instead (the one-wave form)
     QflJumpPlan jp;
     uint32_t* parts = nullptr;
+    uint32_t* lstate = nullptr;     // KQ1a's local blocks
     SideStream* sb = nullptr;
 };
+// Which sender form a call takes (launch_quicfl_send): 0 the jump path, 1 the team kernel
+// (KQ1t), 2 the one-wave kernel (KQ1).
+static int qfl_send_form(int64_t n, int64_t D, bool jump_use) {
+    const int hooks = g_quicfl_hooks.load();
+    if (jump_use) return 0;
+    const QflJumpPlan jp = qfl_jump_plan(n, D);
+    if (!(hooks & 2) && ((hooks & 5) || !jp.use) && n <= kQfTeamMaxN && D >= (int64_t)kMtN * kQfRuns &&
+        D <= kQfTeamMaxD)
+        return 1;
+    return 2;
+}
 static int quicfl_jump_fork(int64_t n, int64_t D, int64_t dim, const int32_t* prng_seeds, const uint32_t* px_state,
-                            const int32_t* px_seeds, char* wsb, hipStream_t st, QflJumpLaunch* jl) {
+                            const int32_t* px_seeds, int32_t h_len, char* wsb, hipStream_t st, QflJumpLaunch* jl) {
     *jl = QflJumpLaunch{};
     const int hooks = g_quicfl_hooks.load();
     const QflJumpPlan jp = qfl_jump_plan(n, D);
-    if ((hooks & 7) || !jp.use) return UQ_OK;
+    if ((hooks & 7) || !jp.use) {
+        if (qfl_send_form(n, D, false) != 2) return UQ_OK;
+        // the one-wave form: its pass A (h from the message seeds) beside the RHT and the norm
+        SideStream* sb = nullptr;
+        int rc = side_stream(&sb);
+        if (rc) return rc;
+        if ((rc = hip_check(hipEventRecord(sb->fork, st), "record fork"))) return rc;
+        if ((rc = hip_check(hipStreamWaitEvent(sb->s, sb->fork, 0), "wait fork"))) return rc;
+        QflSendArgs qa{};
+        qa.prng_seeds = prng_seeds;
+        qa.hbuf = (uint8_t*)(wsb + quicfl_h_off(n, dim));
+        qa.h_len = h_len;
+        qa.D = D;
+        qa.n = n;
+        uint32_t* ls = (uint32_t*)(wsb + quicfl_jump_off(n, dim));
+        hipLaunchKernelGGL(quicfl_pass_a_kernel, dim3((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)),
+                           dim3(64 * kQfWavesPerWG), 0, sb->s, qa, ls);
+        rc = hip_check(hipGetLastError(), "quicfl_pass_a_kernel launch");
+        const int rj = hip_check(hipEventRecord(sb->join, sb->s), "record join");
+        if (!rj) {
+            jl->passa = true;                   // the guard and the wave launch wait on the join
+            jl->lstate = ls;
+            jl->sb = sb;
+        } else if (hipEventRecord(sb->join, sb->s) == hipSuccess) {
+            (void)hipStreamWaitEvent(st, sb->join, 0);
+        }
+        return rc ? rc : rj;
+    }
     const uint32_t* polys = nullptr;
     int rc = qfl_jump_polys(jp, false, &polys);
     if (rc) return rc;
@@ -4347,7 +4388,7 @@ struct QflJoinGuard {
     const QflJumpLaunch& jl;
     hipStream_t st;
     ~QflJoinGuard() {
-        if (jl.use) (void)hipStreamWaitEvent(st, jl.sb->join, 0);
+        if (jl.use || jl.passa) (void)hipStreamWaitEvent(st, jl.sb->join, 0);
     }
 };
 
@@ -4374,7 +4415,7 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     QflJumpLaunch jl;
-    int rc = quicfl_jump_fork(n, w.D, dim, prng_seeds, px_state, px_seeds, wsb, st, &jl);
+    int rc = quicfl_jump_fork(n, w.D, dim, prng_seeds, px_state, px_seeds, h_len, wsb, st, &jl);
     if (rc) return rc;
     const QflJoinGuard join_guard{jl, st};
     FwhtArgs a;
@@ -4448,6 +4489,11 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunc
         return hip_check(hipGetLastError(), "quicfl_send_team_kernel launch");
     }
     const dim3 grid((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG));
+    if (jl.passa) {                                  // KQ1a (pass A) ran on the side stream
+        const int rc = hip_check(hipStreamWaitEvent(st, jl.sb->join, 0), "wait join");
+        if (rc) return rc;
+        q.lstate = jl.lstate;
+    }
     if (x_kind == 0)
         hipLaunchKernelGGL(quicfl_send_wave_kernel<0>, grid, dim3(64 * kQfWavesPerWG), 0, st, q);
     else
@@ -4480,7 +4526,7 @@ int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     hipStream_t st = (hipStream_t)stream;
     char* wsb = (char*)ws;
     QflJumpLaunch jl;
-    int rc = quicfl_jump_fork(n, w.D, dim, prng_seeds, px_state, px_seeds, wsb, st, &jl);
+    int rc = quicfl_jump_fork(n, w.D, dim, prng_seeds, px_state, px_seeds, h_len, wsb, st, &jl);
     if (rc) return rc;
     const QflJoinGuard join_guard{jl, st};
     FwhtArgs a;

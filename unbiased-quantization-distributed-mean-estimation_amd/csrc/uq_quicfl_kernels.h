@@ -150,6 +150,9 @@ struct QflSendArgs {
     const float* rtab;          // receiver table (rtab_n <= 1024 floats)
     int32_t rtab_n;
     float* pre;                 // [n][D] (may alias rot: each coordinate is read before it is written)
+    // [n][624] the local stream's block after pass A, when KQ1a (quicfl_pass_a_kernel) ran pass A
+    // on the side stream beside the RHT and the norm; null: KQ1 runs pass A itself
+    const uint32_t* lstate;
 };
 
 // Round state carried from stage 1 (words, flags, gather issued) to stage 2 (X, stores).
@@ -465,7 +468,10 @@ quicfl_send_wave_kernel(QflSendArgs a) {
     wave_lds_fence();
     const QflCtx c = qfl_ctx<XK>(a, j, gleft, gnext);
     const int64_t nch = (a.D + kMtN - 1) / kMtN;
-    qfl_pass_a(c, sL, 0, nch, lane);
+    if (a.lstate)                                               // pass A done by KQ1a
+        mt_load(sL, a.lstate + j * kMtN, lane);
+    else
+        qfl_pass_a(c, sL, 0, nch, lane);
     int64_t haveL = nch, haveG = 0;
     mt_store(sL, WL + (haveL & 1) * kMtN, lane);
     mt_store(sG, WG, lane);
@@ -479,6 +485,31 @@ quicfl_send_wave_kernel(QflSendArgs a) {
         if (a.scale) a.scale[j] = c.sc;
         a.info[j] = flags;
     }
+}
+
+// KQ1a: pass A of the one-wave kernel alone (h = randint(0, h_len, (D,), local), AS:465/469):
+// it needs only the message seeds, so it runs on the side stream beside the sender's RHT and
+// norm, and KQ1 starts pass B from the local block it leaves in lstate.
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_pass_a_kernel(QflSendArgs a, uint32_t* __restrict__ lstate) {
+    __shared__ uint32_t WLsh[kQfWavesPerWG][kMtN];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    if (j >= a.n) return;
+    uint32_t* WL = WLsh[wv];
+    uint32_t sL[kMtGroups];
+    if (lane == 0) mt_seed(WL, (uint32_t)a.prng_seeds[j]);
+    wave_lds_fence();
+    mt_load(sL, WL, lane);
+    QflCtx c;                                                   // what pass A reads of the context
+    c.D = a.D;
+    c.row = j * a.D;
+    c.rh = make_rsrc(a.hbuf + c.row, (uint32_t)a.D);
+    c.h_len = (uint32_t)a.h_len;
+    c.hpow2 = (c.h_len & (c.h_len - 1)) == 0;
+    const int64_t nch = (a.D + kMtN - 1) / kMtN;
+    qfl_pass_a(c, sL, 0, nch, lane);
+    mt_store(sL, lstate + j * kMtN, lane);
 }
 
 // KQ1 for a few messages (the per-call drop-in): one 512-thread workgroup per message.  Wave
