@@ -2618,8 +2618,10 @@ int ilog2_pow2(int64_t D) {
 // while KE2s reads the vectors twice.
 constexpr int64_t kSegNormMaxN = 256;
 // ... and the dot's (KE4s): its one-wave-per-client form runs 6-19 VALU per step, so the
-// segmented form pays for its second read only with few clients
-constexpr int64_t kDotSegMaxN = 64;
+// segmented form pays for its second read only with few clients.  KE4's time is one client's
+// chain whatever n (2.67 ms at D = 2^22: 44 % of a 101-client EDEN call, profiles/r6z_*), KE4s
+// costs ~15 us per client of 2^22 (~4 per client of 2^20): they cross near 170 clients.
+constexpr int64_t kDotSegMaxN = 128;
 // biased quantizer: batches of at most this many clients run the candidate digits (KB4d) over
 // many workgroups per client (one workgroup per client walks up to d/8 keys twice)
 constexpr int64_t kCandMultiMaxN = 16;
