@@ -125,3 +125,28 @@ def test_bad_arguments():
     assert lib.uq_legacy_draw_f32(*args, 0, 0.0, 1.0, 1, 4, None, nrm.ctypes.data, 1) == -1
     with pytest.raises(KeyError):
         legacy_draw(np.random.RandomState(0), "no-such", 1, 4)
+
+
+def test_empty_draws_leave_the_state():
+    for n, d in ((0, 16), (3, 0), (0, 0)):
+        rs, ref = np.random.RandomState(11), np.random.RandomState(11)
+        rs.normal(size=3)
+        ref.normal(size=3)                        # a cached gauss in both
+        b, nrm = legacy_draw(rs, "normal", n, d, threads=4)
+        assert b.shape == (n, d) and b.dtype == np.float32 and nrm.shape == (n,) and not nrm.any()
+        assert _same_state(rs, ref)
+
+
+def test_out_buffer_checked():
+    rs = np.random.RandomState(0)
+    with pytest.raises(ValueError):
+        legacy_draw(rs, "normal", 2, 8, out=np.empty((2, 9), np.float32))
+    with pytest.raises(ValueError):
+        legacy_draw(rs, "normal", 2, 8, out=np.empty((2, 8), np.float64))
+    with pytest.raises(ValueError):
+        legacy_draw(rs, "normal", 2, 8, out=np.empty((8, 2), np.float32).T)
+    buf = np.empty((2, 8), np.float32)
+    got, _ = legacy_draw(np.random.RandomState(5), "laplace", 2, 8, out=buf)
+    assert got is buf
+    want, _ = _want(np.random.RandomState(5), "laplace", 2, 8)
+    assert np.array_equal(buf, want.astype(np.float32))
