@@ -2748,7 +2748,7 @@ EdenLayout eden_layout(int64_t n, int64_t dim) {
 // 256 x 64 high pass, the generic LDS kernel otherwise (same stages, same bits).
 template <int M, bool L, bool R>
 void fwht_dispatch(dim3 grid, const FwhtArgs& b, int lo, int k, hipStream_t st) {
-    if (lo == 0 && k == kFwhtLow16Bits && (M == 1 || M == 2) && !L)
+    if (lo == 0 && k == kFwhtLow16Bits && !L)
         hipLaunchKernelGGL((fwht_low16k_kernel<M>), dim3((unsigned)(b.D >> kFwhtLow16Bits), grid.y), dim3(1024), 0, st, b);
     else if (lo == 0 && k == kFwhtLowBits && (M != 2 || (b.D % 16) == 0))
         hipLaunchKernelGGL((fwht_low4096_kernel<M, L, R>), grid, dim3(256), 0, st, b);
@@ -4559,9 +4559,9 @@ int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.pre = rot;                       // in place: a coordinate's rot is loaded a round before its value is stored
     rc = launch_quicfl_send(q, 0, jl, st);                                                        // AS:455-503, 526-532
     if (rc) return rc;
-    // AS:533-535: the receiver's inverse RHT (H, then * diag), [:dim]
+    // AS:533-535: the receiver's inverse RHT (H, then * diag), [:dim]; D = 2^22 as 14 + 8 bits
     const int p = ilog2_pow2(w.D);
-    int lo = 0, k = std::min(p, kFwhtLowBits);
+    int lo = 0, k = p == kFwhtLow16Bits + kFwhtHighBits ? kFwhtLow16Bits : std::min(p, kFwhtLowBits);
     for (;;) {
         const bool last = lo + k >= p;
         const int cols = lo == 0 ? 1 : kFwhtCols;

@@ -353,7 +353,8 @@ fwht_low4096_kernel(FwhtArgs a) {
 // (b3: 2 bits).  Rounds as fwht_low4096_kernel (b0, b1, b2 in registers in turn, padded LDS
 // transposes), then bits 12-13: a thread takes four columns p = b0 + 16 b1 + 256 b2 and their
 // four b3 values.  The same stages in the same order, so the same bits as 12 + 8 + 2.
-// MODE 1: sender (pad, * diag), 2: receiver (centroids of the bins); never the last pass.
+// MODE 0: plain (QUIC-FL's receiver, in place), 1: sender (pad, * diag), 2: receiver (centroids
+// of the bins); never the last pass.
 template <int MODE>
 __global__ void __launch_bounds__(1024)
 fwht_low16k_kernel(FwhtArgs a) {
@@ -366,7 +367,14 @@ fwht_low16k_kernel(FwhtArgs a) {
     float v[16];
     {   // round-1 layout: 16 contiguous elements
         const int64_t i0 = base + (int64_t)tid * 16;
-        if (MODE == 1) {
+        if (MODE == 0) {
+            const float* p = (const float*)a.in + vec * D + i0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
+                v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+            }
+        } else if (MODE == 1) {
             const int8_t* sg = a.signs + (int64_t)(a.sign_row ? a.sign_row[vec] : 0) * D;
             const float* x = (const float*)a.in + vec * a.dim;
             const bool full = i0 + 16 <= a.dim && (((uintptr_t)(x + i0)) & 15) == 0;
