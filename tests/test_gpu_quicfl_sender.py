@@ -325,12 +325,13 @@ def test_packed_table_same_bits(fx, monkeypatch):
 
 
 @pytest.mark.parametrize("n,dim", [(1, 4096), (1, 5000), (3, 9000), (17, 1 << 15), (128, 1 << 14), (2, (1 << 21) + 7),
-                                   (1, 3 << 18), (5, 1 << 20)])
+                                   (1, 3 << 18), (5, 1 << 20), (300, 1 << 16), (342, 1 << 18)])
 def test_jump_path_equals_one_wave_across_shapes(fx, n, dim):
     """The jump path (its run count and length come from a cost model of (n, D), so every shape
     cuts the streams differently) against the one-wave kernel (test hook 2) on the same
     messages: X, mask, exact values, scales, generator end states; px states off the block
-    edge and fresh px seeds."""
+    edge and fresh px seeds.  (300, 2^16): 3 runs per message past the team kernel's 256;
+    (342, 2^18): 5 runs, 1710 run waves, the two-waves-per-SIMD runs kernel."""
     import uqdme_amd.quicfl as q
     from uqdme_amd._lib import load
     meta, z, rmeta, rz = fx

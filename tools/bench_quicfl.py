@@ -28,6 +28,19 @@ def recv_table(bits):
     return np.load(os.path.join(ROOT, "tests", "golden", "quicfl_recv_vectors.npz"))[f"recv{bits}"]
 
 
+def digest(msg, out):
+    import hashlib
+    h = hashlib.sha256()
+    for t in (msg.X, msg.exact_mask, msg.exact_dense(), msg.scale, out):
+        t = t.contiguous()
+        t = t.view(torch.int32) if t.dtype == torch.float32 else t
+        w = torch.arange(t.shape[-1], device=t.device, dtype=torch.int64) % 65521 + 1
+        rows = (t.to(torch.int64) * w).sum(dim=-1) if t.dim() > 1 else t.to(torch.int64)
+        h.update(rows.cpu().numpy().tobytes())
+    h.update(np.asarray(msg.exact_count).tobytes())
+    return h.hexdigest()[:16]
+
+
 def timed(f, steps):
     f()
     torch.cuda.synchronize()
@@ -47,6 +60,7 @@ def main():
     ap.add_argument("--bits", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--per-call", type=int, default=5, help="single-message compress calls to time (0: skip)")
+    ap.add_argument("--digest", action="store_true", help="add a digest of the messages and the decompressed batch")
     a = ap.parse_args()
     import uqdme
     snd = make_sender(uqdme, a.bits)
@@ -67,6 +81,8 @@ def main():
     res = {"tool": "bench_quicfl", "clients": a.clients, "d": a.dim, "bits": a.bits, "compress_ms": round(ms_c, 4),
            "decompress_ms": round(ms_d, 4), "exact_per_client": float(msg.exact_count.float().mean()),
            "M_vectors_per_s_compress": round(a.clients / ms_c / 1e3, 6)}
+    if a.digest:                           # to compare library variants' outputs (tools/exp/variants.py)
+        res["digest"] = digest(msg, uqdme.quicfl_decompress_messages(msg, rt))
     if a.per_call:
         v = x[0].clone()
         data = {"vec": v, "seed": 7, "nbits": a.bits, "rotation_seed": 123}

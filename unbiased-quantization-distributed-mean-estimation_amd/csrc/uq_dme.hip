@@ -28,6 +28,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/uq_dme.h"
@@ -3853,26 +3854,35 @@ struct QflJumpPlan {
     int64_t L = 0, qL = 0;
 };
 
-// (Up to 128 messages: at 256 x 2^20 only R = 4 runs fit beside each other and the team kernel
-// measured 5.4 against 6.0 ms; 128 x 2^20: 3.4 against 4.5 ms, profiles/r5h_quicfl_batch_sizes.jsonl.)
-constexpr int64_t kQfJumpMaxN = 128;
+// Up to 1024 run waves a wave per SIMD; up to 2048 two (quicfl_send_runs_kernel<., true>), a
+// round then costing ~1.8 tR (round 6, profiles/r6k_*: 512 x 2^20 compress 12.0 -> 8.9 ms,
+// 256 x 2^22 round trip 24.2 -> 18.4, 101 x 2^22 8.9 -> 8.2; 1024 x 2^20 keeps KQ1, whose pass A
+// runs beside the RHT).
+constexpr int64_t kQfJumpMaxN = 1024;
+constexpr int64_t kQfRunWaves1 = 1024, kQfRunWaves2 = 2048;
 static QflJumpPlan qfl_jump_plan(int64_t n, int64_t D) {
     QflJumpPlan p;
     const int64_t nch = (D + kMtN - 1) / kMtN;
     if (n < 1 || n > kQfJumpMaxN || nch < 8 || D > ((int64_t)1 << 28)) return p;
-    const double tS = 20.0, tJ = 0.12, tR = 7.5;
+    const double tS = 20.0, tJ = 0.12, tR = 7.5, f2 = 1.8;
     double best = 1e300;
     for (int64_t R = 1; R <= 1024 && R <= nch; ++R) {
         const int64_t L = (nch + R - 1) / R, Ru = (nch + L - 1) / L;
-        if (Ru != R || n * R > 1024) continue;
-        const double t = tS + (double)(n * (3 * R - 2)) * tJ + (double)L * tR;
+        if (Ru != R || n * R > kQfRunWaves2) continue;
+        const double t = tS + (double)(n * (3 * R - 2)) * tJ + (double)L * tR * (n * R > kQfRunWaves1 ? f2 : 1.0);
         if (t < best) {
             best = t;
             p.R = (int32_t)R;
             p.L = L;
         }
     }
-    p.use = best < 0.8 * (double)((n + 1023) / 1024) * (double)nch * tR;
+    // against: up to 128 messages the team kernel as round 5 measured it; 129-256 the team kernel
+    // at ~2.85 us per round, the model ~1.4x optimistic (r6l: 256 x 2^20 team 5.5 / jump 5.9 ms,
+    // 2^21 11.3 / 10.3, 2^22 round trip 24.3 / 18.7); above, a wave per message
+    if (n <= 128 || n > kQfTeamMaxN)
+        p.use = best < 0.8 * (double)((n + 1023) / 1024) * (double)nch * tR;
+    else
+        p.use = best < 2.0 * (double)nch;
     p.qL = ((int64_t)kMtN + D) / kMtN;               // block of the first pass-B local word (qfl_ctx)
     return p;
 }
@@ -3883,7 +3893,7 @@ static QflJumpPlan qfl_jump_plan(int64_t n, int64_t D) {
 static QflJumpPlan qfl_recv_jump_plan(int64_t n, int64_t D) {
     QflJumpPlan p;
     const int64_t nch = (D + kMtN - 1) / kMtN;
-    if (n < 1 || n > kQfTeamMaxN || nch < 8 || D > ((int64_t)1 << 28)) return p;
+    if (n < 1 || n > kQfJumpMaxN || nch < 8 || D > ((int64_t)1 << 28)) return p;
     const double tS = 20.0, tJ = 0.12, tR = 3.0;
     double best = 1e300;
     for (int64_t R = 1; R <= 1024 && R <= nch; ++R) {
@@ -3896,7 +3906,9 @@ static QflJumpPlan qfl_recv_jump_plan(int64_t n, int64_t D) {
             p.L = L;
         }
     }
-    p.use = best < 0.8 * (double)nch;
+    // against the team kernel (~1 us per round) up to 256 messages, a wave per message (~tR per
+    // round, one wave per SIMD) above
+    p.use = best < 0.8 * (double)nch * (n <= kQfTeamMaxN ? 1.0 : tR);
     return p;
 }
 
@@ -4451,9 +4463,10 @@ int uq_quicfl_compress_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     return launch_quicfl_send(q, x_kind, jl, st);
 }
 
-// By batch size: up to 128 messages the jump path (KQ0s + KQ0j + KQ1j + KQ1f: every run of
-// every message at once from jumped stream blocks), up to 256 the team kernel KQ1t (scouts + runs
-// in one workgroup per message), batches a wave per message (KQ1).  Test hooks: bit 1 the
+// By batch size and the plan's cost model: the jump path (KQ0s + KQ0j + KQ1j + KQ1f: every run
+// of every message at once from jumped stream blocks) when it beats a wave per message, else up
+// to 256 the team kernel KQ1t (scouts + runs in one workgroup per message), batches a wave per
+// message (KQ1).  Test hooks: bit 1 the
 // one-wave kernel, bit 2 (or bit 0, whose timeouts only the team's runs can report) KQ1t.
 static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunch& jl, hipStream_t st) {
     const int hooks = g_quicfl_hooks.load();
@@ -4474,8 +4487,11 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunc
             rc = hip_check(hipGetLastError(), "quicfl_send_count_kernel launch");
             if (rc) return rc;
         }
-        if (x_kind == 0) hipLaunchKernelGGL(quicfl_send_runs_kernel<0>, rgrid, blk, 0, st, q, ra);
-        else hipLaunchKernelGGL(quicfl_send_runs_kernel<1>, rgrid, blk, 0, st, q, ra);
+        const bool w2 = n * jl.jp.R > kQfRunWaves1;
+        if (x_kind == 0 && w2) hipLaunchKernelGGL((quicfl_send_runs_kernel<0, true>), rgrid, blk, 0, st, q, ra);
+        else if (x_kind == 0) hipLaunchKernelGGL((quicfl_send_runs_kernel<0, false>), rgrid, blk, 0, st, q, ra);
+        else if (w2) hipLaunchKernelGGL((quicfl_send_runs_kernel<1, true>), rgrid, blk, 0, st, q, ra);
+        else hipLaunchKernelGGL((quicfl_send_runs_kernel<1, false>), rgrid, blk, 0, st, q, ra);
         rc = hip_check(hipGetLastError(), "quicfl_send_runs_kernel launch");
         if (rc) return rc;
         hipLaunchKernelGGL(quicfl_send_fin_kernel, dim3((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk, 0, st,

@@ -1072,13 +1072,14 @@ eden_segwalk_kernel(const float* __restrict__ v, int64_t D, const float* __restr
 // (0 + 1) + (2 + 3).  One wave per client: lane l runs chain l over the client's rotated
 // vector (64 consecutive floats per step: one coalesced 256-byte load per wave), writes each
 // coordinate's bin (u8) and folds c[bin] * v into its chain; two register sets of kDotU steps of
-// loads in flight.  The bin needs no division per element: y = v * f32(sqrt D) (AS:329) falls
+// loads in flight (32: with few clients one wave's loads in flight bound the kernel, round 6:
+// 256 x 2^22 EDEN 10.98 -> 10.48 ms, profiles/r6k_ab_c4_eden_ke4u32.jsonl).  The bin needs no division per element: y = v * f32(sqrt D) (AS:329) falls
 // in bin sum_j [!(y <= T_j)] where T_j is the largest f32 y with RN(y / norm) <= boundary j --
 // y -> RN(y / norm) is non-decreasing for a positive finite norm, so this is exactly
 // torch.bucketize of the quotient (NaN included); T_j is found once per client by bisection
 // over the floats' order.  Other norms (0, inf, NaN) take the per-element division.
 constexpr int kDotWaves = 4;
-constexpr int kDotU = 16;
+constexpr int kDotU = 32;
 
 __device__ __forceinline__ uint32_t ford_key(float y) {          // order-preserving u32 image
     const uint32_t u = __float_as_uint(y);
@@ -1121,25 +1122,33 @@ __device__ __forceinline__ float dotbins_chains(const float* __restrict__ vj, in
         acc = fmaf(eden_cent(cs, b), x, acc);                               // AS:335
     };
     const int64_t steps = D / 64;
-    if (steps >= 2 * kDotU && steps % (2 * kDotU) == 0) {
-        float A[kDotU], B[kDotU];
-        auto load = [&](float (&R)[kDotU], int64_t s0) {
+    auto pipelined = [&](auto u) {                                         // u steps per register set
+        constexpr int U = decltype(u)::value;
+        float A[U], B[U];
+        auto load = [&](float (&R)[U], int64_t s0) {
 #pragma unroll
-            for (int k = 0; k < kDotU; ++k)
+            for (int k = 0; k < U; ++k)
                 R[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                     rv, (uint32_t)((s0 + k) * 64 + lane) * 4u, 0, kAuxNT));     // beyond D: 0, unused
         };
-        auto run = [&](const float (&R)[kDotU], int64_t s0) {
+        auto run = [&](const float (&R)[U], int64_t s0) {
 #pragma unroll
-            for (int k = 0; k < kDotU; ++k) step(R[k], (s0 + k) * 64 + lane);
+            for (int k = 0; k < U; ++k) step(R[k], (s0 + k) * 64 + lane);
         };
         load(A, 0);
-        for (int64_t s0 = 0; s0 < steps; s0 += 2 * kDotU) {
-            load(B, s0 + kDotU);
+        for (int64_t s0 = 0; s0 < steps; s0 += 2 * U) {
+            load(B, s0 + U);
             run(A, s0);
-            load(A, s0 + 2 * kDotU);
-            run(B, s0 + kDotU);
+            load(A, s0 + 2 * U);
+            run(B, s0 + U);
         }
+    };
+    if (steps >= 2 * kDotU && steps % (2 * kDotU) == 0) {
+        pipelined(std::integral_constant<int, kDotU>{});
+        return acc;
+    }
+    if (steps >= kDotU && steps % kDotU == 0) {                            // e.g. D = 2048
+        pipelined(std::integral_constant<int, kDotU / 2>{});
         return acc;
     }
     int64_t i0 = 0;

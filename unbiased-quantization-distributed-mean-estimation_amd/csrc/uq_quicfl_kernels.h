@@ -909,8 +909,10 @@ quicfl_send_count_kernel(QflSendArgs a, QflRunArgs ra) {
     if (lane == 0) ra.runinfo[(j * ra.R + r) * 2] = cnt;
 }
 
-template <int XK>
-__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+// W2: two waves per SIMD (the registers capped at 256, a few spilled), for plans of more than
+// 1024 run waves; otherwise one (no spills)
+template <int XK, bool W2>
+__global__ void __launch_bounds__(64 * kQfWavesPerWG, W2 ? 2 : 1)
 quicfl_send_runs_kernel(QflSendArgs a, QflRunArgs ra) {
     __shared__ uint32_t WLsh[kQfWavesPerWG][2 * kMtN];
     __shared__ uint32_t WGsh[kQfWavesPerWG][2 * kMtN];
