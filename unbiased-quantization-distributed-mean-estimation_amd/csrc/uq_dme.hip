@@ -3228,7 +3228,11 @@ int unbiased_codes_impl(const float* x, float* out, int64_t ldo, int8_t* codes, 
             int slots = 0;
             rc = stream_slots(&slots);
             if (rc) return rc;
-            R = (int32_t)std::max<int64_t>(1, (total_tiles + slots - 1) / slots);
+            // at most `slots` workgroups in all, so that they run as one wave: ceil(total / slots)
+            // tiles each made nj * ceil(tiles / R) > slots workgroups for most nj (101 x 2^22:
+            // 1111 of 1024 slots, the last 87 workgroups a second round of R tiles)
+            const int64_t segs = std::max<int64_t>(1, slots / nj);
+            R = (int32_t)((w.tiles + segs - 1) / segs);
             nseg = (w.tiles + R - 1) / R;
             hipLaunchKernelGGL(agg_stream_kernel, dim3((unsigned)(nj * nseg)), dim3(kQBlock), 0, st, xj, d, w.tiles, fm,
                                l1j, R, nseg, agg, reccnt);
