@@ -141,13 +141,14 @@ def test_receiver_team_equals_wave(fx):
     assert few[3].cpu().numpy().view(np.uint32).tolist() == exp.view(np.uint32).tolist()
 
 
-@pytest.mark.parametrize("n,D", [(3, 1 << 16), (3, 1 << 20), (300, 1 << 16)])
+@pytest.mark.parametrize("n,D", [(3, 1 << 16), (3, 1 << 20), (300, 1 << 16), (342, 1 << 18)])
 def test_receiver_jump_equals_team_and_wave(fx, n, D):
     """A few messages of 2^16 / 2^20 coordinates take the receiver's jump path (KQ0s + KQ0j on
     the h stream, every run at once, compact slots from KQ2c's counts): the same bits as the
     team kernel (test hook 4) and the one-wave kernel (hook 2), both exact layouts, and the
     oracle on one message.  300 messages: the jump path past the team kernel's 256 (hook 4
-    falls back to the one-wave kernel there)."""
+    falls back to the one-wave kernel there); 342 x 2^18: 5 runs per message, 1710 run waves,
+    two per SIMD."""
     import uqdme
     from uqdme_amd._lib import load
     meta, z = fx

@@ -3892,8 +3892,9 @@ static QflJumpPlan qfl_jump_plan(int64_t n, int64_t D) {
 }
 
 // The receiver's jump path: one stream, one jump per run; a round (one wave: the h word, the
-// table gather, X, the mask and the exact value) ~tR.  Taken when it beats the team kernel
-// (~1 us per round of the h scout's twists and the runs behind it).
+// table gather, X, the mask and the exact value) ~tR, ~1.8 tR at two waves per SIMD (more than
+// 1024 run waves; 512 x 2^20 decompress 5.60 -> 4.23 ms, profiles/r6r_*).  Taken when it beats
+// the team kernel (~1 us per round of the h scout's twists and the runs behind it).
 static QflJumpPlan qfl_recv_jump_plan(int64_t n, int64_t D) {
     QflJumpPlan p;
     const int64_t nch = (D + kMtN - 1) / kMtN;
@@ -3902,8 +3903,8 @@ static QflJumpPlan qfl_recv_jump_plan(int64_t n, int64_t D) {
     double best = 1e300;
     for (int64_t R = 1; R <= 1024 && R <= nch; ++R) {
         const int64_t L = (nch + R - 1) / R, Ru = (nch + L - 1) / L;
-        if (Ru != R || n * R > 1024) continue;
-        const double t = tS + (double)(n * (R - 1)) * tJ + (double)L * tR;
+        if (Ru != R || n * R > kQfRunWaves2) continue;                 // (its kernels fit 2 waves per SIMD)
+        const double t = tS + (double)(n * (R - 1)) * tJ + (double)L * tR * (n * R > kQfRunWaves1 ? 1.8 : 1.0);
         if (t < best) {
             best = t;
             p.R = (int32_t)R;
