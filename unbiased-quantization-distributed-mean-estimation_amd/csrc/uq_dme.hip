@@ -4312,6 +4312,7 @@ int uq_quicfl_workspace_bytes(int64_t n, int64_t dim, size_t* bytes_out) {
 struct QflJumpLaunch {
     bool use = false;
     bool passa = false;             // KQ1a runs on the side stream instead (the one-wave form)
+    bool passa_runs = false;        // KQ1ar ran every run's pass A on the side stream (the jump path)
     QflJumpPlan jp;
     uint32_t* parts = nullptr;
     uint32_t* lstate = nullptr;     // KQ1a's local blocks
@@ -4390,8 +4391,24 @@ static int quicfl_jump_fork(int64_t n, int64_t D, int64_t dim, const int32_t* pr
     if ((rc = hip_check(hipGetLastError(), "quicfl_stream_kernel launch"))) return join_on_error(rc);
     hipLaunchKernelGGL(quicfl_jump_kernel, dim3((unsigned)(n * jp.R * 3 * kMjParts)), dim3(256), 0, sb->s, ja);
     if ((rc = hip_check(hipGetLastError(), "quicfl_jump_kernel launch"))) return join_on_error(rc);
+    {   // KQ1ar: the runs' pass A (h) beside the RHT and the norm
+        QflSendArgs qa{};
+        qa.prng_seeds = prng_seeds;
+        qa.hbuf = (uint8_t*)(wsb + quicfl_h_off(n, dim));
+        qa.h_len = h_len;
+        qa.D = D;
+        qa.n = n;
+        QflRunArgs ra{};
+        ra.parts = parts;
+        ra.R = jp.R;
+        ra.L = jp.L;
+        hipLaunchKernelGGL(quicfl_pass_a_runs_kernel, dim3((unsigned)((n * jp.R + kQfWavesPerWG - 1) / kQfWavesPerWG)),
+                           dim3(64 * kQfWavesPerWG), 0, sb->s, qa, ra);
+        if ((rc = hip_check(hipGetLastError(), "quicfl_pass_a_runs_kernel launch"))) return join_on_error(rc);
+    }
     if ((rc = hip_check(hipEventRecord(sb->join, sb->s), "record join"))) return join_on_error(rc);
     jl->use = true;
+    jl->passa_runs = true;
     jl->jp = jp;
     jl->parts = parts;
     jl->sb = sb;
@@ -4486,6 +4503,7 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunc
         ra.runinfo = (int32_t*)(jl.parts + (size_t)n * jl.jp.R * 3 * kMjParts * kMtN);
         ra.R = jl.jp.R;
         ra.L = jl.jp.L;
+        ra.passa_done = jl.passa_runs ? 1 : 0;
         const dim3 rgrid((unsigned)((n * jl.jp.R + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk(64 * kQfWavesPerWG);
         if (!q.pre) {
             hipLaunchKernelGGL(quicfl_send_count_kernel, rgrid, blk, 0, st, q, ra);

@@ -252,7 +252,7 @@ __device__ __forceinline__ void qfl_window_to(uint32_t (&s)[kMtGroups], uint32_t
 // Every per-element global access goes through a buffer descriptor (out-of-range loads return
 // 0, stores are dropped): no per-element branch, and a lane's ten loads of a round are in flight
 // together.
-template <int XK>
+template <int XK, bool LEAN = false>
 __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict__ ev, uint32_t (&sL)[kMtGroups],
                                               uint32_t* WL, int64_t& haveL, uint32_t (&sG)[kMtGroups], uint32_t* WG,
                                               int64_t& haveG, int64_t c0, int64_t c1, int64_t ev_base, int32_t& flags,
@@ -330,12 +330,10 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
         }
     };
 
-    // one round: loads for round rd + 1 into `nxt`, stage 1 of round rd from `cur` into `cr`
-    // (its gathers issued), then stage 2 of round rd - 1 (`pr`) while those gathers fly
-    auto round = [&](int64_t rd, const In& cur, In& nxt, QflRound& cr, const QflRound& pr, bool fin) {
+    // stage 1 of round rd from `cur` into `cr` (its gathers issued)
+    auto stage1 = [&](int64_t rd, const In& cur, QflRound& cr) {
         const uint32_t i0 = (uint32_t)(rd * kMtN);
         const int lastE = (int)((D - 1 - (int64_t)i0) < (kMtN - 1) ? (D - 1 - (int64_t)i0) : (kMtN - 1));
-        load_in(i0 + (uint32_t)kMtN, nxt);                           // (beyond D: the descriptor returns 0)
         // the words of this round: slots rX .. rX + lastE of block qX + rd and, past 623, of
         // block qX + rd + 1 (twisted only when the round reaches it, so the global stream ends
         // on the block holding its last word)
@@ -395,6 +393,23 @@ __device__ __forceinline__ int64_t qfl_pass_b(const QflCtx& c, float* __restrict
             cr.act |= (active ? 1u : 0u) << k;
             cr.hp[k >> 2] |= (cur.h[k] & 0xFFu) << (8 * (k & 3));
         }
+    };
+    if (LEAN) {
+        // one register set each (two waves per SIMD hide the latencies instead): stage 1 of
+        // round rd, the loads of round rd + 1, then stage 2 of round rd
+        for (int64_t rd = c0; rd < c1; ++rd) {
+            stage1(rd, I0, R0);
+            load_in((uint32_t)((rd + 1) * kMtN), I0);                // (beyond D: the descriptor returns 0)
+            finish(R0, (uint32_t)(rd * kMtN));
+        }
+        return etot;
+    }
+    // one round: loads for round rd + 1 into `nxt`, stage 1 of round rd from `cur` into `cr`
+    // (its gathers issued), then stage 2 of round rd - 1 (`pr`) while those gathers fly
+    auto round = [&](int64_t rd, const In& cur, In& nxt, QflRound& cr, const QflRound& pr, bool fin) {
+        const uint32_t i0 = (uint32_t)(rd * kMtN);
+        load_in(i0 + (uint32_t)kMtN, nxt);                           // (beyond D: the descriptor returns 0)
+        stage1(rd, cur, cr);
         if (fin) finish(pr, i0 - (uint32_t)kMtN);
     };
     for (int64_t rd = c0; rd < c1; rd += 2) {
@@ -884,7 +899,40 @@ struct QflRunArgs {
     int32_t* runinfo;           // [n][R][2]: exact values of the run (KQ1c), its UQ_QFL_* flags (KQ1j)
     int32_t R;
     int64_t L;                  // rounds per run (the last run may have fewer)
+    int32_t passa_done;         // KQ1ar wrote every run's h already (the side stream): KQ1j skips pass A
 };
+
+// KQ1ar: pass A of every run (h for its rounds, AS:465/469) from its jumped local block c0 (run
+// 0: the seed), one wave per (message, run): issued on the side stream right behind KQ0j, so it
+// runs beside the sender's RHT and norm and KQ1j is left with pass B.
+__global__ void __launch_bounds__(64 * kQfWavesPerWG)
+quicfl_pass_a_runs_kernel(QflSendArgs a, QflRunArgs ra) {
+    __shared__ uint32_t WLsh[kQfWavesPerWG][kMtN];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t id = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
+    const int64_t j = id / ra.R;
+    const int r = (int)(id % ra.R);
+    if (j >= a.n) return;
+    const int64_t nch = (a.D + kMtN - 1) / kMtN;
+    const int64_t c0 = (int64_t)r * ra.L, c1 = min(nch, c0 + ra.L);
+    if (c0 >= c1) return;
+    uint32_t sL[kMtGroups];
+    if (r == 0) {
+        uint32_t* WL = WLsh[wv];
+        if (lane == 0) mt_seed(WL, (uint32_t)a.prng_seeds[j]);
+        wave_lds_fence();
+        mt_load(sL, WL, lane);
+    } else {
+        mj_block(sL, ra.parts + (j * ra.R + r) * 3 * kMjParts * kMtN, lane);   // local block c0
+    }
+    QflCtx c;                                                   // what pass A reads of the context
+    c.D = a.D;
+    c.row = j * a.D;
+    c.rh = make_rsrc(a.hbuf + c.row, (uint32_t)a.D);
+    c.h_len = (uint32_t)a.h_len;
+    c.hpow2 = (c.h_len & (c.h_len - 1)) == 0;
+    qfl_pass_a(c, sL, c0, c1, lane);
+}
 
 // KQ1c (compress only): the exact coordinates of each run (AS:472-478: v = rot * scale, |v| > T
 // in f32, as pass B decides them), so that every run writes its exact values straight to their
@@ -940,15 +988,17 @@ quicfl_send_runs_kernel(QflSendArgs a, QflRunArgs ra) {
     int32_t gnext = a.px_state ? (int32_t)a.px_state[j * kQfStateWords + 1] : 0;
     const QflCtx c = qfl_ctx<XK>(a, j, gleft, gnext);
     uint32_t sL[kMtGroups], sG[kMtGroups];
-    if (r == 0) {                                        // local block 0: the seed itself
-        if (lane == 0) mt_seed(WL, (uint32_t)a.prng_seeds[j]);
-        wave_lds_fence();
-        mt_load(sL, WL, lane);
-        wave_lds_fence();
-    } else {
-        mj_block(sL, st, lane);                          // local block c0
+    if (!ra.passa_done) {
+        if (r == 0) {                                    // local block 0: the seed itself
+            if (lane == 0) mt_seed(WL, (uint32_t)a.prng_seeds[j]);
+            wave_lds_fence();
+            mt_load(sL, WL, lane);
+            wave_lds_fence();
+        } else {
+            mj_block(sL, st, lane);                      // local block c0
+        }
+        qfl_pass_a(c, sL, c0, c1, lane);                 // AS:465 h for the run's rounds
     }
-    qfl_pass_a(c, sL, c0, c1, lane);                     // AS:465 h for the run's rounds
     int64_t haveL = c.qL + c0, haveG = c0;
     mj_block(sL, st + kMjParts * kMtN, lane);            // local block qL + c0
     if (r == 0) {
@@ -965,7 +1015,7 @@ quicfl_send_runs_kernel(QflSendArgs a, QflRunArgs ra) {
         for (int o = 32; o >= 1; o >>= 1) ebase += __shfl_xor(ebase, o);
     }
     int32_t flags = 0;
-    qfl_pass_b<XK>(c, a.ev, sL, WL, haveL, sG, WG, haveG, c0, c1, ebase, flags, rtab, lane);
+    qfl_pass_b<XK, W2>(c, a.ev, sL, WL, haveL, sG, WG, haveG, c0, c1, ebase, flags, rtab, lane);
     for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
     if (c1 == nch && a.px_state_out)
         qfl_state_out(a.px_state_out + j * kQfStateWords, sG, a.D, gleft, gnext, c.qG * kMtN + c.rG, lane);
