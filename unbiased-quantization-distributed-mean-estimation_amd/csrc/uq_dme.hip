@@ -4505,11 +4505,6 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunc
         ra.L = jl.jp.L;
         ra.passa_done = jl.passa_runs ? 1 : 0;
         const dim3 rgrid((unsigned)((n * jl.jp.R + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk(64 * kQfWavesPerWG);
-        if (!q.pre) {
-            hipLaunchKernelGGL(quicfl_send_count_kernel, rgrid, blk, 0, st, q, ra);
-            rc = hip_check(hipGetLastError(), "quicfl_send_count_kernel launch");
-            if (rc) return rc;
-        }
         const bool w2 = n * jl.jp.R > kQfRunWaves1;
         if (x_kind == 0 && w2) hipLaunchKernelGGL((quicfl_send_runs_kernel<0, true>), rgrid, blk, 0, st, q, ra);
         else if (x_kind == 0) hipLaunchKernelGGL((quicfl_send_runs_kernel<0, false>), rgrid, blk, 0, st, q, ra);

@@ -702,12 +702,11 @@ quicfl_send_team_kernel(QflSendArgs a) {
 //        staged in LDS (22 KB: several workgroups per CU); a wave XORs 4-word quads of x per set
 //        coefficient (one ds_read_b128 per quad, a scalar branch per coefficient nibble); the
 //        partial windows go to HBM, and the run XORs the four and twists once.
-//   KQ1c quicfl_send_count_kernel   (compress only) one wave per (message, run): its exact
-//        coordinates, so that the runs write their exact values straight into index order.
 //   KQ1j quicfl_send_runs_kernel   one wave per (message, run), four per workgroup: pass A over
 //        its rounds from the local block c0 (run 0: the seed), pass B from local block qL + c0
 //        and global block c0 (run 0: the generator's own state); flags per run.
-//   KQ1f quicfl_send_fin_kernel   one wave per message: flags ORed, ecount, scale.
+//   KQ1f quicfl_send_fin_kernel   one wave per message: flags ORed, the runs' exact values moved
+//        into index order, ecount, scale.
 constexpr int kMjBlocks = 33;                 // x[0 .. 33 * 624) covers k + w <= 19936 + 623 (+ quad tails)
 constexpr int kMjX = kMjBlocks * kMtN;        // stream words kept per (message, stream)
 constexpr int kMjParts = 4;                   // workgroups per jump, 156 coefficient words each
@@ -896,7 +895,7 @@ __device__ __forceinline__ void mj_block(uint32_t (&st)[kMtGroups], const uint32
 
 struct QflRunArgs {
     const uint32_t* parts;      // KQ0j's partial windows [n][R][3][kMjParts][624]
-    int32_t* runinfo;           // [n][R][2]: exact values of the run (KQ1c), its UQ_QFL_* flags (KQ1j)
+    int32_t* runinfo;           // [n][R][2]: exact values of the run (KQ1j / KQ2c), its UQ_QFL_* flags
     int32_t R;
     int64_t L;                  // rounds per run (the last run may have fewer)
     int32_t passa_done;         // KQ1ar wrote every run's h already (the side stream): KQ1j skips pass A
@@ -934,29 +933,6 @@ quicfl_pass_a_runs_kernel(QflSendArgs a, QflRunArgs ra) {
     qfl_pass_a(c, sL, c0, c1, lane);
 }
 
-// KQ1c (compress only): the exact coordinates of each run (AS:472-478: v = rot * scale, |v| > T
-// in f32, as pass B decides them), so that every run writes its exact values straight to their
-// index-order slots (after the earlier runs' counts).  One wave per (message, run).
-__global__ void __launch_bounds__(64 * kQfWavesPerWG)
-quicfl_send_count_kernel(QflSendArgs a, QflRunArgs ra) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t id = (int64_t)blockIdx.x * kQfWavesPerWG + wv;
-    const int64_t j = id / ra.R;
-    const int r = (int)(id % ra.R);
-    if (j >= a.n) return;
-    const float sc = (1.0f / a.nrm[j]) * a.sqrtD;            // AS:466/470, as qfl_ctx
-    const float thr = kQflExactT;
-    const int64_t e0 = (int64_t)r * ra.L * kMtN, e1 = min(a.D, e0 + ra.L * kMtN);
-    const float* rot = a.rot + j * a.D;
-    int32_t cnt = 0;
-    for (int64_t i = e0 + lane; i < e1; i += 64) {
-        const float v = rot[i] * sc;
-        cnt += (v > thr) || (v < -thr) ? 1 : 0;
-    }
-    for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
-    if (lane == 0) ra.runinfo[(j * ra.R + r) * 2] = cnt;
-}
-
 // W2: two waves per SIMD (the registers capped at 256, a few spilled), for plans of more than
 // 1024 run waves; otherwise one (no spills)
 template <int XK, bool W2>
@@ -978,7 +954,7 @@ quicfl_send_runs_kernel(QflSendArgs a, QflRunArgs ra) {
     const int64_t c0 = (int64_t)r * ra.L, c1 = min(nch, c0 + ra.L);
     int32_t* info = ra.runinfo + (j * ra.R + r) * 2;
     if (c0 >= c1) {
-        if (lane == 0) info[1] = 0;
+        if (lane == 0) info[0] = info[1] = 0;
         return;
     }
     uint32_t* WL = WLsh[wv];
@@ -1009,13 +985,13 @@ quicfl_send_runs_kernel(QflSendArgs a, QflRunArgs ra) {
     }
     mt_store(sL, WL + (haveL & 1) * kMtN, lane);
     mt_store(sG, WG + (haveG & 1) * kMtN, lane);
-    int64_t ebase = 0;                                   // the exact values of the earlier runs (KQ1c)
-    if (!c.fused) {
-        for (int q = lane; q < r; q += 64) ebase += ra.runinfo[(j * ra.R + q) * 2];
-        for (int o = 32; o >= 1; o >>= 1) ebase += __shfl_xor(ebase, o);
-    }
+    // exact values into the run's own span of ev (from coordinate c0 * 624); KQ1f moves them
+    // into index order behind the earlier runs' (~0.4 % of the coordinates: no counting pass
+    // over rot before the runs)
+    const int64_t ebase = c0 * kMtN;
     int32_t flags = 0;
-    qfl_pass_b<XK, W2>(c, a.ev, sL, WL, haveL, sG, WG, haveG, c0, c1, ebase, flags, rtab, lane);
+    const int64_t ecnt = qfl_pass_b<XK, W2>(c, a.ev, sL, WL, haveL, sG, WG, haveG, c0, c1, ebase, flags, rtab, lane);
+    if (lane == 0 && !c.fused) info[0] = (int32_t)ecnt;
     for (int o = 32; o >= 1; o >>= 1) flags |= __shfl_xor(flags, o);
     if (c1 == nch && a.px_state_out)
         qfl_state_out(a.px_state_out + j * kQfStateWords, sG, a.D, gleft, gnext, c.qG * kMtN + c.rG, lane);
@@ -1037,6 +1013,20 @@ quicfl_send_fin_kernel(QflSendArgs a, QflRunArgs ra) {
     for (int o = 32; o >= 1; o >>= 1) {
         flags |= __shfl_xor(flags, o);
         tot += __shfl_xor(tot, o);
+    }
+    if (!a.pre) {                                       // runs' exact values -> index order
+        int64_t base = 0;
+        const int64_t row = j * a.D;
+        for (int r = 0; r < ra.R; ++r) {
+            const int64_t src = (int64_t)r * ra.L * kMtN, n_r = info[2 * r];
+            if (src != base)
+                for (int64_t i0 = 0; i0 < n_r; i0 += 64) {   // (base < src: a downward move, chunk by chunk)
+                    const int64_t i = i0 + lane;
+                    const float v = i < n_r ? a.ev[row + src + i] : 0.f;
+                    if (i < n_r) a.ev[row + base + i] = v;
+                }
+            base += n_r;
+        }
     }
     if (lane == 0) {
         if (a.ecount) a.ecount[j] = (int32_t)tot;
@@ -1300,7 +1290,19 @@ quicfl_recv_count_kernel(QflRecvArgs a, QflRunArgs ra) {
     if (a.compact && a.exact_mask) {
         const uint8_t* mk = a.exact_mask + j * a.D;
         const int64_t e0 = (int64_t)r * ra.L * kMtN, e1 = min(a.D, e0 + ra.L * kMtN);
-        for (int64_t i = e0 + lane; i < e1; i += 64) cnt += mk[i] != 0;
+        if ((((uintptr_t)(mk + e0) | (uintptr_t)(mk + e1)) & 15) == 0) {
+            // 16 bytes per lane (a 1 KB wave load); nonzero bytes of a word: the top bit of
+            // ((w & 0x7F..) + 0x7F..) | w
+            for (int64_t i = e0 + 16 * lane; i < e1; i += 1024) {
+                const u32x4v q = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(mk + i));
+                const uint32_t ws[4] = {q[0], q[1], q[2], q[3]};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    cnt += __popc((((ws[k] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | ws[k]) & 0x80808080u);
+            }
+        } else {
+            for (int64_t i = e0 + lane; i < e1; i += 64) cnt += mk[i] != 0;
+        }
         for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
     }
     if (lane == 0) ra.runinfo[(j * ra.R + r) * 2] = cnt;
