@@ -3859,16 +3859,16 @@ struct QflJumpPlan {
 };
 
 // Up to 1024 run waves a wave per SIMD; up to 2048 two (quicfl_send_runs_kernel<., true>), a
-// round then costing ~1.8 tR (round 6, profiles/r6k_*: 512 x 2^20 compress 12.0 -> 8.9 ms,
-// 256 x 2^22 round trip 24.2 -> 18.4, 101 x 2^22 8.9 -> 8.2; 1024 x 2^20 keeps KQ1, whose pass A
-// runs beside the RHT).
+// round then costing ~1.3 tR (round 6, profiles/r6k_* .. r6x_*: 512 x 2^20 compress 12.0 -> 7.6
+// ms, 1024 x 2^20 14.4 -> 12.9 with R = 2 once the runs' pass A moved to the side stream and the
+// counting pass went; 256 x 2^22 round trip 24.2 -> 17.5).
 constexpr int64_t kQfJumpMaxN = 1024;
 constexpr int64_t kQfRunWaves1 = 1024, kQfRunWaves2 = 2048;
 static QflJumpPlan qfl_jump_plan(int64_t n, int64_t D) {
     QflJumpPlan p;
     const int64_t nch = (D + kMtN - 1) / kMtN;
     if (n < 1 || n > kQfJumpMaxN || nch < 8 || D > ((int64_t)1 << 28)) return p;
-    const double tS = 20.0, tJ = 0.12, tR = 7.5, f2 = 1.8;
+    const double tS = 20.0, tJ = 0.12, tR = 7.5, f2 = 1.3;
     double best = 1e300;
     for (int64_t R = 1; R <= 1024 && R <= nch; ++R) {
         const int64_t L = (nch + R - 1) / R, Ru = (nch + L - 1) / L;
@@ -3892,9 +3892,10 @@ static QflJumpPlan qfl_jump_plan(int64_t n, int64_t D) {
 }
 
 // The receiver's jump path: one stream, one jump per run; a round (one wave: the h word, the
-// table gather, X, the mask and the exact value) ~tR, ~1.8 tR at two waves per SIMD (more than
-// 1024 run waves; 512 x 2^20 decompress 5.60 -> 4.23 ms, profiles/r6r_*).  Taken when it beats
-// the team kernel (~1 us per round of the h scout's twists and the runs behind it).
+// table gather, X, the mask and the exact value) ~tR, ~1.3 tR at two waves per SIMD (more than
+// 1024 run waves; 512 x 2^20 decompress 5.60 -> 3.53 ms, 1024 x 2^20 7.4 -> 6.4, profiles/r6r_*,
+// r6w_*, r6x_*).  Taken when it beats the team kernel (~1 us per round of the h scout's twists
+// and the runs behind it).
 static QflJumpPlan qfl_recv_jump_plan(int64_t n, int64_t D) {
     QflJumpPlan p;
     const int64_t nch = (D + kMtN - 1) / kMtN;
@@ -3904,7 +3905,7 @@ static QflJumpPlan qfl_recv_jump_plan(int64_t n, int64_t D) {
     for (int64_t R = 1; R <= 1024 && R <= nch; ++R) {
         const int64_t L = (nch + R - 1) / R, Ru = (nch + L - 1) / L;
         if (Ru != R || n * R > kQfRunWaves2) continue;                 // (its kernels fit 2 waves per SIMD)
-        const double t = tS + (double)(n * (R - 1)) * tJ + (double)L * tR * (n * R > kQfRunWaves1 ? 1.8 : 1.0);
+        const double t = tS + (double)(n * (R - 1)) * tJ + (double)L * tR * (n * R > kQfRunWaves1 ? 1.3 : 1.0);
         if (t < best) {
             best = t;
             p.R = (int32_t)R;
