@@ -366,3 +366,35 @@ def test_jump_path_equals_one_wave_across_shapes(fx, n, dim):
                 c = int(a.exact_count[j])
                 assert torch.equal(a.exact_vals[j, :c], b.exact_vals[j, :c]), j
             assert (sa is None and sb is None) or np.array_equal(sa, sb)
+
+
+def test_two_runs_per_message_at_900_messages(fx):
+    """900 messages of 2^18: the cost model takes the jump path with two runs per message (1800
+    run waves, two per SIMD: the lean KQ1j) for the sender and the receiver; X, mask, exact
+    values, scales and the decompressed batch equal the one-wave kernels' (test hook 2) on the
+    same messages, from GPU-resident input."""
+    import uqdme_amd.quicfl as q
+    from uqdme_amd._lib import load
+    meta, z, rmeta, rz = fx
+    snd = senders(meta)["pub"]
+    n, dim, nbits = 900, 1 << 18, 1
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.randn(n, dim, generator=g, device="cuda") * 2.0
+    x[0, 1] = 1e4
+    seeds = list(range(n))
+    rots = [int(s) for s in np.random.default_rng(9).integers(0, 100, n)]
+    pxs = list(range(5000, 5000 + n))
+    rt = rz[f"recv{nbits}"]
+    out = {}
+    for hooks in (0, 2):
+        prev = load().uq_test_set_quicfl_hooks(hooks)
+        try:
+            m = q.quicfl_compress(x, nbits, seeds, rots, sender=snd, px_seeds=pxs)
+            out[hooks] = (m, q.quicfl_decompress_messages(m, rt))
+        finally:
+            load().uq_test_set_quicfl_hooks(prev)
+    (a, da), (b, db) = out[0], out[2]
+    assert torch.equal(a.X, b.X) and torch.equal(a.exact_mask, b.exact_mask)
+    assert torch.equal(a.exact_count, b.exact_count) and torch.equal(a.scale, b.scale)
+    assert torch.equal(a.exact_dense(), b.exact_dense())
+    assert torch.equal(da.view(torch.int32), db.view(torch.int32))
