@@ -202,9 +202,10 @@ def test_build_id_matches_sources(lib):
 
 
 def test_quicfl_workspaces_cover_the_jump_paths(lib):
-    """The QUIC-FL workspaces grow by the jump path's scratch where it applies (few messages of
-    >= 8 rounds: the sender's streams, partial windows and run records; the receiver's with a
-    workspace entry) and stay as before elsewhere (host-only: no kernel runs)."""
+    """The QUIC-FL workspaces grow by the jump path's scratch where it applies (up to 1024
+    messages of >= 8 rounds, by the cost model: the sender's streams, partial windows and run
+    records; the receiver's with a workspace entry) and stay as before elsewhere (host-only: no
+    kernel runs)."""
     sz = ctypes.c_size_t()
     base = {}
     for n, d in ((1, 2048), (1, 1 << 20), (128, 1 << 20), (300, 1 << 20)):
@@ -215,7 +216,11 @@ def test_quicfl_workspaces_cover_the_jump_paths(lib):
     assert base[(1, 1 << 20)] - (1 << 20) * 5 >= (2 * 33 * 624 + 12 * 624) * 4
     assert lib.uq_quicfl_receive_workspace_bytes(1, 2048, ctypes.byref(sz)) == 0 and sz.value == 0
     assert lib.uq_quicfl_receive_workspace_bytes(1, 1 << 20, ctypes.byref(sz)) == 0 and sz.value >= 33 * 624 * 4
-    assert lib.uq_quicfl_receive_workspace_bytes(1024, 1 << 20, ctypes.byref(sz)) == 0 and sz.value == 0
+    # 1024 messages of 2^20 take the receiver's jump path too (two runs each, round 6); batches
+    # beyond 1024 messages do not
+    assert lib.uq_quicfl_receive_workspace_bytes(1024, 1 << 20, ctypes.byref(sz)) == 0
+    assert sz.value >= 1024 * 33 * 624 * 4
+    assert lib.uq_quicfl_receive_workspace_bytes(2048, 1 << 20, ctypes.byref(sz)) == 0 and sz.value == 0
     assert lib.uq_quicfl_receive_workspace_bytes(-1, 16, ctypes.byref(sz)) < 0
     assert lib.uq_rht_sign_bits(None, -1, 16, None, None) < 0
     assert lib.uq_rht_sign_bits(None, 0, 16, None, None) == 0        # nothing to pack
