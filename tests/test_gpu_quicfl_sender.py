@@ -372,7 +372,8 @@ def test_two_runs_per_message_at_900_messages(fx):
     """900 messages of 2^18: the cost model takes the jump path with two runs per message (1800
     run waves, two per SIMD: the lean KQ1j) for the sender and the receiver; X, mask, exact
     values, scales and the decompressed batch equal the one-wave kernels' (test hook 2) on the
-    same messages, from GPU-resident input."""
+    same messages, from GPU-resident input; the fused quantize (the receiver inside the
+    two-wave runs) equals compress -> decompress."""
     import uqdme_amd.quicfl as q
     from uqdme_amd._lib import load
     meta, z, rmeta, rz = fx
@@ -398,3 +399,6 @@ def test_two_runs_per_message_at_900_messages(fx):
     assert torch.equal(a.exact_count, b.exact_count) and torch.equal(a.scale, b.scale)
     assert torch.equal(a.exact_dense(), b.exact_dense())
     assert torch.equal(da.view(torch.int32), db.view(torch.int32))
+    # the receiver fused into the two-wave runs (QUICFL_quantize's path) gives the same batch
+    fo, _, fsc = q.quicfl_quantize(x, nbits, seeds, rots, sender=snd, recv_table=rt, px_seeds=pxs)
+    assert torch.equal(fo.view(torch.int32), da.view(torch.int32)) and torch.equal(fsc, a.scale)
