@@ -4507,10 +4507,11 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunc
         ra.passa_done = jl.passa_runs ? 1 : 0;
         const dim3 rgrid((unsigned)((n * jl.jp.R + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk(64 * kQfWavesPerWG);
         const bool w2 = n * jl.jp.R > kQfRunWaves1;
-        if (x_kind == 0 && w2) hipLaunchKernelGGL((quicfl_send_runs_kernel<0, true>), rgrid, blk, 0, st, q, ra);
-        else if (x_kind == 0) hipLaunchKernelGGL((quicfl_send_runs_kernel<0, false>), rgrid, blk, 0, st, q, ra);
-        else if (w2) hipLaunchKernelGGL((quicfl_send_runs_kernel<1, true>), rgrid, blk, 0, st, q, ra);
-        else hipLaunchKernelGGL((quicfl_send_runs_kernel<1, false>), rgrid, blk, 0, st, q, ra);
+#define UQ_QRUNS(XK)                                                                                        \
+    if (w2) hipLaunchKernelGGL((quicfl_send_runs_kernel<XK, true>), rgrid, blk, 0, st, q, ra);               \
+    else hipLaunchKernelGGL((quicfl_send_runs_kernel<XK, false>), rgrid, blk, 0, st, q, ra);
+        if (x_kind == 2) { UQ_QRUNS(2) } else if (x_kind == 0) { UQ_QRUNS(0) } else { UQ_QRUNS(1) }
+#undef UQ_QRUNS
         rc = hip_check(hipGetLastError(), "quicfl_send_runs_kernel launch");
         if (rc) return rc;
         hipLaunchKernelGGL(quicfl_send_fin_kernel, dim3((unsigned)((n + kQfWavesPerWG - 1) / kQfWavesPerWG)), blk, 0, st,
@@ -4519,7 +4520,9 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunc
     }
     if (!(hooks & 2) && ((hooks & 5) || !jp.use) && n <= kQfTeamMaxN && q.D >= (int64_t)kMtN * kQfRuns &&
         q.D <= kQfTeamMaxD) {
-        if (x_kind == 0)
+        if (x_kind == 2)
+            hipLaunchKernelGGL(quicfl_send_team_kernel<2>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
+        else if (x_kind == 0)
             hipLaunchKernelGGL(quicfl_send_team_kernel<0>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
         else
             hipLaunchKernelGGL(quicfl_send_team_kernel<1>, dim3((unsigned)n), dim3(64 * kQfTeamWaves), 0, st, q);
@@ -4531,7 +4534,9 @@ static int launch_quicfl_send(QflSendArgs& q, int32_t x_kind, const QflJumpLaunc
         if (rc) return rc;
         q.lstate = jl.lstate;
     }
-    if (x_kind == 0)
+    if (x_kind == 2)
+        hipLaunchKernelGGL(quicfl_send_wave_kernel<2>, grid, dim3(64 * kQfWavesPerWG), 0, st, q);
+    else if (x_kind == 0)
         hipLaunchKernelGGL(quicfl_send_wave_kernel<0>, grid, dim3(64 * kQfWavesPerWG), 0, st, q);
     else
         hipLaunchKernelGGL(quicfl_send_wave_kernel<1>, grid, dim3(64 * kQfWavesPerWG), 0, st, q);
@@ -4592,7 +4597,7 @@ int uq_quicfl_quantize_f32(const float* x, int64_t n, int64_t dim, const int8_t*
     q.rtab = recv_table;
     q.rtab_n = recv_numel;
     q.pre = rot;                       // in place: a coordinate's rot is loaded a round before its value is stored
-    rc = launch_quicfl_send(q, 0, jl, st);                                                        // AS:455-503, 526-532
+    rc = launch_quicfl_send(q, 2, jl, st);              // (2: the fused instances)                 AS:455-503, 526-532
     if (rc) return rc;
     // AS:533-535: the receiver's inverse RHT (H, then * diag), [:dim]; D = 2^22 as 14 + 8 bits
     const int p = ilog2_pow2(w.D);

@@ -198,14 +198,16 @@ __device__ __forceinline__ QflCtx qfl_ctx(const QflSendArgs& a, int64_t j, int32
     c.rr = make_rsrc(a.rot + c.row, Du * 4u);
     c.rh = make_rsrc(a.hbuf + c.row, Du);
     c.rm = make_rsrc(a.mask + c.row, Du);
+    // XK 2: the fused receiver (QUICFL_quantize, a.pre set): no X / mask / exact values written,
+    // and the compiler drops those paths (and their scalar state) from the instance
     c.rX = make_rsrc(XK == 0 ? (void*)((int64_t*)a.X + c.row) : (void*)((uint8_t*)a.X + c.row), XK == 0 ? Du * 8u : Du);
     c.packed = a.tabp != nullptr;
     c.rt = c.packed ? make_rsrc(a.tabp, (uint32_t)a.numel * 4u) : make_rsrc(a.tab, (uint32_t)a.numel * 8u);
     c.sc = (1.0f / a.nrm[j]) * a.sqrtD;                             // AS:466/470 (IEEE 1/x, then f32 mul)
     c.dp = div_plan_norm(a.delta);                                  // q = v / delta: reciprocal + Markstein (exact)
     c.dps = div_plan_norm(c.sc);
-    c.fused = a.pre != nullptr;
-    c.rP = make_rsrc(c.fused ? (void*)(a.pre + c.row) : (void*)a.rot, c.fused ? Du * 4u : 0u);
+    c.fused = XK == 2;
+    c.rP = make_rsrc(XK == 2 ? (void*)(a.pre + c.row) : (void*)a.rot, XK == 2 ? Du * 4u : 0u);
     c.rtab_n = a.rtab_n;
     c.fh = (float)a.h_len;
     c.fhalf = (float)a.half;
@@ -465,7 +467,7 @@ quicfl_send_wave_kernel(QflSendArgs a) {
     __shared__ uint32_t WLsh[kQfWavesPerWG][2 * kMtN];    // local stream ring per wave (first: the seed scratch)
     __shared__ uint32_t WGsh[kQfWavesPerWG][2 * kMtN];    // global stream ring per wave
     __shared__ float rtab[kQflRecvTab];                   // the fused receiver's table
-    if (a.pre) {
+    if (XK == 2) {
         for (int i = threadIdx.x; i < a.rtab_n; i += 64 * kQfWavesPerWG) rtab[i] = a.rtab[i];
         __syncthreads();
     }
@@ -589,7 +591,7 @@ quicfl_send_team_kernel(QflSendArgs a) {
     __shared__ float rtab[kQflRecvTab];                  // the fused receiver's table
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t j = blockIdx.x;
-    if (a.pre)
+    if (XK == 2)
         for (int i = threadIdx.x; i < a.rtab_n; i += 64 * kQfTeamWaves) rtab[i] = a.rtab[i];
     const int64_t D = a.D;
     const int64_t nch = (D + kMtN - 1) / kMtN;
@@ -941,7 +943,7 @@ quicfl_send_runs_kernel(QflSendArgs a, QflRunArgs ra) {
     __shared__ uint32_t WLsh[kQfWavesPerWG][2 * kMtN];
     __shared__ uint32_t WGsh[kQfWavesPerWG][2 * kMtN];
     __shared__ float rtab[kQflRecvTab];
-    if (a.pre) {
+    if (XK == 2) {
         for (int i = threadIdx.x; i < a.rtab_n; i += 64 * kQfWavesPerWG) rtab[i] = a.rtab[i];
         __syncthreads();
     }

@@ -234,11 +234,18 @@ class QuicFLMessages:
     h_len: int
 
     def exact_dense(self) -> torch.Tensor:
-        """[n, D] f32: each message's exact values at their coordinates, 0 elsewhere."""
+        """[n, D] f32: each message's exact values at their coordinates, 0 elsewhere.  (In row
+        blocks of < 2^31 elements: boolean indexing of larger tensors overflows on this torch.)"""
         n, D = self.exact_mask.shape
-        dense = torch.zeros((n, D), dtype=torch.float32, device=self.exact_vals.device)
-        keep = torch.arange(D, device=self.exact_vals.device)[None, :] < self.exact_count.to(self.exact_vals.device)[:, None]
-        dense[self.exact_mask] = self.exact_vals[keep]
+        dev = self.exact_vals.device
+        dense = torch.zeros((n, D), dtype=torch.float32, device=dev)
+        cnt = self.exact_count.to(dev)
+        ar = torch.arange(D, device=dev)[None, :]
+        rows = max(1, ((1 << 31) - 1) // max(D, 1))
+        for j0 in range(0, n, rows):
+            j1 = min(n, j0 + rows)
+            keep = ar < cnt[j0:j1, None]
+            dense[j0:j1][self.exact_mask[j0:j1]] = self.exact_vals[j0:j1][keep]
         return dense
 
 
