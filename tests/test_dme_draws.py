@@ -48,3 +48,30 @@ def test_draw_ahead_stops_early_and_raises():
         pass
     else:
         raise AssertionError("expected KeyError")
+
+
+def test_parallel_client_draws_equal_the_sequential_loop():
+    """The harness's torch draws per instance (ND:133-140: EDEN's seed, unbiased's X, QUIC-FL's
+    seed, generator state and D skipped words per client and rate), computed client by client in
+    threads from jumped starts, equal the sequential loop's values and leave the generator in the
+    same state -- with a short D (jumps inside a block) and C4's padded D = 2^22 (real jumps)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from uqdme_amd.dme import _client_draws, _client_draws_parallel
+    from uqdme_amd.quicfl import generator_words
+    order = ("eden", "unbiased", "biased", "quicfl")
+    with ThreadPoolExecutor(4) as pool:
+        for n, qD in ((5, 300), (4, 1 << 22), (1, 1 << 22), (0, 64)):
+            ga, gb = torch.Generator().manual_seed(42), torch.Generator().manual_seed(42)
+            torch.rand(777, generator=ga)
+            torch.rand(777, generator=gb)                 # off a block edge
+            want = _client_draws(ga, n, order, (1, 2), qD)
+            got = _client_draws_parallel(gb, n, order, (1, 2), qD, pool)
+            assert got.keys() == want.keys()
+            for k in want:
+                if k[0] == "quicfl":
+                    assert [s for s, _ in got[k]] == [s for s, _ in want[k]], (n, qD, k)
+                    assert all(np.array_equal(a, b) for (_, a), (_, b) in zip(got[k], want[k])), (n, qD, k)
+                else:
+                    assert got[k] == want[k], (n, qD, k)
+            assert np.array_equal(generator_words(ga)[1], generator_words(gb)[1]), (n, qD)
+            assert float(torch.rand(1, generator=ga)) == float(torch.rand(1, generator=gb))

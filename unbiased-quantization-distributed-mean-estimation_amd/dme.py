@@ -237,6 +237,62 @@ def _save_checkpoint(path, meta, ui, rs_state, gen_state, script):
     os.replace(tmp, path)
 
 
+def _client_draws(gen, n, order, rates, qD):
+    """ND:133-140's torch draws of n clients, client-major and scheme / rate-minor, from `gen`
+    (which ends where the reference's loop leaves torch's global generator): EDEN's rotation
+    seed (AS:797), unbiased's X (AS:634), QUIC-FL's prng seed (AS:820), its generator state, and
+    its D bernoulli(p_X) words skipped by jump-ahead (AS:489)."""
+    from .quicfl import advance_generator, generator_words
+    draws = {(sc, r): [] for sc in order for r in rates}
+    for _ in range(n):
+        for sc in order:
+            for r in rates:
+                if sc == "eden":
+                    draws[(sc, r)].append(int(torch.randint(0, 100, (1,), generator=gen)))   # AS:797
+                elif sc == "unbiased":
+                    draws[(sc, r)].append(float(torch.rand(1, generator=gen)))               # AS:634
+                elif sc == "quicfl":
+                    seed = int(torch.randint(0, 100, (1,), generator=gen))                    # AS:820
+                    draws[(sc, r)].append((seed, generator_words(gen)[1]))
+                    advance_generator(gen, qD)             # past the D bernoulli(p_X) words (AS:489)
+    return draws
+
+
+def _client_words(order, rates, qD):
+    """32-bit words of torch's CPU generator one client takes in _client_draws: randint(0, 100)
+    and rand(1) one each (ATen's random() for a range below 2^32 / a float), QUIC-FL's seed plus its
+    D words."""
+    per = {"eden": 1, "unbiased": 1, "biased": 0, "quicfl": 1 + (qD or 0)}
+    return sum(per[sc] for sc in order) * len(rates)
+
+
+def _client_draws_parallel(gen, n, order, rates, qD, pool):
+    """_client_draws with each client's share of the stream in its own thread: a client takes a
+    fixed number of words (_client_words), so client j starts where j of them leave the stream
+    -- one jump-ahead from the instance's first state -- and its QUIC-FL skips are jumps too;
+    the jumps (uq_mt_jump_host, ~0.6 ms each, outside the GIL) overlap.  Same values and the same
+    end state as the sequential loop (tests/test_dme_draws.py)."""
+    from .quicfl import advance_generator, generator_words, set_generator_words
+    if n == 0:
+        return {(sc, r): [] for sc in order for r in rates}
+    st, w0 = generator_words(gen)
+    W = _client_words(order, rates, qD)
+
+    def one(j):
+        g = torch.Generator()
+        set_generator_words(g, st, w0)
+        if j:
+            advance_generator(g, j * W)
+        d = _client_draws(g, 1, order, rates, qD)
+        return d, (generator_words(g) if j == n - 1 else None)
+
+    res = list(pool.map(one, range(n))) if pool is not None else [one(j) for j in range(n)]
+    draws = {(sc, r): [x for d, _ in res for x in d[(sc, r)]] for sc in order for r in rates}
+    end_st, end_w = res[-1][1]
+    set_generator_words(gen, end_st, end_w)
+    return draws
+
+
 def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_instances: int = 50,
                     num_trials: int = 50, rates=(1, 2), seed: int = 42, torch_threads: int = 1,
                     device=None, schemes=("unbiased",), progress=None, eden_scales=None, eden_scales_out=None,
@@ -263,7 +319,7 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
     order = [sc for sc in SCHEME_ORDER if sc in schemes]
     if "quicfl" in order:
         from .eden import padded_dim
-        from .quicfl import _dropin_pair, advance_generator, generator_words
+        from .quicfl import _dropin_pair
         qsend, qrecv = quicfl if quicfl is not None else _dropin_pair()
         qD = padded_dim(dim)
     rs = np.random.RandomState(seed)                 # legacy stream == np.random.seed(seed)
@@ -283,6 +339,10 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
             for sc, r in keys:
                 script[(sc, r)][:] = ck[f"script_{sc}_{r}"]
     t_start = time.perf_counter()
+    jump_pool = None
+    if "quicfl" in order:
+        from concurrent.futures import ThreadPoolExecutor
+        jump_pool = ThreadPoolExecutor(max_workers=max(1, min(8, host_threads() // 2)))
     batches = _draw_ahead(dist, users[start_ui:], num_instances, dim, rs, device=device, threads=threads)
     for ui in range(start_ui, len(users)):
         n = users[ui]
@@ -298,18 +358,10 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                     raise Suspended(f"suspended before user count {n} (index {ui}); resume from {checkpoint}")
             if xd.is_cuda:
                 xd.record_stream(torch.cuda.current_stream(device))   # copied on the side stream, used here
-            draws = {k: [] for k in keys}
-            for _ in range(n):                        # ND:133-140: client-major, scheme/rate-minor
-                for sc in order:
-                    for r in rates:
-                        if sc == "eden":
-                            draws[(sc, r)].append(int(torch.randint(0, 100, (1,), generator=gen)))   # AS:797
-                        elif sc == "unbiased":
-                            draws[(sc, r)].append(float(torch.rand(1, generator=gen)))               # AS:634
-                        elif sc == "quicfl":
-                            seed = int(torch.randint(0, 100, (1,), generator=gen))                    # AS:820
-                            draws[(sc, r)].append((seed, generator_words(gen)[1]))
-                            advance_generator(gen, qD)             # past the D bernoulli(p_X) words (AS:489)
+            if "quicfl" in order:                     # the clients' torch draws in parallel (exact)
+                draws = _client_draws_parallel(gen, n, order, rates, qD, jump_pool)
+            else:
+                draws = _client_draws(gen, n, order, rates, None)
             for sc, r in keys:
                 if sc == "unbiased":
                     q = quantize_dequantize(xd, r, X=torch.tensor(draws[(sc, r)], dtype=torch.float32),
@@ -334,6 +386,8 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                 script[(sc, r)][ui, inst] = float(torch.norm(est - emp).pow(2) / (num_trials * vns * n))   # ND:155
             if progress is not None:
                 progress(n, inst)
+    if jump_pool is not None:
+        jump_pool.shutdown()
     if checkpoint is not None:                        # finished: a rerun returns the same rows
         _save_checkpoint(checkpoint, meta, len(users), rs.get_state(legacy=True), gen.get_state(), script)
     out = {}
