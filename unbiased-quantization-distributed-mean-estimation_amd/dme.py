@@ -339,10 +339,11 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
             for sc, r in keys:
                 script[(sc, r)][:] = ck[f"script_{sc}_{r}"]
     t_start = time.perf_counter()
+    from concurrent.futures import ThreadPoolExecutor
     jump_pool = None
     if "quicfl" in order:
-        from concurrent.futures import ThreadPoolExecutor
         jump_pool = ThreadPoolExecutor(max_workers=max(1, min(8, host_threads() // 2)))
+    host_pool = ThreadPoolExecutor(max_workers=4) if len(keys) > 1 else None   # the NMSE norms on the host
     batches = _draw_ahead(dist, users[start_ui:], num_instances, dim, rs, device=device, threads=threads)
     for ui in range(start_ui, len(users)):
         n = users[ui]
@@ -355,6 +356,9 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                 _save_checkpoint(checkpoint, meta, ui, rs_before, gen.get_state(), script)
                 if time_limit_s is not None and ui > start_ui and time.perf_counter() - t_start > time_limit_s:
                     batches.close()
+                    for pool in (jump_pool, host_pool):
+                        if pool is not None:
+                            pool.shutdown()
                     raise Suspended(f"suspended before user count {n} (index {ui}); resume from {checkpoint}")
             if xd.is_cuda:
                 xd.record_stream(torch.cuda.current_stream(device))   # copied on the side stream, used here
@@ -362,6 +366,7 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                 draws = _client_draws_parallel(gen, n, order, rates, qD, jump_pool)
             else:
                 draws = _client_draws(gen, n, order, rates, None)
+            ests = {}
             for sc, r in keys:
                 if sc == "unbiased":
                     q = quantize_dequantize(xd, r, X=torch.tensor(draws[(sc, r)], dtype=torch.float32),
@@ -382,12 +387,21 @@ def nmse_simulation(dist: str = "normal", dim: int = 2048, users=USERS_ND, num_i
                     if eden_scales is not None:
                         msg.scale = torch.as_tensor(np.asarray(eden_scales[(n, inst, r)], np.float32)).to(device)
                     q = eden_decompress(msg)
-                est = client_mean(q, n).cpu()
-                script[(sc, r)][ui, inst] = float(torch.norm(est - emp).pow(2) / (num_trials * vns * n))   # ND:155
+                ests[(sc, r)] = client_mean(q, n)
+                del q
+
+            def nmse(k):                              # ND:155, on the host as the reference computes it
+                return float(torch.norm(ests[k].cpu() - emp).pow(2) / (num_trials * vns * n))
+            # every scheme's estimate queued first: the copies and the CPU norms overlap each other
+            # and the GPU work still running (same values: each norm is the same call on the same data)
+            vals = list(host_pool.map(nmse, keys)) if host_pool is not None else [nmse(k) for k in keys]
+            for k, v in zip(keys, vals):
+                script[k][ui, inst] = v
             if progress is not None:
                 progress(n, inst)
-    if jump_pool is not None:
-        jump_pool.shutdown()
+    for pool in (jump_pool, host_pool):
+        if pool is not None:
+            pool.shutdown()
     if checkpoint is not None:                        # finished: a rerun returns the same rows
         _save_checkpoint(checkpoint, meta, len(users), rs.get_state(legacy=True), gen.get_state(), script)
     out = {}
